@@ -1,0 +1,395 @@
+#!/usr/bin/env python3
+"""Benchmark: batch 2-bit encode on MI355X (BASELINE.json configs[1]: 100M x 32-nt reads, 1 GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one ss_encode_fixed launch over one rank's batch of synthetic reads already resident in
+HBM (SURVEY §8(d) generator, generated on the device).  Ranks shard the read stream by contiguous
+index ranges (weak scaling, no data-path collective).  `value` = all ranks' nt / max-over-ranks
+time.  The same JSON line carries the other BASELINE configs as `extra` (C3 fused encode+hamming,
+C4 encode+decode round trip, C5 sharded counter with an RCCL all-to-all merge), the `roofline` of
+the dominant kernel (algorithmic bytes / HIP-event kernel time vs 8 TB/s) and the `cpu_baseline`
+(the reference's own compiled _marshall_bytes_64 kernel, oracle/_ref, timed on 1 host core).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def splitmix64(x: int) -> int:
+    M = (1 << 64) - 1
+    z = (x + 0x9E3779B97F4A7C15) & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
+
+
+def known_words(seed: int, i: int, L: int) -> list:
+    """The generator's words for read i = the expected encode output."""
+    W = (L + 31) // 32
+    out = []
+    for w in range(W):
+        nb = min(32, L - 32 * w)
+        r = splitmix64(seed + i * W + w)
+        out.append(r if nb == 32 else r & ((1 << (2 * nb)) - 1))
+    return out
+
+
+class Timer:
+    """HIP events on the stream the kernels are launched on (torch's current stream)."""
+
+    def __init__(self):
+        self.pairs = []
+
+    def __enter__(self):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        self.pairs.append((s, e))
+        return self
+
+    def __exit__(self, *exc):
+        self.pairs[-1][1].record()
+
+    def mean_ms(self) -> float:
+        torch.cuda.synchronize()
+        return float(np.mean([s.elapsed_time(e) for s, e in self.pairs]))
+
+
+def timed_loop(step, steps, warmup, world):
+    """W untimed steps, then K steps between barrier + synchronize; returns max-over-ranks seconds."""
+    for _ in range(warmup):
+        step(None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer = Timer()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(timer)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, timer
+
+
+def check_known_answer(words: torch.Tensor, seed: int, i0: int, L: int, n: int):
+    idx = np.unique(np.linspace(0, n - 1, 257).astype(np.int64))
+    got = words[torch.from_numpy(idx).to(words.device)].cpu().numpy().view(np.uint64)
+    for k, i in enumerate(idx):
+        exp = known_words(seed, i0 + int(i), L)
+        if [int(x) for x in got[k][: len(exp)]] != exp:
+            raise SystemExit(f"PARITY FAILURE: read {i0 + i} L={L}: {got[k]} != {exp}")
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed PMC summary (profiles/), if one exists."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except Exception:  # noqa: BLE001
+        return None
+
+
+# ------------------------------------------------------------------------------------------------
+def bench_encode(B, lib, dev, rank, world, n, L, steps, warmup, seed=1):
+    i0 = rank * n
+    ascii = B.synth_reads(n, L, seed=seed, i0=i0, device=dev)
+    wpr = B.wpr_for(L)
+    words = torch.empty((n, wpr), dtype=torch.int64, device=dev)
+    fb = B.first_bad_buffer(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ap, wp, fp = ascii.data_ptr(), words.data_ptr(), fb.data_ptr()
+
+    def step(timer):
+        if timer is None:
+            rc = lib.ss_encode_fixed(ap, n, L, L, wp, wpr, fp, stream)
+        else:
+            with timer:
+                rc = lib.ss_encode_fixed(ap, n, L, L, wp, wpr, fp, stream)
+        if rc:
+            raise RuntimeError(lib.ss_last_error_string())
+
+    el, timer = timed_loop(step, steps, warmup, world)
+    if int(fb.item()) != -1:
+        raise SystemExit("PARITY FAILURE: synthetic batch flagged an invalid base")
+    check_known_answer(words, seed, i0, L, n)
+    del ascii, words
+    return el, timer.mean_ms()
+
+
+def bench_encode_hamming(B, lib, dev, rank, world, n, L, steps, warmup, seed=2):
+    i0 = rank * n
+    ascii = B.synth_reads(n, L, seed=seed, i0=i0, device=dev)
+    wpr = B.wpr_for(L)
+    words = torch.empty((n, wpr), dtype=torch.int64, device=dev)
+    dist_out = torch.empty(n, dtype=torch.int32, device=dev)
+    ref = torch.empty((1, wpr), dtype=torch.int64, device=dev)
+    fb = B.first_bad_buffer(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(timer):
+        # reference read = read 0 of the batch, encoded first (tiny launch), then one fused pass
+        rc = lib.ss_encode_fixed(ascii.data_ptr(), 1, L, L, ref.data_ptr(), wpr, fb.data_ptr(), stream)
+        if timer is None:
+            rc |= lib.ss_encode_hamming_ref(ascii.data_ptr(), n, L, L, words.data_ptr(), wpr, ref.data_ptr(),
+                                            dist_out.data_ptr(), fb.data_ptr(), stream)
+        else:
+            with timer:
+                rc |= lib.ss_encode_hamming_ref(ascii.data_ptr(), n, L, L, words.data_ptr(), wpr,
+                                                ref.data_ptr(), dist_out.data_ptr(), fb.data_ptr(), stream)
+        if rc:
+            raise RuntimeError(lib.ss_last_error_string())
+
+    el, timer = timed_loop(step, steps, warmup, world)
+    check_known_answer(words, seed, i0, L, n)
+    # distances: property check against the packed words (hamming kernel on the stored words)
+    d2 = B.hamming_ref(words, L, words[0])
+    if not torch.equal(d2, dist_out):
+        raise SystemExit("PARITY FAILURE: fused hamming != hamming on packed words")
+    del ascii, words, dist_out, d2
+    return el, timer.mean_ms()
+
+
+def bench_roundtrip(B, lib, dev, rank, world, n, L, steps, warmup, seed=3):
+    i0 = rank * n
+    ascii = B.synth_reads(n, L, seed=seed, i0=i0, device=dev)
+    wpr = B.wpr_for(L)
+    words = torch.empty((n, wpr), dtype=torch.int64, device=dev)
+    back = torch.empty((n, L), dtype=torch.uint8, device=dev)
+    fb = B.first_bad_buffer(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    t_enc, t_dec = Timer(), Timer()
+
+    def step(timer):
+        if timer is None:
+            rc = lib.ss_encode_fixed(ascii.data_ptr(), n, L, L, words.data_ptr(), wpr, fb.data_ptr(), stream)
+            rc |= lib.ss_decode_fixed(words.data_ptr(), n, L, wpr, back.data_ptr(), L, stream)
+        else:
+            with t_enc:
+                rc = lib.ss_encode_fixed(ascii.data_ptr(), n, L, L, words.data_ptr(), wpr, fb.data_ptr(), stream)
+            with t_dec:
+                rc |= lib.ss_decode_fixed(words.data_ptr(), n, L, wpr, back.data_ptr(), L, stream)
+        if rc:
+            raise RuntimeError(lib.ss_last_error_string())
+
+    el, _ = timed_loop(step, steps, warmup, world)
+    if not torch.equal(back, ascii):
+        raise SystemExit("PARITY FAILURE: encode -> decode round trip")
+    check_known_answer(words, seed, i0, L, n)
+    del ascii, words, back
+    return el, t_enc.mean_ms(), t_dec.mean_ms()
+
+
+def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool_seed=77):
+    """C5: per rank n reads drawn from a pool of U 32-mers; count locally, partition by owner,
+    all-to-all the (key, count, first) triples over RCCL, owners merge."""
+    i0 = rank * n
+    ascii = B.synth_pool_reads(n, L, seed, pool_seed, U, i0=i0, device=dev)
+    cap = 1 << max(10, int(np.ceil(np.log2(2 * U))))
+    local = B.GpuCounter(cap, device=dev)
+    owner = B.GpuCounter(cap, device=dev) if world > 1 else None
+    t_ins = Timer()
+    state = {}
+
+    def step(timer):
+        local.reset()
+        if timer is None:
+            local.insert(ascii, L, base_index=i0, check_errors=False)
+        else:
+            with t_ins:
+                local.insert(ascii, L, base_index=i0, check_errors=False)
+        keys, lens, counts, first, parts = local.extract(n_parts=world)
+        if world > 1:
+            owner.reset()
+            send = torch.stack([keys, counts, first], 1)
+            sc = parts.cpu().tolist()
+            m = sum(sc)
+            rc_t = torch.empty(world, dtype=torch.int64, device=dev)
+            dist.all_to_all_single(rc_t, parts)
+            rc = rc_t.cpu().tolist()
+            recv = torch.empty((sum(rc), 3), dtype=torch.int64, device=dev)
+            dist.all_to_all_single(recv, send[:m].contiguous(), output_split_sizes=rc, input_split_sizes=sc)
+            owner.merge(recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous(), L)
+            state["result"] = owner
+        else:
+            state["result"] = local
+            state["m"] = parts
+
+    el, _ = timed_loop(step, steps, warmup, world)
+    res = state["result"]
+    k, c, f = res.items_sorted()
+    tot = torch.tensor([int(c.sum()), len(k)], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    if int(tot[0]) != n * world:
+        raise SystemExit(f"PARITY FAILURE: counter total {int(tot[0])} != {n * world}")
+    uniq = int(tot[1])
+    local.close()
+    if owner is not None:
+        owner.close()
+    del ascii
+    return el, t_ins.mean_ms(), uniq
+
+
+# ------------------------------------------------------------------------------------------------
+def cpu_baseline(L=32, target_s=10.0):
+    """The reference's compiled _marshall_bytes_64 (oracle/_ref) on 1 host core over a bounded
+    sample of the same workload; falls back to the C restatement (kind "port") if _ref is absent."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test/baseline infrastructure only — never the measured GPU path
+    n = 4_000_000
+    ascii = oracle.gen_reads(1, 0, n, L)
+    kind = "reference" if oracle.ref_available() else "port"
+    if kind == "reference":
+        def run():
+            return oracle.ref_encode_batch(ascii, n, L)
+    else:
+        def run():
+            return oracle.encode_batch(ascii, n, L)[0]
+    out = run()  # warm
+    if not np.array_equal(out[:16], oracle.gen_words(1, 0, 16, L)):
+        raise SystemExit("cpu baseline produced wrong words")
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= target_s:
+            break
+    nt = passes * n * L
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": nt / el, "unit": "nt/s", "cores": 1, "kind": kind,
+            "sample": f"{passes} passes x {n} reads x {L} nt ({el:.1f} s), "
+                      f"{'shortseq.short_seq_64._marshall_bytes_64 (reference, -O3 -mbmi2)' if kind == 'reference' else 'oracle C restatement'}"
+                      f"; host cpu: {cpu}, nproc {os.cpu_count()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=100_000_000, help="reads per GPU (C2)")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import lib as _lib
+    lib = _lib()
+
+    L, n = 32, args.n
+    log(f"rank {rank}/{world}: C2 encode {n} x {L} nt")
+    el, kern_ms = bench_encode(B, lib, dev, rank, world, n, L, args.steps, args.warmup)
+    ms_step = el / args.steps * 1e3
+    total_nt = n * L * world
+    value = total_nt / (el / args.steps)
+    algo_bytes = n * (L + 8)  # 32 B ASCII in + 8 B packed word out per read
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    result = {
+        "metric": "nt/sec 2-bit encode (32/96/512-nt batches) + hamming pairs/sec; % HBM roofline",
+        "value": value, "unit": "nt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic (device-side splitmix64 reads, SURVEY §8(d))",
+        "config": {"workload": "C2: 100M x 32-nt batch encode (short_seq_64 path), per GPU",
+                   "reads_per_gpu": n, "read_len": L, "global_batch": n * world,
+                   "parallelism": f"dp{world} (read shards, no collective)"},
+        "roofline": {"bound": "hbm", "kernel": "k_encode_g16<dense>", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic("encode32"), "algo_bytes_per_launch": algo_bytes,
+                     "kernel_ms": kern_ms},
+    }
+    log(f"C2: {value / 1e12:.3f} T nt/s, kernel {kern_ms:.3f} ms, {achieved:.0f} GB/s")
+
+    if not args.no_extras:
+        extra = {}
+        L3, n3 = 96, args.n
+        log(f"C3 fused encode+hamming {n3} x {L3}")
+        el3, k3 = bench_encode_hamming(B, lib, dev, rank, world, n3, L3, args.steps, args.warmup)
+        b3 = n3 * (96 + 24 + 4)
+        extra["C3_encode_hamming_96"] = {
+            "pairs_per_s": n3 * world / (el3 / args.steps), "nt_per_s": n3 * L3 * world / (el3 / args.steps),
+            "ms_per_step": el3 / args.steps * 1e3, "kernel_ms": k3,
+            "roofline": {"achieved": b3 / (k3 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": b3 / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, "algo_bytes_per_launch": b3}}
+        L4, n4 = 512, args.n // 2
+        log(f"C4 encode+decode {n4} x {L4}")
+        el4, ke, kd = bench_roundtrip(B, lib, dev, rank, world, n4, L4, max(5, args.steps // 2), args.warmup)
+        b4e, b4d = n4 * (512 + 128), n4 * (128 + 512)
+        extra["C4_roundtrip_512"] = {
+            "nt_per_s": n4 * L4 * world / (el4 / max(5, args.steps // 2)),
+            "ms_per_step": el4 / max(5, args.steps // 2) * 1e3, "encode_kernel_ms": ke, "decode_kernel_ms": kd,
+            "roofline": {"achieved": (b4e + b4d) / ((ke + kd) * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": (b4e + b4d) / ((ke + kd) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "algo_bytes_per_step": b4e + b4d}}
+        n5, U5 = 125_000_000, 1 << 24
+        log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
+        el5, ki, uniq = bench_counter(B, lib, dev, rank, world, n5, 32, U5, max(3, args.steps // 4), 2)
+        s5 = max(3, args.steps // 4)
+        extra["C5_counter_32"] = {
+            "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "insert_kernel_ms": ki,
+            "reads_per_gpu": n5, "pool": U5, "unique": uniq,
+            "merge": "RCCL all_to_all_single of (key, count, first) by owner" if world > 1 else "none (1 GPU)"}
+        result["extra"] = extra
+
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline ...")
+            result["cpu_baseline"] = cpu_baseline(32, args.cpu_seconds)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,180 @@
+/*
+ * shortseq_amd.h — C ABI of the MI355X (gfx950) batch 2-bit DNA engine.
+ *
+ * Drop-in boundary for the reference's native kernel layer (AlexTate/ShortSeq, Cython cdef functions
+ * exported as PyCapsules in each module's __pyx_capi__).  The reference kernels work
+ * on ONE read per call; each entry point below does the same work for a whole batch on the GPU.
+ *
+ * Conventions
+ *   - Plain C types only.  `d_*` arguments are device pointers (hipMalloc / torch CUDA tensors);
+ *     `h_*` arguments are host pointers.  `stream` is a hipStream_t passed as void* (NULL = default).
+ *   - Device entry points are asynchronous on `stream`, never allocate, never synchronise, and are
+ *     safe to capture in a hipGraph.  They return SS_OK or a launch/argument error immediately.
+ *   - Validation mirrors util.pxd:98-99 (bloom filter 0xFFFFFFFFFFEFFF75, util.pyx:75).  A kernel
+ *     that meets an invalid byte writes the index of the FIRST invalid read (input order) into
+ *     *d_first_bad (atomicMin; the entry point resets it to UINT64_MAX first).  The caller re-scans
+ *     that read with ss_host_encode() to obtain the reference's exact error (byte or 8-byte chunk).
+ *   - Layouts: read i of a fixed-length batch starts at d_ascii + i*stride (bytes); its packed words
+ *     are d_words[i*wpr .. i*wpr + wpr), nt j in word j/32 at bits 2*(j%32) (nt 0 = LSBs), codes
+ *     A=0 C=1 T=2 G=3 (README.md:101-112).  wpr >= ceil(L/32) (>= 1); extra words are written 0.
+ *
+ * Error codes (ss_status): negative = API/runtime error, positive = data error.
+ */
+#ifndef SHORTSEQ_AMD_H
+#define SHORTSEQ_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SS_ABI_VERSION 1
+
+enum ss_status {
+    SS_OK = 0,
+    SS_EINVALID_BASE = 1,   /* "Unsupported base character: ..."  (short_seq_64.pyx:105, util.pyx:115/137) */
+    SS_ETOO_LONG = 2,       /* "Sequences longer than 1024 bases are not supported." (short_seq.pyx:74) */
+    SS_EARG = -1,           /* bad argument (NULL pointer, L out of range, wpr too small, misalignment) */
+    SS_EHIP = -2,           /* HIP runtime error; see ss_last_error_string() */
+    SS_ENOMEM = -3,         /* allocation failed (counter handles only) */
+    SS_EFULL = -4           /* counter table full */
+};
+
+#define SS_MAX_NT 1024u     /* short_seq_var.pyx:9 */
+#define SS_MAX_64_NT 32u    /* short_seq_64.pyx:28 */
+#define SS_MAX_192_NT 96u   /* short_seq_192.pyx:22 */
+
+/* Error detail for the host codec (ss_host_encode).  kind = ss_status; for SS_EINVALID_BASE,
+ * [byte_offset, byte_offset + nbytes) are the bytes the reference names in its message: 1 byte on
+ * the table path (the LAST offending byte, reverse scan), 8 bytes (the chunk) on the full-block path
+ * (blocks in order, chunks 3->0 within a block). */
+typedef struct ss_err {
+    int32_t kind;
+    int32_t nbytes;
+    int64_t read_index;
+    int64_t byte_offset;
+} ss_err;
+
+/* ------------------------------------------------------------------------------------------------
+ * Library / runtime
+ * ---------------------------------------------------------------------------------------------- */
+int ss_abi_version(void);
+const char* ss_last_error_string(void);          /* thread-local message of the last SS_EHIP/EARG */
+int ss_device_count(int* h_count);
+int ss_set_device(int device);
+
+/* Pinned host staging buffers (hipHostMalloc / hipHostFree) for H2D batch staging. */
+int ss_pinned_alloc(void** h_ptr, size_t bytes);
+int ss_pinned_free(void* h_ptr);
+
+/* ------------------------------------------------------------------------------------------------
+ * Batch encode — replaces, per read:
+ *   _marshall_bytes_64   (short_seq_64.pyx:96-108)   L <= 32: table path (SURVEY Q1 carry kept)
+ *   _marshall_bytes_192  (short_seq_192.pyx:103-108) 33..96  -> _marshall_bytes_array
+ *   _marshall_bytes_var  (short_seq_var.pyx:123-132) 97..1024 -> _marshall_bytes_array
+ *   _marshall_bytes_array/_full_blocks/_partial_block (util.pyx:78-140): full 32-nt blocks by the
+ *   PEXT rule (c>>1)&3, the L%32 tail by the table rule.
+ * Fixed length L (1..1024) for every read.  Fast path when L % 16 == 0, stride % 16 == 0 and
+ * d_ascii is 16-byte aligned; otherwise a general path (any L, stride >= L).
+ * ---------------------------------------------------------------------------------------------- */
+int ss_encode_fixed(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                    uint64_t* d_words, uint32_t wpr, uint64_t* d_first_bad, void* stream);
+
+/* Variable-length batch: read i = d_ascii[d_offsets[i] .. + d_lens[i]), 0 <= len <= 1024
+ * (short_seq.pyx:54-74 length-class switch: 0 -> packed 0, <= 32 table path, else array path).
+ * Reads longer than 1024 are reported through *d_first_bad like invalid bases. */
+int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint32_t* d_lens,
+                  uint64_t n, uint64_t* d_words, uint32_t wpr, uint64_t* d_first_bad, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Batch decode — replaces _unmarshall_bytes_64/_192/_var (short_seq_64.pyx:114-121,
+ * short_seq_192.pyx:114-127, short_seq_var.pyx:98-120): nt j -> "ACTG"[code] (util.pyx:52).
+ * Writes exactly L bytes per read at d_ascii + i*stride (no terminator).
+ * ---------------------------------------------------------------------------------------------- */
+int ss_decode_fixed(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr,
+                    uint8_t* d_ascii, uint64_t stride, void* stream);
+
+int ss_decode_var(const uint64_t* d_words, const uint32_t* d_lens, uint64_t n, uint32_t wpr,
+                  uint8_t* d_ascii, const uint64_t* d_offsets, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Hamming — replaces ShortSeq64/192/Var.__xor__ (short_seq_64.pyx:77-84, short_seq_192.pyx:74-91,
+ * short_seq_var.pyx:64-81): sum over W = (L <= 32 ? 1 : ceil(L/32)) words of
+ * popcount(((x >> 1) | x) & 0x5555555555555555), x = a ^ b.  Whole-word, like the reference.
+ * ---------------------------------------------------------------------------------------------- */
+int ss_hamming_ref(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr,
+                   const uint64_t* d_ref, uint32_t* d_out, void* stream);
+int ss_hamming_pair(const uint64_t* d_a, const uint64_t* d_b, uint64_t n, uint32_t L, uint32_t wpr,
+                    uint32_t* d_out, void* stream);
+
+/* Fused encode + hamming vs one packed reference read (d_ref_words, wpr words, e.g. read 0 encoded
+ * first): one pass over the ASCII, writes the packed words (if d_words != NULL) and the distance. */
+int ss_encode_hamming_ref(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                          uint64_t* d_words, uint32_t wpr, const uint64_t* d_ref_words,
+                          uint32_t* d_out, uint64_t* d_first_bad, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Dedup counter — replaces ShortSeqCounter._count_sequence (counter.pyx:41-54): key = (length,
+ * packed words) (short_seq_64.pyx:41-44; short_seq_192.pyx:35-41), count += 1, first-occurrence
+ * index kept so the host can rebuild dict insertion order.  Open-addressing table in HBM, one per
+ * handle; keys of one handle have L <= 32 (one word; the length is part of the key).
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct ss_counter ss_counter;
+
+int ss_counter_create(uint64_t capacity, ss_counter** out);      /* capacity rounded up to 2^k */
+int ss_counter_destroy(ss_counter* c);
+int ss_counter_reset(ss_counter* c, void* stream);
+uint64_t ss_counter_capacity(const ss_counter* c);
+
+/* Encode + count a fixed-length batch (L <= 32).  Read i gets global index base_index + i. */
+int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L,
+                            uint64_t stride, uint64_t base_index, uint64_t* d_first_bad, void* stream);
+
+/* Merge already-counted entries (e.g. received from other GPUs): counts add, first index = min. */
+int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_lens,
+                     const uint64_t* d_counts, const uint64_t* d_first, uint64_t m, void* stream);
+
+/* Fix the key length of an empty handle (also done by the first insert); -1 from ss_counter_length
+ * means not fixed yet. */
+int ss_counter_set_length(ss_counter* c, uint32_t L);
+int ss_counter_length(const ss_counter* c);
+
+/* Copy the handle's overflow word to *d_flag (device u64): bit 0 = table full during an insert or
+ * merge, bit 1 = an extract found more entries than `cap`.  Nonzero means the result is invalid. */
+int ss_counter_overflow(ss_counter* c, uint64_t* d_flag, void* stream);
+
+/* Number of occupied slots -> *d_size (device u64). */
+int ss_counter_size(ss_counter* c, uint64_t* d_size, void* stream);
+
+/* Compact the table into arrays of capacity `cap` (>= size).  Entries are grouped by owner
+ * (hash % n_parts); d_part_counts[n_parts] receives the entries per part, in part order.
+ * n_parts = 1 gives a plain compaction.  Order inside a part is unspecified (sort by first index
+ * on the host to recover insertion order). */
+int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens,
+                       uint64_t* d_counts, uint64_t* d_first, uint64_t cap,
+                       uint64_t* d_part_counts, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):
+ * read i word w: r = splitmix64(seed + i*W + w) masked to its nts, byte j = "ACTG"[(r >> 2j) & 3].
+ * Pool variant: read i is pool item splitmix64(pool_seed ^ (i * 0xD1B54A32D192ED03)) % U.
+ * ---------------------------------------------------------------------------------------------- */
+int ss_synth_reads(uint8_t* d_ascii, uint64_t seed, uint64_t i0, uint64_t n, uint32_t L,
+                   uint64_t stride, void* stream);
+int ss_synth_pool_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, uint64_t U,
+                        uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Host codec (per-object path, no GPU): the drop-in Python objects use these for single reads,
+ * where a kernel launch (~µs) would cost more than the work (SURVEY §7 hard parts).
+ * ---------------------------------------------------------------------------------------------- */
+int ss_host_encode(const uint8_t* h_seq, uint64_t L, uint64_t* h_words, ss_err* h_err);
+void ss_host_decode(const uint64_t* h_words, uint64_t L, char* h_out);
+uint64_t ss_host_hamming(const uint64_t* h_a, const uint64_t* h_b, uint64_t L);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHORTSEQ_AMD_H */

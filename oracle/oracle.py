@@ -1,0 +1,222 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes/numpy wrapper around oracle/liboracle.so.
+
+The oracle is the checker: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+import this module.  shortseq_amd/ never imports it (tests/test_boundary.py enforces that).
+
+Functions mirror oracle/ss_oracle.c (which cites the reference file:line of every rule).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+REF_DIR = os.path.join(HERE, "_ref")
+
+
+class OraErr(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("nbytes", C.c_int32),
+                ("read_index", C.c_int64), ("byte_offset", C.c_int64)]
+
+
+def build() -> None:
+    """Compile liboracle.so (gcc) and, when /root/reference exists, the reference into _ref/."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    if os.path.isdir("/root/reference"):
+        subprocess.run([os.path.join(HERE, "build_ref.sh")], check=True,
+                       stdout=subprocess.DEVNULL)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P, U64, U32, I64 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int64
+        L.ora_encode.argtypes = [P, U32, P, C.POINTER(OraErr)]
+        L.ora_encode.restype = C.c_int
+        L.ora_words_for.argtypes = [U32]
+        L.ora_words_for.restype = U32
+        L.ora_decode.argtypes = [P, U32, P]
+        L.ora_hamming.argtypes = [P, P, U32]
+        L.ora_hamming.restype = U32
+        L.ora_encode_batch.argtypes = [P, U64, U32, U64, P, U32, C.POINTER(OraErr)]
+        L.ora_encode_batch.restype = C.c_int
+        L.ora_decode_batch.argtypes = [P, U64, U32, U32, P, U64]
+        L.ora_hamming_ref_batch.argtypes = [P, U64, U32, U32, P, P]
+        L.ora_hamming_pair_batch.argtypes = [P, P, U64, U32, U32, P]
+        L.ora_gen_word.argtypes = [U64, U64, U32, U32]
+        L.ora_gen_word.restype = U64
+        L.ora_gen_reads.argtypes = [U64, U64, U64, U32, U64, P]
+        L.ora_pool_index.argtypes = [U64, U64, U64]
+        L.ora_pool_index.restype = U64
+        L.ora_gen_pool_reads.argtypes = [U64, U64, U64, U64, U64, U32, U64, P]
+        L.ora_count.argtypes = [P, P, P, U64, P, P, P, P, C.POINTER(OraErr)]
+        L.ora_count.restype = I64
+        _lib = L
+    return _lib
+
+
+_plib = None
+
+
+def plib():
+    """Second handle (PyDLL: the GIL stays held) for the calls into the reference's own kernels,
+    which take the GIL to raise on an invalid byte."""
+    global _plib
+    if _plib is None:
+        lib()
+        L = C.PyDLL(LIB_PATH)
+        P, U64, U32 = C.c_void_p, C.c_uint64, C.c_uint32
+        L.ref_encode64_batch.argtypes = [P, P, U64, U32, U64, P]
+        L.ref_encode_array_batch.argtypes = [P, P, U64, U32, U64, P, U32]
+        _plib = L
+    return _plib
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def words_for(L: int) -> int:
+    return (L + 31) // 32
+
+
+def wpr_for(L: int) -> int:
+    """Words a read of length L occupies in batch layouts (1 for L <= 32, incl. L == 0)."""
+    return max(1, words_for(L))
+
+
+def encode_one(seq: bytes, wpr: int | None = None):
+    """Encode one read like shortseq._new. Returns (words ndarray[uint64], OraErr)."""
+    L = len(seq)
+    n = wpr if wpr is not None else max(3 if 33 <= L <= 96 else 1, words_for(L))
+    out = np.zeros(max(n, 32), dtype=np.uint64)
+    buf = np.frombuffer(seq, dtype=np.uint8) if L else np.zeros(1, np.uint8)
+    err = OraErr()
+    lib().ora_encode(_p(buf), L, _p(out), C.byref(err))
+    return out[:n], err
+
+
+def encode_batch(ascii: np.ndarray, n: int, L: int, stride: int | None = None, wpr: int | None = None):
+    stride = L if stride is None else stride
+    wpr = wpr_for(L) if wpr is None else wpr
+    out = np.zeros(n * wpr, dtype=np.uint64)
+    err = OraErr()
+    rc = lib().ora_encode_batch(_p(ascii), n, L, stride, _p(out), wpr, C.byref(err))
+    return out.reshape(n, wpr), rc, err
+
+
+def decode_batch(words: np.ndarray, n: int, L: int, wpr: int | None = None) -> np.ndarray:
+    wpr = wpr_for(L) if wpr is None else wpr
+    out = np.zeros(max(1, n * L), dtype=np.uint8)
+    w = np.ascontiguousarray(words, dtype=np.uint64)
+    lib().ora_decode_batch(_p(w), n, L, wpr, _p(out), L)
+    return out[: n * L]
+
+
+def hamming_ref_batch(words: np.ndarray, n: int, L: int, ref: np.ndarray, wpr: int | None = None):
+    wpr = wpr_for(L) if wpr is None else wpr
+    out = np.zeros(n, dtype=np.uint32)
+    w = np.ascontiguousarray(words, dtype=np.uint64)
+    r = np.ascontiguousarray(ref, dtype=np.uint64)
+    lib().ora_hamming_ref_batch(_p(w), n, L, wpr, _p(r), _p(out))
+    return out
+
+
+def hamming_pair_batch(a: np.ndarray, b: np.ndarray, n: int, L: int, wpr: int | None = None):
+    wpr = wpr_for(L) if wpr is None else wpr
+    out = np.zeros(n, dtype=np.uint32)
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    b = np.ascontiguousarray(b, dtype=np.uint64)
+    lib().ora_hamming_pair_batch(_p(a), _p(b), n, L, wpr, _p(out))
+    return out
+
+
+def gen_reads(seed: int, i0: int, n: int, L: int, stride: int | None = None) -> np.ndarray:
+    stride = L if stride is None else stride
+    out = np.zeros(max(1, n * stride), dtype=np.uint8)
+    lib().ora_gen_reads(seed, i0, n, L, stride, _p(out))
+    return out[: n * stride]
+
+
+def gen_words(seed: int, i0: int, n: int, L: int) -> np.ndarray:
+    """Known-answer words of gen_reads (the generator's r values, masked)."""
+    W = words_for(L)
+    f = lib().ora_gen_word
+    return np.array([[f(seed, i0 + k, L, w) for w in range(W)] for k in range(n)], dtype=np.uint64)
+
+
+def gen_pool_reads(seed: int, pool_seed: int, U: int, i0: int, n: int, L: int) -> np.ndarray:
+    out = np.zeros(max(1, n * L), dtype=np.uint8)
+    lib().ora_gen_pool_reads(seed, pool_seed, U, i0, n, L, L, _p(out))
+    return out[: n * L]
+
+
+def count(reads):
+    """Counter oracle over a list of bytes.  Returns [(words tuple, L, count, first_index)] in
+    first-occurrence order, or raises ValueError(err) on the first invalid read."""
+    n = len(reads)
+    lens = np.array([len(r) for r in reads], dtype=np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(reads) or b"\0", dtype=np.uint8)
+    uw = np.zeros(max(1, n) * 32, dtype=np.uint64)
+    ul = np.zeros(max(1, n), dtype=np.uint32)
+    uc = np.zeros(max(1, n), dtype=np.uint64)
+    uf = np.zeros(max(1, n), dtype=np.uint64)
+    err = OraErr()
+    nu = lib().ora_count(_p(blob), _p(offs), _p(lens), n, _p(uw), _p(ul), _p(uc), _p(uf), C.byref(err))
+    if nu < 0:
+        raise ValueError((err.kind, err.read_index, err.byte_offset, err.nbytes))
+    res = []
+    for u in range(nu):
+        L = int(ul[u])
+        nw = 1 if L <= 32 else words_for(L)
+        res.append((tuple(int(x) for x in uw[32 * u: 32 * u + nw]), L, int(uc[u]), int(uf[u])))
+    return res
+
+
+# --- the reference's own kernels (oracle/_ref), for validation and the CPU baseline -------------
+
+def ref_available() -> bool:
+    return os.path.isdir(os.path.join(REF_DIR, "shortseq"))
+
+
+def ref_kernel_ptrs():
+    """Raw function pointers of the reference's capsule-exported encode kernels."""
+    import importlib
+    import sys
+    if REF_DIR not in sys.path:
+        sys.path.insert(0, REF_DIR)
+    m64 = importlib.import_module("shortseq.short_seq_64")
+    util = importlib.import_module("shortseq.util")
+    get = C.pythonapi.PyCapsule_GetPointer
+    get.restype = C.c_void_p
+    get.argtypes = [C.py_object, C.c_char_p]
+    cap64 = m64.__pyx_capi__["_marshall_bytes_64"]
+    capar = util.__pyx_capi__["_marshall_bytes_array"]
+    p64 = get(cap64, b"uint64_t (uint8_t *, uint8_t)")
+    par = get(capar, b"void (uint64_t *, uint8_t *, size_t)")
+    return p64, par
+
+
+def ref_encode_batch(ascii: np.ndarray, n: int, L: int, wpr: int | None = None) -> np.ndarray:
+    """Encode a valid fixed-length batch with the reference's own compiled kernels."""
+    wpr = wpr_for(L) if wpr is None else wpr
+    out = np.zeros(n * wpr, dtype=np.uint64)
+    p64, par = ref_kernel_ptrs()
+    if L <= 32:
+        plib().ref_encode64_batch(p64, _p(ascii), n, L, L, _p(out))
+    else:
+        plib().ref_encode_array_batch(par, _p(ascii), n, L, L, _p(out), wpr)
+    return out.reshape(n, wpr)

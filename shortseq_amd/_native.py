@@ -1,0 +1,88 @@
+"""ctypes binding of lib/libshortseq_amd.so — the C ABI declared in include/shortseq_amd.h.
+
+There is no fallback: if the library is missing or fails to load, every GPU entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .build import LIB
+
+SS_OK = 0
+SS_EINVALID_BASE = 1
+SS_ETOO_LONG = 2
+SS_EARG = -1
+SS_EHIP = -2
+SS_ENOMEM = -3
+SS_EFULL = -4
+
+
+class SsErr(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("nbytes", C.c_int32),
+                ("read_index", C.c_int64), ("byte_offset", C.c_int64)]
+
+
+class NativeError(RuntimeError):
+    """A C-ABI call failed (argument or HIP runtime error)."""
+
+
+# (name, restype, argtypes) for every exported symbol of include/shortseq_amd.h
+_P, _U64, _U32, _I32, _SZ = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int32, C.c_size_t
+SIGNATURES = [
+    ("ss_abi_version", C.c_int, []),
+    ("ss_last_error_string", C.c_char_p, []),
+    ("ss_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("ss_set_device", C.c_int, [C.c_int]),
+    ("ss_pinned_alloc", C.c_int, [C.POINTER(C.c_void_p), _SZ]),
+    ("ss_pinned_free", C.c_int, [_P]),
+    ("ss_encode_fixed", C.c_int, [_P, _U64, _U32, _U64, _P, _U32, _P, _P]),
+    ("ss_encode_var", C.c_int, [_P, _P, _P, _U64, _P, _U32, _P, _P]),
+    ("ss_decode_fixed", C.c_int, [_P, _U64, _U32, _U32, _P, _U64, _P]),
+    ("ss_decode_var", C.c_int, [_P, _P, _U64, _U32, _P, _P, _P]),
+    ("ss_hamming_ref", C.c_int, [_P, _U64, _U32, _U32, _P, _P, _P]),
+    ("ss_hamming_pair", C.c_int, [_P, _P, _U64, _U32, _U32, _P, _P]),
+    ("ss_encode_hamming_ref", C.c_int, [_P, _U64, _U32, _U64, _P, _U32, _P, _P, _P, _P]),
+    ("ss_counter_create", C.c_int, [_U64, C.POINTER(C.c_void_p)]),
+    ("ss_counter_destroy", C.c_int, [_P]),
+    ("ss_counter_reset", C.c_int, [_P, _P]),
+    ("ss_counter_capacity", _U64, [_P]),
+    ("ss_counter_insert_fixed", C.c_int, [_P, _P, _U64, _U32, _U64, _U64, _P, _P]),
+    ("ss_counter_merge", C.c_int, [_P, _P, _P, _P, _P, _U64, _P]),
+    ("ss_counter_set_length", C.c_int, [_P, _U32]),
+    ("ss_counter_length", C.c_int, [_P]),
+    ("ss_counter_overflow", C.c_int, [_P, _P, _P]),
+    ("ss_counter_size", C.c_int, [_P, _P, _P]),
+    ("ss_counter_extract", C.c_int, [_P, _U32, _P, _P, _P, _P, _U64, _P, _P]),
+    ("ss_synth_reads", C.c_int, [_P, _U64, _U64, _U64, _U32, _U64, _P]),
+    ("ss_synth_pool_reads", C.c_int, [_P, _U64, _U64, _U64, _U64, _U64, _U32, _U64, _P]),
+    ("ss_host_encode", C.c_int, [_P, _U64, _P, C.POINTER(SsErr)]),
+    ("ss_host_decode", None, [_P, _U64, _P]),
+    ("ss_host_hamming", _U64, [_P, _P, _U64]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (building it first if this is a dev checkout without it)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            from .build import build_hip
+            build_hip()
+        L = C.CDLL(LIB)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        if L.ss_abi_version() != 1:
+            raise NativeError("libshortseq_amd ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SS_OK:
+        msg = lib().ss_last_error_string().decode(errors="replace")
+        raise NativeError(f"{what} failed (status {rc}): {msg}")

@@ -1,0 +1,344 @@
+"""Batch API on the GPU — torch CUDA tensors in, torch CUDA tensors out, one HIP kernel per call.
+
+This is the data-parallel hot path behind the C ABI in
+include/shortseq_amd.h.  PyTorch only provides device memory, streams and the caching allocator;
+every byte of encode / decode / hamming / counting is done by the HIP kernels in csrc/.
+
+Packed words are returned as int64 tensors holding the raw 64-bit patterns (view them as uint64 on
+the host: ``t.cpu().numpy().view(np.uint64)``).  Layout: read i -> words[i, 0:wpr], nt j in word
+j // 32 at bits 2*(j % 32), codes A=0 C=1 T=2 G=3 (README.md:101-112).
+
+Errors: a batch containing a read the reference would reject raises the reference's exception for
+the FIRST such read in input order (the one ShortSeqCounter's loop, counter.pyx:22-29, would hit):
+``Exception("Unsupported base character: X")`` / ``UnicodeDecodeError`` / ``Exception("Sequences
+longer than 1024 bases are not supported.")``, with ``.read_index`` set.  The kernels only flag the
+read; its exact message comes from re-scanning that one read with the host codec.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ._native import SsErr, check, lib
+
+MAX_NT = 1024
+_NO_BAD = -1  # UINT64_MAX viewed as int64
+
+__all__ = ["words_for", "wpr_for", "encode", "encode_var", "decode", "decode_var", "hamming_ref",
+           "hamming_pair", "encode_hamming_ref", "synth_reads", "synth_pool_reads", "GpuCounter",
+           "raise_read_error", "first_bad_buffer"]
+
+
+def words_for(L: int) -> int:
+    """ceil(L / 32): util.pyx:30-33."""
+    return (L + 31) // 32
+
+
+def wpr_for(L: int) -> int:
+    """Words per read in batch layouts: 1 for L <= 32 (ShortSeq64 keeps one word even for L = 0)."""
+    return max(1, words_for(L))
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _require_cuda(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA (HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+_first_bad_cache: dict = {}
+
+
+def first_bad_buffer(dev: torch.device) -> torch.Tensor:
+    """Per-device 1-word scratch the kernels atomicMin the first invalid read index into."""
+    key = (dev.type, dev.index)
+    t = _first_bad_cache.get(key)
+    if t is None:
+        t = torch.empty(1, dtype=torch.int64, device=dev)
+        _first_bad_cache[key] = t
+    return t
+
+
+def raise_read_error(read: bytes, read_index: int) -> None:
+    """Raise exactly what shortseq.pack(read) raises in the reference (SURVEY §8 error contract)."""
+    if len(read) > MAX_NT:
+        e = Exception(f"Sequences longer than {MAX_NT} bases are not supported.")  # short_seq.pyx:74
+        e.read_index = read_index
+        raise e
+    buf = np.frombuffer(read, dtype=np.uint8) if read else np.zeros(1, np.uint8)
+    words = np.zeros(32, dtype=np.uint64)
+    err = SsErr()
+    rc = lib().ss_host_encode(buf.ctypes.data, len(read), words.ctypes.data, C.byref(err))
+    if rc == 0:
+        raise AssertionError(f"read {read_index} was flagged by the GPU but encodes on the host")
+    bad = read[err.byte_offset: err.byte_offset + err.nbytes]
+    # short_seq_64.pyx:105 / util.pyx:115,137 — PyUnicode_DecodeASCII of the byte(s); a non-ASCII
+    # byte makes that decode itself raise UnicodeDecodeError, as in the reference.
+    e = Exception(f"Unsupported base character: {bad.decode('ascii')}")
+    e.read_index = read_index
+    raise e
+
+
+def _check_first_bad(fb: torch.Tensor, fetch_read) -> None:
+    v = int(fb.item())
+    if v != _NO_BAD:
+        raise_read_error(fetch_read(v), v)
+
+
+def _as_rows(ascii: torch.Tensor, L: Optional[int], stride: Optional[int]):
+    _require_cuda(ascii, "ascii")
+    if ascii.dtype != torch.uint8:
+        raise TypeError("ascii must be a uint8 tensor")
+    if ascii.dim() == 2:
+        n, width = ascii.shape
+        L = width if L is None else L
+        stride = width if stride is None else stride
+        if stride != width:
+            raise ValueError("for a 2-D ascii tensor the stride is its row width")
+    else:
+        if L is None:
+            raise ValueError("L is required for a flat ascii tensor")
+        stride = L if stride is None else stride
+        n = ascii.numel() // stride if stride else 0
+    if not (1 <= L <= MAX_NT):
+        if L > MAX_NT:
+            raise Exception(f"Sequences longer than {MAX_NT} bases are not supported.")
+        raise ValueError("L must be >= 1 (empty reads are the empty singleton, no kernel needed)")
+    if stride < L:
+        raise ValueError("stride < L")
+    return n, L, stride
+
+
+def _fetch_row(ascii: torch.Tensor, stride: int, L: int):
+    flat = ascii.reshape(-1)
+    return lambda i: bytes(flat[i * stride: i * stride + L].cpu().numpy())
+
+
+def encode(ascii: torch.Tensor, L: Optional[int] = None, *, stride: Optional[int] = None,
+           wpr: Optional[int] = None, out: Optional[torch.Tensor] = None,
+           check_errors: bool = True) -> torch.Tensor:
+    """Encode a fixed-length batch (one ss_encode_fixed launch).  ascii: uint8 [n, L] or flat."""
+    n, L, stride = _as_rows(ascii, L, stride)
+    wpr = wpr_for(L) if wpr is None else wpr
+    dev = ascii.device
+    if out is None:
+        out = torch.empty((n, wpr), dtype=torch.int64, device=dev)
+    fb = first_bad_buffer(dev)
+    check(lib().ss_encode_fixed(ascii.data_ptr(), n, L, stride, out.data_ptr(), wpr, fb.data_ptr(),
+                                _stream(dev)), "ss_encode_fixed")
+    if check_errors:
+        _check_first_bad(fb, _fetch_row(ascii, stride, L))
+    return out
+
+
+def encode_var(blob: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor, *,
+               wpr: Optional[int] = None, out: Optional[torch.Tensor] = None,
+               check_errors: bool = True) -> torch.Tensor:
+    """Encode a ragged batch: read i = blob[offsets[i] : offsets[i] + lens[i]] (0..1024 nt)."""
+    for t, nm in ((blob, "blob"), (offsets, "offsets"), (lens, "lens")):
+        _require_cuda(t, nm)
+    if offsets.dtype != torch.int64 or lens.dtype != torch.int32 or blob.dtype != torch.uint8:
+        raise TypeError("blob uint8, offsets int64, lens int32 expected")
+    n = lens.numel()
+    if wpr is None:
+        wpr = wpr_for(min(int(lens.max().item()), MAX_NT)) if n else 1
+    dev = blob.device
+    if out is None:
+        out = torch.empty((n, wpr), dtype=torch.int64, device=dev)
+    fb = first_bad_buffer(dev)
+    check(lib().ss_encode_var(blob.data_ptr(), offsets.data_ptr(), lens.data_ptr(), n, out.data_ptr(),
+                              wpr, fb.data_ptr(), _stream(dev)), "ss_encode_var")
+    if check_errors:
+        def fetch(i):
+            o, ln = int(offsets[i].item()), int(lens[i].item())
+            return bytes(blob[o:o + ln].cpu().numpy())
+        _check_first_bad(fb, fetch)
+    return out
+
+
+def decode(words: torch.Tensor, L: int, *, wpr: Optional[int] = None,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed words [n, wpr] -> ASCII uint8 [n, L] (one ss_decode_fixed launch)."""
+    _require_cuda(words, "words")
+    wpr = words.shape[1] if words.dim() == 2 else (wpr_for(L) if wpr is None else wpr)
+    n = words.numel() // wpr
+    dev = words.device
+    if out is None:
+        out = torch.empty((n, L), dtype=torch.uint8, device=dev)
+    check(lib().ss_decode_fixed(words.data_ptr(), n, L, wpr, out.data_ptr(), L, _stream(dev)),
+          "ss_decode_fixed")
+    return out
+
+
+def decode_var(words: torch.Tensor, lens: torch.Tensor, offsets: torch.Tensor,
+               out_bytes: Optional[int] = None) -> torch.Tensor:
+    """Ragged decode into one blob; read i lands at blob[offsets[i] : offsets[i] + lens[i]]."""
+    _require_cuda(words, "words")
+    n, wpr = words.shape
+    dev = words.device
+    total = out_bytes if out_bytes is not None else (
+        int((offsets[-1] + lens[-1]).item()) if n else 0)
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    check(lib().ss_decode_var(words.data_ptr(), lens.data_ptr(), n, wpr, out.data_ptr(),
+                              offsets.data_ptr(), _stream(dev)), "ss_decode_var")
+    return out[:total]
+
+
+def hamming_ref(words: torch.Tensor, L: int, ref: torch.Tensor) -> torch.Tensor:
+    """Per-read __xor__ distance to one packed reference read -> int32 [n]."""
+    _require_cuda(words, "words")
+    n, wpr = words.shape
+    out = torch.empty(n, dtype=torch.int32, device=words.device)
+    ref = ref.to(words.device).contiguous()
+    check(lib().ss_hamming_ref(words.data_ptr(), n, L, wpr, ref.data_ptr(), out.data_ptr(),
+                               _stream(words.device)), "ss_hamming_ref")
+    return out
+
+
+def hamming_pair(a: torch.Tensor, b: torch.Tensor, L: int) -> torch.Tensor:
+    """Element-wise a[i] ^ b[i] (ShortSeq.__xor__) -> int32 [n]."""
+    _require_cuda(a, "a")
+    _require_cuda(b, "b")
+    if a.shape != b.shape:
+        raise ValueError("a and b must have the same shape")
+    n, wpr = a.shape
+    out = torch.empty(n, dtype=torch.int32, device=a.device)
+    check(lib().ss_hamming_pair(a.data_ptr(), b.data_ptr(), n, L, wpr, out.data_ptr(), _stream(a.device)),
+          "ss_hamming_pair")
+    return out
+
+
+def encode_hamming_ref(ascii: torch.Tensor, L: Optional[int], ref_words: torch.Tensor, *,
+                       store_words: bool = True, wpr: Optional[int] = None,
+                       check_errors: bool = True):
+    """Fused encode + hamming vs one packed reference: returns (words or None, distances int32)."""
+    n, L, stride = _as_rows(ascii, L, None if ascii.dim() == 2 else L)
+    wpr = wpr_for(L) if wpr is None else wpr
+    dev = ascii.device
+    words = torch.empty((n, wpr), dtype=torch.int64, device=dev) if store_words else None
+    dist = torch.empty(n, dtype=torch.int32, device=dev)
+    ref = ref_words.to(dev).contiguous()
+    if ref.numel() < wpr:
+        ref = torch.cat([ref.reshape(-1), torch.zeros(wpr - ref.numel(), dtype=torch.int64, device=dev)])
+    fb = first_bad_buffer(dev)
+    check(lib().ss_encode_hamming_ref(ascii.data_ptr(), n, L, stride, _ptr(words), wpr, ref.data_ptr(),
+                                      dist.data_ptr(), fb.data_ptr(), _stream(dev)),
+          "ss_encode_hamming_ref")
+    if check_errors:
+        _check_first_bad(fb, _fetch_row(ascii, stride, L))
+    return words, dist
+
+
+def synth_reads(n: int, L: int, seed: int, *, i0: int = 0, device=None, stride: Optional[int] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Device-side synthetic reads (SURVEY §8(d) generator, bit-identical to the oracle's)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    stride = L if stride is None else stride
+    if out is None:
+        out = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    check(lib().ss_synth_reads(out.data_ptr(), seed, i0, n, L, stride, _stream(dev)), "ss_synth_reads")
+    return out
+
+
+def synth_pool_reads(n: int, L: int, seed: int, pool_seed: int, U: int, *, i0: int = 0, device=None,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if out is None:
+        out = torch.empty((n, L), dtype=torch.uint8, device=dev)
+    check(lib().ss_synth_pool_reads(out.data_ptr(), seed, pool_seed, U, i0, n, L, L, _stream(dev)),
+          "ss_synth_pool_reads")
+    return out
+
+
+class GpuCounter:
+    """Dedup counter in HBM for reads of ONE length L <= 32 (ShortSeqCounter's hot loop,
+    counter.pyx:41-54).  Counts and first-occurrence indices per distinct packed word."""
+
+    def __init__(self, capacity: int, device=None):
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().ss_counter_create(capacity, C.byref(h)), "ss_counter_create")
+        self._h = h
+        self.capacity = int(lib().ss_counter_capacity(h))
+        self._scratch = torch.empty(2, dtype=torch.int64, device=self.device)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().ss_counter_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 — interpreter shutdown
+            pass
+
+    @property
+    def length(self) -> int:
+        return int(lib().ss_counter_length(self._h))
+
+    def reset(self) -> None:
+        check(lib().ss_counter_reset(self._h, _stream(self.device)), "ss_counter_reset")
+
+    def insert(self, ascii: torch.Tensor, L: Optional[int] = None, *, base_index: int = 0,
+               stride: Optional[int] = None, check_errors: bool = True) -> None:
+        n, L, stride = _as_rows(ascii, L, stride)
+        fb = first_bad_buffer(self.device)
+        check(lib().ss_counter_insert_fixed(self._h, ascii.data_ptr(), n, L, stride, base_index,
+                                            fb.data_ptr(), _stream(self.device)), "ss_counter_insert_fixed")
+        if check_errors:
+            _check_first_bad(fb, _fetch_row(ascii, stride, L))
+
+    def merge(self, keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, L: int) -> None:
+        m = keys.numel()
+        check(lib().ss_counter_set_length(self._h, L), "ss_counter_set_length")
+        check(lib().ss_counter_merge(self._h, keys.data_ptr(), None, counts.data_ptr(), first.data_ptr(), m,
+                                     _stream(self.device)), "ss_counter_merge")
+
+    def size(self) -> int:
+        check(lib().ss_counter_size(self._h, self._scratch.data_ptr(), _stream(self.device)), "ss_counter_size")
+        return int(self._scratch[0].item())
+
+    def overflowed(self) -> bool:
+        check(lib().ss_counter_overflow(self._h, self._scratch[1:].data_ptr(), _stream(self.device)),
+              "ss_counter_overflow")
+        return int(self._scratch[1].item()) != 0
+
+    def extract(self, n_parts: int = 1, cap: Optional[int] = None):
+        """Occupied slots grouped by owner part -> (keys, lens, counts, first, part_counts), all on
+        the device; arrays sized `cap` (default: capacity + 1), valid prefix = part_counts.sum()."""
+        cap = self.capacity + 1 if cap is None else cap
+        d = self.device
+        keys = torch.empty(cap, dtype=torch.int64, device=d)
+        lens = torch.empty(cap, dtype=torch.int32, device=d)
+        counts = torch.empty(cap, dtype=torch.int64, device=d)
+        first = torch.empty(cap, dtype=torch.int64, device=d)
+        parts = torch.empty(n_parts, dtype=torch.int64, device=d)
+        check(lib().ss_counter_extract(self._h, n_parts, keys.data_ptr(), lens.data_ptr(), counts.data_ptr(),
+                                       first.data_ptr(), cap, parts.data_ptr(), _stream(d)), "ss_counter_extract")
+        return keys, lens, counts, first, parts
+
+    def items_sorted(self):
+        """Host copy of (keys u64, counts, first) sorted by first occurrence (= dict order)."""
+        keys, lens, counts, first, parts = self.extract(1)
+        m = int(parts.sum().item())
+        if self.overflowed():
+            raise RuntimeError("GPU counter table overflowed; use a larger capacity")
+        k = keys[:m].cpu().numpy().view(np.uint64)
+        c = counts[:m].cpu().numpy()
+        f = first[:m].cpu().numpy()
+        o = np.argsort(f, kind="stable")
+        return k[o], c[o], f[o]

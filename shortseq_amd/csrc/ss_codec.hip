@@ -1,0 +1,455 @@
+// ss_codec.hip — batch 2-bit encode / decode / hamming / synthetic-read kernels for gfx950.
+//
+// Kernel families:
+//   k_encode_g16   fast path, L % 16 == 0: one lane per 16-byte ASCII chunk (one dwordx4 load,
+//                  fully coalesced), one u32 half-word out per lane.  Lanes are grouped per read in
+//                  power-of-two groups of G >= 2*wpr lanes so carries (table path) move by one
+//                  __shfl_xor and per-read sums (fused hamming) reduce inside the group.
+//   k_encode_gen   any L / stride / variable lengths: one lane per output word, aligned dword
+//                  loads + v_alignbyte; the general and ragged path.
+//   k_decode_g16 / k_decode_gen, k_ham_group, k_synth_*.
+#include "ss_device.h"
+#include "ss_internal.h"
+
+namespace {
+
+using namespace ssd;
+
+constexpr int kThreads = 256;
+
+__host__ __device__ inline uint32_t words_for(uint32_t L) { return (L + 31u) / 32u; }
+__host__ __device__ inline uint32_t ham_words(uint32_t L) { return L <= 32u ? 1u : words_for(L); }
+
+inline uint32_t log2_ceil(uint32_t x) {
+    uint32_t l = 0;
+    while ((1u << l) < x) ++l;
+    return l;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fast path.  Lane slot g -> read r = g >> logG, chunk k = g & (G-1).  Chunks k < cpr carry data;
+// lanes cpr <= k < wpr2 produce the zero (or carry-only) padding half-words.
+//   table path for chunk k iff L <= 32 (short_seq.pyx:57) or k >= full2 (tail block, util.pyx:92)
+// ------------------------------------------------------------------------------------------------
+struct G16Args {
+    const uint4* in;          // 16-B aligned
+    uint64_t in_stride16;     // read stride in 16-B chunks
+    uint32_t* out32;          // packed words viewed as u32 half-words (may be null: no store)
+    uint32_t wpr2;            // 2 * words per read
+    uint64_t n;
+    uint32_t cpr;             // L / 16
+    uint32_t full2;           // 2 * (L / 32): chunks that belong to full PEXT blocks
+    uint32_t all_table;       // L <= 32
+    uint32_t logG;
+    const uint32_t* ref32;    // fused hamming: reference half-words (wpr2 of them)
+    uint32_t ham2;            // 2 * ham_words(L)
+    uint32_t* counts;
+    unsigned long long* first_bad;
+};
+
+// DENSE: stride == L, wpr == L/32, L % 32 == 0 -> lane slot g IS the chunk index and the u32
+// output index (no per-lane read/chunk arithmetic, a pure 16 B -> 4 B stream).
+template <bool HAM, bool DENSE, int U>
+__global__ __launch_bounds__(kThreads) void k_encode_g16(G16Args a) {
+    const uint32_t G = 1u << a.logG;
+    const uint64_t base = (uint64_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+    const uint64_t nslots = DENSE ? a.n * a.cpr : 0;
+    uint4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * kThreads;
+        if constexpr (DENSE) {
+            x[j] = g < nslots ? ld_stream(&a.in[g]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+        } else {
+            const uint64_t r = g >> a.logG;
+            const uint32_t k = (uint32_t)g & (G - 1u);
+            if (r < a.n && k < a.cpr)
+                x[j] = ld_stream(&a.in[r * a.in_stride16 + k]);
+            else
+                x[j] = make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);  // "AAAA": code 0, valid
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t r = g >> a.logG;
+        const uint32_t k = (uint32_t)g & (G - 1u);
+        const bool table = a.all_table || k >= a.full2;
+        Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, table);
+        const uint32_t cin = swap_pair(e.cout);
+        const uint32_t v = e.v | ((k & 1u) ? cin : 0u);
+        const bool live = DENSE ? g < nslots : r < a.n;
+        report_bad(live && e.bad != 0u, r, a.first_bad);
+        if constexpr (DENSE) {
+            if (a.out32 && live) a.out32[g] = v;
+        } else {
+            if (a.out32 && live && k < a.wpr2) a.out32[r * a.wpr2 + k] = v;
+        }
+        if constexpr (HAM) {
+            uint32_t part = (k < a.ham2) ? ham32(v ^ a.ref32[k]) : 0u;
+            for (uint32_t s = 1; s < G; s <<= 1) part += __shfl_xor(part, s);
+            if (live && k == 0) a.counts[r] = part;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// General path: one lane per (read, word).  Bytes come from aligned dword loads (only dwords that
+// hold at least one byte of the read) realigned with v_alignbyte; bytes past the read are replaced
+// by 'A' (code 0, no carry), so the tail word's Q1 carry lands at bit 2*nb exactly as the reference.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t encode_word_at(const uint8_t* p, uint32_t nb, bool table, uint32_t& bad) {
+    const uintptr_t addr = (uintptr_t)p;
+    const uint32_t* d = (const uint32_t*)(addr & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(addr & 3);
+    const uint32_t nd = (sh + nb + 3u) >> 2;
+    uint32_t dw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dw[i] = ((uint32_t)i < nd) ? d[i] : 0x41414141u;
+    uint32_t xw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t v = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
+        const int m = (int)nb - 4 * i;
+        if (m <= 0) {
+            v = 0x41414141u;
+        } else if (m < 4) {
+            const uint32_t keep = (1u << (8 * m)) - 1u;
+            v = (v & keep) | (0x41414141u & ~keep);
+        }
+        xw[i] = v;
+    }
+    Enc32 lo = encode16(xw[0], xw[1], xw[2], xw[3], table);
+    Enc32 hi = encode16(xw[4], xw[5], xw[6], xw[7], table);
+    bad |= lo.bad | hi.bad;
+    return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
+}
+
+template <bool VAR>
+__global__ __launch_bounds__(kThreads) void k_encode_gen(const uint8_t* in, uint64_t stride,
+                                                         const uint64_t* offs, const uint32_t* lens,
+                                                         uint32_t Lfix, uint64_t n, uint64_t* out,
+                                                         uint32_t wpr, unsigned long long* first_bad) {
+    const uint64_t total = n * wpr;
+    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * kThreads) {
+        const uint64_t r = g / wpr;
+        const uint32_t w = (uint32_t)(g - r * wpr);
+        const uint32_t L = VAR ? lens[r] : Lfix;
+        const uint64_t off = VAR ? offs[r] : r * stride;
+        uint32_t bad = 0;
+        uint64_t word = 0;
+        if (L > SS_MAX_NT) {
+            bad = (w == 0);                     // short_seq.pyx:74 (too long) — reported per read
+        } else if (32u * w < L) {
+            const uint32_t nb = min(32u, L - 32u * w);
+            const bool table = (L <= 32u) || (nb < 32u);
+            word = encode_word_at(in + off + 32u * w, nb, table, bad);
+        }
+        out[g] = word;
+        if (bad) atomicMin(first_bad, (unsigned long long)r);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Decode
+// ------------------------------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(kThreads) void k_decode_g16(const uint32_t* __restrict__ w32, uint32_t wpr2,
+                                                         uint64_t n, uint32_t cpr, uint32_t logG,
+                                                         uint4* __restrict__ out, uint64_t out_stride16) {
+    const uint32_t G = 1u << logG;
+    const uint64_t base = (uint64_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+    uint32_t v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t r = g >> logG;
+        const uint32_t k = (uint32_t)g & (G - 1u);
+        v[j] = (r < n && k < cpr) ? __builtin_nontemporal_load(&w32[r * wpr2 + k]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t r = g >> logG;
+        const uint32_t k = (uint32_t)g & (G - 1u);
+        if (r < n && k < cpr) out[r * out_stride16 + k] = decode16(v[j]);
+    }
+}
+
+__device__ __forceinline__ void store_chars(uint8_t* dst, uint64_t word, uint32_t nb) {
+    const uint32_t lo = (uint32_t)word, hi = (uint32_t)(word >> 32);
+    const uint4 a = decode16(lo), b = decode16(hi);
+    const uint32_t c[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if ((((uintptr_t)dst) & 3) == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = (int)nb - 4 * i;
+            if (m >= 4) {
+                *(uint32_t*)(dst + 4 * i) = c[i];
+            } else if (m > 0) {
+                for (int b2 = 0; b2 < m; ++b2) dst[4 * i + b2] = (uint8_t)(c[i] >> (8 * b2));
+            }
+        }
+    } else {
+        for (uint32_t i = 0; i < nb; ++i) dst[i] = (uint8_t)(c[i >> 2] >> (8 * (i & 3)));
+    }
+}
+
+template <bool VAR>
+__global__ __launch_bounds__(kThreads) void k_decode_gen(const uint64_t* words, const uint32_t* lens,
+                                                         uint32_t Lfix, uint64_t n, uint32_t wpr,
+                                                         uint8_t* out, uint64_t stride, const uint64_t* offs) {
+    const uint64_t total = n * wpr;
+    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * kThreads) {
+        const uint64_t r = g / wpr;
+        const uint32_t w = (uint32_t)(g - r * wpr);
+        const uint32_t L = VAR ? lens[r] : Lfix;
+        if (L > SS_MAX_NT || 32u * w >= L) continue;
+        const uint32_t nb = min(32u, L - 32u * w);
+        const uint64_t off = VAR ? offs[r] : r * stride;
+        store_chars(out + off + 32u * w, words[g], nb);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Hamming on packed words: lane per word, power-of-two lane groups per read, shfl_xor reduction.
+// ------------------------------------------------------------------------------------------------
+template <bool PAIR>
+__global__ __launch_bounds__(kThreads) void k_ham_group(const uint64_t* __restrict__ a,
+                                                        const uint64_t* __restrict__ b, uint64_t n,
+                                                        uint32_t W, uint32_t wpr, uint32_t logG,
+                                                        uint32_t* __restrict__ out) {
+    const uint32_t G = 1u << logG;
+    const uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    const uint64_t r = g >> logG;
+    const uint32_t k = (uint32_t)g & (G - 1u);
+    uint32_t part = 0;
+    if (r < n && k < W) {
+        const uint64_t x = a[r * wpr + k] ^ (PAIR ? b[r * wpr + k] : b[k]);
+        part = ham64(x);
+    }
+    for (uint32_t s = 1; s < G; s <<= 1) part += __shfl_xor(part, s);
+    if (r < n && k == 0) out[r] = part;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Synthetic reads; lane per (read, word).
+// ------------------------------------------------------------------------------------------------
+template <bool POOL>
+__global__ __launch_bounds__(kThreads) void k_synth(uint8_t* out, uint64_t seed, uint64_t pool_seed,
+                                                    uint64_t U, uint64_t i0, uint64_t n, uint32_t L,
+                                                    uint64_t stride) {
+    const uint32_t W = words_for(L);
+    const uint64_t total = n * W;
+    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * kThreads) {
+        const uint64_t k = g / W;
+        const uint32_t w = (uint32_t)(g - k * W);
+        uint64_t id = i0 + k;
+        if (POOL) id = splitmix64(pool_seed ^ (id * 0xD1B54A32D192ED03ull)) % U;
+        const uint32_t nb = min(32u, L - 32u * w);
+        uint64_t r = splitmix64(seed + id * W + w);
+        if (nb < 32u) r &= (1ull << (2 * nb)) - 1ull;
+        uint8_t* dst = out + k * stride + 32u * w;
+        if ((((uintptr_t)dst) & 15) == 0 && (nb & 15u) == 0) {
+            ((uint4*)dst)[0] = decode16((uint32_t)r);
+            if (nb == 32u) ((uint4*)dst)[1] = decode16((uint32_t)(r >> 32));
+        } else {
+            store_chars(dst, r, nb);
+        }
+    }
+}
+
+inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap = 0) {
+    uint64_t b = (items + per_block - 1) / per_block;
+    if (b == 0) b = 1;
+    if (cap && b > cap) b = cap;
+    return (unsigned)b;
+}
+
+constexpr unsigned kGenGridCap = 256u * 16u;   // grid-stride general kernels: 16 blocks per CU
+
+}  // namespace
+
+// ==================================================================================================
+// C ABI
+// ==================================================================================================
+extern "C" {
+
+static int reset_first_bad(uint64_t* d_first_bad, hipStream_t s) {
+    if (!d_first_bad) return SS_OK;
+    return ss_check(hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s), "reset first_bad");
+}
+
+int ss_encode_fixed_impl(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                         uint64_t* d_words, uint32_t wpr, uint64_t* d_first_bad,
+                         const uint64_t* d_ref_words, uint32_t* d_out, void* stream) {
+    if (L == 0 || L > SS_MAX_NT) return ss_fail(SS_EARG, "L must be in 1..1024");
+    if (wpr < words_for(L) || wpr > 32) return ss_fail(SS_EARG, "wpr must be in ceil(L/32)..32");
+    if (stride < L) return ss_fail(SS_EARG, "stride < L");
+    if (!d_first_bad) return ss_fail(SS_EARG, "d_first_bad is required");
+    if (n && (!d_ascii || (!d_words && !d_out))) return ss_fail(SS_EARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = reset_first_bad(d_first_bad, s);
+    if (rc || n == 0) return rc;
+    const bool ham = d_out != nullptr;
+    if (ham && !d_ref_words) return ss_fail(SS_EARG, "d_ref_words is required for hamming");
+    const bool fast = (L % 16u == 0) && (stride % 16u == 0) && ((((uintptr_t)d_ascii) & 15) == 0) &&
+                      (d_words == nullptr || (((uintptr_t)d_words) & 7) == 0);
+    if (fast) {
+        G16Args a;
+        a.in = (const uint4*)d_ascii;
+        a.in_stride16 = stride / 16;
+        a.out32 = (uint32_t*)d_words;
+        a.wpr2 = 2 * wpr;
+        a.n = n;
+        a.cpr = L / 16;
+        a.full2 = 2 * (L / 32);
+        a.all_table = L <= 32;
+        a.logG = log2_ceil(a.wpr2);
+        a.ref32 = (const uint32_t*)d_ref_words;
+        a.ham2 = 2 * ham_words(L);
+        a.counts = d_out;
+        a.first_bad = (unsigned long long*)d_first_bad;
+        constexpr int U = 4;
+        const bool dense = stride == L && L % 32u == 0 && a.wpr2 == a.cpr && (1u << a.logG) == a.cpr;
+        const uint64_t slots = dense ? n * a.cpr : (n << a.logG);
+        const unsigned grid = grid_for(slots, (uint64_t)U * kThreads);
+        if (ham && dense)
+            hipLaunchKernelGGL((k_encode_g16<true, true, U>), dim3(grid), dim3(kThreads), 0, s, a);
+        else if (ham)
+            hipLaunchKernelGGL((k_encode_g16<true, false, U>), dim3(grid), dim3(kThreads), 0, s, a);
+        else if (dense)
+            hipLaunchKernelGGL((k_encode_g16<false, true, U>), dim3(grid), dim3(kThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_encode_g16<false, false, U>), dim3(grid), dim3(kThreads), 0, s, a);
+        return ss_check(hipGetLastError(), "k_encode_g16");
+    }
+    if (ham) {
+        // General-path fused hamming: encode then hamming on the packed words (two passes).
+        if (!d_words) return ss_fail(SS_EARG, "general-path hamming needs d_words");
+    }
+    const unsigned grid = grid_for(n * wpr, kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_encode_gen<false>), dim3(grid), dim3(kThreads), 0, s, d_ascii, stride,
+                       (const uint64_t*)nullptr, (const uint32_t*)nullptr, L, n, d_words, wpr,
+                       (unsigned long long*)d_first_bad);
+    rc = ss_check(hipGetLastError(), "k_encode_gen");
+    if (rc || !ham) return rc;
+    return ss_hamming_ref(d_words, n, L, wpr, d_ref_words, d_out, stream);
+}
+
+int ss_encode_fixed(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                    uint64_t* d_words, uint32_t wpr, uint64_t* d_first_bad, void* stream) {
+    if (!d_words && n) return ss_fail(SS_EARG, "d_words is null");
+    return ss_encode_fixed_impl(d_ascii, n, L, stride, d_words, wpr, d_first_bad, nullptr, nullptr, stream);
+}
+
+int ss_encode_hamming_ref(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                          uint64_t* d_words, uint32_t wpr, const uint64_t* d_ref_words,
+                          uint32_t* d_out, uint64_t* d_first_bad, void* stream) {
+    if (!d_out && n) return ss_fail(SS_EARG, "d_out is null");
+    return ss_encode_fixed_impl(d_ascii, n, L, stride, d_words, wpr, d_first_bad, d_ref_words, d_out, stream);
+}
+
+int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint32_t* d_lens,
+                  uint64_t n, uint64_t* d_words, uint32_t wpr, uint64_t* d_first_bad, void* stream) {
+    if (wpr == 0 || wpr > 32) return ss_fail(SS_EARG, "wpr must be in 1..32");
+    if (!d_first_bad) return ss_fail(SS_EARG, "d_first_bad is required");
+    if (n && (!d_ascii || !d_offsets || !d_lens || !d_words)) return ss_fail(SS_EARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = reset_first_bad(d_first_bad, s);
+    if (rc || n == 0) return rc;
+    const unsigned grid = grid_for(n * wpr, kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_encode_gen<true>), dim3(grid), dim3(kThreads), 0, s, d_ascii, (uint64_t)0,
+                       d_offsets, d_lens, 0u, n, d_words, wpr, (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_encode_gen<var>");
+}
+
+int ss_decode_fixed(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr,
+                    uint8_t* d_ascii, uint64_t stride, void* stream) {
+    if (L > SS_MAX_NT) return ss_fail(SS_EARG, "L must be <= 1024");
+    if (wpr < words_for(L) || wpr == 0 || wpr > 32) return ss_fail(SS_EARG, "bad wpr");
+    if (stride < L) return ss_fail(SS_EARG, "stride < L");
+    if (n == 0 || L == 0) return SS_OK;
+    if (!d_words || !d_ascii) return ss_fail(SS_EARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    const bool fast = (L % 16u == 0) && (stride % 16u == 0) && ((((uintptr_t)d_ascii) & 15) == 0) &&
+                      ((((uintptr_t)d_words) & 7) == 0);
+    if (fast) {
+        const uint32_t cpr = L / 16, wpr2 = 2 * wpr, logG = log2_ceil(cpr);
+        constexpr int U = 4;
+        const unsigned grid = grid_for(n << logG, (uint64_t)U * kThreads);
+        hipLaunchKernelGGL((k_decode_g16<U>), dim3(grid), dim3(kThreads), 0, s, (const uint32_t*)d_words,
+                           wpr2, n, cpr, logG, (uint4*)d_ascii, stride / 16);
+        return ss_check(hipGetLastError(), "k_decode_g16");
+    }
+    const unsigned grid = grid_for(n * wpr, kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_decode_gen<false>), dim3(grid), dim3(kThreads), 0, s, d_words,
+                       (const uint32_t*)nullptr, L, n, wpr, d_ascii, stride, (const uint64_t*)nullptr);
+    return ss_check(hipGetLastError(), "k_decode_gen");
+}
+
+int ss_decode_var(const uint64_t* d_words, const uint32_t* d_lens, uint64_t n, uint32_t wpr,
+                  uint8_t* d_ascii, const uint64_t* d_offsets, void* stream) {
+    if (wpr == 0 || wpr > 32) return ss_fail(SS_EARG, "bad wpr");
+    if (n == 0) return SS_OK;
+    if (!d_words || !d_lens || !d_ascii || !d_offsets) return ss_fail(SS_EARG, "null buffer");
+    const unsigned grid = grid_for(n * wpr, kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_decode_gen<true>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_words,
+                       d_lens, 0u, n, wpr, d_ascii, (uint64_t)0, d_offsets);
+    return ss_check(hipGetLastError(), "k_decode_gen<var>");
+}
+
+static int launch_ham(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t L, uint32_t wpr,
+                      uint32_t* out, void* stream, bool pair) {
+    if (L > SS_MAX_NT) return ss_fail(SS_EARG, "L must be <= 1024");
+    const uint32_t W = ham_words(L);
+    if (wpr < W || wpr > 32) return ss_fail(SS_EARG, "bad wpr");
+    if (n == 0) return SS_OK;
+    if (!a || !b || !out) return ss_fail(SS_EARG, "null buffer");
+    const uint32_t logG = log2_ceil(W);
+    const unsigned grid = grid_for(n << logG, kThreads);
+    if (pair)
+        hipLaunchKernelGGL((k_ham_group<true>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, a, b,
+                           n, W, wpr, logG, out);
+    else
+        hipLaunchKernelGGL((k_ham_group<false>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, a, b,
+                           n, W, wpr, logG, out);
+    return ss_check(hipGetLastError(), "k_ham_group");
+}
+
+int ss_hamming_ref(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr,
+                   const uint64_t* d_ref, uint32_t* d_out, void* stream) {
+    return launch_ham(d_words, d_ref, n, L, wpr, d_out, stream, false);
+}
+
+int ss_hamming_pair(const uint64_t* d_a, const uint64_t* d_b, uint64_t n, uint32_t L, uint32_t wpr,
+                    uint32_t* d_out, void* stream) {
+    return launch_ham(d_a, d_b, n, L, wpr, d_out, stream, true);
+}
+
+int ss_synth_reads(uint8_t* d_ascii, uint64_t seed, uint64_t i0, uint64_t n, uint32_t L,
+                   uint64_t stride, void* stream) {
+    if (L == 0 || L > SS_MAX_NT || stride < L) return ss_fail(SS_EARG, "bad L/stride");
+    if (n == 0) return SS_OK;
+    if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
+    const unsigned grid = grid_for(n * words_for(L), kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_synth<false>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
+                       (uint64_t)0, (uint64_t)1, i0, n, L, stride);
+    return ss_check(hipGetLastError(), "k_synth");
+}
+
+int ss_synth_pool_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, uint64_t U,
+                        uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream) {
+    if (L == 0 || L > SS_MAX_NT || stride < L || U == 0) return ss_fail(SS_EARG, "bad L/stride/U");
+    if (n == 0) return SS_OK;
+    if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
+    const unsigned grid = grid_for(n * words_for(L), kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_synth<true>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
+                       pool_seed, U, i0, n, L, stride);
+    return ss_check(hipGetLastError(), "k_synth<pool>");
+}
+
+}  // extern "C"

@@ -1,0 +1,391 @@
+// ss_counter.hip — ShortSeqCounter on the GPU: fused encode -> open-addressing hash table in HBM
+// with atomic counts and first-occurrence indices (counter.pyx:41-54 semantics).
+//
+// Table (structure of arrays, capacity C = 2^k, plus one sentinel slot at index C):
+//   keys[C]    u64 packed word; EMPTY = ~0.  Claimed once by atomicCAS EMPTY -> key, never changed.
+//   counts[C+1] u64 atomicAdd.   first[C+1] u64 atomicMin (UINT64_MAX = unset).
+// The packed word ~0 ("G" * 32) collides with EMPTY and lives in the sentinel slot C.
+// Every key of one handle has the same length L <= 32 (the host groups a mixed batch by length, so
+// the dict key (length, packed) of short_seq_64.pyx:41-44 is (handle, word) here).
+//
+// Probing: Fibonacci hash of the key -> top k bits, linear probing.  A plain (possibly L1-stale)
+// load of keys[h] can only be stale as EMPTY (keys never change once claimed); the CAS then returns
+// the true value, so no acquire fence is needed (MI355X_MICROARCH.md §visibility).
+#include "ss_device.h"
+#include "ss_internal.h"
+
+using namespace ssd;
+
+struct ss_counter {
+    uint64_t cap = 0;
+    uint32_t log2cap = 0;
+    int32_t L = -1;                      // length of every key in this handle (-1: not fixed yet)
+    uint64_t* keys = nullptr;            // [cap]
+    unsigned long long* counts = nullptr;  // [cap + 1]
+    unsigned long long* first = nullptr;   // [cap + 1]
+    unsigned long long* work = nullptr;    // [0]: overflow flag, [1..]: part offsets/cursors (2*kMaxParts)
+};
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr uint32_t kMaxParts = 1024;
+
+struct Tbl {
+    uint64_t* keys;
+    unsigned long long* counts;
+    unsigned long long* first;
+    unsigned long long* overflow;
+    uint64_t mask;
+    uint32_t shift;
+};
+
+__device__ __forceinline__ uint64_t slot_hash(uint64_t key, uint32_t shift) {
+    return (key * 0x9E3779B97F4A7C15ull) >> shift;
+}
+
+// Owner partition for the multi-GPU merge (independent of the table's hash bits).
+__host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t nparts) {
+    return (uint32_t)((splitmix64(key) >> 32) % nparts);
+}
+
+__device__ __forceinline__ void tbl_add(const Tbl& t, uint64_t key, unsigned long long cnt,
+                                        unsigned long long idx) {
+    uint64_t s;
+    if (key == kEmpty) {
+        s = t.mask + 1;  // sentinel slot
+    } else {
+        uint64_t h = t.shift >= 64 ? 0 : slot_hash(key, t.shift);
+        uint64_t probes = 0;
+        for (;;) {
+            const uint64_t cur = t.keys[h];
+            if (cur == key) break;
+            if (cur == kEmpty) {
+                const unsigned long long prev =
+                    atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)kEmpty, (unsigned long long)key);
+                if (prev == kEmpty || prev == key) break;
+            }
+            h = (h + 1) & t.mask;
+            if (++probes > t.mask) {
+                atomicOr(t.overflow, 1ull);
+                return;
+            }
+        }
+        s = h;
+    }
+    atomicAdd(&t.counts[s], cnt);
+    if (t.first[s] > idx) atomicMin(&t.first[s], idx);
+}
+
+// Fast path, L in {16, 32}, 16-B aligned rows: two lanes per read (lane pair = one packed word,
+// same chunk encoder as k_encode_g16), the even lane inserts.
+template <int U>
+__global__ __launch_bounds__(kThreads) void k_count_g16(Tbl t, const uint4* __restrict__ in,
+                                                        uint64_t stride16, uint64_t n, uint32_t cpr,
+                                                        uint64_t base_index, unsigned long long* first_bad) {
+    const uint64_t base = (uint64_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+    uint4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t r = g >> 1;
+        const uint32_t k = (uint32_t)g & 1u;
+        x[j] = (r < n && k < cpr) ? ld_stream(&in[r * stride16 + k])
+                                  : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t r = g >> 1;
+        const uint32_t k = (uint32_t)g & 1u;
+        Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, true);   // L <= 32: table path
+        const uint32_t cin = swap_pair(e.cout);
+        const uint32_t v = e.v | (k ? cin : 0u);
+        const uint32_t hi = swap_pair(v);
+        const uint32_t bad_pair = e.bad | swap_pair(e.bad);
+        const bool live = r < n && k == 0;
+        report_bad(live && bad_pair != 0u, r, first_bad);
+        if (live && bad_pair == 0u) tbl_add(t, (uint64_t)v | ((uint64_t)hi << 32), 1ull, base_index + r);
+    }
+}
+
+__device__ __forceinline__ uint64_t load_word_general(const uint8_t* p, uint32_t nb, uint32_t& bad);
+
+// General path (any L <= 32, any stride): one lane per read.
+__global__ __launch_bounds__(kThreads) void k_count_gen(Tbl t, const uint8_t* in, uint64_t stride,
+                                                        uint64_t n, uint32_t L, uint64_t base_index,
+                                                        unsigned long long* first_bad) {
+    for (uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x; r < n; r += (uint64_t)gridDim.x * kThreads) {
+        uint32_t bad = 0;
+        const uint64_t key = load_word_general(in + r * stride, L, bad);
+        if (bad) {
+            atomicMin(first_bad, (unsigned long long)r);
+            continue;
+        }
+        tbl_add(t, key, 1ull, base_index + r);
+    }
+}
+
+__device__ __forceinline__ uint64_t load_word_general(const uint8_t* p, uint32_t nb, uint32_t& bad) {
+    if (nb == 0) return 0;
+    const uintptr_t addr = (uintptr_t)p;
+    const uint32_t* d = (const uint32_t*)(addr & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(addr & 3);
+    const uint32_t nd = (sh + nb + 3u) >> 2;
+    uint32_t dw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dw[i] = ((uint32_t)i < nd) ? d[i] : 0x41414141u;
+    uint32_t xw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t v = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
+        const int m = (int)nb - 4 * i;
+        if (m <= 0) {
+            v = 0x41414141u;
+        } else if (m < 4) {
+            const uint32_t keep = (1u << (8 * m)) - 1u;
+            v = (v & keep) | (0x41414141u & ~keep);
+        }
+        xw[i] = v;
+    }
+    Enc32 lo = encode16(xw[0], xw[1], xw[2], xw[3], true);
+    Enc32 hi = encode16(xw[4], xw[5], xw[6], xw[7], true);
+    bad |= lo.bad | hi.bad;
+    return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
+}
+
+__global__ __launch_bounds__(kThreads) void k_merge(Tbl t, const uint64_t* keys, const uint64_t* counts,
+                                                    const uint64_t* first, uint64_t m) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kThreads)
+        tbl_add(t, keys[i], counts[i], first[i]);
+}
+
+__device__ __forceinline__ bool slot_used(const Tbl& t, uint64_t s, uint64_t& key) {
+    if (s <= t.mask) {
+        key = t.keys[s];
+        return key != kEmpty;
+    }
+    key = kEmpty;
+    return t.counts[s] != 0;   // sentinel slot
+}
+
+__global__ __launch_bounds__(kThreads) void k_size(Tbl t, unsigned long long* out) {
+    __shared__ unsigned int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    unsigned int local = 0;
+    for (uint64_t s = (uint64_t)blockIdx.x * kThreads + threadIdx.x; s <= t.mask + 1; s += (uint64_t)gridDim.x * kThreads) {
+        uint64_t key;
+        local += slot_used(t, s, key) ? 1u : 0u;
+    }
+    atomicAdd(&cnt, local);
+    __syncthreads();
+    if (threadIdx.x == 0 && cnt) atomicAdd(out, (unsigned long long)cnt);
+}
+
+// Extract pass 1: per-part histogram (LDS), one global add per part per block.
+__global__ __launch_bounds__(kThreads) void k_part_hist(Tbl t, uint32_t nparts, unsigned long long* part_counts) {
+    __shared__ unsigned int hist[kMaxParts];
+    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) hist[p] = 0;
+    __syncthreads();
+    for (uint64_t s = (uint64_t)blockIdx.x * kThreads + threadIdx.x; s <= t.mask + 1; s += (uint64_t)gridDim.x * kThreads) {
+        uint64_t key;
+        if (slot_used(t, s, key)) atomicAdd(&hist[owner_of(key, nparts)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads)
+        if (hist[p]) atomicAdd(&part_counts[p], (unsigned long long)hist[p]);
+}
+
+// Extract pass 2: exclusive scan of the part counts into cursors (one block).
+__global__ void k_part_scan(uint32_t nparts, const unsigned long long* part_counts, unsigned long long* cursors) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        unsigned long long acc = 0;
+        for (uint32_t p = 0; p < nparts; ++p) {
+            cursors[p] = acc;
+            acc += part_counts[p];
+        }
+    }
+}
+
+// Extract pass 3: scatter occupied slots into their part's range.
+__global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t nparts, int32_t L,
+                                                           unsigned long long* cursors, uint64_t* okeys,
+                                                           uint32_t* olens, uint64_t* ocounts, uint64_t* ofirst,
+                                                           uint64_t cap_out, unsigned long long* overflow) {
+    for (uint64_t s = (uint64_t)blockIdx.x * kThreads + threadIdx.x; s <= t.mask + 1; s += (uint64_t)gridDim.x * kThreads) {
+        uint64_t key;
+        if (!slot_used(t, s, key)) continue;
+        const unsigned long long pos = atomicAdd(&cursors[owner_of(key, nparts)], 1ull);
+        if (pos >= cap_out) {
+            atomicOr(overflow, 2ull);
+            continue;
+        }
+        okeys[pos] = key;
+        olens[pos] = (uint32_t)L;
+        ocounts[pos] = t.counts[s];
+        ofirst[pos] = t.first[s];
+    }
+}
+
+Tbl tbl_of(const ss_counter* c) {
+    Tbl t;
+    t.keys = c->keys;
+    t.counts = c->counts;
+    t.first = c->first;
+    t.overflow = c->work;
+    t.mask = c->cap - 1;
+    t.shift = 64 - c->log2cap;
+    return t;
+}
+
+unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
+    uint64_t b = (items + per_block - 1) / per_block;
+    if (b == 0) b = 1;
+    if (cap && b > cap) b = cap;
+    return (unsigned)b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ss_counter_create(uint64_t capacity, ss_counter** out) {
+    if (!out) return ss_fail(SS_EARG, "null out");
+    if (capacity < 64) capacity = 64;
+    uint32_t lg = 0;
+    while ((1ull << lg) < capacity) ++lg;
+    if (lg > 40) return ss_fail(SS_EARG, "capacity too large");
+    ss_counter* c = new ss_counter();
+    c->cap = 1ull << lg;
+    c->log2cap = lg;
+    hipError_t e = hipMalloc((void**)&c->keys, c->cap * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->counts, (c->cap + 1) * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->first, (c->cap + 1) * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->work, (1 + 2 * kMaxParts) * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        ss_counter_destroy(c);
+        ss_check(e, "ss_counter_create hipMalloc");
+        return SS_ENOMEM;
+    }
+    int rc = ss_counter_reset(c, nullptr);
+    if (rc == SS_OK) rc = ss_check(hipStreamSynchronize(nullptr), "ss_counter_create sync");
+    if (rc) {
+        ss_counter_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return SS_OK;
+}
+
+int ss_counter_destroy(ss_counter* c) {
+    if (!c) return SS_OK;
+    if (c->keys) (void)hipFree(c->keys);
+    if (c->counts) (void)hipFree(c->counts);
+    if (c->first) (void)hipFree(c->first);
+    if (c->work) (void)hipFree(c->work);
+    delete c;
+    return SS_OK;
+}
+
+int ss_counter_reset(ss_counter* c, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    hipStream_t s = (hipStream_t)stream;
+    c->L = -1;
+    hipError_t e = hipMemsetAsync(c->keys, 0xFF, c->cap * sizeof(uint64_t), s);
+    if (e == hipSuccess) e = hipMemsetAsync(c->counts, 0, (c->cap + 1) * sizeof(unsigned long long), s);
+    if (e == hipSuccess) e = hipMemsetAsync(c->first, 0xFF, (c->cap + 1) * sizeof(unsigned long long), s);
+    if (e == hipSuccess) e = hipMemsetAsync(c->work, 0, (1 + 2 * kMaxParts) * sizeof(unsigned long long), s);
+    return ss_check(e, "ss_counter_reset");
+}
+
+uint64_t ss_counter_capacity(const ss_counter* c) { return c ? c->cap : 0; }
+
+static int fix_length(ss_counter* c, uint32_t L) {
+    if (L > 32) return ss_fail(SS_EARG, "GPU counter keys must have L <= 32");
+    if (c->L < 0) c->L = (int32_t)L;
+    if ((uint32_t)c->L != L) return ss_fail(SS_EARG, "all keys of one counter handle must share one length");
+    return SS_OK;
+}
+
+int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L,
+                            uint64_t stride, uint64_t base_index, uint64_t* d_first_bad, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (!d_first_bad) return ss_fail(SS_EARG, "d_first_bad is required");
+    if (stride < L) return ss_fail(SS_EARG, "stride < L");
+    int rc = fix_length(c, L);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    rc = ss_check(hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s), "reset first_bad");
+    if (rc || n == 0) return rc;
+    if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
+    Tbl t = tbl_of(c);
+    const bool fast = (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
+    if (fast) {
+        constexpr int U = 4;
+        const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 0);
+        hipLaunchKernelGGL((k_count_g16<U>), dim3(grid), dim3(kThreads), 0, s, t, (const uint4*)d_ascii,
+                           stride / 16, n, L / 16, base_index, (unsigned long long*)d_first_bad);
+        return ss_check(hipGetLastError(), "k_count_g16");
+    }
+    const unsigned grid = grid_for(n, kThreads, 256 * 16);
+    hipLaunchKernelGGL(k_count_gen, dim3(grid), dim3(kThreads), 0, s, t, d_ascii, stride, n, L, base_index,
+                       (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_count_gen");
+}
+
+int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_lens,
+                     const uint64_t* d_counts, const uint64_t* d_first, uint64_t m, void* stream) {
+    (void)d_lens;   // every entry of a handle has the handle's length (checked by the caller)
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (m == 0) return SS_OK;
+    if (!d_keys || !d_counts || !d_first) return ss_fail(SS_EARG, "null buffer");
+    const unsigned grid = grid_for(m, kThreads, 256 * 16);
+    hipLaunchKernelGGL(k_merge, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, tbl_of(c), d_keys, d_counts,
+                       d_first, m);
+    return ss_check(hipGetLastError(), "k_merge");
+}
+
+int ss_counter_set_length(ss_counter* c, uint32_t L) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    return fix_length(c, L);
+}
+
+int ss_counter_length(const ss_counter* c) { return c ? c->L : -1; }
+
+int ss_counter_size(ss_counter* c, uint64_t* d_size, void* stream) {
+    if (!c || !d_size) return ss_fail(SS_EARG, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ss_check(hipMemsetAsync(d_size, 0, sizeof(uint64_t), s), "size memset");
+    if (rc) return rc;
+    const unsigned grid = grid_for(c->cap + 1, kThreads, 256 * 8);
+    hipLaunchKernelGGL(k_size, dim3(grid), dim3(kThreads), 0, s, tbl_of(c), (unsigned long long*)d_size);
+    return ss_check(hipGetLastError(), "k_size");
+}
+
+int ss_counter_overflow(ss_counter* c, uint64_t* d_flag, void* stream) {
+    if (!c || !d_flag) return ss_fail(SS_EARG, "null argument");
+    return ss_check(hipMemcpyAsync(d_flag, c->work, sizeof(uint64_t), hipMemcpyDeviceToDevice, (hipStream_t)stream),
+                    "overflow copy");
+}
+
+int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens,
+                       uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
+                       void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (n_parts == 0 || n_parts > kMaxParts) return ss_fail(SS_EARG, "n_parts must be in 1..1024");
+    if (!d_keys || !d_lens || !d_counts || !d_first || !d_part_counts) return ss_fail(SS_EARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    Tbl t = tbl_of(c);
+    unsigned long long* cursors = c->work + 1;
+    int rc = ss_check(hipMemsetAsync(d_part_counts, 0, n_parts * sizeof(uint64_t), s), "part memset");
+    if (rc) return rc;
+    const unsigned grid = grid_for(c->cap + 1, kThreads, 256 * 8);
+    hipLaunchKernelGGL(k_part_hist, dim3(grid), dim3(kThreads), 0, s, t, n_parts, (unsigned long long*)d_part_counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, n_parts, (const unsigned long long*)d_part_counts, cursors);
+    hipLaunchKernelGGL(k_part_scatter, dim3(grid), dim3(kThreads), 0, s, t, n_parts, c->L < 0 ? 0 : c->L, cursors,
+                       d_keys, d_lens, d_counts, d_first, cap, c->work);
+    return ss_check(hipGetLastError(), "ss_counter_extract");
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+"""The C-ABI boundary: the library loads on a CPU-only host, exports every symbol declared in
+include/shortseq_amd.h, the host codec matches the oracle, and the product never touches oracle/."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(REPO, "include", "shortseq_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ss_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    from shortseq_amd import _native
+    lib = _native.lib()
+    names = declared_symbols()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(lib, n), n
+    bound = {s[0] for s in _native.SIGNATURES}
+    assert set(names) == bound, set(names) ^ bound
+    assert lib.ss_abi_version() == 1
+
+
+def test_no_device_is_an_error_not_a_fallback():
+    """Without a GPU the device entry points fail loudly (SS_EHIP/EARG), they never compute."""
+    from shortseq_amd import _native
+    lib = _native.lib()
+    n = C.c_int(-1)
+    rc = lib.ss_device_count(C.byref(n))
+    if n.value > 0:
+        return  # on a GPU box this test has nothing to say
+    fb = C.c_uint64(0)
+    rc = lib.ss_encode_fixed(None, 10, 32, 32, None, 1, C.addressof(fb), None)
+    assert rc != 0
+
+
+def test_product_does_not_import_oracle():
+    """Only tests/, smoke() and bench.py's cpu_baseline may use oracle/ (the checker)."""
+    pat = re.compile(r"\bimport\s+oracle|\bfrom\s+oracle|liboracle|\bora_[a-z_]+\s*\(|oracle/_ref")
+    pkg = os.path.join(REPO, "shortseq_amd")
+    for root, _dirs, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".pyx", ".pxd", ".hip", ".h", ".cpp")):
+                text = open(os.path.join(root, f), encoding="utf-8", errors="replace").read()
+                assert not pat.search(text), f
+
+
+def test_host_codec_matches_oracle(oracle, golden):
+    from shortseq_amd import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(3)
+    alphabet = np.frombuffer(b"ACGT\x01\x03\x07\x14NacgU*\n\xc1\x81\xff", np.uint8)
+    for L in list(range(0, 100)) + [127, 128, 129, 500, 1023, 1024, 1025]:
+        for rep in range(20):
+            p_bad = [0.0, 0.01, 0.2][rep % 3]
+            codes = np.where(rng.random(L) < p_bad, rng.integers(4, len(alphabet), L), rng.integers(0, 7, L))
+            seq = alphabet[codes].astype(np.uint8).tobytes()
+            wo, eo = oracle.encode_one(seq, 32)
+            wh = np.zeros(32, np.uint64)
+            eh = _native.SsErr()
+            buf = np.frombuffer(seq, np.uint8) if L else np.zeros(1, np.uint8)
+            rc = lib.ss_host_encode(buf.ctypes.data, L, wh.ctypes.data, C.byref(eh))
+            assert rc == eo.kind, (L, seq)
+            if rc == 1:
+                assert (eh.byte_offset, eh.nbytes) == (eo.byte_offset, eo.nbytes)
+            elif rc == 0:
+                nw = max(1, (L + 31) // 32)
+                assert np.array_equal(wh[:nw], wo[:nw]), (L, seq)
+    # decode + hamming on the golden vectors
+    for v in golden["vectors"]:
+        L = v["L"]
+        wa = np.array([int(h, 16) for h in v["words_a"]] + [0] * 32, np.uint64)
+        wb = np.array([int(h, 16) for h in v["words_b"]] + [0] * 32, np.uint64)
+        out = C.create_string_buffer(max(L, 1))
+        lib.ss_host_decode(wa.ctypes.data, L, out)
+        assert out.raw[:L].decode() == v["str_a"]
+        assert lib.ss_host_hamming(wa.ctypes.data, wb.ctypes.data, L) == v["hamming"]

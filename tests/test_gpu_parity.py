@@ -1,0 +1,291 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the oracle and the reference's fixtures.
+
+Bit-exact for everything (integer work).  Small/medium sizes compare element-wise with the oracle;
+full BASELINE sizes are checked through size-independent properties (known-answer generator words,
+encode -> decode round trip, checksum of per-read distances).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ALIASES = np.array([1, 3, 7, 20], np.uint8)
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def _rand_reads(rng, n, L, p_alias=0.0, p_bad=0.0):
+    a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=n * L)]
+    if p_alias:
+        m = rng.random(n * L) < p_alias
+        a = np.where(m, ALIASES[rng.integers(0, 4, size=n * L)], a)
+    if p_bad:
+        m = rng.random(n * L) < p_bad
+        a = np.where(m, np.uint8(ord("N")), a)
+    return a.astype(np.uint8)
+
+
+LENGTHS = sorted(set(list(range(1, 100)) + [112, 127, 128, 129, 160, 255, 256, 257, 500, 511, 512,
+                                            513, 768, 1000, 1008, 1023, 1024]))
+
+
+@pytest.mark.parametrize("p_alias", [0.0, 0.03])
+def test_encode_fixed_all_lengths(gpu, oracle, p_alias):
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(11)
+    for L in LENGTHS:
+        n = 257
+        a = _rand_reads(rng, n, L, p_alias)
+        exp, rc, _ = oracle.encode_batch(a, n, L)
+        assert rc == 0
+        got = B.encode(torch.from_numpy(a).to(gpu).view(n, L), L)
+        assert np.array_equal(_u64(got), exp), L
+
+
+@pytest.mark.parametrize("L", [16, 32, 48, 64, 96, 100, 512, 1024])
+def test_encode_stride_and_padding(gpu, oracle, L):
+    """stride > L (general path even for L % 16 == 0 when stride is odd) and wpr > ceil(L/32)."""
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(L)
+    n = 300
+    for stride in (L, L + 16, L + 3):
+        a = _rand_reads(rng, n, stride, p_alias=0.02)
+        exp, rc, _ = oracle.encode_batch(a, n, L, stride=stride, wpr=B.wpr_for(L) + 1)
+        got = B.encode(torch.from_numpy(a).to(gpu), L, stride=stride, wpr=B.wpr_for(L) + 1)
+        assert np.array_equal(_u64(got), exp), (L, stride)
+
+
+def test_golden_vectors_gpu(gpu, golden):
+    import shortseq_amd.batch as B
+    for v in golden["vectors"]:
+        L = v["L"]
+        if L == 0:
+            continue
+        t = torch.tensor(list(v["a"].encode()), dtype=torch.uint8, device=gpu).view(1, L)
+        w = _u64(B.encode(t, L))[0]
+        exp = [int(h, 16) for h in v["words_a"]][: B.wpr_for(L)]
+        assert [int(x) for x in w] == exp, L
+        s = B.decode(B.encode(t, L), L)
+        assert bytes(s.cpu().numpy()[0]).decode() == v["str_a"]
+        tb = torch.tensor(list(v["b"].encode()), dtype=torch.uint8, device=gpu).view(1, L)
+        d = B.hamming_pair(B.encode(t, L), B.encode(tb, L), L)
+        assert int(d[0]) == v["hamming"]
+
+
+def test_golden_aliased_gpu(gpu, golden):
+    import shortseq_amd.batch as B
+    for c in golden["aliased"]:
+        seq = bytes.fromhex(c["input_hex"])
+        L = len(seq)
+        t = torch.tensor(list(seq), dtype=torch.uint8, device=gpu).view(1, L)
+        w = _u64(B.encode(t, L))[0]
+        exp = [int(h, 16) for h in c["words"]][: B.wpr_for(L)]
+        assert [int(x) for x in w] == exp, (L, c["pos"])
+
+
+def test_errors_first_bad_read(gpu, oracle, golden):
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(5)
+    for L in [1, 7, 16, 31, 32, 33, 48, 64, 96, 100, 512, 1024]:
+        n = 1000
+        a = _rand_reads(rng, n, L)
+        bad_rows = sorted(rng.choice(n, size=3, replace=False))
+        for r in bad_rows:
+            a[r * L + rng.integers(0, L)] = ord("N")
+        with pytest.raises(Exception) as ei:
+            B.encode(torch.from_numpy(a).to(gpu).view(n, L), L)
+        assert ei.value.read_index == bad_rows[0]
+        seq = a[bad_rows[0] * L:(bad_rows[0] + 1) * L].tobytes()
+        _, err = oracle.encode_one(seq, 32)
+        bad = seq[err.byte_offset: err.byte_offset + err.nbytes]
+        assert str(ei.value) == "Unsupported base character: " + bad.decode()
+    # the golden error messages, one read per batch
+    for c in golden["errors"]["pack"]:
+        if c["ctor"] not in ("pack_bytes", "pack_bytes_hex") or "raises" not in c:
+            continue
+        seq = c["input"].encode() if c["ctor"] == "pack_bytes" else bytes.fromhex(c["input"])
+        if len(seq) > 1024:
+            continue
+        t = torch.tensor(list(seq), dtype=torch.uint8, device=gpu).view(1, len(seq))
+        with pytest.raises(BaseException) as ei:
+            B.encode(t, len(seq))
+        assert (type(ei.value).__name__, str(ei.value)) == (c["raises"], c["message"])
+
+
+def test_decode_roundtrip_and_var(gpu, oracle):
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(9)
+    for L in LENGTHS:
+        n = 129
+        a = _rand_reads(rng, n, L)
+        w = B.encode(torch.from_numpy(a).to(gpu).view(n, L), L)
+        back = B.decode(w, L)
+        assert np.array_equal(back.cpu().numpy().reshape(-1), a), L
+        assert np.array_equal(back.cpu().numpy().reshape(-1), oracle.decode_batch(_u64(w), n, L))
+    # ragged batch 0..1024 incl. empty reads
+    lens = np.array([0, 1, 31, 32, 33, 64, 95, 96, 97, 1000, 1024, 5, 0, 512] * 20, np.int32)
+    reads = [_rand_reads(rng, 1, int(L), p_alias=0.02).tobytes() for L in lens]
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1])
+    blob = np.frombuffer(b"".join(reads) + b"\0", np.uint8)
+    words = B.encode_var(torch.from_numpy(blob.copy()).to(gpu), torch.from_numpy(offs).to(gpu),
+                         torch.from_numpy(lens).to(gpu), wpr=32)
+    wn = _u64(words)
+    for i, r in enumerate(reads):
+        exp, _ = oracle.encode_one(r, 32)
+        assert np.array_equal(wn[i], exp), (i, len(r))
+    out = B.decode_var(words, torch.from_numpy(lens).to(gpu), torch.from_numpy(offs).to(gpu))
+    clean = b"".join(oracle.decode_batch(wn[i:i + 1], 1, int(L), 32).tobytes() for i, L in enumerate(lens))
+    assert out.cpu().numpy().tobytes() == clean
+    # too-long read in a ragged batch
+    lens2 = np.array([10, 1025, 10], np.int32)
+    offs2 = np.array([0, 10, 1035], np.int64)
+    blob2 = np.frombuffer(b"A" * 1045, np.uint8).copy()
+    with pytest.raises(Exception) as ei:
+        B.encode_var(torch.from_numpy(blob2).to(gpu), torch.from_numpy(offs2).to(gpu),
+                     torch.from_numpy(lens2).to(gpu))
+    assert str(ei.value) == "Sequences longer than 1024 bases are not supported."
+    assert ei.value.read_index == 1
+
+
+def test_hamming(gpu, oracle):
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(13)
+    for L in LENGTHS:
+        n = 200
+        a = _rand_reads(rng, n, L, p_alias=0.01)
+        b = a.copy()
+        flip = rng.random(n * L) < 0.1
+        b[flip] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, flip.sum())]
+        wa = B.encode(torch.from_numpy(a).to(gpu).view(n, L), L)
+        wb = B.encode(torch.from_numpy(b).to(gpu).view(n, L), L)
+        pair = B.hamming_pair(wa, wb, L).cpu().numpy().astype(np.uint32)
+        assert np.array_equal(pair, oracle.hamming_pair_batch(_u64(wa), _u64(wb), n, L)), L
+        ref = B.hamming_ref(wa, L, wb[7]).cpu().numpy().astype(np.uint32)
+        assert np.array_equal(ref, oracle.hamming_ref_batch(_u64(wa), n, L, _u64(wb)[7])), L
+        words, dist = B.encode_hamming_ref(torch.from_numpy(a).to(gpu).view(n, L), L, wb[7])
+        assert np.array_equal(_u64(words), _u64(wa))
+        assert np.array_equal(dist.cpu().numpy().astype(np.uint32), ref), L
+        _, dist2 = B.encode_hamming_ref(torch.from_numpy(a).to(gpu).view(n, L), L, wb[7], store_words=False)
+        assert np.array_equal(dist2.cpu().numpy().astype(np.uint32), ref), L
+
+
+def test_synth_matches_oracle_generator(gpu, oracle):
+    import shortseq_amd.batch as B
+    for L in [1, 16, 31, 32, 33, 96, 100, 512, 1024]:
+        n = 500
+        t = B.synth_reads(n, L, seed=42, i0=1000, device=gpu)
+        assert np.array_equal(t.cpu().numpy().reshape(-1), oracle.gen_reads(42, 1000, n, L)), L
+        p = B.synth_pool_reads(n, L, 3, 4, 97, i0=77, device=gpu)
+        exp = oracle.gen_pool_reads(3, 4, 97, 77, n, L)
+        assert np.array_equal(p.cpu().numpy().reshape(-1), exp), L
+
+
+@pytest.mark.parametrize("key", ["1000000x32", "1000000x96", "200000x512", "300000x100"])
+def test_golden_digests_gpu(gpu, digests, key):
+    """Reference-produced SHA-256 of the packed words / distances, reproduced on the GPU."""
+    import shortseq_amd.batch as B
+    d = digests[key]
+    n, L = d["n"], d["L"]
+    ascii = B.synth_reads(n, L, seed=d["seed"], device=gpu)
+    words = B.encode(ascii, L)
+    assert _sha(_u64(words)) == d["words_sha256"]
+    m = d["hamming_vs_read0_n"]
+    _, dist = B.encode_hamming_ref(ascii[:m], L, words[0], store_words=False)
+    dist = dist.cpu().numpy().astype(np.uint32)
+    assert _sha(dist) == d["hamming_vs_read0_sha256"]
+
+
+@pytest.mark.parametrize("L,n", [(32, 100_000_000), (96, 100_000_000), (512, 50_000_000)])
+def test_full_size_properties(gpu, oracle, L, n):
+    """BASELINE sizes: round trip + checksum of sampled reads vs oracle + fused hamming sum."""
+    import shortseq_amd.batch as B
+    torch.cuda.empty_cache()
+    ascii = B.synth_reads(n, L, seed=1, device=gpu)
+    words = B.encode(ascii, L)
+    back = B.decode(words, L)
+    assert torch.equal(back, ascii)
+    del back
+    idx = np.linspace(0, n - 1, 4096).astype(np.int64)
+    samp = _u64(words[torch.from_numpy(idx).to(gpu)])
+    exp = np.stack([oracle.gen_words(1, int(i), 1, L)[0] for i in idx])
+    assert np.array_equal(samp, exp)
+    if L == 96:
+        _, dist = B.encode_hamming_ref(ascii, L, words[0], store_words=False)
+        dsum = int(dist.to(torch.int64).sum().item())
+        d2 = B.hamming_ref(words, L, words[0])
+        assert int(d2.to(torch.int64).sum().item()) == dsum
+        assert torch.equal(dist, d2)
+    del ascii, words
+    torch.cuda.empty_cache()
+
+
+def test_counter_gpu(gpu, oracle, digests):
+    import shortseq_amd.batch as B
+    d = digests["counter_1000000x32_pool65536"]
+    n, L = d["n"], d["L"]
+    ascii = B.synth_pool_reads(n, L, d["seed"], d["pool_seed"], d["U"], device=gpu)
+    c = B.GpuCounter(1 << 18, device=gpu)
+    half = n // 2
+    c.insert(ascii[:half], L, base_index=0)
+    c.insert(ascii[half:], L, base_index=half)
+    assert c.size() == d["unique"]
+    keys, counts, first = c.items_sorted()
+    ordered = np.stack([keys, np.full(len(keys), L, np.uint64), counts.astype(np.uint64)], 1)
+    assert _sha(ordered.astype(np.uint64)) == d["ordered_sha256"]
+    c.close()
+    # mixed small cases vs oracle, incl. the EMPTY-colliding word (G * 32) and L = 16 / odd L
+    rng = np.random.default_rng(1)
+    for L in [1, 5, 16, 31, 32]:
+        pool = [_rand_reads(rng, 1, L, p_alias=0.05).tobytes() for _ in range(50)]
+        if L == 32:
+            pool[3] = b"G" * 32
+        reads = [pool[i] for i in rng.integers(0, len(pool), 5000)]
+        exp = oracle.count(reads)
+        c = B.GpuCounter(1024, device=gpu)
+        t = torch.from_numpy(np.frombuffer(b"".join(reads), np.uint8).copy()).to(gpu).view(-1, L)
+        c.insert(t, L)
+        k, cnt, f = c.items_sorted()
+        assert [(int(x),) for x in k] == [w for (w, _L, _c, _f) in exp]
+        assert list(cnt) == [cc for (_w, _L, cc, _f) in exp]
+        assert list(f) == [ff for (_w, _L, _c, ff) in exp]
+        c.close()
+
+
+def test_counter_extract_parts_and_merge(gpu, oracle):
+    import shortseq_amd.batch as B
+    n, L, U = 200_000, 32, 5000
+    ascii = B.synth_pool_reads(n, L, 9, 10, U, device=gpu)
+    full = B.GpuCounter(1 << 14, device=gpu)
+    full.insert(ascii, L)
+    k0, c0, f0 = full.items_sorted()
+    # two "ranks": each counts half, partitions by owner, owners merge
+    parts = []
+    for r in range(2):
+        c = B.GpuCounter(1 << 14, device=gpu)
+        c.insert(ascii[r * n // 2:(r + 1) * n // 2], L, base_index=r * n // 2)
+        parts.append(c.extract(n_parts=3))
+    merged = [B.GpuCounter(1 << 14, device=gpu) for _ in range(3)]
+    for keys, lens, counts, first, pc in parts:
+        pc = pc.cpu().numpy()
+        off = np.concatenate([[0], np.cumsum(pc)])
+        for p in range(3):
+            s, e = int(off[p]), int(off[p + 1])
+            merged[p].merge(keys[s:e], counts[s:e], first[s:e], L)
+    allk, allc, allf = [], [], []
+    for m in merged:
+        k, c, f = m.items_sorted()
+        allk.append(k), allc.append(c), allf.append(f)
+    k, c, f = np.concatenate(allk), np.concatenate(allc), np.concatenate(allf)
+    o = np.argsort(f, kind="stable")
+    assert np.array_equal(k[o], k0) and np.array_equal(c[o], c0) and np.array_equal(f[o], f0)
+    assert c0.sum() == n
