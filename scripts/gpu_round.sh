@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# One GPU call: tests, tuning sweep, bench, rocprofv3 kernel-trace + PMC traffic passes.
+# Each step has its own time limit; a fatal step (fault/abort/timeout) ends the call.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r1}
+S=scripts/gpu_step.sh
+$S 600 pytest_gpu python -m pytest tests -m gpu -q || exit 1
+if [ -x tools/tune_encode ]; then $S 300 tune_encode tools/tune_encode 100000000 20 || exit 1; fi
+$S 400 bench python bench.py --steps 20 --warmup 5 || exit 1
+mkdir -p gpurun_out/prof_$TAG
+$S 400 rocprof_stats rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit 1
+$S 400 rocprof_fetch rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_$TAG/fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline || exit 1
+$S 400 rocprof_write rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_$TAG/write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline || exit 1
+echo ALLDONE

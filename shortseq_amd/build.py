@@ -59,7 +59,8 @@ def build_cython(force: bool = False, verbose: bool = False) -> str:
         build_dir = os.path.join(REPO, "build", "cython")
         os.makedirs(build_dir, exist_ok=True)
         cpp = os.path.join(build_dir, "_shortseq.cpp")
-        subprocess.run([sys.executable, "-m", "cython", "-3", "--cplus", "-I", CSRC, pyx, "-o", cpp],
+        subprocess.run([sys.executable, "-m", "cython", "-3", "--cplus", "--module-name", "shortseq_amd._shortseq",
+                        "-I", CSRC, pyx, "-o", cpp],
                        check=True, stdout=None if verbose else subprocess.DEVNULL)
         inc = sysconfig.get_paths()["include"]
         tmp = out + ".tmp"

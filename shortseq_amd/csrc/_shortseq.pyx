@@ -1,0 +1,554 @@
+# cython: language_level=3, boundscheck=False, wraparound=False, cdivision=True
+"""Drop-in front for the reference's Python API (shortseq/__init__.py:1-14).
+
+Per-object operations (pack / str / ^ / == / [] on single reads) run on the host C++ codec
+(csrc/host_codec.h): one read is ~tens of ns of work, a kernel launch is microseconds (SURVEY §7).
+Batch operations — ShortSeqCounter over a large list, read_and_count_fastq — stage the reads in a
+contiguous buffer and run on the GPU through the C ABI (shortseq_amd.batch -> libshortseq_amd.so);
+the GPU path raises if the HIP library cannot be used, it never degrades silently.
+
+Object layouts match the reference so sys.getsizeof agrees (short_seq_64.pxd:11-14,
+short_seq_192.pxd:11-14, short_seq_var.pxd:14-17): 32 / 48 / 32 + 8*ceil(L/32) bytes.
+
+Documented deviations (DESIGN.md §6): hash() and the counter agree for every key (reference Q5
+inserts with the raw word, so counts[pack("G"*32)] raises KeyError there); ShortSeqVar keys are
+deduplicated by content (reference Q6 keys them by heap pointer).
+"""
+from libc.stdint cimport uint8_t, uint64_t, int64_t, int32_t
+from libc.string cimport memcmp, memcpy, memset, strlen
+from libc.stdio cimport FILE, fopen, fclose
+from libc.stdlib cimport free
+from cpython.bytes cimport PyBytes_AS_STRING, PyBytes_GET_SIZE, PyBytes_FromStringAndSize
+from cpython.mem cimport PyObject_Calloc, PyObject_Free
+from cpython.unicode cimport PyUnicode_DecodeASCII
+from cpython.object cimport PyObject
+from cpython.list cimport PyList_GET_ITEM, PyList_GET_SIZE
+
+import time
+
+cdef extern from "Python.h":
+    void* PyUnicode_DATA(object o)
+    Py_ssize_t PyUnicode_GET_LENGTH(object o)
+    bint PyUnicode_Check(object o)
+    bint PyBytes_Check(object o)
+    bint PyBytes_CheckExact(object o)
+
+cdef extern from "stdio.h":
+    ssize_t getline(char** lineptr, size_t* n, FILE* stream) nogil
+
+cdef extern from "host_codec.h":
+    ctypedef struct ss_err:
+        int32_t kind
+        int32_t nbytes
+        int64_t read_index
+        int64_t byte_offset
+    int ssh_encode "ssh::encode"(const uint8_t* s, size_t L, uint64_t* words, ss_err* err) nogil
+    void ssh_decode "ssh::decode"(const uint64_t* words, size_t L, char* out) nogil
+    uint64_t ssh_hamming "ssh::hamming"(const uint64_t* a, const uint64_t* b, size_t L) nogil
+
+# Domain constants (short_seq_64.pyx:27-28, short_seq_192.pyx:21-22, short_seq_var.pyx:8-10)
+MIN_64_NT = 0
+MAX_64_NT = 32
+MIN_192_NT = 33
+MAX_192_NT = 96
+MIN_VAR_NT = 97
+MAX_VAR_NT = 1024
+DEF C_MAX_64 = 32
+DEF C_MAX_192 = 96
+DEF C_MAX_VAR = 1024
+DEF MAX_REPR_LEN = 75
+
+def get_domain_64(): return MIN_64_NT, MAX_64_NT
+def get_domain_192(): return MIN_192_NT, MAX_192_NT
+def get_domain_var(): return MIN_VAR_NT, MAX_VAR_NT
+
+
+cdef inline size_t _nwords(size_t L) noexcept nogil:
+    return (L + 31) // 32
+
+
+cdef object _raise_encode_error(const uint8_t* seq, ss_err* err):
+    """The reference's exception for a failed marshal (short_seq_64.pyx:105, util.pyx:115/137)."""
+    if err.kind == 2:
+        raise Exception(f"Sequences longer than {MAX_VAR_NT} bases are not supported.")
+    # PyUnicode_DecodeASCII of the offending byte / 8-byte chunk; raises UnicodeDecodeError itself
+    # for a non-ASCII byte, exactly as in the reference.
+    cdef object bad = PyUnicode_DecodeASCII(<const char*>seq + err.byte_offset, err.nbytes, NULL)
+    raise Exception(f"Unsupported base character: {bad}")
+
+
+# ==================================================================================================
+cdef class ShortSeq64:
+    """0-32 nt: one packed word + length (short_seq_64.pyx:33-90)."""
+    cdef uint64_t _packed
+    cdef uint8_t _length
+
+    def __hash__(self):
+        return <Py_ssize_t>self._packed            # short_seq_64.pyx:35-36 (-1 -> -2 by CPython)
+
+    def __len__(self):
+        return self._length
+
+    def __eq__(self, other):
+        if type(other) is ShortSeq64:
+            return self._length == (<ShortSeq64>other)._length and \
+                   self._packed == (<ShortSeq64>other)._packed
+        elif isinstance(other, (str, bytes)):
+            return self._length == len(other) and str(self) == other
+        return False
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    def __getitem__(self, item):
+        return _getitem(&self._packed, self._length, item)
+
+    def __xor__(self, ShortSeq64 other):
+        if self._length != other._length:
+            raise Exception(f"Hamming distance requires sequences of equal length "
+                            f"({self._length} != {other._length})")
+        return ssh_hamming(&self._packed, &other._packed, 1)
+
+    def __str__(self):
+        cdef char buf[32]
+        ssh_decode(&self._packed, self._length, buf)
+        return PyUnicode_DecodeASCII(buf, self._length, NULL)
+
+    def __repr__(self):
+        return f"<ShortSeq64 ({self._length} nt): {self}>"
+
+    @property
+    def packed(self):
+        """The packed words as a tuple of ints (batch-layout interop)."""
+        return (self._packed,)
+
+
+cdef class ShortSeq192:
+    """33-96 nt: three inline words + length (short_seq_192.pyx:27-97)."""
+    cdef uint64_t _packed[3]
+    cdef uint8_t _length
+
+    def __hash__(self):
+        return <Py_ssize_t>self._packed[0]         # short_seq_192.pyx:29-30
+
+    def __len__(self):
+        return self._length
+
+    def __eq__(self, other):
+        if type(other) is ShortSeq192:
+            return self._length == (<ShortSeq192>other)._length and \
+                   memcmp(self._packed, (<ShortSeq192>other)._packed, _nwords(self._length) * 8) == 0
+        elif isinstance(other, (str, bytes)):
+            return self._length == len(other) and str(self) == other
+        return False
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    def __getitem__(self, item):
+        return _getitem(self._packed, self._length, item)
+
+    def __xor__(self, ShortSeq192 other):
+        if self._length != other._length:
+            raise Exception(f"Hamming distance requires sequences of equal length "
+                            f"({self._length} != {other._length})")
+        return ssh_hamming(self._packed, other._packed, self._length)
+
+    def __str__(self):
+        cdef char buf[96]
+        ssh_decode(self._packed, self._length, buf)
+        return PyUnicode_DecodeASCII(buf, self._length, NULL)
+
+    def __repr__(self):
+        return f"<ShortSeq192 ({self._length} nt): {self}>"
+
+    @property
+    def packed(self):
+        return tuple(self._packed[i] for i in range(_nwords(self._length)))
+
+
+cdef class ShortSeqVar:
+    """97-1024 nt: heap words + length (short_seq_var.pyx:15-93)."""
+    cdef uint64_t* _packed
+    cdef size_t _length
+
+    def __hash__(self):
+        return <Py_ssize_t>self._packed[0]         # short_seq_var.pyx:16-17
+
+    def __len__(self):
+        return self._length
+
+    def __eq__(self, other):
+        if type(other) is ShortSeqVar:
+            return self._length == (<ShortSeqVar>other)._length and \
+                   memcmp(self._packed, (<ShortSeqVar>other)._packed, _nwords(self._length) * 8) == 0
+        elif isinstance(other, (str, bytes)):
+            return self._length == len(other) and str(self) == other
+        return False
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    def __getitem__(self, item):
+        return _getitem(self._packed, self._length, item)
+
+    def __xor__(self, ShortSeqVar other):
+        if self._length != other._length:
+            raise Exception(f"Hamming distance requires sequences of equal length "
+                            f"({self._length} != {other._length})")
+        return ssh_hamming(self._packed, other._packed, self._length)
+
+    def __str__(self):
+        cdef char buf[1024]
+        ssh_decode(self._packed, self._length, buf)
+        return PyUnicode_DecodeASCII(buf, self._length, NULL)
+
+    def __repr__(self):
+        cdef char buf[MAX_REPR_LEN]
+        ssh_decode(self._packed, MAX_REPR_LEN, buf)   # short_seq_var.pyx:86-89
+        return f"<ShortSeqVar ({self._length} nt): {PyUnicode_DecodeASCII(buf, MAX_REPR_LEN, NULL)} ... >"
+
+    def __sizeof__(self):
+        return sizeof(PyObject) + 16 + _nwords(self._length) * 8   # short_seq_var.pyx:83-84
+
+    def __dealloc__(self):
+        if self._packed is not NULL:
+            PyObject_Free(self._packed)
+
+    @property
+    def packed(self):
+        return tuple(self._packed[i] for i in range(_nwords(self._length)))
+
+
+# Singleton (short_seq.pyx:7)
+cdef ShortSeq64 empty = ShortSeq64.__new__(ShortSeq64)
+
+
+# ==================================================================================================
+# Construction (short_seq.pyx:13-74)
+cdef object _new(const uint8_t* seq, size_t length):
+    cdef ss_err err
+    cdef ShortSeq64 o64
+    cdef ShortSeq192 o192
+    cdef ShortSeqVar ovar
+    cdef uint64_t* words
+    if length == 0:
+        return empty
+    elif length <= C_MAX_64:
+        o64 = ShortSeq64.__new__(ShortSeq64)
+        if ssh_encode(seq, length, &o64._packed, &err):
+            _raise_encode_error(seq, &err)
+        o64._length = <uint8_t>length
+        return o64
+    elif length <= C_MAX_192:
+        o192 = ShortSeq192.__new__(ShortSeq192)
+        if ssh_encode(seq, length, o192._packed, &err):
+            _raise_encode_error(seq, &err)
+        o192._length = <uint8_t>length
+        return o192
+    elif length <= C_MAX_VAR:
+        words = <uint64_t*>PyObject_Calloc(_nwords(length), sizeof(uint64_t))
+        if words is NULL:
+            raise MemoryError(f"Error while allocating new ShortSeq of length {length}.")
+        if ssh_encode(seq, length, words, &err):
+            PyObject_Free(words)
+            _raise_encode_error(seq, &err)
+        ovar = ShortSeqVar.__new__(ShortSeqVar)
+        ovar._packed = words
+        ovar._length = length
+        return ovar
+    raise Exception(f"Sequences longer than {MAX_VAR_NT} bases are not supported.")
+
+
+cdef object _from_words(const uint64_t* w, size_t length):
+    """Object for already-packed words (batch results -> drop-in objects)."""
+    cdef ShortSeq64 o64
+    cdef ShortSeq192 o192
+    cdef ShortSeqVar ovar
+    if length == 0:
+        return empty
+    if length <= C_MAX_64:
+        o64 = ShortSeq64.__new__(ShortSeq64)
+        o64._packed = w[0]
+        o64._length = <uint8_t>length
+        return o64
+    if length <= C_MAX_192:
+        o192 = ShortSeq192.__new__(ShortSeq192)
+        memcpy(o192._packed, w, _nwords(length) * 8)
+        o192._length = <uint8_t>length
+        return o192
+    ovar = ShortSeqVar.__new__(ShortSeqVar)
+    ovar._packed = <uint64_t*>PyObject_Calloc(_nwords(length), sizeof(uint64_t))
+    if ovar._packed is NULL:
+        raise MemoryError()
+    memcpy(ovar._packed, w, _nwords(length) * 8)
+    ovar._length = length
+    return ovar
+
+
+def from_words(words, size_t length):
+    """Build a ShortSeq from packed words (sequence of ints)."""
+    cdef uint64_t buf[32]
+    cdef size_t i, n = _nwords(length)
+    if length > C_MAX_VAR:
+        raise Exception(f"Sequences longer than {MAX_VAR_NT} bases are not supported.")
+    memset(buf, 0, sizeof(buf))
+    for i in range(n):
+        buf[i] = <uint64_t>(int(words[i]) & 0xFFFFFFFFFFFFFFFF)
+    return _from_words(buf, length)
+
+
+cdef inline object _from_py_str(str s):
+    # short_seq.pyx:40-43: the raw PyUnicode buffer, length in code points (SURVEY: UCS-2 quirk kept)
+    return _new(<const uint8_t*>PyUnicode_DATA(s), <size_t>PyUnicode_GET_LENGTH(s))
+
+
+cdef inline object _from_py_bytes(bytes b):
+    return _new(<const uint8_t*>PyBytes_AS_STRING(b), <size_t>PyBytes_GET_SIZE(b))
+
+
+def pack(seq, /):
+    """short_seq.pyx:13-28."""
+    if PyUnicode_Check(seq):
+        if not seq:
+            return empty
+        return _from_py_str(seq)
+    elif PyBytes_Check(seq):
+        if not seq:
+            return empty
+        return _from_py_bytes(seq)
+    elif type(seq) is ShortSeq64 or type(seq) is ShortSeq192 or type(seq) is ShortSeqVar:
+        return seq
+    raise TypeError(f'Cannot pack objects of type "{type(seq)}"')
+
+
+def from_str(str seq_str):
+    if not seq_str:
+        return empty
+    return _from_py_str(seq_str)
+
+
+def from_bytes(bytes seq_bytes):
+    if not seq_bytes:
+        return empty
+    return _from_py_bytes(seq_bytes)
+
+
+# ==================================================================================================
+# Subscript / slice (short_seq.pyx:78-238, short_seq_64.pyx:53-75): bit-exact funnel-shift copy of
+# nts [start, start + n), trimmed to 2n bits.
+cdef object _slice_words(const uint64_t* src, size_t start, size_t n):
+    cdef uint64_t buf[32]
+    cdef size_t bit = 2 * start, nw = _nwords(n), i, w, o
+    cdef size_t tail = (2 * n) % 64
+    memset(buf, 0, sizeof(buf))
+    w = bit // 64
+    o = bit % 64
+    for i in range(nw):
+        if o == 0:
+            buf[i] = src[w + i]
+        else:
+            buf[i] = src[w + i] >> o
+            if (w + i + 1) * 32 < start + n:       # only words that hold nts of the slice
+                buf[i] |= src[w + i + 1] << (64 - o)
+    if tail:
+        buf[nw - 1] &= (1ULL << tail) - 1
+    return _from_words(buf, n)
+
+
+cdef object _getitem(const uint64_t* packed, size_t length, item):
+    cdef Py_ssize_t index, start, stop, step, slen
+    cdef ShortSeq64 one
+    if isinstance(item, slice):
+        start, stop, step = item.indices(length)
+        if step != 1:
+            raise TypeError("Slice step not supported")
+        slen = stop - start if stop > start else 0
+        if slen == 0:
+            return empty
+        return _slice_words(packed, start, slen)
+    elif isinstance(item, int):
+        index = item
+        if index < 0:
+            index += length
+        if index < 0 or index >= <Py_ssize_t>length:
+            raise IndexError("Sequence index out of range")
+        one = ShortSeq64.__new__(ShortSeq64)
+        one._packed = (packed[index // 32] >> (2 * (index % 32))) & 3
+        one._length = 1
+        return one
+    raise TypeError(f"Invalid index type: {type(item)}")
+
+
+# ==================================================================================================
+# Counter (counter.pyx:10-70)
+GPU_MIN_READS = 1 << 16     # below this a list is counted on the host (launch + copy overhead)
+
+
+cdef class ShortSeqCounter(dict):
+    """dict subclass {ShortSeq: count} in first-occurrence order (counter.pyx:10-54).
+
+    ShortSeqCounter(list_of_bytes, device="auto"): lists of >= GPU_MIN_READS reads are encoded and
+    counted on the GPU (one hash-and-atomic-count kernel per read length <= 32); device="host"
+    forces the per-object host path, device="cuda"/"cuda:N" forces the GPU.
+    """
+
+    def __init__(self, source=None, device="auto"):
+        super().__init__()
+        if type(source) is list:                    # counter.pyx:14: only lists are consumed
+            self._count_list(source, device)
+
+    def __setitem__(self, key, val):
+        if type(key) not in (ShortSeq64, ShortSeq192, ShortSeqVar):
+            raise TypeError(f"{self.__class__} does not support {type(key)} keys")
+        dict.__setitem__(self, key, val)
+
+    cdef _count_list(self, list it, device):
+        cdef Py_ssize_t n = PyList_GET_SIZE(it)
+        use_gpu = False
+        if device != "host" and n >= (GPU_MIN_READS if device == "auto" else 0):
+            if device == "auto":
+                import torch
+                use_gpu = torch.cuda.is_available()
+            else:
+                use_gpu = True
+        if use_gpu:
+            _count_batch_gpu(self, it, device)
+        else:
+            self._count_host(it)
+
+    cdef _count_host(self, list it):
+        cdef Py_ssize_t i, n = PyList_GET_SIZE(it)
+        cdef object item, seq
+        for i in range(n):
+            item = <object>PyList_GET_ITEM(it, i)
+            if not PyBytes_CheckExact(item):
+                raise TypeError(f"expected bytes, {type(item).__name__} found")
+            seq = _from_py_bytes(item)
+            dict.__setitem__(self, seq, dict.get(self, seq, 0) + 1)
+
+
+def _count_batch_gpu(ShortSeqCounter self, list reads, device):
+    """Batch path: stage the reads, count each length-group <= 32 nt on the GPU, rebuild the dict in
+    first-occurrence order.  Longer reads use the host objects (multi-word GPU keys: next round)."""
+    import numpy as np
+    import torch
+    from . import batch as B
+
+    cdef Py_ssize_t i, n = PyList_GET_SIZE(reads)
+    cdef object item
+    lens_np = np.empty(n, dtype=np.int64)
+    cdef int64_t[:] lens = lens_np
+    cdef int64_t total = 0
+    for i in range(n):
+        item = <object>PyList_GET_ITEM(reads, i)
+        if not PyBytes_CheckExact(item):
+            # the host loop would raise here unless an earlier read is invalid: find out first
+            _raise_first_error(reads, i)
+            raise TypeError(f"expected bytes, {type(item).__name__} found")
+        lens[i] = PyBytes_GET_SIZE(item)
+        total += lens[i]
+    blob_np = np.frombuffer(b"".join(reads), dtype=np.uint8) if total else np.zeros(0, np.uint8)
+    offs_np = np.zeros(n, dtype=np.int64)
+    if n:
+        np.cumsum(lens_np[:-1], out=offs_np[1:])
+    dev = torch.device("cuda", torch.cuda.current_device()) if device in ("auto", "cuda") else torch.device(device)
+
+    entries = []                      # (first_index, key_object, count)
+    first_bad = n                     # smallest invalid read index seen on any path
+    for L in np.unique(lens_np):
+        L = int(L)
+        idx = np.nonzero(lens_np == L)[0]
+        if L == 0:
+            entries.append((int(idx[0]), empty, int(len(idx))))
+            continue
+        if L > C_MAX_64:
+            sub = ShortSeqCounter(device="host")
+            firsts = {}
+            for j in idx:
+                item = <object>PyList_GET_ITEM(reads, j)
+                try:
+                    seq = _from_py_bytes(item)
+                except BaseException:
+                    first_bad = min(first_bad, int(j))
+                    break
+                if seq not in firsts:
+                    firsts[seq] = int(j)
+                dict.__setitem__(sub, seq, dict.get(sub, seq, 0) + 1)
+            for seq, c in dict.items(sub):
+                entries.append((firsts[seq], seq, c))
+            continue
+        if len(idx) == n:
+            host = torch.from_numpy(blob_np).pin_memory()
+        else:
+            rows = (offs_np[idx][:, None] + np.arange(L)[None, :]).reshape(-1)
+            host = torch.from_numpy(blob_np[rows]).pin_memory()
+        d_ascii = host.to(dev, non_blocking=True).view(-1, L)
+        cnt = B.GpuCounter(max(1024, 2 * len(idx)), device=dev)
+        try:
+            cnt.insert(d_ascii, L, base_index=0, check_errors=False)
+            fb = int(B.first_bad_buffer(dev).item())
+            if fb != -1:
+                first_bad = min(first_bad, int(idx[fb]))
+                continue
+            keys, counts, firsts = cnt.items_sorted()
+        finally:
+            cnt.close()
+        gfirst = idx[firsts.astype(np.int64)]
+        for k in range(len(keys)):
+            w = <uint64_t>keys[k]
+            entries.append((int(gfirst[k]), _from_words(&w, L), int(counts[k])))
+    if first_bad < n:
+        _raise_first_error(reads, first_bad + 1)
+        raise AssertionError("GPU flagged a read the host codec accepts")
+    entries.sort(key=lambda e: e[0])
+    for _f, key, c in entries:
+        dict.__setitem__(self, key, c)
+
+
+def _raise_first_error(list reads, Py_ssize_t upto):
+    """Re-run the reference's loop on reads[0:upto] (host codec) so the first failure raises exactly
+    the exception the reference raises."""
+    cdef Py_ssize_t i
+    cdef object item
+    for i in range(upto):
+        item = <object>PyList_GET_ITEM(reads, i)
+        if not PyBytes_CheckExact(item):
+            raise TypeError(f"expected bytes, {type(item).__name__} found")
+        _from_py_bytes(item)
+
+
+def read_and_count_fastq(filename, device="auto"):
+    """counter.pyx:57-70 + fast_read.pyx:3-20: keep line 2 of every 4 lines; each kept line loses
+    exactly its last character (strlen - 1, short_seq.pyx:50-52); prints the reference's timings."""
+    cdef FILE* f
+    cdef char* line = NULL
+    cdef size_t cap = 0
+    cdef ssize_t got
+    cdef size_t count = 1
+    cdef size_t ln
+    seqs = []
+    t1 = time.time()
+    fname = filename.encode("utf-8")
+    f = fopen(fname, "rb")
+    if f == NULL:
+        raise Exception(f"{str(fname)}: Something went wrong while reading this file.")
+    try:
+        while True:
+            got = getline(&line, &cap, f)
+            if got == -1:
+                break
+            if count % 2 == 0 and count % 4 != 0:
+                ln = strlen(line)
+                if ln == 0:   # strlen - 1 underflows in the reference -> the too-long error
+                    raise Exception(f"Sequences longer than {MAX_VAR_NT} bases are not supported.")
+                seqs.append(PyBytes_FromStringAndSize(line, ln - 1))
+            count += 1
+    finally:
+        fclose(f)
+        free(line)
+    t2 = time.time()
+    counts = ShortSeqCounter(seqs, device=device)
+    t3 = time.time()
+    print(f"{t2-t1:.2f}s to read {len(seqs)} total seqs, and {t3 - t2:.2f}s to count {len(counts)} unique sequences")
+    return counts

@@ -208,15 +208,36 @@ __global__ void k_part_scan(uint32_t nparts, const unsigned long long* part_coun
     }
 }
 
-// Extract pass 3: scatter occupied slots into their part's range.
+// Extract pass 3: scatter occupied slots into their part's range.  Positions are reserved per wave:
+// the wave peels off one distinct part at a time (readfirstlane + ballot), one lane does a single
+// atomicAdd for all the wave's entries of that part, lanes take base + rank (mbcnt).  With one part
+// (1 GPU) that is one global atomic per wave instead of one per entry.
 __global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t nparts, int32_t L,
                                                            unsigned long long* cursors, uint64_t* okeys,
                                                            uint32_t* olens, uint64_t* ocounts, uint64_t* ofirst,
                                                            uint64_t cap_out, unsigned long long* overflow) {
-    for (uint64_t s = (uint64_t)blockIdx.x * kThreads + threadIdx.x; s <= t.mask + 1; s += (uint64_t)gridDim.x * kThreads) {
-        uint64_t key;
-        if (!slot_used(t, s, key)) continue;
-        const unsigned long long pos = atomicAdd(&cursors[owner_of(key, nparts)], 1ull);
+    const uint64_t nslots = t.mask + 2;
+    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
+    // uniform trip count so every lane of a wave takes part in the ballots
+    for (uint64_t s0 = (uint64_t)blockIdx.x * kThreads; s0 < nslots; s0 += stride) {
+        const uint64_t s = s0 + threadIdx.x;
+        uint64_t key = kEmpty;
+        const bool used = s < nslots && slot_used(t, s, key);
+        const uint32_t part = used ? owner_of(key, nparts) : 0u;
+        uint64_t pending = __ballot(used);
+        unsigned long long pos = 0;
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const uint32_t p0 = (uint32_t)__shfl((int)part, leader);
+            const uint64_t mine = __ballot(used && part == p0);
+            const uint32_t rank = __popcll(mine & ((1ull << (threadIdx.x & 63)) - 1ull));
+            unsigned long long base = 0;
+            if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&cursors[p0], (unsigned long long)__popcll(mine));
+            base = __shfl(base, leader);
+            if (used && part == p0) pos = base + rank;
+            pending &= ~mine;
+        }
+        if (!used) continue;
         if (pos >= cap_out) {
             atomicOr(overflow, 2ull);
             continue;

@@ -1,0 +1,119 @@
+"""Multi-rank ShortSeqCounter protocol on CPU: world_size 2 (and 3) over gloo.
+
+The per-rank tables are a host double with GpuCounter's interface (encode via the oracle, exact
+counts / first indices, owner partition via shortseq_amd.dist.owner_of_np); the exchange, merge
+and gather logic is the product code in shortseq_amd/dist.py, the same that runs over RCCL on GPUs.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class HostTable:
+    """Test double of GpuCounter (same method names and tensor conventions)."""
+
+    def __init__(self, capacity, device=None):
+        self.d = {}
+
+    def reset(self):
+        self.d = {}
+
+    def close(self):
+        pass
+
+    def insert(self, ascii, L, base_index=0, check_errors=True):
+        import oracle
+        a = ascii.numpy().reshape(-1)
+        n = a.size // L
+        words, rc, _ = oracle.encode_batch(a, n, L)
+        assert rc == 0
+        for i, w in enumerate(words[:, 0]):
+            k = int(w)
+            c, f = self.d.get(k, (0, 1 << 62))
+            self.d[k] = (c + 1, min(f, base_index + i))
+
+    def merge(self, keys, counts, first, L):
+        for k, c, f in zip(keys.numpy().view(np.uint64).tolist(), counts.tolist(), first.tolist()):
+            c0, f0 = self.d.get(k, (0, 1 << 62))
+            self.d[k] = (c0 + c, min(f0, f))
+
+    def extract(self, n_parts=1, cap=None):
+        from shortseq_amd.dist import owner_of_np
+        ks = np.array(sorted(self.d), dtype=np.uint64)
+        own = owner_of_np(ks, n_parts) if len(ks) else np.zeros(0, np.int64)
+        o = np.argsort(own, kind="stable")
+        ks = ks[o]
+        cs = np.array([self.d[int(k)][0] for k in ks], np.int64)
+        fs = np.array([self.d[int(k)][1] for k in ks], np.int64)
+        parts = np.bincount(own, minlength=n_parts).astype(np.int64)
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x))  # noqa: E731
+        return t(ks.view(np.int64)), t(np.full(len(ks), 32, np.int32)), t(cs), t(fs), t(parts)
+
+
+def _worker(rank, world, port, n, L, U, q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from shortseq_amd.dist import ShardedCounter
+        per = n // world
+        a = oracle.gen_pool_reads(5, 6, U, rank * per, per, L)
+        sc = ShardedCounter(1024, device="cpu", table_factory=HostTable)
+        sc.count(torch.from_numpy(a).view(per, L), L, base_index=rank * per)
+        # every owned key really belongs to this rank
+        keys, _l, _c, _f, parts = sc.owned().extract(1)
+        from shortseq_amd.dist import owner_of_np
+        own = owner_of_np(keys.numpy().view(np.uint64), world)
+        assert (own == rank).all()
+        res = sc.gather_items(dst=0)
+        if rank == 0:
+            q.put([np.asarray(x).tolist() for x in res])
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_counter_gloo(oracle, world):
+    n, L, U = 3000, 32, 200
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, L, U, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    keys, counts, first = res
+    per = n // world
+    a = oracle.gen_pool_reads(5, 6, U, 0, per * world, L)
+    exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(per * world)])
+    assert [int(k) for k in keys] == [w[0] for (w, _L, _c, _f) in exp]
+    assert counts == [c for (_w, _L, c, _f) in exp]
+    assert first == [f for (_w, _L, _c, f) in exp]
+
+
+def test_owner_partition_is_balanced():
+    from shortseq_amd.dist import owner_of_np
+    keys = np.arange(100000, dtype=np.uint64) * np.uint64(0x9E3779B1)
+    for world in (2, 4, 8):
+        c = np.bincount(owner_of_np(keys, world), minlength=world)
+        assert c.min() > 0.9 * len(keys) / world

@@ -1,0 +1,140 @@
+// tools/tune_encode.hip — parameter sweep for the 32-nt dense encode (BASELINE configs[1]).
+//
+// Builds a standalone binary: hipcc -O3 --offload-arch=gfx950 -I include tools/tune_encode.hip -o tools/tune_encode
+// Run: tools/tune_encode [n_reads=100000000] [reps=20]
+// For each variant prints GB/s of algorithmic bytes (32 B in + 8 B out per read) from hipEvents,
+// next to two ceilings with the SAME access pattern and trivial compute:
+//   copy4to1: the same loads/stores, v = x.x ^ x.y ^ x.z ^ x.w    (memory-only ceiling)
+//   readonly: the same loads, one store per block               (read ceiling)
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#include "../shortseq_amd/csrc/ss_device.h"
+
+using namespace ssd;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld(const uint4* p) {
+    if constexpr (NT) return ld_stream(p);
+    else return *p;
+}
+
+enum Mode { ENC = 0, COPY = 1, READ = 2 };
+
+template <int T, int U, bool NT, bool PERSIST, bool ST64, int MODE>
+__global__ __launch_bounds__(T) void k_var(const uint4* __restrict__ in, uint32_t* __restrict__ out,
+                                          uint64_t nchunks, unsigned long long* fb) {
+    const uint64_t step = PERSIST ? (uint64_t)gridDim.x * T * U : 0;
+    uint32_t acc = 0;
+    for (uint64_t base = (uint64_t)blockIdx.x * T * U + threadIdx.x; base < nchunks; base += step) {
+        uint4 x[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint64_t g = base + (uint64_t)j * T;
+            x[j] = g < nchunks ? ld<NT>(&in[g]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint64_t g = base + (uint64_t)j * T;
+            uint32_t v;
+            if constexpr (MODE == ENC) {
+                Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, true);
+                v = e.v | ((threadIdx.x & 1u) ? swap_pair(e.cout) : 0u);
+                report_bad(g < nchunks && e.bad != 0u, g >> 1, fb);
+            } else {
+                v = x[j].x ^ x[j].y ^ x[j].z ^ x[j].w;
+            }
+            if constexpr (MODE == READ) {
+                acc ^= v;
+            } else if constexpr (ST64) {
+                const uint32_t hi = swap_pair(v);
+                if (!(threadIdx.x & 1u) && g < nchunks) ((uint64_t*)out)[g >> 1] = (uint64_t)v | ((uint64_t)hi << 32);
+            } else {
+                if (g < nchunks) out[g] = v;
+            }
+        }
+        if (!PERSIST) break;
+    }
+    if constexpr (MODE == READ) {
+        if (acc == 0x12345678u) out[blockIdx.x] = acc;   // keep the loads alive
+    }
+}
+
+__global__ void k_fill(uint8_t* p, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 16; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t r = splitmix64(i);
+        ((uint4*)p)[i] = decode16((uint32_t)r);
+    }
+}
+
+struct Buf { uint4* in; uint32_t* out; unsigned long long* fb; uint64_t nchunks; uint64_t nreads; };
+
+template <int T, int U, bool NT, bool PERSIST, bool ST64, int MODE>
+void run(const char* name, Buf& b, int reps, int blocks_per_cu) {
+    int cus = 256;
+    uint64_t per_block = (uint64_t)T * U;
+    uint64_t full = (b.nchunks + per_block - 1) / per_block;
+    unsigned grid = PERSIST ? (unsigned)std::min<uint64_t>(full, (uint64_t)cus * blocks_per_cu) : (unsigned)full;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int w = 0; w < 3; ++w)
+        hipLaunchKernelGGL((k_var<T, U, NT, PERSIST, ST64, MODE>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
+    CK(hipDeviceSynchronize());
+    std::vector<float> ms(reps);
+    for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL((k_var<T, U, NT, PERSIST, ST64, MODE>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms[r], e0, e1));
+    }
+    double s = 0, mn = 1e9;
+    for (float m : ms) { s += m; mn = std::min<double>(mn, m); }
+    double avg = s / reps;
+    double bytes = (double)b.nreads * (MODE == READ ? 32.0 : 40.0);
+    printf("%-44s grid %7u  avg %.4f ms  min %.4f ms  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", name, grid, avg, mn,
+           bytes / avg / 1e6, bytes / mn / 1e6);
+    fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 100000000ull;
+    int reps = argc > 2 ? atoi(argv[2]) : 20;
+    Buf b;
+    b.nreads = n;
+    b.nchunks = 2 * n;
+    CK(hipMalloc(&b.in, n * 32));
+    CK(hipMalloc(&b.out, n * 8));
+    CK(hipMalloc(&b.fb, 8));
+    CK(hipMemset(b.fb, 0xFF, 8));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint8_t*)b.in, n * 32);
+    CK(hipDeviceSynchronize());
+    printf("reads %llu (%.2f GB in, %.2f GB out)\n", (unsigned long long)n, n * 32 / 1e9, n * 8 / 1e9);
+    // ceilings
+    run<256, 4, true, false, false, COPY>("copy4to1 T256 U4 nt", b, reps, 0);
+    run<256, 4, false, false, false, COPY>("copy4to1 T256 U4", b, reps, 0);
+    run<256, 8, true, true, false, COPY>("copy4to1 T256 U8 nt persist8", b, reps, 8);
+    run<256, 4, true, false, false, READ>("readonly T256 U4 nt", b, reps, 0);
+    run<256, 8, false, true, false, READ>("readonly T256 U8 persist8", b, reps, 8);
+    // encode variants
+    run<256, 4, true, false, false, ENC>("enc T256 U4 nt (production)", b, reps, 0);
+    run<256, 4, false, false, false, ENC>("enc T256 U4", b, reps, 0);
+    run<256, 1, true, false, false, ENC>("enc T256 U1 nt", b, reps, 0);
+    run<256, 2, true, false, false, ENC>("enc T256 U2 nt", b, reps, 0);
+    run<256, 8, true, false, false, ENC>("enc T256 U8 nt", b, reps, 0);
+    run<512, 4, true, false, false, ENC>("enc T512 U4 nt", b, reps, 0);
+    run<1024, 2, true, false, false, ENC>("enc T1024 U2 nt", b, reps, 0);
+    run<256, 4, true, false, true, ENC>("enc T256 U4 nt st64", b, reps, 0);
+    run<256, 4, true, true, false, ENC>("enc T256 U4 nt persist4", b, reps, 4);
+    run<256, 4, true, true, false, ENC>("enc T256 U4 nt persist8", b, reps, 8);
+    run<256, 8, true, true, false, ENC>("enc T256 U8 nt persist8", b, reps, 8);
+    run<256, 8, false, true, false, ENC>("enc T256 U8 persist8", b, reps, 8);
+    run<256, 4, true, true, false, ENC>("enc T256 U4 nt persist16", b, reps, 16);
+    run<512, 8, true, true, false, ENC>("enc T512 U8 nt persist4", b, reps, 4);
+    return 0;
+}
