@@ -59,6 +59,7 @@ class Timer:
 
     def __init__(self):
         self.pairs = []
+        self.region_ms = float("nan")
 
     def __enter__(self):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -75,17 +76,24 @@ class Timer:
 
 
 def timed_loop(step, steps, warmup, world):
-    """W untimed steps, then K steps between barrier + synchronize; returns max-over-ranks seconds."""
+    """W untimed steps, then K steps between barrier + synchronize; returns max-over-ranks seconds
+    and a Timer.  The Timer's `region` pair brackets all K steps on the launch stream, so
+    region_ms / K is the per-step device time with the launch queue kept full (no host launch
+    latency inside the window); per-kernel pairs are recorded by steps that time sub-kernels."""
     for _ in range(warmup):
         step(None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     timer = Timer()
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    r0.record()
     for _ in range(steps):
         step(timer)
+    r1.record()
     torch.cuda.synchronize()
+    timer.region_ms = r0.elapsed_time(r1)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -129,11 +137,7 @@ def bench_encode(B, lib, dev, rank, world, n, L, steps, warmup, seed=1):
     ap, wp, fp = ascii.data_ptr(), words.data_ptr(), fb.data_ptr()
 
     def step(timer):
-        if timer is None:
-            rc = lib.ss_encode_fixed(ap, n, L, L, wp, wpr, fp, stream)
-        else:
-            with timer:
-                rc = lib.ss_encode_fixed(ap, n, L, L, wp, wpr, fp, stream)
+        rc = lib.ss_encode_fixed(ap, n, L, L, wp, wpr, fp, stream)
         if rc:
             raise RuntimeError(lib.ss_last_error_string())
 
@@ -142,7 +146,8 @@ def bench_encode(B, lib, dev, rank, world, n, L, steps, warmup, seed=1):
         raise SystemExit("PARITY FAILURE: synthetic batch flagged an invalid base")
     check_known_answer(words, seed, i0, L, n)
     del ascii, words
-    return el, timer.mean_ms()
+    # every step is exactly one encode launch (the first-bad reset is a 8-byte memset node)
+    return el, timer.region_ms / steps
 
 
 def bench_encode_hamming(B, lib, dev, rank, world, n, L, steps, warmup, seed=2):
@@ -175,7 +180,7 @@ def bench_encode_hamming(B, lib, dev, rank, world, n, L, steps, warmup, seed=2):
     if not torch.equal(d2, dist_out):
         raise SystemExit("PARITY FAILURE: fused hamming != hamming on packed words")
     del ascii, words, dist_out, d2
-    return el, timer.mean_ms()
+    return el, timer.mean_ms(), timer.region_ms / steps
 
 
 def bench_roundtrip(B, lib, dev, rank, world, n, L, steps, warmup, seed=3):
@@ -200,63 +205,39 @@ def bench_roundtrip(B, lib, dev, rank, world, n, L, steps, warmup, seed=3):
         if rc:
             raise RuntimeError(lib.ss_last_error_string())
 
-    el, _ = timed_loop(step, steps, warmup, world)
+    el, tr = timed_loop(step, steps, warmup, world)
     if not torch.equal(back, ascii):
         raise SystemExit("PARITY FAILURE: encode -> decode round trip")
     check_known_answer(words, seed, i0, L, n)
     del ascii, words, back
-    return el, t_enc.mean_ms(), t_dec.mean_ms()
+    return el, t_enc.mean_ms(), t_dec.mean_ms(), tr.region_ms / steps
 
 
 def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool_seed=77):
-    """C5: per rank n reads drawn from a pool of U 32-mers; count locally, partition by owner,
-    all-to-all the (key, count, first) triples over RCCL, owners merge."""
+    """C5: per rank n reads drawn from a pool of U 32-mers (shard = contiguous read-index range);
+    shortseq_amd.dist.ShardedCounter: local HBM table -> partition by owner -> RCCL all-to-all of
+    (key, count, first) -> owners merge."""
+    from shortseq_amd.dist import ShardedCounter
     i0 = rank * n
     ascii = B.synth_pool_reads(n, L, seed, pool_seed, U, i0=i0, device=dev)
     cap = 1 << max(10, int(np.ceil(np.log2(2 * U))))
-    local = B.GpuCounter(cap, device=dev)
-    owner = B.GpuCounter(cap, device=dev) if world > 1 else None
-    t_ins = Timer()
-    state = {}
+    sc = ShardedCounter(cap, device=dev)
 
     def step(timer):
-        local.reset()
-        if timer is None:
-            local.insert(ascii, L, base_index=i0, check_errors=False)
-        else:
-            with t_ins:
-                local.insert(ascii, L, base_index=i0, check_errors=False)
-        keys, lens, counts, first, parts = local.extract(n_parts=world)
-        if world > 1:
-            owner.reset()
-            send = torch.stack([keys, counts, first], 1)
-            sc = parts.cpu().tolist()
-            m = sum(sc)
-            rc_t = torch.empty(world, dtype=torch.int64, device=dev)
-            dist.all_to_all_single(rc_t, parts)
-            rc = rc_t.cpu().tolist()
-            recv = torch.empty((sum(rc), 3), dtype=torch.int64, device=dev)
-            dist.all_to_all_single(recv, send[:m].contiguous(), output_split_sizes=rc, input_split_sizes=sc)
-            owner.merge(recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous(), L)
-            state["result"] = owner
-        else:
-            state["result"] = local
-            state["m"] = parts
+        sc.count(ascii, L, base_index=i0, check_errors=False)
 
-    el, _ = timed_loop(step, steps, warmup, world)
-    res = state["result"]
-    k, c, f = res.items_sorted()
+    el, tr = timed_loop(step, steps, warmup, world)
+    owned = sc.owned()
+    k, c, f = owned.items_sorted()
     tot = torch.tensor([int(c.sum()), len(k)], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(tot)
     if int(tot[0]) != n * world:
         raise SystemExit(f"PARITY FAILURE: counter total {int(tot[0])} != {n * world}")
     uniq = int(tot[1])
-    local.close()
-    if owner is not None:
-        owner.close()
+    sc.close()
     del ascii
-    return el, t_ins.mean_ms(), uniq
+    return el, tr.region_ms / steps, uniq
 
 
 # ------------------------------------------------------------------------------------------------
@@ -352,29 +333,32 @@ def main():
         extra = {}
         L3, n3 = 96, args.n
         log(f"C3 fused encode+hamming {n3} x {L3}")
-        el3, k3 = bench_encode_hamming(B, lib, dev, rank, world, n3, L3, args.steps, args.warmup)
+        el3, k3, d3 = bench_encode_hamming(B, lib, dev, rank, world, n3, L3, args.steps, args.warmup)
         b3 = n3 * (96 + 24 + 4)
         extra["C3_encode_hamming_96"] = {
             "pairs_per_s": n3 * world / (el3 / args.steps), "nt_per_s": n3 * L3 * world / (el3 / args.steps),
-            "ms_per_step": el3 / args.steps * 1e3, "kernel_ms": k3,
-            "roofline": {"achieved": b3 / (k3 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": b3 / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, "algo_bytes_per_launch": b3}}
+            "ms_per_step": el3 / args.steps * 1e3, "kernel_ms_events": k3, "device_ms_per_step": d3,
+            "roofline": {"kernel": "k_encode_ham_dense", "achieved": b3 / (d3 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": b3 / (d3 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "algo_bytes_per_step": b3,
+                         "note": "device time per step over the timed region (incl. the 1-read ref encode)"}}
         L4, n4 = 512, args.n // 2
         log(f"C4 encode+decode {n4} x {L4}")
-        el4, ke, kd = bench_roundtrip(B, lib, dev, rank, world, n4, L4, max(5, args.steps // 2), args.warmup)
+        s4 = max(5, args.steps // 2)
+        el4, ke, kd, d4 = bench_roundtrip(B, lib, dev, rank, world, n4, L4, s4, args.warmup)
         b4e, b4d = n4 * (512 + 128), n4 * (128 + 512)
         extra["C4_roundtrip_512"] = {
-            "nt_per_s": n4 * L4 * world / (el4 / max(5, args.steps // 2)),
-            "ms_per_step": el4 / max(5, args.steps // 2) * 1e3, "encode_kernel_ms": ke, "decode_kernel_ms": kd,
-            "roofline": {"achieved": (b4e + b4d) / ((ke + kd) * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": (b4e + b4d) / ((ke + kd) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "nt_per_s": n4 * L4 * world / (el4 / s4), "ms_per_step": el4 / s4 * 1e3,
+            "encode_kernel_ms_events": ke, "decode_kernel_ms_events": kd, "device_ms_per_step": d4,
+            "roofline": {"kernel": "k_encode_g16<pext> + k_decode_g16", "achieved": (b4e + b4d) / (d4 * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (b4e + b4d) / (d4 * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "algo_bytes_per_step": b4e + b4d}}
         n5, U5 = 125_000_000, 1 << 24
         log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
-        el5, ki, uniq = bench_counter(B, lib, dev, rank, world, n5, 32, U5, max(3, args.steps // 4), 2)
         s5 = max(3, args.steps // 4)
+        el5, d5, uniq = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
         extra["C5_counter_32"] = {
-            "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "insert_kernel_ms": ki,
+            "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
             "reads_per_gpu": n5, "pool": U5, "unique": uniq,
             "merge": "RCCL all_to_all_single of (key, count, first) by owner" if world > 1 else "none (1 GPU)"}
         result["extra"] = extra

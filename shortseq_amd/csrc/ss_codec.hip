@@ -15,7 +15,7 @@ namespace {
 
 using namespace ssd;
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;        // general / grid-stride kernels
 
 __host__ __device__ inline uint32_t words_for(uint32_t L) { return (L + 31u) / 32u; }
 __host__ __device__ inline uint32_t ham_words(uint32_t L) { return L <= 32u ? 1u : words_for(L); }
@@ -47,17 +47,46 @@ struct G16Args {
     unsigned long long* first_bad;
 };
 
+// Compile-time path of every chunk of a launch (the launcher picks it from L):
+//   kPathTable: L <= 32, every chunk on the table path (short_seq_64.pyx:96-108)
+//   kPathPext:  L % 32 == 0 and L >= 64, every chunk a full PEXT block chunk (util.pyx:100-119):
+//               no alias carries at all, so no neighbour exchange
+//   kPathMixed: per chunk, k >= full2 -> table path (the L % 32 tail block, util.pyx:92-94)
+enum { kPathMixed = 0, kPathTable = 1, kPathPext = 2 };
+
+template <int PATH>
+__device__ __forceinline__ uint32_t encode_chunk(const uint4& x, uint32_t k, const G16Args& a, uint32_t& bad) {
+    const bool table = PATH == kPathTable ? true : (PATH == kPathPext ? false : (a.all_table || k >= a.full2));
+    const Enc32 e = encode16(x.x, x.y, x.z, x.w, table);
+    bad = e.bad;
+    if constexpr (PATH == kPathPext) return e.v;
+    const uint32_t cin = swap_pair(e.cout);            // carry from the neighbouring (lower) half
+    return e.v | ((k & 1u) ? cin : 0u);
+}
+
+// XCD-contiguous block order: the dispatcher deals blocks round-robin over the 8 XCDs (observed,
+// MI355X_MICROARCH.md §Workgroup dispatch; speed only, never correctness), so block b runs on XCD
+// b % 8; remapping gives each XCD one contiguous eighth of the stream.
+template <bool XCD>
+__device__ __forceinline__ uint64_t block_order() {
+    if constexpr (!XCD) return blockIdx.x;
+    const uint32_t per = (gridDim.x + 7u) / 8u;
+    const uint64_t b = (uint64_t)(blockIdx.x % 8u) * per + blockIdx.x / 8u;
+    return b;
+}
+
 // DENSE: stride == L, wpr == L/32, L % 32 == 0 -> lane slot g IS the chunk index and the u32
 // output index (no per-lane read/chunk arithmetic, a pure 16 B -> 4 B stream).
-template <bool HAM, bool DENSE, int U>
-__global__ __launch_bounds__(kThreads) void k_encode_g16(G16Args a) {
+// Otherwise lane slot g -> read r = g >> logG, chunk k = g & (G-1) (G = next_pow2(2*wpr)).
+template <bool HAM, bool DENSE, int PATH, int T, int U, bool XCD, bool NTST>
+__global__ __launch_bounds__(T) void k_encode_g16(G16Args a) {
     const uint32_t G = 1u << a.logG;
-    const uint64_t base = (uint64_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+    const uint64_t base = block_order<XCD>() * (U * T) + threadIdx.x;
     const uint64_t nslots = DENSE ? a.n * a.cpr : 0;
     uint4 x[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t g = base + (uint64_t)j * T;
         if constexpr (DENSE) {
             x[j] = g < nslots ? ld_stream(&a.in[g]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
         } else {
@@ -71,25 +100,70 @@ __global__ __launch_bounds__(kThreads) void k_encode_g16(G16Args a) {
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t g = base + (uint64_t)j * T;
         const uint64_t r = g >> a.logG;
         const uint32_t k = (uint32_t)g & (G - 1u);
-        const bool table = a.all_table || k >= a.full2;
-        Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, table);
-        const uint32_t cin = swap_pair(e.cout);
-        const uint32_t v = e.v | ((k & 1u) ? cin : 0u);
+        uint32_t bad;
+        const uint32_t v = encode_chunk<PATH>(x[j], k, a, bad);
         const bool live = DENSE ? g < nslots : r < a.n;
-        report_bad(live && e.bad != 0u, r, a.first_bad);
+        if constexpr (DENSE) report_bad_div(live && bad != 0u, g, a.cpr, a.first_bad);
+        else report_bad(live && bad != 0u, r, a.first_bad);
+        uint32_t* dst = nullptr;
         if constexpr (DENSE) {
-            if (a.out32 && live) a.out32[g] = v;
+            if (a.out32 && live) dst = &a.out32[g];
         } else {
-            if (a.out32 && live && k < a.wpr2) a.out32[r * a.wpr2 + k] = v;
+            if (a.out32 && live && k < a.wpr2) dst = &a.out32[r * a.wpr2 + k];
+        }
+        if (dst) {
+            if constexpr (NTST) st_stream(dst, v);
+            else *dst = v;
         }
         if constexpr (HAM) {
             uint32_t part = (k < a.ham2) ? ham32(v ^ a.ref32[k]) : 0u;
             for (uint32_t s = 1; s < G; s <<= 1) part += __shfl_xor(part, s);
             if (live && k == 0) a.counts[r] = part;
         }
+    }
+}
+
+// Dense fused encode + hamming for any even chunks-per-read (e.g. 96 nt: 6 chunks = 3 words): the
+// block owns rpb whole reads = rpb*cpr consecutive chunks (dense, coalesced loads/stores as in the
+// DENSE encode); per-read sums go through LDS atomics, then one coalesced u32 store per read.
+// Local read index = floor((cl + 0.5) * (1/cpr)) in f32 (exact for cl < 4096, cpr <= 64; checked
+// exhaustively, and written with _rn intrinsics so no FMA contraction changes the rounding).
+template <int PATH, int T, int U, bool NTST>
+__global__ __launch_bounds__(T) void k_encode_ham_dense(G16Args a, uint32_t rpb, float inv_cpr) {
+    __shared__ uint8_t part[T * U];                  // per-chunk distance (<= 16), chunk order
+    const uint64_t r0 = (uint64_t)blockIdx.x * rpb;
+    const uint32_t nr = (uint32_t)min((uint64_t)rpb, a.n - r0);
+    const uint32_t nloc = nr * a.cpr;
+    const uint64_t c0 = r0 * a.cpr;
+    uint4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t cl = j * T + threadIdx.x;
+        x[j] = cl < nloc ? ld_stream(&a.in[c0 + cl]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t cl = j * T + threadIdx.x;
+        const uint32_t rl = (uint32_t)__fmul_rn(__fadd_rn((float)cl, 0.5f), inv_cpr);
+        const uint32_t k = cl - rl * a.cpr;
+        uint32_t bad;
+        const uint32_t v = encode_chunk<PATH>(x[j], k, a, bad);
+        const bool live = cl < nloc;
+        report_bad(live && bad != 0u, r0 + rl, a.first_bad);
+        if (live && a.out32) {
+            if constexpr (NTST) st_stream(&a.out32[c0 + cl], v);
+            else a.out32[c0 + cl] = v;
+        }
+        part[cl] = (uint8_t)((live && k < a.ham2) ? ham32(v ^ a.ref32[k]) : 0u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nr; i += T) {
+        uint32_t sum = 0;
+        for (uint32_t k = 0; k < a.cpr; ++k) sum += part[i * a.cpr + k];
+        a.counts[r0 + i] = sum;
     }
 }
 
@@ -125,55 +199,74 @@ __device__ __forceinline__ uint64_t encode_word_at(const uint8_t* p, uint32_t nb
     return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
 }
 
-template <bool VAR>
+// Lane slot g -> read r = g >> logG, word w = g & (G-1) (G = next_pow2(wpr)); lanes w >= wpr idle.
+// The grid-stride loop has a uniform trip count so the hamming reduction's shuffles see whole waves.
+template <bool VAR, bool HAM>
 __global__ __launch_bounds__(kThreads) void k_encode_gen(const uint8_t* in, uint64_t stride,
                                                          const uint64_t* offs, const uint32_t* lens,
                                                          uint32_t Lfix, uint64_t n, uint64_t* out,
-                                                         uint32_t wpr, unsigned long long* first_bad) {
-    const uint64_t total = n * wpr;
-    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total;
-         g += (uint64_t)gridDim.x * kThreads) {
-        const uint64_t r = g / wpr;
-        const uint32_t w = (uint32_t)(g - r * wpr);
-        const uint32_t L = VAR ? lens[r] : Lfix;
-        const uint64_t off = VAR ? offs[r] : r * stride;
+                                                         uint32_t wpr, uint32_t logG, const uint64_t* ref,
+                                                         uint32_t hamw, uint32_t* counts,
+                                                         unsigned long long* first_bad) {
+    const uint32_t G = 1u << logG;
+    const uint64_t total = n << logG;
+    const uint64_t gstride = (uint64_t)gridDim.x * kThreads;
+    for (uint64_t g0 = (uint64_t)blockIdx.x * kThreads; g0 < total; g0 += gstride) {
+        const uint64_t g = g0 + threadIdx.x;
+        const uint64_t r = g >> logG;
+        const uint32_t w = (uint32_t)g & (G - 1u);
+        const bool live = r < n;
         uint32_t bad = 0;
         uint64_t word = 0;
-        if (L > SS_MAX_NT) {
-            bad = (w == 0);                     // short_seq.pyx:74 (too long) — reported per read
-        } else if (32u * w < L) {
-            const uint32_t nb = min(32u, L - 32u * w);
-            const bool table = (L <= 32u) || (nb < 32u);
-            word = encode_word_at(in + off + 32u * w, nb, table, bad);
+        if (live && w < wpr) {
+            const uint32_t L = VAR ? lens[r] : Lfix;
+            const uint64_t off = VAR ? offs[r] : r * stride;
+            if (L > SS_MAX_NT) {
+                bad = (w == 0);                     // short_seq.pyx:74 (too long), reported per read
+            } else if (32u * w < L) {
+                const uint32_t nb = min(32u, L - 32u * w);
+                const bool table = (L <= 32u) || (nb < 32u);
+                word = encode_word_at(in + off + 32u * w, nb, table, bad);
+            }
+            if (out) out[r * wpr + w] = word;
         }
-        out[g] = word;
         if (bad) atomicMin(first_bad, (unsigned long long)r);
+        if constexpr (HAM) {
+            uint32_t part = (live && w < hamw) ? ham64(word ^ ref[w]) : 0u;
+            for (uint32_t sft = 1; sft < G; sft <<= 1) part += __shfl_xor(part, sft);
+            if (live && w == 0) counts[r] = part;
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // Decode
 // ------------------------------------------------------------------------------------------------
-template <int U>
-__global__ __launch_bounds__(kThreads) void k_decode_g16(const uint32_t* __restrict__ w32, uint32_t wpr2,
-                                                         uint64_t n, uint32_t cpr, uint32_t logG,
-                                                         uint4* __restrict__ out, uint64_t out_stride16) {
+template <int T, int U, bool NTLD, bool NTST>
+__global__ __launch_bounds__(T) void k_decode_g16(const uint32_t* __restrict__ w32, uint32_t wpr2,
+                                                  uint64_t n, uint32_t cpr, uint32_t logG,
+                                                  uint4* __restrict__ out, uint64_t out_stride16) {
     const uint32_t G = 1u << logG;
-    const uint64_t base = (uint64_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * (U * T) + threadIdx.x;
     uint32_t v[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t g = base + (uint64_t)j * T;
         const uint64_t r = g >> logG;
         const uint32_t k = (uint32_t)g & (G - 1u);
-        v[j] = (r < n && k < cpr) ? __builtin_nontemporal_load(&w32[r * wpr2 + k]) : 0u;
+        const bool ok = r < n && k < cpr;
+        if constexpr (NTLD) v[j] = ok ? __builtin_nontemporal_load(&w32[r * wpr2 + k]) : 0u;
+        else v[j] = ok ? w32[r * wpr2 + k] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const uint64_t g = base + (uint64_t)j * kThreads;
+        const uint64_t g = base + (uint64_t)j * T;
         const uint64_t r = g >> logG;
         const uint32_t k = (uint32_t)g & (G - 1u);
-        if (r < n && k < cpr) out[r * out_stride16 + k] = decode16(v[j]);
+        if (r < n && k < cpr) {
+            if constexpr (NTST) st_stream(&out[r * out_stride16 + k], decode16(v[j]));
+            else out[r * out_stride16 + k] = decode16(v[j]);
+        }
     }
 }
 
@@ -274,6 +367,59 @@ constexpr unsigned kGenGridCap = 256u * 16u;   // grid-stride general kernels: 1
 }  // namespace
 
 // ==================================================================================================
+// Launch configurations.  Streaming kernels: T threads x U chunks of 16 B per thread, NT loads;
+// shapes picked by tools/tune_kernels.hip sweeps of these exact kernels on MI355X (profiles/r1/).
+// ==================================================================================================
+namespace {
+
+template <bool HAM, bool DENSE, int PATH, int T, int U, bool XCD, bool NTST>
+void launch_g16(const G16Args& a, hipStream_t s) {
+    const uint64_t slots = DENSE ? a.n * a.cpr : (a.n << a.logG);
+    unsigned grid = grid_for(slots, (uint64_t)T * U);
+    if (XCD) grid = (grid + 7u) / 8u * 8u;
+    hipLaunchKernelGGL((k_encode_g16<HAM, DENSE, PATH, T, U, XCD, NTST>), dim3(grid), dim3(T), 0, s, a);
+}
+
+template <int PATH, int T, int U, bool NTST>
+void launch_ham_dense(const G16Args& a, hipStream_t s) {
+    const uint32_t rpb = (U * T) / a.cpr;
+    hipLaunchKernelGGL((k_encode_ham_dense<PATH, T, U, NTST>), dim3(grid_for(a.n, rpb)), dim3(T), 0, s, a, rpb,
+                       1.0f / (float)a.cpr);
+}
+
+template <int T, int U, bool NTLD, bool NTST>
+void launch_decode_g16(const uint32_t* w32, uint32_t wpr2, uint64_t n, uint32_t cpr, uint32_t logG, uint4* out,
+                       uint64_t out_stride16, hipStream_t s) {
+    const unsigned grid = grid_for(n << logG, (uint64_t)U * T);
+    hipLaunchKernelGGL((k_decode_g16<T, U, NTLD, NTST>), dim3(grid), dim3(T), 0, s, w32, wpr2, n, cpr, logG, out,
+                       out_stride16);
+}
+
+// Production shapes
+constexpr int kEncT = 768, kEncU = 2;        // dense encode (32 / 64.. / 512 / 1024 nt)
+constexpr bool kEncXcd = false, kEncNtSt = true;
+constexpr int kHamT = 768, kHamU = 2;        // fused encode + hamming (dense, LDS reduction)
+constexpr int kDecT = 256, kDecU = 2;        // decode
+constexpr bool kDecNtLd = false, kDecNtSt = false;
+
+void launch_encode_fast(const G16Args& a, bool dense, bool ham, uint32_t L, hipStream_t s) {
+    const int path = L <= 32 ? kPathTable : (L % 32 == 0 ? kPathPext : kPathMixed);
+    if (ham && dense) {
+        if (path == kPathTable) launch_ham_dense<kPathTable, kHamT, kHamU, true>(a, s);
+        else launch_ham_dense<kPathPext, kHamT, kHamU, true>(a, s);
+    } else if (ham) {
+        launch_g16<true, false, kPathMixed, 256, 4, false, true>(a, s);
+    } else if (dense) {
+        if (path == kPathTable) launch_g16<false, true, kPathTable, kEncT, kEncU, kEncXcd, kEncNtSt>(a, s);
+        else launch_g16<false, true, kPathPext, kEncT, kEncU, kEncXcd, kEncNtSt>(a, s);
+    } else {
+        launch_g16<false, false, kPathMixed, 256, 4, false, true>(a, s);
+    }
+}
+
+}  // namespace
+
+// ==================================================================================================
 // C ABI
 // ==================================================================================================
 extern "C" {
@@ -313,31 +459,21 @@ int ss_encode_fixed_impl(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_
         a.ham2 = 2 * ham_words(L);
         a.counts = d_out;
         a.first_bad = (unsigned long long*)d_first_bad;
-        constexpr int U = 4;
-        const bool dense = stride == L && L % 32u == 0 && a.wpr2 == a.cpr && (1u << a.logG) == a.cpr;
-        const uint64_t slots = dense ? n * a.cpr : (n << a.logG);
-        const unsigned grid = grid_for(slots, (uint64_t)U * kThreads);
-        if (ham && dense)
-            hipLaunchKernelGGL((k_encode_g16<true, true, U>), dim3(grid), dim3(kThreads), 0, s, a);
-        else if (ham)
-            hipLaunchKernelGGL((k_encode_g16<true, false, U>), dim3(grid), dim3(kThreads), 0, s, a);
-        else if (dense)
-            hipLaunchKernelGGL((k_encode_g16<false, true, U>), dim3(grid), dim3(kThreads), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_encode_g16<false, false, U>), dim3(grid), dim3(kThreads), 0, s, a);
+        const bool dense = stride == L && L % 32u == 0 && a.wpr2 == a.cpr;
+        launch_encode_fast(a, dense, ham, L, s);
         return ss_check(hipGetLastError(), "k_encode_g16");
     }
-    if (ham) {
-        // General-path fused hamming: encode then hamming on the packed words (two passes).
-        if (!d_words) return ss_fail(SS_EARG, "general-path hamming needs d_words");
-    }
-    const unsigned grid = grid_for(n * wpr, kThreads, kGenGridCap);
-    hipLaunchKernelGGL((k_encode_gen<false>), dim3(grid), dim3(kThreads), 0, s, d_ascii, stride,
-                       (const uint64_t*)nullptr, (const uint32_t*)nullptr, L, n, d_words, wpr,
-                       (unsigned long long*)d_first_bad);
-    rc = ss_check(hipGetLastError(), "k_encode_gen");
-    if (rc || !ham) return rc;
-    return ss_hamming_ref(d_words, n, L, wpr, d_ref_words, d_out, stream);
+    const uint32_t logG = log2_ceil(wpr);
+    const unsigned grid = grid_for(n << logG, kThreads, kGenGridCap);
+    if (ham)
+        hipLaunchKernelGGL((k_encode_gen<false, true>), dim3(grid), dim3(kThreads), 0, s, d_ascii, stride,
+                           (const uint64_t*)nullptr, (const uint32_t*)nullptr, L, n, d_words, wpr, logG,
+                           d_ref_words, ham_words(L), d_out, (unsigned long long*)d_first_bad);
+    else
+        hipLaunchKernelGGL((k_encode_gen<false, false>), dim3(grid), dim3(kThreads), 0, s, d_ascii, stride,
+                           (const uint64_t*)nullptr, (const uint32_t*)nullptr, L, n, d_words, wpr, logG,
+                           (const uint64_t*)nullptr, 0u, (uint32_t*)nullptr, (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_encode_gen");
 }
 
 int ss_encode_fixed(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
@@ -361,9 +497,11 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     hipStream_t s = (hipStream_t)stream;
     int rc = reset_first_bad(d_first_bad, s);
     if (rc || n == 0) return rc;
-    const unsigned grid = grid_for(n * wpr, kThreads, kGenGridCap);
-    hipLaunchKernelGGL((k_encode_gen<true>), dim3(grid), dim3(kThreads), 0, s, d_ascii, (uint64_t)0,
-                       d_offsets, d_lens, 0u, n, d_words, wpr, (unsigned long long*)d_first_bad);
+    const uint32_t logG = log2_ceil(wpr);
+    const unsigned grid = grid_for(n << logG, kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_encode_gen<true, false>), dim3(grid), dim3(kThreads), 0, s, d_ascii, (uint64_t)0,
+                       d_offsets, d_lens, 0u, n, d_words, wpr, logG, (const uint64_t*)nullptr, 0u,
+                       (uint32_t*)nullptr, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_gen<var>");
 }
 
@@ -379,10 +517,8 @@ int ss_decode_fixed(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wp
                       ((((uintptr_t)d_words) & 7) == 0);
     if (fast) {
         const uint32_t cpr = L / 16, wpr2 = 2 * wpr, logG = log2_ceil(cpr);
-        constexpr int U = 4;
-        const unsigned grid = grid_for(n << logG, (uint64_t)U * kThreads);
-        hipLaunchKernelGGL((k_decode_g16<U>), dim3(grid), dim3(kThreads), 0, s, (const uint32_t*)d_words,
-                           wpr2, n, cpr, logG, (uint4*)d_ascii, stride / 16);
+        launch_decode_g16<kDecT, kDecU, kDecNtLd, kDecNtSt>((const uint32_t*)d_words, wpr2, n, cpr, logG,
+                                                            (uint4*)d_ascii, stride / 16, s);
         return ss_check(hipGetLastError(), "k_decode_g16");
     }
     const unsigned grid = grid_for(n * wpr, kThreads, kGenGridCap);

@@ -1,40 +1,49 @@
 // ss_counter.hip — ShortSeqCounter on the GPU: fused encode -> open-addressing hash table in HBM
 // with atomic counts and first-occurrence indices (counter.pyx:41-54 semantics).
 //
-// Table (structure of arrays, capacity C = 2^k, plus one sentinel slot at index C):
-//   keys[C]    u64 packed word; EMPTY = ~0.  Claimed once by atomicCAS EMPTY -> key, never changed.
-//   counts[C+1] u64 atomicAdd.   first[C+1] u64 atomicMin (UINT64_MAX = unset).
+// Table: C = 2^k slots of 32 B (array of structs, one slot per 32-B sector) plus one sentinel slot:
+//   key    u64 packed word; EMPTY = ~0.  Claimed once by atomicCAS EMPTY -> key, never changed.
+//   ncount u64 = ~count (so a single 0xFF memset resets key, count and first together);
+//          incremented with atomicAdd(-1).
+//   first  u64 atomicMin of the global read index (~0 = unset).
+// One slot = one sector: the probe load, the count atomic and the first-index check touch the same
+// 32 B, instead of three random lines for three separate arrays.
 // The packed word ~0 ("G" * 32) collides with EMPTY and lives in the sentinel slot C.
 // Every key of one handle has the same length L <= 32 (the host groups a mixed batch by length, so
 // the dict key (length, packed) of short_seq_64.pyx:41-44 is (handle, word) here).
 //
 // Probing: Fibonacci hash of the key -> top k bits, linear probing.  A plain (possibly L1-stale)
-// load of keys[h] can only be stale as EMPTY (keys never change once claimed); the CAS then returns
+// load of a key can only be stale as EMPTY (keys never change once claimed); the CAS then returns
 // the true value, so no acquire fence is needed (MI355X_MICROARCH.md §visibility).
 #include "ss_device.h"
 #include "ss_internal.h"
 
 using namespace ssd;
 
+namespace {
+struct alignas(32) Slot {
+    unsigned long long key;
+    unsigned long long ncount;
+    unsigned long long first;
+    unsigned long long pad;
+};
+constexpr int kThreads = 256;
+constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
+constexpr uint32_t kExtractBlocks = 1024;  // extract passes: fixed grid, contiguous slot ranges
+}  // namespace
+
 struct ss_counter {
     uint64_t cap = 0;
     uint32_t log2cap = 0;
-    int32_t L = -1;                      // length of every key in this handle (-1: not fixed yet)
-    uint64_t* keys = nullptr;            // [cap]
-    unsigned long long* counts = nullptr;  // [cap + 1]
-    unsigned long long* first = nullptr;   // [cap + 1]
-    unsigned long long* work = nullptr;    // [0]: overflow flag, [1..]: part offsets/cursors (2*kMaxParts)
+    int32_t L = -1;                        // length of every key in this handle (-1: not fixed yet)
+    Slot* slots = nullptr;                 // [cap + 1]
+    unsigned long long* work = nullptr;    // [0]: overflow flags, [1..]: per-(part, block) counts
 };
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr uint32_t kMaxParts = 1024;
-
 struct Tbl {
-    uint64_t* keys;
-    unsigned long long* counts;
-    unsigned long long* first;
+    Slot* slots;
     unsigned long long* overflow;
     uint64_t mask;
     uint32_t shift;
@@ -45,6 +54,7 @@ __device__ __forceinline__ uint64_t slot_hash(uint64_t key, uint32_t shift) {
 }
 
 // Owner partition for the multi-GPU merge (independent of the table's hash bits).
+// Mirrored on the host by shortseq_amd/dist.py owner_of_np.
 __host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t nparts) {
     return (uint32_t)((splitmix64(key) >> 32) % nparts);
 }
@@ -58,11 +68,11 @@ __device__ __forceinline__ void tbl_add(const Tbl& t, uint64_t key, unsigned lon
         uint64_t h = t.shift >= 64 ? 0 : slot_hash(key, t.shift);
         uint64_t probes = 0;
         for (;;) {
-            const uint64_t cur = t.keys[h];
+            const unsigned long long cur = t.slots[h].key;
             if (cur == key) break;
             if (cur == kEmpty) {
-                const unsigned long long prev =
-                    atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)kEmpty, (unsigned long long)key);
+                const unsigned long long prev = atomicCAS(&t.slots[h].key, (unsigned long long)kEmpty,
+                                                          (unsigned long long)key);
                 if (prev == kEmpty || prev == key) break;
             }
             h = (h + 1) & t.mask;
@@ -73,8 +83,9 @@ __device__ __forceinline__ void tbl_add(const Tbl& t, uint64_t key, unsigned lon
         }
         s = h;
     }
-    atomicAdd(&t.counts[s], cnt);
-    if (t.first[s] > idx) atomicMin(&t.first[s], idx);
+    Slot* sl = &t.slots[s];
+    atomicAdd(&sl->ncount, 0ull - cnt);
+    if (sl->first > idx) atomicMin(&sl->first, idx);
 }
 
 // Fast path, L in {16, 32}, 16-B aligned rows: two lanes per read (lane pair = one packed word,
@@ -161,12 +172,13 @@ __global__ __launch_bounds__(kThreads) void k_merge(Tbl t, const uint64_t* keys,
 }
 
 __device__ __forceinline__ bool slot_used(const Tbl& t, uint64_t s, uint64_t& key) {
+    const Slot& sl = t.slots[s];
     if (s <= t.mask) {
-        key = t.keys[s];
+        key = sl.key;
         return key != kEmpty;
     }
     key = kEmpty;
-    return t.counts[s] != 0;   // sentinel slot
+    return sl.ncount != ~0ull;   // sentinel slot: used iff its count is nonzero
 }
 
 __global__ __launch_bounds__(kThreads) void k_size(Tbl t, unsigned long long* out) {
@@ -183,77 +195,111 @@ __global__ __launch_bounds__(kThreads) void k_size(Tbl t, unsigned long long* ou
     if (threadIdx.x == 0 && cnt) atomicAdd(out, (unsigned long long)cnt);
 }
 
-// Extract pass 1: per-part histogram (LDS), one global add per part per block.
-__global__ __launch_bounds__(kThreads) void k_part_hist(Tbl t, uint32_t nparts, unsigned long long* part_counts) {
-    __shared__ unsigned int hist[kMaxParts];
+// Wave-aggregated "reserve `mine` positions of part p0" helper: for every distinct part present in
+// the wave (peeled with readfirstlane + ballot), ONE lane adds the wave's count to an LDS counter.
+// Returns this lane's position (base + rank) for its part, or 0 for lanes with !used.
+__device__ __forceinline__ unsigned long long wave_reserve(bool used, uint32_t part, unsigned long long* lds_ctr) {
+    uint64_t pending = __ballot(used);
+    unsigned long long pos = 0;
+    const int lane = (int)(threadIdx.x & 63);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t p0 = (uint32_t)__shfl((int)part, leader);
+        const uint64_t mine = __ballot(used && part == p0);
+        const uint32_t rank = __popcll(mine & ((1ull << lane) - 1ull));
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(&lds_ctr[p0], (unsigned long long)__popcll(mine));
+        base = __shfl(base, leader);
+        if (used && part == p0) pos = base + rank;
+        pending &= ~mine;
+    }
+    return pos;
+}
+
+// Extract pass 1: block b counts the used slots of its contiguous range per part -> bc[p*B + b].
+__global__ __launch_bounds__(kThreads) void k_part_count(Tbl t, uint32_t nparts, unsigned long long* bc) {
+    __shared__ unsigned long long hist[kMaxParts];
     for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) hist[p] = 0;
     __syncthreads();
-    for (uint64_t s = (uint64_t)blockIdx.x * kThreads + threadIdx.x; s <= t.mask + 1; s += (uint64_t)gridDim.x * kThreads) {
-        uint64_t key;
-        if (slot_used(t, s, key)) atomicAdd(&hist[owner_of(key, nparts)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads)
-        if (hist[p]) atomicAdd(&part_counts[p], (unsigned long long)hist[p]);
-}
-
-// Extract pass 2: exclusive scan of the part counts into cursors (one block).
-__global__ void k_part_scan(uint32_t nparts, const unsigned long long* part_counts, unsigned long long* cursors) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        unsigned long long acc = 0;
-        for (uint32_t p = 0; p < nparts; ++p) {
-            cursors[p] = acc;
-            acc += part_counts[p];
-        }
-    }
-}
-
-// Extract pass 3: scatter occupied slots into their part's range.  Positions are reserved per wave:
-// the wave peels off one distinct part at a time (readfirstlane + ballot), one lane does a single
-// atomicAdd for all the wave's entries of that part, lanes take base + rank (mbcnt).  With one part
-// (1 GPU) that is one global atomic per wave instead of one per entry.
-__global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t nparts, int32_t L,
-                                                           unsigned long long* cursors, uint64_t* okeys,
-                                                           uint32_t* olens, uint64_t* ocounts, uint64_t* ofirst,
-                                                           uint64_t cap_out, unsigned long long* overflow) {
     const uint64_t nslots = t.mask + 2;
-    const uint64_t stride = (uint64_t)gridDim.x * kThreads;
-    // uniform trip count so every lane of a wave takes part in the ballots
-    for (uint64_t s0 = (uint64_t)blockIdx.x * kThreads; s0 < nslots; s0 += stride) {
+    const uint64_t per = (nslots + kExtractBlocks - 1) / kExtractBlocks;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(nslots, lo + per);
+    for (uint64_t s0 = lo; s0 < hi; s0 += kThreads) {
         const uint64_t s = s0 + threadIdx.x;
         uint64_t key = kEmpty;
-        const bool used = s < nslots && slot_used(t, s, key);
-        const uint32_t part = used ? owner_of(key, nparts) : 0u;
-        uint64_t pending = __ballot(used);
-        unsigned long long pos = 0;
-        while (pending) {
-            const int leader = __ffsll((long long)pending) - 1;
-            const uint32_t p0 = (uint32_t)__shfl((int)part, leader);
-            const uint64_t mine = __ballot(used && part == p0);
-            const uint32_t rank = __popcll(mine & ((1ull << (threadIdx.x & 63)) - 1ull));
-            unsigned long long base = 0;
-            if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&cursors[p0], (unsigned long long)__popcll(mine));
-            base = __shfl(base, leader);
-            if (used && part == p0) pos = base + rank;
-            pending &= ~mine;
-        }
+        const bool used = s < hi && slot_used(t, s, key);
+        wave_reserve(used, used ? owner_of(key, nparts) : 0u, hist);
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) bc[(uint64_t)p * kExtractBlocks + blockIdx.x] = hist[p];
+}
+
+// Extract pass 2 (one block of 1024): exclusive scan of bc in (part, block) order = each block's
+// start offset in its part's region; part totals -> part_counts.
+__global__ __launch_bounds__(1024) void k_part_offsets(uint32_t nparts, unsigned long long* bc,
+                                                        unsigned long long* part_counts) {
+    __shared__ unsigned long long sums[1024];
+    const uint32_t total = nparts * kExtractBlocks;
+    const uint32_t seg = (total + 1023) / 1024;
+    const uint32_t lo = threadIdx.x * seg, hi = min(total, lo + seg);
+    unsigned long long local = 0;
+    for (uint32_t i = lo; i < hi; ++i) local += bc[i];
+    sums[threadIdx.x] = local;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const unsigned long long v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0ull;
+        __syncthreads();
+        sums[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned long long run = sums[threadIdx.x] - local;   // exclusive prefix of this segment
+    for (uint32_t i = lo; i < hi; ++i) {
+        const unsigned long long c = bc[i];
+        bc[i] = run;
+        run += c;
+    }
+    __syncthreads();
+    // part totals: part p spans bc[p*B .. (p+1)*B); total = next region start - this start
+    for (uint32_t p = threadIdx.x; p < nparts; p += 1024) {
+        const unsigned long long start = bc[(uint64_t)p * kExtractBlocks];
+        const unsigned long long end = (p + 1 < nparts) ? bc[(uint64_t)(p + 1) * kExtractBlocks] : sums[1023];
+        part_counts[p] = end - start;
+    }
+}
+
+// Extract pass 3: same ranges as pass 1; LDS cursors start at the block's offsets, so every slot's
+// position is reserved without any global atomic.
+__global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t nparts, int32_t L,
+                                                           const unsigned long long* bc, uint64_t* okeys,
+                                                           uint32_t* olens, uint64_t* ocounts, uint64_t* ofirst,
+                                                           uint64_t cap_out, unsigned long long* overflow) {
+    __shared__ unsigned long long cursor[kMaxParts];
+    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) cursor[p] = bc[(uint64_t)p * kExtractBlocks + blockIdx.x];
+    __syncthreads();
+    const uint64_t nslots = t.mask + 2;
+    const uint64_t per = (nslots + kExtractBlocks - 1) / kExtractBlocks;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(nslots, lo + per);
+    for (uint64_t s0 = lo; s0 < hi; s0 += kThreads) {
+        const uint64_t s = s0 + threadIdx.x;
+        uint64_t key = kEmpty;
+        const bool used = s < hi && slot_used(t, s, key);
+        const unsigned long long pos = wave_reserve(used, used ? owner_of(key, nparts) : 0u, cursor);
         if (!used) continue;
         if (pos >= cap_out) {
             atomicOr(overflow, 2ull);
             continue;
         }
+        const Slot& sl = t.slots[s];
         okeys[pos] = key;
         olens[pos] = (uint32_t)L;
-        ocounts[pos] = t.counts[s];
-        ofirst[pos] = t.first[s];
+        ocounts[pos] = ~sl.ncount;
+        ofirst[pos] = sl.first;
     }
 }
 
 Tbl tbl_of(const ss_counter* c) {
     Tbl t;
-    t.keys = c->keys;
-    t.counts = c->counts;
-    t.first = c->first;
+    t.slots = c->slots;
     t.overflow = c->work;
     t.mask = c->cap - 1;
     t.shift = 64 - c->log2cap;
@@ -280,10 +326,9 @@ int ss_counter_create(uint64_t capacity, ss_counter** out) {
     ss_counter* c = new ss_counter();
     c->cap = 1ull << lg;
     c->log2cap = lg;
-    hipError_t e = hipMalloc((void**)&c->keys, c->cap * sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->counts, (c->cap + 1) * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->first, (c->cap + 1) * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->work, (1 + 2 * kMaxParts) * sizeof(unsigned long long));
+    hipError_t e = hipMalloc((void**)&c->slots, (c->cap + 1) * sizeof(Slot));
+    if (e == hipSuccess)
+        e = hipMalloc((void**)&c->work, (1 + (size_t)kMaxParts * kExtractBlocks) * sizeof(unsigned long long));
     if (e != hipSuccess) {
         ss_counter_destroy(c);
         ss_check(e, "ss_counter_create hipMalloc");
@@ -301,9 +346,7 @@ int ss_counter_create(uint64_t capacity, ss_counter** out) {
 
 int ss_counter_destroy(ss_counter* c) {
     if (!c) return SS_OK;
-    if (c->keys) (void)hipFree(c->keys);
-    if (c->counts) (void)hipFree(c->counts);
-    if (c->first) (void)hipFree(c->first);
+    if (c->slots) (void)hipFree(c->slots);
     if (c->work) (void)hipFree(c->work);
     delete c;
     return SS_OK;
@@ -313,10 +356,8 @@ int ss_counter_reset(ss_counter* c, void* stream) {
     if (!c) return ss_fail(SS_EARG, "null counter");
     hipStream_t s = (hipStream_t)stream;
     c->L = -1;
-    hipError_t e = hipMemsetAsync(c->keys, 0xFF, c->cap * sizeof(uint64_t), s);
-    if (e == hipSuccess) e = hipMemsetAsync(c->counts, 0, (c->cap + 1) * sizeof(unsigned long long), s);
-    if (e == hipSuccess) e = hipMemsetAsync(c->first, 0xFF, (c->cap + 1) * sizeof(unsigned long long), s);
-    if (e == hipSuccess) e = hipMemsetAsync(c->work, 0, (1 + 2 * kMaxParts) * sizeof(unsigned long long), s);
+    hipError_t e = hipMemsetAsync(c->slots, 0xFF, (c->cap + 1) * sizeof(Slot), s);
+    if (e == hipSuccess) e = hipMemsetAsync(c->work, 0, sizeof(unsigned long long), s);
     return ss_check(e, "ss_counter_reset");
 }
 
@@ -394,18 +435,15 @@ int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32
                        uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
                        void* stream) {
     if (!c) return ss_fail(SS_EARG, "null counter");
-    if (n_parts == 0 || n_parts > kMaxParts) return ss_fail(SS_EARG, "n_parts must be in 1..1024");
+    if (n_parts == 0 || n_parts > kMaxParts) return ss_fail(SS_EARG, "n_parts must be in 1..64");
     if (!d_keys || !d_lens || !d_counts || !d_first || !d_part_counts) return ss_fail(SS_EARG, "null buffer");
     hipStream_t s = (hipStream_t)stream;
     Tbl t = tbl_of(c);
-    unsigned long long* cursors = c->work + 1;
-    int rc = ss_check(hipMemsetAsync(d_part_counts, 0, n_parts * sizeof(uint64_t), s), "part memset");
-    if (rc) return rc;
-    const unsigned grid = grid_for(c->cap + 1, kThreads, 256 * 8);
-    hipLaunchKernelGGL(k_part_hist, dim3(grid), dim3(kThreads), 0, s, t, n_parts, (unsigned long long*)d_part_counts);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(64), 0, s, n_parts, (const unsigned long long*)d_part_counts, cursors);
-    hipLaunchKernelGGL(k_part_scatter, dim3(grid), dim3(kThreads), 0, s, t, n_parts, c->L < 0 ? 0 : c->L, cursors,
-                       d_keys, d_lens, d_counts, d_first, cap, c->work);
+    unsigned long long* bc = c->work + 1;
+    hipLaunchKernelGGL(k_part_count, dim3(kExtractBlocks), dim3(kThreads), 0, s, t, n_parts, bc);
+    hipLaunchKernelGGL(k_part_offsets, dim3(1), dim3(1024), 0, s, n_parts, bc, (unsigned long long*)d_part_counts);
+    hipLaunchKernelGGL(k_part_scatter, dim3(kExtractBlocks), dim3(kThreads), 0, s, t, n_parts, c->L < 0 ? 0 : c->L,
+                       (const unsigned long long*)bc, d_keys, d_lens, d_counts, d_first, cap, c->work);
     return ss_check(hipGetLastError(), "ss_counter_extract");
 }
 

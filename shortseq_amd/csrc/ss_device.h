@@ -82,6 +82,14 @@ __device__ __forceinline__ uint4 decode16(uint32_t v) {
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// Streamed-once output (the packed words / ASCII are not re-read by this kernel): non-temporal
+// stores (global_store ... nt).  Measured +2..4% on the 32-nt encode (tools/tune_encode.hip).
+__device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void st_stream(uint4* p, uint4 v) {
+    const u32x4 q = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(q, (u32x4*)p);
+}
+
 // Hamming contribution of one 32- or 64-bit xor (short_seq_64.pyx:82-84): codes that xor to 3
 // collapse onto the low bit, then popcount.
 __device__ __forceinline__ uint32_t ham32(uint32_t x) { return __popc(((x >> 1) | x) & 0x55555555u); }
@@ -99,6 +107,14 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // Value of the neighbouring lane (lane ^ 1): one DPP quad_perm [1,0,3,2] VALU op, no LDS traffic.
 __device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+
+// First-invalid-read report where the read index is only needed on the (rare) bad path:
+// read = slot / div, computed inside the ballot branch.
+__device__ __forceinline__ void report_bad_div(bool bad, uint64_t slot, uint64_t div, unsigned long long* first_bad) {
+    if (__ballot(bad)) {
+        if (bad) atomicMin(first_bad, (unsigned long long)(slot / div));
+    }
 }
 
 // First-invalid-read report: one atomic per wave that saw a bad lane (rare path).

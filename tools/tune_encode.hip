@@ -25,12 +25,14 @@ __device__ __forceinline__ uint4 ld(const uint4* p) {
 
 enum Mode { ENC = 0, COPY = 1, READ = 2 };
 
-template <int T, int U, bool NT, bool PERSIST, bool ST64, int MODE>
+template <int T, int U, bool NT, bool PERSIST, bool ST64, int MODE, bool XCD = false, bool NTST = false>
 __global__ __launch_bounds__(T) void k_var(const uint4* __restrict__ in, uint32_t* __restrict__ out,
                                           uint64_t nchunks, unsigned long long* fb) {
     const uint64_t step = PERSIST ? (uint64_t)gridDim.x * T * U : 0;
     uint32_t acc = 0;
-    for (uint64_t base = (uint64_t)blockIdx.x * T * U + threadIdx.x; base < nchunks; base += step) {
+    // XCD: blocks are dealt round-robin over 8 XCDs; give each XCD one contiguous 1/8 of the data.
+    const uint64_t bid = XCD ? (uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+    for (uint64_t base = bid * T * U + threadIdx.x; base < nchunks; base += step) {
         uint4 x[U];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -54,7 +56,10 @@ __global__ __launch_bounds__(T) void k_var(const uint4* __restrict__ in, uint32_
                 const uint32_t hi = swap_pair(v);
                 if (!(threadIdx.x & 1u) && g < nchunks) ((uint64_t*)out)[g >> 1] = (uint64_t)v | ((uint64_t)hi << 32);
             } else {
-                if (g < nchunks) out[g] = v;
+                if (g < nchunks) {
+                    if constexpr (NTST) __builtin_nontemporal_store(v, &out[g]);
+                    else out[g] = v;
+                }
             }
         }
         if (!PERSIST) break;
@@ -62,6 +67,55 @@ __global__ __launch_bounds__(T) void k_var(const uint4* __restrict__ in, uint32_
     if constexpr (MODE == READ) {
         if (acc == 0x12345678u) out[blockIdx.x] = acc;   // keep the loads alive
     }
+}
+
+template <int T, int U, bool NT, bool NTST>
+__global__ __launch_bounds__(T) void k_dec(const uint32_t* __restrict__ w, uint4* __restrict__ out, uint64_t nchunks) {
+    const uint64_t base = (uint64_t)blockIdx.x * T * U + threadIdx.x;
+    uint32_t v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * T;
+        v[j] = g < nchunks ? (NT ? __builtin_nontemporal_load(&w[g]) : w[g]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * T;
+        if (g < nchunks) {
+            uint4 o = decode16(v[j]);
+            if constexpr (NTST) {
+                u32x4 q = {o.x, o.y, o.z, o.w};
+                __builtin_nontemporal_store(q, (u32x4*)&out[g]);
+            } else {
+                out[g] = o;
+            }
+        }
+    }
+}
+
+template <int T, int U, bool NT, bool NTST>
+void run_dec(const char* name, uint32_t* w, uint4* out, uint64_t nchunks, int reps) {
+    unsigned grid = (unsigned)((nchunks + (uint64_t)T * U - 1) / ((uint64_t)T * U));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_dec<T, U, NT, NTST>), dim3(grid), dim3(T), 0, 0, w, out, nchunks);
+    CK(hipDeviceSynchronize());
+    double s = 0, mn = 1e9;
+    for (int r = 0; r < reps; ++r) {
+        float ms;
+        CK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL((k_dec<T, U, NT, NTST>), dim3(grid), dim3(T), 0, 0, w, out, nchunks);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        s += ms;
+        mn = std::min<double>(mn, ms);
+    }
+    double bytes = (double)nchunks * 20.0;
+    printf("%-44s grid %7u  avg %.4f ms  min %.4f ms  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", name, grid, s / reps, mn,
+           bytes / (s / reps) / 1e6, bytes / mn / 1e6);
+    fflush(stdout);
 }
 
 __global__ void k_fill(uint8_t* p, uint64_t n) {
@@ -73,22 +127,23 @@ __global__ void k_fill(uint8_t* p, uint64_t n) {
 
 struct Buf { uint4* in; uint32_t* out; unsigned long long* fb; uint64_t nchunks; uint64_t nreads; };
 
-template <int T, int U, bool NT, bool PERSIST, bool ST64, int MODE>
+template <int T, int U, bool NT, bool PERSIST, bool ST64, int MODE, bool XCD = false, bool NTST = false>
 void run(const char* name, Buf& b, int reps, int blocks_per_cu) {
     int cus = 256;
     uint64_t per_block = (uint64_t)T * U;
     uint64_t full = (b.nchunks + per_block - 1) / per_block;
     unsigned grid = PERSIST ? (unsigned)std::min<uint64_t>(full, (uint64_t)cus * blocks_per_cu) : (unsigned)full;
+    if (XCD) grid = (grid + 7) / 8 * 8;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int w = 0; w < 3; ++w)
-        hipLaunchKernelGGL((k_var<T, U, NT, PERSIST, ST64, MODE>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
+        hipLaunchKernelGGL((k_var<T, U, NT, PERSIST, ST64, MODE, XCD, NTST>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
     CK(hipDeviceSynchronize());
     std::vector<float> ms(reps);
     for (int r = 0; r < reps; ++r) {
         CK(hipEventRecord(e0, 0));
-        hipLaunchKernelGGL((k_var<T, U, NT, PERSIST, ST64, MODE>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
+        hipLaunchKernelGGL((k_var<T, U, NT, PERSIST, ST64, MODE, XCD, NTST>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&ms[r], e0, e1));
@@ -116,25 +171,26 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     printf("reads %llu (%.2f GB in, %.2f GB out)\n", (unsigned long long)n, n * 32 / 1e9, n * 8 / 1e9);
     // ceilings
-    run<256, 4, true, false, false, COPY>("copy4to1 T256 U4 nt", b, reps, 0);
-    run<256, 4, false, false, false, COPY>("copy4to1 T256 U4", b, reps, 0);
-    run<256, 8, true, true, false, COPY>("copy4to1 T256 U8 nt persist8", b, reps, 8);
+    run<1024, 2, true, false, false, COPY, false, true>("copy4to1 T1024 U2 nt ntstore", b, reps, 0);
     run<256, 4, true, false, false, READ>("readonly T256 U4 nt", b, reps, 0);
-    run<256, 8, false, true, false, READ>("readonly T256 U8 persist8", b, reps, 8);
-    // encode variants
-    run<256, 4, true, false, false, ENC>("enc T256 U4 nt (production)", b, reps, 0);
-    run<256, 4, false, false, false, ENC>("enc T256 U4", b, reps, 0);
-    run<256, 1, true, false, false, ENC>("enc T256 U1 nt", b, reps, 0);
-    run<256, 2, true, false, false, ENC>("enc T256 U2 nt", b, reps, 0);
-    run<256, 8, true, false, false, ENC>("enc T256 U8 nt", b, reps, 0);
-    run<512, 4, true, false, false, ENC>("enc T512 U4 nt", b, reps, 0);
-    run<1024, 2, true, false, false, ENC>("enc T1024 U2 nt", b, reps, 0);
-    run<256, 4, true, false, true, ENC>("enc T256 U4 nt st64", b, reps, 0);
-    run<256, 4, true, true, false, ENC>("enc T256 U4 nt persist4", b, reps, 4);
-    run<256, 4, true, true, false, ENC>("enc T256 U4 nt persist8", b, reps, 8);
-    run<256, 8, true, true, false, ENC>("enc T256 U8 nt persist8", b, reps, 8);
-    run<256, 8, false, true, false, ENC>("enc T256 U8 persist8", b, reps, 8);
-    run<256, 4, true, true, false, ENC>("enc T256 U4 nt persist16", b, reps, 16);
-    run<512, 8, true, true, false, ENC>("enc T512 U8 nt persist4", b, reps, 4);
+    // encode variants around the round-2 winner
+    run<1024, 2, true, false, false, ENC, false, true>("enc T1024 U2 nt ntstore (production r1b)", b, reps, 0);
+    run<1024, 2, true, false, false, ENC, true, true>("enc T1024 U2 nt ntstore xcd", b, reps, 0);
+    run<512, 2, true, false, false, ENC, false, true>("enc T512 U2 nt ntstore", b, reps, 0);
+    run<512, 4, true, false, false, ENC, false, true>("enc T512 U4 nt ntstore", b, reps, 0);
+    run<768, 2, true, false, false, ENC, false, true>("enc T768 U2 nt ntstore", b, reps, 0);
+    run<1024, 3, true, false, false, ENC, false, true>("enc T1024 U3 nt ntstore", b, reps, 0);
+    run<256, 8, true, false, false, ENC, false, true>("enc T256 U8 nt ntstore", b, reps, 0);
+    run<256, 4, true, false, false, ENC, false, true>("enc T256 U4 nt ntstore", b, reps, 0);
+    run<1024, 2, false, false, false, ENC, false, true>("enc T1024 U2 ntstore", b, reps, 0);
+    run<1024, 2, true, false, false, ENC, false, true>("enc T1024 U2 nt ntstore (repeat)", b, reps, 0);
+    // decode
+    run_dec<1024, 2, true, true>("dec T1024 U2 nt ntstore (production r1b)", b.out, b.in, b.nchunks, reps);
+    run_dec<1024, 2, false, true>("dec T1024 U2 ntstore", b.out, b.in, b.nchunks, reps);
+    run_dec<512, 2, true, true>("dec T512 U2 nt ntstore", b.out, b.in, b.nchunks, reps);
+    run_dec<512, 4, true, true>("dec T512 U4 nt ntstore", b.out, b.in, b.nchunks, reps);
+    run_dec<256, 2, false, false>("dec T256 U2", b.out, b.in, b.nchunks, reps);
+    run_dec<1024, 1, true, true>("dec T1024 U1 nt ntstore", b.out, b.in, b.nchunks, reps);
+    run_dec<1024, 2, true, true>("dec T1024 U2 nt ntstore (repeat)", b.out, b.in, b.nchunks, reps);
     return 0;
 }
