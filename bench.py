@@ -98,7 +98,8 @@ def timed_loop(step, steps, warmup, world):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el, timer
@@ -229,7 +230,8 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
     el, tr = timed_loop(step, steps, warmup, world)
     owned = sc.owned()
     k, c, f = owned.items_sorted()
-    tot = torch.tensor([int(c.sum()), len(k)], dtype=torch.int64, device=dev)
+    tot = torch.tensor([int(c.sum()), len(k)], dtype=torch.int64,
+                       device=dev if world == 1 or dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(tot)
     if int(tot[0]) != n * world:
@@ -284,12 +286,18 @@ def cpu_baseline(L=32, target_s=10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    # the MI355X clock needs tens of ms of sustained load to settle (tools/diag_bench.py: the first
+    # ~20 back-to-back launches run ~3% slower); 50 warmup launches of the 0.6-ms kernel ~= 30 ms
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--n", type=int, default=100_000_000, help="reads per GPU (C2)")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--dist-backend", default=os.environ.get("SHORTSEQ_DIST_BACKEND", "nccl"),
+                    help="nccl (= RCCL over xGMI, default) or gloo (rehearsal: several ranks on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="map every rank to cuda:0 (multi-rank rehearsal on a 1-GPU box)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -297,10 +305,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_idx = 0 if args.same_device else local_rank
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import shortseq_amd.batch as B
     from shortseq_amd._native import lib as _lib

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-r1}
 S=scripts/gpu_step.sh
 $S 600 pytest_gpu python -m pytest tests -m gpu -q || exit 1
-if [ -x tools/tune_encode ]; then $S 300 tune_encode tools/tune_encode 100000000 20 || exit 1; fi
+if [ -x tools/tune_kernels ] && [ "${TUNE:-0}" = 1 ]; then $S 400 tune_kernels tools/tune_kernels 20 || exit 1; fi
 $S 400 bench python bench.py --steps 20 --warmup 5 || exit 1
 P=gpurun_out/prof_$TAG
 mkdir -p $P

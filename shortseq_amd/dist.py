@@ -42,6 +42,10 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, part
     Works on any backend whose all_to_all_single supports uneven splits (nccl/RCCL, gloo)."""
     world = dist.get_world_size(group)
     dev = keys.device
+    if dev.type != "cpu" and dist.get_backend(group) == "gloo":
+        # rehearsal / CPU-collective path: gloo moves host tensors only
+        k, c, f = exchange(keys.cpu(), counts.cpu(), first.cpu(), part_counts.cpu(), group)
+        return k.to(dev), c.to(dev), f.to(dev)
     sc = part_counts.to(torch.int64)
     rc = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_to_all_single(rc, sc, group=group)
