@@ -114,15 +114,20 @@ def check_known_answer(words: torch.Tensor, seed: int, i0: int, L: int, n: int):
             raise SystemExit(f"PARITY FAILURE: read {i0 + i} L={L}: {got[k]} != {exp}")
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch from the committed PMC summary (profiles/), if one exists."""
+def load_traffic(workload: str, reads: int):
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json, written by
+    tools/save_profiles.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench),
+    scaled to this launch's read count (the profiled launch's bytes per read x reads)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d.get(workload, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(workload, {})
+        per_read = e.get("hbm_bytes_per_read")
+        if per_read is None and "hbm_bytes_per_launch" in e and e.get("reads"):
+            per_read = e["hbm_bytes_per_launch"] / e["reads"]
+        return None if per_read is None else per_read * reads
     except Exception:  # noqa: BLE001
         return None
 
@@ -290,7 +295,7 @@ def main():
     # the MI355X clock needs tens of ms of sustained load to settle (tools/diag_bench.py: the first
     # ~20 back-to-back launches run ~3% slower); 50 warmup launches of the 0.6-ms kernel ~= 30 ms
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--n", type=int, default=100_000_000, help="reads per GPU (C2)")
+    ap.add_argument("--reads-per-gpu", type=int, default=100_000_000, help="reads per GPU (C2, C3; C4 uses half)")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -318,7 +323,7 @@ def main():
     from shortseq_amd._native import lib as _lib
     lib = _lib()
 
-    L, n = 32, args.n
+    L, n = 32, args.reads_per_gpu
     log(f"rank {rank}/{world}: C2 encode {n} x {L} nt")
     el, kern_ms = bench_encode(B, lib, dev, rank, world, n, L, args.steps, args.warmup)
     ms_step = el / args.steps * 1e3
@@ -331,19 +336,19 @@ def main():
         "value": value, "unit": "nt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic (device-side splitmix64 reads, SURVEY §8(d))",
-        "config": {"workload": "C2: 100M x 32-nt batch encode (short_seq_64 path), per GPU",
+        "config": {"workload": f"C2: {n / 1e6:g}M x 32-nt batch encode (short_seq_64 path) per GPU",
                    "reads_per_gpu": n, "read_len": L, "global_batch": n * world,
                    "parallelism": f"dp{world} (read shards, no collective)"},
         "roofline": {"bound": "hbm", "kernel": "k_encode_g16<dense>", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_traffic("encode32"), "algo_bytes_per_launch": algo_bytes,
+                     "traffic": load_traffic("encode32", n), "algo_bytes_per_launch": algo_bytes,
                      "kernel_ms": kern_ms},
     }
     log(f"C2: {value / 1e12:.3f} T nt/s, kernel {kern_ms:.3f} ms, {achieved:.0f} GB/s")
 
     if not args.no_extras:
         extra = {}
-        L3, n3 = 96, args.n
+        L3, n3 = 96, args.reads_per_gpu
         log(f"C3 fused encode+hamming {n3} x {L3}")
         el3, k3, d3 = bench_encode_hamming(B, lib, dev, rank, world, n3, L3, args.steps, args.warmup)
         b3 = n3 * (96 + 24 + 4)
@@ -354,7 +359,7 @@ def main():
                          "unit": "GB/s", "frac": b3 / (d3 * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "algo_bytes_per_step": b3,
                          "note": "device time per step over the timed region (incl. the 1-read ref encode)"}}
-        L4, n4 = 512, args.n // 2
+        L4, n4 = 512, args.reads_per_gpu // 2
         log(f"C4 encode+decode {n4} x {L4}")
         s4 = max(5, args.steps // 2)
         el4, ke, kd, d4 = bench_roundtrip(B, lib, dev, rank, world, n4, L4, s4, args.warmup)
@@ -372,7 +377,9 @@ def main():
         extra["C5_counter_32"] = {
             "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
             "reads_per_gpu": n5, "pool": U5, "unique": uniq,
-            "merge": "RCCL all_to_all_single of (key, count, first) by owner" if world > 1 else "none (1 GPU)"}
+            "merge": (f"all_to_all_single of (key, count, first) by owner over {dist.get_backend()}"
+                      f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
+                     if world > 1 else "none (1 GPU)"}
         result["extra"] = extra
 
     if rank == 0:

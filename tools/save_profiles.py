@@ -12,6 +12,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+READS = 100_000_000   # the profiled command is the default bench (C2: 100M x 32 nt per launch)
 REPO = os.path.dirname(HERE)
 
 
@@ -44,6 +45,7 @@ def main():
     for e in summ.get("c2", []):
         if e["kernel"].startswith("void k_encode_g16<false, true, 1") and "hbm_bytes_per_launch" in e:
             traffic["encode32"] = {"kernel": e["kernel"], "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
+                                   "reads": READS, "hbm_bytes_per_read": e["hbm_bytes_per_launch"] / READS,
                                    "fetch_kb_raw": e.get("fetch_kb_raw"), "write_kb_raw": e.get("write_kb_raw"),
                                    "avg_ms_rocprof": e["avg_ms"], "source": os.path.relpath(dst, REPO),
                                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; "
