@@ -478,11 +478,12 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, device):
             for seq, c in dict.items(sub):
                 entries.append((firsts[seq], seq, c))
             continue
+        host = torch.empty(len(idx) * L, dtype=torch.uint8).pin_memory()   # pinned staging
         if len(idx) == n:
-            host = torch.from_numpy(blob_np).pin_memory()
+            host.numpy()[:] = blob_np
         else:
             rows = (offs_np[idx][:, None] + np.arange(L)[None, :]).reshape(-1)
-            host = torch.from_numpy(blob_np[rows]).pin_memory()
+            host.numpy()[:] = blob_np[rows]
         d_ascii = host.to(dev, non_blocking=True).view(-1, L)
         cnt = B.GpuCounter(max(1024, 2 * len(idx)), device=dev)
         try:

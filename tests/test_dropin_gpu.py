@@ -1,0 +1,86 @@
+"""Drop-in API batch paths on the GPU: ShortSeqCounter(list, device="cuda") and
+read_and_count_fastq(device="cuda") must equal the host path and the reference fixtures exactly
+(keys, counts, dict order, exceptions)."""
+import random
+
+import pytest
+
+import shortseq_amd as sq
+from shortseq_amd import ShortSeqCounter
+
+pytestmark = pytest.mark.gpu
+
+
+def _items(c):
+    return [(type(k).__name__, str(k), len(k), v) for k, v in c.items()]
+
+
+def test_golden_counter_gpu(gpu, golden):
+    for case in golden["counter"]:
+        if "reads_str" in case:
+            with pytest.raises(TypeError) as ei:
+                ShortSeqCounter(case["reads_str"], device="cuda")
+            assert str(ei.value) == case["message"]
+            continue
+        reads = [bytes.fromhex(h) for h in case["reads_hex"]]
+        if "raises" in case:
+            with pytest.raises(Exception) as ei:
+                ShortSeqCounter(reads, device="cuda")
+            assert str(ei.value) == case["message"]
+            continue
+        c = ShortSeqCounter(reads, device="cuda")
+        exp = [(it["class"], it["str"], it["length"], it["count"]) for it in case["items"]]
+        assert _items(c) == exp
+
+
+def test_counter_gpu_equals_host_mixed(gpu):
+    rng = random.Random(3)
+    pool = []
+    for L in [0, 1, 2, 5, 16, 17, 31, 32, 33, 40, 64, 96, 97, 150, 1024]:
+        for _ in range(6):
+            pool.append(bytes(rng.choice(b"ACGT") for _ in range(L)))
+    pool.append(b"G" * 32)                 # the packed word that collides with the table's EMPTY
+    pool.append(b"\x01A\x14" * 5)          # aliased bytes (table-path carry)
+    reads = [rng.choice(pool) for _ in range(100_000)]
+    host = ShortSeqCounter(reads, device="host")
+    dev = ShortSeqCounter(reads, device="cuda")
+    assert _items(dev) == _items(host)
+    auto = ShortSeqCounter(reads)          # >= GPU_MIN_READS -> GPU
+    assert _items(auto) == _items(host)
+    assert dev[sq.pack("G" * 32)] == host[sq.pack("G" * 32)]
+
+
+def test_counter_gpu_errors_first_bad(gpu):
+    rng = random.Random(4)
+    reads = [bytes(rng.choice(b"ACGT") for _ in range(rng.choice([8, 32, 50]))) for _ in range(70_000)]
+    reads[50_000] = b"ACGTN" + b"A" * 27          # 32 nt, table path: last bad byte
+    reads[60_000] = b"A" * 40 + b"N"              # 41 nt, host path group
+    reads[65_000] = b"A" * 40 + b"*" * 10
+    with pytest.raises(Exception) as ei_h:
+        ShortSeqCounter(reads, device="host")
+    with pytest.raises(Exception) as ei_d:
+        ShortSeqCounter(reads, device="cuda")
+    assert str(ei_d.value) == str(ei_h.value) == "Unsupported base character: N"
+    reads[50_000] = b"A" * 32
+    with pytest.raises(Exception) as ei_d:
+        ShortSeqCounter(reads, device="cuda")
+    assert str(ei_d.value) == "Unsupported base character: N"
+    reads2 = list(reads)
+    reads2[10] = "ACGT"
+    with pytest.raises(TypeError):
+        ShortSeqCounter(reads2, device="cuda")
+
+
+def test_fastq_gpu(gpu, tmp_path):
+    rng = random.Random(5)
+    pool = [bytes(rng.choice(b"ACGT") for _ in range(rng.choice([20, 32, 33, 75]))) for _ in range(500)]
+    lines = []
+    for i in range(80_000):
+        s = rng.choice(pool).decode()
+        lines.append(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
+    p = tmp_path / "big.fq"
+    p.write_text("".join(lines))
+    h = sq.read_and_count_fastq(str(p), device="host")
+    d = sq.read_and_count_fastq(str(p), device="cuda")
+    assert _items(d) == _items(h)
+    assert sum(d.values()) == 80_000
