@@ -128,7 +128,18 @@ int ss_counter_destroy(ss_counter* c);
 int ss_counter_reset(ss_counter* c, void* stream);
 uint64_t ss_counter_capacity(const ss_counter* c);
 
-/* Encode + count a fixed-length batch (L <= 32).  Read i gets global index base_index + i. */
+/* Reserve workspace (20 B per read + a small per-region table) so inserts of up to max_reads
+ * reads take the partitioned path: reads are bucketed by table region and each region is
+ * aggregated by one workgroup in LDS (no per-read global atomics).  Host call (allocates); inserts
+ * larger than the reservation, or with L not in {16, 32} / unaligned rows, use the direct
+ * atomic-insert kernels.  Requires capacity <= 2^26 (16384 regions).  max_reads < 2^32. */
+int ss_counter_reserve(ss_counter* c, uint64_t max_reads);
+uint64_t ss_counter_reserved(const ss_counter* c);
+int ss_counter_release(ss_counter* c);       /* free the workspace (inserts take the direct path) */
+
+/* Encode + count a fixed-length batch (L <= 32).  Read i gets global index base_index + i.
+ * If the batch holds an invalid read (reported through *d_first_bad) the table's contents are
+ * unspecified afterwards, like the reference counter that raises mid-list (counter.pyx:22-29). */
 int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L,
                             uint64_t stride, uint64_t base_index, uint64_t* d_first_bad, void* stream);
 

@@ -47,6 +47,9 @@ SIGNATURES = [
     ("ss_counter_destroy", C.c_int, [_P]),
     ("ss_counter_reset", C.c_int, [_P, _P]),
     ("ss_counter_capacity", _U64, [_P]),
+    ("ss_counter_reserve", C.c_int, [_P, _U64]),
+    ("ss_counter_reserved", _U64, [_P]),
+    ("ss_counter_release", C.c_int, [_P]),
     ("ss_counter_insert_fixed", C.c_int, [_P, _P, _U64, _U32, _U64, _U64, _P, _P]),
     ("ss_counter_merge", C.c_int, [_P, _P, _P, _P, _P, _U64, _P]),
     ("ss_counter_set_length", C.c_int, [_P, _U32]),

@@ -293,14 +293,33 @@ class GpuCounter:
     def reset(self) -> None:
         check(lib().ss_counter_reset(self._h, _stream(self.device)), "ss_counter_reset")
 
+    PARTITION_MIN_READS = 1 << 16   # batches at least this large reserve the partitioned path
+
+    def reserve(self, max_reads: int) -> bool:
+        """Workspace for the partitioned insert (20 B/read); False if this table cannot use it."""
+        rc = lib().ss_counter_reserve(self._h, max_reads)
+        return rc == 0
+
     def insert(self, ascii: torch.Tensor, L: Optional[int] = None, *, base_index: int = 0,
-               stride: Optional[int] = None, check_errors: bool = True) -> None:
+               stride: Optional[int] = None, check_errors: bool = True, partitioned: Optional[bool] = None) -> None:
+        """partitioned: None = automatic (large batches), True = reserve workspace and use the
+        partitioned insert if the table allows it, False = direct atomic insert."""
         n, L, stride = _as_rows(ascii, L, stride)
+        if partitioned is None:
+            partitioned = n >= self.PARTITION_MIN_READS
+        if partitioned and n > int(lib().ss_counter_reserved(self._h)) and n < (1 << 32):
+            self.reserve(n)
+        if partitioned is False and int(lib().ss_counter_reserved(self._h)) >= n:
+            self._drop_reservation()
         fb = first_bad_buffer(self.device)
         check(lib().ss_counter_insert_fixed(self._h, ascii.data_ptr(), n, L, stride, base_index,
                                             fb.data_ptr(), _stream(self.device)), "ss_counter_insert_fixed")
         if check_errors:
             _check_first_bad(fb, _fetch_row(ascii, stride, L))
+
+    def _drop_reservation(self) -> None:
+        torch.cuda.synchronize(self.device)
+        check(lib().ss_counter_release(self._h), "ss_counter_release")
 
     def merge(self, keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, L: int) -> None:
         m = keys.numel()

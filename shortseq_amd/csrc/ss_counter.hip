@@ -30,14 +30,25 @@ struct alignas(32) Slot {
 constexpr int kThreads = 256;
 constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
 constexpr uint32_t kExtractBlocks = 1024;  // extract passes: fixed grid, contiguous slot ranges
+constexpr uint32_t kSliceLogMax = 12;      // region slice: 4096 slots (one LDS-resident aggregation)
+constexpr uint32_t kPartBlocks = 1024;     // partition passes: fixed grid, contiguous read ranges
+constexpr uint32_t kMaxRegions = 16384;    // per-block region histogram in LDS (64 KB)
 }  // namespace
 
 struct ss_counter {
     uint64_t cap = 0;
     uint32_t log2cap = 0;
+    uint32_t slice_log = 0;                // table = 2^(log2cap - slice_log) regions of 2^slice_log slots
     int32_t L = -1;                        // length of every key in this handle (-1: not fixed yet)
     Slot* slots = nullptr;                 // [cap + 1]
     unsigned long long* work = nullptr;    // [0]: overflow flags, [1..]: per-(part, block) counts
+    // partitioned-insert workspace (ss_counter_reserve)
+    uint64_t ws_reads = 0;
+    uint64_t* ws_keys = nullptr;           // [ws_reads] packed key of read i
+    uint64_t* ws_bkey = nullptr;           // [ws_reads] keys bucketed by table region
+    uint32_t* ws_bidx = nullptr;           // [ws_reads] batch-local read index, same order
+    uint32_t* ws_hist = nullptr;           // [kPartBlocks * regions] per-(block, region) counts -> offsets
+    uint32_t* ws_rstart = nullptr;         // [regions + 1] region start in the bucket arrays
 };
 
 namespace {
@@ -45,8 +56,10 @@ namespace {
 struct Tbl {
     Slot* slots;
     unsigned long long* overflow;
-    uint64_t mask;
-    uint32_t shift;
+    uint64_t mask;        // cap - 1
+    uint64_t slice_mask;  // slots per region - 1
+    uint32_t shift;       // 64 - log2(cap)
+    uint32_t slice_log;
 };
 
 __device__ __forceinline__ uint64_t slot_hash(uint64_t key, uint32_t shift) {
@@ -59,29 +72,44 @@ __host__ __device__ __forceinline__ uint32_t owner_of(uint64_t key, uint32_t npa
     return (uint32_t)((splitmix64(key) >> 32) % nparts);
 }
 
+// Slot addressing: t = top log2(cap) bits of the Fibonacci hash = (region | offset); linear
+// probing stays inside the region's slice, so a region is a self-contained sub-table that one
+// workgroup can own (the partitioned insert below); with one region this is plain linear probing.
+__device__ __forceinline__ uint64_t slot_top(const Tbl& t, uint64_t key) {
+    return t.shift >= 64 ? 0 : slot_hash(key, t.shift);
+}
+
 __device__ __forceinline__ void tbl_add(const Tbl& t, uint64_t key, unsigned long long cnt,
                                         unsigned long long idx) {
     uint64_t s;
     if (key == kEmpty) {
         s = t.mask + 1;  // sentinel slot
     } else {
-        uint64_t h = t.shift >= 64 ? 0 : slot_hash(key, t.shift);
+        const uint64_t top = slot_top(t, key);
+        const uint64_t base = top & ~t.slice_mask;
+        uint64_t off = top & t.slice_mask;
         uint64_t probes = 0;
         for (;;) {
+            const uint64_t h = base + off;
             const unsigned long long cur = t.slots[h].key;
-            if (cur == key) break;
+            if (cur == key) {
+                s = h;
+                break;
+            }
             if (cur == kEmpty) {
                 const unsigned long long prev = atomicCAS(&t.slots[h].key, (unsigned long long)kEmpty,
                                                           (unsigned long long)key);
-                if (prev == kEmpty || prev == key) break;
+                if (prev == kEmpty || prev == key) {
+                    s = h;
+                    break;
+                }
             }
-            h = (h + 1) & t.mask;
-            if (++probes > t.mask) {
+            off = (off + 1) & t.slice_mask;
+            if (++probes > t.slice_mask) {
                 atomicOr(t.overflow, 1ull);
                 return;
             }
         }
-        s = h;
     }
     Slot* sl = &t.slots[s];
     atomicAdd(&sl->ncount, 0ull - cnt);
@@ -297,12 +325,222 @@ __global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t npart
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Partitioned insert (the C5 hot path).  Per-read global atomics on a 1-GB table are memory-side
+// atomic-bound; instead every table region (slice of 2^slice_log slots) is aggregated by ONE
+// workgroup in LDS and merged into its slice with plain loads/stores:
+//   P1 k_pc_keys      encode (2 lanes/read, as k_count_g16) -> keys[i]; per-block region histogram
+//   P2 k_pc_tot / k_pc_scan / k_pc_offsets   region starts + per-(block, region) write offsets
+//   P3 k_pc_scatter   keys + batch-local indices bucketed by region (LDS cursors, no global atomics)
+//   P4 k_pc_aggregate one workgroup per region: LDS hash (CAS / add / min) over the bucket, then
+//                     each distinct key probes the region's slice (an LDS claim bitmap arbitrates
+//                     new slots inside the workgroup; nobody else touches the slice)
+// Blocks of P1 and P3 own the same contiguous read ranges, so offsets are exact.
+// ------------------------------------------------------------------------------------------------
+struct PartWs {
+    uint64_t* keys;
+    uint64_t* bkey;
+    uint32_t* bidx;
+    uint32_t* hist;     // [kPartBlocks][R]
+    uint32_t* rstart;   // [R + 1]
+    uint32_t R;
+};
+
+__device__ __forceinline__ uint32_t region_of(const Tbl& t, uint64_t key) {
+    return (uint32_t)(slot_top(t, key) >> t.slice_log);
+}
+
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_pc_keys(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
+                                               uint64_t n, uint32_t cpr, unsigned long long* first_bad) {
+    extern __shared__ uint32_t hist[];
+    for (uint32_t i = threadIdx.x; i < w.R; i += T) hist[i] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
+    constexpr uint32_t kReadsPerTile = T * U / 2;
+    for (uint64_t t0 = lo; t0 < hi; t0 += kReadsPerTile) {
+        uint4 x[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t gl = j * T + threadIdx.x;
+            const uint64_t r = t0 + (gl >> 1);
+            const uint32_t k = gl & 1u;
+            x[j] = (r < hi && k < cpr) ? ld_stream(&in[r * stride16 + k])
+                                       : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t gl = j * T + threadIdx.x;
+            const uint64_t r = t0 + (gl >> 1);
+            const uint32_t k = gl & 1u;
+            const Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, true);   // L <= 32: table path
+            const uint32_t v = e.v | (k ? swap_pair(e.cout) : 0u);
+            const uint32_t hiw = swap_pair(v);
+            const uint32_t bad_pair = e.bad | swap_pair(e.bad);
+            const bool live = r < hi && k == 0;
+            report_bad(live && bad_pair != 0u, r, first_bad);
+            if (live) {
+                const uint64_t key = (uint64_t)v | ((uint64_t)hiw << 32);
+                w.keys[r] = key;
+                atomicAdd(&hist[region_of(t, key)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < w.R; i += T) w.hist[(uint64_t)blockIdx.x * w.R + i] = hist[i];
+}
+
+// region totals (thread per region; coalesced over regions)
+__global__ __launch_bounds__(256) void k_pc_tot(PartWs w) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= w.R) return;
+    uint32_t sum = 0;
+    for (uint32_t b = 0; b < kPartBlocks; ++b) sum += w.hist[(uint64_t)b * w.R + r];
+    w.rstart[r] = sum;
+}
+
+// exclusive scan of region totals (one block of 1024)
+__global__ __launch_bounds__(1024) void k_pc_scan(PartWs w) {
+    __shared__ uint32_t sums[1024];
+    const uint32_t seg = (w.R + 1023) / 1024;
+    const uint32_t lo = threadIdx.x * seg, hi = min(w.R, lo + seg);
+    uint32_t local = 0;
+    for (uint32_t i = lo; i < hi; ++i) local += w.rstart[i];
+    sums[threadIdx.x] = local;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0u;
+        __syncthreads();
+        sums[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = sums[threadIdx.x] - local;
+    for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t c = w.rstart[i];
+        w.rstart[i] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) w.rstart[w.R] = sums[1023];
+}
+
+// per-(block, region) write offsets = region start + counts of earlier blocks (thread per region)
+__global__ __launch_bounds__(256) void k_pc_offsets(PartWs w) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= w.R) return;
+    uint32_t run = w.rstart[r];
+    for (uint32_t b = 0; b < kPartBlocks; ++b) {
+        const uint64_t i = (uint64_t)b * w.R + r;
+        const uint32_t c = w.hist[i];
+        w.hist[i] = run;
+        run += c;
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(T) void k_pc_scatter(Tbl t, PartWs w, uint64_t n) {
+    extern __shared__ uint32_t cursor[];
+    for (uint32_t i = threadIdx.x; i < w.R; i += T) cursor[i] = w.hist[(uint64_t)blockIdx.x * w.R + i];
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
+    for (uint64_t r = lo + threadIdx.x; r < hi; r += T) {
+        const uint64_t key = w.keys[r];
+        const uint32_t pos = atomicAdd(&cursor[region_of(t, key)], 1u);
+        w.bkey[pos] = key;
+        w.bidx[pos] = (uint32_t)r;
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t base_index) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t S = (uint32_t)t.slice_mask + 1;          // slice slots
+    const uint32_t LS = 2 * S;                               // LDS table slots (load <= 50%)
+    unsigned long long* lkey = (unsigned long long*)smem;                 // [LS]
+    uint32_t* lcnt = (uint32_t*)(smem + (size_t)LS * 8);                  // [LS]
+    uint32_t* lfst = lcnt + LS;                                           // [LS]
+    uint32_t* claim = lfst + LS;                                          // [S / 32]
+    uint32_t* sent = claim + S / 32;                                      // [2]: sentinel count, first
+    for (uint32_t i = threadIdx.x; i < LS; i += T) {
+        lkey[i] = kEmpty;
+        lcnt[i] = 0;
+        lfst[i] = 0xFFFFFFFFu;
+    }
+    for (uint32_t i = threadIdx.x; i < S / 32; i += T) claim[i] = 0;
+    if (threadIdx.x == 0) {
+        sent[0] = 0;
+        sent[1] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint32_t region = blockIdx.x;
+    const uint32_t b0 = w.rstart[region], b1 = w.rstart[region + 1];
+    const uint32_t lds_shift = (t.shift >= 64 ? 64 : t.shift) - 1;   // one more hash bit than the slice
+    for (uint32_t e = b0 + threadIdx.x; e < b1; e += T) {
+        const uint64_t key = w.bkey[e];
+        const uint32_t idx = w.bidx[e];
+        if (key == kEmpty) {
+            atomicAdd(&sent[0], 1u);
+            atomicMin(&sent[1], idx);
+            continue;
+        }
+        uint32_t ls = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> lds_shift) & (LS - 1);
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&lkey[ls], (unsigned long long)kEmpty, (unsigned long long)key);
+            if (prev == kEmpty || prev == key) break;
+            ls = (ls + 1) & (LS - 1);
+        }
+        atomicAdd(&lcnt[ls], 1u);
+        atomicMin(&lfst[ls], idx);
+    }
+    __syncthreads();
+    // merge the region's distinct keys into its slice; only this workgroup touches the slice
+    const uint64_t slice_base = (uint64_t)region << t.slice_log;
+    for (uint32_t ls = threadIdx.x; ls < LS; ls += T) {
+        const unsigned long long key = lkey[ls];
+        if (key == kEmpty) continue;
+        const unsigned long long c = lcnt[ls];
+        const unsigned long long f = base_index + lfst[ls];
+        uint32_t off = (uint32_t)(slot_top(t, key) & t.slice_mask);
+        bool done = false;
+        for (uint32_t probe = 0; probe < S; ++probe) {
+            Slot* sl = &t.slots[slice_base + off];
+            const unsigned long long gk = sl->key;
+            if (gk == key) {
+                sl->ncount -= c;
+                if (f < sl->first) sl->first = f;
+                done = true;
+                break;
+            }
+            if (gk == kEmpty) {
+                const uint32_t bit = 1u << (off & 31);
+                if (!(atomicOr(&claim[off >> 5], bit) & bit)) {
+                    sl->key = key;
+                    sl->ncount = ~c;
+                    sl->first = f;
+                    done = true;
+                    break;
+                }
+            }
+            off = (off + 1) & (uint32_t)t.slice_mask;
+        }
+        if (!done) atomicOr(t.overflow, 1ull);
+    }
+    if (threadIdx.x == 0 && sent[0]) {
+        Slot* sl = &t.slots[t.mask + 1];
+        atomicAdd(&sl->ncount, 0ull - (unsigned long long)sent[0]);
+        atomicMin(&sl->first, base_index + sent[1]);
+    }
+}
+
 Tbl tbl_of(const ss_counter* c) {
     Tbl t;
     t.slots = c->slots;
     t.overflow = c->work;
     t.mask = c->cap - 1;
+    t.slice_mask = (1ull << c->slice_log) - 1;
     t.shift = 64 - c->log2cap;
+    t.slice_log = c->slice_log;
     return t;
 }
 
@@ -326,6 +564,7 @@ int ss_counter_create(uint64_t capacity, ss_counter** out) {
     ss_counter* c = new ss_counter();
     c->cap = 1ull << lg;
     c->log2cap = lg;
+    c->slice_log = lg < kSliceLogMax ? lg : kSliceLogMax;
     hipError_t e = hipMalloc((void**)&c->slots, (c->cap + 1) * sizeof(Slot));
     if (e == hipSuccess)
         e = hipMalloc((void**)&c->work, (1 + (size_t)kMaxParts * kExtractBlocks) * sizeof(unsigned long long));
@@ -348,6 +587,11 @@ int ss_counter_destroy(ss_counter* c) {
     if (!c) return SS_OK;
     if (c->slots) (void)hipFree(c->slots);
     if (c->work) (void)hipFree(c->work);
+    if (c->ws_keys) (void)hipFree(c->ws_keys);
+    if (c->ws_bkey) (void)hipFree(c->ws_bkey);
+    if (c->ws_bidx) (void)hipFree(c->ws_bidx);
+    if (c->ws_hist) (void)hipFree(c->ws_hist);
+    if (c->ws_rstart) (void)hipFree(c->ws_rstart);
     delete c;
     return SS_OK;
 }
@@ -370,6 +614,46 @@ static int fix_length(ss_counter* c, uint32_t L) {
     return SS_OK;
 }
 
+int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    const uint64_t R = c->cap >> c->slice_log;
+    if (R > kMaxRegions) return ss_fail(SS_EARG, "capacity too large for the partitioned insert");
+    if (max_reads >= (1ull << 32)) return ss_fail(SS_EARG, "max_reads must be < 2^32 per insert");
+    if (max_reads <= c->ws_reads) return SS_OK;
+    if (c->ws_keys) (void)hipFree(c->ws_keys);
+    if (c->ws_bkey) (void)hipFree(c->ws_bkey);
+    if (c->ws_bidx) (void)hipFree(c->ws_bidx);
+    c->ws_keys = nullptr;
+    c->ws_bkey = nullptr;
+    c->ws_bidx = nullptr;
+    c->ws_reads = 0;
+    hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bkey, max_reads * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
+    if (e == hipSuccess && !c->ws_hist) e = hipMalloc((void**)&c->ws_hist, (size_t)kPartBlocks * R * sizeof(uint32_t));
+    if (e == hipSuccess && !c->ws_rstart) e = hipMalloc((void**)&c->ws_rstart, (R + 1) * sizeof(uint32_t));
+    if (e != hipSuccess) {
+        ss_check(e, "ss_counter_reserve hipMalloc");
+        return SS_ENOMEM;
+    }
+    c->ws_reads = max_reads;
+    return SS_OK;
+}
+
+uint64_t ss_counter_reserved(const ss_counter* c) { return c ? c->ws_reads : 0; }
+
+int ss_counter_release(ss_counter* c) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->ws_keys) (void)hipFree(c->ws_keys);
+    if (c->ws_bkey) (void)hipFree(c->ws_bkey);
+    if (c->ws_bidx) (void)hipFree(c->ws_bidx);
+    c->ws_keys = nullptr;
+    c->ws_bkey = nullptr;
+    c->ws_bidx = nullptr;
+    c->ws_reads = 0;
+    return SS_OK;
+}
+
 int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L,
                             uint64_t stride, uint64_t base_index, uint64_t* d_first_bad, void* stream) {
     if (!c) return ss_fail(SS_EARG, "null counter");
@@ -383,6 +667,42 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
     if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
     Tbl t = tbl_of(c);
     const bool fast = (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
+    if (fast && n <= c->ws_reads) {
+        PartWs w;
+        w.keys = c->ws_keys;
+        w.bkey = c->ws_bkey;
+        w.bidx = c->ws_bidx;
+        w.hist = c->ws_hist;
+        w.rstart = c->ws_rstart;
+        w.R = (uint32_t)(c->cap >> c->slice_log);
+        const size_t hist_lds = (size_t)w.R * sizeof(uint32_t);
+        const uint32_t S = 1u << c->slice_log;
+        const size_t agg_lds = (size_t)2 * S * 16 + (S / 32) * 4 + 8;
+        constexpr int T1 = 512, U1 = 4;
+        // dynamic LDS above the 64 KB default: opt in once per kernel (host-side attribute)
+        static bool attrs_set = false;
+        if (!attrs_set) {
+            hipError_t ea = hipFuncSetAttribute((const void*)k_pc_keys<T1, U1>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, kMaxRegions * 4);
+            if (ea == hipSuccess)
+                ea = hipFuncSetAttribute((const void*)k_pc_scatter<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         kMaxRegions * 4);
+            if (ea == hipSuccess)
+                ea = hipFuncSetAttribute((const void*)k_pc_aggregate<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(2 * (1u << kSliceLogMax) * 16 + (1u << kSliceLogMax) / 8 + 8));
+            if (ea != hipSuccess) return ss_check(ea, "hipFuncSetAttribute (dynamic LDS)");
+            attrs_set = true;
+        }
+        hipLaunchKernelGGL((k_pc_keys<T1, U1>), dim3(kPartBlocks), dim3(T1), hist_lds, s, t, w, (const uint4*)d_ascii,
+                           stride / 16, n, L / 16, (unsigned long long*)d_first_bad);
+        const unsigned rg = (w.R + 255) / 256;
+        hipLaunchKernelGGL(k_pc_tot, dim3(rg), dim3(256), 0, s, w);
+        hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w);
+        hipLaunchKernelGGL(k_pc_offsets, dim3(rg), dim3(256), 0, s, w);
+        hipLaunchKernelGGL((k_pc_scatter<512>), dim3(kPartBlocks), dim3(512), hist_lds, s, t, w, n);
+        hipLaunchKernelGGL((k_pc_aggregate<1024>), dim3(w.R), dim3(1024), agg_lds, s, t, w, base_index);
+        return ss_check(hipGetLastError(), "partitioned insert");
+    }
     if (fast) {
         constexpr int U = 4;
         const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 0);

@@ -290,3 +290,38 @@ def test_counter_extract_parts_and_merge(gpu, oracle):
     o = np.argsort(f, kind="stable")
     assert np.array_equal(k[o], k0) and np.array_equal(c[o], c0) and np.array_equal(f[o], f0)
     assert c0.sum() == n
+
+
+@pytest.mark.parametrize("cap,U,n", [(1 << 12, 300, 200_000), (1 << 16, 20_000, 500_000),
+                                     (1 << 22, 1_000_000, 3_000_000)])
+def test_counter_partitioned_equals_direct(gpu, oracle, cap, U, n):
+    """The partitioned (LDS-aggregated) insert and the direct atomic insert give identical tables,
+    across several inserts (persistent table, global first indices), incl. the EMPTY-colliding key."""
+    import shortseq_amd.batch as B
+    L = 32
+    ascii = B.synth_pool_reads(n, L, 21, 22, U, device=gpu)
+    ascii[7] = ord("G")                     # read 7 = "G" * 32 -> packed word ~0 (sentinel slot)
+    ascii[n // 2 + 3] = ord("G")
+    res = []
+    for partitioned in (True, False):
+        c = B.GpuCounter(cap, device=gpu)
+        third = n // 3
+        for lo, hi in ((0, third), (third, 2 * third), (2 * third, n)):
+            c.insert(ascii[lo:hi], L, base_index=lo, partitioned=partitioned)
+        assert not c.overflowed()
+        res.append(c.items_sorted())
+        c.close()
+    (k1, c1, f1), (k2, c2, f2) = res
+    assert np.array_equal(k1, k2) and np.array_equal(c1, c2) and np.array_equal(f1, f2)
+    assert int(c1.sum()) == n
+    assert k1[np.argmax(f1 == 7)] == np.uint64(0xFFFFFFFFFFFFFFFF)
+    # and against the oracle on the first 200k reads
+    m = min(n, 200_000)
+    c = B.GpuCounter(cap, device=gpu)
+    c.insert(ascii[:m], L, partitioned=True)
+    k, cnt, f = c.items_sorted()
+    a = ascii[:m].cpu().numpy().reshape(-1)
+    exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(m)])
+    assert [int(x) for x in k] == [w[0] for (w, _L, _c, _f) in exp]
+    assert list(cnt) == [cc for (_w, _L, cc, _f) in exp]
+    c.close()
