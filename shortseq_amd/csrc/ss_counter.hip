@@ -30,9 +30,9 @@ struct alignas(32) Slot {
 constexpr int kThreads = 256;
 constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
 constexpr uint32_t kExtractBlocks = 1024;  // extract passes: fixed grid, contiguous slot ranges
-constexpr uint32_t kSliceLogMax = 12;      // region slice: 4096 slots (one LDS-resident aggregation)
+constexpr uint32_t kSliceLogMax = 11;      // region slice: 2048 slots (one LDS-resident aggregation)
 constexpr uint32_t kPartBlocks = 1024;     // partition passes: fixed grid, contiguous read ranges
-constexpr uint32_t kMaxRegions = 16384;    // per-block region histogram in LDS (64 KB)
+constexpr uint32_t kMaxRegions = 32768;    // per-block region histogram in LDS (128 KB)
 }  // namespace
 
 struct ss_counter {
@@ -44,11 +44,13 @@ struct ss_counter {
     unsigned long long* work = nullptr;    // [0]: overflow flags, [1..]: per-(part, block) counts
     // partitioned-insert workspace (ss_counter_reserve)
     uint64_t ws_reads = 0;
-    uint64_t* ws_keys = nullptr;           // [ws_reads] packed key of read i
-    uint64_t* ws_bkey = nullptr;           // [ws_reads] keys bucketed by table region
-    uint32_t* ws_bidx = nullptr;           // [ws_reads] batch-local read index, same order
-    uint32_t* ws_hist = nullptr;           // [kPartBlocks * regions] per-(block, region) counts -> offsets
+    uint64_t* ws_keys = nullptr;           // [ws_reads] packed key of read i; later bucketed by region
+    uint64_t* ws_akey = nullptr;           // [ws_reads] keys bucketed by coarse bin
+    uint32_t* ws_aidx = nullptr;           // [ws_reads] batch-local read index, same order
+    uint32_t* ws_bidx = nullptr;           // [ws_reads] batch-local read index, region order
+    uint32_t* ws_hist = nullptr;           // [kPartBlocks * regions] per-(block, bin) counts -> offsets
     uint32_t* ws_rstart = nullptr;         // [regions + 1] region start in the bucket arrays
+    uint32_t* ws_tot = nullptr;            // [regions + 1] scratch (bin totals / coarse starts)
 };
 
 namespace {
@@ -329,32 +331,54 @@ __global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t npart
 // Partitioned insert (the C5 hot path).  Per-read global atomics on a 1-GB table are memory-side
 // atomic-bound; instead every table region (slice of 2^slice_log slots) is aggregated by ONE
 // workgroup in LDS and merged into its slice with plain loads/stores:
-//   P1 k_pc_keys      encode (2 lanes/read, as k_count_g16) -> keys[i]; per-block region histogram
-//   P2 k_pc_tot / k_pc_scan / k_pc_offsets   region starts + per-(block, region) write offsets
-//   P3 k_pc_scatter   keys + batch-local indices bucketed by region (LDS cursors, no global atomics)
-//   P4 k_pc_aggregate one workgroup per region: LDS hash (CAS / add / min) over the bucket, then
-//                     each distinct key probes the region's slice (an LDS claim bitmap arbitrates
-//                     new slots inside the workgroup; nobody else touches the slice)
-// Blocks of P1 and P3 own the same contiguous read ranges, so offsets are exact.
+//   P1 k_pc_keys       encode (2 lanes/read, as k_count_g16) -> keys[i]; per-block coarse histogram
+//   P2 scan            per-(block, bin) write offsets (k_pc_tot / k_pc_scan / k_pc_offsets)
+//   P3 k_pc_scatter    keys -> (key, read index) grouped by coarse bin (64 bins: long runs, so the
+//                      partial-line stores combine in L2), then k_pc_count + scan + k_pc_scatter
+//                      again by region (<= 256 regions per coarse bin) -- a 2-pass radix partition
+//   P4 k_pc_aggregate  one workgroup per region: LDS hash (CAS / add / min) over its bucket, then
+//                      each distinct key probes the region's slice (an LDS claim bitmap arbitrates
+//                      new slots inside the workgroup; nobody else touches the slice)
+// Every pass gives block b the same contiguous input range, so offsets are exact.
 // ------------------------------------------------------------------------------------------------
+constexpr uint32_t kCoarseBits = 7;    // 128 coarse bins for the first partition pass
+
 struct PartWs {
-    uint64_t* keys;
-    uint64_t* bkey;
-    uint32_t* bidx;
-    uint32_t* hist;     // [kPartBlocks][R]
-    uint32_t* rstart;   // [R + 1]
-    uint32_t R;
+    uint64_t* keys;    // P1 output; P3 second-pass output (bucketed by region)
+    uint64_t* akey;    // first-pass output (bucketed by coarse bin)
+    uint32_t* aidx;
+    uint32_t* bidx;    // second-pass output indices
+    const uint64_t* bkey;  // the region-bucketed keys the aggregate reads (keys or akey)
+    uint32_t* hist;    // [kPartBlocks][bins] per-(block, bin) counts -> offsets
+    uint32_t* rstart;  // [R + 1] region start in the bucketed arrays
+    uint32_t* tot;     // [bins] scratch
+    uint32_t R;        // regions
+    uint32_t rbits;    // log2(R)
 };
 
 __device__ __forceinline__ uint32_t region_of(const Tbl& t, uint64_t key) {
     return (uint32_t)(slot_top(t, key) >> t.slice_log);
 }
 
+// bin of a key for a pass: COARSE -> top kCoarseBits of the region id, else the region id
+template <bool COARSE>
+__device__ __forceinline__ uint32_t bin_of(const Tbl& t, const PartWs& w, uint64_t key) {
+    const uint32_t r = region_of(t, key);
+    if constexpr (COARSE) return w.rbits > kCoarseBits ? (r >> (w.rbits - kCoarseBits)) : r;
+    return r;
+}
+
 template <int T, int U>
-__global__ __launch_bounds__(T) void k_pc_keys(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
-                                               uint64_t n, uint32_t cpr, unsigned long long* first_bad) {
+__global__ __launch_bounds__(T) void k_pc_keys(Tbl t, PartWs w, uint32_t bins, const uint4* __restrict__ in,
+                                               uint64_t stride16, uint64_t n, uint32_t cpr,
+                                               unsigned long long* first_bad) {
+    // one histogram copy per wave when they fit (bins <= 64 in the two-pass case): LDS atomics then
+    // contend only inside a wave
     extern __shared__ uint32_t hist[];
-    for (uint32_t i = threadIdx.x; i < w.R; i += T) hist[i] = 0;
+    constexpr uint32_t kWaves = T / 64;
+    const uint32_t copies = bins * kWaves <= kMaxRegions ? kWaves : 1u;
+    uint32_t* my = hist + (copies > 1 ? (threadIdx.x >> 6) * bins : 0u);
+    for (uint32_t i = threadIdx.x; i < bins * copies; i += T) hist[i] = 0;
     __syncthreads();
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
@@ -383,30 +407,61 @@ __global__ __launch_bounds__(T) void k_pc_keys(Tbl t, PartWs w, const uint4* __r
             if (live) {
                 const uint64_t key = (uint64_t)v | ((uint64_t)hiw << 32);
                 w.keys[r] = key;
-                atomicAdd(&hist[region_of(t, key)], 1u);
+                atomicAdd(&my[bin_of<true>(t, w, key)], 1u);
             }
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < w.R; i += T) w.hist[(uint64_t)blockIdx.x * w.R + i] = hist[i];
+    for (uint32_t i = threadIdx.x; i < bins; i += T) {
+        uint32_t sum = 0;
+        for (uint32_t c = 0; c < copies; ++c) sum += hist[c * bins + i];
+        w.hist[(uint64_t)blockIdx.x * bins + i] = sum;
+    }
 }
 
-// region totals (thread per region; coalesced over regions)
-__global__ __launch_bounds__(256) void k_pc_tot(PartWs w) {
+// per-block histogram of region ids over a coarse-bucketed key array (second pass).  The block's
+// range spans few coarse buckets, so the histogram covers only that window of regions (as in
+// k_pc_scatter_lds); a wider span counts straight into the global row.
+template <int T>
+__global__ __launch_bounds__(T) void k_pc_count(Tbl t, PartWs w, const uint64_t* __restrict__ src, uint64_t n) {
+    constexpr uint32_t kWin = 1024;
+    __shared__ uint32_t hist[kWin];
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
+    uint32_t* row = w.hist + (uint64_t)blockIdx.x * w.R;
+    for (uint32_t i = threadIdx.x; i < w.R; i += T) row[i] = 0;
+    if (lo >= hi) return;
+    const uint32_t shift = w.rbits > kCoarseBits ? (w.rbits - kCoarseBits) : 0;
+    const uint32_t c0 = region_of(t, src[lo]) >> shift, c1 = region_of(t, src[hi - 1]) >> shift;
+    const uint32_t rlo = c0 << shift, nb = (c1 - c0 + 1) << shift;
+    if (nb > kWin) {
+        __syncthreads();   // the row was zeroed by other threads
+        for (uint64_t r = lo + threadIdx.x; r < hi; r += T) atomicAdd(&row[region_of(t, src[r])], 1u);
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < nb; i += T) hist[i] = 0;
+    __syncthreads();
+    for (uint64_t r = lo + threadIdx.x; r < hi; r += T) atomicAdd(&hist[region_of(t, src[r]) - rlo], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += T) row[rlo + i] = hist[i];
+}
+
+// bin totals (thread per bin; coalesced over bins)
+__global__ __launch_bounds__(256) void k_pc_tot(PartWs w, uint32_t bins) {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= w.R) return;
+    if (r >= bins) return;
     uint32_t sum = 0;
-    for (uint32_t b = 0; b < kPartBlocks; ++b) sum += w.hist[(uint64_t)b * w.R + r];
-    w.rstart[r] = sum;
+    for (uint32_t b = 0; b < kPartBlocks; ++b) sum += w.hist[(uint64_t)b * bins + r];
+    w.tot[r] = sum;
 }
 
-// exclusive scan of region totals (one block of 1024)
-__global__ __launch_bounds__(1024) void k_pc_scan(PartWs w) {
+// exclusive scan of bin totals (one block of 1024) -> start[bins + 1]
+__global__ __launch_bounds__(1024) void k_pc_scan(PartWs w, uint32_t bins, uint32_t* start) {
     __shared__ uint32_t sums[1024];
-    const uint32_t seg = (w.R + 1023) / 1024;
-    const uint32_t lo = threadIdx.x * seg, hi = min(w.R, lo + seg);
+    const uint32_t seg = (bins + 1023) / 1024;
+    const uint32_t lo = threadIdx.x * seg, hi = min(bins, lo + seg);
     uint32_t local = 0;
-    for (uint32_t i = lo; i < hi; ++i) local += w.rstart[i];
+    for (uint32_t i = lo; i < hi; ++i) local += w.tot[i];
     sums[threadIdx.x] = local;
     __syncthreads();
     for (uint32_t off = 1; off < 1024; off <<= 1) {
@@ -417,40 +472,156 @@ __global__ __launch_bounds__(1024) void k_pc_scan(PartWs w) {
     }
     uint32_t run = sums[threadIdx.x] - local;
     for (uint32_t i = lo; i < hi; ++i) {
-        const uint32_t c = w.rstart[i];
-        w.rstart[i] = run;
+        const uint32_t c = w.tot[i];   // read before the write: start may alias tot
+        start[i] = run;
         run += c;
     }
-    if (threadIdx.x == 1023) w.rstart[w.R] = sums[1023];
+    if (threadIdx.x == 1023) start[bins] = sums[1023];
 }
 
-// per-(block, region) write offsets = region start + counts of earlier blocks (thread per region)
-__global__ __launch_bounds__(256) void k_pc_offsets(PartWs w) {
+// per-(block, bin) write offsets = bin start + counts of earlier blocks (thread per bin)
+__global__ __launch_bounds__(256) void k_pc_offsets(PartWs w, uint32_t bins, const uint32_t* start) {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= w.R) return;
-    uint32_t run = w.rstart[r];
+    if (r >= bins) return;
+    uint32_t run = start[r];
     for (uint32_t b = 0; b < kPartBlocks; ++b) {
-        const uint64_t i = (uint64_t)b * w.R + r;
+        const uint64_t i = (uint64_t)b * bins + r;
         const uint32_t c = w.hist[i];
         w.hist[i] = run;
         run += c;
     }
 }
 
-template <int T>
-__global__ __launch_bounds__(T) void k_pc_scatter(Tbl t, PartWs w, uint64_t n) {
-    extern __shared__ uint32_t cursor[];
-    for (uint32_t i = threadIdx.x; i < w.R; i += T) cursor[i] = w.hist[(uint64_t)blockIdx.x * w.R + i];
+// LDS-staged scatter (both partition passes).  Per tile of kTile elements: local histogram of the
+// block's active bins -> exclusive scan -> elements placed in LDS sorted by bin -> written out so
+// consecutive lanes store consecutive positions of one bin's run (full-line stores), then the
+// block's per-bin cursors advance.  Active bins: COARSE pass = the 64 coarse bins; fine pass =
+// the regions of the (1-2) coarse buckets the block's range spans (range-sorted input), mapped to
+// local bins region - lo_region; a block spanning more than kMaxLocalBins falls back to direct
+// (unstaged) stores through the same cursors.
+constexpr uint32_t kTile = 2048;
+constexpr uint32_t kMaxLocalBins = 1024;
+
+// exclusive scan of data[0..n) (n <= 1024) by a 512-thread block; returns the total
+__device__ __forceinline__ uint32_t block_scan_512(uint32_t* data, uint32_t n, uint32_t* wsum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t i0 = 2 * tid, i1 = 2 * tid + 1;
+    const uint32_t a = i0 < n ? data[i0] : 0u, b = i1 < n ? data[i1] : 0u;
+    uint32_t v = a + b, incl = v;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
     __syncthreads();
+    if (tid < 8) {
+        uint32_t run = 0;
+        for (uint32_t w = 0; w < 8; ++w) {
+            const uint32_t t = wsum[w];
+            if (w == tid) wsum[8 + w] = run;
+            run += t;
+        }
+        if (tid == 0) wsum[16] = run;
+    }
+    __syncthreads();
+    const uint32_t excl = incl - v + wsum[8 + wave];
+    if (i0 < n) data[i0] = excl;
+    if (i1 < n) data[i1] = excl + a;
+    const uint32_t total = wsum[16];
+    __syncthreads();
+    return total;
+}
+
+template <bool COARSE, bool HAS_IDX>
+__global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_t bins,
+                                                        const uint64_t* __restrict__ src,
+                                                        const uint32_t* __restrict__ src_idx,
+                                                        uint64_t* __restrict__ dst, uint32_t* __restrict__ dst_idx,
+                                                        uint64_t n) {
+    constexpr int T = 512;
+    __shared__ uint32_t cursor[kMaxLocalBins];
+    __shared__ uint32_t lstart[kMaxLocalBins];
+    __shared__ uint32_t lcount[kMaxLocalBins];
+    __shared__ uint64_t skey[kTile];
+    __shared__ uint32_t sidx[kTile];
+    __shared__ uint16_t sbin[kTile];
+    __shared__ uint32_t wsum[17];
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
-    for (uint64_t r = lo + threadIdx.x; r < hi; r += T) {
-        const uint64_t key = w.keys[r];
-        const uint32_t pos = atomicAdd(&cursor[region_of(t, key)], 1u);
-        w.bkey[pos] = key;
-        w.bidx[pos] = (uint32_t)r;
+    if (lo >= hi) return;
+    // active bin window of this block
+    uint32_t bin_lo = 0, nb = bins;
+    if constexpr (!COARSE) {
+        const uint32_t shift = w.rbits > kCoarseBits ? (w.rbits - kCoarseBits) : 0;
+        const uint32_t c0 = region_of(t, src[lo]) >> shift, c1 = region_of(t, src[hi - 1]) >> shift;
+        bin_lo = c0 << shift;
+        nb = (c1 - c0 + 1) << shift;
+    }
+    const bool staged = nb <= kMaxLocalBins;
+    if (staged) {
+        for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] = w.hist[(uint64_t)blockIdx.x * bins + bin_lo + i];
+    }
+    __syncthreads();
+    if (!staged) {   // rare (a block spanning many tiny coarse buckets): direct stores, global offsets
+        for (uint64_t r = lo + threadIdx.x; r < hi; r += T) {
+            const uint64_t key = src[r];
+            const uint32_t b = bin_of<COARSE>(t, w, key);
+            const uint32_t pos = atomicAdd(&w.hist[(uint64_t)blockIdx.x * bins + b], 1u);
+            dst[pos] = key;
+            dst_idx[pos] = HAS_IDX ? src_idx[r] : (uint32_t)r;
+        }
+        return;
+    }
+    for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
+        for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
+        __syncthreads();
+        uint64_t key[kTile / T];
+        uint32_t idx[kTile / T], lb[kTile / T], rank[kTile / T];
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
+            const uint32_t e = j * T + threadIdx.x;
+            if (e < cnt) {
+                key[j] = src[t0 + e];
+                idx[j] = HAS_IDX ? src_idx[t0 + e] : (uint32_t)(t0 + e);
+                lb[j] = bin_of<COARSE>(t, w, key[j]) - bin_lo;
+                rank[j] = atomicAdd(&lcount[lb[j]], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nb; i += T) lstart[i] = lcount[i];
+        __syncthreads();
+        block_scan_512(lstart, nb, wsum);
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
+            const uint32_t e = j * T + threadIdx.x;
+            if (e < cnt) {
+                const uint32_t sp = lstart[lb[j]] + rank[j];
+                skey[sp] = key[j];
+                sidx[sp] = idx[j];
+                sbin[sp] = (uint16_t)lb[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < cnt; i += T) {
+            const uint32_t b = sbin[i];
+            const uint32_t gpos = cursor[b] + (i - lstart[b]);
+            dst[gpos] = skey[i];
+            dst_idx[gpos] = sidx[i];
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] += lcount[i];
+        __syncthreads();
     }
 }
+
+// P4.  LDS: the aggregation table (2S entries of key + count + first-offset) and a copy of the
+// slice's S keys.  Phase 1 aggregates the region's bucket in LDS.  Phase 2 resolves every distinct
+// key's slot inside the LDS key copy (an LDS CAS on the copy claims a new slot; no global
+// atomics).  Phase 3 issues the global read-modify-writes of all the thread's slots together
+// (independent loads, so their latencies overlap), then the stores.
+constexpr uint32_t kAggT = 1024;
+constexpr uint32_t kAggPerThread = (2u << kSliceLogMax) / kAggT;   // LDS table slots per thread
 
 template <int T>
 __global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t base_index) {
@@ -458,22 +629,24 @@ __global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t ba
     const uint32_t S = (uint32_t)t.slice_mask + 1;          // slice slots
     const uint32_t LS = 2 * S;                               // LDS table slots (load <= 50%)
     unsigned long long* lkey = (unsigned long long*)smem;                 // [LS]
-    uint32_t* lcnt = (uint32_t*)(smem + (size_t)LS * 8);                  // [LS]
+    unsigned long long* skey = lkey + LS;                                 // [S] slice key copy
+    uint32_t* lcnt = (uint32_t*)(skey + S);                               // [LS]
     uint32_t* lfst = lcnt + LS;                                           // [LS]
-    uint32_t* claim = lfst + LS;                                          // [S / 32]
-    uint32_t* sent = claim + S / 32;                                      // [2]: sentinel count, first
+    uint32_t* sent = lfst + LS;                                           // [2]: sentinel count, first
+    const uint32_t region = blockIdx.x;
+    const uint64_t slice_base = (uint64_t)region << t.slice_log;
     for (uint32_t i = threadIdx.x; i < LS; i += T) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
         lfst[i] = 0xFFFFFFFFu;
     }
-    for (uint32_t i = threadIdx.x; i < S / 32; i += T) claim[i] = 0;
+    for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = t.slots[slice_base + i].key;
     if (threadIdx.x == 0) {
         sent[0] = 0;
         sent[1] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    const uint32_t region = blockIdx.x;
+    // phase 1: aggregate the bucket
     const uint32_t b0 = w.rstart[region], b1 = w.rstart[region + 1];
     const uint32_t lds_shift = (t.shift >= 64 ? 64 : t.shift) - 1;   // one more hash bit than the slice
     for (uint32_t e = b0 + threadIdx.x; e < b1; e += T) {
@@ -494,37 +667,61 @@ __global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t ba
         atomicMin(&lfst[ls], idx);
     }
     __syncthreads();
-    // merge the region's distinct keys into its slice; only this workgroup touches the slice
-    const uint64_t slice_base = (uint64_t)region << t.slice_log;
-    for (uint32_t ls = threadIdx.x; ls < LS; ls += T) {
+    // phase 2: slot of each distinct key in the slice (LDS only)
+    uint32_t slot[kAggPerThread];
+    bool fresh[kAggPerThread];
+#pragma unroll
+    for (uint32_t j = 0; j < kAggPerThread; ++j) {
+        const uint32_t ls = j * T + threadIdx.x;
+        slot[j] = 0xFFFFFFFFu;
+        fresh[j] = false;
+        if (ls >= LS) continue;
         const unsigned long long key = lkey[ls];
         if (key == kEmpty) continue;
-        const unsigned long long c = lcnt[ls];
-        const unsigned long long f = base_index + lfst[ls];
         uint32_t off = (uint32_t)(slot_top(t, key) & t.slice_mask);
-        bool done = false;
         for (uint32_t probe = 0; probe < S; ++probe) {
-            Slot* sl = &t.slots[slice_base + off];
-            const unsigned long long gk = sl->key;
-            if (gk == key) {
-                sl->ncount -= c;
-                if (f < sl->first) sl->first = f;
-                done = true;
+            const unsigned long long cur = skey[off];
+            if (cur == key) {
+                slot[j] = off;
                 break;
             }
-            if (gk == kEmpty) {
-                const uint32_t bit = 1u << (off & 31);
-                if (!(atomicOr(&claim[off >> 5], bit) & bit)) {
-                    sl->key = key;
-                    sl->ncount = ~c;
-                    sl->first = f;
-                    done = true;
+            if (cur == kEmpty) {
+                const unsigned long long prev = atomicCAS(&skey[off], (unsigned long long)kEmpty, key);
+                if (prev == kEmpty) {
+                    slot[j] = off;
+                    fresh[j] = true;
+                    break;
+                }
+                if (prev == key) {   // cannot happen (keys are distinct in the LDS table); be safe
+                    slot[j] = off;
                     break;
                 }
             }
             off = (off + 1) & (uint32_t)t.slice_mask;
         }
-        if (!done) atomicOr(t.overflow, 1ull);
+        if (slot[j] == 0xFFFFFFFFu) atomicOr(t.overflow, 1ull);
+    }
+    // phase 3: global read-modify-writes, loads first (independent), then stores
+    unsigned long long nc[kAggPerThread], fs[kAggPerThread];
+#pragma unroll
+    for (uint32_t j = 0; j < kAggPerThread; ++j) {
+        nc[j] = ~0ull;
+        fs[j] = ~0ull;
+        if (slot[j] != 0xFFFFFFFFu && !fresh[j]) {
+            const Slot* sl = &t.slots[slice_base + slot[j]];
+            nc[j] = sl->ncount;
+            fs[j] = sl->first;
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kAggPerThread; ++j) {
+        if (slot[j] == 0xFFFFFFFFu) continue;
+        const uint32_t ls = j * T + threadIdx.x;
+        Slot* sl = &t.slots[slice_base + slot[j]];
+        const unsigned long long f = base_index + lfst[ls];
+        if (fresh[j]) sl->key = lkey[ls];
+        sl->ncount = nc[j] - lcnt[ls];
+        sl->first = f < fs[j] ? f : fs[j];
     }
     if (threadIdx.x == 0 && sent[0]) {
         Slot* sl = &t.slots[t.mask + 1];
@@ -587,11 +784,10 @@ int ss_counter_destroy(ss_counter* c) {
     if (!c) return SS_OK;
     if (c->slots) (void)hipFree(c->slots);
     if (c->work) (void)hipFree(c->work);
-    if (c->ws_keys) (void)hipFree(c->ws_keys);
-    if (c->ws_bkey) (void)hipFree(c->ws_bkey);
-    if (c->ws_bidx) (void)hipFree(c->ws_bidx);
+    ss_counter_release(c);
     if (c->ws_hist) (void)hipFree(c->ws_hist);
     if (c->ws_rstart) (void)hipFree(c->ws_rstart);
+    if (c->ws_tot) (void)hipFree(c->ws_tot);
     delete c;
     return SS_OK;
 }
@@ -620,19 +816,16 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     if (R > kMaxRegions) return ss_fail(SS_EARG, "capacity too large for the partitioned insert");
     if (max_reads >= (1ull << 32)) return ss_fail(SS_EARG, "max_reads must be < 2^32 per insert");
     if (max_reads <= c->ws_reads) return SS_OK;
-    if (c->ws_keys) (void)hipFree(c->ws_keys);
-    if (c->ws_bkey) (void)hipFree(c->ws_bkey);
-    if (c->ws_bidx) (void)hipFree(c->ws_bidx);
-    c->ws_keys = nullptr;
-    c->ws_bkey = nullptr;
-    c->ws_bidx = nullptr;
-    c->ws_reads = 0;
+    ss_counter_release(c);
     hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bkey, max_reads * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, max_reads * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, max_reads * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_hist) e = hipMalloc((void**)&c->ws_hist, (size_t)kPartBlocks * R * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_rstart) e = hipMalloc((void**)&c->ws_rstart, (R + 1) * sizeof(uint32_t));
+    if (e == hipSuccess && !c->ws_tot) e = hipMalloc((void**)&c->ws_tot, (R + 1) * sizeof(uint32_t));
     if (e != hipSuccess) {
+        ss_counter_release(c);
         ss_check(e, "ss_counter_reserve hipMalloc");
         return SS_ENOMEM;
     }
@@ -645,10 +838,12 @@ uint64_t ss_counter_reserved(const ss_counter* c) { return c ? c->ws_reads : 0; 
 int ss_counter_release(ss_counter* c) {
     if (!c) return ss_fail(SS_EARG, "null counter");
     if (c->ws_keys) (void)hipFree(c->ws_keys);
-    if (c->ws_bkey) (void)hipFree(c->ws_bkey);
+    if (c->ws_akey) (void)hipFree(c->ws_akey);
+    if (c->ws_aidx) (void)hipFree(c->ws_aidx);
     if (c->ws_bidx) (void)hipFree(c->ws_bidx);
     c->ws_keys = nullptr;
-    c->ws_bkey = nullptr;
+    c->ws_akey = nullptr;
+    c->ws_aidx = nullptr;
     c->ws_bidx = nullptr;
     c->ws_reads = 0;
     return SS_OK;
@@ -670,37 +865,56 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
     if (fast && n <= c->ws_reads) {
         PartWs w;
         w.keys = c->ws_keys;
-        w.bkey = c->ws_bkey;
+        w.akey = c->ws_akey;
+        w.aidx = c->ws_aidx;
         w.bidx = c->ws_bidx;
         w.hist = c->ws_hist;
         w.rstart = c->ws_rstart;
+        w.tot = c->ws_tot;
+        w.bkey = nullptr;
         w.R = (uint32_t)(c->cap >> c->slice_log);
-        const size_t hist_lds = (size_t)w.R * sizeof(uint32_t);
+        w.rbits = c->log2cap - c->slice_log;
         const uint32_t S = 1u << c->slice_log;
-        const size_t agg_lds = (size_t)2 * S * 16 + (S / 32) * 4 + 8;
-        constexpr int T1 = 512, U1 = 4;
+        const size_t agg_lds = (size_t)2 * S * 16 + (size_t)S * 8 + 8;
+        const bool two_pass = w.rbits > kCoarseBits;             // > 64 regions: coarse pass first
+        const uint32_t bins1 = two_pass ? (1u << kCoarseBits) : w.R;
+        constexpr int T1 = 512, U1 = 4, TS = 512;
         // dynamic LDS above the 64 KB default: opt in once per kernel (host-side attribute)
         static bool attrs_set = false;
         if (!attrs_set) {
             hipError_t ea = hipFuncSetAttribute((const void*)k_pc_keys<T1, U1>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kMaxRegions * 4);
             if (ea == hipSuccess)
-                ea = hipFuncSetAttribute((const void*)k_pc_scatter<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         kMaxRegions * 4);
-            if (ea == hipSuccess)
-                ea = hipFuncSetAttribute((const void*)k_pc_aggregate<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)(2 * (1u << kSliceLogMax) * 16 + (1u << kSliceLogMax) / 8 + 8));
+                ea = hipFuncSetAttribute((const void*)k_pc_aggregate<kAggT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(2 * (1u << kSliceLogMax) * 16 + (1u << kSliceLogMax) * 8 + 8));
             if (ea != hipSuccess) return ss_check(ea, "hipFuncSetAttribute (dynamic LDS)");
             attrs_set = true;
         }
-        hipLaunchKernelGGL((k_pc_keys<T1, U1>), dim3(kPartBlocks), dim3(T1), hist_lds, s, t, w, (const uint4*)d_ascii,
-                           stride / 16, n, L / 16, (unsigned long long*)d_first_bad);
-        const unsigned rg = (w.R + 255) / 256;
-        hipLaunchKernelGGL(k_pc_tot, dim3(rg), dim3(256), 0, s, w);
-        hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w);
-        hipLaunchKernelGGL(k_pc_offsets, dim3(rg), dim3(256), 0, s, w);
-        hipLaunchKernelGGL((k_pc_scatter<512>), dim3(kPartBlocks), dim3(512), hist_lds, s, t, w, n);
-        hipLaunchKernelGGL((k_pc_aggregate<1024>), dim3(w.R), dim3(1024), agg_lds, s, t, w, base_index);
+        auto scan = [&](uint32_t bins, uint32_t* start) {
+            const unsigned g = (bins + 255) / 256;
+            hipLaunchKernelGGL(k_pc_tot, dim3(g), dim3(256), 0, s, w, bins);
+            hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, bins, start);
+            hipLaunchKernelGGL(k_pc_offsets, dim3(g), dim3(256), 0, s, w, bins, (const uint32_t*)start);
+        };
+        const size_t keys_lds = (bins1 * (T1 / 64) <= kMaxRegions ? bins1 * (T1 / 64) : bins1) * 4;
+        hipLaunchKernelGGL((k_pc_keys<T1, U1>), dim3(kPartBlocks), dim3(T1), keys_lds, s, t, w, bins1,
+                           (const uint4*)d_ascii, stride / 16, n, L / 16, (unsigned long long*)d_first_bad);
+        if (two_pass) {
+            scan(bins1, w.tot + 0);   // coarse starts are not needed later; tot is reused as scratch
+            hipLaunchKernelGGL((k_pc_scatter_lds<true, false>), dim3(kPartBlocks), dim3(512), 0, s, t, w, bins1,
+                               (const uint64_t*)w.keys, (const uint32_t*)nullptr, w.akey, w.aidx, n);
+            hipLaunchKernelGGL((k_pc_count<TS>), dim3(kPartBlocks), dim3(TS), 0, s, t, w, (const uint64_t*)w.akey, n);
+            scan(w.R, w.rstart);
+            hipLaunchKernelGGL((k_pc_scatter_lds<false, true>), dim3(kPartBlocks), dim3(512), 0, s, t, w, w.R,
+                               (const uint64_t*)w.akey, (const uint32_t*)w.aidx, w.keys, w.bidx, n);
+            w.bkey = w.keys;
+        } else {
+            scan(w.R, w.rstart);   // <= 64 regions: one pass, bins = regions (bin_of<true> == region)
+            hipLaunchKernelGGL((k_pc_scatter_lds<true, false>), dim3(kPartBlocks), dim3(512), 0, s, t, w, w.R,
+                               (const uint64_t*)w.keys, (const uint32_t*)nullptr, w.akey, w.bidx, n);
+            w.bkey = w.akey;
+        }
+        hipLaunchKernelGGL((k_pc_aggregate<kAggT>), dim3(w.R), dim3(kAggT), agg_lds, s, t, w, base_index);
         return ss_check(hipGetLastError(), "partitioned insert");
     }
     if (fast) {
