@@ -119,7 +119,9 @@ int ss_encode_hamming_ref(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64
  * Dedup counter — replaces ShortSeqCounter._count_sequence (counter.pyx:41-54): key = (length,
  * packed words) (short_seq_64.pyx:41-44; short_seq_192.pyx:35-41), count += 1, first-occurrence
  * index kept so the host can rebuild dict insertion order.  Open-addressing table in HBM, one per
- * handle; keys of one handle have L <= 32 (one word; the length is part of the key).
+ * handle; all keys of one handle share one length L <= 1024 (the length is part of the key).
+ * L <= 32: the slot key is the packed word.  L > 32: W = ceil(L/32) words per key, kept beside the
+ * slots; the slot holds a 64-bit fingerprint of the words and equality is decided on the words.
  * ---------------------------------------------------------------------------------------------- */
 typedef struct ss_counter ss_counter;
 
@@ -137,7 +139,9 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads);
 uint64_t ss_counter_reserved(const ss_counter* c);
 int ss_counter_release(ss_counter* c);       /* free the workspace (inserts take the direct path) */
 
-/* Encode + count a fixed-length batch (L <= 32).  Read i gets global index base_index + i.
+/* Encode + count a fixed-length batch (L <= 1024).  Read i gets global index base_index + i.
+ * Multi-word handles (L > 32) always take the partitioned path and grow the workspace to n reads
+ * (plus n * W words for the packed batch) when the reservation is smaller. 
  * If the batch holds an invalid read (reported through *d_first_bad) the table's contents are
  * unspecified afterwards, like the reference counter that raises mid-list (counter.pyx:22-29). */
 int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L,
@@ -166,6 +170,20 @@ int ss_counter_size(ss_counter* c, uint64_t* d_size, void* stream);
 int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens,
                        uint64_t* d_counts, uint64_t* d_first, uint64_t cap,
                        uint64_t* d_part_counts, void* stream);
+
+/* Words per key of the handle: 1 for L <= 32, ceil(L/32) for multi-word keys (L 33..1024, the
+ * ShortSeq192 / ShortSeqVar keys of short_seq_192.pyx:35-41 / short_seq_var.pyx:22-28; counted
+ * under a 64-bit fingerprint of the words, equality always on the full words).  0 for NULL. */
+int ss_counter_words(const ss_counter* c);
+
+/* ss_counter_extract for any key length: as ss_counter_extract, plus d_words[cap * W] receives the
+ * W packed words of each entry (row i = entry i).  For multi-word handles d_fps gets the entries'
+ * fingerprints (the owner partition is owner_of(fingerprint)); for single-word handles d_fps and
+ * d_words both get the packed word.  ss_counter_extract itself rejects multi-word handles, and
+ * ss_counter_merge takes single-word keys only. */
+int ss_counter_extract_words(ss_counter* c, uint32_t n_parts, uint64_t* d_fps, uint32_t* d_lens,
+                             uint64_t* d_words, uint64_t* d_counts, uint64_t* d_first, uint64_t cap,
+                             uint64_t* d_part_counts, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):

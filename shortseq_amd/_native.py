@@ -57,6 +57,8 @@ SIGNATURES = [
     ("ss_counter_overflow", C.c_int, [_P, _P, _P]),
     ("ss_counter_size", C.c_int, [_P, _P, _P]),
     ("ss_counter_extract", C.c_int, [_P, _U32, _P, _P, _P, _P, _U64, _P, _P]),
+    ("ss_counter_words", C.c_int, [_P]),
+    ("ss_counter_extract_words", C.c_int, [_P, _U32, _P, _P, _P, _P, _P, _U64, _P, _P]),
     ("ss_synth_reads", C.c_int, [_P, _U64, _U64, _U64, _U32, _U64, _P]),
     ("ss_synth_pool_reads", C.c_int, [_P, _U64, _U64, _U64, _U64, _U64, _U32, _U64, _P]),
     ("ss_host_encode", C.c_int, [_P, _U64, _P, C.POINTER(SsErr)]),

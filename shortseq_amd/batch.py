@@ -262,8 +262,9 @@ def synth_pool_reads(n: int, L: int, seed: int, pool_seed: int, U: int, *, i0: i
 
 
 class GpuCounter:
-    """Dedup counter in HBM for reads of ONE length L <= 32 (ShortSeqCounter's hot loop,
-    counter.pyx:41-54).  Counts and first-occurrence indices per distinct packed word."""
+    """Dedup counter in HBM for reads of ONE length L <= 1024 (ShortSeqCounter's hot loop,
+    counter.pyx:41-54).  Counts and first-occurrence indices per distinct key: the packed word for
+    L <= 32, the W = ceil(L/32) packed words for longer reads (fingerprinted, compared on words)."""
 
     def __init__(self, capacity: int, device=None):
         self.device = torch.device(device) if device is not None else torch.device(
@@ -290,6 +291,11 @@ class GpuCounter:
     def length(self) -> int:
         return int(lib().ss_counter_length(self._h))
 
+    @property
+    def words(self) -> int:
+        """Words per key (1 for L <= 32); fixed by the first insert."""
+        return int(lib().ss_counter_words(self._h))
+
     def reset(self) -> None:
         check(lib().ss_counter_reset(self._h, _stream(self.device)), "ss_counter_reset")
 
@@ -305,7 +311,9 @@ class GpuCounter:
         """partitioned: None = automatic (large batches), True = reserve workspace and use the
         partitioned insert if the table allows it, False = direct atomic insert."""
         n, L, stride = _as_rows(ascii, L, stride)
-        if partitioned is None:
+        if L > 32:   # multi-word keys: always partitioned, the library grows the workspace itself
+            partitioned = None
+        elif partitioned is None:
             partitioned = n >= self.PARTITION_MIN_READS
         if partitioned and n > int(lib().ss_counter_reserved(self._h)) and n < (1 << 32):
             self.reserve(n)
@@ -349,6 +357,35 @@ class GpuCounter:
         check(lib().ss_counter_extract(self._h, n_parts, keys.data_ptr(), lens.data_ptr(), counts.data_ptr(),
                                        first.data_ptr(), cap, parts.data_ptr(), _stream(d)), "ss_counter_extract")
         return keys, lens, counts, first, parts
+
+    def extract_words(self, n_parts: int = 1, cap: Optional[int] = None):
+        """As extract, for any key length: (fps, lens, words [cap, W], counts, first, part_counts);
+        fps = the multi-word fingerprints (the packed word itself for W = 1)."""
+        cap = self.capacity + 1 if cap is None else cap
+        d = self.device
+        W = max(1, self.words)
+        fps = torch.empty(cap, dtype=torch.int64, device=d)
+        lens = torch.empty(cap, dtype=torch.int32, device=d)
+        words = torch.empty((cap, W), dtype=torch.int64, device=d)
+        counts = torch.empty(cap, dtype=torch.int64, device=d)
+        first = torch.empty(cap, dtype=torch.int64, device=d)
+        parts = torch.empty(n_parts, dtype=torch.int64, device=d)
+        check(lib().ss_counter_extract_words(self._h, n_parts, fps.data_ptr(), lens.data_ptr(), words.data_ptr(),
+                                             counts.data_ptr(), first.data_ptr(), cap, parts.data_ptr(), _stream(d)),
+              "ss_counter_extract_words")
+        return fps, lens, words, counts, first, parts
+
+    def items_sorted_words(self):
+        """Host copy of (words u64 [m, W], counts, first) sorted by first occurrence (= dict order)."""
+        _, _, words, counts, first, parts = self.extract_words(1)
+        m = int(parts.sum().item())
+        if self.overflowed():
+            raise RuntimeError("GPU counter table overflowed; use a larger capacity")
+        k = words[:m].cpu().numpy().view(np.uint64)
+        c = counts[:m].cpu().numpy()
+        f = first[:m].cpu().numpy()
+        o = np.argsort(f, kind="stable")
+        return k[o], c[o], f[o]
 
     def items_sorted(self):
         """Host copy of (keys u64, counts, first) sorted by first occurrence (= dict order)."""

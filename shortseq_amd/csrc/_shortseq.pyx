@@ -429,14 +429,16 @@ cdef class ShortSeqCounter(dict):
 
 
 def _count_batch_gpu(ShortSeqCounter self, list reads, device):
-    """Batch path: stage the reads, count each length-group <= 32 nt on the GPU, rebuild the dict in
-    first-occurrence order.  Longer reads use the host objects (multi-word GPU keys: next round)."""
+    """Batch path: stage the reads, count each length group on the GPU (one table per length: the
+    length is part of the key, short_seq_64.pyx:41-44), rebuild the dict in first-occurrence order.
+    Reads longer than 1024 nt go through the host loop, which raises the reference's error."""
     import numpy as np
     import torch
     from . import batch as B
 
     cdef Py_ssize_t i, n = PyList_GET_SIZE(reads)
     cdef object item
+    cdef uint64_t[:, ::1] kv
     lens_np = np.empty(n, dtype=np.int64)
     cdef int64_t[:] lens = lens_np
     cdef int64_t total = 0
@@ -462,7 +464,7 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, device):
         if L == 0:
             entries.append((int(idx[0]), empty, int(len(idx))))
             continue
-        if L > C_MAX_64:
+        if L > C_MAX_VAR:
             sub = ShortSeqCounter(device="host")
             firsts = {}
             for j in idx:
@@ -492,13 +494,14 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, device):
             if fb != -1:
                 first_bad = min(first_bad, int(idx[fb]))
                 continue
-            keys, counts, firsts = cnt.items_sorted()
+            keys, counts, firsts = cnt.items_sorted_words()
         finally:
             cnt.close()
         gfirst = idx[firsts.astype(np.int64)]
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        kv = keys
         for k in range(len(keys)):
-            w = <uint64_t>keys[k]
-            entries.append((int(gfirst[k]), _from_words(&w, L), int(counts[k])))
+            entries.append((int(gfirst[k]), _from_words(&kv[k, 0], L), int(counts[k])))
     if first_bad < n:
         _raise_first_error(reads, first_bad + 1)
         raise AssertionError("GPU flagged a read the host codec accepts")

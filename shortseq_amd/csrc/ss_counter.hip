@@ -40,7 +40,12 @@ struct ss_counter {
     uint32_t log2cap = 0;
     uint32_t slice_log = 0;                // table = 2^(log2cap - slice_log) regions of 2^slice_log slots
     int32_t L = -1;                        // length of every key in this handle (-1: not fixed yet)
-    Slot* slots = nullptr;                 // [cap + 1]
+    uint32_t W = 1;                        // words per key: 1 (L <= 32) or ceil(L/32) (multi-word keys)
+    Slot* slots = nullptr;                 // [cap + 1]; multi-word: slot.key = 64-bit fingerprint
+    uint64_t* keywords = nullptr;          // multi-word keys: [cap * W] the key words of slot s
+    uint64_t* ws_words = nullptr;          // multi-word insert workspace: [ws_words_cap] packed reads
+    uint64_t ws_words_cap = 0;             // words allocated at ws_words
+    uint32_t keywords_W = 0;               // W the keywords array was allocated for
     unsigned long long* work = nullptr;    // [0]: overflow flags, [1..]: per-(part, block) counts
     // partitioned-insert workspace (ss_counter_reserve)
     uint64_t ws_reads = 0;
@@ -57,6 +62,8 @@ namespace {
 
 struct Tbl {
     Slot* slots;
+    uint64_t* keywords;   // multi-word keys only
+    uint32_t W;
     unsigned long long* overflow;
     uint64_t mask;        // cap - 1
     uint64_t slice_mask;  // slots per region - 1
@@ -302,7 +309,8 @@ __global__ __launch_bounds__(1024) void k_part_offsets(uint32_t nparts, unsigned
 __global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t nparts, int32_t L,
                                                            const unsigned long long* bc, uint64_t* okeys,
                                                            uint32_t* olens, uint64_t* ocounts, uint64_t* ofirst,
-                                                           uint64_t cap_out, unsigned long long* overflow) {
+                                                           uint64_t cap_out, unsigned long long* overflow,
+                                                           uint64_t* owords) {
     __shared__ unsigned long long cursor[kMaxParts];
     for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) cursor[p] = bc[(uint64_t)p * kExtractBlocks + blockIdx.x];
     __syncthreads();
@@ -320,6 +328,14 @@ __global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t npart
             continue;
         }
         const Slot& sl = t.slots[s];
+        if (owords) {   // key words (multi-word: okeys gets the fingerprint; one word: the key)
+            if (t.W == 1) {
+                owords[pos] = key;
+            } else {
+                const uint64_t* kw = t.keywords + s * t.W;
+                for (uint32_t q = 0; q < t.W; ++q) owords[pos * t.W + q] = kw[q];
+            }
+        }
         okeys[pos] = key;
         olens[pos] = (uint32_t)L;
         ocounts[pos] = ~sl.ncount;
@@ -730,9 +746,168 @@ __global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t ba
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Multi-word keys (33..1024 nt: W = ceil(L/32) words; ShortSeq192 / ShortSeqVar keys,
+// short_seq_192.pyx:35-41 / short_seq_var.pyx:22-28: equal iff length and all words equal).
+// The reads are packed first (ss_encode_fixed into ws_words), keyed by a 64-bit fingerprint of
+// their words, and go through the same partition passes.  Equality is always decided on the full
+// words: the LDS table claims a slot with ONE 64-bit CAS of (fingerprint high half | representative
+// read index), so a thread that meets a claimed slot can compare words immediately (no waiting on
+// another lane's second store); the global slice stores the full fingerprint plus the key words.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t words_fp(const uint64_t* w, uint32_t W) {
+    uint64_t h = 0x243F6A8885A308D3ull ^ W;
+    for (uint32_t j = 0; j < W; ++j) h = splitmix64(h ^ w[j]);
+    return h == kEmpty ? ~1ull : h;   // EMPTY marks free slots
+}
+
+__device__ __forceinline__ bool words_eq(const uint64_t* a, const uint64_t* b, uint32_t W) {
+    bool eq = true;
+    for (uint32_t j = 0; j < W; ++j) eq &= a[j] == b[j];
+    return eq;
+}
+
+template <int T>
+__global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, const uint64_t* __restrict__ words,
+                                             uint64_t n) {
+    extern __shared__ uint32_t hist[];
+    constexpr uint32_t kWaves = T / 64;
+    const uint32_t copies = bins * kWaves <= kMaxRegions ? kWaves : 1u;
+    uint32_t* my = hist + (copies > 1 ? (threadIdx.x >> 6) * bins : 0u);
+    for (uint32_t i = threadIdx.x; i < bins * copies; i += T) hist[i] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
+    for (uint64_t r = lo + threadIdx.x; r < hi; r += T) {
+        const uint64_t fp = words_fp(words + r * t.W, t.W);
+        w.keys[r] = fp;
+        atomicAdd(&my[bin_of<true>(t, w, fp)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < bins; i += T) {
+        uint32_t sum = 0;
+        for (uint32_t c = 0; c < copies; ++c) sum += hist[c * bins + i];
+        w.hist[(uint64_t)blockIdx.x * bins + i] = sum;
+    }
+}
+
+constexpr uint32_t kMwT = 1024;
+constexpr uint32_t kMwPerThread = (2u << kSliceLogMax) / kMwT;
+
+template <int T>
+__global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint64_t* __restrict__ words,
+                                                    uint64_t base_index) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t S = (uint32_t)t.slice_mask + 1;
+    const uint32_t LS = 2 * S;
+    const uint32_t W = t.W;
+    unsigned long long* lkey = (unsigned long long*)smem;                 // [LS] (fp_hi << 32 | rep)
+    unsigned long long* skey = lkey + LS;                                 // [S] slice fingerprints
+    uint32_t* lcnt = (uint32_t*)(skey + S);                               // [LS]
+    uint32_t* lfst = lcnt + LS;                                           // [LS]
+    const uint32_t region = blockIdx.x;
+    const uint64_t slice_base = (uint64_t)region << t.slice_log;
+    for (uint32_t i = threadIdx.x; i < LS; i += T) {
+        lkey[i] = kEmpty;
+        lcnt[i] = 0;
+        lfst[i] = 0xFFFFFFFFu;
+    }
+    for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = t.slots[slice_base + i].key;
+    __syncthreads();
+    const uint32_t b0 = w.rstart[region], b1 = w.rstart[region + 1];
+    const uint32_t lds_shift = (t.shift >= 64 ? 64 : t.shift) - 1;
+    for (uint32_t e = b0 + threadIdx.x; e < b1; e += T) {
+        const uint64_t fp = w.bkey[e];
+        const uint32_t idx = w.bidx[e];
+        const uint64_t tag = (fp >> 32) << 32;
+        uint32_t ls = (uint32_t)((fp * 0x9E3779B97F4A7C15ull) >> lds_shift) & (LS - 1);
+        for (;;) {
+            unsigned long long cur = lkey[ls];
+            if (cur == kEmpty) {
+                cur = atomicCAS(&lkey[ls], (unsigned long long)kEmpty, (unsigned long long)(tag | idx));
+                if (cur == kEmpty) break;   // claimed, this read is the representative
+            }
+            if ((cur & 0xFFFFFFFF00000000ull) == tag &&
+                words_eq(words + (cur & 0xFFFFFFFFull) * W, words + (uint64_t)idx * W, W))
+                break;
+            ls = (ls + 1) & (LS - 1);
+        }
+        atomicAdd(&lcnt[ls], 1u);
+        atomicMin(&lfst[ls], idx);
+    }
+    __syncthreads();
+    // phase 2a: distinct keys already in the slice (fingerprint + words match; the slice's key
+    // words were written by earlier launches, so they are stable here).  skey is not modified.
+    uint32_t slot[kMwPerThread];
+    uint64_t fps[kMwPerThread];
+#pragma unroll
+    for (uint32_t j = 0; j < kMwPerThread; ++j) {
+        const uint32_t ls = j * T + threadIdx.x;
+        slot[j] = 0xFFFFFFFFu;
+        fps[j] = kEmpty;
+        if (ls >= LS) continue;
+        const unsigned long long lk = lkey[ls];
+        if (lk == kEmpty) continue;
+        const uint64_t* kw = words + (lk & 0xFFFFFFFFull) * W;
+        const uint64_t fp = words_fp(kw, W);
+        fps[j] = fp;
+        uint32_t off = (uint32_t)(slot_top(t, fp) & t.slice_mask);
+        for (uint32_t probe = 0; probe < S; ++probe) {
+            const unsigned long long cur = skey[off];
+            if (cur == kEmpty) break;
+            if (cur == fp && words_eq(t.keywords + (slice_base + off) * W, kw, W)) {
+                slot[j] = off;
+                break;
+            }
+            off = (off + 1) & (uint32_t)t.slice_mask;
+        }
+    }
+    __syncthreads();
+    // phase 2b: new keys claim free slice slots.  Every key that could match was resolved in 2a, and
+    // the LDS entries are distinct keys, so a claimed slot is never a match: skip all non-empty slots.
+    bool fresh[kMwPerThread];
+#pragma unroll
+    for (uint32_t j = 0; j < kMwPerThread; ++j) {
+        fresh[j] = false;
+        if (fps[j] == kEmpty || slot[j] != 0xFFFFFFFFu) continue;
+        uint32_t off = (uint32_t)(slot_top(t, fps[j]) & t.slice_mask);
+        for (uint32_t probe = 0; probe < S; ++probe) {
+            if (skey[off] == kEmpty &&
+                atomicCAS(&skey[off], (unsigned long long)kEmpty, (unsigned long long)fps[j]) == kEmpty) {
+                slot[j] = off;
+                fresh[j] = true;
+                break;
+            }
+            off = (off + 1) & (uint32_t)t.slice_mask;
+        }
+        if (slot[j] == 0xFFFFFFFFu) atomicOr(t.overflow, 1ull);
+    }
+    // phase 3: slot read-modify-writes (the workgroup owns the slice) and key words of new slots
+#pragma unroll
+    for (uint32_t j = 0; j < kMwPerThread; ++j) {
+        if (slot[j] == 0xFFFFFFFFu) continue;
+        const uint32_t ls = j * T + threadIdx.x;
+        Slot* sl = &t.slots[slice_base + slot[j]];
+        const unsigned long long f = base_index + lfst[ls];
+        if (fresh[j]) {
+            const uint64_t* kw = words + (lkey[ls] & 0xFFFFFFFFull) * W;
+            uint64_t* dst = t.keywords + (slice_base + slot[j]) * W;
+            for (uint32_t q = 0; q < W; ++q) dst[q] = kw[q];
+            sl->key = fps[j];
+            sl->ncount = ~(unsigned long long)lcnt[ls];
+            sl->first = f;
+        } else {
+            sl->ncount -= lcnt[ls];
+            if (f < sl->first) sl->first = f;
+        }
+    }
+}
+
 Tbl tbl_of(const ss_counter* c) {
     Tbl t;
     t.slots = c->slots;
+    t.keywords = c->keywords;
+    t.W = c->W;
     t.overflow = c->work;
     t.mask = c->cap - 1;
     t.slice_mask = (1ull << c->slice_log) - 1;
@@ -784,6 +959,7 @@ int ss_counter_destroy(ss_counter* c) {
     if (!c) return SS_OK;
     if (c->slots) (void)hipFree(c->slots);
     if (c->work) (void)hipFree(c->work);
+    if (c->keywords) (void)hipFree(c->keywords);
     ss_counter_release(c);
     if (c->ws_hist) (void)hipFree(c->ws_hist);
     if (c->ws_rstart) (void)hipFree(c->ws_rstart);
@@ -804,9 +980,24 @@ int ss_counter_reset(ss_counter* c, void* stream) {
 uint64_t ss_counter_capacity(const ss_counter* c) { return c ? c->cap : 0; }
 
 static int fix_length(ss_counter* c, uint32_t L) {
-    if (L > 32) return ss_fail(SS_EARG, "GPU counter keys must have L <= 32");
-    if (c->L < 0) c->L = (int32_t)L;
-    if ((uint32_t)c->L != L) return ss_fail(SS_EARG, "all keys of one counter handle must share one length");
+    if (L > SS_MAX_NT) return ss_fail(SS_ETOO_LONG, "Sequences longer than 1024 bases are not supported.");
+    if (c->L >= 0) {
+        if ((uint32_t)c->L != L) return ss_fail(SS_EARG, "all keys of one counter handle must share one length");
+        return SS_OK;
+    }
+    const uint32_t W = L <= 32 ? 1u : (L + 31) / 32;
+    if (W > 1 && c->keywords_W != W) {   // key words of a multi-word table: [cap * W]
+        if (c->keywords) (void)hipFree(c->keywords);
+        c->keywords = nullptr;
+        c->keywords_W = 0;
+        if (hipMalloc((void**)&c->keywords, c->cap * W * sizeof(uint64_t)) != hipSuccess) {
+            ss_check(hipGetLastError(), "counter key words hipMalloc");
+            return ss_fail(SS_ENOMEM, "counter key words: out of device memory");
+        }
+        c->keywords_W = W;
+    }
+    c->W = W;
+    c->L = (int32_t)L;
     return SS_OK;
 }
 
@@ -841,6 +1032,9 @@ int ss_counter_release(ss_counter* c) {
     if (c->ws_akey) (void)hipFree(c->ws_akey);
     if (c->ws_aidx) (void)hipFree(c->ws_aidx);
     if (c->ws_bidx) (void)hipFree(c->ws_bidx);
+    if (c->ws_words) (void)hipFree(c->ws_words);
+    c->ws_words = nullptr;
+    c->ws_words_cap = 0;
     c->ws_keys = nullptr;
     c->ws_akey = nullptr;
     c->ws_aidx = nullptr;
@@ -861,8 +1055,26 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
     if (rc || n == 0) return rc;
     if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
     Tbl t = tbl_of(c);
+    const bool multi = c->W > 1;
     const bool fast = (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
-    if (fast && n <= c->ws_reads) {
+    if (multi) {
+        // multi-word keys: always partitioned; grow the workspace to this batch if needed
+        if (n > c->ws_reads && (rc = ss_counter_reserve(c, n)) != SS_OK) return rc;
+        const uint64_t need = c->ws_reads * c->W;
+        if (c->ws_words_cap < need) {
+            if (c->ws_words) (void)hipFree(c->ws_words);
+            c->ws_words = nullptr;
+            c->ws_words_cap = 0;
+            if (hipMalloc((void**)&c->ws_words, need * sizeof(uint64_t)) != hipSuccess) {
+                ss_check(hipGetLastError(), "counter word workspace hipMalloc");
+                return ss_fail(SS_ENOMEM, "counter word workspace: out of device memory");
+            }
+            c->ws_words_cap = need;
+        }
+        rc = ss_encode_fixed_impl(d_ascii, n, L, stride, c->ws_words, c->W, d_first_bad, nullptr, nullptr, stream);
+        if (rc) return rc;
+    }
+    if (multi || (fast && n <= c->ws_reads)) {
         PartWs w;
         w.keys = c->ws_keys;
         w.akey = c->ws_akey;
@@ -876,17 +1088,25 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         w.rbits = c->log2cap - c->slice_log;
         const uint32_t S = 1u << c->slice_log;
         const size_t agg_lds = (size_t)2 * S * 16 + (size_t)S * 8 + 8;
+        const size_t mw_lds = (size_t)2 * S * 16 + (size_t)S * 8;
         const bool two_pass = w.rbits > kCoarseBits;             // > 64 regions: coarse pass first
         const uint32_t bins1 = two_pass ? (1u << kCoarseBits) : w.R;
-        constexpr int T1 = 512, U1 = 4, TS = 512;
+        constexpr int T1 = 512, U1 = 4, TS = 512, TF = 512;
         // dynamic LDS above the 64 KB default: opt in once per kernel (host-side attribute)
         static bool attrs_set = false;
         if (!attrs_set) {
+            const int agg_max = (int)(2 * (1u << kSliceLogMax) * 16 + (1u << kSliceLogMax) * 8 + 8);
             hipError_t ea = hipFuncSetAttribute((const void*)k_pc_keys<T1, U1>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kMaxRegions * 4);
             if (ea == hipSuccess)
+                ea = hipFuncSetAttribute((const void*)k_mw_fp<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         kMaxRegions * 4);
+            if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_pc_aggregate<kAggT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)(2 * (1u << kSliceLogMax) * 16 + (1u << kSliceLogMax) * 8 + 8));
+                                         agg_max);
+            if (ea == hipSuccess)
+                ea = hipFuncSetAttribute((const void*)k_mw_aggregate<kMwT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         agg_max);
             if (ea != hipSuccess) return ss_check(ea, "hipFuncSetAttribute (dynamic LDS)");
             attrs_set = true;
         }
@@ -896,9 +1116,15 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, bins, start);
             hipLaunchKernelGGL(k_pc_offsets, dim3(g), dim3(256), 0, s, w, bins, (const uint32_t*)start);
         };
-        const size_t keys_lds = (bins1 * (T1 / 64) <= kMaxRegions ? bins1 * (T1 / 64) : bins1) * 4;
-        hipLaunchKernelGGL((k_pc_keys<T1, U1>), dim3(kPartBlocks), dim3(T1), keys_lds, s, t, w, bins1,
-                           (const uint4*)d_ascii, stride / 16, n, L / 16, (unsigned long long*)d_first_bad);
+        if (multi) {
+            const size_t fp_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
+            hipLaunchKernelGGL((k_mw_fp<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1,
+                               (const uint64_t*)c->ws_words, n);
+        } else {
+            const size_t keys_lds = (bins1 * (T1 / 64) <= kMaxRegions ? bins1 * (T1 / 64) : bins1) * 4;
+            hipLaunchKernelGGL((k_pc_keys<T1, U1>), dim3(kPartBlocks), dim3(T1), keys_lds, s, t, w, bins1,
+                               (const uint4*)d_ascii, stride / 16, n, L / 16, (unsigned long long*)d_first_bad);
+        }
         if (two_pass) {
             scan(bins1, w.tot + 0);   // coarse starts are not needed later; tot is reused as scratch
             hipLaunchKernelGGL((k_pc_scatter_lds<true, false>), dim3(kPartBlocks), dim3(512), 0, s, t, w, bins1,
@@ -914,7 +1140,11 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint64_t*)w.keys, (const uint32_t*)nullptr, w.akey, w.bidx, n);
             w.bkey = w.akey;
         }
-        hipLaunchKernelGGL((k_pc_aggregate<kAggT>), dim3(w.R), dim3(kAggT), agg_lds, s, t, w, base_index);
+        if (multi)
+            hipLaunchKernelGGL((k_mw_aggregate<kMwT>), dim3(w.R), dim3(kMwT), mw_lds, s, t, w,
+                               (const uint64_t*)c->ws_words, base_index);
+        else
+            hipLaunchKernelGGL((k_pc_aggregate<kAggT>), dim3(w.R), dim3(kAggT), agg_lds, s, t, w, base_index);
         return ss_check(hipGetLastError(), "partitioned insert");
     }
     if (fast) {
@@ -936,6 +1166,7 @@ int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_le
     if (!c) return ss_fail(SS_EARG, "null counter");
     if (m == 0) return SS_OK;
     if (!d_keys || !d_counts || !d_first) return ss_fail(SS_EARG, "null buffer");
+    if (c->W > 1) return ss_fail(SS_EARG, "ss_counter_merge takes single-word keys (L <= 32)");
     const unsigned grid = grid_for(m, kThreads, 256 * 16);
     hipLaunchKernelGGL(k_merge, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, tbl_of(c), d_keys, d_counts,
                        d_first, m);
@@ -965,10 +1196,9 @@ int ss_counter_overflow(ss_counter* c, uint64_t* d_flag, void* stream) {
                     "overflow copy");
 }
 
-int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens,
-                       uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
-                       void* stream) {
-    if (!c) return ss_fail(SS_EARG, "null counter");
+static int extract_impl(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens, uint64_t* d_words,
+                        uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
+                        void* stream) {
     if (n_parts == 0 || n_parts > kMaxParts) return ss_fail(SS_EARG, "n_parts must be in 1..64");
     if (!d_keys || !d_lens || !d_counts || !d_first || !d_part_counts) return ss_fail(SS_EARG, "null buffer");
     hipStream_t s = (hipStream_t)stream;
@@ -977,8 +1207,26 @@ int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32
     hipLaunchKernelGGL(k_part_count, dim3(kExtractBlocks), dim3(kThreads), 0, s, t, n_parts, bc);
     hipLaunchKernelGGL(k_part_offsets, dim3(1), dim3(1024), 0, s, n_parts, bc, (unsigned long long*)d_part_counts);
     hipLaunchKernelGGL(k_part_scatter, dim3(kExtractBlocks), dim3(kThreads), 0, s, t, n_parts, c->L < 0 ? 0 : c->L,
-                       (const unsigned long long*)bc, d_keys, d_lens, d_counts, d_first, cap, c->work);
+                       (const unsigned long long*)bc, d_keys, d_lens, d_counts, d_first, cap, c->work, d_words);
     return ss_check(hipGetLastError(), "ss_counter_extract");
+}
+
+int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens,
+                       uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
+                       void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->W > 1) return ss_fail(SS_EARG, "multi-word keys (L > 32): use ss_counter_extract_words");
+    return extract_impl(c, n_parts, d_keys, d_lens, nullptr, d_counts, d_first, cap, d_part_counts, stream);
+}
+
+int ss_counter_words(const ss_counter* c) { return c ? (int)c->W : 0; }
+
+int ss_counter_extract_words(ss_counter* c, uint32_t n_parts, uint64_t* d_fps, uint32_t* d_lens,
+                             uint64_t* d_words, uint64_t* d_counts, uint64_t* d_first, uint64_t cap,
+                             uint64_t* d_part_counts, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (!d_words) return ss_fail(SS_EARG, "null buffer");
+    return extract_impl(c, n_parts, d_fps, d_lens, d_words, d_counts, d_first, cap, d_part_counts, stream);
 }
 
 }  // extern "C"

@@ -325,3 +325,48 @@ def test_counter_partitioned_equals_direct(gpu, oracle, cap, U, n):
     assert [int(x) for x in k] == [w[0] for (w, _L, _c, _f) in exp]
     assert list(cnt) == [cc for (_w, _L, cc, _f) in exp]
     c.close()
+
+
+@pytest.mark.parametrize("L,cap,U,n", [(33, 1 << 12, 500, 50_000), (64, 1 << 16, 5000, 200_000),
+                                       (96, 1 << 20, 20_000, 300_000), (100, 1 << 14, 3000, 100_000),
+                                       (150, 1 << 18, 50_000, 200_000), (512, 1 << 13, 800, 30_000),
+                                       (1024, 1 << 12, 300, 10_000)])
+def test_counter_multiword(gpu, oracle, L, cap, U, n):
+    """Multi-word keys (L > 32: ShortSeq192 / ShortSeqVar keys): fingerprint-partitioned insert with
+    word comparison, over three inserts into one table (global first indices), against the oracle
+    on the same reads (keys, counts, first occurrence, dict order).  Pool reads one base apart
+    (same fingerprint region unlikely, same words except one) check the word comparison."""
+    import shortseq_amd.batch as B
+    ascii = B.synth_pool_reads(n, L, 31 + L, 32, U, device=gpu)
+    ascii[5] = ascii[4]
+    ascii[5, L - 1] = ord("A") if int(ascii[4, L - 1]) != ord("A") else ord("C")   # last base differs
+    ascii[6] = ascii[4]
+    ascii[6, 0] = ord("G") if int(ascii[4, 0]) != ord("G") else ord("T")           # first base differs
+    c = B.GpuCounter(cap, device=gpu)
+    third = n // 3
+    for lo, hi in ((0, third), (third, 2 * third), (2 * third, n)):
+        c.insert(ascii[lo:hi], L, base_index=lo)
+    assert c.words == (L + 31) // 32
+    assert not c.overflowed()
+    words, cnt, f = c.items_sorted_words()
+    a = ascii.cpu().numpy().reshape(-1)
+    exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(n)])
+    assert [tuple(int(x) for x in row) for row in words] == [w for (w, _L, _c, _f) in exp]
+    assert list(cnt) == [cc for (_w, _L, cc, _f) in exp]
+    assert list(f) == [ff for (_w, _L, _c, ff) in exp]
+    assert c.size() == len(exp)
+    c.close()
+
+
+def test_counter_multiword_bad_read(gpu):
+    import shortseq_amd.batch as B
+    L, n = 150, 70_000
+    ascii = B.synth_pool_reads(n, L, 3, 4, 100, device=gpu)
+    ascii[40_000, 77] = ord("N")
+    ascii[50_000, 3] = ord("*")
+    c = B.GpuCounter(1 << 12, device=gpu)
+    c.insert(ascii, L, check_errors=False)
+    assert int(B.first_bad_buffer(gpu).item()) == 40_000
+    with pytest.raises(Exception):
+        c.insert(ascii, L)
+    c.close()
