@@ -132,8 +132,9 @@ uint64_t ss_counter_capacity(const ss_counter* c);
 
 /* Reserve workspace (20 B per read + a small per-region table) so inserts of up to max_reads
  * reads take the partitioned path: reads are bucketed by table region and each region is
- * aggregated by one workgroup in LDS (no per-read global atomics).  Host call (allocates); inserts
- * larger than the reservation, or with L not in {16, 32} / unaligned rows, use the direct
+ * aggregated by one workgroup in LDS (no per-read global atomics).  Host call (allocates).  L 16/32
+ * with 16-B aligned rows encode inside the first partition pass; any other L <= 32 / layout is
+ * packed into the workspace first.  Inserts larger than the reservation use the direct
  * atomic-insert kernels.  Requires capacity <= 2^26 (16384 regions).  max_reads < 2^32. */
 int ss_counter_reserve(ss_counter* c, uint64_t max_reads);
 uint64_t ss_counter_reserved(const ss_counter* c);
@@ -184,6 +185,36 @@ int ss_counter_words(const ss_counter* c);
 int ss_counter_extract_words(ss_counter* c, uint32_t n_parts, uint64_t* d_fps, uint32_t* d_lens,
                              uint64_t* d_words, uint64_t* d_counts, uint64_t* d_first, uint64_t cap,
                              uint64_t* d_part_counts, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * FASTQ ingest on the device — replaces _read_fastq_short_seqs (fast_read.pyx:3-20) + _from_chars
+ * (short_seq.pyx:49-52) as called by read_and_count_fastq (counter.pyx:57-70): lines split at '\n',
+ * 0-based line j kept iff j % 4 == 1, length = strlen(line) - 1 (the '\n' dropped; a final line
+ * without '\n' loses its last character; an embedded NUL ends the line).
+ * A chunk is < 4 GiB, starts at a line boundary and ends right after a '\n' (or at EOF: at_eof != 0);
+ * line0 = lines before the chunk.  d_buf 16-B aligned.
+ *   1. ss_fastq_scan: newlines per 16-KiB tile + scan into d_ws (ss_fastq_scan_ws_bytes(nbytes)
+ *      bytes); *d_nlines = newlines in the chunk.
+ *   2. ss_fastq_index (same d_ws): d_offsets[i] / d_lens[i] of sequence line i (chunk-relative),
+ *      *d_nreads = sequence lines in the chunk (may exceed max_reads: then only max_reads are
+ *      written; size max_reads from *d_nlines: at most nlines / 4 + 1).  d_aux: max_reads u64 of
+ *      scratch.  d_lens[i] = 0xFFFFFFFF where strlen is 0 (the reference's size_t underflow, i.e.
+ *      the too-long error); > 1024 is the too-long error as well.
+ * The (d_offsets, d_lens) pair is the ragged layout of ss_encode_var and ss_gather_rows.
+ * ---------------------------------------------------------------------------------------------- */
+uint64_t ss_fastq_scan_ws_bytes(uint64_t nbytes);
+int ss_fastq_scan(const uint8_t* d_buf, uint64_t nbytes, void* d_ws, uint64_t ws_bytes, uint64_t* d_nlines,
+                  void* stream);
+int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, const void* d_ws,
+                   uint64_t* d_offsets, uint32_t* d_lens, uint64_t* d_aux, uint64_t max_reads,
+                   uint64_t* d_nreads, void* stream);
+
+/* Gather ragged rows into a dense batch: dst row r = d_src[d_offsets[s] .. + L) with s = d_sel[r]
+ * (or r when d_sel is NULL); dst_stride % 16 == 0, >= round_up(L, 16); d_dst 16-B aligned; bytes of
+ * the last 16-B chunk past L are 'A'.  Reads of d_src stay below src_bytes.  Feeds one length
+ * group of a ragged batch (FASTQ, ShortSeqCounter lists) to the fixed-length encode / counter. */
+int ss_gather_rows(const uint8_t* d_src, uint64_t src_bytes, const uint64_t* d_offsets, const uint64_t* d_sel,
+                   uint64_t m, uint32_t L, uint8_t* d_dst, uint64_t dst_stride, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):

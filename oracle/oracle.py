@@ -61,6 +61,8 @@ def lib():
         L.ora_gen_pool_reads.argtypes = [U64, U64, U64, U64, U64, U32, U64, P]
         L.ora_count.argtypes = [P, P, P, U64, P, P, P, P, C.POINTER(OraErr)]
         L.ora_count.restype = I64
+        L.ora_fastq_index.argtypes = [P, U64, P, P, U64]
+        L.ora_fastq_index.restype = U64
         _lib = L
     return _lib
 
@@ -220,3 +222,13 @@ def ref_encode_batch(ascii: np.ndarray, n: int, L: int, wpr: int | None = None) 
     else:
         plib().ref_encode_array_batch(par, _p(ascii), n, L, L, _p(out), wpr)
     return out.reshape(n, wpr)
+
+
+def fastq_index(data: bytes):
+    """(offsets u64, lens u32) of the kept sequence lines (fast_read.pyx:3-20 rule)."""
+    buf = np.frombuffer(data, dtype=np.uint8)
+    n = lib().ora_fastq_index(buf.ctypes.data, len(buf), None, None, 0)
+    offs = np.zeros(n, dtype=np.uint64)
+    lens = np.zeros(n, dtype=np.uint32)
+    lib().ora_fastq_index(buf.ctypes.data, len(buf), offs.ctypes.data, lens.ctypes.data, n)
+    return offs, lens

@@ -264,3 +264,32 @@ int64_t ora_count(const uint8_t* ascii, const uint64_t* offsets, const uint32_t*
     free(table);
     return nu;
 }
+
+/* ------------------------------------------------------------------------------------------------
+ * FASTQ sequence-line selection (test infrastructure; restates fast_read.pyx:3-20 and
+ * short_seq.pyx:49-52 as a plain scalar loop).  getline() semantics: a line is everything up to and
+ * including '\n', the last line may lack it.  count starts at 1; kept iff count % 2 == 0 and
+ * count % 4 != 0.  len = strlen(line) - 1, strlen stopping at the first NUL of the line buffer.
+ * lens[i] = 0xFFFFFFFF when strlen is 0 (size_t underflow in the reference).  Returns the number of
+ * kept lines (only the first `cap` are written).
+ * ---------------------------------------------------------------------------------------------- */
+uint64_t ora_fastq_index(const uint8_t* buf, uint64_t nbytes, uint64_t* offsets, uint32_t* lens, uint64_t cap) {
+    uint64_t pos = 0, count = 1, kept = 0;
+    while (pos < nbytes) {                                  /* getline returns -1 at EOF */
+        uint64_t end = pos;
+        while (end < nbytes && buf[end] != '\n') ++end;
+        const uint64_t line_len = (end < nbytes) ? end - pos + 1 : end - pos;   /* incl. '\n' */
+        if (count % 2 == 0 && count % 4 != 0) {
+            uint64_t slen = 0;
+            while (slen < line_len && buf[pos + slen] != 0) ++slen;
+            if (kept < cap) {
+                offsets[kept] = pos;
+                lens[kept] = slen == 0 ? 0xFFFFFFFFu : (uint32_t)(slen - 1 > 0xFFFFFFFEu ? 0xFFFFFFFEu : slen - 1);
+            }
+            ++kept;
+        }
+        ++count;
+        pos += line_len;
+    }
+    return kept;
+}

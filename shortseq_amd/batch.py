@@ -29,7 +29,7 @@ _NO_BAD = -1  # UINT64_MAX viewed as int64
 
 __all__ = ["words_for", "wpr_for", "encode", "encode_var", "decode", "decode_var", "hamming_ref",
            "hamming_pair", "encode_hamming_ref", "synth_reads", "synth_pool_reads", "GpuCounter",
-           "raise_read_error", "first_bad_buffer"]
+           "raise_read_error", "first_bad_buffer", "fastq_index", "gather_rows"]
 
 
 def words_for(L: int) -> int:
@@ -258,6 +258,57 @@ def synth_pool_reads(n: int, L: int, seed: int, pool_seed: int, U: int, *, i0: i
         out = torch.empty((n, L), dtype=torch.uint8, device=dev)
     check(lib().ss_synth_pool_reads(out.data_ptr(), seed, pool_seed, U, i0, n, L, L, _stream(dev)),
           "ss_synth_pool_reads")
+    return out
+
+
+LEN_UNDERFLOW = 0xFFFFFFFF   # ss_fastq_index: strlen 0 (the reference's size_t underflow -> too long)
+
+
+def fastq_index(buf: torch.Tensor, nbytes: Optional[int] = None, *, line0: int = 0, at_eof: bool = True):
+    """Sequence lines of a FASTQ chunk resident on the device (fast_read.pyx:3-20 rule, see
+    include/shortseq_amd.h ss_fastq_index) -> (offsets int64 [n], lens int64 [n], newlines).
+    lens holds the reference's strlen - 1 (LEN_UNDERFLOW where strlen is 0).  The chunk must start
+    at a line boundary and end right after a newline unless at_eof."""
+    _require_cuda(buf, "buf")
+    if buf.dtype != torch.uint8:
+        raise TypeError("buf must be a uint8 tensor")
+    nbytes = buf.numel() if nbytes is None else nbytes
+    dev = buf.device
+    L_ = lib()
+    s = _stream(dev)
+    ws_bytes = int(L_.ss_fastq_scan_ws_bytes(nbytes))
+    ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.int64, device=dev)
+    cnt = torch.empty(2, dtype=torch.int64, device=dev)
+    check(L_.ss_fastq_scan(buf.data_ptr(), nbytes, ws.data_ptr(), ws_bytes, cnt.data_ptr(), s), "ss_fastq_scan")
+    nl = int(cnt[0].item())
+    cap = nl // 4 + 2
+    offs = torch.empty(cap, dtype=torch.int64, device=dev)
+    lens = torch.empty(cap, dtype=torch.int32, device=dev)
+    aux = torch.empty(cap, dtype=torch.int64, device=dev)
+    check(L_.ss_fastq_index(buf.data_ptr(), nbytes, line0, 1 if at_eof else 0, ws.data_ptr(), offs.data_ptr(),
+                            lens.data_ptr(), aux.data_ptr(), cap, cnt[1:].data_ptr(), s), "ss_fastq_index")
+    n = int(cnt[1].item())
+    if n > cap:
+        raise AssertionError("FASTQ index capacity exceeded")
+    return offs[:n], lens[:n].to(torch.int64) & 0xFFFFFFFF, nl
+
+
+def gather_rows(src: torch.Tensor, offsets: torch.Tensor, L: int, *, sel: Optional[torch.Tensor] = None,
+                src_bytes: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Dense [m, round_up(L, 16)] uint8 rows gathered from a ragged byte buffer on the device:
+    row r = src[offsets[sel[r]] : + L] (sel None: r).  Feeds one length group of a ragged batch to the
+    fixed-length kernels."""
+    _require_cuda(src, "src")
+    _require_cuda(offsets, "offsets")
+    if offsets.dtype != torch.int64 or (sel is not None and sel.dtype != torch.int64):
+        raise TypeError("offsets / sel must be int64 tensors")
+    m = (sel if sel is not None else offsets).numel()
+    S = (L + 15) // 16 * 16
+    if out is None:
+        out = torch.empty((m, S), dtype=torch.uint8, device=src.device)
+    src_bytes = src.numel() if src_bytes is None else src_bytes
+    check(lib().ss_gather_rows(src.data_ptr(), src_bytes, offsets.data_ptr(), _ptr(sel), m, L, out.data_ptr(),
+                               out.shape[1] if out.dim() == 2 else S, _stream(src.device)), "ss_gather_rows")
     return out
 
 

@@ -428,20 +428,25 @@ cdef class ShortSeqCounter(dict):
             dict.__setitem__(self, seq, dict.get(self, seq, 0) + 1)
 
 
-def _count_batch_gpu(ShortSeqCounter self, list reads, device):
-    """Batch path: stage the reads, count each length group on the GPU (one table per length: the
-    length is part of the key, short_seq_64.pyx:41-44), rebuild the dict in first-occurrence order.
-    Reads longer than 1024 nt go through the host loop, which raises the reference's error."""
-    import numpy as np
+def _resolve_device(device):
     import torch
-    from . import batch as B
+    if device in ("auto", "cuda"):
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(device)
+
+
+def _count_batch_gpu(ShortSeqCounter self, list reads, device):
+    """Batch path (shortseq_amd/ingest.py): the reads are joined into one pinned buffer, copied up
+    once, split by length on the device (the length is part of the key, short_seq_64.pyx:41-44),
+    each length group gathered densely and counted by one GPU table; the dict is rebuilt in
+    first-occurrence order.  The first rejected read in list order raises the reference's error."""
+    import numpy as np
+    from . import ingest
 
     cdef Py_ssize_t i, n = PyList_GET_SIZE(reads)
     cdef object item
-    cdef uint64_t[:, ::1] kv
     lens_np = np.empty(n, dtype=np.int64)
     cdef int64_t[:] lens = lens_np
-    cdef int64_t total = 0
     for i in range(n):
         item = <object>PyList_GET_ITEM(reads, i)
         if not PyBytes_CheckExact(item):
@@ -449,62 +454,23 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, device):
             _raise_first_error(reads, i)
             raise TypeError(f"expected bytes, {type(item).__name__} found")
         lens[i] = PyBytes_GET_SIZE(item)
-        total += lens[i]
-    blob_np = np.frombuffer(b"".join(reads), dtype=np.uint8) if total else np.zeros(0, np.uint8)
-    offs_np = np.zeros(n, dtype=np.int64)
-    if n:
-        np.cumsum(lens_np[:-1], out=offs_np[1:])
-    dev = torch.device("cuda", torch.cuda.current_device()) if device in ("auto", "cuda") else torch.device(device)
+    gc = ingest.count_list(reads, lens_np, _resolve_device(device))
+    _fill_from_groups(self, gc)
 
+
+cdef _fill_from_groups(ShortSeqCounter self, gc):
+    """Insert the per-length GPU results into the dict in first-occurrence (= reference) order."""
+    import numpy as np
+    cdef uint64_t[:, ::1] kv
+    cdef Py_ssize_t k
+    groups, (ecount, efirst) = gc.finish()
     entries = []                      # (first_index, key_object, count)
-    first_bad = n                     # smallest invalid read index seen on any path
-    for L in np.unique(lens_np):
-        L = int(L)
-        idx = np.nonzero(lens_np == L)[0]
-        if L == 0:
-            entries.append((int(idx[0]), empty, int(len(idx))))
-            continue
-        if L > C_MAX_VAR:
-            sub = ShortSeqCounter(device="host")
-            firsts = {}
-            for j in idx:
-                item = <object>PyList_GET_ITEM(reads, j)
-                try:
-                    seq = _from_py_bytes(item)
-                except BaseException:
-                    first_bad = min(first_bad, int(j))
-                    break
-                if seq not in firsts:
-                    firsts[seq] = int(j)
-                dict.__setitem__(sub, seq, dict.get(sub, seq, 0) + 1)
-            for seq, c in dict.items(sub):
-                entries.append((firsts[seq], seq, c))
-            continue
-        host = torch.empty(len(idx) * L, dtype=torch.uint8).pin_memory()   # pinned staging
-        if len(idx) == n:
-            host.numpy()[:] = blob_np
-        else:
-            rows = (offs_np[idx][:, None] + np.arange(L)[None, :]).reshape(-1)
-            host.numpy()[:] = blob_np[rows]
-        d_ascii = host.to(dev, non_blocking=True).view(-1, L)
-        cnt = B.GpuCounter(max(1024, 2 * len(idx)), device=dev)
-        try:
-            cnt.insert(d_ascii, L, base_index=0, check_errors=False)
-            fb = int(B.first_bad_buffer(dev).item())
-            if fb != -1:
-                first_bad = min(first_bad, int(idx[fb]))
-                continue
-            keys, counts, firsts = cnt.items_sorted_words()
-        finally:
-            cnt.close()
-        gfirst = idx[firsts.astype(np.int64)]
-        keys = np.ascontiguousarray(keys, dtype=np.uint64)
-        kv = keys
-        for k in range(len(keys)):
-            entries.append((int(gfirst[k]), _from_words(&kv[k, 0], L), int(counts[k])))
-    if first_bad < n:
-        _raise_first_error(reads, first_bad + 1)
-        raise AssertionError("GPU flagged a read the host codec accepts")
+    if ecount:
+        entries.append((efirst, empty, ecount))
+    for L, words, counts, firsts in groups:
+        kv = words
+        for k in range(words.shape[0]):
+            entries.append((int(firsts[k]), _from_words(&kv[k, 0], L), int(counts[k])))
     entries.sort(key=lambda e: e[0])
     for _f, key, c in entries:
         dict.__setitem__(self, key, c)
@@ -524,7 +490,17 @@ def _raise_first_error(list reads, Py_ssize_t upto):
 
 def read_and_count_fastq(filename, device="auto"):
     """counter.pyx:57-70 + fast_read.pyx:3-20: keep line 2 of every 4 lines; each kept line loses
-    exactly its last character (strlen - 1, short_seq.pyx:50-52); prints the reference's timings."""
+    exactly its last character (strlen - 1, short_seq.pyx:50-52); prints the reference's timings.
+    device "auto" (a GPU when present) / "cuda[:N]": the file is streamed to HBM in pinned chunks
+    and indexed, split by length and counted there (shortseq_amd/ingest.py); "host": the
+    reference's per-line loop."""
+    if device != "host":
+        use_gpu = True
+        if device == "auto":
+            import torch
+            use_gpu = torch.cuda.is_available()
+        if use_gpu:
+            return _read_and_count_fastq_gpu(filename, device)
     cdef FILE* f
     cdef char* line = NULL
     cdef size_t cap = 0
@@ -552,7 +528,23 @@ def read_and_count_fastq(filename, device="auto"):
         fclose(f)
         free(line)
     t2 = time.time()
-    counts = ShortSeqCounter(seqs, device=device)
+    counts = ShortSeqCounter(seqs, device="host")
     t3 = time.time()
     print(f"{t2-t1:.2f}s to read {len(seqs)} total seqs, and {t3 - t2:.2f}s to count {len(counts)} unique sequences")
+    return counts
+
+
+def _read_and_count_fastq_gpu(filename, device):
+    import os
+    from . import ingest
+    fname = filename.encode("utf-8")
+    if not os.path.isfile(filename):
+        raise Exception(f"{str(fname)}: Something went wrong while reading this file.")
+    t1 = time.time()
+    gc, nseqs = ingest.count_fastq(filename, _resolve_device(device))
+    t2 = time.time()
+    counts = ShortSeqCounter()
+    _fill_from_groups(counts, gc)
+    t3 = time.time()
+    print(f"{t2-t1:.2f}s to read {nseqs} total seqs, and {t3 - t2:.2f}s to count {len(counts)} unique sequences")
     return counts

@@ -398,7 +398,8 @@ void launch_decode_g16(const uint32_t* w32, uint32_t wpr2, uint64_t n, uint32_t 
 // Production shapes
 constexpr int kEncT = 768, kEncU = 2;        // dense encode (32 / 64.. / 512 / 1024 nt)
 constexpr bool kEncXcd = false, kEncNtSt = true;
-constexpr int kHamT = 768, kHamU = 2;        // fused encode + hamming (dense, LDS reduction)
+constexpr int kHamT = 192, kHamU = 4;        // fused encode + hamming (dense, LDS reduction): 768-chunk
+                                             // blocks, 128 whole 96-nt reads (tools/tune_stream.hip)
 constexpr int kDecT = 256, kDecU = 2;        // decode
 constexpr bool kDecNtLd = false, kDecNtSt = false;
 
@@ -424,8 +425,12 @@ void launch_encode_fast(const G16Args& a, bool dense, bool ham, uint32_t L, hipS
 // ==================================================================================================
 extern "C" {
 
+// The first-bad slot is reset by a stream write packet (no fill-kernel dispatch in front of every
+// encode); hipMemsetAsync only where the runtime refuses the write packet.
 static int reset_first_bad(uint64_t* d_first_bad, hipStream_t s) {
     if (!d_first_bad) return SS_OK;
+    if (hipStreamWriteValue64(s, d_first_bad, ~0ull, 0) == hipSuccess) return SS_OK;
+    (void)hipGetLastError();
     return ss_check(hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s), "reset first_bad");
 }
 

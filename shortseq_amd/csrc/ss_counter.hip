@@ -435,6 +435,27 @@ __global__ __launch_bounds__(T) void k_pc_keys(Tbl t, PartWs w, uint32_t bins, c
     }
 }
 
+// P1 for already-packed single-word keys (any L <= 32, any stride: the batch was packed into
+// w.keys by ss_encode_fixed first): the same per-block histogram over the same block ranges.
+template <int T>
+__global__ __launch_bounds__(T) void k_pc_hist(Tbl t, PartWs w, uint32_t bins, uint64_t n) {
+    extern __shared__ uint32_t hist[];
+    constexpr uint32_t kWaves = T / 64;
+    const uint32_t copies = bins * kWaves <= kMaxRegions ? kWaves : 1u;
+    uint32_t* my = hist + (copies > 1 ? (threadIdx.x >> 6) * bins : 0u);
+    for (uint32_t i = threadIdx.x; i < bins * copies; i += T) hist[i] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
+    for (uint64_t r = lo + threadIdx.x; r < hi; r += T) atomicAdd(&my[bin_of<true>(t, w, w.keys[r])], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < bins; i += T) {
+        uint32_t sum = 0;
+        for (uint32_t c = 0; c < copies; ++c) sum += hist[c * bins + i];
+        w.hist[(uint64_t)blockIdx.x * bins + i] = sum;
+    }
+}
+
 // per-block histogram of region ids over a coarse-bucketed key array (second pass).  The block's
 // range spans few coarse buckets, so the histogram covers only that window of regions (as in
 // k_pc_scatter_lds); a wider span counts straight into the global row.
@@ -1074,7 +1095,14 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         rc = ss_encode_fixed_impl(d_ascii, n, L, stride, c->ws_words, c->W, d_first_bad, nullptr, nullptr, stream);
         if (rc) return rc;
     }
-    if (multi || (fast && n <= c->ws_reads)) {
+    // single-word keys of any other length / layout: pack into the key workspace first, then the
+    // same partitioned passes (k_pc_hist replaces the fused encode of k_pc_keys)
+    const bool packed_keys = !multi && !fast && n <= c->ws_reads;
+    if (packed_keys) {
+        rc = ss_encode_fixed_impl(d_ascii, n, L, stride, c->ws_keys, 1, d_first_bad, nullptr, nullptr, stream);
+        if (rc) return rc;
+    }
+    if (multi || packed_keys || (fast && n <= c->ws_reads)) {
         PartWs w;
         w.keys = c->ws_keys;
         w.akey = c->ws_akey;
@@ -1099,6 +1127,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipError_t ea = hipFuncSetAttribute((const void*)k_pc_keys<T1, U1>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kMaxRegions * 4);
             if (ea == hipSuccess)
+                ea = hipFuncSetAttribute((const void*)k_pc_hist<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         kMaxRegions * 4);
+            if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_mw_fp<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          kMaxRegions * 4);
             if (ea == hipSuccess)
@@ -1120,6 +1151,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             const size_t fp_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             hipLaunchKernelGGL((k_mw_fp<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1,
                                (const uint64_t*)c->ws_words, n);
+        } else if (packed_keys) {
+            const size_t h_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
+            hipLaunchKernelGGL((k_pc_hist<TF>), dim3(kPartBlocks), dim3(TF), h_lds, s, t, w, bins1, n);
         } else {
             const size_t keys_lds = (bins1 * (T1 / 64) <= kMaxRegions ? bins1 * (T1 / 64) : bins1) * 4;
             hipLaunchKernelGGL((k_pc_keys<T1, U1>), dim3(kPartBlocks), dim3(T1), keys_lds, s, t, w, bins1,

@@ -1,0 +1,213 @@
+"""Ragged read streams on the GPU: ShortSeqCounter lists and FASTQ files.
+
+The reference counts a list of reads (counter.pyx:22-39) or the sequence lines of a FASTQ file
+(counter.pyx:57-70 + fast_read.pyx:3-20) one Python object at a time.  Here the reads stay one
+byte buffer in HBM plus (offsets, lens):
+
+  * FASTQ: the file is streamed in pinned chunks that end after a newline; ss_fastq_scan /
+    ss_fastq_index find the sequence lines on the device (batch.fastq_index).
+  * list: the bytes objects are joined once into a pinned buffer and copied up once.
+
+Reads are then split by length (the length is part of the dict key, short_seq_64.pyx:41-44;
+short_seq_192.pyx:35-41), each length group gathered into a dense batch on the device
+(ss_gather_rows) and counted by one GPU table per length (batch.GpuCounter).  The result is a list
+of per-length groups (packed words, counts, global first-occurrence index) from which the Cython
+front rebuilds the dict in first-occurrence order.
+
+Errors follow the reference: the FIRST bad read in input order decides the exception (an invalid
+base, or a read longer than 1024 nt), raised only after every read before it was checked.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+
+from . import batch as B
+
+MAX_NT = B.MAX_NT
+TOO_LONG_MSG = f"Sequences longer than {MAX_NT} bases are not supported."   # short_seq.pyx:74
+
+
+def _pow2_at_least(x: int) -> int:
+    return 1 << max(10, int(x - 1).bit_length())
+
+
+class LengthGroupCounter:
+    """One GpuCounter per read length over a ragged stream.  Every read gets a global index (its
+    position in the stream); `first` indices returned by finish() are global."""
+
+    MAX_TABLE = 1 << 26      # the partitioned insert's largest table (ss_counter_reserve)
+
+    def __init__(self, device: torch.device, expected_reads: Optional[int] = None):
+        self.device = device
+        self.expected = expected_reads
+        self.tables: dict[int, B.GpuCounter] = {}
+        self.rows: dict[int, list] = {}          # L -> [global index arrays of the rows inserted]
+        self.nrows: dict[int, int] = {}
+        self.empty_count = 0
+        self.empty_first: Optional[int] = None
+        self.bad_index: Optional[int] = None     # smallest global index of a rejected read
+        self.bad_read: Optional[bytes] = None    # its bytes (None: too long)
+
+    def _flag(self, gidx: int, read: Optional[bytes]) -> None:
+        if self.bad_index is None or gidx < self.bad_index:
+            self.bad_index, self.bad_read = gidx, read
+
+    def _table(self, L: int, m: int) -> B.GpuCounter:
+        t = self.tables.get(L)
+        if t is None:
+            want = max(m, self.expected or 0)
+            t = B.GpuCounter(min(self.MAX_TABLE, _pow2_at_least(2 * want)), device=self.device)
+            self.tables[L] = t
+            self.rows[L] = []
+            self.nrows[L] = 0
+        return t
+
+    def add(self, src: torch.Tensor, src_bytes: int, offsets: torch.Tensor, lens_np: np.ndarray, base: int,
+            fetch: Callable[[int], bytes]) -> None:
+        """Count reads i (global index base + i): src[offsets[i] : + lens_np[i]] on the device.
+        fetch(i) returns read i's bytes (only called for a rejected read)."""
+        lens_np = np.asarray(lens_np, dtype=np.int64)
+        if lens_np.size == 0:
+            return
+        order = np.argsort(lens_np, kind="stable")
+        sl = lens_np[order]
+        cuts = np.flatnonzero(np.diff(sl)) + 1
+        for grp in np.split(order, cuts):
+            L = int(lens_np[grp[0]])
+            if self.bad_index is not None and base + int(grp[0]) > self.bad_index:
+                continue                                  # nothing here can come first any more
+            if L == 0:
+                self.empty_count += len(grp)
+                f = base + int(grp[0])
+                self.empty_first = f if self.empty_first is None else min(self.empty_first, f)
+                continue
+            if L > MAX_NT:
+                self._flag(base + int(grp[0]), None)
+                continue
+            m = len(grp)
+            sel = torch.from_numpy(grp.astype(np.int64)).to(self.device, non_blocking=True)
+            dense = B.gather_rows(src, offsets, L, sel=sel, src_bytes=src_bytes)
+            t = self._table(L, m)
+            row0 = self.nrows[L]
+            t.insert(dense, L, base_index=row0, check_errors=False)
+            fb = int(B.first_bad_buffer(self.device).item())
+            if fb != -1:
+                i = int(grp[fb])
+                self._flag(base + i, fetch(i))
+            self.rows[L].append(base + grp)
+            self.nrows[L] = row0 + m
+
+    def raise_if_bad(self) -> None:
+        if self.bad_index is None:
+            return
+        if self.bad_read is None:
+            e = Exception(TOO_LONG_MSG)
+            e.read_index = self.bad_index
+            raise e
+        B.raise_read_error(self.bad_read, self.bad_index)
+
+    def finish(self):
+        """-> (groups, empty) with groups = [(L, words u64 [m, W], counts, first_global)] and empty =
+        (count, first_global) of the zero-length reads (count 0 if none).  Raises the reference's
+        exception first if a read was rejected."""
+        try:
+            self.raise_if_bad()
+            groups = []
+            for L, t in self.tables.items():
+                words, counts, firsts = t.items_sorted_words()
+                gidx = np.concatenate(self.rows[L])
+                groups.append((L, np.ascontiguousarray(words, dtype=np.uint64), counts, gidx[firsts.astype(np.int64)]))
+            return groups, (self.empty_count, self.empty_first)
+        finally:
+            self.close()
+
+    def close(self) -> None:
+        for t in self.tables.values():
+            t.close()
+        self.tables = {}
+
+
+def count_list(reads: list, lens_np: np.ndarray, device: torch.device) -> "LengthGroupCounter":
+    """ShortSeqCounter(list_of_bytes) on the GPU: one pinned join, one H2D copy."""
+    gc = LengthGroupCounter(device)
+    n = len(reads)
+    total = int(lens_np.sum())
+    if n == 0:
+        return gc
+    host = torch.empty(max(total, 1), dtype=torch.uint8).pin_memory()
+    if total:
+        host.numpy()[:total] = np.frombuffer(b"".join(reads), dtype=np.uint8)
+    src = host.to(device, non_blocking=True)
+    offs_np = np.zeros(n, dtype=np.int64)
+    np.cumsum(lens_np[:-1], out=offs_np[1:])
+    offs = torch.from_numpy(offs_np).to(device, non_blocking=True)
+    gc.add(src, total, offs, lens_np, 0, lambda i: bytes(reads[i]))
+    return gc
+
+
+DEFAULT_CHUNK = 1 << 30
+
+
+def count_fastq(path: str, device: torch.device, chunk_bytes: int = DEFAULT_CHUNK):
+    """read_and_count_fastq on the GPU: -> (LengthGroupCounter, number of sequence lines)."""
+    size = os.path.getsize(path)
+    cap = max(16, min(chunk_bytes, size + 16))
+    if cap >= (1 << 32):
+        raise ValueError("chunk_bytes must be < 4 GiB")
+    pinned = torch.empty(cap, dtype=torch.uint8).pin_memory()
+    hv = pinned.numpy()
+    dbuf = torch.empty(cap, dtype=torch.uint8, device=device)
+    est_reads = None
+    gc = LengthGroupCounter(device)
+    line0 = read0 = carry = 0
+    with open(path, "rb") as f:
+        while True:
+            got = f.readinto(memoryview(hv)[carry:])
+            n = carry + got
+            at_eof = got == 0 or f.tell() >= size
+            if n == 0:
+                break
+            if at_eof:
+                use = n
+            else:
+                use = 0
+                lo = n
+                while use == 0 and lo > 0:            # last newline of the chunk, searched backwards
+                    a = max(0, lo - (1 << 20))
+                    k = hv[a:lo].tobytes().rfind(b"\n")
+                    if k >= 0:
+                        use = a + k + 1
+                    lo = a
+                if use == 0:                          # one line fills the chunk: grow the buffers
+                    if 2 * cap >= (1 << 32):
+                        raise ValueError("a FASTQ line is longer than 2 GiB")
+                    cap *= 2
+                    grown = torch.empty(cap, dtype=torch.uint8).pin_memory()
+                    grown.numpy()[:n] = hv[:n]
+                    pinned, hv = grown, grown.numpy()
+                    dbuf = torch.empty(cap, dtype=torch.uint8, device=device)
+                    carry = n
+                    continue
+            dbuf[:use].copy_(pinned[:use], non_blocking=True)
+            offs, lens, nl = B.fastq_index(dbuf, use, line0=line0, at_eof=at_eof)
+            lens_np = lens.cpu().numpy()
+            if est_reads is None and not at_eof:
+                est_reads = int(len(lens_np) * size / max(1, use)) + 1
+                gc.expected = est_reads
+
+            def fetch(i, _o=offs, _l=lens_np):
+                o = int(_o[i].item())
+                return dbuf[o:o + int(_l[i])].cpu().numpy().tobytes()
+
+            gc.add(dbuf, use, offs, lens_np, read0, fetch)
+            read0 += len(lens_np)
+            line0 += nl
+            if at_eof or gc.bad_index is not None:
+                break
+            carry = n - use
+            hv[:carry] = hv[use:n].copy()
+    return gc, read0

@@ -183,6 +183,58 @@ def counter_cases(rng):
     return cases
 
 
+def fastq_files(rng):
+    """FASTQ inputs (bytes) for read_and_count_fastq (counter.pyx:57-70 / fast_read.pyx:3-20)."""
+    def rec(i, seq, nl=b"\n"):
+        return b"@r%d" % i + nl + seq + nl + b"+" + nl + b"I" * len(seq) + nl
+    files = {}
+    files["basic_no_trailing_newline"] = b"".join(rec(i, s) for i, s in enumerate(
+        [b"ACGT", b"ACGT", b"GGGGA", b"T" * 40, b"ACGT"])) + b"@last\nACGTA"
+    mixed = [b"", b"A", b"C" * 32, b"G" * 33, b"ACGT" * 24, b"T" * 97, b"ACG" * 67, b"A", b""]
+    files["mixed_lengths"] = b"".join(rec(i, s) for i, s in enumerate(mixed + mixed[::-1]))
+    files["crlf"] = b"".join(rec(i, s, b"\r\n") for i, s in enumerate([b"ACGT", b"GGCC"]))
+    files["nul_inside"] = rec(0, b"ACGT") + b"@n\nGG\x00TT\n+\nIIIII\n" + rec(2, b"GG")
+    files["nul_first"] = rec(0, b"ACGT") + b"@n\n\x00ACGT\n+\nIIIII\n"
+    files["invalid_base"] = rec(0, b"ACGT") + rec(1, b"ACGNT") + rec(2, b"AC")
+    files["invalid_base_long"] = rec(0, b"ACGT" * 20) + rec(1, b"ACGT" * 10 + b"N" + b"ACGT" * 10)
+    files["too_long"] = rec(0, b"ACGT") + rec(1, b"A" * 1025)
+    files["max_len"] = rec(0, b"ACGT" * 256) + rec(1, b"ACGT" * 256) + rec(2, b"G" * 1024)
+    files["truncated_record"] = rec(0, b"ACGT") + b"@r1\nGGTT\n"
+    files["header_only_tail"] = rec(0, b"ACGT") + b"@r1\n"
+    files["empty_file"] = b""
+    files["seq_no_newline_single"] = b"@r0\nA"
+    pool = [bytes(rng.choice(b"ACGT") for _ in range(rng.choice([20, 32, 50, 100]))) for _ in range(50)]
+    files["pool_2000"] = b"".join(rec(i, rng.choice(pool)) for i in range(2000))
+    return files
+
+
+def fastq_cases(rng):
+    import contextlib
+    import io
+    import tempfile
+    cases = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, data in fastq_files(rng).items():
+            path = os.path.join(td, name + ".fq")
+            with open(path, "wb") as f:
+                f.write(data)
+            case = {"file_hex": data.hex()}
+            try:
+                with contextlib.redirect_stdout(io.StringIO()):
+                    c = refcounter.read_and_count_fastq(path)
+                items = []
+                for k, v in c.items():
+                    cls, ws, L = packed_words(k)
+                    items.append({"class": cls, "words": hexw(ws), "length": L, "str": str(k), "count": v})
+                case["items"] = items
+                case["raises"] = None
+            except BaseException as e:  # noqa: BLE001
+                case["raises"] = type(e).__name__
+                case["message"] = str(e)
+            cases[name] = case
+    return cases
+
+
 def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
@@ -221,6 +273,16 @@ def digests():
 
 
 def main():
+    if "--only-fastq" in sys.argv:
+        # add / refresh the FASTQ cases without regenerating the other fixtures
+        path = os.path.join(OUT, "golden_cases.json")
+        with open(path) as f:
+            data = json.load(f)
+        data["fastq"] = fastq_cases(random.Random(20260101))
+        with open(path, "w") as f:
+            json.dump(data, f, indent=0, sort_keys=True)
+        print("wrote fastq cases to", path)
+        return
     rng = random.Random(20250216)
     data = {
         "provenance": {"reference": "/root/reference (AlexTate/ShortSeq snapshot 2025-02-16)",
@@ -229,6 +291,7 @@ def main():
         "aliased": aliased(rng),
         "errors": errors(rng),
         "counter": counter_cases(rng),
+        "fastq": fastq_cases(random.Random(20260101)),
     }
     with open(os.path.join(OUT, "golden_cases.json"), "w") as f:
         json.dump(data, f, indent=0, sort_keys=True)

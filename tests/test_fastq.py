@@ -1,0 +1,238 @@
+"""FASTQ ingest: read_and_count_fastq (counter.pyx:57-70, fast_read.pyx:3-20).
+
+Golden cases: tests/golden/golden_cases.json["fastq"], the unmodified reference's
+read_and_count_fastq on each file (tests/golden/gen_golden.py --only-fastq).  The reference keys
+ShortSeqVar objects by heap pointer, so equal reads > 96 nt stay separate entries
+there; this build merges them by content (documented deviation), and the expected items are the
+golden items merged the same way (counts summed, first occurrence kept).
+
+CPU: the oracle's line selection (oracle/ss_oracle.c ora_fastq_index) + counter oracle reproduce
+the golden items; the host front does too.  GPU: ss_fastq_index / ss_gather_rows against the
+oracle on the fixtures, on random edge-case files and over random chunkings; the GPU
+read_and_count_fastq against the golden items; the partitioned counter on packed keys (L not 16/32).
+"""
+import random
+
+import numpy as np
+import pytest
+
+import shortseq_amd as sq
+
+TOO_LONG = "Sequences longer than 1024 bases are not supported."
+
+
+def _merged_golden(case):
+    """Golden items with the reference's pointer-keyed ShortSeqVar duplicates merged (Q6)."""
+    out, pos = [], {}
+    for it in case["items"]:
+        key = (it["length"], it["str"])
+        if key in pos:
+            out[pos[key]][3] += it["count"]
+        else:
+            pos[key] = len(out)
+            out.append([it["class"], it["str"], it["length"], it["count"]])
+    return [tuple(x) for x in out]
+
+
+def _items(c):
+    return [(type(k).__name__, str(k), len(k), v) for k, v in c.items()]
+
+
+def _oracle_items(oracle, data: bytes):
+    """Oracle line selection + counter oracle -> merged items, or ('raises', message)."""
+    offs, lens = oracle.fastq_index(data)
+    reads = []
+    for o, ln in zip(offs, lens):
+        if ln > 1024:
+            return ("raises", TOO_LONG)
+        reads.append(data[int(o):int(o) + int(ln)])
+    try:
+        res = oracle.count(reads)
+    except ValueError as e:
+        kind, ri, bo, nb = e.args[0]
+        if kind == 2:
+            return ("raises", TOO_LONG)
+        return ("raises", "Unsupported base character: " + reads[ri][bo:bo + nb].decode("ascii"))
+    items = []
+    for words, L, c, _f in res:
+        cls = "ShortSeq64" if L <= 32 else ("ShortSeq192" if L <= 96 else "ShortSeqVar")
+        s = str(sq.from_words(list(words), L)) if L else ""
+        items.append((cls, s, L, c))
+    return items
+
+
+def _cases(golden):
+    return sorted(golden["fastq"].items())
+
+
+def test_oracle_fastq_pinned_to_reference(oracle, golden):
+    assert len(golden["fastq"]) >= 10
+    for name, case in _cases(golden):
+        data = bytes.fromhex(case["file_hex"])
+        got = _oracle_items(oracle, data)
+        if case["raises"]:
+            assert got == ("raises", case["message"]), name
+        else:
+            assert got == _merged_golden(case), name
+
+
+def test_host_front_fastq_golden(golden, tmp_path, capsys):
+    for name, case in _cases(golden):
+        p = tmp_path / (name + ".fq")
+        p.write_bytes(bytes.fromhex(case["file_hex"]))
+        if case["raises"]:
+            with pytest.raises(Exception) as ei:
+                sq.read_and_count_fastq(str(p), device="host")
+            assert str(ei.value) == case["message"], name
+        else:
+            c = sq.read_and_count_fastq(str(p), device="host")
+            assert _items(c) == _merged_golden(case), name
+    assert "total seqs" in capsys.readouterr().out
+
+
+def _random_fastq(rng, nrec, edge=True):
+    """Random FASTQ bytes: variable headers / lengths, optional edge cases (empty seq lines, NULs,
+    missing final newline)."""
+    parts = []
+    for i in range(nrec):
+        L = rng.choice([0, 1, 15, 16, 20, 31, 32, 33, 64, 96, 100, 150]) if edge else rng.choice([20, 32, 96])
+        seq = bytes(rng.choice(b"ACGT") for _ in range(L))
+        if edge and rng.random() < 0.01 and L > 2:
+            k = rng.randrange(L)
+            seq = seq[:k] + b"\x00" + seq[k + 1:]
+        hdr = b"@read_%d" % i + b"x" * rng.randrange(0, 40)
+        parts.append(hdr + b"\n" + seq + b"\n+\n" + b"I" * len(seq) + b"\n")
+    data = b"".join(parts)
+    if edge and rng.random() < 0.5:
+        data = data[:-1]          # drop the final newline
+    return data
+
+
+def _gpu_index(B, torch, dev, data, cuts=()):
+    """Index `data` on the device in chunks ending right after the newlines at `cuts` (byte
+    positions); returns global (offsets, lens)."""
+    bounds = [0] + sorted(cuts) + [len(data)]
+    offs_all, lens_all = [], []
+    line0 = 0
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        chunk = data[a:b]
+        buf = torch.tensor(np.frombuffer(chunk, np.uint8) if chunk else np.zeros(0, np.uint8),
+                           dtype=torch.uint8, device=dev)
+        offs, lens, nl = B.fastq_index(buf, len(chunk), line0=line0, at_eof=(b == len(data)))
+        offs_all.append(offs.cpu().numpy().astype(np.uint64) + np.uint64(a))
+        lens_all.append(lens.cpu().numpy().astype(np.uint32))
+        line0 += nl
+    return np.concatenate(offs_all), np.concatenate(lens_all)
+
+
+@pytest.mark.gpu
+def test_fastq_index_gpu_matches_oracle(gpu, oracle, golden):
+    import torch
+    import shortseq_amd.batch as B
+    files = [bytes.fromhex(c["file_hex"]) for _n, c in _cases(golden)]
+    rng = random.Random(11)
+    files += [_random_fastq(rng, n) for n in (1, 2, 3, 7, 500, 3000)]
+    files += [b"\n", b"\n\n", b"\n\n\n", b"a\nb\nc\nd\ne\nf", b"x" * 20000 + b"\n" + b"AC" * 9000 + b"\n"]
+    for data in files:
+        eo, el = oracle.fastq_index(data)
+        go, gl = _gpu_index(B, torch, gpu, data)
+        assert np.array_equal(go, eo) and np.array_equal(gl, el), data[:60]
+        # chunked: random cut points right after newlines
+        nls = [i + 1 for i in range(len(data)) if data[i] == 10 and i + 1 < len(data)]
+        for _ in range(3):
+            cuts = rng.sample(nls, min(len(nls), rng.randrange(1, 6))) if nls else []
+            go, gl = _gpu_index(B, torch, gpu, data, cuts)
+            assert np.array_equal(go, eo) and np.array_equal(gl, el), (data[:60], cuts)
+
+
+@pytest.mark.gpu
+def test_fastq_index_gpu_large(gpu, oracle):
+    """A multi-tile file (many 16-KiB tiles) against the oracle."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = random.Random(12)
+    data = _random_fastq(rng, 40_000)
+    eo, el = oracle.fastq_index(data)
+    go, gl = _gpu_index(B, torch, gpu, data)
+    assert len(eo) == 40_000 and np.array_equal(go, eo) and np.array_equal(gl, el)
+
+
+@pytest.mark.gpu
+def test_gather_rows_gpu(gpu):
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(13)
+    blob = rng.integers(0, 256, size=100_003, dtype=np.uint8)
+    src = torch.from_numpy(blob).to(gpu)
+    for L in (1, 3, 15, 16, 17, 32, 33, 100, 1024):
+        offs = rng.integers(0, len(blob) - L + 1, size=777).astype(np.int64)
+        offs[-1] = len(blob) - L                      # a row that ends exactly at the buffer end
+        sel = rng.permutation(777)[:500].astype(np.int64)
+        out = B.gather_rows(src, torch.from_numpy(offs).to(gpu), L, sel=torch.from_numpy(sel).to(gpu))
+        got = out.cpu().numpy()
+        S = (L + 15) // 16 * 16
+        assert got.shape == (500, S)
+        exp = np.stack([blob[offs[s]:offs[s] + L] for s in sel])
+        assert np.array_equal(got[:, :L], exp), L
+        assert (got[:, L:] == ord("A")).all()
+
+
+@pytest.mark.gpu
+def test_fastq_golden_gpu(gpu, golden, tmp_path, capsys):
+    from shortseq_amd import ingest
+    for name, case in _cases(golden):
+        p = tmp_path / (name + ".fq")
+        p.write_bytes(bytes.fromhex(case["file_hex"]))
+        if case["raises"]:
+            with pytest.raises(Exception) as ei:
+                sq.read_and_count_fastq(str(p), device="cuda")
+            assert str(ei.value) == case["message"], name
+            continue
+        c = sq.read_and_count_fastq(str(p), device="cuda")
+        assert _items(c) == _merged_golden(case), name
+        # the same through tiny ingest chunks (every chunk boundary path)
+        if len(case["file_hex"]) > 200:
+            gc, n = ingest.count_fastq(str(p), gpu, chunk_bytes=96)
+            c2 = sq.ShortSeqCounter()
+            groups, (ec, ef) = gc.finish()
+            ent = [(ef, sq.pack(""), ec)] if ec else []
+            for L, words, counts, firsts in groups:
+                for k in range(words.shape[0]):
+                    ent.append((int(firsts[k]), sq.from_words([int(x) for x in words[k]], L), int(counts[k])))
+            ent.sort(key=lambda e: e[0])
+            assert [(type(k).__name__, str(k), len(k), v) for _f, k, v in ent] == _merged_golden(case), name
+    assert "total seqs" in capsys.readouterr().out
+
+
+@pytest.mark.gpu
+def test_fastq_gpu_random_vs_host(gpu, tmp_path):
+    rng = random.Random(14)
+    data = _random_fastq(rng, 20_000)
+    data = data.replace(b"\x00", b"A")              # keep it valid
+    p = tmp_path / "r.fq"
+    p.write_bytes(data)
+    h = sq.read_and_count_fastq(str(p), device="host")
+    d = sq.read_and_count_fastq(str(p), device="cuda")
+    assert _items(d) == _items(h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [20, 31, 17])
+def test_counter_packed_keys_partitioned(gpu, oracle, L):
+    """L not in {16, 32}: the batch is packed into the key workspace, then partitioned."""
+    import torch
+    import shortseq_amd.batch as B
+    n = 200_000
+    pool = oracle.gen_pool_reads(21, 22, 5000, 0, n, L)
+    c = B.GpuCounter(1 << 14, device=gpu)
+    try:
+        c.insert(torch.from_numpy(pool).to(gpu).view(n, L), L, partitioned=True)
+        assert int(B.lib().ss_counter_reserved(c._h)) >= n
+        k, cnt, f = c.items_sorted()
+    finally:
+        c.close()
+    reads = [pool[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    exp = oracle.count(reads)
+    assert [int(x) for x in k] == [w[0] for (w, _L, _c, _f) in exp]
+    assert [int(x) for x in cnt] == [cc for (_w, _L, cc, _f) in exp]
+    assert [int(x) for x in f] == [ff for (_w, _L, _c, ff) in exp]
