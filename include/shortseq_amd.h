@@ -116,6 +116,31 @@ int ss_encode_hamming_ref(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64
                           uint32_t* d_out, uint64_t* d_first_bad, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Batch slice / subscript — replaces ShortSeq64/192/Var.__getitem__ (short_seq_64.pyx:53-75,
+ * short_seq_192.pyx:50-72, short_seq_var.pyx:37-59) -> _slice / _slice_to_ShortSeq64/192/Var /
+ * _shift_copy_trim (short_seq.pyx:93-238) and _subscript (short_seq.pyx:78-90, a 1-nt slice):
+ * out row r = nts [start, start + len) of read r, packed from bit 0, trimmed to 2*len bits, words
+ * past the slice zero.  out_wpr >= max(1, ceil(len/32)).
+ * fixed: one (start, len) for the batch, start + len <= L.
+ * var:   per-read d_starts / d_lens; with d_read_lens (nullable) they are clamped to the read
+ *        (start' = min(start, L_r), len' = min(len, L_r - start')), as Python slice bounds are.
+ * ---------------------------------------------------------------------------------------------- */
+int ss_slice_fixed(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr, uint32_t start, uint32_t len,
+                   uint64_t* d_out, uint32_t out_wpr, void* stream);
+int ss_slice_var(const uint64_t* d_words, uint64_t n, uint32_t wpr, const uint32_t* d_read_lens,
+                 const uint32_t* d_starts, const uint32_t* d_lens, uint64_t* d_out, uint32_t out_wpr, void* stream);
+
+/* All-pairs thresholded hamming (UMI-style dedup; distance = __xor__ above) over
+ * one batch of n < 2^32 packed reads of length L: for every unordered pair i < j with distance
+ * <= max_dist, d_counts[i] and d_counts[j] += 1 (neighbours per read; if d_counts != NULL) and the
+ * pair (i, j) is appended as two u32 to d_pairs (if != NULL) while fewer than max_pairs were written.
+ * *d_npairs = all such pairs (may exceed max_pairs).  The entry point zeroes d_counts / *d_npairs.
+ * Pair order is unspecified.  n <= 65535 * 1024 per call (L <= 32). */
+int ss_hamming_all_pairs(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr, uint32_t max_dist,
+                         uint32_t* d_counts, uint32_t* d_pairs, uint64_t max_pairs, uint64_t* d_npairs,
+                         void* stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Dedup counter — replaces ShortSeqCounter._count_sequence (counter.pyx:41-54): key = (length,
  * packed words) (short_seq_64.pyx:41-44; short_seq_192.pyx:35-41), count += 1, first-occurrence
  * index kept so the host can rebuild dict insertion order.  Open-addressing table in HBM, one per

@@ -63,6 +63,8 @@ def lib():
         L.ora_count.restype = I64
         L.ora_fastq_index.argtypes = [P, U64, P, P, U64]
         L.ora_fastq_index.restype = U64
+        L.ora_slice.argtypes = [P, U32, U32, U32, P]
+        L.ora_slice.restype = None
         _lib = L
     return _lib
 
@@ -232,3 +234,11 @@ def fastq_index(data: bytes):
     lens = np.zeros(n, dtype=np.uint32)
     lib().ora_fastq_index(buf.ctypes.data, len(buf), offs.ctypes.data, lens.ctypes.data, n)
     return offs, lens
+
+
+def slice_words(words, start: int, n: int) -> list:
+    """Packed words of nts [start, start + n) of a read (short_seq.pyx:93-238 restated)."""
+    src = np.ascontiguousarray(words, dtype=np.uint64)
+    dst = np.zeros(max(1, words_for(n)), dtype=np.uint64)
+    lib().ora_slice(_p(src), len(src), start, n, _p(dst))
+    return [int(x) for x in dst]

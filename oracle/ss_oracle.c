@@ -293,3 +293,34 @@ uint64_t ora_fastq_index(const uint8_t* buf, uint64_t nbytes, uint64_t* offsets,
     }
     return kept;
 }
+
+/* ------------------------------------------------------------------------------------------------
+ * Slice (test infrastructure; restates short_seq.pyx:93-238): nts [start, start + n) of a packed
+ * read `src` (wpr words), as _slice: offset = 2*start bits into block start/32; ShortSeq64 result
+ * (n <= 32): (packed[0] >> offset) | (packed[1] << (64 - offset)) when the slice crosses the block,
+ * _bzhi to 2n bits; longer: _shift_copy_trim (memcpy at offset 0, else per destination block
+ * (src[i] >> offset) | (src[i+1] << (64 - offset)), the final block trimmed to tail bits).
+ * Reads of src beyond wpr words count as 0 here (the reference reads past its array there; those
+ * bits are always trimmed away).  dst gets ceil(2n/64) words (>= 1).
+ * ---------------------------------------------------------------------------------------------- */
+static inline uint64_t ora_bzhi(uint64_t x, uint64_t nbits) { return nbits >= 64 ? x : (x & ((1ull << nbits) - 1)); }
+
+void ora_slice(const uint64_t* src, uint32_t wpr, uint32_t start, uint32_t n, uint64_t* dst) {
+    const uint32_t blk = start / 32, off = 2 * (start % 32);
+    const uint64_t bits = 2ull * n;
+    const uint64_t* p = src + blk;
+    const uint32_t avail = wpr - blk;                 /* words readable from p */
+#define ORA_SRC(i) ((uint32_t)(i) < avail ? p[(i)] : 0ull)
+    if (n <= 32) {
+        uint64_t r;
+        if (off + bits > 64) r = ora_bzhi((ORA_SRC(0) >> off) | (ORA_SRC(1) << (64 - off)), bits);
+        else r = ora_bzhi(ORA_SRC(0) >> off, bits);
+        dst[0] = r;
+        return;
+    }
+    const uint64_t nblk = (bits + 63) / 64, tail = bits % 64;
+    for (uint64_t i = 0; i < nblk; ++i)
+        dst[i] = off == 0 ? ORA_SRC(i) : ((ORA_SRC(i) >> off) | (ORA_SRC(i + 1) << (64 - off)));
+    if (tail) dst[nblk - 1] = ora_bzhi(dst[nblk - 1], tail);
+#undef ORA_SRC
+}

@@ -29,7 +29,8 @@ _NO_BAD = -1  # UINT64_MAX viewed as int64
 
 __all__ = ["words_for", "wpr_for", "encode", "encode_var", "decode", "decode_var", "hamming_ref",
            "hamming_pair", "encode_hamming_ref", "synth_reads", "synth_pool_reads", "GpuCounter",
-           "raise_read_error", "first_bad_buffer", "fastq_index", "gather_rows"]
+           "raise_read_error", "first_bad_buffer", "fastq_index", "gather_rows", "slice_fixed",
+           "slice_var", "hamming_all_pairs"]
 
 
 def words_for(L: int) -> int:
@@ -259,6 +260,61 @@ def synth_pool_reads(n: int, L: int, seed: int, pool_seed: int, U: int, *, i0: i
     check(lib().ss_synth_pool_reads(out.data_ptr(), seed, pool_seed, U, i0, n, L, L, _stream(dev)),
           "ss_synth_pool_reads")
     return out
+
+
+def slice_fixed(words: torch.Tensor, L: int, start: Optional[int] = None, stop: Optional[int] = None,
+                *, out: Optional[torch.Tensor] = None):
+    """reads[start:stop] for every read of a fixed-length packed batch (Python slice bounds, step 1,
+    as ShortSeq.__getitem__; short_seq.pyx:93-238) -> (words [n, max(1, ceil(len/32))], len)."""
+    _require_cuda(words, "words")
+    n, wpr = words.shape
+    st, sp, step = slice(start, stop).indices(L)
+    ln = max(0, sp - st)
+    if ln == 0:
+        st = 0
+    ow = wpr_for(ln)
+    if out is None:
+        out = torch.empty((n, ow), dtype=torch.int64, device=words.device)
+    check(lib().ss_slice_fixed(words.data_ptr(), n, L, wpr, st, ln, out.data_ptr(), out.shape[1],
+                               _stream(words.device)), "ss_slice_fixed")
+    return out, ln
+
+
+def slice_var(words: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, *,
+              read_lens: Optional[torch.Tensor] = None, out_wpr: Optional[int] = None) -> torch.Tensor:
+    """Per-read slices of a packed batch (adapter / UMI trimming): row r = nts [starts[r],
+    starts[r] + lens[r]) of read r, clamped to read_lens[r] when given (int32 tensors)."""
+    for t, nm in ((words, "words"), (starts, "starts"), (lens, "lens")):
+        _require_cuda(t, nm)
+    n, wpr = words.shape
+    if out_wpr is None:
+        out_wpr = wpr
+    out = torch.empty((n, out_wpr), dtype=torch.int64, device=words.device)
+    check(lib().ss_slice_var(words.data_ptr(), n, wpr, _ptr(read_lens), starts.data_ptr(), lens.data_ptr(),
+                             out.data_ptr(), out_wpr, _stream(words.device)), "ss_slice_var")
+    return out
+
+
+def hamming_all_pairs(words: torch.Tensor, L: int, max_dist: int, *, counts: bool = True,
+                      max_pairs: int = 0):
+    """Unordered pairs (i < j) of a packed batch within `max_dist` (the reference __xor__ distance)
+    -> (neighbour counts int32 [n] or None, pairs int32 [m, 2] or None, total pairs).  Pairs are
+    returned sorted; at most max_pairs are kept (0: count only)."""
+    _require_cuda(words, "words")
+    n, wpr = words.shape
+    dev = words.device
+    cnt = torch.empty(n, dtype=torch.int32, device=dev) if counts else None
+    pairs = torch.empty((max(1, max_pairs), 2), dtype=torch.int32, device=dev) if max_pairs else None
+    tot = torch.empty(1, dtype=torch.int64, device=dev)
+    check(lib().ss_hamming_all_pairs(words.data_ptr(), n, L, wpr, max_dist, _ptr(cnt), _ptr(pairs), max_pairs,
+                                     tot.data_ptr(), _stream(dev)), "ss_hamming_all_pairs")
+    total = int(tot.item())
+    if pairs is not None:
+        m = min(total, max_pairs)
+        p = pairs[:m].to(torch.int64)
+        key = p[:, 0] * (1 << 32) + p[:, 1]
+        pairs = pairs[:m][torch.argsort(key)]
+    return cnt, pairs, total
 
 
 LEN_UNDERFLOW = 0xFFFFFFFF   # ss_fastq_index: strlen 0 (the reference's size_t underflow -> too long)

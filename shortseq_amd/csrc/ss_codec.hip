@@ -328,6 +328,49 @@ __global__ __launch_bounds__(kThreads) void k_ham_group(const uint64_t* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
+// Slice / subscript on packed words (short_seq.pyx:78-238: _slice -> _slice_to_ShortSeq64 /
+// _shift_copy_trim; _subscript = a 1-nt slice): output word i of read r is the 64-bit funnel shift
+// of source words w, w+1 at bit 2*start + 64*i, the last word trimmed to the slice (_bzhi_u64),
+// words past the slice zero.  Lane per (read, output word), power-of-two lane groups per read.
+// RLEN: per-read lengths clamp (start, len) to the read (start' = min(start, L), len' = min(len,
+// L - start')), Python slice semantics for trimming ragged reads.
+// ------------------------------------------------------------------------------------------------
+template <bool VAR>
+__global__ __launch_bounds__(kThreads) void k_slice(const uint64_t* __restrict__ src, uint64_t n, uint32_t wpr,
+                                                    uint32_t start_fix, uint32_t len_fix,
+                                                    const uint32_t* __restrict__ starts,
+                                                    const uint32_t* __restrict__ slens,
+                                                    const uint32_t* __restrict__ rlens, uint64_t* __restrict__ out,
+                                                    uint32_t out_wpr, uint32_t logG) {
+    const uint32_t G = 1u << logG;
+    const uint64_t total = n << logG;
+    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * kThreads) {
+        const uint64_t r = g >> logG;
+        const uint32_t i = (uint32_t)g & (G - 1u);
+        if (i >= out_wpr) continue;
+        uint32_t st = VAR ? starts[r] : start_fix;
+        uint32_t ln = VAR ? slens[r] : len_fix;
+        if (rlens) {
+            const uint32_t L = rlens[r];
+            st = min(st, L);
+            ln = min(ln, L - st);
+        }
+        const uint32_t bits = 2u * ln;
+        uint64_t v = 0;
+        if (64u * i < bits) {
+            const uint32_t bit = 2u * st + 64u * i, w = bit >> 6, o = bit & 63u;
+            const uint64_t* s = src + r * wpr;
+            v = (w < wpr ? s[w] : 0ull) >> o;
+            if (o && w + 1 < wpr) v |= s[w + 1] << (64u - o);
+            const uint32_t rem = bits - 64u * i;
+            if (rem < 64u) v &= (1ull << rem) - 1ull;
+        }
+        out[r * out_wpr + i] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Synthetic reads; lane per (read, word).
 // ------------------------------------------------------------------------------------------------
 template <bool POOL>
@@ -569,6 +612,33 @@ int ss_hamming_ref(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr
 int ss_hamming_pair(const uint64_t* d_a, const uint64_t* d_b, uint64_t n, uint32_t L, uint32_t wpr,
                     uint32_t* d_out, void* stream) {
     return launch_ham(d_a, d_b, n, L, wpr, d_out, stream, true);
+}
+
+int ss_slice_fixed(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr, uint32_t start, uint32_t len,
+                   uint64_t* d_out, uint32_t out_wpr, void* stream) {
+    if (L > SS_MAX_NT || wpr < words_for(L) || wpr == 0 || wpr > 32) return ss_fail(SS_EARG, "bad L / wpr");
+    if ((uint64_t)start + len > L) return ss_fail(SS_EARG, "slice past the read");
+    if (out_wpr < (words_for(len) ? words_for(len) : 1u) || out_wpr > 32) return ss_fail(SS_EARG, "bad out_wpr");
+    if (n == 0) return SS_OK;
+    if (!d_words || !d_out) return ss_fail(SS_EARG, "null buffer");
+    const uint32_t logG = log2_ceil(out_wpr);
+    const unsigned grid = grid_for(n << logG, kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_slice<false>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_words, n, wpr, start,
+                       len, (const uint32_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr, d_out,
+                       out_wpr, logG);
+    return ss_check(hipGetLastError(), "k_slice");
+}
+
+int ss_slice_var(const uint64_t* d_words, uint64_t n, uint32_t wpr, const uint32_t* d_read_lens,
+                 const uint32_t* d_starts, const uint32_t* d_lens, uint64_t* d_out, uint32_t out_wpr, void* stream) {
+    if (wpr == 0 || wpr > 32 || out_wpr == 0 || out_wpr > 32) return ss_fail(SS_EARG, "bad wpr / out_wpr");
+    if (n == 0) return SS_OK;
+    if (!d_words || !d_starts || !d_lens || !d_out) return ss_fail(SS_EARG, "null buffer");
+    const uint32_t logG = log2_ceil(out_wpr);
+    const unsigned grid = grid_for(n << logG, kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_slice<true>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_words, n, wpr, 0u, 0u,
+                       d_starts, d_lens, d_read_lens, d_out, out_wpr, logG);
+    return ss_check(hipGetLastError(), "k_slice<var>");
 }
 
 int ss_synth_reads(uint8_t* d_ascii, uint64_t seed, uint64_t i0, uint64_t n, uint32_t L,

@@ -235,6 +235,45 @@ def fastq_cases(rng):
     return cases
 
 
+def slice_cases(rng):
+    """ShortSeq.__getitem__ with slices and ints (short_seq.pyx:78-238, short_seq_64.pyx:53-75,
+    short_seq_192.pyx:50-72, short_seq_var.pyx:37-59) on the reference objects."""
+    cases = []
+    lengths = [1, 2, 5, 31, 32, 33, 63, 64, 65, 95, 96, 97, 127, 128, 129, 200, 511, 512, 1000, 1024]
+    for L in lengths:
+        seq = "".join(rng.choice("ACGT") for _ in range(L))
+        obj = ref_sq.pack(seq)
+        items = []
+        picks = set()
+        for _ in range(40):
+            a = rng.randrange(-L - 3, L + 4)
+            b = rng.randrange(-L - 3, L + 4)
+            picks.add((rng.choice([a, None]), rng.choice([b, None])))
+        for a in (0, 1, 31, 32, 33, 63, 64, 65, 95, 96):
+            for ln in (1, 31, 32, 33, 64, 96, 97):
+                picks.add((a, a + ln))
+        for a, b in sorted(picks, key=lambda t: (str(t[0]), str(t[1]))):
+            out = obj[a:b]
+            cls, ws, ln = packed_words(out)
+            items.append({"start": a, "stop": b, "class": cls, "words": hexw(ws), "length": ln, "str": str(out)})
+        for step in (2, -1):
+            try:
+                obj[::step]
+                items.append({"step": step, "raises": None})
+            except BaseException as e:  # noqa: BLE001
+                items.append({"step": step, "raises": type(e).__name__, "message": str(e)})
+        idx = []
+        for i in sorted({0, L - 1, -1, -L, L, -L - 1, rng.randrange(L)}):
+            try:
+                out = obj[i]
+                cls, ws, ln = packed_words(out)
+                idx.append({"index": i, "class": cls, "words": hexw(ws), "length": ln})
+            except BaseException as e:  # noqa: BLE001
+                idx.append({"index": i, "raises": type(e).__name__, "message": str(e)})
+        cases.append({"seq": seq, "slices": items, "indices": idx})
+    return cases
+
+
 def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
@@ -273,15 +312,19 @@ def digests():
 
 
 def main():
-    if "--only-fastq" in sys.argv:
-        # add / refresh the FASTQ cases without regenerating the other fixtures
+    only = [a[len("--only-"):] for a in sys.argv[1:] if a.startswith("--only-")]
+    if only:
+        # add / refresh some case families without regenerating the other fixtures
         path = os.path.join(OUT, "golden_cases.json")
         with open(path) as f:
             data = json.load(f)
-        data["fastq"] = fastq_cases(random.Random(20260101))
+        if "fastq" in only:
+            data["fastq"] = fastq_cases(random.Random(20260101))
+        if "slices" in only:
+            data["slices"] = slice_cases(random.Random(20260102))
         with open(path, "w") as f:
             json.dump(data, f, indent=0, sort_keys=True)
-        print("wrote fastq cases to", path)
+        print("wrote", only, "to", path)
         return
     rng = random.Random(20250216)
     data = {
@@ -292,6 +335,7 @@ def main():
         "errors": errors(rng),
         "counter": counter_cases(rng),
         "fastq": fastq_cases(random.Random(20260101)),
+        "slices": slice_cases(random.Random(20260102)),
     }
     with open(os.path.join(OUT, "golden_cases.json"), "w") as f:
         json.dump(data, f, indent=0, sort_keys=True)
