@@ -28,6 +28,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+SETTLE_S = 0.1         # untimed clock-settle load before every timed region (see timed_loop)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
 
 
@@ -83,6 +84,13 @@ def timed_loop(step, steps, warmup, world):
     for _ in range(warmup):
         step(None)
     torch.cuda.synchronize()
+    # clock settle: the MI355X needs ~20-30 ms of sustained load before its clocks stop ramping
+    # (tools/tune_stream.hip ramp trace: first ~30 back-to-back 0.6-ms launches 2-6 % slower), so
+    # untimed steps continue until SETTLE_S of load has passed, whatever W is
+    t_s = time.perf_counter()
+    while time.perf_counter() - t_s < SETTLE_S:
+        step(None)
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     timer = Timer()
@@ -247,6 +255,65 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
     return el, tr.region_ms / steps, uniq
 
 
+def bench_fastq_index(B, lib, dev, n_rec=8 << 20, L=100, reps=10):
+    """ss_fastq_scan + ss_fastq_index over a device-resident synthetic FASTQ text
+    (n_rec records of L nt, 20-40-byte headers); checks every record's offset/length."""
+    from shortseq_amd._native import check
+    rng = np.random.default_rng(1)
+    m = 1 << 16
+    parts = []
+    for i in range(m):
+        seq = rng.choice(np.frombuffer(b"ACGT", np.uint8), L).tobytes()
+        parts.append(b"@SYN:%08d:" % i + b"x" * int(rng.integers(8, 28)) + b"\n" + seq + b"\n+\n" + b"I" * L + b"\n")
+    block = np.frombuffer(b"".join(parts), np.uint8).copy()
+    reps_blk = n_rec // m
+    buf = torch.from_numpy(block).to(dev).repeat(reps_blk)
+    nbytes, nrec = buf.numel(), m * reps_blk
+    s = torch.cuda.current_stream(dev).cuda_stream
+    ws_bytes = int(lib.ss_fastq_scan_ws_bytes(nbytes))
+    ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.int64, device=dev)
+    cnt = torch.empty(2, dtype=torch.int64, device=dev)
+    offs = torch.empty(nrec + 2, dtype=torch.int64, device=dev)
+    lens = torch.empty(nrec + 2, dtype=torch.int32, device=dev)
+    aux = torch.empty(nrec + 2, dtype=torch.int64, device=dev)
+
+    def step(_t):
+        check(lib.ss_fastq_scan(buf.data_ptr(), nbytes, ws.data_ptr(), ws_bytes, cnt.data_ptr(), s), "scan")
+        check(lib.ss_fastq_index(buf.data_ptr(), nbytes, 0, 1, ws.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                 aux.data_ptr(), nrec + 2, cnt[1:].data_ptr(), s), "index")
+    el, tr = timed_loop(step, reps, 3, 1)
+    if int(cnt[1]) != nrec or int(lens[:nrec].min()) != L or int(lens[:nrec].max()) != L:
+        raise SystemExit("PARITY FAILURE: FASTQ index")
+    starts = torch.from_numpy(np.cumsum([0] + [len(p) for p in parts[:-1]]) + np.array(
+        [p.index(b"\n") + 1 for p in parts])).to(dev)
+    if not torch.equal(offs[:m], starts):
+        raise SystemExit("PARITY FAILURE: FASTQ offsets")
+    ms = tr.region_ms / reps
+    return {"file_bytes": nbytes, "records": nrec, "read_len": L, "ms_per_step": ms,
+            "file_GB_per_s": nbytes / ms / 1e6, "records_per_s": nrec / ms * 1e3,
+            "note": "scan + index passes (file read twice); device-resident synthetic FASTQ"}
+
+
+def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):
+    """all unordered pairs of n UMIs (L nt) within hamming k."""
+    from shortseq_amd._native import check
+    w = B.encode(B.synth_reads(n, L, seed=7, device=dev), L)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev)
+    tot = torch.empty(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(_t):
+        check(lib.ss_hamming_all_pairs(w.data_ptr(), n, L, w.shape[1], k, cnt.data_ptr(), None, 0,
+                                       tot.data_ptr(), s), "all_pairs")
+    el, tr = timed_loop(step, reps, 2, 1)
+    if int(cnt.sum().item()) != 2 * int(tot.item()):
+        raise SystemExit("PARITY FAILURE: all-pairs counts")
+    ms = tr.region_ms / reps
+    pairs = n * (n - 1) // 2
+    return {"n": n, "read_len": L, "max_dist": k, "pairs": pairs, "ms_per_step": ms,
+            "pairs_per_s": pairs / ms * 1e3, "hits": int(tot.item()), "bound": "valu (bit-plane popcount)"}
+
+
 # ------------------------------------------------------------------------------------------------
 def cpu_baseline(L=32, target_s=10.0):
     """The reference's compiled _marshall_bytes_64 (oracle/_ref) on 1 host core over a bounded
@@ -334,7 +401,7 @@ def main():
     result = {
         "metric": "nt/sec 2-bit encode (32/96/512-nt batches) + hamming pairs/sec; % HBM roofline",
         "value": value, "unit": "nt/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": ms_step, "higher_is_better": True, "settle_s": SETTLE_S, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic (device-side splitmix64 reads, SURVEY §8(d))",
         "config": {"workload": f"C2: {n / 1e6:g}M x 32-nt batch encode (short_seq_64 path) per GPU",
                    "reads_per_gpu": n, "read_len": L, "global_batch": n * world,
@@ -380,6 +447,10 @@ def main():
             "merge": (f"all_to_all_single of (key, count, first) by owner over {dist.get_backend()}"
                       f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
                      if world > 1 else "none (1 GPU)"}
+        if rank == 0 or world == 1:
+            log("F1 FASTQ index / F4 all-pairs")
+            extra["F1_fastq_index_100nt"] = bench_fastq_index(B, lib, dev)
+            extra["F4_all_pairs_umi12"] = bench_all_pairs(B, lib, dev)
         result["extra"] = extra
 
     if rank == 0:
