@@ -31,7 +31,10 @@ constexpr int kThreads = 256;
 constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
 constexpr uint32_t kExtractBlocks = 1024;  // extract passes: fixed grid, contiguous slot ranges
 constexpr uint32_t kSliceLogMax = 11;      // region slice: 2048 slots (one LDS-resident aggregation)
-constexpr uint32_t kPartBlocks = 1024;     // partition passes: fixed grid, contiguous read ranges
+#ifndef SS_PC_BLOCKS
+#define SS_PC_BLOCKS 1024
+#endif
+constexpr uint32_t kPartBlocks = SS_PC_BLOCKS;  // partition passes: fixed grid, contiguous read ranges
 constexpr uint32_t kMaxRegions = 32768;    // per-block region histogram in LDS (128 KB)
 }  // namespace
 
@@ -398,30 +401,42 @@ __global__ __launch_bounds__(T) void k_pc_keys(Tbl t, PartWs w, uint32_t bins, c
     __syncthreads();
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
-    constexpr uint32_t kReadsPerTile = T * U / 2;
-    for (uint64_t t0 = lo; t0 < hi; t0 += kReadsPerTile) {
-        uint4 x[U];
+    // one lane per read (U reads per lane per tile): both 16-B chunks of a read in the lane, so the
+    // table-path carry, the key, its hash and the histogram atomic need no lane exchange and every
+    // lane does useful work (SQ counters on the 2-lanes-per-read form: 62 % issue-stalled)
+    constexpr uint32_t kReadsPerTile = T * U;
+    uint4 nx[U][2];
+    auto load_tile = [&](uint64_t t0) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const uint32_t gl = j * T + threadIdx.x;
-            const uint64_t r = t0 + (gl >> 1);
-            const uint32_t k = gl & 1u;
-            x[j] = (r < hi && k < cpr) ? ld_stream(&in[r * stride16 + k])
-                                       : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+            const uint64_t r = t0 + j * T + threadIdx.x;
+            const bool ok = r < hi;
+            nx[j][0] = ok ? ld_stream(&in[r * stride16]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+            nx[j][1] = (ok && cpr > 1) ? ld_stream(&in[r * stride16 + 1])
+                                      : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
         }
+    };
+    if (lo < hi) load_tile(lo);
+    for (uint64_t t0 = lo; t0 < hi; t0 += kReadsPerTile) {
+        uint4 x[U][2];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const uint32_t gl = j * T + threadIdx.x;
-            const uint64_t r = t0 + (gl >> 1);
-            const uint32_t k = gl & 1u;
-            const Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, true);   // L <= 32: table path
-            const uint32_t v = e.v | (k ? swap_pair(e.cout) : 0u);
-            const uint32_t hiw = swap_pair(v);
-            const uint32_t bad_pair = e.bad | swap_pair(e.bad);
-            const bool live = r < hi && k == 0;
-            report_bad(live && bad_pair != 0u, r, first_bad);
+            x[j][0] = nx[j][0];
+            x[j][1] = nx[j][1];
+        }
+        if (t0 + kReadsPerTile < hi) load_tile(t0 + kReadsPerTile);
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint64_t r = t0 + j * T + threadIdx.x;
+            // L <= 32: table path for both chunks; the low chunk's alias carry goes into the high
+            // half (for L = 16 the high chunk is "A" padding and the carry lands at bit 32, as the
+            // reference's acc << 2 loop puts it)
+            const Enc32 a = encode16(x[j][0].x, x[j][0].y, x[j][0].z, x[j][0].w, true);
+            const Enc32 b = encode16(x[j][1].x, x[j][1].y, x[j][1].z, x[j][1].w, true);
+            const bool live = r < hi;
+            report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
             if (live) {
-                const uint64_t key = (uint64_t)v | ((uint64_t)hiw << 32);
+                const uint64_t key = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
                 w.keys[r] = key;
                 atomicAdd(&my[bin_of<true>(t, w, key)], 1u);
             }
@@ -536,7 +551,10 @@ __global__ __launch_bounds__(256) void k_pc_offsets(PartWs w, uint32_t bins, con
 // the regions of the (1-2) coarse buckets the block's range spans (range-sorted input), mapped to
 // local bins region - lo_region; a block spanning more than kMaxLocalBins falls back to direct
 // (unstaged) stores through the same cursors.
-constexpr uint32_t kTile = 2048;
+#ifndef SS_PC_TILE
+#define SS_PC_TILE 4096     // elements per LDS-staged scatter tile (tools/tune_counter.hip sweeps it)
+#endif
+constexpr uint32_t kTile = SS_PC_TILE;
 constexpr uint32_t kMaxLocalBins = 1024;
 
 // exclusive scan of data[0..n) (n <= 1024) by a 512-thread block; returns the total
@@ -609,6 +627,22 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
         }
         return;
     }
+    // register double buffer: the next tile's keys / indices load while this tile is ranked,
+    // scanned and written out
+    uint64_t nkey[kTile / T];
+    uint32_t nidx[kTile / T];
+    auto load_tile = [&](uint64_t t0) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
+            const uint32_t e = j * T + threadIdx.x;
+            if (e < cnt) {
+                nkey[j] = src[t0 + e];
+                nidx[j] = HAS_IDX ? src_idx[t0 + e] : (uint32_t)(t0 + e);
+            }
+        }
+    };
+    load_tile(lo);
     for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
         const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
         for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
@@ -617,10 +651,14 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
         uint32_t idx[kTile / T], lb[kTile / T], rank[kTile / T];
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
+            key[j] = nkey[j];
+            idx[j] = nidx[j];
+        }
+        if (t0 + kTile < hi) load_tile(t0 + kTile);
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
             const uint32_t e = j * T + threadIdx.x;
             if (e < cnt) {
-                key[j] = src[t0 + e];
-                idx[j] = HAS_IDX ? src_idx[t0 + e] : (uint32_t)(t0 + e);
                 lb[j] = bin_of<COARSE>(t, w, key[j]) - bin_lo;
                 rank[j] = atomicAdd(&lcount[lb[j]], 1u);
             }
@@ -686,22 +724,34 @@ __global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t ba
     // phase 1: aggregate the bucket
     const uint32_t b0 = w.rstart[region], b1 = w.rstart[region + 1];
     const uint32_t lds_shift = (t.shift >= 64 ? 64 : t.shift) - 1;   // one more hash bit than the slice
-    for (uint32_t e = b0 + threadIdx.x; e < b1; e += T) {
-        const uint64_t key = w.bkey[e];
-        const uint32_t idx = w.bidx[e];
-        if (key == kEmpty) {
-            atomicAdd(&sent[0], 1u);
-            atomicMin(&sent[1], idx);
-            continue;
+    constexpr int kP1 = 4;   // bucket elements loaded per thread before the LDS work (latency overlap)
+    for (uint32_t e0 = b0; e0 < b1; e0 += kP1 * T) {
+        uint64_t key[kP1];
+        uint32_t idx[kP1];
+#pragma unroll
+        for (int q = 0; q < kP1; ++q) {
+            const uint32_t e = e0 + q * T + threadIdx.x;
+            key[q] = e < b1 ? w.bkey[e] : kEmpty;
+            idx[q] = e < b1 ? w.bidx[e] : 0xFFFFFFFFu;
         }
-        uint32_t ls = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> lds_shift) & (LS - 1);
-        for (;;) {
-            const unsigned long long prev = atomicCAS(&lkey[ls], (unsigned long long)kEmpty, (unsigned long long)key);
-            if (prev == kEmpty || prev == key) break;
-            ls = (ls + 1) & (LS - 1);
+#pragma unroll
+        for (int q = 0; q < kP1; ++q) {
+            if (idx[q] == 0xFFFFFFFFu && key[q] == kEmpty) continue;   // past the bucket
+            if (key[q] == kEmpty) {
+                atomicAdd(&sent[0], 1u);
+                atomicMin(&sent[1], idx[q]);
+                continue;
+            }
+            uint32_t ls = (uint32_t)((key[q] * 0x9E3779B97F4A7C15ull) >> lds_shift) & (LS - 1);
+            for (;;) {
+                const unsigned long long prev = atomicCAS(&lkey[ls], (unsigned long long)kEmpty,
+                                                          (unsigned long long)key[q]);
+                if (prev == kEmpty || prev == key[q]) break;
+                ls = (ls + 1) & (LS - 1);
+            }
+            atomicAdd(&lcnt[ls], 1u);
+            atomicMin(&lfst[ls], idx[q]);
         }
-        atomicAdd(&lcnt[ls], 1u);
-        atomicMin(&lfst[ls], idx);
     }
     __syncthreads();
     // phase 2: slot of each distinct key in the slice (LDS only)
@@ -1119,7 +1169,10 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         const size_t mw_lds = (size_t)2 * S * 16 + (size_t)S * 8;
         const bool two_pass = w.rbits > kCoarseBits;             // > 64 regions: coarse pass first
         const uint32_t bins1 = two_pass ? (1u << kCoarseBits) : w.R;
-        constexpr int T1 = 512, U1 = 4, TS = 512, TF = 512;
+        #ifndef SS_PC_KEYS_U
+#define SS_PC_KEYS_U 2
+#endif
+        constexpr int T1 = 512, U1 = SS_PC_KEYS_U, TS = 512, TF = 512;
         // dynamic LDS above the 64 KB default: opt in once per kernel (host-side attribute)
         static bool attrs_set = false;
         if (!attrs_set) {

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Cost of the C5 exchange-side kernels on one GPU: extract(n_parts=8) of a 125M-read table (pool
+2^24) and the owner-side merge of as many (key, count, first) entries as one of 8 owners receives
+(~ the table's unique keys: every rank holds most of the pool)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import shortseq_amd.batch as B  # noqa: E402
+
+
+def t(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+dev = torch.device("cuda", 0)
+n, L, U = 125_000_000, 32, 1 << 24
+ascii = B.synth_pool_reads(n, L, 5, 77, U, device=dev)
+local = B.GpuCounter(1 << 25, device=dev)
+local.insert(ascii, L)
+del ascii
+keys, lens, counts, first, parts = local.extract(n_parts=8)
+m = int(parts.sum().item())
+print("unique", m, "parts", parts.tolist(), flush=True)
+print(f"extract(8): {t(lambda: local.extract(n_parts=8)):.3f} ms", flush=True)
+owner = B.GpuCounter(1 << 25, device=dev)
+k, c, f = keys[:m].contiguous(), counts[:m].contiguous(), first[:m].contiguous()
+
+
+def merge():
+    owner.reset()
+    owner.merge(k, c, f, L)
+
+
+print(f"merge {m} entries: {t(merge):.3f} ms (incl. 1-GB table reset)", flush=True)
+print(f"reset only: {t(owner.reset):.3f} ms", flush=True)
