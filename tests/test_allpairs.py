@@ -41,7 +41,8 @@ def test_brute_force_matches_oracle_pairwise(oracle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("L,n,k", [(12, 3000, 1), (10, 2500, 2), (32, 1500, 3), (33, 1100, 2),
-                                   (96, 1200, 4), (150, 700, 6), (1024, 300, 700), (1, 2000, 0)])
+                                   (96, 1200, 4), (100, 600, 3), (128, 500, 5), (64, 900, 3),
+                                   (150, 700, 6), (1024, 300, 700), (1, 2000, 0)])
 def test_all_pairs_gpu(gpu, oracle, L, n, k):
     import torch
     import shortseq_amd.batch as B
