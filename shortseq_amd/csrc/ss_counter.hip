@@ -59,6 +59,9 @@ struct ss_counter {
     uint32_t* ws_hist = nullptr;           // [kPartBlocks * regions] per-(block, bin) counts -> offsets
     uint32_t* ws_rstart = nullptr;         // [regions + 1] region start in the bucket arrays
     uint32_t* ws_tot = nullptr;            // [regions + 1] scratch (bin totals / coarse starts)
+    // optimistic coarse partition (k_pf_coarse): ws_akey / ws_aidx hold 128 bins of ws_cap1 slots
+    uint64_t ws_cap1 = 0;
+    uint32_t* ws_fill = nullptr;           // [128] bin fill counters, [128] overflow flag
 };
 
 namespace {
@@ -133,8 +136,12 @@ __device__ __forceinline__ void tbl_add(const Tbl& t, uint64_t key, unsigned lon
 template <int U>
 __global__ __launch_bounds__(kThreads) void k_count_g16(Tbl t, const uint4* __restrict__ in,
                                                         uint64_t stride16, uint64_t n, uint32_t cpr,
-                                                        uint64_t base_index, unsigned long long* first_bad) {
-    const uint64_t base = (uint64_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+                                                        uint64_t base_index, unsigned long long* first_bad,
+                                                        const uint32_t* only_if = nullptr) {
+    if (only_if && *only_if == 0u) return;   // fallback launch of the optimistic partition: idle
+    // grid-stride over block tiles (uniform trip count: the lane-pair exchanges need whole waves)
+    for (uint64_t tb = (uint64_t)blockIdx.x * (U * kThreads); tb < 2 * n; tb += (uint64_t)gridDim.x * (U * kThreads)) {
+    const uint64_t base = tb + threadIdx.x;
     uint4 x[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -157,6 +164,7 @@ __global__ __launch_bounds__(kThreads) void k_count_g16(Tbl t, const uint4* __re
         const bool live = r < n && k == 0;
         report_bad(live && bad_pair != 0u, r, first_bad);
         if (live && bad_pair == 0u) tbl_add(t, (uint64_t)v | ((uint64_t)hi << 32), 1ull, base_index + r);
+    }
     }
 }
 
@@ -508,8 +516,10 @@ __global__ __launch_bounds__(256) void k_pc_tot(PartWs w, uint32_t bins) {
 }
 
 // exclusive scan of bin totals (one block of 1024) -> start[bins + 1]
-__global__ __launch_bounds__(1024) void k_pc_scan(PartWs w, uint32_t bins, uint32_t* start) {
+__global__ __launch_bounds__(1024) void k_pc_scan(PartWs w, uint32_t bins, uint32_t* start,
+                                                  const uint32_t* skip_if = nullptr) {
     __shared__ uint32_t sums[1024];
+    if (skip_if && *skip_if) return;
     const uint32_t seg = (bins + 1023) / 1024;
     const uint32_t lo = threadIdx.x * seg, hi = min(bins, lo + seg);
     uint32_t local = 0;
@@ -690,6 +700,247 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Optimistic coarse partition (the C5 path for L 16 / 32, > 128 regions).  The exact passes above
+// need a histogram of the whole batch before the coarse scatter (P1 writes every key, P3 reads
+// them back).  Here the encode pass scatters directly: each 4096-read tile is ranked by coarse
+// bin in LDS and reserves its runs with ONE atomicAdd per (tile, bin) on the bin's fill counter;
+// bin b owns slots [b * cap1, (b + 1) * cap1) of the coarse arrays (cap1 = 1.25 x the mean bin
+// load + 8192).  Order inside a bin is arbitrary, which the aggregation does not care about
+// (count = sum, first = min of the carried read index).  A bin that would overflow raises the
+// overflow word: every later pass then idles and k_count_g16 inserts the batch directly
+// (adversarial inputs that pile one bin, e.g. a few keys repeated, still count exactly).
+// Fine pass: 8 blocks per coarse bin, each over 1/8 of its filled slots; all of a block's keys
+// lie in the bin's 2^(rbits - 7) regions, so the histogram and the LDS staging use that window.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kCB = 1u << kCoarseBits;          // 128 coarse bins
+constexpr uint32_t kFinePerBin = 8;                  // fine-pass blocks per coarse bin
+#ifndef SS_PF_RPL
+#define SS_PF_RPL 8
+#endif
+constexpr uint32_t kPfT = 512, kPfRPL = SS_PF_RPL;   // k_pf_coarse: kPfT * kPfRPL-read tiles
+
+template <int T, int RPL>
+__global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
+                                                 uint64_t n, uint32_t cpr, uint64_t cap1, uint32_t* fill,
+                                                 unsigned long long* first_bad) {
+    constexpr uint32_t TILE = T * RPL;
+    __shared__ uint32_t lcount[kCB], lstart[kCB], gbase[kCB];
+    __shared__ uint64_t skey[TILE];
+    __shared__ uint32_t sidx[TILE];
+    __shared__ uint8_t sbin[TILE];
+    __shared__ uint32_t wsum[17];
+    uint32_t* ovf = fill + kCB;
+    const uint32_t shift = w.rbits - kCoarseBits;
+    const uint64_t tiles = (n + TILE - 1) / TILE;
+    uint4 nx[RPL][2];
+    auto load_tile = [&](uint64_t tile) {
+#pragma unroll
+        for (int j = 0; j < RPL; ++j) {
+            const uint64_t r = tile * TILE + j * T + threadIdx.x;
+            const bool ok = r < n;
+            nx[j][0] = ok ? ld_stream(&in[r * stride16]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+            nx[j][1] = (ok && cpr > 1) ? ld_stream(&in[r * stride16 + 1])
+                                      : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+        }
+    };
+    if (blockIdx.x < tiles) load_tile(blockIdx.x);
+    for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
+        uint4 x[RPL][2];
+#pragma unroll
+        for (int j = 0; j < RPL; ++j) {
+            x[j][0] = nx[j][0];
+            x[j][1] = nx[j][1];
+        }
+        if (tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
+        __syncthreads();
+        uint64_t key[RPL];
+        uint32_t bin[RPL], rank[RPL];
+        const uint64_t t0 = tile * TILE;
+        const uint32_t cnt = (uint32_t)min((uint64_t)TILE, n - t0);
+#pragma unroll
+        for (int j = 0; j < RPL; ++j) {
+            const uint64_t r = t0 + j * T + threadIdx.x;
+            // table path for both chunks (L <= 32); the low chunk's alias carry into the high half
+            const Enc32 a = encode16(x[j][0].x, x[j][0].y, x[j][0].z, x[j][0].w, true);
+            const Enc32 b = encode16(x[j][1].x, x[j][1].y, x[j][1].z, x[j][1].w, true);
+            const bool live = r < n;
+            report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
+            key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
+            if (live) {
+                bin[j] = region_of(t, key[j]) >> shift;
+                rank[j] = atomicAdd(&lcount[bin[j]], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < kCB; i += T) lstart[i] = lcount[i];
+        __syncthreads();
+        block_scan_512(lstart, kCB, wsum);
+        for (uint32_t i = threadIdx.x; i < kCB; i += T)
+            gbase[i] = lcount[i] ? atomicAdd(&fill[i], lcount[i]) : 0u;
+#pragma unroll
+        for (int j = 0; j < RPL; ++j) {
+            const uint32_t e = j * T + threadIdx.x;
+            if (e < cnt) {
+                const uint32_t sp = lstart[bin[j]] + rank[j];
+                skey[sp] = key[j];
+                sidx[sp] = (uint32_t)(t0 + e);
+                sbin[sp] = (uint8_t)bin[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < cnt; i += T) {
+            const uint32_t b = sbin[i];
+            const uint64_t pos = (uint64_t)gbase[b] + (i - lstart[b]);
+            if (pos < cap1) {
+                w.akey[b * cap1 + pos] = skey[i];
+                w.aidx[b * cap1 + pos] = sidx[i];
+            } else {
+                *ovf = 1u;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void fine_range(uint32_t fb, const uint32_t* fill, uint64_t cap1, uint32_t& bin,
+                                           uint64_t& lo, uint64_t& hi) {
+    bin = fb / kFinePerBin;
+    const uint32_t sub = fb % kFinePerBin;
+    const uint64_t f = min((uint64_t)fill[bin], cap1);
+    lo = sub * f / kFinePerBin;
+    hi = (sub + 1) * f / kFinePerBin;
+}
+
+// fine histogram: block fb counts the regions of its slice of coarse bin fb / 8 -> hist[fb][rpb]
+template <int T>
+__global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
+    __shared__ uint32_t h[kMaxLocalBins];
+    if (fill[kCB]) return;
+    const uint32_t rpb = 1u << (w.rbits - kCoarseBits);
+    uint32_t bin;
+    uint64_t lo, hi;
+    fine_range(blockIdx.x, fill, cap1, bin, lo, hi);
+    for (uint32_t i = threadIdx.x; i < rpb; i += T) h[i] = 0;
+    __syncthreads();
+    const uint64_t* src = w.akey + bin * cap1;
+    const uint32_t r0 = bin * rpb;
+    for (uint64_t e = lo + threadIdx.x; e < hi; e += T) atomicAdd(&h[region_of(t, src[e]) - r0], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < rpb; i += T) w.hist[(uint64_t)blockIdx.x * rpb + i] = h[i];
+}
+
+// region totals over the bin's 8 fine blocks (thread per region) -> w.tot; then k_pc_scan (one
+// block) -> rstart; then k_pf_offsets (thread per region) -> each fine block's write cursors
+__global__ __launch_bounds__(256) void k_pf_tot(PartWs w, const uint32_t* fill) {
+    if (fill[kCB]) return;
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= w.R) return;
+    const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t sub = 0; sub < kFinePerBin; ++sub) tot += w.hist[(uint64_t)(bin * kFinePerBin + sub) * rpb + j];
+    w.tot[r] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_pf_offsets(PartWs w, const uint32_t* fill) {
+    if (fill[kCB]) return;
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= w.R) return;
+    const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
+    uint32_t cur = w.rstart[r];
+#pragma unroll
+    for (uint32_t sub = 0; sub < kFinePerBin; ++sub) {
+        const uint64_t idx = (uint64_t)(bin * kFinePerBin + sub) * rpb + j;
+        const uint32_t c = w.hist[idx];
+        w.hist[idx] = cur;
+        cur += c;
+    }
+}
+
+// fine scatter: coarse bin slice -> (key, read index) grouped by region, LDS-staged like
+// k_pc_scatter_lds (local bins = the coarse bin's regions)
+__global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
+    constexpr int T = 512;
+    __shared__ uint32_t cursor[kMaxLocalBins];
+    __shared__ uint32_t lstart[kMaxLocalBins];
+    __shared__ uint32_t lcount[kMaxLocalBins];
+    __shared__ uint64_t skey[kTile];
+    __shared__ uint32_t sidx[kTile];
+    __shared__ uint16_t sbin[kTile];
+    __shared__ uint32_t wsum[17];
+    if (fill[kCB]) return;
+    const uint32_t nb = 1u << (w.rbits - kCoarseBits);
+    uint32_t bin;
+    uint64_t lo, hi;
+    fine_range(blockIdx.x, fill, cap1, bin, lo, hi);
+    const uint32_t r0 = bin * nb;
+    const uint64_t* src = w.akey + bin * cap1;
+    const uint32_t* src_idx = w.aidx + bin * cap1;
+    for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] = w.hist[(uint64_t)blockIdx.x * nb + i];
+    __syncthreads();
+    uint64_t nkey[kTile / T];
+    uint32_t nidx[kTile / T];
+    auto load_tile = [&](uint64_t t0) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
+            const uint32_t e = j * T + threadIdx.x;
+            if (e < cnt) {
+                nkey[j] = src[t0 + e];
+                nidx[j] = src_idx[t0 + e];
+            }
+        }
+    };
+    if (lo < hi) load_tile(lo);
+    for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
+        for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
+        __syncthreads();
+        uint64_t key[kTile / T];
+        uint32_t idx[kTile / T], lb[kTile / T], rank[kTile / T];
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
+            key[j] = nkey[j];
+            idx[j] = nidx[j];
+        }
+        if (t0 + kTile < hi) load_tile(t0 + kTile);
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
+            const uint32_t e = j * T + threadIdx.x;
+            if (e < cnt) {
+                lb[j] = region_of(t, key[j]) - r0;
+                rank[j] = atomicAdd(&lcount[lb[j]], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nb; i += T) lstart[i] = lcount[i];
+        __syncthreads();
+        block_scan_512(lstart, nb, wsum);
+#pragma unroll
+        for (int j = 0; j < (int)(kTile / T); ++j) {
+            const uint32_t e = j * T + threadIdx.x;
+            if (e < cnt) {
+                const uint32_t sp = lstart[lb[j]] + rank[j];
+                skey[sp] = key[j];
+                sidx[sp] = idx[j];
+                sbin[sp] = (uint16_t)lb[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < cnt; i += T) {
+            const uint32_t b = sbin[i];
+            const uint32_t gpos = cursor[b] + (i - lstart[b]);
+            w.keys[gpos] = skey[i];
+            w.bidx[gpos] = sidx[i];
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] += lcount[i];
+        __syncthreads();
+    }
+}
+
 // P4.  LDS: the aggregation table (2S entries of key + count + first-offset) and a copy of the
 // slice's S keys.  Phase 1 aggregates the region's bucket in LDS.  Phase 2 resolves every distinct
 // key's slot inside the LDS key copy (an LDS CAS on the copy claims a new slot; no global
@@ -699,7 +950,9 @@ constexpr uint32_t kAggT = 1024;
 constexpr uint32_t kAggPerThread = (2u << kSliceLogMax) / kAggT;   // LDS table slots per thread
 
 template <int T>
-__global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t base_index) {
+__global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t base_index,
+                                                    const uint32_t* skip_if = nullptr) {
+    if (skip_if && *skip_if) return;         // the optimistic partition overflowed: direct insert instead
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t S = (uint32_t)t.slice_mask + 1;          // slice slots
     const uint32_t LS = 2 * S;                               // LDS table slots (load <= 50%)
@@ -1035,6 +1288,7 @@ int ss_counter_destroy(ss_counter* c) {
     if (c->ws_hist) (void)hipFree(c->ws_hist);
     if (c->ws_rstart) (void)hipFree(c->ws_rstart);
     if (c->ws_tot) (void)hipFree(c->ws_tot);
+    if (c->ws_fill) (void)hipFree(c->ws_fill);
     delete c;
     return SS_OK;
 }
@@ -1079,9 +1333,15 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     if (max_reads >= (1ull << 32)) return ss_fail(SS_EARG, "max_reads must be < 2^32 per insert");
     if (max_reads <= c->ws_reads) return SS_OK;
     ss_counter_release(c);
+    // coarse arrays: room for the exact passes (max_reads) and for the optimistic partition's 128
+    // bins of cap1 = 1.25 x the mean bin load + 8192 slots
+    const uint64_t cap1 = (max_reads + max_reads / 4 + kCB - 1) / kCB + 8192;
+    const uint64_t acap = kCB * cap1 > max_reads ? kCB * cap1 : max_reads;
     hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, max_reads * sizeof(uint64_t));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, max_reads * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
+    if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, (2 * kCB) * sizeof(uint32_t));
+    c->ws_cap1 = cap1;
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_hist) e = hipMalloc((void**)&c->ws_hist, (size_t)kPartBlocks * R * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_rstart) e = hipMalloc((void**)&c->ws_rstart, (R + 1) * sizeof(uint32_t));
@@ -1200,6 +1460,42 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, bins, start);
             hipLaunchKernelGGL(k_pc_offsets, dim3(g), dim3(256), 0, s, w, bins, (const uint32_t*)start);
         };
+        if (!multi && !packed_keys && two_pass && w.rbits - kCoarseBits <= 8) {
+            // optimistic coarse partition: encode + coarse scatter in one pass, fine pass by bin
+            const uint64_t cap1 = c->ws_cap1;
+            rc = ss_check(hipMemsetAsync(c->ws_fill, 0, 2 * kCB * sizeof(uint32_t), s), "fill reset");
+            if (rc) return rc;
+            // grid-stride over tiles: exactly the resident blocks (no second, partial round)
+            static int pf_grid = 0;
+            if (!pf_grid) {
+                int dev = 0, cus = 0, per = 0;
+                hipGetDevice(&dev);
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL>, kPfT, 0);
+                pf_grid = (cus > 0 && per > 0) ? cus * per : (int)kPartBlocks;
+            }
+            hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
+                               (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
+                               (unsigned long long*)d_first_bad);
+            const unsigned fine_blocks = kCB * kFinePerBin;
+            const uint32_t* ovf = (const uint32_t*)(c->ws_fill + kCB);
+            hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
+                               (const uint32_t*)c->ws_fill);
+            const unsigned rg = (w.R + 255) / 256;
+            hipLaunchKernelGGL(k_pf_tot, dim3(rg), dim3(256), 0, s, w, (const uint32_t*)c->ws_fill);
+            hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, w.R, w.rstart, ovf);
+            hipLaunchKernelGGL(k_pf_offsets, dim3(rg), dim3(256), 0, s, w, (const uint32_t*)c->ws_fill);
+            hipLaunchKernelGGL(k_pf_scatter, dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
+                               (const uint32_t*)c->ws_fill);
+            w.bkey = w.keys;
+            hipLaunchKernelGGL((k_pc_aggregate<kAggT>), dim3(w.R), dim3(kAggT), agg_lds, s, t, w, base_index, ovf);
+            // overflow (a bin past cap1): the passes above idled; insert the batch directly
+            constexpr int U = 4;
+            const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 256 * 16);
+            hipLaunchKernelGGL((k_count_g16<U>), dim3(grid), dim3(kThreads), 0, s, t, (const uint4*)d_ascii,
+                               stride / 16, n, L / 16, base_index, (unsigned long long*)d_first_bad, ovf);
+            return ss_check(hipGetLastError(), "optimistic partitioned insert");
+        }
         if (multi) {
             const size_t fp_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             hipLaunchKernelGGL((k_mw_fp<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1,
