@@ -293,7 +293,10 @@ def test_counter_extract_parts_and_merge(gpu, oracle):
 
 
 @pytest.mark.parametrize("cap,U,n", [(1 << 12, 300, 200_000), (1 << 16, 20_000, 500_000),
-                                     (1 << 22, 1_000_000, 3_000_000)])
+                                     (1 << 22, 1_000_000, 3_000_000),
+                                     # > 128 regions: the optimistic coarse partition; few keys pile
+                                     # up in a few coarse bins -> overflow -> direct-insert fallback
+                                     (1 << 20, 5, 400_000), (1 << 20, 3000, 400_000)])
 def test_counter_partitioned_equals_direct(gpu, oracle, cap, U, n):
     """The partitioned (LDS-aggregated) insert and the direct atomic insert give identical tables,
     across several inserts (persistent table, global first indices), incl. the EMPTY-colliding key."""
