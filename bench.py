@@ -30,6 +30,7 @@ sys.path.insert(0, REPO)
 
 SETTLE_S = 0.1         # untimed clock-settle load before every timed region (see timed_loop)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+I8_PEAK_TOPS = 5000.0  # dense i8 MFMA: 2x the ~2.5 PF bf16 dense peak (MI355X_MICROARCH.md matrix cores)
 
 
 def log(*a):
@@ -310,8 +311,14 @@ def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):
         raise SystemExit("PARITY FAILURE: all-pairs counts")
     ms = tr.region_ms / reps
     pairs = n * (n - 1) // 2
+    # issued i8 MACs: one-hot codes, 8 positions (32 MACs) per k-step, ceil(min(L + 1, 32) / 8) steps
+    ks = (min(L + 1, 32) + 7) // 8
+    tops = pairs * 2 * 32 * ks / (ms * 1e-3) / 1e12
     return {"n": n, "read_len": L, "max_dist": k, "pairs": pairs, "ms_per_step": ms,
-            "pairs_per_s": pairs / ms * 1e3, "hits": int(tot.item()), "bound": "valu (bit-plane popcount)"}
+            "pairs_per_s": pairs / ms * 1e3, "hits": int(tot.item()),
+            "roofline": {"bound": "mfma", "kernel": "k_allpairs_mfma (v_mfma_i32_32x32x32_i8)", "achieved": tops,
+                         "peak": I8_PEAK_TOPS, "unit": "TOP/s", "frac": tops / I8_PEAK_TOPS,
+                         "note": "issued i8 MAC ops x2 (one-hot K padded to whole k-steps); dense i8 peak = 2x bf16"}}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -441,9 +448,20 @@ def main():
         log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
         s5 = max(3, args.steps // 4)
         el5, d5, uniq = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
+        # per-read bytes of the partitioned pipeline: coarse pass 32 in + 12 out,
+        # fine count 8, fine scatter 12 + 12, aggregate 12 + the table slices (2 x 32 B per unique
+        # slot, amortised over the reads); the floor of the problem is the 32 B of ASCII per read
+        table_b = 2 * 32 * min(U5, n5) / n5
+        pipe_b = 32 + 12 + 8 + 24 + 12 + table_b
         extra["C5_counter_32"] = {
             "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
             "reads_per_gpu": n5, "pool": U5, "unique": uniq,
+            "roofline": {"bound": "hbm", "kernel": "partitioned insert (k_pf_coarse, k_pf_count, k_pf_scatter, "
+                                                    "k_pc_aggregate)",
+                         "achieved": n5 * pipe_b / (d5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": n5 * pipe_b / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_read": pipe_b,
+                         "floor_frac": n5 * 32 / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "frac: the pipeline's own pass bytes; floor_frac: 32 B of ASCII per read"},
             "merge": (f"all_to_all_single of (key, count, first) by owner over {dist.get_backend()}"
                       f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
                      if world > 1 else "none (1 GPU)"}
