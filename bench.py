@@ -242,9 +242,8 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
         sc.count(ascii, L, base_index=i0, check_errors=False)
 
     el, tr = timed_loop(step, steps, warmup, world)
-    owned = sc.owned()
-    k, c, f = owned.items_sorted()
-    tot = torch.tensor([int(c.sum()), len(k)], dtype=torch.int64,
+    k, c, f = sc.owned_items()
+    tot = torch.tensor([int(c.sum().item()), k.numel()], dtype=torch.int64,
                        device=dev if world == 1 or dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(tot)

@@ -241,6 +241,26 @@ int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at
 int ss_gather_rows(const uint8_t* d_src, uint64_t src_bytes, const uint64_t* d_offsets, const uint64_t* d_sel,
                    uint64_t m, uint32_t L, uint8_t* d_dst, uint64_t dst_stride, void* stream);
 
+/* Multi-GPU counter with region-range ownership: part p of n owns the table regions
+ * [ceil(p R / n), ceil((p + 1) R / n)) (R = capacity / slice slots, ss_counter_geometry); the sentinel
+ * key ~0 belongs to the owner of its hash region.  Every rank counts its own reads into its own
+ * table, extracts the entries of the OTHER ranks' regions (ss_counter_extract_ranges: grouped by
+ * part, each part sorted by region, the sentinel last), exchanges them (all-to-all), and folds what it
+ * receives into its own table's owned regions (ss_counter_merge_runs).  The regions a rank does not own
+ * are stale afterwards; the union of all ranks' owned regions is the exact counter.
+ *   ss_counter_geometry:       host query, log2(capacity) and log2(slots per region).
+ *   ss_counter_extract_ranges: as ss_counter_extract with parts = region ranges (single-word keys).
+ *   ss_counter_merge_runs:     d_run_offsets = n_runs (begin, end) u64 pairs (device) into the received
+ *                              arrays; every run sorted by region and all keys in `part`'s regions;
+ *                              d_bounds: n_runs * (regions of part + 1) u32 of scratch. */
+int ss_counter_geometry(const ss_counter* c, uint32_t* h_log2cap, uint32_t* h_slice_log);
+int ss_counter_extract_ranges(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens,
+                              uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
+                              void* stream);
+int ss_counter_merge_runs(ss_counter* c, const uint64_t* d_keys, const uint64_t* d_counts, const uint64_t* d_first,
+                          const uint64_t* d_run_offsets, uint32_t n_runs, uint64_t m, uint32_t part,
+                          uint32_t n_parts, uint32_t L, uint32_t* d_bounds, void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):
  * read i word w: r = splitmix64(seed + i*W + w) masked to its nts, byte j = "ACTG"[(r >> 2j) & 3].

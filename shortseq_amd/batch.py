@@ -465,6 +465,44 @@ class GpuCounter:
                                        first.data_ptr(), cap, parts.data_ptr(), _stream(d)), "ss_counter_extract")
         return keys, lens, counts, first, parts
 
+    def geometry(self):
+        """(log2 capacity, log2 slots per region) of the table (region-range ownership)."""
+        a, b = C.c_uint32(), C.c_uint32()
+        check(lib().ss_counter_geometry(self._h, C.byref(a), C.byref(b)), "ss_counter_geometry")
+        return int(a.value), int(b.value)
+
+    def extract_ranges(self, n_parts: int, cap: Optional[int] = None):
+        """As extract, with part p = the table regions owner p holds under region-range ownership
+        (include/shortseq_amd.h); each part is sorted by region, the sentinel key last."""
+        cap = self.capacity + 1 if cap is None else cap
+        d = self.device
+        keys = torch.empty(cap, dtype=torch.int64, device=d)
+        lens = torch.empty(cap, dtype=torch.int32, device=d)
+        counts = torch.empty(cap, dtype=torch.int64, device=d)
+        first = torch.empty(cap, dtype=torch.int64, device=d)
+        parts = torch.empty(n_parts, dtype=torch.int64, device=d)
+        check(lib().ss_counter_extract_ranges(self._h, n_parts, keys.data_ptr(), lens.data_ptr(), counts.data_ptr(),
+                                              first.data_ptr(), cap, parts.data_ptr(), _stream(d)),
+              "ss_counter_extract_ranges")
+        return keys, lens, counts, first, parts
+
+    def merge_runs(self, keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, runs, part: int,
+                   n_parts: int, L: int) -> None:
+        """Fold region-sorted runs (list of (begin, end) into keys / counts / first) into the regions
+        this table owns as `part` of `n_parts` (ss_counter_merge_runs)."""
+        d = self.device
+        m = keys.numel()
+        if not runs:
+            return
+        offs = torch.tensor([x for be in runs for x in be], dtype=torch.int64).to(d, non_blocking=True)
+        log2cap, slice_log = self.geometry()
+        R = 1 << (log2cap - slice_log)
+        nreg = -(-(part + 1) * R // n_parts) - (-(part * R) // n_parts)
+        bounds = torch.empty(len(runs) * (nreg + 1) + 1, dtype=torch.int32, device=d)
+        check(lib().ss_counter_merge_runs(self._h, keys.data_ptr(), counts.data_ptr(), first.data_ptr(),
+                                          offs.data_ptr(), len(runs), m, part, n_parts, L, bounds.data_ptr(),
+                                          _stream(d)), "ss_counter_merge_runs")
+
     def extract_words(self, n_parts: int = 1, cap: Optional[int] = None):
         """As extract, for any key length: (fps, lens, words [cap, W], counts, first, part_counts);
         fps = the multi-word fingerprints (the packed word itself for W = 1)."""

@@ -29,7 +29,8 @@ struct alignas(32) Slot {
 };
 constexpr int kThreads = 256;
 constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
-constexpr uint32_t kExtractBlocks = 1024;  // extract passes: fixed grid, contiguous slot ranges
+constexpr uint32_t kExtractBlocks = 4096;  // extract passes: fixed grid, contiguous slot ranges
+constexpr uint32_t kExtractT = 64;         // ONE wave per extract block: slot order is output order
 constexpr uint32_t kSliceLogMax = 11;      // region slice: 2048 slots (one LDS-resident aggregation)
 #ifndef SS_PC_BLOCKS
 #define SS_PC_BLOCKS 1024
@@ -264,22 +265,36 @@ __device__ __forceinline__ unsigned long long wave_reserve(bool used, uint32_t p
     return pos;
 }
 
-// Extract pass 1: block b counts the used slots of its contiguous range per part -> bc[p*B + b].
-__global__ __launch_bounds__(kThreads) void k_part_count(Tbl t, uint32_t nparts, unsigned long long* bc) {
+// Owner part of an occupied slot.  Hash owners (ranges = false): owner_of(key) — any table
+// geometry.  Region-range owners (ranges = true, the multi-GPU counter): part p owns the table
+// regions [p R / n, (p + 1) R / n) — slot s sits in region s >> slice_log; the sentinel slot (key
+// ~0) belongs to the owner of region_of(~0).  Extracted in slot order, each part's entries are
+// then sorted by region, which ss_counter_merge_runs relies on.
+__device__ __forceinline__ uint32_t part_of(const Tbl& t, uint64_t s, uint64_t key, uint32_t nparts, bool ranges) {
+    if (!ranges) return owner_of(key, nparts);
+    const uint64_t R = (t.mask + 1) >> t.slice_log;
+    const uint64_t region = s <= t.mask ? (s >> t.slice_log) : (slot_top(t, kEmpty) >> t.slice_log);
+    return (uint32_t)(region * nparts / R);
+}
+
+// Extract pass 1: block b (one wave) counts the used slots of its contiguous range per part ->
+// bc[p*B + b].  Pass 3 walks the same range in the same order, so within a part the output is in
+// slot order (blocks in block order, a wave's lanes in lane order).
+__global__ __launch_bounds__(kExtractT) void k_part_count(Tbl t, uint32_t nparts, unsigned long long* bc, bool ranges) {
     __shared__ unsigned long long hist[kMaxParts];
-    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) hist[p] = 0;
+    for (uint32_t p = threadIdx.x; p < nparts; p += kExtractT) hist[p] = 0;
     __syncthreads();
     const uint64_t nslots = t.mask + 2;
     const uint64_t per = (nslots + kExtractBlocks - 1) / kExtractBlocks;
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(nslots, lo + per);
-    for (uint64_t s0 = lo; s0 < hi; s0 += kThreads) {
+    for (uint64_t s0 = lo; s0 < hi; s0 += kExtractT) {
         const uint64_t s = s0 + threadIdx.x;
         uint64_t key = kEmpty;
         const bool used = s < hi && slot_used(t, s, key);
-        wave_reserve(used, used ? owner_of(key, nparts) : 0u, hist);
+        wave_reserve(used, used ? part_of(t, s, key, nparts, ranges) : 0u, hist);
     }
     __syncthreads();
-    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) bc[(uint64_t)p * kExtractBlocks + blockIdx.x] = hist[p];
+    for (uint32_t p = threadIdx.x; p < nparts; p += kExtractT) bc[(uint64_t)p * kExtractBlocks + blockIdx.x] = hist[p];
 }
 
 // Extract pass 2 (one block of 1024): exclusive scan of bc in (part, block) order = each block's
@@ -317,22 +332,22 @@ __global__ __launch_bounds__(1024) void k_part_offsets(uint32_t nparts, unsigned
 
 // Extract pass 3: same ranges as pass 1; LDS cursors start at the block's offsets, so every slot's
 // position is reserved without any global atomic.
-__global__ __launch_bounds__(kThreads) void k_part_scatter(Tbl t, uint32_t nparts, int32_t L,
+__global__ __launch_bounds__(kExtractT) void k_part_scatter(Tbl t, uint32_t nparts, int32_t L,
                                                            const unsigned long long* bc, uint64_t* okeys,
                                                            uint32_t* olens, uint64_t* ocounts, uint64_t* ofirst,
                                                            uint64_t cap_out, unsigned long long* overflow,
-                                                           uint64_t* owords) {
+                                                           uint64_t* owords, bool ranges) {
     __shared__ unsigned long long cursor[kMaxParts];
-    for (uint32_t p = threadIdx.x; p < nparts; p += kThreads) cursor[p] = bc[(uint64_t)p * kExtractBlocks + blockIdx.x];
+    for (uint32_t p = threadIdx.x; p < nparts; p += kExtractT) cursor[p] = bc[(uint64_t)p * kExtractBlocks + blockIdx.x];
     __syncthreads();
     const uint64_t nslots = t.mask + 2;
     const uint64_t per = (nslots + kExtractBlocks - 1) / kExtractBlocks;
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(nslots, lo + per);
-    for (uint64_t s0 = lo; s0 < hi; s0 += kThreads) {
+    for (uint64_t s0 = lo; s0 < hi; s0 += kExtractT) {
         const uint64_t s = s0 + threadIdx.x;
         uint64_t key = kEmpty;
         const bool used = s < hi && slot_used(t, s, key);
-        const unsigned long long pos = wave_reserve(used, used ? owner_of(key, nparts) : 0u, cursor);
+        const unsigned long long pos = wave_reserve(used, used ? part_of(t, s, key, nparts, ranges) : 0u, cursor);
         if (!used) continue;
         if (pos >= cap_out) {
             atomicOr(overflow, 2ull);
@@ -1071,6 +1086,115 @@ __global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t ba
 }
 
 // ------------------------------------------------------------------------------------------------
+// Owner-side merge of region-sorted runs (the multi-GPU counter's exchange step).
+// Each source rank extracts the regions this rank owns in slot order (ss_counter_extract_ranges),
+// so every received run is sorted by region.  k_run_bounds finds where each owned region starts
+// in each run (thread per entry, a boundary writes the starts of the regions it crosses);
+// k_merge_runs then gives every owned region one workgroup that loads the region's table slice
+// into LDS (keys, counts, first), folds in the run segments of that region (LDS CAS claims new
+// keys, LDS 64-bit adds / mins), and writes the slice back: no global atomics, no partition
+// passes, and the owner keeps counting in its own table (non-owned regions are simply stale).
+// The sentinel key ~0 (EMPTY) is always the last entry of the run that carries it.  Runs are given
+// as (begin, end) index pairs into the received arrays, so the receiver's own part, which is
+// already in its table, is simply left out.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_run_bounds(Tbl t, const uint64_t* __restrict__ keys,
+                                                   const uint64_t* __restrict__ run_off, uint32_t n_runs,
+                                                   uint32_t reg_lo, uint32_t nreg, uint32_t* __restrict__ bounds) {
+    // run_off: (begin, end) pairs; entries outside every run (e.g. this rank's own part) are skipped
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t run = 0;
+    while (run < n_runs && !(run_off[2 * run] <= i && i < run_off[2 * run + 1])) ++run;
+    if (run == n_runs) return;
+    const uint64_t beg = run_off[2 * run], end = run_off[2 * run + 1];
+    auto rel = [&](uint64_t j) -> uint32_t {    // region relative to reg_lo; the sentinel sorts last
+        const uint64_t k = keys[j];
+        if (k == kEmpty) return nreg;
+        const uint32_t r = region_of(t, k);
+        return r < reg_lo ? 0u : min(r - reg_lo, nreg);
+    };
+    const uint32_t r = rel(i);
+    const uint32_t prev = i == beg ? 0u : rel(i - 1) + 1u;   // regions [prev, r] start at i
+    uint32_t* b = bounds + (uint64_t)run * (nreg + 1);
+    for (uint32_t q = (i == beg ? 0u : prev); q <= r; ++q) b[q] = (uint32_t)(i - beg);
+    if (i + 1 == end)                                          // regions after the last entry: empty
+        for (uint32_t q = r + 1; q <= nreg; ++q) b[q] = (uint32_t)(end - beg);
+}
+
+constexpr uint32_t kMergeT = 512;
+
+__global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, const uint64_t* __restrict__ keys,
+                                                       const uint64_t* __restrict__ counts,
+                                                       const uint64_t* __restrict__ first,
+                                                       const uint64_t* __restrict__ run_off, uint32_t n_runs,
+                                                       uint32_t reg_lo, uint32_t nreg,
+                                                       const uint32_t* __restrict__ bounds) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t S = (uint32_t)t.slice_mask + 1;
+    unsigned long long* skey = (unsigned long long*)smem;     // [S]
+    unsigned long long* scnt = skey + S;                       // [S] counts (not complemented)
+    unsigned long long* sfst = scnt + S;                       // [S]
+    const uint32_t j = blockIdx.x;                             // owned region reg_lo + j
+    const uint64_t base = (uint64_t)(reg_lo + j) << t.slice_log;
+    for (uint32_t q = threadIdx.x; q < S; q += kMergeT) {
+        const Slot& sl = t.slots[base + q];
+        skey[q] = sl.key;
+        scnt[q] = ~sl.ncount;
+        sfst[q] = sl.first;
+    }
+    __syncthreads();
+    for (uint32_t run = 0; run < n_runs; ++run) {
+        const uint64_t r0 = run_off[2 * run];
+        if (run_off[2 * run + 1] == r0) continue;              // empty run: no bounds were written
+        const uint32_t* b = bounds + (uint64_t)run * (nreg + 1);
+        const uint32_t lo = b[j], hi = b[j + 1];
+        for (uint32_t e = lo + threadIdx.x; e < hi; e += kMergeT) {
+            const uint64_t key = keys[r0 + e];
+            const unsigned long long c = counts[r0 + e], f = first[r0 + e];
+            uint32_t off = (uint32_t)(slot_top(t, key) & t.slice_mask);
+            uint32_t probe = 0;
+            for (; probe < S; ++probe) {
+                const unsigned long long cur = skey[off];
+                if (cur == key) break;
+                if (cur == kEmpty) {
+                    const unsigned long long prev = atomicCAS(&skey[off], (unsigned long long)kEmpty,
+                                                              (unsigned long long)key);
+                    if (prev == kEmpty || prev == key) break;
+                }
+                off = (off + 1) & (uint32_t)t.slice_mask;
+            }
+            if (probe == S) {
+                atomicOr(t.overflow, 1ull);
+                continue;
+            }
+            atomicAdd(&scnt[off], c);
+            atomicMin(&sfst[off], f);
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < S; q += kMergeT) {
+        Slot* sl = &t.slots[base + q];
+        sl->key = skey[q];
+        sl->ncount = ~scnt[q];
+        sl->first = sfst[q];
+    }
+}
+
+// the sentinel key (~0 = "G" * 32) of each run: the last entry, if any
+__global__ void k_merge_sentinel(Tbl t, const uint64_t* keys, const uint64_t* counts, const uint64_t* first,
+                                 const uint64_t* run_off, uint32_t n_runs) {
+    if (threadIdx.x != 0) return;
+    for (uint32_t run = 0; run < n_runs; ++run) {
+        const uint64_t beg = run_off[2 * run], end = run_off[2 * run + 1];
+        if (end > beg && keys[end - 1] == kEmpty) {
+            Slot* sl = &t.slots[t.mask + 1];
+            atomicAdd(&sl->ncount, 0ull - counts[end - 1]);
+            atomicMin(&sl->first, first[end - 1]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Multi-word keys (33..1024 nt: W = ceil(L/32) words; ShortSeq192 / ShortSeqVar keys,
 // short_seq_192.pyx:35-41 / short_seq_var.pyx:22-28: equal iff length and all words equal).
 // The reads are packed first (ss_encode_fixed into ws_words), keyed by a 64-bit fingerprint of
@@ -1581,16 +1705,17 @@ int ss_counter_overflow(ss_counter* c, uint64_t* d_flag, void* stream) {
 
 static int extract_impl(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens, uint64_t* d_words,
                         uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
-                        void* stream) {
+                        void* stream, bool ranges = false) {
     if (n_parts == 0 || n_parts > kMaxParts) return ss_fail(SS_EARG, "n_parts must be in 1..64");
     if (!d_keys || !d_lens || !d_counts || !d_first || !d_part_counts) return ss_fail(SS_EARG, "null buffer");
     hipStream_t s = (hipStream_t)stream;
     Tbl t = tbl_of(c);
     unsigned long long* bc = c->work + 1;
-    hipLaunchKernelGGL(k_part_count, dim3(kExtractBlocks), dim3(kThreads), 0, s, t, n_parts, bc);
+    hipLaunchKernelGGL(k_part_count, dim3(kExtractBlocks), dim3(kExtractT), 0, s, t, n_parts, bc, ranges);
     hipLaunchKernelGGL(k_part_offsets, dim3(1), dim3(1024), 0, s, n_parts, bc, (unsigned long long*)d_part_counts);
-    hipLaunchKernelGGL(k_part_scatter, dim3(kExtractBlocks), dim3(kThreads), 0, s, t, n_parts, c->L < 0 ? 0 : c->L,
-                       (const unsigned long long*)bc, d_keys, d_lens, d_counts, d_first, cap, c->work, d_words);
+    hipLaunchKernelGGL(k_part_scatter, dim3(kExtractBlocks), dim3(kExtractT), 0, s, t, n_parts, c->L < 0 ? 0 : c->L,
+                       (const unsigned long long*)bc, d_keys, d_lens, d_counts, d_first, cap, c->work, d_words,
+                       ranges);
     return ss_check(hipGetLastError(), "ss_counter_extract");
 }
 
@@ -1600,6 +1725,48 @@ int ss_counter_extract(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32
     if (!c) return ss_fail(SS_EARG, "null counter");
     if (c->W > 1) return ss_fail(SS_EARG, "multi-word keys (L > 32): use ss_counter_extract_words");
     return extract_impl(c, n_parts, d_keys, d_lens, nullptr, d_counts, d_first, cap, d_part_counts, stream);
+}
+
+int ss_counter_geometry(const ss_counter* c, uint32_t* h_log2cap, uint32_t* h_slice_log) {
+    if (!c || !h_log2cap || !h_slice_log) return ss_fail(SS_EARG, "null argument");
+    *h_log2cap = c->log2cap;
+    *h_slice_log = c->slice_log;
+    return SS_OK;
+}
+
+int ss_counter_extract_ranges(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint32_t* d_lens,
+                              uint64_t* d_counts, uint64_t* d_first, uint64_t cap, uint64_t* d_part_counts,
+                              void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->W > 1) return ss_fail(SS_EARG, "region-range extraction takes single-word keys (L <= 32)");
+    return extract_impl(c, n_parts, d_keys, d_lens, nullptr, d_counts, d_first, cap, d_part_counts, stream, true);
+}
+
+int ss_counter_merge_runs(ss_counter* c, const uint64_t* d_keys, const uint64_t* d_counts, const uint64_t* d_first,
+                          const uint64_t* d_run_offsets, uint32_t n_runs, uint64_t m, uint32_t part,
+                          uint32_t n_parts, uint32_t L, uint32_t* d_bounds, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->W > 1 || L > 32) return ss_fail(SS_EARG, "merge_runs takes single-word keys (L <= 32)");
+    if (n_parts == 0 || part >= n_parts || n_runs == 0 || n_runs > kMaxParts) return ss_fail(SS_EARG, "bad part / runs");
+    int rc = fix_length(c, L);
+    if (rc) return rc;
+    const uint64_t R = c->cap >> c->slice_log;
+    const uint32_t reg_lo = (uint32_t)((part * R + n_parts - 1) / n_parts);
+    const uint32_t reg_hi = (uint32_t)(((part + 1) * R + n_parts - 1) / n_parts);
+    const uint32_t nreg = reg_hi - reg_lo;
+    if (m == 0) return SS_OK;
+    if (!d_keys || !d_counts || !d_first || !d_run_offsets || !d_bounds) return ss_fail(SS_EARG, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    Tbl t = tbl_of(c);
+    hipLaunchKernelGGL(k_run_bounds, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, t, d_keys, d_run_offsets,
+                       n_runs, reg_lo, nreg, d_bounds);
+    if (nreg) {
+        const size_t lds = (size_t)3 * ((size_t)1 << c->slice_log) * 8;
+        hipLaunchKernelGGL(k_merge_runs, dim3(nreg), dim3(kMergeT), lds, s, t, d_keys, d_counts, d_first,
+                           d_run_offsets, n_runs, reg_lo, nreg, (const uint32_t*)d_bounds);
+    }
+    hipLaunchKernelGGL(k_merge_sentinel, dim3(1), dim3(64), 0, s, t, d_keys, d_counts, d_first, d_run_offsets, n_runs);
+    return ss_check(hipGetLastError(), "ss_counter_merge_runs");
 }
 
 int ss_counter_words(const ss_counter* c) { return c ? (int)c->W : 0; }

@@ -1,12 +1,17 @@
 """Sharded ShortSeqCounter across GPUs: one process per GPU, torch.distributed.
 
+Region-range ownership: the table's R regions (slices of 2048 slots, the unit the partitioned
+insert aggregates) are split into `world` contiguous ranges, rank p owning
+[ceil(p R / world), ceil((p + 1) R / world)); every rank's table has the same geometry.
   1. each rank counts its contiguous shard of the read stream in its own HBM table
-     (GpuCounter.insert: fused encode + hash + atomic count + first-occurrence index);
-  2. the table is compacted and partitioned by owner = hash(key) % world (GpuCounter.extract);
+     (GpuCounter.insert: fused encode + partitioned LDS aggregation);
+  2. it extracts the entries of the OTHER ranks' regions, grouped by owner and sorted by region
+     (GpuCounter.extract_ranges, one pass over the table);
   3. ONE exchange step: all_to_all_single of the per-owner sizes, then of the (key, count, first)
      triples — RCCL over xGMI on MI355X (backend "nccl"), gloo in the CPU tests;
-  4. each owner merges what it received (GpuCounter.merge: counts add, first index = min).
-The result is the union of disjoint owner tables; gather_items() brings it to one rank in
+  4. each rank folds what it received into its OWN table's owned regions (GpuCounter.merge_runs:
+     one workgroup per region, the region's slice in LDS, no global atomics, no second table).
+The result is the union of the ranks' owned regions; gather_items() brings it to one rank in
 first-occurrence order (the reference dict's insertion order, counter.pyx:41-54).
 
 Encode / decode / hamming need no collective at all: their shards are independent.
@@ -33,19 +38,32 @@ def owner_of_np(keys: np.ndarray, nparts: int) -> np.ndarray:
     return ((z >> np.uint64(32)) % np.uint64(nparts)).astype(np.int64)
 
 
+def owner_of_region_np(keys: np.ndarray, nparts: int, log2cap: int, slice_log: int) -> np.ndarray:
+    """Host mirror of the region-range owner (csrc/ss_counter.hip part_of, ranges = true): region =
+    top log2cap bits of the Fibonacci hash >> slice_log; owner = region * nparts // R."""
+    k = keys.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        h = k * np.uint64(0x9E3779B97F4A7C15)
+    top = (h >> np.uint64(64 - log2cap)) if log2cap > 0 else np.zeros_like(h)
+    region = (top >> np.uint64(slice_log)).astype(np.int64)
+    R = 1 << (log2cap - slice_log)
+    return region * nparts // R
+
+
 def exchange(keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, part_counts: torch.Tensor,
-             group=None):
+             group=None, with_sizes: bool = False):
     """All-to-all of owner-grouped (key, count, first) int64 triples.
 
     keys/counts/first: entries grouped by destination rank, part_counts[r] of them for rank r (in
-    rank order).  Returns the (keys, counts, first) this rank owns, concatenated in source-rank order.
-    Works on any backend whose all_to_all_single supports uneven splits (nccl/RCCL, gloo)."""
+    rank order).  Returns the (keys, counts, first) this rank receives, concatenated in source-rank
+    order (and the per-source sizes if with_sizes).  Works on any backend whose all_to_all_single
+    supports uneven splits (nccl/RCCL, gloo)."""
     world = dist.get_world_size(group)
     dev = keys.device
     if dev.type != "cpu" and dist.get_backend(group) == "gloo":
         # rehearsal / CPU-collective path: gloo moves host tensors only
-        k, c, f = exchange(keys.cpu(), counts.cpu(), first.cpu(), part_counts.cpu(), group)
-        return k.to(dev), c.to(dev), f.to(dev)
+        out = exchange(keys.cpu(), counts.cpu(), first.cpu(), part_counts.cpu(), group, with_sizes)
+        return tuple(x.to(dev) for x in out[:3]) + tuple(out[3:])
     sc = part_counts.to(torch.int64)
     rc = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_to_all_single(rc, sc, group=group)
@@ -55,14 +73,16 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, part
     send = torch.stack([keys[:m], counts[:m], first[:m]], 1).contiguous()
     recv = torch.empty((sum(rc_l), 3), dtype=torch.int64, device=dev)
     dist.all_to_all_single(recv, send, output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
-    return recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous()
+    out = (recv[:, 0].contiguous(), recv[:, 1].contiguous(), recv[:, 2].contiguous())
+    return out + (rc_l,) if with_sizes else out
 
 
 class ShardedCounter:
-    """Per-rank handle: a local table and (for world > 1) an owner table, reused across batches."""
+    """Per-rank handle: one table per rank (it counts the rank's reads and, after the exchange, holds
+    the rank's owned regions), reused across batches."""
 
     def __init__(self, capacity: int, device=None, group=None, table_factory=None):
-        """table_factory(capacity, device) builds the per-rank tables; default GpuCounter (HBM).
+        """table_factory(capacity, device) builds the per-rank table; default GpuCounter (HBM).
         Tests inject a host double with the same methods to exercise the exchange on gloo."""
         if table_factory is None:
             from .batch import GpuCounter as table_factory
@@ -73,43 +93,53 @@ class ShardedCounter:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
         self.local = table_factory(capacity, device=self.device)
-        self.owner = table_factory(capacity, device=self.device) if self.world > 1 else None
         self.L: Optional[int] = None
 
     def close(self) -> None:
         self.local.close()
-        if self.owner is not None:
-            self.owner.close()
 
     def count(self, ascii_local: torch.Tensor, L: int, base_index: int, check_errors: bool = True):
         """Count this rank's shard (global read indices base_index ...) and run the exchange.
-        Returns the table this rank owns afterwards (a GpuCounter)."""
+        Returns the rank's table; its owned regions hold the exact counts afterwards."""
         self.L = L
         self.local.reset()
         self.local.insert(ascii_local, L, base_index=base_index, check_errors=check_errors)
         if self.world == 1:
             return self.local
-        keys, _lens, counts, first, parts = self.local.extract(n_parts=self.world)
-        rk, rc, rf = exchange(keys, counts, first, parts, self.group)
-        self.owner.reset()
-        self.owner.merge(rk, rc, rf, L)
-        return self.owner
+        keys, _lens, counts, first, parts = self.local.extract_ranges(self.world)
+        # the rank's own part is already in its table: it travels to itself (a local copy inside the
+        # collective) and is left out of the merge
+        rk, rc, rf, rsizes = exchange(keys, counts, first, parts, group=self.group, with_sizes=True)
+        runs, pos = [], 0
+        for src, n in enumerate(rsizes):
+            if n and src != self.rank:
+                runs.append((pos, pos + n))
+            pos += n
+        self.local.merge_runs(rk, rc, rf, runs, self.rank, self.world, L)
+        return self.local
 
     def owned(self):
-        return self.owner if self.world > 1 else self.local
+        return self.local
+
+    def owned_items(self):
+        """(keys, counts, first) of the regions this rank owns, on its device."""
+        if self.world == 1:
+            keys, _l, counts, first, parts = self.local.extract(n_parts=1)
+            m = int(parts.sum().item())
+            return keys[:m], counts[:m], first[:m]
+        keys, _l, counts, first, parts = self.local.extract_ranges(self.world)
+        starts = [0] + np.cumsum(parts.cpu().numpy()).tolist()
+        a, b = int(starts[self.rank]), int(starts[self.rank + 1])
+        return keys[a:b], counts[a:b], first[a:b]
 
     def gather_items(self, dst: int = 0):
         """All owners' entries on rank `dst`, sorted by first occurrence: (keys u64, counts, first)
         as numpy arrays on dst, None elsewhere."""
-        t = self.owned()
-        keys, _lens, counts, first, parts = t.extract(n_parts=1)
-        m = int(parts.sum().item())
-        if self.world == 1:
-            k, c, f = keys[:m], counts[:m], first[:m]
-        else:
+        k, c, f = self.owned_items()
+        if self.world > 1:
             sizes = torch.zeros(self.world, dtype=torch.int64, device=self.device)
-            sizes[dst] = m
-            k, c, f = exchange(keys, counts, first, sizes, self.group)
+            sizes[dst] = k.numel()
+            k, c, f = exchange(k, c, f, sizes, self.group)
         if self.rank != dst:
             return None
         kk = k.cpu().numpy().view(np.uint64)

@@ -1,8 +1,9 @@
 """Multi-rank ShortSeqCounter protocol on CPU: world_size 2 (and 3) over gloo.
 
 The per-rank tables are a host double with GpuCounter's interface (encode via the oracle, exact
-counts / first indices, owner partition via shortseq_amd.dist.owner_of_np); the exchange, merge
-and gather logic is the product code in shortseq_amd/dist.py, the same that runs over RCCL on GPUs.
+counts / first indices, region-range ownership via shortseq_amd.dist.owner_of_region_np with the
+device table's geometry); the extract / exchange / merge / gather logic is the product code in
+shortseq_amd/dist.py, the same that runs over RCCL on GPUs.
 """
 import os
 import socket
@@ -22,12 +23,17 @@ class HostTable:
 
     def __init__(self, capacity, device=None):
         self.d = {}
+        self.log2cap = max(10, int(capacity - 1).bit_length())
+        self.slice_log = min(self.log2cap, 11)
 
     def reset(self):
         self.d = {}
 
     def close(self):
         pass
+
+    def geometry(self):
+        return self.log2cap, self.slice_log
 
     def insert(self, ascii, L, base_index=0, check_errors=True):
         import oracle
@@ -40,22 +46,40 @@ class HostTable:
             c, f = self.d.get(k, (0, 1 << 62))
             self.d[k] = (c + 1, min(f, base_index + i))
 
-    def merge(self, keys, counts, first, L):
-        for k, c, f in zip(keys.numpy().view(np.uint64).tolist(), counts.tolist(), first.tolist()):
-            c0, f0 = self.d.get(k, (0, 1 << 62))
-            self.d[k] = (c0 + c, min(f0, f))
+    def _region(self, ks):
+        with np.errstate(over="ignore"):
+            h = ks.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        return (h >> np.uint64(64 - self.log2cap)) >> np.uint64(self.slice_log)
 
-    def extract(self, n_parts=1, cap=None):
-        from shortseq_amd.dist import owner_of_np
-        ks = np.array(sorted(self.d), dtype=np.uint64)
-        own = owner_of_np(ks, n_parts) if len(ks) else np.zeros(0, np.int64)
-        o = np.argsort(own, kind="stable")
+    def _rows(self, ks, own, n_parts):
+        o = np.lexsort((ks == np.uint64(0xFFFFFFFFFFFFFFFF), self._region(ks), own)) if len(ks) else np.zeros(0, int)
         ks = ks[o]
         cs = np.array([self.d[int(k)][0] for k in ks], np.int64)
         fs = np.array([self.d[int(k)][1] for k in ks], np.int64)
         parts = np.bincount(own, minlength=n_parts).astype(np.int64)
         t = lambda x: torch.from_numpy(np.ascontiguousarray(x))  # noqa: E731
         return t(ks.view(np.int64)), t(np.full(len(ks), 32, np.int32)), t(cs), t(fs), t(parts)
+
+    def extract(self, n_parts=1, cap=None):
+        from shortseq_amd.dist import owner_of_np
+        ks = np.array(sorted(self.d), dtype=np.uint64)
+        own = owner_of_np(ks, n_parts) if len(ks) else np.zeros(0, np.int64)
+        return self._rows(ks, own, n_parts)
+
+    def extract_ranges(self, n_parts, cap=None):
+        from shortseq_amd.dist import owner_of_region_np
+        ks = np.array(sorted(self.d), dtype=np.uint64)
+        own = owner_of_region_np(ks, n_parts, self.log2cap, self.slice_log) if len(ks) else np.zeros(0, np.int64)
+        return self._rows(ks, own, n_parts)
+
+    def merge_runs(self, keys, counts, first, runs, part, n_parts, L):
+        from shortseq_amd.dist import owner_of_region_np
+        kk = keys.numpy().view(np.uint64)
+        for b, e in runs:
+            assert (owner_of_region_np(kk[b:e], n_parts, self.log2cap, self.slice_log) == part).all()
+            for k, c, f in zip(kk[b:e].tolist(), counts[b:e].tolist(), first[b:e].tolist()):
+                c0, f0 = self.d.get(k, (0, 1 << 62))
+                self.d[k] = (c0 + c, min(f0, f))
 
 
 def _worker(rank, world, port, n, L, U, q):
@@ -67,12 +91,12 @@ def _worker(rank, world, port, n, L, U, q):
         from shortseq_amd.dist import ShardedCounter
         per = n // world
         a = oracle.gen_pool_reads(5, 6, U, rank * per, per, L)
-        sc = ShardedCounter(1024, device="cpu", table_factory=HostTable)
+        sc = ShardedCounter(1 << 14, device="cpu", table_factory=HostTable)
         sc.count(torch.from_numpy(a).view(per, L), L, base_index=rank * per)
         # every owned key really belongs to this rank
-        keys, _l, _c, _f, parts = sc.owned().extract(1)
-        from shortseq_amd.dist import owner_of_np
-        own = owner_of_np(keys.numpy().view(np.uint64), world)
+        keys, _c, _f = sc.owned_items()
+        from shortseq_amd.dist import owner_of_region_np
+        own = owner_of_region_np(keys.numpy().view(np.uint64), world, *sc.local.geometry())
         assert (own == rank).all()
         res = sc.gather_items(dst=0)
         if rank == 0:
@@ -116,4 +140,12 @@ def test_owner_partition_is_balanced():
     keys = np.arange(100000, dtype=np.uint64) * np.uint64(0x9E3779B1)
     for world in (2, 4, 8):
         c = np.bincount(owner_of_np(keys, world), minlength=world)
+        assert c.min() > 0.9 * len(keys) / world
+
+
+def test_region_owner_is_balanced():
+    from shortseq_amd.dist import owner_of_region_np
+    keys = np.arange(200000, dtype=np.uint64) * np.uint64(0x9E3779B1) + np.uint64(12345)
+    for world in (2, 3, 8):
+        c = np.bincount(owner_of_region_np(keys, world, 25, 11), minlength=world)
         assert c.min() > 0.9 * len(keys) / world

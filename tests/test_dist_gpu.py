@@ -21,15 +21,14 @@ def _worker(rank, world, port, n, L, U, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import shortseq_amd.batch as B
-        from shortseq_amd.dist import ShardedCounter, owner_of_np
+        from shortseq_amd.dist import ShardedCounter, owner_of_region_np
         dev = torch.device("cuda", 0)
         per = n // world
         ascii = B.synth_pool_reads(per, L, 5, 6, U, i0=rank * per, device=dev)
         sc = ShardedCounter(1 << 16, device=dev)
         sc.count(ascii, L, base_index=rank * per)
-        keys, _l, _c, _f, parts = sc.owned().extract(1)
-        m = int(parts.sum().item())
-        own = owner_of_np(keys[:m].cpu().numpy().view(np.uint64), world)
+        keys, _c, _f = sc.owned_items()
+        own = owner_of_region_np(keys.cpu().numpy().view(np.uint64), world, *sc.local.geometry())
         assert (own == rank).all()
         res = sc.gather_items(dst=0)
         sc.close()

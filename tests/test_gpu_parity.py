@@ -373,3 +373,55 @@ def test_counter_multiword_bad_read(gpu):
     with pytest.raises(Exception):
         c.insert(ascii, L)
     c.close()
+
+
+@pytest.mark.parametrize("world,cap,U,n", [(3, 1 << 16, 20_000, 300_000), (8, 1 << 22, 500_000, 1_000_000),
+                                           (2, 1 << 12, 300, 50_000)])
+def test_counter_region_owner_merge(gpu, oracle, world, cap, U, n):
+    """Region-range ownership on one GPU: `world` tables count their shards, extract the other
+    owners' regions (region-sorted runs), each owner folds the runs into its own table; the union
+    of the owned regions equals the oracle over the whole stream (incl. the sentinel key ~0)."""
+    import torch
+    import shortseq_amd.batch as B
+    from shortseq_amd.dist import owner_of_region_np
+    L = 32
+    ascii = B.synth_pool_reads(n, L, 31, 32, U, device=gpu)
+    ascii[5] = ord("G")                        # "G" * 32: the EMPTY-colliding sentinel key
+    ascii[n - 2] = ord("G")
+    per = n // world
+    tabs = [B.GpuCounter(cap, device=gpu) for _ in range(world)]
+    ex = []
+    for r, t in enumerate(tabs):
+        hi = n if r == world - 1 else (r + 1) * per
+        t.insert(ascii[r * per:hi], L, base_index=r * per)
+        keys, _l, counts, first, parts = t.extract_ranges(world)
+        starts = [0] + np.cumsum(parts.cpu().numpy()).tolist()
+        ex.append((keys, counts, first, starts))
+    for p, t in enumerate(tabs):
+        ks, cs, fs, runs, pos = [], [], [], [], 0
+        for src in range(world):
+            keys, counts, first, starts = ex[src]
+            a, b = int(starts[p]), int(starts[p + 1])
+            ks.append(keys[a:b]), cs.append(counts[a:b]), fs.append(first[a:b])
+            if src != p and b > a:
+                runs.append((pos, pos + b - a))
+            pos += b - a
+        t.merge_runs(torch.cat(ks), torch.cat(cs), torch.cat(fs), runs, p, world, L)
+    torch.cuda.synchronize()
+    allk, allc, allf = [], [], []
+    for p, t in enumerate(tabs):
+        assert not t.overflowed()
+        keys, _l, counts, first, parts = t.extract_ranges(world)
+        starts = [0] + np.cumsum(parts.cpu().numpy()).tolist()
+        a, b = int(starts[p]), int(starts[p + 1])
+        k = keys[a:b].cpu().numpy().view(np.uint64)
+        assert (owner_of_region_np(k, world, *t.geometry()) == p).all()
+        allk.append(k), allc.append(counts[a:b].cpu().numpy()), allf.append(first[a:b].cpu().numpy())
+        t.close()
+    k, c, f = np.concatenate(allk), np.concatenate(allc), np.concatenate(allf)
+    o = np.argsort(f, kind="stable")
+    a = ascii.cpu().numpy().reshape(-1)
+    exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(n)])
+    assert [int(x) for x in k[o]] == [w[0] for (w, _L, _c, _f) in exp]
+    assert [int(x) for x in c[o]] == [cc for (_w, _L, cc, _f) in exp]
+    assert [int(x) for x in f[o]] == [ff for (_w, _L, _c, ff) in exp]

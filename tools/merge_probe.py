@@ -44,3 +44,24 @@ def merge():
 
 print(f"merge {m} entries: {t(merge):.3f} ms (incl. 1-GB table reset)", flush=True)
 print(f"reset only: {t(owner.reset):.3f} ms", flush=True)
+
+# region-range protocol: extract_ranges(8) + owner 0 folding 7 runs of ~2.1M entries
+keys, lens, counts, first, parts = local.extract_ranges(8)
+torch.cuda.synchronize()
+print(f"extract_ranges(8): {t(lambda: local.extract_ranges(8)):.3f} ms", flush=True)
+p0 = int(parts[0].item())
+k7 = keys[:p0].repeat(7)
+c7 = counts[:p0].repeat(7)
+f7 = first[:p0].repeat(7)
+runs = [(i * p0, (i + 1) * p0) for i in range(7)]
+dst = B.GpuCounter(1 << 25, device=dev)
+
+
+def merge_runs():
+    dst.reset()
+    dst.merge_runs(k7, c7, f7, runs, 0, 8, L)
+
+
+print(f"merge_runs 7 x {p0} entries into owner 0: {t(merge_runs):.3f} ms (incl. table reset)", flush=True)
+dst.merge_runs(k7, c7, f7, runs, 0, 8, L)
+assert not dst.overflowed()
