@@ -372,16 +372,19 @@ __global__ __launch_bounds__(kExtractT) void k_part_scatter(Tbl t, uint32_t npar
 // ------------------------------------------------------------------------------------------------
 // Partitioned insert (the C5 hot path).  Per-read global atomics on a 1-GB table are memory-side
 // atomic-bound; instead every table region (slice of 2^slice_log slots) is aggregated by ONE
-// workgroup in LDS and merged into its slice with plain loads/stores:
-//   P1 k_pc_keys       encode (2 lanes/read, as k_count_g16) -> keys[i]; per-block coarse histogram
-//   P2 scan            per-(block, bin) write offsets (k_pc_tot / k_pc_scan / k_pc_offsets)
-//   P3 k_pc_scatter    keys -> (key, read index) grouped by coarse bin (64 bins: long runs, so the
-//                      partial-line stores combine in L2), then k_pc_count + scan + k_pc_scatter
-//                      again by region (<= 256 regions per coarse bin) -- a 2-pass radix partition
-//   P4 k_pc_aggregate  one workgroup per region: LDS hash (CAS / add / min) over its bucket, then
-//                      each distinct key probes the region's slice (an LDS claim bitmap arbitrates
-//                      new slots inside the workgroup; nobody else touches the slice)
-// Every pass gives block b the same contiguous input range, so offsets are exact.
+// workgroup in LDS and merged into its slice with plain loads/stores.
+//   L 16 / 32, aligned rows, > 128 regions (the C5 case): the optimistic coarse partition below
+//     (k_pf_coarse: encode + coarse scatter with per-(tile, bin) atomic reservations; k_pf_count,
+//     k_pf_tot / k_pc_scan / k_pf_offsets, k_pf_scatter: fine pass by coarse bin).
+//   Otherwise the exact passes:
+//     P1 k_pc_keys (or ss_encode_fixed + k_pc_hist for other L) -> keys[i], per-block coarse histogram
+//     P2 scan      per-(block, bin) write offsets (k_pc_tot / k_pc_scan / k_pc_offsets)
+//     P3 k_pc_scatter_lds by coarse bin, then k_pc_count + scan + k_pc_scatter_lds by region
+//        (<= 256 regions per coarse bin) -- a 2-pass radix partition; every pass gives block b the
+//        same contiguous input range, so offsets are exact.
+//   P4 k_pc_aggregate_slice: one workgroup per region folds its bucket straight into an LDS copy of
+//      the region's slice (the slice is the hash table: probe, LDS CAS for a new key, LDS add / min),
+//      then writes the touched slots back; nobody else touches the slice.
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kCoarseBits = 7;    // 128 coarse bins for the first partition pass
 
@@ -956,127 +959,87 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
     }
 }
 
-// P4.  LDS: the aggregation table (2S entries of key + count + first-offset) and a copy of the
-// slice's S keys.  Phase 1 aggregates the region's bucket in LDS.  Phase 2 resolves every distinct
-// key's slot inside the LDS key copy (an LDS CAS on the copy claims a new slot; no global
-// atomics).  Phase 3 issues the global read-modify-writes of all the thread's slots together
-// (independent loads, so their latencies overlap), then the stores.
-constexpr uint32_t kAggT = 1024;
-constexpr uint32_t kAggPerThread = (2u << kSliceLogMax) / kAggT;   // LDS table slots per thread
 
+#ifndef SS_AGG_SLICE_T
+#define SS_AGG_SLICE_T 512
+#endif
+constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools/tune_counter.hip)
+
+// P4, slice-direct form: the region's slice itself is the LDS hash table.  Keys are copied into LDS
+// (16 KB for 2048 slots) next to two per-batch u32 arrays (count, first read index); every bucket
+// element probes the slice from its home slot (a new key claims an EMPTY slot with one LDS CAS),
+// then one LDS add and one LDS min.  The whole slice is written back coalesced (key, count, first
+// combined with the slot's old values).  32 KB of LDS per workgroup instead of 80 KB, one phase.
 template <int T>
-__global__ __launch_bounds__(T) void k_pc_aggregate(Tbl t, PartWs w, uint64_t base_index,
-                                                    const uint32_t* skip_if = nullptr) {
-    if (skip_if && *skip_if) return;         // the optimistic partition overflowed: direct insert instead
+__global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index,
+                                                          const uint32_t* skip_if = nullptr) {
+    if (skip_if && *skip_if) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t S = (uint32_t)t.slice_mask + 1;          // slice slots
-    const uint32_t LS = 2 * S;                               // LDS table slots (load <= 50%)
-    unsigned long long* lkey = (unsigned long long*)smem;                 // [LS]
-    unsigned long long* skey = lkey + LS;                                 // [S] slice key copy
-    uint32_t* lcnt = (uint32_t*)(skey + S);                               // [LS]
-    uint32_t* lfst = lcnt + LS;                                           // [LS]
-    uint32_t* sent = lfst + LS;                                           // [2]: sentinel count, first
+    const uint32_t S = (uint32_t)t.slice_mask + 1;
+    unsigned long long* skey = (unsigned long long*)smem;   // [S]
+    uint32_t* bcnt = (uint32_t*)(skey + S);                   // [S] this batch's count
+    uint32_t* bfst = bcnt + S;                                // [S] this batch's first read index
+    __shared__ uint32_t sent[2];
     const uint32_t region = blockIdx.x;
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
-    for (uint32_t i = threadIdx.x; i < LS; i += T) {
-        lkey[i] = kEmpty;
-        lcnt[i] = 0;
-        lfst[i] = 0xFFFFFFFFu;
+    for (uint32_t i = threadIdx.x; i < S; i += T) {
+        skey[i] = t.slots[slice_base + i].key;
+        bcnt[i] = 0;
+        bfst[i] = 0xFFFFFFFFu;
     }
-    for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = t.slots[slice_base + i].key;
     if (threadIdx.x == 0) {
         sent[0] = 0;
         sent[1] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    // phase 1: aggregate the bucket
     const uint32_t b0 = w.rstart[region], b1 = w.rstart[region + 1];
-    const uint32_t lds_shift = (t.shift >= 64 ? 64 : t.shift) - 1;   // one more hash bit than the slice
-    constexpr int kP1 = 4;   // bucket elements loaded per thread before the LDS work (latency overlap)
-    for (uint32_t e0 = b0; e0 < b1; e0 += kP1 * T) {
-        uint64_t key[kP1];
-        uint32_t idx[kP1];
+    constexpr int kP = 4;
+    for (uint32_t e0 = b0; e0 < b1; e0 += kP * T) {
+        uint64_t key[kP];
+        uint32_t idx[kP];
 #pragma unroll
-        for (int q = 0; q < kP1; ++q) {
+        for (int q = 0; q < kP; ++q) {
             const uint32_t e = e0 + q * T + threadIdx.x;
             key[q] = e < b1 ? w.bkey[e] : kEmpty;
             idx[q] = e < b1 ? w.bidx[e] : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int q = 0; q < kP1; ++q) {
+        for (int q = 0; q < kP; ++q) {
             if (idx[q] == 0xFFFFFFFFu && key[q] == kEmpty) continue;   // past the bucket
             if (key[q] == kEmpty) {
                 atomicAdd(&sent[0], 1u);
                 atomicMin(&sent[1], idx[q]);
                 continue;
             }
-            uint32_t ls = (uint32_t)((key[q] * 0x9E3779B97F4A7C15ull) >> lds_shift) & (LS - 1);
-            for (;;) {
-                const unsigned long long prev = atomicCAS(&lkey[ls], (unsigned long long)kEmpty,
-                                                          (unsigned long long)key[q]);
-                if (prev == kEmpty || prev == key[q]) break;
-                ls = (ls + 1) & (LS - 1);
+            uint32_t off = (uint32_t)(slot_top(t, key[q]) & t.slice_mask);
+            uint32_t probe = 0;
+            for (; probe < S; ++probe) {
+                const unsigned long long cur = skey[off];
+                if (cur == key[q]) break;
+                if (cur == kEmpty) {
+                    const unsigned long long prev = atomicCAS(&skey[off], (unsigned long long)kEmpty,
+                                                              (unsigned long long)key[q]);
+                    if (prev == kEmpty || prev == key[q]) break;
+                }
+                off = (off + 1) & (uint32_t)t.slice_mask;
             }
-            atomicAdd(&lcnt[ls], 1u);
-            atomicMin(&lfst[ls], idx[q]);
+            if (probe == S) {
+                atomicOr(t.overflow, 1ull);
+                continue;
+            }
+            atomicAdd(&bcnt[off], 1u);
+            atomicMin(&bfst[off], idx[q]);
         }
     }
     __syncthreads();
-    // phase 2: slot of each distinct key in the slice (LDS only)
-    uint32_t slot[kAggPerThread];
-    bool fresh[kAggPerThread];
-#pragma unroll
-    for (uint32_t j = 0; j < kAggPerThread; ++j) {
-        const uint32_t ls = j * T + threadIdx.x;
-        slot[j] = 0xFFFFFFFFu;
-        fresh[j] = false;
-        if (ls >= LS) continue;
-        const unsigned long long key = lkey[ls];
-        if (key == kEmpty) continue;
-        uint32_t off = (uint32_t)(slot_top(t, key) & t.slice_mask);
-        for (uint32_t probe = 0; probe < S; ++probe) {
-            const unsigned long long cur = skey[off];
-            if (cur == key) {
-                slot[j] = off;
-                break;
-            }
-            if (cur == kEmpty) {
-                const unsigned long long prev = atomicCAS(&skey[off], (unsigned long long)kEmpty, key);
-                if (prev == kEmpty) {
-                    slot[j] = off;
-                    fresh[j] = true;
-                    break;
-                }
-                if (prev == key) {   // cannot happen (keys are distinct in the LDS table); be safe
-                    slot[j] = off;
-                    break;
-                }
-            }
-            off = (off + 1) & (uint32_t)t.slice_mask;
-        }
-        if (slot[j] == 0xFFFFFFFFu) atomicOr(t.overflow, 1ull);
-    }
-    // phase 3: global read-modify-writes, loads first (independent), then stores
-    unsigned long long nc[kAggPerThread], fs[kAggPerThread];
-#pragma unroll
-    for (uint32_t j = 0; j < kAggPerThread; ++j) {
-        nc[j] = ~0ull;
-        fs[j] = ~0ull;
-        if (slot[j] != 0xFFFFFFFFu && !fresh[j]) {
-            const Slot* sl = &t.slots[slice_base + slot[j]];
-            nc[j] = sl->ncount;
-            fs[j] = sl->first;
-        }
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kAggPerThread; ++j) {
-        if (slot[j] == 0xFFFFFFFFu) continue;
-        const uint32_t ls = j * T + threadIdx.x;
-        Slot* sl = &t.slots[slice_base + slot[j]];
-        const unsigned long long f = base_index + lfst[ls];
-        if (fresh[j]) sl->key = lkey[ls];
-        sl->ncount = nc[j] - lcnt[ls];
-        sl->first = f < fs[j] ? f : fs[j];
+    for (uint32_t i = threadIdx.x; i < S; i += T) {
+        if (!bcnt[i]) continue;
+        Slot* sl = &t.slots[slice_base + i];
+        const unsigned long long nc = sl->ncount, fs = sl->first;
+        const unsigned long long f = base_index + bfst[i];
+        sl->key = skey[i];
+        sl->ncount = nc - bcnt[i];
+        sl->first = f < fs ? f : fs;
     }
     if (threadIdx.x == 0 && sent[0]) {
         Slot* sl = &t.slots[t.mask + 1];
@@ -1549,7 +1512,6 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         w.R = (uint32_t)(c->cap >> c->slice_log);
         w.rbits = c->log2cap - c->slice_log;
         const uint32_t S = 1u << c->slice_log;
-        const size_t agg_lds = (size_t)2 * S * 16 + (size_t)S * 8 + 8;
         const size_t mw_lds = (size_t)2 * S * 16 + (size_t)S * 8;
         const bool two_pass = w.rbits > kCoarseBits;             // > 64 regions: coarse pass first
         const uint32_t bins1 = two_pass ? (1u << kCoarseBits) : w.R;
@@ -1570,8 +1532,6 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                 ea = hipFuncSetAttribute((const void*)k_mw_fp<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          kMaxRegions * 4);
             if (ea == hipSuccess)
-                ea = hipFuncSetAttribute((const void*)k_pc_aggregate<kAggT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         agg_max);
             if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_mw_aggregate<kMwT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          agg_max);
@@ -1612,7 +1572,8 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL(k_pf_scatter, dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill);
             w.bkey = w.keys;
-            hipLaunchKernelGGL((k_pc_aggregate<kAggT>), dim3(w.R), dim3(kAggT), agg_lds, s, t, w, base_index, ovf);
+            hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
+                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, ovf);
             // overflow (a bin past cap1): the passes above idled; insert the batch directly
             constexpr int U = 4;
             const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 256 * 16);
@@ -1651,7 +1612,8 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL((k_mw_aggregate<kMwT>), dim3(w.R), dim3(kMwT), mw_lds, s, t, w,
                                (const uint64_t*)c->ws_words, base_index);
         else
-            hipLaunchKernelGGL((k_pc_aggregate<kAggT>), dim3(w.R), dim3(kAggT), agg_lds, s, t, w, base_index);
+            hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
+                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index);
         return ss_check(hipGetLastError(), "partitioned insert");
     }
     if (fast) {
