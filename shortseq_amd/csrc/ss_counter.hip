@@ -762,16 +762,20 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                                       : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
         }
     };
-    if (blockIdx.x < tiles) load_tile(blockIdx.x);
+#ifndef SS_PF_PREFETCH
+#define SS_PF_PREFETCH 0   // register double buffer off: 190 -> fewer VGPRs, 2 blocks per CU (tune_counter A/B: -5 %)
+#endif
+    if (SS_PF_PREFETCH && blockIdx.x < tiles) load_tile(blockIdx.x);
     for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
+        if (!SS_PF_PREFETCH) load_tile(tile);
         uint4 x[RPL][2];
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
             x[j][0] = nx[j][0];
             x[j][1] = nx[j][1];
         }
-        if (tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
+        if (SS_PF_PREFETCH && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
         __syncthreads();
         uint64_t key[RPL];
         uint32_t bin[RPL], rank[RPL];
