@@ -144,6 +144,46 @@ __global__ __launch_bounds__(T) void k_enc_pers(const uint4* __restrict__ in, ui
     }
 }
 
+// wave-staged 16-B stores: a wave owns 64*U consecutive chunks (coalesced dwordx4 loads, lane l
+// takes chunk wbase + 64 j + l), writes its U u32 results to a per-wave LDS strip, and each lane
+// stores 4 consecutive results as one dwordx4 (1 KB per wave store instruction).
+template <int WPB, int U, bool NTST>
+__global__ __launch_bounds__(64 * WPB) void k_enc_wst(const uint4* __restrict__ in, uint32_t* __restrict__ out,
+                                                     uint64_t nchunks, unsigned long long* fb) {
+    __shared__ uint32_t strip[WPB][64 * U];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t wbase = ((uint64_t)blockIdx.x * WPB + wave) * (64 * U);
+    uint4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = wbase + j * 64 + lane;
+        x[j] = g < nchunks ? ld_stream(&in[g]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = wbase + j * 64 + lane;
+        const Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, true);
+        const uint32_t v = e.v | ((lane & 1u) ? swap_pair(e.cout) : 0u);
+        report_bad_div(g < nchunks && e.bad != 0u, g, 2, fb);
+        strip[wave][j * 64 + lane] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < U / 4; ++q) {
+        const uint32_t c = (q * 64 + lane) * 4;          // first of 4 consecutive chunks
+        const uint64_t g = wbase + c;
+        if (g + 3 < nchunks) {
+            const u32x4 v = {strip[wave][c], strip[wave][c + 1], strip[wave][c + 2], strip[wave][c + 3]};
+            if (NTST) __builtin_nontemporal_store(v, (u32x4*)&out[g]);
+            else *(u32x4*)&out[g] = v;
+        } else {
+            for (uint32_t k = 0; k < 4; ++k)
+                if (g + k < nchunks) out[g + k] = strip[wave][c + k];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // C3 variant: wave-owned reads, ds_bpermute gather of packed 5-bit chunk distances.
 // CPR chunks per read (even, PEXT path, L % 32 == 0, L >= 64), CPR <= 12 (two packed words).
@@ -289,7 +329,19 @@ int main(int argc, char** argv) {
         const double bytes = (double)n2 * 40;
         G16Args a = make_args(in, n2, L, w_ref, nullptr, nullptr, fb);
         printf("C2 32-nt encode, %llu reads (pass %d)\n", (unsigned long long)n2, pass);
+        launch_g16<false, true, kPathTable, 768, 2, false, true>(a, 0);
         timeit("C2 production k_encode_g16 T768 U2", bytes, [&] { launch_g16<false, true, kPathTable, 768, 2, false, true>(a, 0); });
+        if (pass == 0) {
+            CK(hipMemset(w_var, 0, n2 * 8));
+            hipLaunchKernelGGL((k_enc_wst<4, 4, true>), dim3((unsigned)((2 * n2 + 1023) / 1024)), dim3(256), 0, 0,
+                               (const uint4*)in, (uint32_t*)w_var, 2 * n2, fb);
+            same(w_ref, w_var, n2 * 8, "wst WPB4 U4 vs production");
+        }
+        timeit("C2 wst WPB4 U4 nt", bytes, [&] { hipLaunchKernelGGL((k_enc_wst<4, 4, true>), dim3((unsigned)((2 * n2 + 1023) / 1024)), dim3(256), 0, 0, (const uint4*)in, (uint32_t*)w_var, 2 * n2, fb); });
+        timeit("C2 wst WPB8 U4 nt", bytes, [&] { hipLaunchKernelGGL((k_enc_wst<8, 4, true>), dim3((unsigned)((2 * n2 + 2047) / 2048)), dim3(512), 0, 0, (const uint4*)in, (uint32_t*)w_var, 2 * n2, fb); });
+        timeit("C2 wst WPB12 U4 nt", bytes, [&] { hipLaunchKernelGGL((k_enc_wst<12, 4, true>), dim3((unsigned)((2 * n2 + 3071) / 3072)), dim3(768), 0, 0, (const uint4*)in, (uint32_t*)w_var, 2 * n2, fb); });
+        timeit("C2 wst WPB4 U8 nt", bytes, [&] { hipLaunchKernelGGL((k_enc_wst<4, 8, true>), dim3((unsigned)((2 * n2 + 2047) / 2048)), dim3(256), 0, 0, (const uint4*)in, (uint32_t*)w_var, 2 * n2, fb); });
+        timeit("C2 wst WPB8 U4", bytes, [&] { hipLaunchKernelGGL((k_enc_wst<8, 4, false>), dim3((unsigned)((2 * n2 + 2047) / 2048)), dim3(512), 0, 0, (const uint4*)in, (uint32_t*)w_var, 2 * n2, fb); });
         timeit("C2 k_encode_g16 T512 U2", bytes, [&] { launch_g16<false, true, kPathTable, 512, 2, false, true>(a, 0); });
         timeit("C2 k_encode_g16 T1024 U2", bytes, [&] { launch_g16<false, true, kPathTable, 1024, 2, false, true>(a, 0); });
         timeit("C2 k_encode_g16 T768 U1", bytes, [&] { launch_g16<false, true, kPathTable, 768, 1, false, true>(a, 0); });
