@@ -546,7 +546,9 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     int rc = reset_first_bad(d_first_bad, s);
     if (rc || n == 0) return rc;
     const uint32_t logG = log2_ceil(wpr);
-    const unsigned grid = grid_for(n << logG, kThreads, kGenGridCap);
+    // one slot per lane (no grid-stride loop): every lane's two dependent loads (offset / length,
+    // then the bytes) overlap across many resident waves; latency-bound at the capped grid
+    const unsigned grid = grid_for(n << logG, kThreads, 0x7FFFFFFFu);
     hipLaunchKernelGGL((k_encode_gen<true, false>), dim3(grid), dim3(kThreads), 0, s, d_ascii, (uint64_t)0,
                        d_offsets, d_lens, 0u, n, d_words, wpr, logG, (const uint64_t*)nullptr, 0u,
                        (uint32_t*)nullptr, (unsigned long long*)d_first_bad);

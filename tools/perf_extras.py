@@ -80,6 +80,18 @@ def main():
           f"index {ti:.3f} ms ({nbytes / ti / 1e6:.0f} GB/s), total {nbytes / (ts + ti) / 1e6:.0f} GB/s of file, "
           f"{nrec / (ts + ti) / 1e6:.0f} G records/s", flush=True)
 
+    # ragged encode straight from the FASTQ text (ss_encode_var on the index's offsets / lengths)
+    o = offs[:nrec]
+    ln = lens[:nrec]
+    words_v = torch.empty((nrec, 4), dtype=torch.int64, device=dev)
+    fbv = torch.empty(1, dtype=torch.int64, device=dev)
+    tv = timed(lambda: check(L_.ss_encode_var(buf.data_ptr(), o.data_ptr(), ln.data_ptr(), nrec, words_v.data_ptr(), 4,
+                                              fbv.data_ptr(), s), "encode_var"), args.reps)
+    gbv = nrec * (100 + 32 + 12) / 1e9
+    print(f"encode_var: {nrec} x 100 nt in FASTQ text: {tv:.3f} ms, {gbv / tv * 1e3:.0f} GB/s algorithmic "
+          f"({nrec * 100 / tv / 1e9:.2f} T nt/s)", flush=True)
+    del words_v
+
     # gather the 100-nt rows densely (stride 112)
     o = offs[:nrec]
     dense = torch.empty((nrec, 112), dtype=torch.uint8, device=dev)
