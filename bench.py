@@ -320,6 +320,66 @@ def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):
                          "note": "issued i8 MAC ops x2 (one-hot K padded to whole k-steps); dense i8 peak = 2x bf16"}}
 
 
+def bench_c1_dropin(n=1_000_000, L=32):
+    """BASELINE configs[0] (C1): 1M x 32-nt synthetic reads through the drop-in Python API —
+    sq.pack() per object (host codec) and ShortSeqCounter(list) (GPU batch path)."""
+    import shortseq_amd as sq
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # the generator only (same synthetic reads as the CPU baseline)
+    a = oracle.gen_reads(11, 0, n, L)
+    reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    t0 = time.perf_counter()
+    objs = [sq.pack(r) for r in reads]
+    t_pack = time.perf_counter() - t0
+    sq.ShortSeqCounter(reads[:100_000])                    # warm the GPU path
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    c = sq.ShortSeqCounter(reads)
+    t_cnt = time.perf_counter() - t0
+    if len(c) != len(set(reads)) or sum(c.values()) != n or str(objs[7]) != reads[7].decode():
+        raise SystemExit("PARITY FAILURE: C1 drop-in")
+    # the same API on a duplicate-heavy list (2^14-read pool): the dict the API must return is small
+    pa = oracle.gen_pool_reads(12, 13, 1 << 14, 0, n, L)
+    preads = [pa[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    t0 = time.perf_counter()
+    pc = sq.ShortSeqCounter(preads)
+    t_pool = time.perf_counter() - t0
+    if sum(pc.values()) != n:
+        raise SystemExit("PARITY FAILURE: C1 drop-in (pool)")
+    return {"reads": n, "read_len": L, "pack_per_s": n / t_pack, "counter_reads_per_s": n / t_cnt,
+            "unique": len(c), "counter_pool16k_reads_per_s": n / t_pool, "pool_unique": len(pc),
+            "note": "wall time incl. Python object creation (the reference's own API shape)"}
+
+
+def cpu_baseline_c1(n=1_000_000, L=32):
+    """The reference's own Python API on the same C1 reads (oracle/_ref, 1 host core): pack per
+    object and ShortSeqCounter(list)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    if not oracle.ref_available():
+        return None
+    if oracle.REF_DIR not in sys.path:
+        sys.path.insert(0, oracle.REF_DIR)
+    import shortseq.counter as ref_counter      # the reference, built from its sources (oracle/_ref)
+    import shortseq.short_seq as ref_sq
+    a = oracle.gen_reads(11, 0, n, L)
+    reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    t0 = time.perf_counter()
+    [ref_sq.pack(r) for r in reads]
+    t_pack = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ref_counter.ShortSeqCounter(reads)
+    t_cnt = time.perf_counter() - t0
+    pa = oracle.gen_pool_reads(12, 13, 1 << 14, 0, n, L)
+    preads = [pa[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    t0 = time.perf_counter()
+    ref_counter.ShortSeqCounter(preads)
+    t_pool = time.perf_counter() - t0
+    return {"pack_per_s": n / t_pack, "counter_reads_per_s": n / t_cnt, "counter_pool16k_reads_per_s": n / t_pool,
+            "cores": 1, "kind": "reference",
+            "sample": f"{n} x {L}-nt reads, shortseq.pack / ShortSeqCounter from oracle/_ref"}
+
+
 # ------------------------------------------------------------------------------------------------
 def cpu_baseline(L=32, target_s=10.0):
     """The reference's compiled _marshall_bytes_64 (oracle/_ref) on 1 host core over a bounded
@@ -468,12 +528,16 @@ def main():
             log("F1 FASTQ index / F4 all-pairs")
             extra["F1_fastq_index_100nt"] = bench_fastq_index(B, lib, dev)
             extra["F4_all_pairs_umi12"] = bench_all_pairs(B, lib, dev)
+            log("C1 drop-in API")
+            extra["C1_dropin_1M_32"] = bench_c1_dropin()
         result["extra"] = extra
 
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
             result["cpu_baseline"] = cpu_baseline(32, args.cpu_seconds)
+            if not args.no_extras:
+                result["cpu_baseline"]["c1_reference_api"] = cpu_baseline_c1()
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)

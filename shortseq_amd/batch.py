@@ -520,6 +520,14 @@ class GpuCounter:
               "ss_counter_extract_words")
         return fps, lens, words, counts, first, parts
 
+    def items_words(self):
+        """Host copy of (words u64 [m, W], counts, first) in table order (unsorted)."""
+        _, _, words, counts, first, parts = self.extract_words(1)
+        m = int(parts.sum().item())
+        if self.overflowed():
+            raise RuntimeError("GPU counter table overflowed; use a larger capacity")
+        return words[:m].cpu().numpy().view(np.uint64), counts[:m].cpu().numpy(), first[:m].cpu().numpy()
+
     def items_sorted_words(self):
         """Host copy of (words u64 [m, W], counts, first) sorted by first occurrence (= dict order)."""
         _, _, words, counts, first, parts = self.extract_words(1)

@@ -118,7 +118,7 @@ class LengthGroupCounter:
             self.raise_if_bad()
             groups = []
             for L, t in self.tables.items():
-                words, counts, firsts = t.items_sorted_words()
+                words, counts, firsts = t.items_words()        # unsorted: the front sorts once
                 gidx = np.concatenate(self.rows[L])
                 groups.append((L, np.ascontiguousarray(words, dtype=np.uint64), counts, gidx[firsts.astype(np.int64)]))
             return groups, (self.empty_count, self.empty_first)
@@ -131,17 +131,28 @@ class LengthGroupCounter:
         self.tables = {}
 
 
+_pinned: Optional[torch.Tensor] = None     # grow-only staging buffer (hipHostMalloc is not free)
+
+
+def _staging(nbytes: int) -> torch.Tensor:
+    global _pinned
+    if _pinned is None or _pinned.numel() < nbytes:
+        _pinned = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8).pin_memory()
+    return _pinned
+
+
 def count_list(reads: list, lens_np: np.ndarray, device: torch.device) -> "LengthGroupCounter":
-    """ShortSeqCounter(list_of_bytes) on the GPU: one pinned join, one H2D copy."""
+    """ShortSeqCounter(list_of_bytes) on the GPU: one join into pinned staging, one H2D copy."""
     gc = LengthGroupCounter(device)
     n = len(reads)
     total = int(lens_np.sum())
     if n == 0:
         return gc
-    host = torch.empty(max(total, 1), dtype=torch.uint8).pin_memory()
+    host = _staging(total)
     if total:
         host.numpy()[:total] = np.frombuffer(b"".join(reads), dtype=np.uint8)
-    src = host.to(device, non_blocking=True)
+    src = host[:max(total, 1)].to(device, non_blocking=True)
+    torch.cuda.current_stream(device).synchronize()      # the staging buffer is reused next call
     offs_np = np.zeros(n, dtype=np.int64)
     np.cumsum(lens_np[:-1], out=offs_np[1:])
     offs = torch.from_numpy(offs_np).to(device, non_blocking=True)
