@@ -243,3 +243,27 @@ def test_read_and_count_fastq(tmp_path, capsys):
     c = sq.read_and_count_fastq(str(p), device="host")
     assert [(str(k), v) for k, v in c.items()] == [("ACGT", 4), ("GGGGA", 1), ("T" * 40, 1)]
     assert "total seqs" in capsys.readouterr().out
+
+
+def test_fill_groups_order_and_empty():
+    """The GPU paths' dict rebuild (host side): keys from several length groups and the empty read
+    come out in first-occurrence order with their counts and hashes (dict lookups work)."""
+    import numpy as np
+    from shortseq_amd import _shortseq as S
+
+    def words_of(s):
+        return [int(x) for x in sq.pack(s).packed]
+    g32 = ["A" * 32, "G" * 32, "ACGT" * 8]            # "G" * 32 packs to ~0: hash -1 -> -2
+    g40 = ["C" * 40, "T" * 40]
+    w32 = np.array([words_of(s) for s in g32], dtype=np.uint64)
+    w40 = np.array([words_of(s) + [0] * (2 - len(words_of(s))) for s in g40], dtype=np.uint64)
+
+    class G:
+        def finish(self):
+            return ([(32, w32, np.array([3, 1, 2]), np.array([7, 2, 9])),
+                     (40, w40, np.array([5, 4]), np.array([0, 8]))], (6, 4))
+    c = ShortSeqCounter()
+    S._fill_groups(c, G())
+    assert [(str(k), v) for k, v in c.items()] == [
+        ("C" * 40, 5), ("G" * 32, 1), ("", 6), ("A" * 32, 3), ("T" * 40, 4), ("ACGT" * 8, 2)]
+    assert c[sq.pack("G" * 32)] == 1 and c[sq.pack("ACGT" * 8)] == 2 and c[sq.pack("")] == 6
