@@ -14,10 +14,10 @@ Documented deviations (DESIGN.md §6): hash() and the counter agree for every ke
 inserts with the raw word, so counts[pack("G"*32)] raises KeyError there); ShortSeqVar keys are
 deduplicated by content (reference Q6 keys them by heap pointer).
 """
-from libc.stdint cimport uint8_t, uint64_t, int64_t, int32_t
+from libc.stdint cimport uint8_t, uint64_t, int64_t, int32_t, int16_t
 from libc.string cimport memcmp, memcpy, memset, strlen
 from libc.stdio cimport FILE, fopen, fclose
-from libc.stdlib cimport free
+from libc.stdlib cimport free, malloc, calloc
 from cpython.bytes cimport PyBytes_AS_STRING, PyBytes_GET_SIZE, PyBytes_FromStringAndSize
 from cpython.mem cimport PyObject_Calloc, PyObject_Free
 from cpython.unicode cimport PyUnicode_DecodeASCII
@@ -445,8 +445,10 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, device):
     import numpy as np
     from . import ingest
 
-    cdef Py_ssize_t i, n = PyList_GET_SIZE(reads)
+    cdef Py_ssize_t i, n = PyList_GET_SIZE(reads), ln
+    cdef size_t total = 0
     cdef object item
+    cdef char* dst
     lens_np = np.empty(n, dtype=np.int64)
     cdef int64_t[:] lens = lens_np
     for i in range(n):
@@ -456,68 +458,114 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, device):
             _raise_first_error(reads, i)
             raise TypeError(f"expected bytes, {type(item).__name__} found")
         lens[i] = PyBytes_GET_SIZE(item)
-    gc = ingest.count_list(reads, lens_np, _resolve_device(device))
+        total += lens[i]
+    # concatenate straight into the pinned staging buffer (no intermediate joined bytes object)
+    dst = <char*><size_t>ingest._staging(total).data_ptr()
+    for i in range(n):
+        ln = lens[i]
+        memcpy(dst, PyBytes_AS_STRING(<object>PyList_GET_ITEM(reads, i)), ln)
+        dst += ln
+    gc = ingest.count_list(reads, lens_np, _resolve_device(device), staged=True)
     _fill_from_groups(self, gc)
 
 
-cdef _fill_from_groups(ShortSeqCounter self, gc):
-    """Insert the per-length GPU results into the dict in first-occurrence (= reference) order: the
-    groups' first indices ordered by one O(n) scatter, then a typed loop that builds each key
-    object and inserts it with its known hash (no per-key Python tuples, sort or __hash__ call)."""
+def _order_groups_host(groups):
+    """finish() groups in any row order -> (groups sorted by first index, group sequence or None);
+    the host-side equivalent of LengthGroupCounter.finish_ordered's device sort."""
     import numpy as np
-    cdef uint64_t[:, ::1] kv
-    cdef int64_t[::1] cnt_v, grp_v, row_v, order_v, f_v
-    cdef Py_ssize_t i, m, g, row, cur_g = -1, o
+    out, firsts = [], []
+    for (Lg, w, c, f) in groups:
+        f = np.asarray(f, dtype=np.int64)
+        o = np.argsort(f, kind="stable")
+        out.append((Lg, np.ascontiguousarray(np.asarray(w, dtype=np.uint64)[o]), np.asarray(c, dtype=np.int64)[o],
+                    f[o]))
+        firsts.append(f[o])
+    if len(out) <= 1:
+        return out, None
+    allf = np.concatenate(firsts)
+    allg = np.repeat(np.arange(len(out), dtype=np.int16), [len(f) for f in firsts])
+    return out, allg[np.argsort(allf, kind="stable")]
+
+
+cdef _fill_from_groups(ShortSeqCounter self, gc):
+    """Insert the per-length GPU results into the dict in first-occurrence (= reference) order.
+    The order comes from the device (gc.finish_ordered: every group sorted by first index plus the
+    group of each key in global order), so this loop reads every array front to back, builds each
+    key object and inserts it with its known hash: no per-key __hash__ call, tuple or sort.  (A
+    presized scratch dict merged into self measured slower: the merge re-touches every key.)"""
+    import numpy as np
+    cdef int16_t[::1] gseq_v
+    cdef Py_ssize_t i, m = 0, ng, g = 0
     cdef int64_t ef = 0
-    cdef bint empty_pending
-    cdef size_t L = 0
+    cdef bint empty_pending, one = True
     cdef Py_hash_t h
-    groups, (ecount, efirst) = gc.finish()
+    cdef const uint64_t* wp
+    cdef int64_t[::1] cv
+    cdef int64_t[::1] fv
+    if hasattr(gc, "finish_ordered"):
+        groups, (ecount, efirst), gseq = gc.finish_ordered()
+    else:
+        groups, (ecount, efirst) = gc.finish()
+        groups, gseq = _order_groups_host(groups)
     if not groups:
         if ecount:
             dict.__setitem__(self, empty, ecount)
         return
-    firsts = [np.asarray(f, dtype=np.int64) for (_L, _w, _c, f) in groups]
-    sizes = [len(f) for f in firsts]
-    grp = np.repeat(np.arange(len(groups), dtype=np.int64), sizes)
-    rows = np.concatenate([np.arange(z, dtype=np.int64) for z in sizes])
-    allf = np.concatenate(firsts)
-    allc = np.concatenate([np.asarray(c, dtype=np.int64) for (_L, _w, c, _f) in groups])
-    # first indices are distinct read indices: a scatter into an index-sized array orders them in
-    # O(n) (an argsort of 1M random keys costs ~0.1 s on one core)
-    slot = np.full(int(allf.max()) + 1 if allf.size else 0, -1, dtype=np.int64)
-    slot[allf] = np.arange(allf.size, dtype=np.int64)
-    order = slot[slot >= 0]
-    words = [np.ascontiguousarray(w, dtype=np.uint64) for (_L, w, _c, _f) in groups]
-    lens = [Lg for (Lg, _w, _c, _f) in groups]
-    grp_v = grp
-    row_v = rows
-    cnt_v = allc
-    order_v = order
-    f_v = allf
-    m = order.shape[0]
-    empty_pending = ecount > 0
-    if empty_pending:
-        ef = efirst
-    for i in range(m):
-        o = order_v[i]
-        g = grp_v[o]
-        row = row_v[o]
-        if empty_pending and f_v[o] > ef:
+    ng = len(groups)
+    # per-group cursors over C pointers (the groups' arrays stay referenced by `keep`)
+    keep = []
+    cdef uint64_t** wps = <uint64_t**>malloc(ng * sizeof(uint64_t*))
+    cdef int64_t** cps = <int64_t**>malloc(ng * sizeof(int64_t*))
+    cdef int64_t** fps = <int64_t**>malloc(ng * sizeof(int64_t*))
+    cdef size_t* lens = <size_t*>malloc(ng * sizeof(size_t))
+    cdef size_t* wstride = <size_t*>malloc(ng * sizeof(size_t))
+    cdef Py_ssize_t* cur = <Py_ssize_t*>calloc(ng, sizeof(Py_ssize_t))
+    cdef uint64_t[:, ::1] kv
+    if wps == NULL or cps == NULL or fps == NULL or lens == NULL or wstride == NULL or cur == NULL:
+        free(wps); free(cps); free(fps); free(lens); free(wstride); free(cur)
+        raise MemoryError()
+    try:
+        for g in range(ng):
+            Lg, w, c, f = groups[g]
+            w = np.ascontiguousarray(w, dtype=np.uint64)
+            if w.ndim == 1:
+                w = w.reshape(-1, 1)
+            c = np.ascontiguousarray(c, dtype=np.int64)
+            f = np.ascontiguousarray(f, dtype=np.int64)
+            keep.append((w, c, f))
+            kv = w
+            cv = c
+            fv = f
+            wps[g] = &kv[0, 0] if kv.shape[0] else NULL
+            cps[g] = &cv[0] if cv.shape[0] else NULL
+            fps[g] = &fv[0] if fv.shape[0] else NULL
+            lens[g] = Lg
+            wstride[g] = kv.shape[1]
+            m += kv.shape[0]
+        if gseq is not None:
+            one = False
+            gseq_v = np.ascontiguousarray(gseq, dtype=np.int16)
+        empty_pending = ecount > 0
+        if empty_pending:
+            ef = efirst
+        for i in range(m):
+            if not one:
+                g = gseq_v[i]
+            if empty_pending and fps[g][cur[g]] > ef:
+                dict.__setitem__(self, empty, ecount)
+                empty_pending = False
+            wp = wps[g] + cur[g] * wstride[g]
+            # the objects' own __hash__ (packed word 0; CPython maps -1 to -2), given to the dict
+            # directly as the reference's counter does (counter.pyx:44-50)
+            h = <Py_hash_t>wp[0]
+            if h == -1:
+                h = -2
+            _PyDict_SetItem_KnownHash(self, _from_words(wp, lens[g]), cps[g][cur[g]], h)
+            cur[g] += 1
+        if empty_pending:
             dict.__setitem__(self, empty, ecount)
-            empty_pending = False
-        if g != cur_g:
-            kv = words[g]
-            L = lens[g]
-            cur_g = g
-        # the objects' own __hash__ (packed word 0; CPython maps -1 to -2), given to the dict
-        # directly as the reference's counter does (counter.pyx:44-50)
-        h = <Py_hash_t>kv[row, 0]
-        if h == -1:
-            h = -2
-        _PyDict_SetItem_KnownHash(self, _from_words(&kv[row, 0], L), cnt_v[o], h)
-    if empty_pending:
-        dict.__setitem__(self, empty, ecount)
+    finally:
+        free(wps); free(cps); free(fps); free(lens); free(wstride); free(cur)
 
 
 def _fill_groups(ShortSeqCounter counter, gc):

@@ -45,7 +45,8 @@ class LengthGroupCounter:
         self.device = device
         self.expected = expected_reads
         self.tables: dict[int, B.GpuCounter] = {}
-        self.rows: dict[int, list] = {}          # L -> [global index arrays of the rows inserted]
+        self.rows: dict[int, list] = {}          # L -> [global indices of the rows inserted: an
+                                                 # index array, or (start, count) for a range]
         self.nrows: dict[int, int] = {}
         self.empty_count = 0
         self.empty_first: Optional[int] = None
@@ -66,12 +67,34 @@ class LengthGroupCounter:
             self.nrows[L] = 0
         return t
 
+    def _insert(self, t: B.GpuCounter, L: int, rows, m: int, ascii: torch.Tensor, stride: int,
+                fetch_row: Callable[[int], int], fetch: Callable[[int], bytes], base: int) -> None:
+        row0 = self.nrows[L]
+        t.insert(ascii, L, base_index=row0, stride=stride, check_errors=False)
+        fb = int(B.first_bad_buffer(self.device).item())
+        if fb != -1:
+            i = fetch_row(fb)
+            self._flag(base + i, fetch(i))
+        self.rows[L].append(rows)
+        self.nrows[L] = row0 + m
+
     def add(self, src: torch.Tensor, src_bytes: int, offsets: torch.Tensor, lens_np: np.ndarray, base: int,
-            fetch: Callable[[int], bytes]) -> None:
+            fetch: Callable[[int], bytes], dense: bool = False) -> None:
         """Count reads i (global index base + i): src[offsets[i] : + lens_np[i]] on the device.
-        fetch(i) returns read i's bytes (only called for a rejected read)."""
+        fetch(i) returns read i's bytes (only called for a rejected read).  dense: the reads lie
+        back to back in src (offsets = exclusive cumsum of lens), so a batch of one length is
+        counted in place with no gather."""
         lens_np = np.asarray(lens_np, dtype=np.int64)
         if lens_np.size == 0:
+            return
+        if self.bad_index is not None and base > self.bad_index:
+            return
+        L0 = int(lens_np[0])
+        if dense and 0 < L0 <= MAX_NT and int(lens_np.min()) == L0 == int(lens_np.max()):
+            m = lens_np.size
+            t = self._table(L0, m)
+            ascii = src[:m * L0] if src.dim() == 1 else src.reshape(-1)[:m * L0]
+            self._insert(t, L0, (base, m), m, ascii, L0, lambda r: r, fetch, base)
             return
         order = np.argsort(lens_np, kind="stable")
         sl = lens_np[order]
@@ -90,16 +113,9 @@ class LengthGroupCounter:
                 continue
             m = len(grp)
             sel = torch.from_numpy(grp.astype(np.int64)).to(self.device, non_blocking=True)
-            dense = B.gather_rows(src, offsets, L, sel=sel, src_bytes=src_bytes)
+            rows = B.gather_rows(src, offsets, L, sel=sel, src_bytes=src_bytes)
             t = self._table(L, m)
-            row0 = self.nrows[L]
-            t.insert(dense, L, base_index=row0, check_errors=False)
-            fb = int(B.first_bad_buffer(self.device).item())
-            if fb != -1:
-                i = int(grp[fb])
-                self._flag(base + i, fetch(i))
-            self.rows[L].append(base + grp)
-            self.nrows[L] = row0 + m
+            self._insert(t, L, base + grp, m, rows, rows.shape[1], lambda r, _g=grp: int(_g[r]), fetch, base)
 
     def raise_if_bad(self) -> None:
         if self.bad_index is None:
@@ -110,18 +126,55 @@ class LengthGroupCounter:
             raise e
         B.raise_read_error(self.bad_read, self.bad_index)
 
+    def _row_index(self, L: int) -> np.ndarray:
+        return np.concatenate([np.arange(r[0], r[0] + r[1], dtype=np.int64) if isinstance(r, tuple) else r
+                               for r in self.rows[L]])
+
     def finish(self):
-        """-> (groups, empty) with groups = [(L, words u64 [m, W], counts, first_global)] and empty =
-        (count, first_global) of the zero-length reads (count 0 if none).  Raises the reference's
-        exception first if a read was rejected."""
+        """-> (groups, empty) with groups = [(L, words u64 [m, W], counts, first_global)] in table
+        order and empty = (count, first_global) of the zero-length reads (count 0 if none).  Raises
+        the reference's exception first if a read was rejected."""
         try:
             self.raise_if_bad()
             groups = []
             for L, t in self.tables.items():
-                words, counts, firsts = t.items_words()        # unsorted: the front sorts once
-                gidx = np.concatenate(self.rows[L])
+                words, counts, firsts = t.items_words()
+                gidx = self._row_index(L)
                 groups.append((L, np.ascontiguousarray(words, dtype=np.uint64), counts, gidx[firsts.astype(np.int64)]))
             return groups, (self.empty_count, self.empty_first)
+        finally:
+            self.close()
+
+    def finish_ordered(self):
+        """As finish(), with the dict order worked out on the device: -> (groups, empty, gseq) where
+        each group's rows are sorted by global first index and gseq (int16 [total rows], None for
+        one group) names the group of every key in global first-occurrence order.  The host rebuild
+        then walks every array front to back (a random-order walk over 1M keys costs ~2x the dict
+        inserts themselves)."""
+        try:
+            self.raise_if_bad()
+            d = self.device
+            groups, dev_firsts = [], []
+            for L, t in self.tables.items():
+                _, _, words, counts, first, parts = t.extract_words(1)
+                m = int(parts.sum().item())
+                if t.overflowed():
+                    raise RuntimeError("GPU counter table overflowed; use a larger capacity")
+                rows = self.rows[L]
+                if len(rows) == 1 and isinstance(rows[0], tuple):      # one dense range: no upload
+                    gf, perm = torch.sort(first[:m] + rows[0][0])
+                else:
+                    gf, perm = torch.sort(torch.from_numpy(self._row_index(L)).to(d)[first[:m]])
+                groups.append((L, words[:m][perm].cpu().numpy().view(np.uint64), counts[:m][perm].cpu().numpy(),
+                               gf.cpu().numpy()))
+                dev_firsts.append(gf)
+            gseq = None
+            if len(groups) > 1:
+                allf = torch.cat(dev_firsts)
+                allg = torch.cat([torch.full((f.numel(),), g, dtype=torch.int16, device=d)
+                                  for g, f in enumerate(dev_firsts)])
+                gseq = allg[torch.sort(allf).indices].cpu().numpy()
+            return groups, (self.empty_count, self.empty_first), gseq
         finally:
             self.close()
 
@@ -141,22 +194,24 @@ def _staging(nbytes: int) -> torch.Tensor:
     return _pinned
 
 
-def count_list(reads: list, lens_np: np.ndarray, device: torch.device) -> "LengthGroupCounter":
-    """ShortSeqCounter(list_of_bytes) on the GPU: one join into pinned staging, one H2D copy."""
+def count_list(reads: list, lens_np: np.ndarray, device: torch.device, staged: bool = False) -> "LengthGroupCounter":
+    """ShortSeqCounter(list_of_bytes) on the GPU: the reads concatenated into pinned staging (by
+    the caller when staged=True: the Cython front copies each bytes object straight into
+    _staging(total)), one H2D copy."""
     gc = LengthGroupCounter(device)
     n = len(reads)
     total = int(lens_np.sum())
     if n == 0:
         return gc
     host = _staging(total)
-    if total:
+    if total and not staged:
         host.numpy()[:total] = np.frombuffer(b"".join(reads), dtype=np.uint8)
     src = host[:max(total, 1)].to(device, non_blocking=True)
     torch.cuda.current_stream(device).synchronize()      # the staging buffer is reused next call
     offs_np = np.zeros(n, dtype=np.int64)
     np.cumsum(lens_np[:-1], out=offs_np[1:])
     offs = torch.from_numpy(offs_np).to(device, non_blocking=True)
-    gc.add(src, total, offs, lens_np, 0, lambda i: bytes(reads[i]))
+    gc.add(src, total, offs, lens_np, 0, lambda i: bytes(reads[i]), dense=True)
     return gc
 
 
