@@ -272,6 +272,32 @@ int ss_synth_pool_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, uin
                         uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Host-resident batches (the host side stages read batches in pinned
+ * memory).  Replaces, for a whole host array, the per-object marshal/unmarshal loops the Cython front
+ * runs today (short_seq_64.pyx:96-121, util.pyx:78-140, short_seq_var.pyx:98-120).
+ * A stager owns a ring of `nslots` (2..16) pinned + device chunk slots of `chunk_bytes` each and
+ * three HIP streams (H2D, kernel, D2H); a call streams the batch through it chunk by chunk so the
+ * copies and the kernel of neighbouring chunks overlap.  Host buffers may be pageable (staged by
+ * `copy_threads` memcpy threads; 0 = the calling thread) or pinned (DMA'd directly, detected per
+ * call).  Calls are synchronous (they return when the outputs are in host memory) and must not be
+ * made concurrently on one stager.  *h_first_bad = first invalid read (input order) or UINT64_MAX;
+ * the rc stays SS_OK for data errors, as for the device entry points.
+ * ss_decode_host writes L bytes per read at h_ascii + i*stride; bytes L..stride of a row are
+ * unspecified.  d_ref_words (encode_hamming) is a device pointer, ready before the call.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct ss_stager ss_stager;
+int ss_stager_create(int device, uint64_t chunk_bytes, uint32_t nslots, uint32_t copy_threads,
+                     ss_stager** h_out);
+int ss_stager_destroy(ss_stager* st);
+int ss_encode_host(ss_stager* st, const uint8_t* h_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                   uint64_t* h_words, uint32_t wpr, uint64_t* h_first_bad);
+int ss_encode_hamming_ref_host(ss_stager* st, const uint8_t* h_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                               uint64_t* h_words, uint32_t wpr, const uint64_t* d_ref_words, uint32_t* h_out,
+                               uint64_t* h_first_bad);
+int ss_decode_host(ss_stager* st, const uint64_t* h_words, uint64_t n, uint32_t L, uint32_t wpr,
+                   uint8_t* h_ascii, uint64_t stride);
+
+/* ------------------------------------------------------------------------------------------------
  * Host codec (per-object path, no GPU): the drop-in Python objects use these for single reads,
  * where a kernel launch (~µs) would cost more than the work (SURVEY §7 hard parts).
  * ---------------------------------------------------------------------------------------------- */

@@ -71,6 +71,11 @@ SIGNATURES = [
     ("ss_fastq_scan", C.c_int, [_P, _U64, _P, _U64, _P, _P]),
     ("ss_fastq_index", C.c_int, [_P, _U64, _U64, C.c_int, _P, _P, _P, _P, _U64, _P, _P]),
     ("ss_gather_rows", C.c_int, [_P, _U64, _P, _P, _U64, _U32, _P, _U64, _P]),
+    ("ss_stager_create", C.c_int, [C.c_int, _U64, _U32, _U32, C.POINTER(C.c_void_p)]),
+    ("ss_stager_destroy", C.c_int, [_P]),
+    ("ss_encode_host", C.c_int, [_P, _P, _U64, _U32, _U64, _P, _U32, C.POINTER(C.c_uint64)]),
+    ("ss_encode_hamming_ref_host", C.c_int, [_P, _P, _U64, _U32, _U64, _P, _U32, _P, _P, C.POINTER(C.c_uint64)]),
+    ("ss_decode_host", C.c_int, [_P, _P, _U64, _U32, _U32, _P, _U64]),
     ("ss_host_encode", C.c_int, [_P, _U64, _P, C.POINTER(SsErr)]),
     ("ss_host_decode", None, [_P, _U64, _P]),
     ("ss_host_hamming", _U64, [_P, _P, _U64]),

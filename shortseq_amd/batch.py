@@ -30,7 +30,7 @@ _NO_BAD = -1  # UINT64_MAX viewed as int64
 __all__ = ["words_for", "wpr_for", "encode", "encode_var", "decode", "decode_var", "hamming_ref",
            "hamming_pair", "encode_hamming_ref", "synth_reads", "synth_pool_reads", "GpuCounter",
            "raise_read_error", "first_bad_buffer", "fastq_index", "gather_rows", "slice_fixed",
-           "slice_var", "hamming_all_pairs"]
+           "slice_var", "hamming_all_pairs", "HostStager", "host_stager", "encode_host", "decode_host"]
 
 
 def words_for(L: int) -> int:
@@ -239,6 +239,139 @@ def encode_hamming_ref(ascii: torch.Tensor, L: Optional[int], ref_words: torch.T
     if check_errors:
         _check_first_bad(fb, _fetch_row(ascii, stride, L))
     return words, dist
+
+
+def _host_rows(ascii, L: Optional[int], stride: Optional[int]):
+    """numpy uint8 [n, >=L] (rows may be padded: stride = row pitch) or flat bytes-like + L."""
+    a = np.frombuffer(ascii, dtype=np.uint8) if isinstance(ascii, (bytes, bytearray, memoryview)) else ascii
+    if not isinstance(a, np.ndarray) or a.dtype != np.uint8:
+        raise TypeError("host reads must be a uint8 numpy array or a bytes-like object")
+    if a.ndim == 2:
+        if a.strides[1] != 1 or (a.shape[0] > 1 and a.strides[0] < a.shape[1]):
+            raise ValueError("rows must be contiguous bytes")
+        L = a.shape[1] if L is None else L
+        stride = a.strides[0] if a.shape[0] > 1 else a.shape[1]
+        n = a.shape[0]
+    else:
+        if L is None:
+            raise ValueError("L is required for a flat host buffer")
+        a = np.ascontiguousarray(a).reshape(-1)
+        stride = L if stride is None else stride
+        n = a.size // stride if stride else 0
+    if not (1 <= L <= MAX_NT):
+        if L > MAX_NT:
+            raise Exception(f"Sequences longer than {MAX_NT} bases are not supported.")
+        raise ValueError("L must be >= 1")
+    if stride < L:
+        raise ValueError("stride < L")
+    return a, n, L, stride
+
+
+class HostStager:
+    """Host-resident batches through the GPU (ss_stager_*, csrc/ss_stage.hip): numpy in, numpy out.
+
+    A batch in host memory is streamed through a ring of pinned + device chunk slots on three HIP
+    streams (H2D / kernel / D2H overlapped across neighbouring chunks).  Pageable arrays are staged
+    by `copy_threads` memcpy threads; pinned arrays (torch .pin_memory().numpy()) are DMA'd
+    directly.  This is the PCIe-inclusive path for data that lives on the host; for data already
+    in HBM use encode()/decode() on tensors."""
+
+    def __init__(self, device=None, chunk_bytes: int = 64 << 20, nslots: int = 3,
+                 copy_threads: Optional[int] = None):
+        import os
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        if copy_threads is None:
+            copy_threads = int(os.environ.get("SHORTSEQ_STAGE_THREADS", min(8, os.cpu_count() or 1)))
+        h = C.c_void_p()
+        check(lib().ss_stager_create(self.device.index or 0, chunk_bytes, nslots, copy_threads, C.byref(h)),
+              "ss_stager_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().ss_stager_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 — interpreter shutdown
+            pass
+
+    @staticmethod
+    def _raise_first_bad(fb: int, a: np.ndarray, stride: int, L: int) -> None:
+        if fb != (1 << 64) - 1:
+            row = a[fb, :L] if a.ndim == 2 else a[fb * stride: fb * stride + L]
+            raise_read_error(bytes(row), fb)
+
+    def encode(self, ascii, L: Optional[int] = None, *, stride: Optional[int] = None, wpr: Optional[int] = None,
+               out: Optional[np.ndarray] = None, check_errors: bool = True) -> np.ndarray:
+        """-> packed words uint64 [n, wpr] in host memory (ss_encode_host)."""
+        a, n, L, stride = _host_rows(ascii, L, stride)
+        wpr = wpr_for(L) if wpr is None else wpr
+        if out is None:
+            out = np.empty((n, wpr), dtype=np.uint64)
+        fb = C.c_uint64()
+        torch.cuda.current_stream(self.device).synchronize()
+        check(lib().ss_encode_host(self._h, a.ctypes.data, n, L, stride, out.ctypes.data, wpr, C.byref(fb)),
+              "ss_encode_host")
+        if check_errors:
+            self._raise_first_bad(fb.value, a, stride, L)
+        return out
+
+    def encode_hamming_ref(self, ascii, L: Optional[int], ref_words, *, check_errors: bool = True):
+        """-> (words uint64 [n, wpr], distances uint32 [n]) vs one packed reference read."""
+        a, n, L, stride = _host_rows(ascii, L, None)
+        wpr = wpr_for(L)
+        ref = torch.zeros(wpr, dtype=torch.int64, device=self.device)
+        r = torch.as_tensor(np.asarray(ref_words, dtype=np.uint64).view(np.int64)).reshape(-1)[:wpr]
+        ref[:r.numel()] = r.to(self.device)
+        torch.cuda.current_stream(self.device).synchronize()
+        words = np.empty((n, wpr), dtype=np.uint64)
+        dist = np.empty(n, dtype=np.uint32)
+        fb = C.c_uint64()
+        check(lib().ss_encode_hamming_ref_host(self._h, a.ctypes.data, n, L, stride, words.ctypes.data, wpr,
+                                               ref.data_ptr(), dist.ctypes.data, C.byref(fb)),
+              "ss_encode_hamming_ref_host")
+        if check_errors:
+            self._raise_first_bad(fb.value, a, stride, L)
+        return words, dist
+
+    def decode(self, words: np.ndarray, L: int, *, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """Packed words uint64 [n, wpr] (host) -> ASCII uint8 [n, L] (host) (ss_decode_host)."""
+        w = np.ascontiguousarray(words)
+        if w.dtype not in (np.uint64, np.int64):
+            raise TypeError("words must be uint64 / int64")
+        if w.ndim == 1:
+            w = w.reshape(-1, wpr_for(L))
+        n, wpr = w.shape
+        if out is None:
+            out = np.empty((n, L), dtype=np.uint8)
+        check(lib().ss_decode_host(self._h, w.ctypes.data, n, L, wpr, out.ctypes.data, out.strides[0] if n else L),
+              "ss_decode_host")
+        return out
+
+
+_stagers: dict = {}
+
+
+def host_stager(device=None) -> HostStager:
+    """The process's default HostStager for a device (created on first use)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    st = _stagers.get(dev.index)
+    if st is None:
+        st = _stagers[dev.index] = HostStager(dev)
+    return st
+
+
+def encode_host(ascii, L: Optional[int] = None, **kw) -> np.ndarray:
+    """Host array of reads -> host array of packed words, streamed through the GPU."""
+    return host_stager(kw.pop("device", None)).encode(ascii, L, **kw)
+
+
+def decode_host(words: np.ndarray, L: int, **kw) -> np.ndarray:
+    return host_stager(kw.pop("device", None)).decode(words, L, **kw)
 
 
 def synth_reads(n: int, L: int, seed: int, *, i0: int = 0, device=None, stride: Optional[int] = None,

@@ -17,7 +17,8 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(PKG, "lib", "libshortseq_amd.so")
-HIP_SOURCES = ["ss_codec.hip", "ss_counter.hip", "ss_fastq.hip", "ss_allpairs.hip", "ss_runtime.hip"]
+HIP_SOURCES = ["ss_codec.hip", "ss_counter.hip", "ss_fastq.hip", "ss_allpairs.hip", "ss_runtime.hip",
+               "ss_stage.hip"]
 HIP_DEPS = HIP_SOURCES + ["ss_device.h", "ss_internal.h", "host_codec.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SHORTSEQ_AMD_ARCH", "gfx950")

@@ -1557,9 +1557,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             static int pf_grid = 0;
             if (!pf_grid) {
                 int dev = 0, cus = 0, per = 0;
-                hipGetDevice(&dev);
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL>, kPfT, 0);
+                (void)hipGetDevice(&dev);
+                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL>, kPfT, 0);
                 pf_grid = (cus > 0 && per > 0) ? cus * per : (int)kPartBlocks;
             }
             hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
