@@ -261,6 +261,22 @@ int ss_counter_merge_runs(ss_counter* c, const uint64_t* d_keys, const uint64_t*
                           const uint64_t* d_run_offsets, uint32_t n_runs, uint64_t m, uint32_t part,
                           uint32_t n_parts, uint32_t L, uint32_t* d_bounds, void* stream);
 
+/* Packed exchange (the multi-GPU counter's one exchange step in 16-B records instead of three u64
+ * arrays): record = {key u64, count u32 | (first - first_base) u32 << 32}.
+ * ss_counter_pack_ranges: the entries of every part except skip_part (-1 = none; the caller's own
+ *   part stays in its table), grouped by part in part order, inside a part by table region, the
+ *   sentinel key ~0 last in its owner's segment; written to d_rec (16-byte aligned, cap records);
+ *   d_part_counts[n_parts] (0 for skip_part).  One pass over the table after a partitioned insert
+ *   (its aggregate keeps the per-region occupancy), two otherwise.  A count or first - first_base
+ *   that does not fit 32 bits, or more than cap records, raises the overflow word (bits 4 / 2).
+ * ss_counter_merge_packed: as ss_counter_merge_runs for packed runs; run r's first indices are
+ *   relative to d_run_first_base[r] (the source rank's first_base). */
+int ss_counter_pack_ranges(ss_counter* c, uint32_t n_parts, int32_t skip_part, uint64_t first_base, void* d_rec,
+                           uint64_t cap, uint64_t* d_part_counts, void* stream);
+int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_run_offsets,
+                            const uint64_t* d_run_first_base, uint32_t n_runs, uint64_t m, uint32_t part,
+                            uint32_t n_parts, uint32_t L, uint32_t* d_bounds, void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):
  * read i word w: r = splitmix64(seed + i*W + w) masked to its nts, byte j = "ACTG"[(r >> 2j) & 3].

@@ -62,6 +62,8 @@ SIGNATURES = [
     ("ss_counter_geometry", C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     ("ss_counter_extract_ranges", C.c_int, [_P, _U32, _P, _P, _P, _P, _U64, _P, _P]),
     ("ss_counter_merge_runs", C.c_int, [_P, _P, _P, _P, _P, _U32, _U64, _U32, _U32, _U32, _P, _P]),
+    ("ss_counter_pack_ranges", C.c_int, [_P, _U32, _I32, _U64, _P, _U64, _P, _P]),
+    ("ss_counter_merge_packed", C.c_int, [_P, _P, _P, _P, _U32, _U64, _U32, _U32, _U32, _P, _P]),
     ("ss_synth_reads", C.c_int, [_P, _U64, _U64, _U64, _U32, _U64, _P]),
     ("ss_synth_pool_reads", C.c_int, [_P, _U64, _U64, _U64, _U64, _U64, _U32, _U64, _P]),
     ("ss_slice_fixed", C.c_int, [_P, _U64, _U32, _U32, _U32, _U32, _P, _U32, _P]),

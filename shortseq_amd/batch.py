@@ -636,6 +636,35 @@ class GpuCounter:
                                           offs.data_ptr(), len(runs), m, part, n_parts, L, bounds.data_ptr(),
                                           _stream(d)), "ss_counter_merge_runs")
 
+    def pack_ranges(self, n_parts: int, skip: int = -1, first_base: int = 0, cap: Optional[int] = None):
+        """Region-range parts as packed 16-B records (ss_counter_pack_ranges) -> (rec int64 [cap, 2],
+        part_counts int64 [n_parts]) on the device; rec[:, 0] = key, rec[:, 1] = count | (first -
+        first_base) << 32; part `skip` is left out (count 0).  Raises if a record field overflowed."""
+        cap = self.capacity + 1 if cap is None else cap
+        d = self.device
+        rec = torch.empty((cap, 2), dtype=torch.int64, device=d)
+        parts = torch.empty(n_parts, dtype=torch.int64, device=d)
+        check(lib().ss_counter_pack_ranges(self._h, n_parts, skip, first_base, rec.data_ptr(), cap, parts.data_ptr(),
+                                           _stream(d)), "ss_counter_pack_ranges")
+        return rec, parts
+
+    def merge_packed(self, rec: torch.Tensor, runs, part: int, n_parts: int, L: int) -> None:
+        """Fold region-sorted packed runs (list of (begin, end, first_base) into rec) into the regions
+        this table owns as `part` of `n_parts` (ss_counter_merge_packed)."""
+        d = self.device
+        if not runs:
+            return
+        m = rec.shape[0]
+        offs = torch.tensor([x for (b, e, _f) in runs for x in (b, e)], dtype=torch.int64).to(d, non_blocking=True)
+        bases = torch.tensor([f for (_b, _e, f) in runs], dtype=torch.int64).to(d, non_blocking=True)
+        log2cap, slice_log = self.geometry()
+        R = 1 << (log2cap - slice_log)
+        nreg = -(-(part + 1) * R // n_parts) - (-(part * R) // n_parts)
+        bounds = torch.empty(len(runs) * (nreg + 1) + 1, dtype=torch.int32, device=d)
+        check(lib().ss_counter_merge_packed(self._h, rec.data_ptr(), offs.data_ptr(), bases.data_ptr(), len(runs), m,
+                                            part, n_parts, L, bounds.data_ptr(), _stream(d)),
+              "ss_counter_merge_packed")
+
     def extract_words(self, n_parts: int = 1, cap: Optional[int] = None):
         """As extract, for any key length: (fps, lens, words [cap, W], counts, first, part_counts);
         fps = the multi-word fingerprints (the packed word itself for W = 1)."""

@@ -63,6 +63,13 @@ struct ss_counter {
     // optimistic coarse partition (k_pf_coarse): ws_akey / ws_aidx hold 128 bins of ws_cap1 slots
     uint64_t ws_cap1 = 0;
     uint32_t* ws_fill = nullptr;           // [128] bin fill counters, [128] overflow flag
+    // per-region occupancy (used slots of each slice), written by the single-word aggregate; lets
+    // ss_counter_pack_ranges skip its counting pass.  occ_src: 0 = stale, 1 = valid, 2 = valid
+    // unless the optimistic partition overflowed (ws_fill[128] != 0: the direct insert ran instead)
+    uint32_t* occ = nullptr;               // [R]
+    unsigned long long* roff = nullptr;    // [R + 2] pack scratch: region offsets, sentinel position
+    uint64_t occ_R = 0;
+    int occ_src = 0;
 };
 
 namespace {
@@ -70,6 +77,7 @@ namespace {
 struct Tbl {
     Slot* slots;
     uint64_t* keywords;   // multi-word keys only
+    uint32_t* occ;        // [R] used slots per region (written by the single-word aggregate) or null
     uint32_t W;
     unsigned long long* overflow;
     uint64_t mask;        // cap - 1
@@ -983,7 +991,7 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     unsigned long long* skey = (unsigned long long*)smem;   // [S]
     uint32_t* bcnt = (uint32_t*)(skey + S);                   // [S] this batch's count
     uint32_t* bfst = bcnt + S;                                // [S] this batch's first read index
-    __shared__ uint32_t sent[2];
+    __shared__ uint32_t sent[3];   // sentinel count, sentinel first, slice occupancy
     const uint32_t region = blockIdx.x;
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
     for (uint32_t i = threadIdx.x; i < S; i += T) {
@@ -994,6 +1002,7 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     if (threadIdx.x == 0) {
         sent[0] = 0;
         sent[1] = 0xFFFFFFFFu;
+        sent[2] = 0;
     }
     __syncthreads();
     const uint32_t b0 = w.rstart[region], b1 = w.rstart[region + 1];
@@ -1036,7 +1045,9 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         }
     }
     __syncthreads();
+    uint32_t used = 0;
     for (uint32_t i = threadIdx.x; i < S; i += T) {
+        used += skey[i] != kEmpty ? 1u : 0u;
         if (!bcnt[i]) continue;
         Slot* sl = &t.slots[slice_base + i];
         const unsigned long long nc = sl->ncount, fs = sl->first;
@@ -1044,6 +1055,11 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         sl->key = skey[i];
         sl->ncount = nc - bcnt[i];
         sl->first = f < fs ? f : fs;
+    }
+    if (t.occ) {   // the slice's occupancy after this batch (ss_counter_pack_ranges)
+        if (used) atomicAdd(&sent[2], used);
+        __syncthreads();
+        if (threadIdx.x == 0) t.occ[region] = sent[2];
     }
     if (threadIdx.x == 0 && sent[0]) {
         Slot* sl = &t.slots[t.mask + 1];
@@ -1065,7 +1081,38 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
 // as (begin, end) index pairs into the received arrays, so the receiver's own part, which is
 // already in its table, is simply left out.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_run_bounds(Tbl t, const uint64_t* __restrict__ keys,
+// Record accessors for the merge kernels: triples (three u64 arrays) or packed records.
+struct TripleRecs {
+    const uint64_t* keys;
+    const uint64_t* counts;
+    const uint64_t* first;
+    __device__ __forceinline__ uint64_t key(uint64_t j) const { return keys[j]; }
+    __device__ __forceinline__ void load(uint64_t j, uint32_t, uint64_t& k, unsigned long long& c,
+                                         unsigned long long& f) const {
+        k = keys[j];
+        c = counts[j];
+        f = first[j];
+    }
+};
+
+struct PackedRecs {
+    const uint4* rec;
+    const uint64_t* run_base;   // per run: first_base of the source rank
+    __device__ __forceinline__ uint64_t key(uint64_t j) const {
+        const uint4 v = rec[j];
+        return ((uint64_t)v.y << 32) | v.x;
+    }
+    __device__ __forceinline__ void load(uint64_t j, uint32_t run, uint64_t& k, unsigned long long& c,
+                                         unsigned long long& f) const {
+        const uint4 v = rec[j];
+        k = ((uint64_t)v.y << 32) | v.x;
+        c = v.z;
+        f = run_base[run] + v.w;
+    }
+};
+
+template <typename Recs>
+__global__ __launch_bounds__(256) void k_run_bounds(Tbl t, Recs recs,
                                                    const uint64_t* __restrict__ run_off, uint32_t n_runs,
                                                    uint32_t reg_lo, uint32_t nreg, uint32_t* __restrict__ bounds) {
     // run_off: (begin, end) pairs; entries outside every run (e.g. this rank's own part) are skipped
@@ -1075,7 +1122,7 @@ __global__ __launch_bounds__(256) void k_run_bounds(Tbl t, const uint64_t* __res
     if (run == n_runs) return;
     const uint64_t beg = run_off[2 * run], end = run_off[2 * run + 1];
     auto rel = [&](uint64_t j) -> uint32_t {    // region relative to reg_lo; the sentinel sorts last
-        const uint64_t k = keys[j];
+        const uint64_t k = recs.key(j);
         if (k == kEmpty) return nreg;
         const uint32_t r = region_of(t, k);
         return r < reg_lo ? 0u : min(r - reg_lo, nreg);
@@ -1090,9 +1137,8 @@ __global__ __launch_bounds__(256) void k_run_bounds(Tbl t, const uint64_t* __res
 
 constexpr uint32_t kMergeT = 512;
 
-__global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, const uint64_t* __restrict__ keys,
-                                                       const uint64_t* __restrict__ counts,
-                                                       const uint64_t* __restrict__ first,
+template <typename Recs>
+__global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
                                                        const uint64_t* __restrict__ run_off, uint32_t n_runs,
                                                        uint32_t reg_lo, uint32_t nreg,
                                                        const uint32_t* __restrict__ bounds) {
@@ -1116,8 +1162,9 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, const uint64_t* _
         const uint32_t* b = bounds + (uint64_t)run * (nreg + 1);
         const uint32_t lo = b[j], hi = b[j + 1];
         for (uint32_t e = lo + threadIdx.x; e < hi; e += kMergeT) {
-            const uint64_t key = keys[r0 + e];
-            const unsigned long long c = counts[r0 + e], f = first[r0 + e];
+            uint64_t key;
+            unsigned long long c, f;
+            recs.load(r0 + e, run, key, c, f);
             uint32_t off = (uint32_t)(slot_top(t, key) & t.slice_mask);
             uint32_t probe = 0;
             for (; probe < S; ++probe) {
@@ -1148,15 +1195,144 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, const uint64_t* _
 }
 
 // the sentinel key (~0 = "G" * 32) of each run: the last entry, if any
-__global__ void k_merge_sentinel(Tbl t, const uint64_t* keys, const uint64_t* counts, const uint64_t* first,
-                                 const uint64_t* run_off, uint32_t n_runs) {
+template <typename Recs>
+__global__ void k_merge_sentinel(Tbl t, Recs recs, const uint64_t* run_off, uint32_t n_runs) {
     if (threadIdx.x != 0) return;
     for (uint32_t run = 0; run < n_runs; ++run) {
         const uint64_t beg = run_off[2 * run], end = run_off[2 * run + 1];
-        if (end > beg && keys[end - 1] == kEmpty) {
+        if (end > beg && recs.key(end - 1) == kEmpty) {
+            uint64_t k;
+            unsigned long long c, f;
+            recs.load(end - 1, run, k, c, f);
             Slot* sl = &t.slots[t.mask + 1];
-            atomicAdd(&sl->ncount, 0ull - counts[end - 1]);
-            atomicMin(&sl->first, first[end - 1]);
+            atomicAdd(&sl->ncount, 0ull - c);
+            atomicMin(&sl->first, f);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Packed exchange records (ss_counter_pack_ranges / ss_counter_merge_packed): 16 B per entry,
+// {key u64, count u32 | (first - first_base) u32 << 32}, grouped by owner part and, inside a part,
+// by table region (any order inside a region).  Two thirds of the (key, count, first) u64 triples
+// extract_ranges produces, written straight into the all-to-all send buffer.
+//   k_region_occ   (only when the aggregate's occupancy is stale) used slots per region
+//   k_region_scan  one block: region offsets skipping the caller's own part, the sentinel slot at
+//                  the end of its owner's segment, part counts
+//   k_region_pack  one workgroup per region: slice -> records at the region's offset
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kPackT = 256;
+
+__device__ __forceinline__ uint32_t part_of_region(uint64_t region, uint64_t R, uint32_t nparts) {
+    return (uint32_t)(region * nparts / R);
+}
+
+__global__ __launch_bounds__(kPackT) void k_region_occ(Tbl t, const uint32_t* skip_if) {
+    if (skip_if && *skip_if == 0) return;          // the aggregate's occupancy is valid
+    __shared__ uint32_t sum;
+    if (threadIdx.x == 0) sum = 0;
+    __syncthreads();
+    const uint32_t S = (uint32_t)t.slice_mask + 1;
+    const uint64_t base = (uint64_t)blockIdx.x << t.slice_log;
+    uint32_t used = 0;
+    for (uint32_t i = threadIdx.x; i < S; i += kPackT) used += t.slots[base + i].key != kEmpty ? 1u : 0u;
+    if (used) atomicAdd(&sum, used);
+    __syncthreads();
+    if (threadIdx.x == 0) t.occ[blockIdx.x] = sum;
+}
+
+// roff[r] = first record of region r; roff[R] = the sentinel's position (or ~0), roff[R + 1] = total
+__global__ __launch_bounds__(1024) void k_region_scan(Tbl t, uint32_t R, uint32_t nparts, int32_t skip,
+                                                      unsigned long long* roff, unsigned long long* part_counts) {
+    __shared__ unsigned long long sums[1024];
+    __shared__ unsigned long long psum[kMaxParts];
+    const uint32_t per = (R + 1023) / 1024;
+    const uint32_t lo = min(R, threadIdx.x * per), hi = min(R, lo + per);
+    for (uint32_t p = threadIdx.x; p < nparts; p += 1024) psum[p] = 0;
+    unsigned long long local = 0;
+    for (uint32_t r = lo; r < hi; ++r)
+        if ((int32_t)part_of_region(r, R, nparts) != skip) local += t.occ[r];
+    sums[threadIdx.x] = local;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const unsigned long long v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0ull;
+        __syncthreads();
+        sums[threadIdx.x] += v;
+        __syncthreads();
+    }
+    // the sentinel slot (key ~0 = "G" * 32) belongs to the owner of region_of(~0); it goes last in
+    // that owner's segment, so every later part shifts by one
+    const uint32_t sreg = region_of(t, kEmpty);
+    const uint32_t sp = part_of_region(sreg, R, nparts);
+    uint64_t skey;
+    const bool sent = slot_used(t, t.mask + 1, skey) && (int32_t)sp != skip;
+    unsigned long long run = sums[threadIdx.x] - local;
+    for (uint32_t r = lo; r < hi; ++r) {
+        const uint32_t p = part_of_region(r, R, nparts);
+        const unsigned long long c = (int32_t)p != skip ? t.occ[r] : 0u;
+        roff[r] = run + (sent && p > sp ? 1u : 0u);
+        run += c;
+        if (c) atomicAdd(&psum[p], c);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // sentinel position: the end of its owner's segment (segments are in part order)
+        unsigned long long before = 0;
+        for (uint32_t p = 0; p <= sp; ++p) before += psum[p];
+        roff[R] = sent ? before : ~0ull;
+        roff[R + 1] = sums[1023] + (sent ? 1u : 0u);
+    }
+    for (uint32_t p = threadIdx.x; p < nparts; p += 1024) part_counts[p] = psum[p] + (sent && p == sp ? 1u : 0u);
+}
+
+__global__ __launch_bounds__(kPackT) void k_region_pack(Tbl t, uint32_t R, uint32_t nparts, int32_t skip,
+                                                        const unsigned long long* __restrict__ roff,
+                                                        uint64_t first_base, uint4* __restrict__ rec, uint64_t cap,
+                                                        unsigned long long* flags) {
+    const uint32_t r = blockIdx.x;
+    __shared__ unsigned long long cursor;
+    if (r == 0 && threadIdx.x == 0 && roff[R] != ~0ull) {   // the sentinel record
+        const Slot& sl = t.slots[t.mask + 1];
+        const unsigned long long c = ~sl.ncount, f = sl.first - first_base;
+        if (c >> 32 || f >> 32 || sl.first < first_base) atomicOr(flags, 4ull);
+        if (roff[R] < cap)
+            rec[roff[R]] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, (uint32_t)c, (uint32_t)f);
+        else
+            atomicOr(flags, 2ull);
+    }
+    if ((int32_t)part_of_region(r, R, nparts) == skip) return;
+    if (threadIdx.x == 0) cursor = roff[r];
+    __syncthreads();
+    const uint32_t S = (uint32_t)t.slice_mask + 1;
+    const uint64_t base = (uint64_t)r << t.slice_log;
+    constexpr int kU = 4;
+    for (uint32_t i0 = 0; i0 < S; i0 += kU * kPackT) {
+        uint4 a[kU];
+        uint64_t fs[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t i = i0 + u * kPackT + threadIdx.x;
+            if (i < S) {
+                const uint4* p = (const uint4*)&t.slots[base + i];
+                a[u] = p[0];
+                fs[u] = t.slots[base + i].first;
+            } else {
+                a[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+                fs[u] = 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const bool used = !(a[u].x == 0xFFFFFFFFu && a[u].y == 0xFFFFFFFFu);
+            const unsigned long long pos = wave_reserve(used, 0u, &cursor);
+            if (!used) continue;
+            const unsigned long long c = ~(((unsigned long long)a[u].w << 32) | a[u].z);
+            const unsigned long long f = fs[u] - first_base;
+            if (c >> 32 || f >> 32 || fs[u] < first_base) atomicOr(flags, 4ull);
+            if (pos < cap)
+                rec[pos] = make_uint4(a[u].x, a[u].y, (uint32_t)c, (uint32_t)f);
+            else
+                atomicOr(flags, 2ull);
         }
     }
 }
@@ -1322,6 +1498,7 @@ Tbl tbl_of(const ss_counter* c) {
     Tbl t;
     t.slots = c->slots;
     t.keywords = c->keywords;
+    t.occ = c->occ;
     t.W = c->W;
     t.overflow = c->work;
     t.mask = c->cap - 1;
@@ -1336,6 +1513,21 @@ unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
     if (b == 0) b = 1;
     if (cap && b > cap) b = cap;
     return (unsigned)b;
+}
+
+template <typename Recs>
+int launch_merge(ss_counter* c, Recs recs, const uint64_t* d_run_offsets, uint32_t n_runs, uint64_t m,
+                        uint32_t reg_lo, uint32_t nreg, uint32_t* d_bounds, hipStream_t s, const char* what) {
+    Tbl t = tbl_of(c);
+    hipLaunchKernelGGL((k_run_bounds<Recs>), dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, t, recs,
+                       d_run_offsets, n_runs, reg_lo, nreg, d_bounds);
+    if (nreg) {
+        const size_t lds = (size_t)3 * ((size_t)1 << c->slice_log) * 8;
+        hipLaunchKernelGGL((k_merge_runs<Recs>), dim3(nreg), dim3(kMergeT), lds, s, t, recs, d_run_offsets, n_runs,
+                           reg_lo, nreg, (const uint32_t*)d_bounds);
+    }
+    hipLaunchKernelGGL((k_merge_sentinel<Recs>), dim3(1), dim3(64), 0, s, t, recs, d_run_offsets, n_runs);
+    return ss_check(hipGetLastError(), what);
 }
 
 }  // namespace
@@ -1355,6 +1547,12 @@ int ss_counter_create(uint64_t capacity, ss_counter** out) {
     hipError_t e = hipMalloc((void**)&c->slots, (c->cap + 1) * sizeof(Slot));
     if (e == hipSuccess)
         e = hipMalloc((void**)&c->work, (1 + (size_t)kMaxParts * kExtractBlocks) * sizeof(unsigned long long));
+    const uint64_t R = c->cap >> c->slice_log;
+    if (e == hipSuccess && R <= kMaxRegions) {   // region occupancy + pack scratch (ss_counter_pack_ranges)
+        e = hipMalloc((void**)&c->occ, R * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc((void**)&c->roff, (R + 2) * sizeof(unsigned long long));
+        c->occ_R = R;
+    }
     if (e != hipSuccess) {
         ss_counter_destroy(c);
         ss_check(e, "ss_counter_create hipMalloc");
@@ -1375,6 +1573,8 @@ int ss_counter_destroy(ss_counter* c) {
     if (c->slots) (void)hipFree(c->slots);
     if (c->work) (void)hipFree(c->work);
     if (c->keywords) (void)hipFree(c->keywords);
+    if (c->occ) (void)hipFree(c->occ);
+    if (c->roff) (void)hipFree(c->roff);
     ss_counter_release(c);
     if (c->ws_hist) (void)hipFree(c->ws_hist);
     if (c->ws_rstart) (void)hipFree(c->ws_rstart);
@@ -1388,6 +1588,7 @@ int ss_counter_reset(ss_counter* c, void* stream) {
     if (!c) return ss_fail(SS_EARG, "null counter");
     hipStream_t s = (hipStream_t)stream;
     c->L = -1;
+    c->occ_src = 0;
     hipError_t e = hipMemsetAsync(c->slots, 0xFF, (c->cap + 1) * sizeof(Slot), s);
     if (e == hipSuccess) e = hipMemsetAsync(c->work, 0, sizeof(unsigned long long), s);
     return ss_check(e, "ss_counter_reset");
@@ -1476,6 +1677,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
     rc = ss_check(hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s), "reset first_bad");
     if (rc || n == 0) return rc;
     if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
+    c->occ_src = 0;   // set again below by the paths whose aggregate records the region occupancy
     Tbl t = tbl_of(c);
     const bool multi = c->W > 1;
     const bool fast = (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
@@ -1536,7 +1738,6 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                 ea = hipFuncSetAttribute((const void*)k_mw_fp<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          kMaxRegions * 4);
             if (ea == hipSuccess)
-            if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_mw_aggregate<kMwT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          agg_max);
             if (ea != hipSuccess) return ss_check(ea, "hipFuncSetAttribute (dynamic LDS)");
@@ -1583,6 +1784,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 256 * 16);
             hipLaunchKernelGGL((k_count_g16<U>), dim3(grid), dim3(kThreads), 0, s, t, (const uint4*)d_ascii,
                                stride / 16, n, L / 16, base_index, (unsigned long long*)d_first_bad, ovf);
+            c->occ_src = 2;   // valid unless the fallback ran (ws_fill[128] set)
             return ss_check(hipGetLastError(), "optimistic partitioned insert");
         }
         if (multi) {
@@ -1618,6 +1820,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         else
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index);
+        if (!multi) c->occ_src = 1;
         return ss_check(hipGetLastError(), "partitioned insert");
     }
     if (fast) {
@@ -1641,6 +1844,7 @@ int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_le
     if (!d_keys || !d_counts || !d_first) return ss_fail(SS_EARG, "null buffer");
     if (c->W > 1) return ss_fail(SS_EARG, "ss_counter_merge takes single-word keys (L <= 32)");
     const unsigned grid = grid_for(m, kThreads, 256 * 16);
+    c->occ_src = 0;
     hipLaunchKernelGGL(k_merge, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, tbl_of(c), d_keys, d_counts,
                        d_first, m);
     return ss_check(hipGetLastError(), "k_merge");
@@ -1723,16 +1927,50 @@ int ss_counter_merge_runs(ss_counter* c, const uint64_t* d_keys, const uint64_t*
     if (m == 0) return SS_OK;
     if (!d_keys || !d_counts || !d_first || !d_run_offsets || !d_bounds) return ss_fail(SS_EARG, "null buffer");
     hipStream_t s = (hipStream_t)stream;
+    c->occ_src = 0;
+    return launch_merge(c, TripleRecs{d_keys, d_counts, d_first}, d_run_offsets, n_runs, m, reg_lo, nreg, d_bounds, s,
+                        "ss_counter_merge_runs");
+}
+
+int ss_counter_pack_ranges(ss_counter* c, uint32_t n_parts, int32_t skip_part, uint64_t first_base, void* d_rec,
+                           uint64_t cap, uint64_t* d_part_counts, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->W > 1) return ss_fail(SS_EARG, "pack_ranges takes single-word keys (L <= 32)");
+    if (n_parts == 0 || n_parts > kMaxParts) return ss_fail(SS_EARG, "n_parts must be in 1..64");
+    if (skip_part < -1 || skip_part >= (int32_t)n_parts) return ss_fail(SS_EARG, "skip_part out of range");
+    if (!d_rec || !d_part_counts) return ss_fail(SS_EARG, "null buffer");
+    if ((((uintptr_t)d_rec) & 15) != 0) return ss_fail(SS_EARG, "d_rec must be 16-byte aligned");
+    if (!c->occ) return ss_fail(SS_EARG, "table too large for region packing");
+    hipStream_t s = (hipStream_t)stream;
     Tbl t = tbl_of(c);
-    hipLaunchKernelGGL(k_run_bounds, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, t, d_keys, d_run_offsets,
-                       n_runs, reg_lo, nreg, d_bounds);
-    if (nreg) {
-        const size_t lds = (size_t)3 * ((size_t)1 << c->slice_log) * 8;
-        hipLaunchKernelGGL(k_merge_runs, dim3(nreg), dim3(kMergeT), lds, s, t, d_keys, d_counts, d_first,
-                           d_run_offsets, n_runs, reg_lo, nreg, (const uint32_t*)d_bounds);
-    }
-    hipLaunchKernelGGL(k_merge_sentinel, dim3(1), dim3(64), 0, s, t, d_keys, d_counts, d_first, d_run_offsets, n_runs);
-    return ss_check(hipGetLastError(), "ss_counter_merge_runs");
+    const uint32_t R = (uint32_t)c->occ_R;
+    if (c->occ_src != 1)
+        hipLaunchKernelGGL(k_region_occ, dim3(R), dim3(kPackT), 0, s, t,
+                           c->occ_src == 2 ? (const uint32_t*)(c->ws_fill + kCB) : (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_region_scan, dim3(1), dim3(1024), 0, s, t, R, n_parts, skip_part, c->roff,
+                       (unsigned long long*)d_part_counts);
+    hipLaunchKernelGGL(k_region_pack, dim3(R), dim3(kPackT), 0, s, t, R, n_parts, skip_part,
+                       (const unsigned long long*)c->roff, first_base, (uint4*)d_rec, cap, c->work);
+    return ss_check(hipGetLastError(), "ss_counter_pack_ranges");
+}
+
+int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_run_offsets,
+                            const uint64_t* d_run_first_base, uint32_t n_runs, uint64_t m, uint32_t part,
+                            uint32_t n_parts, uint32_t L, uint32_t* d_bounds, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->W > 1 || L > 32) return ss_fail(SS_EARG, "merge_packed takes single-word keys (L <= 32)");
+    if (n_parts == 0 || part >= n_parts || n_runs == 0 || n_runs > kMaxParts) return ss_fail(SS_EARG, "bad part / runs");
+    int rc = fix_length(c, L);
+    if (rc) return rc;
+    const uint64_t R = c->cap >> c->slice_log;
+    const uint32_t reg_lo = (uint32_t)((part * R + n_parts - 1) / n_parts);
+    const uint32_t reg_hi = (uint32_t)(((part + 1) * R + n_parts - 1) / n_parts);
+    if (m == 0) return SS_OK;
+    if (!d_rec || !d_run_offsets || !d_run_first_base || !d_bounds) return ss_fail(SS_EARG, "null buffer");
+    if ((((uintptr_t)d_rec) & 15) != 0) return ss_fail(SS_EARG, "d_rec must be 16-byte aligned");
+    c->occ_src = 0;
+    return launch_merge(c, PackedRecs{(const uint4*)d_rec, d_run_first_base}, d_run_offsets, n_runs, m, reg_lo,
+                        reg_hi - reg_lo, d_bounds, (hipStream_t)stream, "ss_counter_merge_packed");
 }
 
 int ss_counter_words(const ss_counter* c) { return c ? (int)c->W : 0; }

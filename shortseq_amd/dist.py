@@ -5,11 +5,12 @@ insert aggregates) are split into `world` contiguous ranges, rank p owning
 [ceil(p R / world), ceil((p + 1) R / world)); every rank's table has the same geometry.
   1. each rank counts its contiguous shard of the read stream in its own HBM table
      (GpuCounter.insert: fused encode + partitioned LDS aggregation);
-  2. it extracts the entries of the OTHER ranks' regions, grouped by owner and sorted by region
-     (GpuCounter.extract_ranges, one pass over the table);
-  3. ONE exchange step: all_to_all_single of the per-owner sizes, then of the (key, count, first)
-     triples — RCCL over xGMI on MI355X (backend "nccl"), gloo in the CPU tests;
-  4. each rank folds what it received into its OWN table's owned regions (GpuCounter.merge_runs:
+  2. it packs the entries of the OTHER ranks' regions into 16-B records {key, count u32, first -
+     base u32}, grouped by owner and sorted by region (GpuCounter.pack_ranges: one workgroup per
+     region, one pass over the table using the occupancy the insert's aggregate recorded);
+  3. ONE exchange step: all_to_all_single of (sizes, base index) per peer, then of the records —
+     RCCL over xGMI on MI355X (backend "nccl"), gloo in the CPU tests;
+  4. each rank folds what it received into its OWN table's owned regions (GpuCounter.merge_packed:
      one workgroup per region, the region's slice in LDS, no global atomics, no second table).
 The result is the union of the ranks' owned regions; gather_items() brings it to one rank in
 first-occurrence order (the reference dict's insertion order, counter.pyx:41-54).
@@ -77,6 +78,31 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, part
     return out + (rc_l,) if with_sizes else out
 
 
+def exchange_packed(rec: torch.Tensor, part_counts: torch.Tensor, first_base: int, group=None):
+    """All-to-all of owner-grouped packed records (int64 [m, 2] = 16 B each, ss_counter_pack_ranges).
+
+    One small all-to-all carries (records for you, my first_base) per peer, then one all-to-all
+    moves the records.  Returns (received records in source-rank order, per-source sizes,
+    per-source first_base)."""
+    world = dist.get_world_size(group)
+    dev = rec.device
+    if dev.type != "cpu" and dist.get_backend(group) == "gloo":
+        out = exchange_packed(rec.cpu(), part_counts.cpu(), first_base, group)
+        return (out[0].to(dev),) + tuple(out[1:])
+    meta = torch.stack([part_counts.to(torch.int64),
+                        torch.full((world,), first_base, dtype=torch.int64, device=dev)], 1)
+    rmeta = torch.empty_like(meta)
+    dist.all_to_all_single(rmeta, meta, group=group)
+    sc_l = [int(x) for x in part_counts.tolist()]
+    rm = rmeta.tolist()
+    rc_l = [int(r[0]) for r in rm]
+    bases = [int(r[1]) for r in rm]
+    m = sum(sc_l)
+    recv = torch.empty((sum(rc_l), 2), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, rec[:m], output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
+    return recv, rc_l, bases
+
+
 class ShardedCounter:
     """Per-rank handle: one table per rank (it counts the rank's reads and, after the exchange, holds
     the rank's owned regions), reused across batches."""
@@ -106,16 +132,17 @@ class ShardedCounter:
         self.local.insert(ascii_local, L, base_index=base_index, check_errors=check_errors)
         if self.world == 1:
             return self.local
-        keys, _lens, counts, first, parts = self.local.extract_ranges(self.world)
-        # the rank's own part is already in its table: it travels to itself (a local copy inside the
-        # collective) and is left out of the merge
-        rk, rc, rf, rsizes = exchange(keys, counts, first, parts, group=self.group, with_sizes=True)
+        # the other owners' regions as 16-B records (the rank's own part stays in its table)
+        rec, parts = self.local.pack_ranges(self.world, skip=self.rank, first_base=base_index)
+        if self.local.overflowed():
+            raise RuntimeError("counter pack overflow (a count or first index past 32 bits, or the table)")
+        recv, rsizes, rbases = exchange_packed(rec, parts, base_index, group=self.group)
         runs, pos = [], 0
         for src, n in enumerate(rsizes):
-            if n and src != self.rank:
-                runs.append((pos, pos + n))
+            if n:
+                runs.append((pos, pos + n, rbases[src]))
             pos += n
-        self.local.merge_runs(rk, rc, rf, runs, self.rank, self.world, L)
+        self.local.merge_packed(recv, runs, self.rank, self.world, L)
         return self.local
 
     def owned(self):

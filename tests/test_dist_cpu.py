@@ -72,6 +72,32 @@ class HostTable:
         own = owner_of_region_np(ks, n_parts, self.log2cap, self.slice_log) if len(ks) else np.zeros(0, np.int64)
         return self._rows(ks, own, n_parts)
 
+    def overflowed(self):
+        return False
+
+    def pack_ranges(self, n_parts, skip=-1, first_base=0, cap=None):
+        """Records [m, 2] int64: key, count | (first - first_base) << 32 (ss_counter_pack_ranges)."""
+        ks, _l, cs, fs, parts = self.extract_ranges(n_parts)
+        own = np.repeat(np.arange(n_parts), parts.numpy())
+        keep = own != skip
+        c = cs.numpy()[keep].astype(np.uint64)
+        f = (fs.numpy()[keep] - first_base).astype(np.uint64)
+        assert (c < (1 << 32)).all() and (f < (1 << 32)).all()
+        rec = np.stack([ks.numpy()[keep], (c | (f << np.uint64(32))).view(np.int64)], 1)
+        parts = parts.clone()
+        if skip >= 0:
+            parts[skip] = 0
+        return torch.from_numpy(np.ascontiguousarray(rec)), parts
+
+    def merge_packed(self, rec, runs, part, n_parts, L):
+        r = rec.numpy()
+        kk = r[:, 0].view(np.uint64)
+        lo = r[:, 1].view(np.uint64) & np.uint64(0xFFFFFFFF)
+        hi = r[:, 1].view(np.uint64) >> np.uint64(32)
+        for b, e, base in runs:
+            self.merge_runs(torch.from_numpy(kk[b:e].view(np.int64)), torch.from_numpy(lo[b:e].astype(np.int64)),
+                            torch.from_numpy(hi[b:e].astype(np.int64) + base), [(0, e - b)], part, n_parts, L)
+
     def merge_runs(self, keys, counts, first, runs, part, n_parts, L):
         from shortseq_amd.dist import owner_of_region_np
         kk = keys.numpy().view(np.uint64)

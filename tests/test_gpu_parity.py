@@ -425,3 +425,105 @@ def test_counter_region_owner_merge(gpu, oracle, world, cap, U, n):
     assert [int(x) for x in k[o]] == [w[0] for (w, _L, _c, _f) in exp]
     assert [int(x) for x in c[o]] == [cc for (_w, _L, cc, _f) in exp]
     assert [int(x) for x in f[o]] == [ff for (_w, _L, _c, ff) in exp]
+
+
+@pytest.mark.parametrize("world,cap,U,n,mode", [
+    (2, 1 << 19, 5000, 300_000, "partitioned"),     # occupancy from the aggregate (one pass)
+    (2, 1 << 17, 5000, 200_000, "partitioned"),     # <= 128 regions: the exact partition passes
+    (3, 1 << 19, 40_000, 400_000, "partitioned"),
+    (8, 1 << 20, 300_000, 1_200_000, "partitioned"),
+    (3, 1 << 19, 3, 300_000, "overflow"),           # 3 keys: the optimistic partition overflows
+    (2, 1 << 16, 900, 20_000, "direct"),            # small batches: direct insert, counting pass
+])
+def test_counter_packed_exchange(gpu, oracle, world, cap, U, n, mode):
+    """The multi-GPU exchange in packed records on one GPU: `world` tables count their shards, pack
+    the other owners' regions (16-B records, first relative to the shard base), each owner folds
+    the records of every other table into its own; the union of the owned regions equals the
+    oracle over the whole stream (incl. the sentinel key ~0)."""
+    import torch
+    import shortseq_amd.batch as B
+    from shortseq_amd.dist import owner_of_region_np
+    L = 32
+    ascii = B.synth_pool_reads(n, L, 41, 42, U, device=gpu)
+    ascii[7] = ord("G")                        # "G" * 32: the EMPTY-colliding sentinel key
+    ascii[n - 3] = ord("G")
+    per = n // world
+    tabs = [B.GpuCounter(cap, device=gpu) for _ in range(world)]
+    packs = []
+    for r, t in enumerate(tabs):
+        hi = n if r == world - 1 else (r + 1) * per
+        t.insert(ascii[r * per:hi], L, base_index=r * per, partitioned=(mode != "direct"))
+        rec, parts = t.pack_ranges(world, skip=r, first_base=r * per)
+        assert not t.overflowed()
+        pc = parts.cpu().numpy()
+        assert pc[r] == 0
+        starts = [0] + np.cumsum(pc).tolist()
+        packs.append((rec, starts))
+    for p, t in enumerate(tabs):
+        segs, runs, pos = [], [], 0
+        for src in range(world):
+            rec, starts = packs[src]
+            a, b = int(starts[p]), int(starts[p + 1])
+            if b > a:
+                segs.append(rec[a:b])
+                runs.append((pos, pos + b - a, src * per))
+                pos += b - a
+        if segs:
+            t.merge_packed(torch.cat(segs), runs, p, world, L)
+    torch.cuda.synchronize()
+    allk, allc, allf = [], [], []
+    for p, t in enumerate(tabs):
+        assert not t.overflowed()
+        keys, _l, counts, first, parts = t.extract_ranges(world)
+        starts = [0] + np.cumsum(parts.cpu().numpy()).tolist()
+        a, b = int(starts[p]), int(starts[p + 1])
+        k = keys[a:b].cpu().numpy().view(np.uint64)
+        assert (owner_of_region_np(k, world, *t.geometry()) == p).all()
+        allk.append(k), allc.append(counts[a:b].cpu().numpy()), allf.append(first[a:b].cpu().numpy())
+        t.close()
+    k, c, f = np.concatenate(allk), np.concatenate(allc), np.concatenate(allf)
+    o = np.argsort(f, kind="stable")
+    a = ascii.cpu().numpy().reshape(-1)
+    exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(n)])
+    assert [int(x) for x in k[o]] == [w[0] for (w, _L, _c, _f) in exp]
+    assert [int(x) for x in c[o]] == [cc for (_w, _L, cc, _f) in exp]
+    assert [int(x) for x in f[o]] == [ff for (_w, _L, _c, ff) in exp]
+
+
+def test_counter_pack_records_layout(gpu):
+    """pack_ranges record fields and grouping: part order, region order inside a part, counts and
+    first indices relative to first_base, the sentinel last in its owner's segment."""
+    import shortseq_amd.batch as B
+    from shortseq_amd.dist import owner_of_region_np
+    L, n, world = 32, 200_000, 4
+    ascii = B.synth_pool_reads(n, L, 3, 4, 20_000, device=gpu)
+    ascii[11] = ord("G")
+    t = B.GpuCounter(1 << 18, device=gpu)
+    t.insert(ascii, L, base_index=1000)
+    rec, parts = t.pack_ranges(world, skip=-1, first_base=1000)
+    keys, _l, counts, first, eparts = t.extract_ranges(world)
+    assert np.array_equal(parts.cpu().numpy(), eparts.cpu().numpy())
+    m = int(parts.sum())
+    r = rec[:m].cpu().numpy()
+    k = r[:, 0].view(np.uint64)
+    c = (r[:, 1].view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    f = (r[:, 1].view(np.uint64) >> np.uint64(32)).astype(np.int64) + 1000
+    log2cap, slice_log = t.geometry()
+    own = owner_of_region_np(k, world, log2cap, slice_log)
+    starts = np.cumsum([0] + parts.cpu().numpy().tolist())
+    for p in range(world):
+        seg = slice(starts[p], starts[p + 1])
+        assert (own[seg] == p).all()
+        kk = k[seg]
+        notsent = kk != np.uint64(0xFFFFFFFFFFFFFFFF)
+        with np.errstate(over="ignore"):
+            reg = ((kk[notsent] * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(64 - log2cap)) >> np.uint64(slice_log)
+        assert (np.diff(reg.astype(np.int64)) >= 0).all()
+        if not notsent.all():
+            assert not notsent[-1] and notsent[:-1].all()
+    ek = keys[:m].cpu().numpy().view(np.uint64)
+    d = dict(zip(ek.tolist(), zip(counts[:m].cpu().numpy().tolist(), first[:m].cpu().numpy().tolist())))
+    assert len(d) == m
+    for kk, cc, ff in zip(k.tolist(), c.tolist(), f.tolist()):
+        assert d[kk] == (cc, ff)
+    t.close()

@@ -65,3 +65,37 @@ def merge_runs():
 print(f"merge_runs 7 x {p0} entries into owner 0: {t(merge_runs):.3f} ms (incl. table reset)", flush=True)
 dst.merge_runs(k7, c7, f7, runs, 0, 8, L)
 assert not dst.overflowed()
+
+# packed protocol: pack_ranges(8, skip=0) right after the insert (aggregate occupancy, one pass),
+# then owner 0 folding 7 packed runs
+local.reset()
+ascii = B.synth_pool_reads(n, L, 5, 77, U, device=dev)
+local.insert(ascii, L)
+del ascii
+
+
+def pack():
+    return local.pack_ranges(8, skip=0, first_base=0)
+
+
+torch.cuda.synchronize()
+rec, pparts = pack()
+torch.cuda.synchronize()
+print(f"pack_ranges(8, skip 0) after the insert: {t(pack, reps=1):.3f} ms (occupancy from the aggregate)",
+      flush=True)
+print(f"pack_ranges(8, skip 0) again: {t(pack):.3f} ms", flush=True)
+local._drop_reservation()
+local.merge(k[:1], c[:1], f[:1], L)   # any other mutation: occupancy stale -> counting pass
+print(f"pack_ranges(8, skip 0) with a counting pass: {t(pack):.3f} ms", flush=True)
+q = int(pparts[1].item())
+rec7 = rec[:q].repeat(7, 1)
+pruns = [(i * q, (i + 1) * q, 0) for i in range(7)]
+
+
+def merge_packed():
+    dst.reset()
+    dst.merge_packed(rec7, pruns, 1, 8, L)
+
+
+print(f"merge_packed 7 x {q} records into owner 1: {t(merge_packed):.3f} ms (incl. table reset)", flush=True)
+assert not dst.overflowed()
