@@ -70,6 +70,9 @@ struct ss_counter {
     unsigned long long* roff = nullptr;    // [R + 2] pack scratch: region offsets, sentinel position
     uint64_t occ_R = 0;
     int occ_src = 0;
+    // ss_counter_reset is lazy for the slot array: the next partitioned single-word insert's
+    // aggregate writes whole slices instead (fresh mode); any other access memsets first
+    bool reset_pending = false;
 };
 
 namespace {
@@ -982,12 +985,23 @@ constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools
 // element probes the slice from its home slot (a new key claims an EMPTY slot with one LDS CAS),
 // then one LDS add and one LDS min.  The whole slice is written back coalesced (key, count, first
 // combined with the slot's old values).  32 KB of LDS per workgroup instead of 80 KB, one phase.
+// fresh: the table was reset and the reset is still pending (ss_counter_reset is lazy): the slice is
+// taken as empty instead of loaded, and written back whole (empty slots as the 0xFF reset pattern),
+// which replaces the 1-GB reset memset and the slice read.  With skip_if set (the optimistic
+// partition overflowed) a fresh aggregate only performs its slice's reset.
 template <int T>
 __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index,
-                                                          const uint32_t* skip_if = nullptr) {
-    if (skip_if && *skip_if) return;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+                                                          const uint32_t* skip_if = nullptr, bool fresh = false) {
     const uint32_t S = (uint32_t)t.slice_mask + 1;
+    if (skip_if && *skip_if) {
+        if (fresh) {
+            uint4* sl = (uint4*)&t.slots[(uint64_t)blockIdx.x << t.slice_log];
+            const uint4 ff = make_uint4(~0u, ~0u, ~0u, ~0u);
+            for (uint32_t i = threadIdx.x; i < 2 * S; i += T) sl[i] = ff;
+        }
+        return;
+    }
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* skey = (unsigned long long*)smem;   // [S]
     uint32_t* bcnt = (uint32_t*)(skey + S);                   // [S] this batch's count
     uint32_t* bfst = bcnt + S;                                // [S] this batch's first read index
@@ -995,7 +1009,7 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     const uint32_t region = blockIdx.x;
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
     for (uint32_t i = threadIdx.x; i < S; i += T) {
-        skey[i] = t.slots[slice_base + i].key;
+        skey[i] = fresh ? kEmpty : t.slots[slice_base + i].key;
         bcnt[i] = 0;
         bfst[i] = 0xFFFFFFFFu;
     }
@@ -1046,7 +1060,22 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     }
     __syncthreads();
     uint32_t used = 0;
-    for (uint32_t i = threadIdx.x; i < S; i += T) {
+    if (fresh) {   // whole slots, two dwordx4 stores each (lane pairs cover one 32-B slot)
+        uint4* sl = (uint4*)&t.slots[slice_base];
+        for (uint32_t h = threadIdx.x; h < 2 * S; h += T) {
+            const uint32_t i = h >> 1;
+            const bool hit = bcnt[i] != 0;
+            if ((h & 1u) == 0) {
+                used += skey[i] != kEmpty ? 1u : 0u;
+                const unsigned long long k = skey[i], nc = ~(unsigned long long)bcnt[i];
+                sl[h] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)nc, (uint32_t)(nc >> 32));
+            } else {
+                const unsigned long long f = hit ? base_index + bfst[i] : ~0ull;
+                sl[h] = make_uint4((uint32_t)f, (uint32_t)(f >> 32), ~0u, ~0u);
+            }
+        }
+    }
+    for (uint32_t i = threadIdx.x; !fresh && i < S; i += T) {
         used += skey[i] != kEmpty ? 1u : 0u;
         if (!bcnt[i]) continue;
         Slot* sl = &t.slots[slice_base + i];
@@ -1508,6 +1537,13 @@ Tbl tbl_of(const ss_counter* c) {
     return t;
 }
 
+// Perform a pending (lazy) reset of the slot array on `s` before anything reads the table.
+int flush_reset(ss_counter* c, hipStream_t s) {
+    if (!c->reset_pending) return SS_OK;
+    c->reset_pending = false;
+    return ss_check(hipMemsetAsync(c->slots, 0xFF, c->cap * sizeof(Slot), s), "ss_counter reset");
+}
+
 unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
     uint64_t b = (items + per_block - 1) / per_block;
     if (b == 0) b = 1;
@@ -1518,6 +1554,8 @@ unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
 template <typename Recs>
 int launch_merge(ss_counter* c, Recs recs, const uint64_t* d_run_offsets, uint32_t n_runs, uint64_t m,
                         uint32_t reg_lo, uint32_t nreg, uint32_t* d_bounds, hipStream_t s, const char* what) {
+    int rc = flush_reset(c, s);
+    if (rc) return rc;
     Tbl t = tbl_of(c);
     hipLaunchKernelGGL((k_run_bounds<Recs>), dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, t, recs,
                        d_run_offsets, n_runs, reg_lo, nreg, d_bounds);
@@ -1559,6 +1597,7 @@ int ss_counter_create(uint64_t capacity, ss_counter** out) {
         return SS_ENOMEM;
     }
     int rc = ss_counter_reset(c, nullptr);
+    if (rc == SS_OK) rc = flush_reset(c, nullptr);
     if (rc == SS_OK) rc = ss_check(hipStreamSynchronize(nullptr), "ss_counter_create sync");
     if (rc) {
         ss_counter_destroy(c);
@@ -1589,7 +1628,8 @@ int ss_counter_reset(ss_counter* c, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     c->L = -1;
     c->occ_src = 0;
-    hipError_t e = hipMemsetAsync(c->slots, 0xFF, (c->cap + 1) * sizeof(Slot), s);
+    c->reset_pending = true;    // the slots [0, cap): flush_reset or a fresh aggregate
+    hipError_t e = hipMemsetAsync(c->slots + c->cap, 0xFF, sizeof(Slot), s);   // the sentinel slot
     if (e == hipSuccess) e = hipMemsetAsync(c->work, 0, sizeof(unsigned long long), s);
     return ss_check(e, "ss_counter_reset");
 }
@@ -1705,7 +1745,16 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         rc = ss_encode_fixed_impl(d_ascii, n, L, stride, c->ws_keys, 1, d_first_bad, nullptr, nullptr, stream);
         if (rc) return rc;
     }
-    if (multi || packed_keys || (fast && n <= c->ws_reads)) {
+    const bool part = multi || packed_keys || (fast && n <= c->ws_reads);
+    // a pending reset: the single-word aggregate writes whole slices (fresh); other paths memset first
+    bool fresh = false;
+    if (part && !multi) {
+        fresh = c->reset_pending;
+        c->reset_pending = false;
+    } else if ((rc = flush_reset(c, s)) != SS_OK) {
+        return rc;
+    }
+    if (part) {
         PartWs w;
         w.keys = c->ws_keys;
         w.akey = c->ws_akey;
@@ -1778,7 +1827,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint32_t*)c->ws_fill);
             w.bkey = w.keys;
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
-                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, ovf);
+                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, ovf, fresh);
             // overflow (a bin past cap1): the passes above idled; insert the batch directly
             constexpr int U = 4;
             const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 256 * 16);
@@ -1819,7 +1868,8 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint64_t*)c->ws_words, base_index);
         else
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
-                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index);
+                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, (const uint32_t*)nullptr,
+                               fresh);
         if (!multi) c->occ_src = 1;
         return ss_check(hipGetLastError(), "partitioned insert");
     }
@@ -1845,6 +1895,8 @@ int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_le
     if (c->W > 1) return ss_fail(SS_EARG, "ss_counter_merge takes single-word keys (L <= 32)");
     const unsigned grid = grid_for(m, kThreads, 256 * 16);
     c->occ_src = 0;
+    int rc = flush_reset(c, (hipStream_t)stream);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_merge, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, tbl_of(c), d_keys, d_counts,
                        d_first, m);
     return ss_check(hipGetLastError(), "k_merge");
@@ -1860,7 +1912,8 @@ int ss_counter_length(const ss_counter* c) { return c ? c->L : -1; }
 int ss_counter_size(ss_counter* c, uint64_t* d_size, void* stream) {
     if (!c || !d_size) return ss_fail(SS_EARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
-    int rc = ss_check(hipMemsetAsync(d_size, 0, sizeof(uint64_t), s), "size memset");
+    int rc = flush_reset(c, s);
+    if (!rc) rc = ss_check(hipMemsetAsync(d_size, 0, sizeof(uint64_t), s), "size memset");
     if (rc) return rc;
     const unsigned grid = grid_for(c->cap + 1, kThreads, 256 * 8);
     hipLaunchKernelGGL(k_size, dim3(grid), dim3(kThreads), 0, s, tbl_of(c), (unsigned long long*)d_size);
@@ -1879,6 +1932,8 @@ static int extract_impl(ss_counter* c, uint32_t n_parts, uint64_t* d_keys, uint3
     if (n_parts == 0 || n_parts > kMaxParts) return ss_fail(SS_EARG, "n_parts must be in 1..64");
     if (!d_keys || !d_lens || !d_counts || !d_first || !d_part_counts) return ss_fail(SS_EARG, "null buffer");
     hipStream_t s = (hipStream_t)stream;
+    int rc = flush_reset(c, s);
+    if (rc) return rc;
     Tbl t = tbl_of(c);
     unsigned long long* bc = c->work + 1;
     hipLaunchKernelGGL(k_part_count, dim3(kExtractBlocks), dim3(kExtractT), 0, s, t, n_parts, bc, ranges);
@@ -1942,6 +1997,8 @@ int ss_counter_pack_ranges(ss_counter* c, uint32_t n_parts, int32_t skip_part, u
     if ((((uintptr_t)d_rec) & 15) != 0) return ss_fail(SS_EARG, "d_rec must be 16-byte aligned");
     if (!c->occ) return ss_fail(SS_EARG, "table too large for region packing");
     hipStream_t s = (hipStream_t)stream;
+    int rc = flush_reset(c, s);
+    if (rc) return rc;
     Tbl t = tbl_of(c);
     const uint32_t R = (uint32_t)c->occ_R;
     if (c->occ_src != 1)

@@ -527,3 +527,40 @@ def test_counter_pack_records_layout(gpu):
     for kk, cc, ff in zip(k.tolist(), c.tolist(), f.tolist()):
         assert d[kk] == (cc, ff)
     t.close()
+
+
+@pytest.mark.parametrize("U,n,cap,partitioned", [
+    (40_000, 400_000, 1 << 19, True),      # optimistic partition, fresh aggregate
+    (3, 300_000, 1 << 19, True),           # optimistic overflow: fresh slice resets + direct insert
+    (5_000, 200_000, 1 << 17, True),       # exact partition passes, fresh aggregate
+    (900, 20_000, 1 << 16, False),         # direct insert: the pending reset is flushed first
+])
+def test_counter_lazy_reset(gpu, oracle, U, n, cap, partitioned):
+    """ss_counter_reset is lazy (the next partitioned insert writes whole slices instead of a memset
+    + slice read): a table filled with other keys, reset, then counted equals the oracle; so does
+    reset -> size (flush) and two inserts after one reset."""
+    import shortseq_amd.batch as B
+    L = 32
+    t = B.GpuCounter(cap, device=gpu)
+    junk = B.synth_pool_reads(n, L, 91, 92, 50_000, device=gpu)
+    t.insert(junk, L, partitioned=partitioned)
+    ascii = B.synth_pool_reads(n, L, 51, 52, U, device=gpu)
+    ascii[9] = ord("G")                        # "G" * 32: the sentinel key
+    t.reset()
+    t.insert(ascii, L, partitioned=partitioned)
+    k, c, f = t.items_sorted()
+    a = ascii.cpu().numpy().reshape(-1)
+    exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(n)])
+    assert [int(x) for x in k] == [w[0] for (w, _L, _c, _f) in exp]
+    assert [int(x) for x in c] == [cc for (_w, _L, cc, _f) in exp]
+    assert [int(x) for x in f] == [ff for (_w, _L, _c, ff) in exp]
+    assert not t.overflowed()
+    t.reset()
+    assert t.size() == 0
+    # two halves after one reset: the second insert sees the first's slices
+    t.reset()
+    t.insert(ascii[: n // 2], L, partitioned=partitioned)
+    t.insert(ascii[n // 2:], L, base_index=n // 2, partitioned=partitioned)
+    k2, c2, f2 = t.items_sorted()
+    assert np.array_equal(k2, k) and np.array_equal(c2, c) and np.array_equal(f2, f)
+    t.close()
