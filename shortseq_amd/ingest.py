@@ -45,8 +45,8 @@ class LengthGroupCounter:
         self.device = device
         self.expected = expected_reads
         self.tables: dict[int, B.GpuCounter] = {}
-        self.rows: dict[int, list] = {}          # L -> [global indices of the rows inserted: an
-                                                 # index array, or (start, count) for a range]
+        self.rows: dict[int, list] = {}          # L -> [global indices of the rows inserted: a
+                                                 # device index tensor, or (start, count) for a range]
         self.nrows: dict[int, int] = {}
         self.empty_count = 0
         self.empty_first: Optional[int] = None
@@ -78,44 +78,55 @@ class LengthGroupCounter:
         self.rows[L].append(rows)
         self.nrows[L] = row0 + m
 
-    def add(self, src: torch.Tensor, src_bytes: int, offsets: torch.Tensor, lens_np: np.ndarray, base: int,
+    def add(self, src: torch.Tensor, src_bytes: int, offsets: torch.Tensor, lens, base: int,
             fetch: Callable[[int], bytes], dense: bool = False) -> None:
-        """Count reads i (global index base + i): src[offsets[i] : + lens_np[i]] on the device.
-        fetch(i) returns read i's bytes (only called for a rejected read).  dense: the reads lie
-        back to back in src (offsets = exclusive cumsum of lens), so a batch of one length is
-        counted in place with no gather."""
-        lens_np = np.asarray(lens_np, dtype=np.int64)
-        if lens_np.size == 0:
+        """Count reads i (global index base + i): src[offsets[i] : + lens[i]] on the device.
+        lens: int64 host array or device tensor (values > 1024, e.g. the FASTQ strlen-underflow
+        marker, are rejected as too long).  fetch(i) returns read i's bytes (only called for a
+        rejected read).  dense: the reads lie back to back in src (offsets = exclusive cumsum of
+        lens), so a batch of one length is counted in place with no gather.
+
+        The split by length runs on the device: a stable sort of the (clamped) lengths, a
+        1026-bin histogram and the first read of every group come back in one small copy; each
+        group is gathered densely (ss_gather_rows) and counted by its length's table."""
+        n = int(lens.shape[0]) if isinstance(lens, torch.Tensor) else int(np.asarray(lens).size)
+        if n == 0:
             return
         if self.bad_index is not None and base > self.bad_index:
             return
-        L0 = int(lens_np[0])
-        if dense and 0 < L0 <= MAX_NT and int(lens_np.min()) == L0 == int(lens_np.max()):
-            m = lens_np.size
-            t = self._table(L0, m)
-            ascii = src[:m * L0] if src.dim() == 1 else src.reshape(-1)[:m * L0]
-            self._insert(t, L0, (base, m), m, ascii, L0, lambda r: r, fetch, base)
-            return
-        order = np.argsort(lens_np, kind="stable")
-        sl = lens_np[order]
-        cuts = np.flatnonzero(np.diff(sl)) + 1
-        for grp in np.split(order, cuts):
-            L = int(lens_np[grp[0]])
-            if self.bad_index is not None and base + int(grp[0]) > self.bad_index:
+        d = self.device
+        if isinstance(lens, torch.Tensor):
+            lens_d = lens.to(d, torch.int64)
+        else:
+            lens_h = np.asarray(lens, dtype=np.int64)
+            L0 = int(lens_h[0])
+            if dense and 0 < L0 <= MAX_NT and int(lens_h.min()) == L0 == int(lens_h.max()):
+                t = self._table(L0, n)
+                ascii = src[:n * L0] if src.dim() == 1 else src.reshape(-1)[:n * L0]
+                self._insert(t, L0, (base, n), n, ascii, L0, lambda r: r, fetch, base)
+                return
+            lens_d = torch.from_numpy(lens_h).to(d, non_blocking=True)
+        key = torch.clamp(lens_d, max=MAX_NT + 1)                  # MAX_NT + 1 = rejected (too long)
+        order = torch.sort(key, stable=True).indices
+        hist = torch.bincount(key, minlength=MAX_NT + 2)
+        starts = torch.cumsum(hist, 0) - hist
+        nz = torch.nonzero(hist).reshape(-1)
+        firsts = order[starts[nz].clamp(max=n - 1)]
+        info = torch.stack([nz, hist[nz], starts[nz], firsts], 1).cpu().tolist()   # one sync
+        for L, m, st, f0 in info:
+            if self.bad_index is not None and base + f0 > self.bad_index:
                 continue                                  # nothing here can come first any more
             if L == 0:
-                self.empty_count += len(grp)
-                f = base + int(grp[0])
-                self.empty_first = f if self.empty_first is None else min(self.empty_first, f)
+                self.empty_count += m
+                self.empty_first = base + f0 if self.empty_first is None else min(self.empty_first, base + f0)
                 continue
             if L > MAX_NT:
-                self._flag(base + int(grp[0]), None)
+                self._flag(base + f0, None)
                 continue
-            m = len(grp)
-            sel = torch.from_numpy(grp.astype(np.int64)).to(self.device, non_blocking=True)
+            sel = order[st:st + m]
             rows = B.gather_rows(src, offsets, L, sel=sel, src_bytes=src_bytes)
             t = self._table(L, m)
-            self._insert(t, L, base + grp, m, rows, rows.shape[1], lambda r, _g=grp: int(_g[r]), fetch, base)
+            self._insert(t, L, sel + base, m, rows, rows.shape[1], lambda r, _s=sel: int(_s[r]), fetch, base)
 
     def raise_if_bad(self) -> None:
         if self.bad_index is None:
@@ -127,8 +138,13 @@ class LengthGroupCounter:
         B.raise_read_error(self.bad_read, self.bad_index)
 
     def _row_index(self, L: int) -> np.ndarray:
-        return np.concatenate([np.arange(r[0], r[0] + r[1], dtype=np.int64) if isinstance(r, tuple) else r
-                               for r in self.rows[L]])
+        return np.concatenate([np.arange(r[0], r[0] + r[1], dtype=np.int64) if isinstance(r, tuple)
+                               else (r.cpu().numpy() if isinstance(r, torch.Tensor) else r) for r in self.rows[L]])
+
+    def _row_index_dev(self, L: int) -> torch.Tensor:
+        d = self.device
+        return torch.cat([torch.arange(r[0], r[0] + r[1], dtype=torch.int64, device=d) if isinstance(r, tuple)
+                          else torch.as_tensor(r, dtype=torch.int64).to(d) for r in self.rows[L]])
 
     def finish(self):
         """-> (groups, empty) with groups = [(L, words u64 [m, W], counts, first_global)] in table
@@ -164,7 +180,7 @@ class LengthGroupCounter:
                 if len(rows) == 1 and isinstance(rows[0], tuple):      # one dense range: no upload
                     gf, perm = torch.sort(first[:m] + rows[0][0])
                 else:
-                    gf, perm = torch.sort(torch.from_numpy(self._row_index(L)).to(d)[first[:m]])
+                    gf, perm = torch.sort(self._row_index_dev(L)[first[:m]])
                 groups.append((L, words[:m][perm].cpu().numpy().view(np.uint64), counts[:m][perm].cpu().numpy(),
                                gf.cpu().numpy()))
                 dev_firsts.append(gf)
@@ -260,17 +276,17 @@ def count_fastq(path: str, device: torch.device, chunk_bytes: int = DEFAULT_CHUN
                     continue
             dbuf[:use].copy_(pinned[:use], non_blocking=True)
             offs, lens, nl = B.fastq_index(dbuf, use, line0=line0, at_eof=at_eof)
-            lens_np = lens.cpu().numpy()
+            nrec = int(lens.shape[0])
             if est_reads is None and not at_eof:
-                est_reads = int(len(lens_np) * size / max(1, use)) + 1
+                est_reads = int(nrec * size / max(1, use)) + 1
                 gc.expected = est_reads
 
-            def fetch(i, _o=offs, _l=lens_np):
+            def fetch(i, _o=offs, _l=lens):
                 o = int(_o[i].item())
-                return dbuf[o:o + int(_l[i])].cpu().numpy().tobytes()
+                return dbuf[o:o + int(_l[i].item())].cpu().numpy().tobytes()
 
-            gc.add(dbuf, use, offs, lens_np, read0, fetch)
-            read0 += len(lens_np)
+            gc.add(dbuf, use, offs, lens, read0, fetch)
+            read0 += nrec
             line0 += nl
             if at_eof or gc.bad_index is not None:
                 break
