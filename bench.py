@@ -377,6 +377,58 @@ def bench_c1_dropin(n=1_000_000, L=32):
             "note": "wall time incl. Python object creation (the reference's own API shape)"}
 
 
+def _fastq_case_file():
+    """The small-RNA-like FASTQ of tools/probe_fastq_e2e.py: 8.4M ragged 18-32-nt records, 65,536
+    distinct sequences each 128 times (528 MB), written once to a temporary file."""
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import probe_fastq_e2e as P
+    d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+    path = os.path.join(d, "smallrna.fq")
+    n = P.write_pool_file(path)
+    return path, n
+
+
+def bench_fastq_dropin(path, n):
+    """a18 drop-in: sq.read_and_count_fastq(path) end to end (file read in pinned chunks, device
+    index + length groups + counters, dict rebuilt in first-occurrence order)."""
+    import contextlib
+    import io
+    import shortseq_amd as sq
+    with contextlib.redirect_stdout(io.StringIO()):
+        sq.read_and_count_fastq(path, device="cuda")                 # warm
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            c = sq.read_and_count_fastq(path, device="cuda")
+            ts.append(time.perf_counter() - t0)
+    if len(c) != 65536 or sum(c.values()) != n:
+        raise SystemExit("PARITY FAILURE: read_and_count_fastq drop-in")
+    t = float(np.median(ts))
+    return {"records": n, "file_bytes": os.path.getsize(path), "s_per_call": t, "records_per_s": n / t,
+            "unique": len(c), "note": "wall time of the drop-in call on a 528-MB small-RNA-like FASTQ "
+                                      "(page-cached), incl. building the 65,536-entry dict"}
+
+
+def cpu_baseline_fastq(path, n):
+    """The reference's own read_and_count_fastq (oracle/_ref, 1 host core) on the same file."""
+    import contextlib
+    import io
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    if not oracle.ref_available():
+        return None
+    if oracle.REF_DIR not in sys.path:
+        sys.path.insert(0, oracle.REF_DIR)
+    import shortseq.counter as ref_counter
+    with contextlib.redirect_stdout(io.StringIO()):
+        t0 = time.perf_counter()
+        c = ref_counter.read_and_count_fastq(path)
+        t = time.perf_counter() - t0
+    return {"s_per_call": t, "records_per_s": n / t, "unique": len(c), "cores": 1, "kind": "reference",
+            "sample": f"{n} records, shortseq.counter.read_and_count_fastq from oracle/_ref"}
+
+
 def cpu_baseline_c1(n=1_000_000, L=32):
     """The reference's own Python API on the same C1 reads (oracle/_ref, 1 host core): pack per
     object and ShortSeqCounter(list)."""
@@ -505,6 +557,7 @@ def main():
     }
     log(f"C2: {value / 1e12:.3f} T nt/s, kernel {kern_ms:.3f} ms, {achieved:.0f} GB/s")
 
+    fq_path, fq_n = None, 0
     if not args.no_extras:
         extra = {}
         L3, n3 = 96, args.reads_per_gpu
@@ -558,6 +611,9 @@ def main():
             extra["C2_host_staged_32"] = bench_host_staged(B, dev)
             log("C1 drop-in API")
             extra["C1_dropin_1M_32"] = bench_c1_dropin()
+            log("a18 read_and_count_fastq drop-in")
+            fq_path, fq_n = _fastq_case_file()
+            extra["A18_read_and_count_fastq_smallrna"] = bench_fastq_dropin(fq_path, fq_n)
         result["extra"] = extra
 
     if rank == 0:
@@ -566,9 +622,13 @@ def main():
             result["cpu_baseline"] = cpu_baseline(32, args.cpu_seconds)
             if not args.no_extras:
                 result["cpu_baseline"]["c1_reference_api"] = cpu_baseline_c1()
+                result["cpu_baseline"]["a18_reference_read_and_count_fastq"] = cpu_baseline_fastq(fq_path, fq_n)
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
+    if fq_path is not None:
+        import shutil
+        shutil.rmtree(os.path.dirname(fq_path), ignore_errors=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
