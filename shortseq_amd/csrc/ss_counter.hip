@@ -62,10 +62,10 @@ struct ss_counter {
     uint32_t* ws_tot = nullptr;            // [regions + 1] scratch (bin totals / coarse starts)
     // optimistic coarse partition (k_pf_coarse): ws_akey / ws_aidx hold 128 bins of ws_cap1 slots
     uint64_t ws_cap1 = 0;
-    uint32_t* ws_fill = nullptr;           // [128] bin fill counters, [128] overflow flag
+    uint32_t* ws_fill = nullptr;           // bin fill counters + overflow flag, kFillStride apart
     // per-region occupancy (used slots of each slice), written by the single-word aggregate; lets
     // ss_counter_pack_ranges skip its counting pass.  occ_src: 0 = stale, 1 = valid, 2 = valid
-    // unless the optimistic partition overflowed (ws_fill[128] != 0: the direct insert ran instead)
+    // unless the optimistic partition overflowed (the ws_fill overflow flag: the direct insert ran instead)
     uint32_t* occ = nullptr;               // [R]
     unsigned long long* roff = nullptr;    // [R + 2] pack scratch: region offsets, sentinel position
     uint64_t occ_R = 0;
@@ -743,27 +743,38 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
 // lie in the bin's 2^(rbits - 7) regions, so the histogram and the LDS staging use that window.
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kCB = 1u << kCoarseBits;          // 128 coarse bins
+// The 128 bin fill counters take one atomicAdd per (4096-read tile, bin), ~3.9M device-scope atomics
+// per 125M reads.  kFillStride spaces them (u32 units); 64 and 1024 measured no different from 1
+// (tools/tune_counter.hip, scripts/ab_counter.sh), so they stay packed.
+#ifndef SS_FILL_STRIDE
+#define SS_FILL_STRIDE 1
+#endif
+constexpr uint32_t kFillStride = SS_FILL_STRIDE;
+constexpr uint32_t kFillWords = (kCB + 1) * kFillStride;   // counters + the overflow flag
+__host__ __device__ __forceinline__ uint32_t fill_at(uint32_t b) { return b * kFillStride; }
 #ifndef SS_FINE_PER_BIN
 #define SS_FINE_PER_BIN 8
 #endif
 constexpr uint32_t kFinePerBin = SS_FINE_PER_BIN;    // fine-pass blocks per coarse bin
 #ifndef SS_PF_RPL
-#define SS_PF_RPL 8
+#define SS_PF_RPL 16
 #endif
-constexpr uint32_t kPfT = 512, kPfRPL = SS_PF_RPL;   // k_pf_coarse: kPfT * kPfRPL-read tiles
+#ifndef SS_PF_T
+#define SS_PF_T 256      // 256 x 16 reads per tile: ~5 % faster than 512 x 8 over 9 same-box samples each
+#endif
+constexpr uint32_t kPfT = SS_PF_T, kPfRPL = SS_PF_RPL;   // k_pf_coarse: kPfT * kPfRPL-read tiles
 
 template <int T, int RPL>
 __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
                                                  uint64_t n, uint32_t cpr, uint64_t cap1, uint32_t* fill,
                                                  unsigned long long* first_bad) {
     constexpr uint32_t TILE = T * RPL;
-    // (two blocks per CU: a 3-block variant without the staged bin array measured 4 % slower)
+    // (two blocks per CU by LDS: a 3-block variant without the staged bin array measured 4 % slower)
     __shared__ uint32_t lcount[kCB], lstart[kCB], gbase[kCB];
     __shared__ uint64_t skey[TILE];
     __shared__ uint32_t sidx[TILE];
     __shared__ uint8_t sbin[TILE];
-    __shared__ uint32_t wsum[17];
-    uint32_t* ovf = fill + kCB;
+    uint32_t* ovf = fill + fill_at(kCB);
     const uint32_t shift = w.rbits - kCoarseBits;
     const uint64_t tiles = (n + TILE - 1) / TILE;
     uint4 nx[RPL][2];
@@ -780,9 +791,15 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
 #ifndef SS_PF_PREFETCH
 #define SS_PF_PREFETCH 0   // register double buffer off: 190 -> fewer VGPRs, 2 blocks per CU (tune_counter A/B: -5 %)
 #endif
+    static_assert(kCB == 128, "wave 0 scans two bins per lane");
+    for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
+    __syncthreads();
     if (SS_PF_PREFETCH && blockIdx.x < tiles) load_tile(blockIdx.x);
+    // three barriers per tile: (A) ranks counted, (B) wave 0 has scanned the bins, reserved the
+    // tile's runs in the global bins and zeroed the counters for the next tile, (C) tile staged in
+    // LDS.  The next tile's rank atomics only touch lcount (zeroed before B) and its staging waits
+    // for its own barrier B, which every wave reaches only after this tile's write-out.
     for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
         if (!SS_PF_PREFETCH) load_tile(tile);
         uint4 x[RPL][2];
 #pragma unroll
@@ -791,7 +808,6 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             x[j][1] = nx[j][1];
         }
         if (SS_PF_PREFETCH && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
-        __syncthreads();
         uint64_t key[RPL];
         uint32_t bin[RPL], rank[RPL];
         const uint64_t t0 = tile * TILE;
@@ -810,12 +826,24 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                 rank[j] = atomicAdd(&lcount[bin[j]], 1u);
             }
         }
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < kCB; i += T) lstart[i] = lcount[i];
-        __syncthreads();
-        block_scan_512(lstart, kCB, wsum);
-        for (uint32_t i = threadIdx.x; i < kCB; i += T)
-            gbase[i] = lcount[i] ? atomicAdd(&fill[i], lcount[i]) : 0u;
+        __syncthreads();                                                  // (A)
+        if (threadIdx.x < 64) {
+            const uint32_t lane = threadIdx.x, b0 = 2 * lane;
+            const uint32_t c0 = lcount[b0], c1 = lcount[b0 + 1];
+            uint32_t incl = c0 + c1;
+            for (uint32_t off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            const uint32_t excl = incl - c0 - c1;
+            lstart[b0] = excl;
+            lstart[b0 + 1] = excl + c0;
+            gbase[b0] = c0 ? atomicAdd(&fill[fill_at(b0)], c0) : 0u;
+            gbase[b0 + 1] = c1 ? atomicAdd(&fill[fill_at(b0 + 1)], c1) : 0u;
+            lcount[b0] = 0;
+            lcount[b0 + 1] = 0;
+        }
+        __syncthreads();                                                  // (B)
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
             const uint32_t e = j * T + threadIdx.x;
@@ -826,7 +854,7 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                 sbin[sp] = (uint8_t)bin[j];
             }
         }
-        __syncthreads();
+        __syncthreads();                                                  // (C)
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
             const uint32_t b = sbin[i];
             const uint64_t pos = (uint64_t)gbase[b] + (i - lstart[b]);
@@ -837,7 +865,6 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                 *ovf = 1u;
             }
         }
-        __syncthreads();
     }
 }
 
@@ -845,7 +872,7 @@ __device__ __forceinline__ void fine_range(uint32_t fb, const uint32_t* fill, ui
                                            uint64_t& lo, uint64_t& hi) {
     bin = fb / kFinePerBin;
     const uint32_t sub = fb % kFinePerBin;
-    const uint64_t f = min((uint64_t)fill[bin], cap1);
+    const uint64_t f = min((uint64_t)fill[fill_at(bin)], cap1);
     lo = sub * f / kFinePerBin;
     hi = (sub + 1) * f / kFinePerBin;
 }
@@ -854,7 +881,7 @@ __device__ __forceinline__ void fine_range(uint32_t fb, const uint32_t* fill, ui
 template <int T>
 __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
     __shared__ uint32_t h[kMaxLocalBins];
-    if (fill[kCB]) return;
+    if (fill[fill_at(kCB)]) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits);
     uint32_t bin;
     uint64_t lo, hi;
@@ -871,7 +898,7 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
 // region totals over the bin's 8 fine blocks (thread per region) -> w.tot; then k_pc_scan (one
 // block) -> rstart; then k_pf_offsets (thread per region) -> each fine block's write cursors
 __global__ __launch_bounds__(256) void k_pf_tot(PartWs w, const uint32_t* fill) {
-    if (fill[kCB]) return;
+    if (fill[fill_at(kCB)]) return;
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= w.R) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
@@ -882,7 +909,7 @@ __global__ __launch_bounds__(256) void k_pf_tot(PartWs w, const uint32_t* fill) 
 }
 
 __global__ __launch_bounds__(256) void k_pf_offsets(PartWs w, const uint32_t* fill) {
-    if (fill[kCB]) return;
+    if (fill[fill_at(kCB)]) return;
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= w.R) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
@@ -909,7 +936,7 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
     __shared__ uint64_t skey[kTile];
     __shared__ uint32_t sidx[kTile];
     __shared__ uint32_t wsum[17];
-    if (fill[kCB]) return;
+    if (fill[fill_at(kCB)]) return;
     const uint32_t nb = 1u << (w.rbits - kCoarseBits);
     uint32_t bin;
     uint64_t lo, hi;
@@ -1678,7 +1705,7 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
-    if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, (2 * kCB) * sizeof(uint32_t));
+    if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, kFillWords * sizeof(uint32_t));
     c->ws_cap1 = cap1;
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_hist) e = hipMalloc((void**)&c->ws_hist, (size_t)kPartBlocks * R * sizeof(uint32_t));
@@ -1807,7 +1834,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         if (!multi && !packed_keys && two_pass && w.rbits - kCoarseBits <= 8) {
             // optimistic coarse partition: encode + coarse scatter in one pass, fine pass by bin
             const uint64_t cap1 = c->ws_cap1;
-            rc = ss_check(hipMemsetAsync(c->ws_fill, 0, 2 * kCB * sizeof(uint32_t), s), "fill reset");
+            rc = ss_check(hipMemsetAsync(c->ws_fill, 0, kFillWords * sizeof(uint32_t), s), "fill reset");
             if (rc) return rc;
             // grid-stride over tiles: exactly the resident blocks (no second, partial round)
             static int pf_grid = 0;
@@ -1822,7 +1849,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
                                (unsigned long long*)d_first_bad);
             const unsigned fine_blocks = kCB * kFinePerBin;
-            const uint32_t* ovf = (const uint32_t*)(c->ws_fill + kCB);
+            const uint32_t* ovf = (const uint32_t*)(c->ws_fill + fill_at(kCB));
             hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill);
             const unsigned rg = (w.R + 255) / 256;
@@ -1839,7 +1866,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 256 * 16);
             hipLaunchKernelGGL((k_count_g16<U>), dim3(grid), dim3(kThreads), 0, s, t, (const uint4*)d_ascii,
                                stride / 16, n, L / 16, base_index, (unsigned long long*)d_first_bad, ovf);
-            c->occ_src = 2;   // valid unless the fallback ran (ws_fill[128] set)
+            c->occ_src = 2;   // valid unless the fallback ran (ws_fill overflow flag set)
             return ss_check(hipGetLastError(), "optimistic partitioned insert");
         }
         if (multi) {
@@ -2009,7 +2036,7 @@ int ss_counter_pack_ranges(ss_counter* c, uint32_t n_parts, int32_t skip_part, u
     const uint32_t R = (uint32_t)c->occ_R;
     if (c->occ_src != 1)
         hipLaunchKernelGGL(k_region_occ, dim3(R), dim3(kPackT), 0, s, t,
-                           c->occ_src == 2 ? (const uint32_t*)(c->ws_fill + kCB) : (const uint32_t*)nullptr);
+                           c->occ_src == 2 ? (const uint32_t*)(c->ws_fill + fill_at(kCB)) : (const uint32_t*)nullptr);
     hipLaunchKernelGGL(k_region_scan, dim3(1), dim3(1024), 0, s, t, R, n_parts, skip_part, c->roff,
                        (unsigned long long*)d_part_counts);
     hipLaunchKernelGGL(k_region_pack, dim3(R), dim3(kPackT), 0, s, t, R, n_parts, skip_part,
