@@ -29,6 +29,8 @@ import time
 cdef extern from "Python.h":
     ctypedef Py_ssize_t Py_hash_t
     int _PyDict_SetItem_KnownHash(object mp, object key, object item, Py_hash_t hash) except -1
+    object PyUnicode_New(Py_ssize_t size, Py_UCS4 maxchar)
+    void* PyUnicode_1BYTE_DATA(object o)
     void* PyUnicode_DATA(object o)
     Py_ssize_t PyUnicode_GET_LENGTH(object o)
     bint PyUnicode_Check(object o)
@@ -67,6 +69,16 @@ def get_domain_var(): return MIN_VAR_NT, MAX_VAR_NT
 
 cdef inline size_t _nwords(size_t L) noexcept nogil:
     return (L + 31) // 32
+
+
+cdef inline str _to_str(const uint64_t* words, size_t L):
+    """_unmarshall_bytes_* (short_seq_64.pyx:114-121, short_seq_192.pyx:114-127,
+    short_seq_var.pyx:98-120): decoded straight into a new compact ASCII str (no staging buffer,
+    no ASCII re-validation; every character is one of "ACTG")."""
+    cdef object s = PyUnicode_New(L, 127)
+    if L:
+        ssh_decode(words, L, <char*>PyUnicode_1BYTE_DATA(s))
+    return s
 
 
 cdef object _raise_encode_error(const uint8_t* seq, ss_err* err):
@@ -112,9 +124,7 @@ cdef class ShortSeq64:
         return ssh_hamming(&self._packed, &other._packed, 1)
 
     def __str__(self):
-        cdef char buf[32]
-        ssh_decode(&self._packed, self._length, buf)
-        return PyUnicode_DecodeASCII(buf, self._length, NULL)
+        return _to_str(&self._packed, self._length)
 
     def __repr__(self):
         return f"<ShortSeq64 ({self._length} nt): {self}>"
@@ -157,9 +167,7 @@ cdef class ShortSeq192:
         return ssh_hamming(self._packed, other._packed, self._length)
 
     def __str__(self):
-        cdef char buf[96]
-        ssh_decode(self._packed, self._length, buf)
-        return PyUnicode_DecodeASCII(buf, self._length, NULL)
+        return _to_str(self._packed, self._length)
 
     def __repr__(self):
         return f"<ShortSeq192 ({self._length} nt): {self}>"
@@ -201,9 +209,7 @@ cdef class ShortSeqVar:
         return ssh_hamming(self._packed, other._packed, self._length)
 
     def __str__(self):
-        cdef char buf[1024]
-        ssh_decode(self._packed, self._length, buf)
-        return PyUnicode_DecodeASCII(buf, self._length, NULL)
+        return _to_str(self._packed, self._length)
 
     def __repr__(self):
         cdef char buf[MAX_REPR_LEN]

@@ -118,9 +118,32 @@ inline int encode(const uint8_t* s, size_t L, uint64_t* words, ss_err* err) {
     return 0;
 }
 
+// "ACTG"[code] (util.pyx:52) four nucleotides at a time: entry b of the table is the 4 characters
+// of the 8-bit packed byte b (nt 0 in the low bits -> the first character, little-endian u32).
+struct DecodeTable {
+    uint32_t v[256];
+    DecodeTable() {
+        static const char kMap[4] = {'A', 'C', 'T', 'G'};
+        for (uint32_t b = 0; b < 256; ++b) {
+            uint32_t x = 0;
+            for (uint32_t j = 0; j < 4; ++j) x |= (uint32_t)(uint8_t)kMap[(b >> (2 * j)) & 3u] << (8 * j);
+            v[b] = x;
+        }
+    }
+};
+
 inline void decode(const uint64_t* words, size_t L, char* out) {
-    static const char kMap[4] = {'A', 'C', 'T', 'G'};   // util.pyx:52
-    for (size_t i = 0; i < L; ++i) out[i] = kMap[(words[i >> 5] >> (2 * (i & 31))) & 3u];
+    static const DecodeTable t;
+    static const char kMap[4] = {'A', 'C', 'T', 'G'};
+    size_t i = 0;
+    for (; i + 32 <= L; i += 32) {   // one word -> 32 characters
+        uint64_t w = words[i >> 5];
+        for (int q = 0; q < 8; ++q, w >>= 8) {
+            const uint32_t c = t.v[w & 0xFFu];
+            memcpy(out + i + 4 * q, &c, 4);
+        }
+    }
+    for (; i < L; ++i) out[i] = kMap[(words[i >> 5] >> (2 * (i & 31))) & 3u];
 }
 
 inline uint64_t hamming(const uint64_t* a, const uint64_t* b, size_t L) {
