@@ -12,7 +12,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
-#if defined(__BMI2__)
+#if defined(__BMI2__) || defined(__AVX2__)
 #include <immintrin.h>
 #endif
 
@@ -78,6 +78,29 @@ inline int64_t full_block(const uint8_t* s, uint64_t* out) {
     return -1;
 }
 
+#if defined(__AVX2__) && defined(__BMI2__)
+// Fast path for the common case: if all 32 bytes at s are exactly 'A' 'C' 'G' 'T' (no aliased or
+// invalid byte), the table rule and the PEXT rule agree ((c >> 1) & 3, no alias carry), so the
+// block packs with four PEXTs.  Each byte is checked against the only ACGT letter with its low
+// nibble ('A' 1, 'C' 3, 'T' 4, 'G' 7).  Returns false (nothing written) for any other byte.
+inline bool acgt_block32(const uint8_t* s, uint64_t* out) {
+    // non-ACGT slots hold i ^ 8: their low nibble differs from i, so no byte can match them
+    const __m256i lut = _mm256_setr_epi8(0x08, 0x41, 0x0A, 0x43, 0x54, 0x0D, 0x0E, 0x47, 0x00, 0x01, 0x02, 0x03,
+                                         0x04, 0x05, 0x06, 0x07, 0x08, 0x41, 0x0A, 0x43, 0x54, 0x0D, 0x0E, 0x47,
+                                         0x00, 0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07);
+    const __m256i x = _mm256_loadu_si256((const __m256i*)s);
+    const __m256i lo = _mm256_and_si256(x, _mm256_set1_epi8(0x0F));
+    const __m256i eq = _mm256_cmpeq_epi8(_mm256_shuffle_epi8(lut, lo), x);
+    if ((uint32_t)_mm256_movemask_epi8(eq) != 0xFFFFFFFFu) return false;
+    uint64_t c[4];
+    memcpy(c, s, 32);
+    *out = _pext_u64(c[0], 0x0606060606060606ull) | (_pext_u64(c[1], 0x0606060606060606ull) << 16) |
+           (_pext_u64(c[2], 0x0606060606060606ull) << 32) | (_pext_u64(c[3], 0x0606060606060606ull) << 48);
+    return true;
+}
+#define SSH_HAVE_ACGT_FAST 1
+#endif
+
 // Encode one read as shortseq._new would.  `words` receives ceil(L/32) words (the caller zeroes
 // any further words).  Returns 0, 1 (unsupported base) or 2 (too long); err may be null.
 inline int encode(const uint8_t* s, size_t L, uint64_t* words, ss_err* err) {
@@ -92,6 +115,9 @@ inline int encode(const uint8_t* s, size_t L, uint64_t* words, ss_err* err) {
         return 2;
     }
     if (L == 0) return 0;
+#ifdef SSH_HAVE_ACGT_FAST
+    if (L == 32 && acgt_block32(s, &words[0])) return 0;
+#endif
     if (L <= 32) {
         int64_t bad = table_block(s, L, &words[0]);
         if (bad >= 0) {
@@ -102,6 +128,9 @@ inline int encode(const uint8_t* s, size_t L, uint64_t* words, ss_err* err) {
     }
     const size_t full = L / 32, rem = L % 32;
     for (size_t b = 0; b < full; ++b) {
+#ifdef SSH_HAVE_ACGT_FAST
+        if (acgt_block32(s + 32 * b, &words[b])) continue;
+#endif
         int64_t bad = full_block(s + 32 * b, &words[b]);
         if (bad >= 0) {
             if (err) { err->kind = 1; err->nbytes = 8; err->byte_offset = (int64_t)(32 * b) + bad; }

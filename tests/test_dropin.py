@@ -267,3 +267,23 @@ def test_fill_groups_order_and_empty():
     assert [(str(k), v) for k, v in c.items()] == [
         ("C" * 40, 5), ("G" * 32, 1), ("", 6), ("A" * 32, 3), ("T" * 40, 4), ("ACGT" * 8, 2)]
     assert c[sq.pack("G" * 32)] == 1 and c[sq.pack("ACGT" * 8)] == 2 and c[sq.pack("")] == 6
+
+
+def test_pack_every_byte_value_in_every_block_position(oracle):
+    """The host codec's exact-ACGT fast path (AVX2 nibble lookup + PEXT) must hand every other
+    byte value to the reference-exact path: each of the 256 byte values at several positions of
+    32-, 64- and 75-nt reads packs (or raises) exactly as the oracle."""
+    for L in (32, 64, 75):
+        for pos in (0, 5, 31, L - 1):
+            for b in range(256):
+                seq = bytearray(b"ACGT" * 19)[:L]
+                seq[pos] = b
+                seq = bytes(seq)
+                words, err = oracle.encode_one(seq, 32)
+                if err.kind == 0:
+                    got = sq.pack(seq)
+                    nw = max(1, (L + 31) // 32)
+                    assert [int(x) for x in got.packed][:nw] == [int(x) for x in words[:nw]], (L, pos, b)
+                else:
+                    with pytest.raises(BaseException):
+                        sq.pack(seq)
