@@ -346,35 +346,40 @@ def bench_host_staged(B, dev, n=32_000_000, L=32, reps=5):
                     "8 staging threads); PCIe-bound, not the roofline number"}
 
 
+def _median_time(fn, reps=3):
+    ts, out = [], None
+    for _ in range(reps):
+        out = None
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), out
+
+
 def bench_c1_dropin(n=1_000_000, L=32):
     """BASELINE configs[0] (C1): 1M x 32-nt synthetic reads through the drop-in Python API —
-    sq.pack() per object (host codec) and ShortSeqCounter(list) (GPU batch path)."""
+    sq.pack() per object (host codec) and ShortSeqCounter(list) (GPU batch path); median of 3
+    calls each (the reference in cpu_baseline_c1 is timed the same way)."""
     import shortseq_amd as sq
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # the generator only (same synthetic reads as the CPU baseline)
     a = oracle.gen_reads(11, 0, n, L)
     reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
-    t0 = time.perf_counter()
-    objs = [sq.pack(r) for r in reads]
-    t_pack = time.perf_counter() - t0
+    t_pack, objs = _median_time(lambda: [sq.pack(r) for r in reads])
     sq.ShortSeqCounter(reads[:100_000])                    # warm the GPU path
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    c = sq.ShortSeqCounter(reads)
-    t_cnt = time.perf_counter() - t0
+    t_cnt, c = _median_time(lambda: sq.ShortSeqCounter(reads))
     if len(c) != len(set(reads)) or sum(c.values()) != n or str(objs[7]) != reads[7].decode():
         raise SystemExit("PARITY FAILURE: C1 drop-in")
     # the same API on a duplicate-heavy list (2^14-read pool): the dict the API must return is small
     pa = oracle.gen_pool_reads(12, 13, 1 << 14, 0, n, L)
     preads = [pa[i * L:(i + 1) * L].tobytes() for i in range(n)]
-    t0 = time.perf_counter()
-    pc = sq.ShortSeqCounter(preads)
-    t_pool = time.perf_counter() - t0
+    t_pool, pc = _median_time(lambda: sq.ShortSeqCounter(preads))
     if sum(pc.values()) != n:
         raise SystemExit("PARITY FAILURE: C1 drop-in (pool)")
     return {"reads": n, "read_len": L, "pack_per_s": n / t_pack, "counter_reads_per_s": n / t_cnt,
             "unique": len(c), "counter_pool16k_reads_per_s": n / t_pool, "pool_unique": len(pc),
-            "note": "wall time incl. Python object creation (the reference's own API shape)"}
+            "note": "wall time incl. Python object creation (the reference's own API shape), median of 3"}
 
 
 def _fastq_case_file():
@@ -442,20 +447,14 @@ def cpu_baseline_c1(n=1_000_000, L=32):
     import shortseq.short_seq as ref_sq
     a = oracle.gen_reads(11, 0, n, L)
     reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
-    t0 = time.perf_counter()
-    [ref_sq.pack(r) for r in reads]
-    t_pack = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    ref_counter.ShortSeqCounter(reads)
-    t_cnt = time.perf_counter() - t0
+    t_pack, _ = _median_time(lambda: [ref_sq.pack(r) for r in reads])
+    t_cnt, _ = _median_time(lambda: ref_counter.ShortSeqCounter(reads))
     pa = oracle.gen_pool_reads(12, 13, 1 << 14, 0, n, L)
     preads = [pa[i * L:(i + 1) * L].tobytes() for i in range(n)]
-    t0 = time.perf_counter()
-    ref_counter.ShortSeqCounter(preads)
-    t_pool = time.perf_counter() - t0
+    t_pool, _ = _median_time(lambda: ref_counter.ShortSeqCounter(preads))
     return {"pack_per_s": n / t_pack, "counter_reads_per_s": n / t_cnt, "counter_pool16k_reads_per_s": n / t_pool,
             "cores": 1, "kind": "reference",
-            "sample": f"{n} x {L}-nt reads, shortseq.pack / ShortSeqCounter from oracle/_ref"}
+            "sample": f"{n} x {L}-nt reads, shortseq.pack / ShortSeqCounter from oracle/_ref, median of 3"}
 
 
 # ------------------------------------------------------------------------------------------------
