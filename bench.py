@@ -272,26 +272,44 @@ def bench_fastq_index(B, lib, dev, n_rec=8 << 20, L=100, reps=10):
     s = torch.cuda.current_stream(dev).cuda_stream
     ws_bytes = int(lib.ss_fastq_scan_ws_bytes(nbytes))
     ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.int64, device=dev)
-    cnt = torch.empty(2, dtype=torch.int64, device=dev)
+    ws1_bytes = int(lib.ss_fastq_onepass_ws_bytes(nbytes, nrec + 2))
+    ws1 = torch.empty((ws1_bytes + 7) // 8, dtype=torch.int64, device=dev)
+    cnt = torch.empty(3, dtype=torch.int64, device=dev)
     offs = torch.empty(nrec + 2, dtype=torch.int64, device=dev)
     lens = torch.empty(nrec + 2, dtype=torch.int32, device=dev)
     aux = torch.empty(nrec + 2, dtype=torch.int64, device=dev)
+    starts = torch.from_numpy(np.cumsum([0] + [len(p) for p in parts[:-1]]) + np.array(
+        [p.index(b"\n") + 1 for p in parts])).to(dev)
 
-    def step(_t):
+    def twopass(_t):
         check(lib.ss_fastq_scan(buf.data_ptr(), nbytes, ws.data_ptr(), ws_bytes, cnt.data_ptr(), s), "scan")
         check(lib.ss_fastq_index(buf.data_ptr(), nbytes, 0, 1, ws.data_ptr(), offs.data_ptr(), lens.data_ptr(),
                                  aux.data_ptr(), nrec + 2, cnt[1:].data_ptr(), s), "index")
-    el, tr = timed_loop(step, reps, 3, 1)
-    if int(cnt[1]) != nrec or int(lens[:nrec].min()) != L or int(lens[:nrec].max()) != L:
-        raise SystemExit("PARITY FAILURE: FASTQ index")
-    starts = torch.from_numpy(np.cumsum([0] + [len(p) for p in parts[:-1]]) + np.array(
-        [p.index(b"\n") + 1 for p in parts])).to(dev)
-    if not torch.equal(offs[:m], starts):
-        raise SystemExit("PARITY FAILURE: FASTQ offsets")
+
+    def onepass(_t):
+        check(lib.ss_fastq_index_onepass(buf.data_ptr(), nbytes, 0, 1, ws1.data_ptr(), ws1_bytes, offs.data_ptr(),
+                                         lens.data_ptr(), aux.data_ptr(), nrec + 2, cnt.data_ptr(), s), "index1")
+
+    def verify(what, nreads):
+        if nreads != nrec or int(lens[:nrec].min()) != L or int(lens[:nrec].max()) != L:
+            raise SystemExit("PARITY FAILURE: FASTQ index (%s)" % what)
+        if not torch.equal(offs[:m], starts) or not torch.equal(offs[nrec - m:nrec] - offs[nrec - m], starts - starts[0]):
+            raise SystemExit("PARITY FAILURE: FASTQ offsets (%s)" % what)
+
+    el2, tr2 = timed_loop(twopass, reps, 3, 1)
+    verify("two-pass", int(cnt[1]))
+    offs.zero_()
+    lens.zero_()
+    el, tr = timed_loop(onepass, reps, 3, 1)
+    if int(cnt[2]) != 0 or int(cnt[0]) != 4 * nrec:
+        raise SystemExit("PARITY FAILURE: FASTQ one-pass staging / newline count")
+    verify("one-pass", int(cnt[1]))
     ms = tr.region_ms / reps
     return {"file_bytes": nbytes, "records": nrec, "read_len": L, "ms_per_step": ms,
             "file_GB_per_s": nbytes / ms / 1e6, "records_per_s": nrec / ms * 1e3,
-            "note": "scan + index passes (file read twice); device-resident synthetic FASTQ"}
+            "two_pass_ms_per_step": tr2.region_ms / reps,
+            "note": "ss_fastq_index_onepass (file read once, newline positions staged per tile); two_pass = ss_fastq_scan + "
+                    "ss_fastq_index; device-resident synthetic FASTQ, every offset / length checked"}
 
 
 def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):

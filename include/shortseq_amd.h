@@ -225,14 +225,26 @@ int ss_counter_extract_words(ss_counter* c, uint32_t n_parts, uint64_t* d_fps, u
  *      written; size max_reads from *d_nlines: at most nlines / 4 + 1).  d_aux: max_reads u64 of
  *      scratch.  d_lens[i] = 0xFFFFFFFF where strlen is 0 (the reference's size_t underflow, i.e.
  *      the too-long error); > 1024 is the too-long error as well.
+ * or, reading the chunk once:
+ *   ss_fastq_index_onepass: the same outputs from one read of the chunk (each 32-KiB tile stages its
+ *      newline positions, 4 B per line, and the line numbers are resolved from the tile counts);
+ *      d_ws of ss_fastq_onepass_ws_bytes(nbytes, max_reads) bytes; d_counts[3] = {newlines,
+ *      sequence lines, staging full}.  max_reads is the caller's bound (a sequence line takes >= 4
+ *      bytes of the file: nbytes / 4 + 2 always suffices); the outputs are complete iff
+ *      d_counts[2] == 0 and d_counts[1] <= max_reads, otherwise the call is repeated with a larger
+ *      max_reads (>= d_counts[1]; doubled when d_counts[2] != 0).
  * The (d_offsets, d_lens) pair is the ragged layout of ss_encode_var and ss_gather_rows.
  * ---------------------------------------------------------------------------------------------- */
 uint64_t ss_fastq_scan_ws_bytes(uint64_t nbytes);
 int ss_fastq_scan(const uint8_t* d_buf, uint64_t nbytes, void* d_ws, uint64_t ws_bytes, uint64_t* d_nlines,
                   void* stream);
-int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, const void* d_ws,
+int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, void* d_ws,
                    uint64_t* d_offsets, uint32_t* d_lens, uint64_t* d_aux, uint64_t max_reads,
                    uint64_t* d_nreads, void* stream);
+uint64_t ss_fastq_onepass_ws_bytes(uint64_t nbytes, uint64_t max_reads);
+int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, void* d_ws,
+                           uint64_t ws_bytes, uint64_t* d_offsets, uint32_t* d_lens, uint64_t* d_aux,
+                           uint64_t max_reads, uint64_t* d_counts, void* stream);
 
 /* Gather ragged rows into a dense batch: dst row r = d_src[d_offsets[s] .. + L) with s = d_sel[r]
  * (or r when d_sel is NULL); dst_stride % 16 == 0, >= round_up(L, 16); d_dst 16-B aligned; bytes of

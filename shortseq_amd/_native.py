@@ -72,6 +72,8 @@ SIGNATURES = [
     ("ss_fastq_scan_ws_bytes", _U64, [_U64]),
     ("ss_fastq_scan", C.c_int, [_P, _U64, _P, _U64, _P, _P]),
     ("ss_fastq_index", C.c_int, [_P, _U64, _U64, C.c_int, _P, _P, _P, _P, _U64, _P, _P]),
+    ("ss_fastq_onepass_ws_bytes", _U64, [_U64, _U64]),
+    ("ss_fastq_index_onepass", C.c_int, [_P, _U64, _U64, C.c_int, _P, _U64, _P, _P, _P, _U64, _P, _P]),
     ("ss_gather_rows", C.c_int, [_P, _U64, _P, _P, _U64, _U32, _P, _U64, _P]),
     ("ss_stager_create", C.c_int, [C.c_int, _U64, _U32, _U32, C.POINTER(C.c_void_p)]),
     ("ss_stager_destroy", C.c_int, [_P]),

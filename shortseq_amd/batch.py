@@ -453,11 +453,15 @@ def hamming_all_pairs(words: torch.Tensor, L: int, max_dist: int, *, counts: boo
 LEN_UNDERFLOW = 0xFFFFFFFF   # ss_fastq_index: strlen 0 (the reference's size_t underflow -> too long)
 
 
-def fastq_index(buf: torch.Tensor, nbytes: Optional[int] = None, *, line0: int = 0, at_eof: bool = True):
+def fastq_index(buf: torch.Tensor, nbytes: Optional[int] = None, *, line0: int = 0, at_eof: bool = True,
+                onepass: bool = True, max_reads: Optional[int] = None):
     """Sequence lines of a FASTQ chunk resident on the device (fast_read.pyx:3-20 rule, see
     include/shortseq_amd.h ss_fastq_index) -> (offsets int64 [n], lens int64 [n], newlines).
     lens holds the reference's strlen - 1 (LEN_UNDERFLOW where strlen is 0).  The chunk must start
-    at a line boundary and end right after a newline unless at_eof."""
+    at a line boundary and end right after a newline unless at_eof.
+    onepass: ss_fastq_index_onepass (the chunk is read once; max_reads is a capacity guess, default
+    nbytes / 16 + 2, and the call is repeated with the exact count if the chunk holds more lines);
+    otherwise ss_fastq_scan + ss_fastq_index (two reads of the chunk, exact capacity)."""
     _require_cuda(buf, "buf")
     if buf.dtype != torch.uint8:
         raise TypeError("buf must be a uint8 tensor")
@@ -465,6 +469,26 @@ def fastq_index(buf: torch.Tensor, nbytes: Optional[int] = None, *, line0: int =
     dev = buf.device
     L_ = lib()
     s = _stream(dev)
+    if onepass:
+        cnt = torch.empty(3, dtype=torch.int64, device=dev)
+        cap = nbytes // 16 + 2 if max_reads is None else max_reads
+        while True:
+            ws_bytes = int(L_.ss_fastq_onepass_ws_bytes(nbytes, cap))
+            ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.int64, device=dev)
+            offs = torch.empty(cap, dtype=torch.int64, device=dev)
+            lens = torch.empty(cap, dtype=torch.int32, device=dev)
+            aux = torch.empty(cap, dtype=torch.int64, device=dev)
+            check(L_.ss_fastq_index_onepass(buf.data_ptr(), nbytes, line0, 1 if at_eof else 0, ws.data_ptr(), ws_bytes,
+                                            offs.data_ptr(), lens.data_ptr(), aux.data_ptr(), cap, cnt.data_ptr(), s),
+                  "ss_fastq_index_onepass")
+            nl, n, full = (int(v) for v in cnt.tolist())
+            if full:                  # a staging region ran full (lines far denser than the bound)
+                cap *= 2
+                continue
+            if n <= cap:
+                break
+            cap = n
+        return offs[:n], lens[:n].to(torch.int64) & 0xFFFFFFFF, nl
     ws_bytes = int(L_.ss_fastq_scan_ws_bytes(nbytes))
     ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.int64, device=dev)
     cnt = torch.empty(2, dtype=torch.int64, device=dev)

@@ -13,10 +13,14 @@
 //                   k_fq_scan_local / k_fq_scan_groups (two-level exclusive scan -> tile bases)
 //   ss_fastq_index: k_fq_emit  (re-reads the tile; the block scan gives every 16-B chunk its line
 //                               number; each '\n' closes a sequence line (end) or opens one (start),
-//                               each NUL inside a sequence line is folded in with atomicMin)
+//                               each NUL inside a sequence line is listed)
 //                   k_fq_lens  (thread per sequence line: the strlen - 1 rule -> lens)
+//                   k_fq_nulfix (the listed lines re-measured)
+//   HBM traffic: the chunk is read twice (count + emit), ~2 B per file byte.
+//   ss_fastq_index_onepass: the chunk read once (k_fq_nlpos stages newline positions per tile,
+//                   k_fq_place resolves line numbers from the tile counts): see below.
 // Output: d_offsets[i] / d_lens[i] of sequence line i, exactly the ragged layout ss_encode_var and
-// ss_gather_rows take.  HBM traffic: the chunk is read twice (count + emit), ~2 B per file byte.
+// ss_gather_rows take.
 #include "ss_device.h"
 #include "ss_internal.h"
 
@@ -135,10 +139,18 @@ __global__ __launch_bounds__(1024) void k_fq_scan_groups(uint64_t* __restrict__ 
     }
 }
 
+// NUL bytes are rare in FASTQ text: a sequence line holding one is appended (once per lane) to a
+// short list in the workspace, and k_fq_nulfix re-measures those lines with a strlen scan.  A list
+// that overflows makes k_fq_nulfix re-measure every line (exact either way).  Neither the offsets
+// nor the ends need a reset: every sequence line of the chunk gets both from its two newlines,
+// except a final line without '\n', which k_fq_lens recognises by its line number.
+constexpr uint32_t kNulCap = 1u << 16;
+
 struct FqOut {
     uint64_t* offsets;
-    uint64_t* ends;      // aux: '\n' position closing sequence line i (~0: none)
-    uint32_t* nul;       // NUL position (chunk-relative u32) inside sequence line i (~0u: none)
+    uint64_t* ends;      // aux: '\n' position closing sequence line i
+    uint32_t* nul_cnt;   // sequence lines with a NUL byte (may exceed kNulCap: overflow)
+    uint32_t* nul_list;  // [kNulCap] their indices
     uint64_t max_reads;
     uint64_t sel0;       // (line0 + 2) / 4 = sequence lines before the chunk
     uint64_t nbytes;
@@ -156,44 +168,84 @@ __device__ __forceinline__ void on_newline(const FqOut& o, uint64_t p, uint64_t 
     }
 }
 
-__global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ buf, FqOut o, uint64_t line0,
-                                                  const uint64_t* __restrict__ tile_base,
-                                                  const uint64_t* __restrict__ group_base) {
-    __shared__ uint64_t wtot[kFqT / 64];
-    const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile;
-    uint4 x[kFqU];
-    uint64_t packed = 0;                   // 16-bit newline count of chunk j at bits 16j
-#pragma unroll
-    for (int j = 0; j < kFqU; ++j) {
-        const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
-        x[j] = off < o.nbytes ? load_chunk(buf, off, o.nbytes) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-        packed |= (uint64_t)count_nl(x[j]) << (16 * j);
-    }
-    // block-wide inclusive scan of the four 16-bit lanes at once (each field's total <= 4096)
+// 16-bit mask of the '\n' bytes of a 16-B chunk (bit b = byte b)
+__device__ __forceinline__ uint32_t nib(uint32_t e) {            // 0x80 per hit byte -> 4 bits
+    return (((e >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+__device__ __forceinline__ uint32_t nl_mask16(const uint4& x) {
+    return nib(eq_bytes(x.x, 0x0A0A0A0Au)) | nib(eq_bytes(x.y, 0x0A0A0A0Au)) << 4 |
+           nib(eq_bytes(x.z, 0x0A0A0A0Au)) << 8 | nib(eq_bytes(x.w, 0x0A0A0A0Au)) << 12;
+}
+__device__ __forceinline__ bool has_nul(const uint4& x) {
+    return (eq_bytes(x.x, 0u) | eq_bytes(x.y, 0u) | eq_bytes(x.z, 0u) | eq_bytes(x.w, 0u)) != 0u;
+}
+
+// Block-wide inclusive scan of the 16-bit per-chunk newline counts, four chunk rows per u64 (each
+// field's block total <= 4096): excl[k] = this lane's exclusive prefix per field, total[k] = the
+// block's per-field totals.
+template <int P>
+__device__ __forceinline__ void scan_packed(const uint64_t (&packed)[P], uint64_t (*wtot)[P], uint64_t (&excl)[P],
+                                            uint64_t (&total)[P]) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint64_t v = packed;
+    uint64_t v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = packed[k];
     for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t u = __shfl_up(v, d);
-        if (lane >= (uint32_t)d) v += u;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const uint64_t u = __shfl_up(v[k], d);
+            if (lane >= (uint32_t)d) v[k] += u;
+        }
     }
-    if (lane == 63) wtot[wave] = v;
+    if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) wtot[wave][k] = v[k];
+    }
     __syncthreads();
-    uint64_t before = 0, total = 0;
 #pragma unroll
-    for (int w = 0; w < kFqT / 64; ++w) {
-        if ((uint32_t)w < wave) before += wtot[w];
-        total += wtot[w];
+    for (int k = 0; k < P; ++k) {
+        uint64_t before = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kFqT / 64; ++w) {
+            if ((uint32_t)w < wave) before += wtot[w][k];
+            tot += wtot[w][k];
+        }
+        excl[k] = before + v[k] - packed[k];
+        total[k] = tot;
     }
-    const uint64_t excl = before + v - packed;
-    uint64_t rows_before = 0;              // newlines in the rows j' < j (whole block)
-    const uint64_t lbase = line0 + group_base[blockIdx.x >> 10] + tile_base[blockIdx.x];
+}
+
+// Emission of one tile given its first line index lbase: every '\n' closes a line; the lines of a
+// block are ordered chunk-row j first, then lane.  Waves without a NUL byte take the 16-bit-mask
+// loop (one iteration per newline of the lane's chunk); a wave with a NUL walks bytes per word and
+// lists the sequence lines its NULs fall in.
+template <int U>
+__device__ __forceinline__ void emit_tile(const FqOut& o, const uint4 (&x)[U], uint64_t t0, uint64_t lbase,
+                                          const uint64_t (&excl)[U / 4], const uint64_t (&total)[U / 4]) {
+    bool nul = false;
 #pragma unroll
-    for (int j = 0; j < kFqU; ++j) {
+    for (int j = 0; j < U; ++j) nul |= has_nul(x[j]);
+    const bool wave_nul = __ballot(nul) != 0;
+    uint64_t rows_before = 0;              // newlines in the rows j' < j (whole block)
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
         const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
-        uint64_t li = lbase + rows_before + ((excl >> (16 * j)) & 0xFFFFu);
-        rows_before += (total >> (16 * j)) & 0xFFFFu;
+        uint64_t li = lbase + rows_before + ((excl[j / 4] >> (16 * (j % 4))) & 0xFFFFu);
+        rows_before += (total[j / 4] >> (16 * (j % 4))) & 0xFFFFu;
         if (off >= o.nbytes) continue;
+        if (!wave_nul) {
+            // bytes past nbytes load as ' ': every hit is inside the chunk
+            uint32_t m = nl_mask16(x[j]);
+            while (m) {
+                const uint32_t bit = __builtin_ctz(m);
+                m &= m - 1;
+                on_newline(o, off + bit, li);
+                ++li;
+            }
+            continue;
+        }
         const uint32_t xw[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+        uint64_t listed = ~0ull;           // the line this lane last put on the NUL list
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t mnl = eq_bytes(xw[q], 0x0A0A0A0Au), mnul = eq_bytes(xw[q], 0u);
@@ -206,36 +258,310 @@ __global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ bu
                 if ((mnl >> bit) & 1u) {
                     on_newline(o, p, li);
                     ++li;
-                } else if ((li & 3u) == 1u) {
+                } else if ((li & 3u) == 1u && li != listed) {
                     const uint64_t i = (li + 2) / 4 - o.sel0;
-                    if (i < o.max_reads) atomicMin(&o.nul[i], (uint32_t)p);
+                    listed = li;
+                    if (i < o.max_reads) {
+                        const uint32_t k = atomicAdd(o.nul_cnt, 1u);
+                        if (k < kNulCap) o.nul_list[k] = (uint32_t)i;
+                    }
                 }
             }
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_fq_lens(const uint8_t* __restrict__ buf, FqOut o, uint64_t line0,
-                                                 int at_eof, uint64_t ntiles, const uint64_t* __restrict__ tile_base,
-                                                 uint32_t* __restrict__ lens, uint64_t* d_nreads) {
-    const uint64_t nl = tile_base[ntiles];
-    const bool partial = at_eof && o.nbytes > 0 && buf[o.nbytes - 1] != '\n';
-    const uint64_t nlines = nl + (partial ? 1u : 0u);
-    const uint64_t nsel = (line0 + nlines + 2) / 4 - o.sel0;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i == 0) *d_nreads = nsel;
-    if (i >= nsel || i >= o.max_reads) return;
-    uint64_t start = o.offsets[i];
-    if (i == 0 && (line0 & 3u) == 1u) {
-        start = 0;                          // the chunk opens with a sequence line
-        o.offsets[0] = 0;
+template <int U>
+__device__ __forceinline__ void load_tile(const uint8_t* buf, uint64_t nbytes, uint64_t t0, uint4 (&x)[U],
+                                          uint64_t (&packed)[U / 4]) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
+        x[j] = off < nbytes ? load_chunk(buf, off, nbytes) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
     }
-    const uint64_t e = o.ends[i];
-    const bool has_nl = e != ~0ull;
-    const uint64_t end = has_nl ? e : o.nbytes;
-    const uint32_t nul = o.nul[i];
-    const uint64_t slen = nul != kNone32 ? (uint64_t)nul - start : end - start + (has_nl ? 1u : 0u);
-    lens[i] = slen == 0 ? kNone32 : (uint32_t)min<uint64_t>(slen - 1, 0xFFFFFFFEull);
+#pragma unroll
+    for (int k = 0; k < U / 4; ++k) packed[k] = 0;   // 16-bit newline count of chunk j at bits 16 (j % 4)
+#pragma unroll
+    for (int j = 0; j < U; ++j) packed[j / 4] |= (uint64_t)count_nl(x[j]) << (16 * (j % 4));
+}
+
+__global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ buf, FqOut o, uint64_t line0,
+                                                  const uint64_t* __restrict__ tile_base,
+                                                  const uint64_t* __restrict__ group_base) {
+    __shared__ uint64_t wtot[kFqT / 64][kFqU / 4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile;
+    uint4 x[kFqU];
+    uint64_t packed[kFqU / 4], excl[kFqU / 4], total[kFqU / 4];
+    load_tile(buf, o.nbytes, t0, x, packed);
+    scan_packed(packed, wtot, excl, total);
+    emit_tile(o, x, t0, line0 + group_base[blockIdx.x >> 10] + tile_base[blockIdx.x], excl, total);
+}
+
+// One read of the file (ss_fastq_index_onepass).  A decoupled look-back over tile counts measured
+// 1.25-1.47 ms for 2 GB (every waiting block polls the same status lines; the two-pass form took
+// 0.82), so the line numbers are resolved after the fact instead:
+//   k_fq_nlpos : 32-KiB tiles; each tile reserves a run of the staging array with one atomicAdd and
+//                writes its newline positions there in file order (u32, chunk-relative), plus its
+//                count and run start.  The reservations go to 64 counters (tile % 64), each on its
+//                own 128-B line with its own staging region: one counter word serves ~88
+//                atomics per us, which capped a single shared counter at 0.75 ms per 60k tiles.
+//                A region that runs full raises the overflow word (the caller retries with a larger
+//                bound).  NUL bytes (rare) go to a position list.
+//   k_fq_scan_local / k_fq_scan_groups over the tile counts -> each tile's first line number
+//   k_fq_place : tile-wise, the staged positions with their line numbers -> offsets / lens
+//   k_fq_nulfix: sequence lines holding a NUL byte re-measured
+// HBM: the file once + 4 B per line written and read back + 12 B per sequence line of output.
+constexpr int kFqU1 = 8;                                       // 16-B chunks per thread
+constexpr uint64_t kFqTile1 = (uint64_t)kFqT * kFqU1 * 16;     // 32 KiB per tile
+
+constexpr uint32_t kStageShards = 64, kShardStride = 32;       // counters 128 B apart
+constexpr uint32_t kLdsPos = 4096;                             // newline positions gathered in LDS
+
+struct FqStage {
+    uint32_t* pos;        // [kStageShards * region] staged newline positions
+    uint64_t region;      // staging words per shard
+    uint32_t* used;       // [kStageShards * kShardStride] run reservations per shard
+    uint32_t* ovf;        // a shard's region ran full
+    uint32_t* tile_cnt;   // [t] newlines per tile
+    uint32_t* tile_run;   // [t] start of the tile's run in pos
+    uint32_t* nul_cnt;    // NUL bytes seen (may exceed kNulCap)
+    uint32_t* nul_pos;    // [kNulCap] their positions
+};
+
+__global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ buf, uint64_t nbytes, FqStage st) {
+    __shared__ uint64_t wtot[kFqT / 64][kFqU1 / 4];
+    __shared__ uint32_t s_run, s_cnt;
+    __shared__ uint32_t spos[kLdsPos];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile1;
+    // the chunks live only until their newline masks are taken: 16 bits per chunk, two per VGPR
+    uint32_t mk[kFqU1 / 2];
+    bool nul = false;
+    {
+        uint4 x[kFqU1];
+#pragma unroll
+        for (int j = 0; j < kFqU1; ++j) {
+            const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
+            x[j] = off < nbytes ? load_chunk(buf, off, nbytes) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+        }
+#pragma unroll
+        for (int j = 0; j < kFqU1; j += 2) {
+            mk[j / 2] = nl_mask16(x[j]) | nl_mask16(x[j + 1]) << 16;
+            nul |= has_nul(x[j]) | has_nul(x[j + 1]);
+        }
+    }
+    uint64_t packed[kFqU1 / 4], excl[kFqU1 / 4], total[kFqU1 / 4];
+#pragma unroll
+    for (int k = 0; k < kFqU1 / 4; ++k) packed[k] = 0;
+#pragma unroll
+    for (int j = 0; j < kFqU1; ++j)
+        packed[j / 4] |= (uint64_t)__popc((mk[j / 2] >> (16 * (j & 1))) & 0xFFFFu) << (16 * (j % 4));
+    scan_packed(packed, wtot, excl, total);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kFqU1 / 4; ++k)
+        cnt += (uint32_t)((total[k] & 0xFFFFu) + ((total[k] >> 16) & 0xFFFFu) + ((total[k] >> 32) & 0xFFFFu) +
+                          (total[k] >> 48));
+    if (threadIdx.x == 0) {
+        // the reservation's round trip overlaps the other waves' LDS staging below
+        const uint32_t sh = blockIdx.x % kStageShards;
+        uint64_t run = (uint64_t)sh * st.region;
+        uint32_t c = cnt;
+        if (c) {
+            const uint32_t r = atomicAdd(&st.used[sh * kShardStride], c);
+            if (r + (uint64_t)c > st.region) {
+                atomicExch(st.ovf, 1u);
+                c = 0;                    // nothing staged; the call reports the overflow
+            }
+            run += r;
+        }
+        st.tile_cnt[blockIdx.x] = c;
+        st.tile_run[blockIdx.x] = (uint32_t)run;
+        s_run = (uint32_t)run;
+        s_cnt = c;
+    }
+    const bool in_lds = cnt <= kLdsPos;   // typical tiles: positions gathered in LDS, stored as one run
+    auto put = [&](uint32_t base) {
+        uint32_t rows_before = 0;
+#pragma unroll
+        for (int j = 0; j < kFqU1; ++j) {
+            const uint32_t off = (uint32_t)(t0 + 16ull * (j * kFqT + threadIdx.x));
+            uint32_t k = base + rows_before + (uint32_t)((excl[j / 4] >> (16 * (j % 4))) & 0xFFFFu);
+            rows_before += (uint32_t)((total[j / 4] >> (16 * (j % 4))) & 0xFFFFu);
+            uint32_t m = (mk[j / 2] >> (16 * (j & 1))) & 0xFFFFu;   // bytes past nbytes loaded as ' '
+            while (m) {
+                const uint32_t bit = __builtin_ctz(m);
+                m &= m - 1;
+                if (in_lds) spos[k++] = off + bit;
+                else st.pos[k++] = off + bit;
+            }
+        }
+    };
+    if (in_lds) put(0);
+    __syncthreads();
+    if (s_cnt) {
+        if (in_lds) {
+            const uint32_t run = s_run;
+            for (uint32_t e = threadIdx.x; e < cnt; e += kFqT) st.pos[run + e] = spos[e];
+        } else {
+            put(s_run);
+        }
+    }
+    if (__ballot(nul)) {                   // rare: reload the lane's chunks (keeps them out of VGPRs)
+#pragma unroll 1
+        for (int j = 0; j < kFqU1; ++j) {
+            const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
+            if (off >= nbytes) break;
+            const uint4 c = load_chunk(buf, off, nbytes);
+            const uint32_t xw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll 1
+            for (int q = 0; q < 4; ++q) {
+                uint32_t m = eq_bytes(xw[q], 0u);
+                while (m) {
+                    const uint32_t bit = __builtin_ctz(m);
+                    m &= m - 1;
+                    const uint64_t p = off + 4 * q + (bit >> 3);
+                    if (p >= nbytes) break;
+                    const uint32_t i = atomicAdd(st.nul_cnt, 1u);
+                    if (i < kNulCap) st.nul_pos[i] = (uint32_t)p;
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t fq_nsel(const uint8_t* buf, const FqOut& o, uint64_t line0, int at_eof,
+                                            uint64_t nl, bool& partial) {
+    partial = at_eof && o.nbytes > 0 && buf[o.nbytes - 1] != '\n';
+    return (line0 + nl + (partial ? 1u : 0u) + 2) / 4 - o.sel0;
+}
+
+// strlen - 1 of sequence line i from its start and its closing '\n' (or the chunk end for a final
+// line without one); slen 0 -> kNone32 (the reference's size_t underflow)
+__device__ __forceinline__ uint32_t fq_len(uint64_t slen) {
+    return slen == 0 ? kNone32 : (uint32_t)min<uint64_t>(slen - 1, 0xFFFFFFFEull);
+}
+
+__device__ __forceinline__ bool fq_has_nl(const FqOut& o, uint64_t line0, uint64_t nl, bool partial, uint64_t i) {
+    return !(partial && 4 * (o.sel0 + i) + 1 == line0 + nl);    // the unterminated last line
+}
+
+// one block per tile: staged newline k of the tile closes line lbase + k.  The newline closing a
+// sequence line (line number = 1 mod 4) gives its end; the newline before it (the tile's previous
+// entry, or the last one staged before the tile) gives its start: offsets[i] and lens[i] directly,
+// no end array and no separate length pass.  Block ntiles - 1 also places a final sequence line
+// without '\n' and writes the sequence-line count.
+constexpr int kPlaceR = 4;                                     // staged entries per thread per round
+
+// start of the line that follows the last newline staged before `tile` (0: none in the chunk)
+__device__ __forceinline__ uint64_t start_before(const FqStage& st, uint64_t tile) {
+    while (tile > 0) {
+        --tile;
+        const uint32_t c = st.tile_cnt[tile];
+        if (c) return (uint64_t)st.pos[st.tile_run[tile] + c - 1] + 1;
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ buf, FqOut o, uint64_t line0,
+                                                  int at_eof, FqStage st, uint64_t ntiles,
+                                                  const uint64_t* __restrict__ tile_base,
+                                                  const uint64_t* __restrict__ group_base,
+                                                  const uint64_t* __restrict__ d_nl, uint32_t* __restrict__ lens,
+                                                  uint64_t* d_nreads) {
+    const uint64_t tile = blockIdx.x;
+    const uint32_t cnt = st.tile_cnt[tile];
+    const uint32_t run = st.tile_run[tile];
+    const uint64_t lbase = line0 + group_base[tile >> 10] + tile_base[tile];
+    for (uint32_t k0 = 0; k0 < cnt; k0 += 256 * kPlaceR) {
+        uint32_t p[kPlaceR];
+#pragma unroll
+        for (int r = 0; r < kPlaceR; ++r) {
+            const uint32_t k = k0 + r * 256 + threadIdx.x;
+            if (k < cnt) p[r] = st.pos[run + k];
+        }
+#pragma unroll
+        for (int r = 0; r < kPlaceR; ++r) {
+            const uint32_t k = k0 + r * 256 + threadIdx.x;
+            const uint64_t li = lbase + k;
+            if (k >= cnt || (li & 3u) != 1u) continue;
+            const uint64_t i = (li >> 2) - o.sel0;
+            if (i >= o.max_reads) continue;
+            const uint64_t start = k ? (uint64_t)st.pos[run + k - 1] + 1 : (li == line0 ? 0 : start_before(st, tile));
+            o.offsets[i] = start;
+            lens[i] = fq_len((uint64_t)p[r] - start + 1);
+        }
+    }
+    if (tile + 1 == ntiles && threadIdx.x == 0) {
+        const uint64_t nl = *d_nl;
+        bool partial;
+        *d_nreads = fq_nsel(buf, o, line0, at_eof, nl, partial);
+        const uint64_t last = line0 + nl;                  // the unterminated final line, if any
+        if (partial && (last & 3u) == 1u) {
+            const uint64_t i = (last >> 2) - o.sel0;
+            if (i < o.max_reads) {
+                const uint64_t start = nl ? start_before(st, ntiles) : 0;
+                o.offsets[i] = start;
+                lens[i] = fq_len(o.nbytes - start);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fq_lens(const uint8_t* __restrict__ buf, FqOut o, uint64_t line0,
+                                                 int at_eof, const uint64_t* __restrict__ d_nl,
+                                                 uint32_t* __restrict__ lens, uint64_t* d_nreads) {
+    const uint64_t nl = *d_nl;
+    bool partial;
+    const uint64_t nsel = fq_nsel(buf, o, line0, at_eof, nl, partial);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *d_nreads = nsel;
+    const uint64_t lim = min(nsel, o.max_reads);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < lim; i += (uint64_t)gridDim.x * 256) {
+        uint64_t start = o.offsets[i];
+        if (i == 0 && (line0 & 3u) == 1u) {
+            start = 0;                      // the chunk opens with a sequence line
+            o.offsets[0] = 0;
+        }
+        const bool has_nl = fq_has_nl(o, line0, nl, partial, i);
+        lens[i] = fq_len(has_nl ? o.ends[i] - start + 1 : o.nbytes - start);
+    }
+}
+
+// Sequence lines with a NUL byte: strlen stops at the first NUL.  The lines that hold a listed NUL
+// (or, after a list overflow, all lines) are re-measured byte by byte; runs after the lengths pass.
+// BYLINE: the list holds sequence-line indices (two-pass emit); otherwise NUL byte positions (one
+// pass), mapped to their line by a binary search over the line starts.
+template <bool BYLINE>
+__global__ __launch_bounds__(256) void k_fq_nulfix(const uint8_t* __restrict__ buf, FqOut o, uint64_t line0,
+                                                   int at_eof, const uint64_t* __restrict__ d_nl,
+                                                   uint32_t* __restrict__ lens) {
+    const uint32_t cnt = *o.nul_cnt;
+    if (cnt == 0) return;
+    bool partial;
+    const uint64_t lim = min(fq_nsel(buf, o, line0, at_eof, *d_nl, partial), o.max_reads);
+    if (lim == 0) return;
+    const bool all = cnt > kNulCap;
+    const uint64_t n = all ? lim : cnt;
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256) {
+        uint64_t i = e;
+        if (!all) {
+            if (BYLINE) {
+                i = o.nul_list[e];
+            } else {
+                const uint64_t p = o.nul_list[e];      // last line starting at or before p
+                uint64_t lo = 0, hi = lim;
+                while (hi - lo > 1) {
+                    const uint64_t mid = (lo + hi) / 2;
+                    if (o.offsets[mid] <= p) lo = mid; else hi = mid;
+                }
+                i = lo;
+                if (o.offsets[i] > p) continue;
+            }
+        }
+        const uint64_t start = o.offsets[i];    // strlen: stop at the line's '\n', a NUL or the chunk end
+        uint64_t p = start;
+        while (p < o.nbytes && buf[p] != 0 && buf[p] != '\n') ++p;
+        if (p < o.nbytes && buf[p] == 0) lens[i] = fq_len(p - start);
+    }
 }
 
 // Gather rows: dst row r (r < m) = src[offsets[sel ? sel[r] : r] ..  + L), L <= 1024, into a dense
@@ -293,10 +619,11 @@ inline uint64_t fq_groups(uint64_t t) { return (t + 1023) / 1024; }
 
 extern "C" {
 
-// workspace: tile_base u64 [t + 1] | group_base u64 [g + 1] | tile_cnt u32 [t]
+// two-pass workspace: tile_base u64 [t + 1] | group_base u64 [g + 1] | nul_cnt u32 (8-B slot) |
+// nul_list u32 [kNulCap] | tile_cnt u32 [t]
 uint64_t ss_fastq_scan_ws_bytes(uint64_t nbytes) {
     const uint64_t t = fq_tiles(nbytes);
-    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4 * t + 16;
+    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 8 + 4ull * kNulCap + 4 * t + 16;
 }
 
 int ss_fastq_scan(const uint8_t* d_buf, uint64_t nbytes, void* d_ws, uint64_t ws_bytes, uint64_t* d_nlines,
@@ -310,7 +637,7 @@ int ss_fastq_scan(const uint8_t* d_buf, uint64_t nbytes, void* d_ws, uint64_t ws
     uint64_t* tile_base = (uint64_t*)d_ws;
     uint64_t* group_base = tile_base + t + 1;
     const uint64_t g = fq_groups(t);
-    uint32_t* tile_cnt = (uint32_t*)(group_base + g + 1);
+    uint32_t* tile_cnt = (uint32_t*)(group_base + g + 1) + 2 + kNulCap;
     if (t) {
         hipLaunchKernelGGL(k_fq_count, dim3((unsigned)t), dim3(kFqT), 0, s, d_buf, nbytes, tile_cnt);
         hipLaunchKernelGGL(k_fq_scan_local, dim3((unsigned)g), dim3(1024), 0, s, (const uint32_t*)tile_cnt, t,
@@ -320,35 +647,114 @@ int ss_fastq_scan(const uint8_t* d_buf, uint64_t nbytes, void* d_ws, uint64_t ws
     return ss_check(hipGetLastError(), "k_fq_count/k_fq_scan");
 }
 
-int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, const void* d_ws,
-                   uint64_t* d_offsets, uint32_t* d_lens, uint64_t* d_aux, uint64_t max_reads,
-                   uint64_t* d_nreads, void* stream) {
+static int fq_check(const uint8_t* d_buf, uint64_t nbytes, const void* d_ws, const void* d_out, uint64_t max_reads,
+                    const void* d_offsets, const void* d_lens, const void* d_aux) {
     if (nbytes >= (1ull << 32)) return ss_fail(SS_EARG, "FASTQ chunk must be < 4 GiB");
-    if (!d_ws || !d_nreads || (nbytes && !d_buf)) return ss_fail(SS_EARG, "null buffer");
+    if (!d_ws || !d_out || (nbytes && !d_buf)) return ss_fail(SS_EARG, "null buffer");
     if (max_reads && (!d_offsets || !d_lens || !d_aux)) return ss_fail(SS_EARG, "null output buffer");
     if ((((uintptr_t)d_buf) & 15) || (((uintptr_t)d_ws) & 7)) return ss_fail(SS_EARG, "d_buf must be 16-B aligned, d_ws 8-B");
+    return SS_OK;
+}
+
+static FqOut fq_out(uint64_t* d_offsets, uint64_t* d_aux, uint32_t* nul_cnt, uint64_t max_reads, uint64_t line0,
+                    uint64_t nbytes) {
+    FqOut o;
+    o.offsets = d_offsets;
+    o.ends = d_aux;
+    o.nul_cnt = nul_cnt;
+    o.nul_list = nul_cnt + 2;
+    o.max_reads = max_reads;
+    o.sel0 = (line0 + 2) / 4;
+    o.nbytes = nbytes;
+    return o;
+}
+
+// lens + NUL fix-up (grid-stride, at most 256 x 64 blocks)
+static int fq_finish(hipStream_t s, const uint8_t* d_buf, const FqOut& o, uint64_t line0, int at_eof,
+                     const uint64_t* d_nl, uint32_t* d_lens, uint64_t* d_nreads) {
+    uint64_t g = o.max_reads ? (o.max_reads + 255) / 256 : 1;
+    if (g > 256ull * 64) g = 256ull * 64;
+    hipLaunchKernelGGL(k_fq_lens, dim3((unsigned)g), dim3(256), 0, s, d_buf, o, line0, at_eof, d_nl, d_lens, d_nreads);
+    hipLaunchKernelGGL(k_fq_nulfix<true>, dim3(256), dim3(256), 0, s, d_buf, o, line0, at_eof, d_nl, d_lens);
+    return ss_check(hipGetLastError(), "k_fq_lens/k_fq_nulfix");
+}
+
+int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, void* d_ws,
+                   uint64_t* d_offsets, uint32_t* d_lens, uint64_t* d_aux, uint64_t max_reads,
+                   uint64_t* d_nreads, void* stream) {
+    int rc = fq_check(d_buf, nbytes, d_ws, d_nreads, max_reads, d_offsets, d_lens, d_aux);
+    if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     const uint64_t t = fq_tiles(nbytes);
     const uint64_t* tile_base = (const uint64_t*)d_ws;
     const uint64_t* group_base = tile_base + t + 1;
-    int rc = SS_OK;
-    if (max_reads) {
-        rc = ss_check(hipMemsetAsync(d_aux, 0xFF, max_reads * sizeof(uint64_t), s), "fastq aux reset");
-        if (!rc) rc = ss_check(hipMemsetAsync(d_lens, 0xFF, max_reads * sizeof(uint32_t), s), "fastq lens reset");
-        if (rc) return rc;
-    }
-    FqOut o;
-    o.offsets = d_offsets;
-    o.ends = d_aux;
-    o.nul = d_lens;               // NUL positions live in the lens array until k_fq_lens replaces them
-    o.max_reads = max_reads;
-    o.sel0 = (line0 + 2) / 4;
-    o.nbytes = nbytes;
+    uint32_t* nul_cnt = (uint32_t*)(group_base + fq_groups(t) + 1);
+    rc = ss_check(hipMemsetAsync(nul_cnt, 0, 4, s), "fastq NUL counter reset");
+    if (rc) return rc;
+    const FqOut o = fq_out(d_offsets, d_aux, nul_cnt, max_reads, line0, nbytes);
     if (t) hipLaunchKernelGGL(k_fq_emit, dim3((unsigned)t), dim3(kFqT), 0, s, d_buf, o, line0, tile_base, group_base);
-    const uint64_t g = max_reads ? (max_reads + 255) / 256 : 1;
-    hipLaunchKernelGGL(k_fq_lens, dim3((unsigned)(g < 0x7FFFFFFFull ? g : 0x7FFFFFFFull)), dim3(256), 0, s, d_buf, o, line0,
-                       at_eof, t, tile_base, d_lens, d_nreads);
-    return ss_check(hipGetLastError(), "k_fq_emit/k_fq_lens");
+    rc = ss_check(hipGetLastError(), "k_fq_emit");
+    return rc ? rc : fq_finish(s, d_buf, o, line0, at_eof, tile_base + t, d_lens, d_nreads);
+}
+
+// one-pass workspace: tile_base u64 [t + 1] | group_base u64 [g + 1] | used u32 [64 x 32] | ovf u32,
+// nul_cnt u32 | nul_pos u32 [kNulCap] | tile_cnt u32 [t] | tile_run u32 [t] | pos u32 [64 x region]
+inline uint64_t fq_tiles1(uint64_t nbytes) { return (nbytes + kFqTile1 - 1) / kFqTile1; }
+
+// staging words per shard: the lines max_reads implies (4 per sequence line) + 25 %, spread over the
+// shards, plus one whole tile of single-byte lines per shard for the uneven spread
+inline uint64_t fq_region(uint64_t max_reads) {
+    const uint64_t lines = 4 * max_reads + 8;
+    return (lines + lines / 4) / kStageShards + kFqTile1;
+}
+
+uint64_t ss_fastq_onepass_ws_bytes(uint64_t nbytes, uint64_t max_reads) {
+    const uint64_t t = fq_tiles1(nbytes);
+    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 8 + 4ull * kNulCap + 8 * t +
+           4 * kStageShards * fq_region(max_reads) + 16;
+}
+
+int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, void* d_ws,
+                           uint64_t ws_bytes, uint64_t* d_offsets, uint32_t* d_lens, uint64_t* d_aux,
+                           uint64_t max_reads, uint64_t* d_counts, void* stream) {
+    int rc = fq_check(d_buf, nbytes, d_ws, d_counts, max_reads, d_offsets, d_lens, d_aux);
+    if (rc) return rc;
+    if (ws_bytes < ss_fastq_onepass_ws_bytes(nbytes, max_reads)) return ss_fail(SS_EARG, "workspace too small");
+    if (kStageShards * fq_region(max_reads) >= (1ull << 32)) return ss_fail(SS_EARG, "max_reads too large");
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t t = fq_tiles1(nbytes), g = fq_groups(t);
+    uint64_t* tile_base = (uint64_t*)d_ws;
+    uint64_t* group_base = tile_base + t + 1;
+    FqStage st;
+    st.used = (uint32_t*)(group_base + g + 1);
+    st.ovf = st.used + kStageShards * kShardStride;
+    st.nul_cnt = st.ovf + 1;
+    st.nul_pos = st.ovf + 2;
+    st.tile_cnt = st.nul_pos + kNulCap;
+    st.tile_run = st.tile_cnt + t;
+    st.pos = st.tile_run + t;
+    st.region = fq_region(max_reads);
+    rc = ss_check(hipMemsetAsync(st.used, 0, 4 * (kStageShards * kShardStride + 2), s), "fastq staging reset");
+    if (rc) return rc;
+    FqOut o = fq_out(d_offsets, d_aux, st.nul_cnt, max_reads, line0, nbytes);
+    o.nul_list = st.nul_pos;
+    if (t) {
+        hipLaunchKernelGGL(k_fq_nlpos, dim3((unsigned)t), dim3(kFqT), 0, s, d_buf, nbytes, st);
+        hipLaunchKernelGGL(k_fq_scan_local, dim3((unsigned)g), dim3(1024), 0, s, (const uint32_t*)st.tile_cnt, t,
+                           tile_base, group_base);
+    }
+    hipLaunchKernelGGL(k_fq_scan_groups, dim3(1), dim3(1024), 0, s, group_base, g, t, tile_base, d_counts);
+    if (t) {
+        hipLaunchKernelGGL(k_fq_place, dim3((unsigned)t), dim3(256), 0, s, d_buf, o, line0, at_eof, st, t, tile_base,
+                           group_base, (const uint64_t*)d_counts, d_lens, d_counts + 1);
+        hipLaunchKernelGGL(k_fq_nulfix<false>, dim3(256), dim3(256), 0, s, d_buf, o, line0, at_eof,
+                           (const uint64_t*)d_counts, d_lens);
+    }
+    rc = ss_check(hipGetLastError(), "k_fq_nlpos/k_fq_place/k_fq_nulfix");
+    if (!rc && t == 0) rc = ss_check(hipMemsetAsync(d_counts + 1, 0, 8, s), "fastq read count");   // empty chunk
+    if (!rc) rc = ss_check(hipMemsetAsync(d_counts + 2, 0, 8, s), "fastq status");
+    if (!rc) rc = ss_check(hipMemcpyAsync(d_counts + 2, st.ovf, 4, hipMemcpyDeviceToDevice, s), "fastq status");
+    return rc;
 }
 
 int ss_gather_rows(const uint8_t* d_src, uint64_t src_bytes, const uint64_t* d_offsets, const uint64_t* d_sel,

@@ -108,7 +108,7 @@ def _random_fastq(rng, nrec, edge=True):
     return data
 
 
-def _gpu_index(B, torch, dev, data, cuts=()):
+def _gpu_index(B, torch, dev, data, cuts=(), **kw):
     """Index `data` on the device in chunks ending right after the newlines at `cuts` (byte
     positions); returns global (offsets, lens)."""
     bounds = [0] + sorted(cuts) + [len(data)]
@@ -118,7 +118,7 @@ def _gpu_index(B, torch, dev, data, cuts=()):
         chunk = data[a:b]
         buf = torch.tensor(np.frombuffer(chunk, np.uint8) if chunk else np.zeros(0, np.uint8),
                            dtype=torch.uint8, device=dev)
-        offs, lens, nl = B.fastq_index(buf, len(chunk), line0=line0, at_eof=(b == len(data)))
+        offs, lens, nl = B.fastq_index(buf, len(chunk), line0=line0, at_eof=(b == len(data)), **kw)
         offs_all.append(offs.cpu().numpy().astype(np.uint64) + np.uint64(a))
         lens_all.append(lens.cpu().numpy().astype(np.uint32))
         line0 += nl
@@ -126,7 +126,8 @@ def _gpu_index(B, torch, dev, data, cuts=()):
 
 
 @pytest.mark.gpu
-def test_fastq_index_gpu_matches_oracle(gpu, oracle, golden):
+@pytest.mark.parametrize("onepass", [True, False])
+def test_fastq_index_gpu_matches_oracle(gpu, oracle, golden, onepass):
     import torch
     import shortseq_amd.batch as B
     files = [bytes.fromhex(c["file_hex"]) for _n, c in _cases(golden)]
@@ -135,26 +136,69 @@ def test_fastq_index_gpu_matches_oracle(gpu, oracle, golden):
     files += [b"\n", b"\n\n", b"\n\n\n", b"a\nb\nc\nd\ne\nf", b"x" * 20000 + b"\n" + b"AC" * 9000 + b"\n"]
     for data in files:
         eo, el = oracle.fastq_index(data)
-        go, gl = _gpu_index(B, torch, gpu, data)
+        go, gl = _gpu_index(B, torch, gpu, data, onepass=onepass)
         assert np.array_equal(go, eo) and np.array_equal(gl, el), data[:60]
         # chunked: random cut points right after newlines
         nls = [i + 1 for i in range(len(data)) if data[i] == 10 and i + 1 < len(data)]
         for _ in range(3):
             cuts = rng.sample(nls, min(len(nls), rng.randrange(1, 6))) if nls else []
-            go, gl = _gpu_index(B, torch, gpu, data, cuts)
+            go, gl = _gpu_index(B, torch, gpu, data, cuts, onepass=onepass)
             assert np.array_equal(go, eo) and np.array_equal(gl, el), (data[:60], cuts)
 
 
 @pytest.mark.gpu
-def test_fastq_index_gpu_large(gpu, oracle):
+@pytest.mark.parametrize("onepass", [True, False])
+def test_fastq_index_gpu_large(gpu, oracle, onepass):
     """A multi-tile file (many 16-KiB tiles) against the oracle."""
     import torch
     import shortseq_amd.batch as B
     rng = random.Random(12)
     data = _random_fastq(rng, 40_000)
     eo, el = oracle.fastq_index(data)
-    go, gl = _gpu_index(B, torch, gpu, data)
+    go, gl = _gpu_index(B, torch, gpu, data, onepass=onepass)
     assert len(eo) == 40_000 and np.array_equal(go, eo) and np.array_equal(gl, el)
+
+
+@pytest.mark.gpu
+def test_fastq_index_onepass_capacity_retry(gpu, oracle):
+    """A capacity guess below the chunk's sequence lines: the one-pass call is repeated exactly."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = random.Random(14)
+    data = _random_fastq(rng, 5000)
+    eo, el = oracle.fastq_index(data)
+    for cap in (1, 17, 4999):
+        go, gl = _gpu_index(B, torch, gpu, data, max_reads=cap)
+        assert np.array_equal(go, eo) and np.array_equal(gl, el), cap
+    # 3 MiB of empty lines with a bound of 1: the per-shard staging regions run full (doubling path)
+    data = b"\n" * (3 << 20) + b"ACGT\n"
+    eo, el = oracle.fastq_index(data)
+    go, gl = _gpu_index(B, torch, gpu, data, max_reads=1)
+    assert np.array_equal(go, eo) and np.array_equal(gl, el)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("onepass", [True, False])
+def test_fastq_index_nul_list_overflow(gpu, oracle, onepass):
+    """More NUL-holding sequence lines than the NUL list holds (65,536): every line is re-measured;
+    NULs at the line start (strlen 0), inside, and doubled, plus NULs outside sequence lines."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(15)
+    parts = []
+    for i in range(70_000):
+        L = int(rng.integers(3, 40))
+        seq = bytearray(rng.choice(np.frombuffer(b"ACGT", np.uint8), L).tobytes())
+        k = int(rng.integers(0, L))
+        seq[k] = 0
+        if i % 3 == 0:
+            seq[min(L - 1, k + 1)] = 0
+        hdr = b"@r\x00%d" % i if i % 5 == 0 else b"@r%d" % i
+        parts.append(hdr + b"\n" + bytes(seq) + b"\n+\n" + b"I" * L + b"\n")
+    data = b"".join(parts)
+    eo, el = oracle.fastq_index(data)
+    go, gl = _gpu_index(B, torch, gpu, data, onepass=onepass)
+    assert len(eo) == 70_000 and np.array_equal(go, eo) and np.array_equal(gl, el)
 
 
 @pytest.mark.gpu
