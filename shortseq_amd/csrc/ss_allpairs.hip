@@ -215,14 +215,32 @@ __device__ __noinline__ void ap_hits(const AllPairsArgs& a, const int* st, uint3
     }
 }
 
+// Upper-triangle tile pair (bi <= bj) of linear block k over t tiles, row-major: row bi holds
+// t - bi pairs.  A float estimate of bi, corrected by integer steps.
+__device__ __forceinline__ void tri_pair(uint64_t k, uint64_t t, uint32_t& bi, uint32_t& bj) {
+    const double b = 2.0 * (double)t + 1.0;
+    int64_t i = (int64_t)((b - sqrt(b * b - 8.0 * (double)k)) / 2.0);
+    auto before = [&](int64_t r) { return (uint64_t)(r * (int64_t)t - r * (r - 1) / 2); };   // pairs in rows < r
+    if (i < 0) i = 0;
+    while (i > 0 && before(i) > k) --i;
+    while (before(i + 1) <= k) ++i;
+    bi = (uint32_t)i;
+    bj = (uint32_t)(i + (int64_t)(k - before(i)));
+}
+
 // TAB: fragments from a 256-entry LDS table (4 codes of a byte -> the 4 one-hot VGPRs of a k-step
 // half, one ds_read_b128) instead of per-VGPR bit arithmetic.  Positions P .. 8 KS - 1 are then
 // code 0 on both sides and add the constant 8 KS - P to every result, folded into the threshold.
-template <int KS, int RB, bool TAB>
+// TRI: the launch may be a 1-D grid over upper-triangle tile pairs (kept out of the RB >= 4
+// instantiations: its registers cost them a wave per SIMD)
+template <int KS, int RB, bool TAB, bool TRI>
 __global__ __launch_bounds__(256) void k_allpairs_mfma(AllPairsArgs a, uint32_t P) {
     constexpr int S = 4 * RB * 32;
     constexpr int NW = (KS + 3) / 4;                       // packed words per read (32 positions each)
-    const uint32_t bi = blockIdx.y, bj = blockIdx.x;
+    // one block per upper-triangle tile pair (a 1-D grid while its work-item count fits 32 bits;
+    // beyond that the square 2-D grid, lower-triangle blocks exiting at once)
+    uint32_t bi = blockIdx.y, bj = blockIdx.x;
+    if (TRI && gridDim.y == 1) tri_pair(blockIdx.x, (a.n + S - 1) / S, bi, bj);
     if (bj < bi) return;
     __shared__ uint64_t cw[S * NW];
     __shared__ uint32_t rowcnt[S], colcnt[S];
@@ -330,7 +348,12 @@ int launch_allpairs_mfma(AllPairsArgs a, uint32_t P, hipStream_t s) {
     constexpr int S = 4 * RB * 32;
     const uint64_t t = (a.n + S - 1) / S;
     if (t > 65535) return ss_fail(SS_EARG, "all-pairs: n too large for one launch (split the batch)");
-    hipLaunchKernelGGL((k_allpairs_mfma<KS, RB, TAB>), dim3((unsigned)t, (unsigned)t), dim3(256), 0, s, a, P);
+    const uint64_t tri = t * (t + 1) / 2;
+    // measured: the 1-D triangle is faster at RB <= 2 (50k x 32 nt 7.45 -> 8.16 T pairs/s, 20k x 96 nt
+    // 1.80 -> 1.92), slower at RB 8 (100k x 12 nt 15.6 -> 13.3), where the square grid stays
+    constexpr bool TRI = RB <= 2;
+    const dim3 grid = (TRI && t > 1 && tri * 256 < (1ull << 32)) ? dim3((unsigned)tri) : dim3((unsigned)t, (unsigned)t);
+    hipLaunchKernelGGL((k_allpairs_mfma<KS, RB, TAB, TRI>), grid, dim3(256), 0, s, a, P);
     return ss_check(hipGetLastError(), "k_allpairs_mfma");
 }
 
