@@ -198,6 +198,33 @@ def bench_encode_hamming(B, lib, dev, rank, world, n, L, steps, warmup, seed=2):
     return el, timer.mean_ms(), timer.region_ms / steps
 
 
+def bench_hamming_only(B, lib, dev, rank, world, n, L, steps, warmup, seed=6):
+    """SURVEY §8(d) C3': hamming vs one reference on pre-packed words (ss_hamming_ref, k_ham_dense);
+    the words come from a device encode of synthetic reads, the timed step is the hamming launch."""
+    i0 = rank * n
+    ascii = B.synth_reads(n, L, seed=seed, i0=i0, device=dev)
+    words = B.encode(ascii, L)
+    del ascii
+    ref = words[0].clone()
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    wpr = words.shape[1]
+    wp, rp, op = words.data_ptr(), ref.data_ptr(), out.data_ptr()
+
+    def step(timer):
+        rc = lib.ss_hamming_ref(wp, n, L, wpr, rp, op, stream)
+        if rc:
+            raise RuntimeError(lib.ss_last_error_string())
+
+    el, tr = timed_loop(step, steps, warmup, world)
+    # parity: distance to read 0 == the fused encode's distance computed against read 0's words
+    _, want = B.encode_hamming_ref(B.synth_reads(n, L, seed=seed, i0=i0, device=dev), L, ref, store_words=False)
+    if not torch.equal(out, want):
+        raise SystemExit(f"PARITY FAILURE: ss_hamming_ref L={L} != fused encode+hamming")
+    del words, out, want
+    return el, tr.region_ms / steps
+
+
 def bench_roundtrip(B, lib, dev, rank, world, n, L, steps, warmup, seed=3):
     i0 = rank * n
     ascii = B.synth_reads(n, L, seed=seed, i0=i0, device=dev)
@@ -588,6 +615,15 @@ def main():
                          "unit": "GB/s", "frac": b3 / (d3 * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "algo_bytes_per_step": b3,
                          "note": "device time per step over the timed region (incl. the 1-read ref encode)"}}
+        for Lh, nh in ((32, args.reads_per_gpu), (96, args.reads_per_gpu), (512, args.reads_per_gpu // 2)):
+            log(f"C3' hamming only (pre-packed) {nh} x {Lh}")
+            elh, dh = bench_hamming_only(B, lib, dev, rank, world, nh, Lh, args.steps, args.warmup)
+            bh = nh * (8 * B.wpr_for(Lh) + 4)   # packed words in + u32 distance out
+            extra[f"C3p_hamming_ref_{Lh}"] = {
+                "pairs_per_s": nh * world / (elh / args.steps), "ms_per_step": elh / args.steps * 1e3,
+                "device_ms_per_step": dh, "reads": nh,
+                "roofline": {"kernel": "k_ham_dense3" if Lh == 96 else "k_ham_dense", "achieved": bh / (dh * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": bh / (dh * 1e-3) / 1e9 / HBM_PEAK_GBS, "algo_bytes_per_step": bh}}
         L4, n4 = 512, args.reads_per_gpu // 2
         log(f"C4 encode+decode {n4} x {L4}")
         s4 = max(5, args.steps // 2)

@@ -7,6 +7,7 @@
 //                  __shfl_xor and per-read sums (fused hamming) reduce inside the group.
 //   k_encode_gen   any L / stride / variable lengths: one lane per output word, aligned dword
 //                  loads + v_alignbyte; the general and ragged path.
+//   k_ham_dense / k_ham_dense3  hamming on dense packed rows (dwordx4 streams; k_ham_group otherwise)
 //   k_decode_g16 / k_decode_gen, k_ham_group, k_synth_*.
 #include "ss_device.h"
 #include "ss_internal.h"
@@ -327,6 +328,158 @@ __global__ __launch_bounds__(kThreads) void k_ham_group(const uint64_t* __restri
     if (r < n && k == 0) out[r] = part;
 }
 
+// Dense hamming for W = 3 (96-nt reads) without LDS: every wave streams chunks of 63 consecutive
+// dwordx4 (lane 63 idles, 1.6 % of the lanes), so a chunk is 21 lane triples = 42 whole reads and a
+// triple (p = 0, 1, 2) holds words 6m .. 6m+5: read 2m = p0.lo + p0.hi + p1.lo, read 2m+1 = p1.hi +
+// p2.lo + p2.hi.  Two shuffles move p1's halves to p0 and p2, which store the two distances.  Chunk c
+// = j * (T / 64) + wave, so at each j the block's waves read one contiguous span.
+template <bool PAIR, int T, int U>
+__global__ __launch_bounds__(T) void k_ham_dense3(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                  const uint64_t* __restrict__ ref, uint64_t n,
+                                                  uint32_t* __restrict__ out) {
+    constexpr uint32_t NWV = T / 64, RPC = 42, QPC = 63;
+    constexpr uint32_t RPB = RPC * NWV * U;          // reads per block (even)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t m = lane / 3u, p = lane - 3u * m;
+    const uint64_t r0 = (uint64_t)blockIdx.x * RPB;
+    const uint32_t nr = (uint32_t)min((uint64_t)RPB, n - r0);
+    const uint32_t nw = 3u * nr, nfull = nw / 2;
+    const uint64_t q0 = r0 * 3u / 2u;
+    auto load = [&](const uint4* src, uint32_t ql) -> uint4 {
+        if (lane < QPC && ql < nfull) return ld_stream(&src[q0 + ql]);
+        if (lane < QPC && ql * 2 < nw) {
+            const uint64_t v = ((const uint64_t*)src)[2 * (q0 + ql)];
+            return make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+        }
+        return make_uint4(0u, 0u, 0u, 0u);
+    };
+    uint4 x[U], y[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t ql = (j * NWV + wv) * QPC + lane;
+        x[j] = load(a, ql);
+        if constexpr (PAIR) y[j] = load(b, ql);
+    }
+    uint64_t rl = 0, rh = 0;   // reference words at this lane's two positions: (2p) % 3, (2p + 1) % 3
+    if constexpr (!PAIR) {
+        rl = ref[p == 0 ? 0 : (p == 1 ? 2 : 1)];
+        rh = ref[p == 0 ? 1 : (p == 1 ? 0 : 2)];
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t wlo = ((uint64_t)x[j].y << 32) | x[j].x, whi = ((uint64_t)x[j].w << 32) | x[j].z;
+        uint64_t clo = rl, chi = rh;
+        if constexpr (PAIR) {
+            clo = ((uint64_t)y[j].y << 32) | y[j].x;
+            chi = ((uint64_t)y[j].w << 32) | y[j].z;
+        }
+        const uint32_t dl = ham64(wlo ^ clo), dh = ham64(whi ^ chi);
+        const uint32_t from_next = __shfl(dl, (int)min(lane + 1u, 63u));   // p0 <- p1.lo
+        const uint32_t from_prev = __shfl(dh, (int)(lane == 0 ? 0u : lane - 1u));   // p2 <- p1.hi
+        const uint32_t rb = (j * NWV + wv) * RPC + 2u * m;                   // block-local read of p0
+        if (lane < QPC) {
+            if (p == 0 && rb < nr) out[r0 + rb] = dl + dh + from_next;
+            if (p == 2 && rb + 1 < nr) out[r0 + rb + 1] = from_prev + dl + dh;
+        }
+    }
+}
+
+// Dense hamming on packed rows (wpr == W, 16-B aligned): the block owns RPB whole reads = RPB*W
+// consecutive words (RPB even, so every block starts on a 16-B boundary) and streams them as
+// dwordx4 pairs of words, U per lane, all loads issued before any use.
+//   W = 1:        a lane's pair of words is two reads -> one 8-B store of two distances
+//   W = 2^k >= 2: a read is W/2 consecutive lanes -> shfl_xor sum, the group's first lane stores
+//   other W:      per-word distances (<= 32) as bytes in LDS, then one thread per read sums its W
+//                 bytes and the block stores its distances coalesced
+template <bool PAIR, bool POW2, int T, int U>
+__global__ __launch_bounds__(T) void k_ham_dense(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                 const uint64_t* __restrict__ ref, uint64_t n, uint32_t W,
+                                                 uint32_t rpb, float inv_w, uint32_t* __restrict__ out) {
+    __shared__ uint8_t part[POW2 ? 1 : 2 * T * U];
+    __shared__ uint64_t sref[PAIR || POW2 ? 1 : 32];   // the reference read (W <= 32 words)
+    if constexpr (!PAIR && !POW2) {
+        if (threadIdx.x < W) sref[threadIdx.x] = ref[threadIdx.x];
+    }
+    // power-of-two W: lane ql's words sit at positions (2 ql) % W and (2 ql + 1) % W of their read,
+    // the same for every j (W divides 2T), so the reference words are fetched once per lane
+    uint64_t pref_lo = 0, pref_hi = 0;
+    if constexpr (!PAIR && POW2) {
+        pref_lo = ref[W == 1 ? 0u : ((2u * threadIdx.x) & (W - 1u))];
+        pref_hi = ref[W == 1 ? 0u : ((2u * threadIdx.x + 1u) & (W - 1u))];
+    }
+    const uint64_t r0 = (uint64_t)blockIdx.x * rpb;
+    const uint32_t nr = (uint32_t)min((uint64_t)rpb, n - r0);
+    const uint32_t nw = nr * W, nfull = nw / 2;    // live words; whole dwordx4 of the block
+    const uint64_t q0 = r0 * W / 2;
+    // an odd word count ends on a half pair: that word is read alone (no over-read past the rows)
+    auto load = [&](const uint4* p, uint32_t ql) -> uint4 {
+        if (ql < nfull) return ld_stream(&p[q0 + ql]);
+        if (ql * 2 < nw) {
+            const uint64_t v = ((const uint64_t*)p)[2 * (q0 + ql)];
+            return make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
+        }
+        return make_uint4(0u, 0u, 0u, 0u);
+    };
+    uint4 x[U], y[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t ql = j * T + threadIdx.x;
+        x[j] = load(a, ql);
+        if constexpr (PAIR) y[j] = load(b, ql);
+    }
+    if constexpr (!PAIR && !POW2) __syncthreads();   // sref
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t ql = j * T + threadIdx.x;
+        const uint32_t wl = 2 * ql;                 // block-local index of the lane's first word
+        uint64_t r_lo, r_hi;
+        if constexpr (PAIR) {
+            r_lo = ((uint64_t)y[j].y << 32) | y[j].x;
+            r_hi = ((uint64_t)y[j].w << 32) | y[j].z;
+        } else if (POW2) {
+            r_lo = pref_lo;
+            r_hi = pref_hi;
+        }
+        if constexpr (POW2) {
+            const uint32_t d_lo = ham64((((uint64_t)x[j].y << 32) | x[j].x) ^ r_lo);
+            const uint32_t d_hi = ham64((((uint64_t)x[j].w << 32) | x[j].z) ^ r_hi);
+            if (W == 1) {
+                const uint32_t r = 2 * ql;          // reads r, r + 1 of the block (nr is even or the tail)
+                if (r + 1 < nr) *(uint2*)&out[r0 + r] = make_uint2(d_lo, d_hi);
+                else if (r < nr) out[r0 + r] = d_lo;
+            } else {
+                const uint32_t G = W / 2;           // lanes per read (a power of two, <= 16)
+                uint32_t s = d_lo + d_hi;
+                for (uint32_t m = 1; m < G; m <<= 1) s += __shfl_xor(s, m);
+                const uint32_t r = ql / G;
+                if ((ql & (G - 1u)) == 0 && r < nr) out[r0 + r] = s;
+            }
+        } else {
+            // word -> read: floor((wl + 0.5) / W) in f32, exact for wl < 4096 and W <= 64 (the same
+            // rule k_encode_ham_dense uses); the pair's two words may belong to two reads
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t w = wl + h;
+                const uint32_t rl = (uint32_t)__fmul_rn(__fadd_rn((float)w, 0.5f), inv_w);
+                const uint32_t k = w - rl * W;
+                const uint64_t v = h ? (((uint64_t)x[j].w << 32) | x[j].z) : (((uint64_t)x[j].y << 32) | x[j].x);
+                uint64_t rv;
+                if constexpr (PAIR) rv = h ? r_hi : r_lo;
+                else rv = sref[k];
+                part[w] = (uint8_t)(w < nw ? ham64(v ^ rv) : 0u);
+            }
+        }
+    }
+    if constexpr (!POW2) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nr; i += T) {
+            uint32_t sum = 0;
+            for (uint32_t k = 0; k < W; ++k) sum += part[i * W + k];
+            out[r0 + i] = sum;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Slice / subscript on packed words (short_seq.pyx:78-238: _slice -> _slice_to_ShortSeq64 /
 // _shift_copy_trim; _subscript = a 1-nt slice): output word i of read r is the 64-bit funnel shift
@@ -444,6 +597,27 @@ constexpr bool kEncXcd = false, kEncNtSt = true;
 constexpr int kHamT = 192, kHamU = 4;        // fused encode + hamming (dense, LDS reduction): 768-chunk
                                              // blocks, 128 whole 96-nt reads (tools/tune_stream.hip)
 constexpr int kDecT = 256, kDecU = 2;        // decode
+constexpr int kHamDT = 256, kHamDU = 4;      // dense hamming on packed rows: 2048 words per block
+
+template <int T, int U>
+void launch_ham_dense_k(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t W, uint32_t* out,
+                               bool pair, hipStream_t s) {
+    static_assert(2 * T * U <= 4096, "block-local word index must stay < 4096 (f32 read index)");
+    const uint32_t rpb = ((2u * T * U) / W) & ~1u;
+    const unsigned grid = grid_for(n, rpb);
+    const bool pow2 = (W & (W - 1u)) == 0;
+    const float inv_w = 1.0f / (float)W;
+    const uint4 *a4 = (const uint4*)a, *b4 = (const uint4*)b;
+    if (pair && pow2)
+        hipLaunchKernelGGL((k_ham_dense<true, true, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
+    else if (pair)
+        hipLaunchKernelGGL((k_ham_dense<true, false, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
+    else if (pow2)
+        hipLaunchKernelGGL((k_ham_dense<false, true, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
+    else
+        hipLaunchKernelGGL((k_ham_dense<false, false, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
+}
+
 constexpr bool kDecNtLd = false, kDecNtSt = false;
 
 void launch_encode_fast(const G16Args& a, bool dense, bool ham, uint32_t L, hipStream_t s) {
@@ -595,6 +769,20 @@ static int launch_ham(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t
     if (wpr < W || wpr > 32) return ss_fail(SS_EARG, "bad wpr");
     if (n == 0) return SS_OK;
     if (!a || !b || !out) return ss_fail(SS_EARG, "null buffer");
+    const bool aligned = (((uintptr_t)a | (uintptr_t)(pair ? b : a)) & 15u) == 0 && (((uintptr_t)out) & 7u) == 0;
+    if (wpr == W && aligned && W <= 32) {   // dense rows: the streaming kernel (W <= 32 keeps wl < 4096 exact)
+        hipStream_t s = (hipStream_t)stream;
+        if (W == 3) {   // 96 nt (C3): lane triples, no LDS (0.63 -> 0.68 of HBM peak, same-box A/B)
+            constexpr int T = 256, U = 4;
+            const unsigned grid = grid_for(n, (uint64_t)42 * (T / 64) * U);
+            const uint4 *a4 = (const uint4*)a, *b4 = (const uint4*)b;
+            if (pair) hipLaunchKernelGGL((k_ham_dense3<true, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
+            else hipLaunchKernelGGL((k_ham_dense3<false, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
+            return ss_check(hipGetLastError(), "k_ham_dense3");
+        }
+        launch_ham_dense_k<kHamDT, kHamDU>(a, b, n, W, out, pair, s);
+        return ss_check(hipGetLastError(), "k_ham_dense");
+    }
     const uint32_t logG = log2_ceil(W);
     const unsigned grid = grid_for(n << logG, kThreads);
     if (pair)

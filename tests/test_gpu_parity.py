@@ -180,6 +180,32 @@ def test_hamming(gpu, oracle):
         assert np.array_equal(dist2.cpu().numpy().astype(np.uint32), ref), L
 
 
+@pytest.mark.parametrize("L", [1, 31, 32, 33, 64, 96, 100, 128, 200, 256, 500, 512, 1000, 1024])
+def test_hamming_dense_multiblock(gpu, oracle, L):
+    """k_ham_dense (packed rows, wpr == words): batches spanning several blocks, odd word counts
+    ending on a half pair, and row views off the 16-B grid (those take k_ham_group)."""
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(1000 + L)
+    for n in (1, 3, 4097, 9001):
+        a = _rand_reads(rng, n, L, p_alias=0.01)
+        b = a.copy()
+        flip = rng.random(n * L) < 0.2
+        b[flip] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, flip.sum())]
+        wa = B.encode(torch.from_numpy(a).to(gpu).view(n, L), L)
+        wb = B.encode(torch.from_numpy(b).to(gpu).view(n, L), L)
+        ua, ub = _u64(wa), _u64(wb)
+        pair = B.hamming_pair(wa, wb, L).cpu().numpy().astype(np.uint32)
+        assert np.array_equal(pair, oracle.hamming_pair_batch(ua, ub, n, L)), (L, n)
+        k = n // 2
+        ref = B.hamming_ref(wa, L, wb[k]).cpu().numpy().astype(np.uint32)
+        assert np.array_equal(ref, oracle.hamming_ref_batch(ua, n, L, ub[k])), (L, n)
+        if n > 1:
+            p1 = B.hamming_pair(wa[1:], wb[1:], L).cpu().numpy().astype(np.uint32)
+            assert np.array_equal(p1, pair[1:]), (L, n)
+            r1 = B.hamming_ref(wa[1:], L, wb[k]).cpu().numpy().astype(np.uint32)
+            assert np.array_equal(r1, ref[1:]), (L, n)
+
+
 def test_synth_matches_oracle_generator(gpu, oracle):
     import shortseq_amd.batch as B
     for L in [1, 16, 31, 32, 33, 96, 100, 512, 1024]:
