@@ -328,6 +328,20 @@ __global__ __launch_bounds__(kThreads) void k_ham_group(const uint64_t* __restri
     if (r < n && k == 0) out[r] = part;
 }
 
+#ifndef SS_HAM_NT
+#define SS_HAM_NT 1   // same-box A/B, C3' 32 / 96 nt: 0.73 -> 0.78, 0.69 -> 0.72 of peak (512 nt unchanged)
+#endif
+// distance stores of the dense hamming kernels (streamed once: nontemporal)
+__device__ __forceinline__ void ham_store(uint32_t* p, uint32_t v) {
+    if (SS_HAM_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void ham_store2(uint32_t* p, uint32_t lo, uint32_t hi) {
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    if (SS_HAM_NT) __builtin_nontemporal_store(v, (uint64_t*)p);
+    else *(uint64_t*)p = v;
+}
+
 // Dense hamming for W = 3 (96-nt reads) without LDS: every wave streams chunks of 63 consecutive
 // dwordx4 (lane 63 idles, 1.6 % of the lanes), so a chunk is 21 lane triples = 42 whole reads and a
 // triple (p = 0, 1, 2) holds words 6m .. 6m+5: read 2m = p0.lo + p0.hi + p1.lo, read 2m+1 = p1.hi +
@@ -378,8 +392,8 @@ __global__ __launch_bounds__(T) void k_ham_dense3(const uint4* __restrict__ a, c
         const uint32_t from_prev = __shfl(dh, (int)(lane == 0 ? 0u : lane - 1u));   // p2 <- p1.hi
         const uint32_t rb = (j * NWV + wv) * RPC + 2u * m;                   // block-local read of p0
         if (lane < QPC) {
-            if (p == 0 && rb < nr) out[r0 + rb] = dl + dh + from_next;
-            if (p == 2 && rb + 1 < nr) out[r0 + rb + 1] = from_prev + dl + dh;
+            if (p == 0 && rb < nr) ham_store(&out[r0 + rb], dl + dh + from_next);
+            if (p == 2 && rb + 1 < nr) ham_store(&out[r0 + rb + 1], from_prev + dl + dh);
         }
     }
 }
@@ -445,14 +459,14 @@ __global__ __launch_bounds__(T) void k_ham_dense(const uint4* __restrict__ a, co
             const uint32_t d_hi = ham64((((uint64_t)x[j].w << 32) | x[j].z) ^ r_hi);
             if (W == 1) {
                 const uint32_t r = 2 * ql;          // reads r, r + 1 of the block (nr is even or the tail)
-                if (r + 1 < nr) *(uint2*)&out[r0 + r] = make_uint2(d_lo, d_hi);
-                else if (r < nr) out[r0 + r] = d_lo;
+                if (r + 1 < nr) ham_store2(&out[r0 + r], d_lo, d_hi);
+                else if (r < nr) ham_store(&out[r0 + r], d_lo);
             } else {
                 const uint32_t G = W / 2;           // lanes per read (a power of two, <= 16)
                 uint32_t s = d_lo + d_hi;
                 for (uint32_t m = 1; m < G; m <<= 1) s += __shfl_xor(s, m);
                 const uint32_t r = ql / G;
-                if ((ql & (G - 1u)) == 0 && r < nr) out[r0 + r] = s;
+                if ((ql & (G - 1u)) == 0 && r < nr) ham_store(&out[r0 + r], s);
             }
         } else {
             // word -> read: floor((wl + 0.5) / W) in f32, exact for wl < 4096 and W <= 64 (the same
@@ -475,7 +489,7 @@ __global__ __launch_bounds__(T) void k_ham_dense(const uint4* __restrict__ a, co
         for (uint32_t i = threadIdx.x; i < nr; i += T) {
             uint32_t sum = 0;
             for (uint32_t k = 0; k < W; ++k) sum += part[i * W + k];
-            out[r0 + i] = sum;
+            ham_store(&out[r0 + i], sum);
         }
     }
 }
