@@ -733,29 +733,36 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
 // Optimistic coarse partition (the C5 path for L 16 / 32, > 128 regions).  The exact passes above
 // need a histogram of the whole batch before the coarse scatter (P1 writes every key, P3 reads
 // them back).  Here the encode pass scatters directly: each 4096-read tile is ranked by coarse
-// bin in LDS and reserves its runs with ONE atomicAdd per (tile, bin) on the bin's fill counter;
-// bin b owns slots [b * cap1, (b + 1) * cap1) of the coarse arrays (cap1 = 1.25 x the mean bin
-// load + 8192).  Order inside a bin is arbitrary, which the aggregation does not care about
-// (count = sum, first = min of the carried read index).  A bin that would overflow raises the
-// overflow word: every later pass then idles and k_count_g16 inserts the batch directly
-// (adversarial inputs that pile one bin, e.g. a few keys repeated, still count exactly).
-// Fine pass: 8 blocks per coarse bin, each over 1/8 of its filled slots; all of a block's keys
-// lie in the bin's 2^(rbits - 7) regions, so the histogram and the LDS staging use that window.
+// bin in LDS and reserves its runs with ONE atomicAdd per (tile, bin) on a fill counter.  Every bin
+// is split into kFinePerBin sub-bins, one per fine-pass block; coarse block k appends to sub-bin
+// k % kFinePerBin, so each counter takes 1/8 of the bin's atomics (the atomics on one address
+// serialize: 128 shared counters cost ~0.57 ms of the pass at 125M reads, 8 x 128 cost the pass
+// 1.54 -> 1.28 ms, profiles/r1/r1k/c5_coarse_probes.txt), while the 64 blocks that share a
+// sub-bin still fill its lines back to back.  Sub-bin f = (bin, sub) owns slots [f * cap1,
+// (f + 1) * cap1) of the coarse arrays (cap1 = 1.25 x the mean sub-bin load + 1024).  Order inside
+// a sub-bin is arbitrary, which the aggregation does not care about (count = sum, first = min of
+// the carried read index).  A sub-bin that would overflow raises the overflow word: every later
+// pass then idles and k_count_g16 inserts the batch directly (adversarial inputs that pile one
+// bin, e.g. a few keys repeated, still count exactly).
+// Fine pass: block f takes sub-bin f whole; all of its keys lie in the bin's 2^(rbits - 7)
+// regions, so the histogram and the LDS staging use that window.
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kCB = 1u << kCoarseBits;          // 128 coarse bins
-// The 128 bin fill counters take one atomicAdd per (4096-read tile, bin), ~3.9M device-scope atomics
-// per 125M reads.  kFillStride spaces them (u32 units); 64 and 1024 measured no different from 1
-// (tools/tune_counter.hip, scripts/ab_counter.sh), so they stay packed.
+// The fill counters take one atomicAdd per (4096-read tile, bin), ~3.9M device-scope atomics per
+// 125M reads.  kFillStride spaces them (u32 units); 64 and 1024 (128 counters) and 32 (8 x 128)
+// measured no different from 1 (tools/tune_counter.hip, scripts/ab_counter.sh): they stay packed.
 #ifndef SS_FILL_STRIDE
 #define SS_FILL_STRIDE 1
 #endif
 constexpr uint32_t kFillStride = SS_FILL_STRIDE;
-constexpr uint32_t kFillWords = (kCB + 1) * kFillStride;   // counters + the overflow flag
-__host__ __device__ __forceinline__ uint32_t fill_at(uint32_t b) { return b * kFillStride; }
 #ifndef SS_FINE_PER_BIN
 #define SS_FINE_PER_BIN 8
 #endif
-constexpr uint32_t kFinePerBin = SS_FINE_PER_BIN;    // fine-pass blocks per coarse bin
+constexpr uint32_t kFinePerBin = SS_FINE_PER_BIN;    // fine-pass blocks per coarse bin = sub-bins per bin
+constexpr uint32_t kNFill = kCB * kFinePerBin;       // sub-bin fill counters
+constexpr uint32_t kOvf = kNFill;                    // the overflow flag's index
+constexpr uint32_t kFillWords = (kNFill + 1) * kFillStride;   // counters + the overflow flag
+__host__ __device__ __forceinline__ uint32_t fill_at(uint32_t b) { return b * kFillStride; }
 #ifndef SS_PF_RPL
 #define SS_PF_RPL 16
 #endif
@@ -774,9 +781,10 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
     __shared__ uint64_t skey[TILE];
     __shared__ uint32_t sidx[TILE];
     __shared__ uint8_t sbin[TILE];
-    uint32_t* ovf = fill + fill_at(kCB);
+    uint32_t* ovf = fill + fill_at(kOvf);
     const uint32_t shift = w.rbits - kCoarseBits;
     const uint64_t tiles = (n + TILE - 1) / TILE;
+    const uint32_t sub = blockIdx.x % kFinePerBin;   // this block's sub-bin of every bin
     uint4 nx[RPL][2];
     auto load_tile = [&](uint64_t tile) {
 #pragma unroll
@@ -838,8 +846,8 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             const uint32_t excl = incl - c0 - c1;
             lstart[b0] = excl;
             lstart[b0 + 1] = excl + c0;
-            gbase[b0] = c0 ? atomicAdd(&fill[fill_at(b0)], c0) : 0u;
-            gbase[b0 + 1] = c1 ? atomicAdd(&fill[fill_at(b0 + 1)], c1) : 0u;
+            gbase[b0] = c0 ? atomicAdd(&fill[fill_at(b0 * kFinePerBin + sub)], c0) : 0u;
+            gbase[b0 + 1] = c1 ? atomicAdd(&fill[fill_at((b0 + 1) * kFinePerBin + sub)], c1) : 0u;
             lcount[b0] = 0;
             lcount[b0 + 1] = 0;
         }
@@ -859,8 +867,9 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             const uint32_t b = sbin[i];
             const uint64_t pos = (uint64_t)gbase[b] + (i - lstart[b]);
             if (pos < cap1) {
-                w.akey[b * cap1 + pos] = skey[i];
-                w.aidx[b * cap1 + pos] = sidx[i];
+                const uint64_t at = (uint64_t)(b * kFinePerBin + sub) * cap1 + pos;
+                w.akey[at] = skey[i];
+                w.aidx[at] = sidx[i];
             } else {
                 *ovf = 1u;
             }
@@ -868,27 +877,26 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
     }
 }
 
+// fine block fb = sub-bin fb (bin fb / kFinePerBin): slots [fb * cap1, fb * cap1 + fill)
 __device__ __forceinline__ void fine_range(uint32_t fb, const uint32_t* fill, uint64_t cap1, uint32_t& bin,
                                            uint64_t& lo, uint64_t& hi) {
     bin = fb / kFinePerBin;
-    const uint32_t sub = fb % kFinePerBin;
-    const uint64_t f = min((uint64_t)fill[fill_at(bin)], cap1);
-    lo = sub * f / kFinePerBin;
-    hi = (sub + 1) * f / kFinePerBin;
+    lo = 0;
+    hi = min((uint64_t)fill[fill_at(fb)], cap1);
 }
 
 // fine histogram: block fb counts the regions of its slice of coarse bin fb / 8 -> hist[fb][rpb]
 template <int T>
 __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
     __shared__ uint32_t h[kMaxLocalBins];
-    if (fill[fill_at(kCB)]) return;
+    if (fill[fill_at(kOvf)]) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits);
     uint32_t bin;
     uint64_t lo, hi;
     fine_range(blockIdx.x, fill, cap1, bin, lo, hi);
     for (uint32_t i = threadIdx.x; i < rpb; i += T) h[i] = 0;
     __syncthreads();
-    const uint64_t* src = w.akey + bin * cap1;
+    const uint64_t* src = w.akey + (uint64_t)blockIdx.x * cap1;
     const uint32_t r0 = bin * rpb;
     for (uint64_t e = lo + threadIdx.x; e < hi; e += T) atomicAdd(&h[region_of(t, src[e]) - r0], 1u);
     __syncthreads();
@@ -898,7 +906,7 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
 // region totals over the bin's 8 fine blocks (thread per region) -> w.tot; then k_pc_scan (one
 // block) -> rstart; then k_pf_offsets (thread per region) -> each fine block's write cursors
 __global__ __launch_bounds__(256) void k_pf_tot(PartWs w, const uint32_t* fill) {
-    if (fill[fill_at(kCB)]) return;
+    if (fill[fill_at(kOvf)]) return;
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= w.R) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
@@ -909,7 +917,7 @@ __global__ __launch_bounds__(256) void k_pf_tot(PartWs w, const uint32_t* fill) 
 }
 
 __global__ __launch_bounds__(256) void k_pf_offsets(PartWs w, const uint32_t* fill) {
-    if (fill[fill_at(kCB)]) return;
+    if (fill[fill_at(kOvf)]) return;
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= w.R) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
@@ -936,14 +944,14 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
     __shared__ uint64_t skey[kTile];
     __shared__ uint32_t sidx[kTile];
     __shared__ uint32_t wsum[17];
-    if (fill[fill_at(kCB)]) return;
+    if (fill[fill_at(kOvf)]) return;
     const uint32_t nb = 1u << (w.rbits - kCoarseBits);
     uint32_t bin;
     uint64_t lo, hi;
     fine_range(blockIdx.x, fill, cap1, bin, lo, hi);
     const uint32_t r0 = bin * nb;
-    const uint64_t* src = w.akey + bin * cap1;
-    const uint32_t* src_idx = w.aidx + bin * cap1;
+    const uint64_t* src = w.akey + (uint64_t)blockIdx.x * cap1;
+    const uint32_t* src_idx = w.aidx + (uint64_t)blockIdx.x * cap1;
     for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] = w.hist[(uint64_t)blockIdx.x * nb + i];
     __syncthreads();
     uint64_t nkey[kTile / T];
@@ -1698,10 +1706,10 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     if (max_reads >= (1ull << 32)) return ss_fail(SS_EARG, "max_reads must be < 2^32 per insert");
     if (max_reads <= c->ws_reads) return SS_OK;
     ss_counter_release(c);
-    // coarse arrays: room for the exact passes (max_reads) and for the optimistic partition's 128
-    // bins of cap1 = 1.25 x the mean bin load + 8192 slots
-    const uint64_t cap1 = (max_reads + max_reads / 4 + kCB - 1) / kCB + 8192;
-    const uint64_t acap = kCB * cap1 > max_reads ? kCB * cap1 : max_reads;
+    // coarse arrays: room for the exact passes (max_reads) and for the optimistic partition's
+    // 128 x 8 sub-bins of cap1 = 1.25 x the mean sub-bin load + 1024 slots
+    const uint64_t cap1 = (max_reads + max_reads / 4 + kNFill - 1) / kNFill + 8192 / kFinePerBin;
+    const uint64_t acap = kNFill * cap1 > max_reads ? kNFill * cap1 : max_reads;
     hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
@@ -1849,7 +1857,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
                                (unsigned long long*)d_first_bad);
             const unsigned fine_blocks = kCB * kFinePerBin;
-            const uint32_t* ovf = (const uint32_t*)(c->ws_fill + fill_at(kCB));
+            const uint32_t* ovf = (const uint32_t*)(c->ws_fill + fill_at(kOvf));
             hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill);
             const unsigned rg = (w.R + 255) / 256;
@@ -2036,7 +2044,7 @@ int ss_counter_pack_ranges(ss_counter* c, uint32_t n_parts, int32_t skip_part, u
     const uint32_t R = (uint32_t)c->occ_R;
     if (c->occ_src != 1)
         hipLaunchKernelGGL(k_region_occ, dim3(R), dim3(kPackT), 0, s, t,
-                           c->occ_src == 2 ? (const uint32_t*)(c->ws_fill + fill_at(kCB)) : (const uint32_t*)nullptr);
+                           c->occ_src == 2 ? (const uint32_t*)(c->ws_fill + fill_at(kOvf)) : (const uint32_t*)nullptr);
     hipLaunchKernelGGL(k_region_scan, dim3(1), dim3(1024), 0, s, t, R, n_parts, skip_part, c->roff,
                        (unsigned long long*)d_part_counts);
     hipLaunchKernelGGL(k_region_pack, dim3(R), dim3(kPackT), 0, s, t, R, n_parts, skip_part,
