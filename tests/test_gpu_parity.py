@@ -206,6 +206,29 @@ def test_hamming_dense_multiblock(gpu, oracle, L):
             assert np.array_equal(r1, ref[1:]), (L, n)
 
 
+def test_hamming_out_alignment(gpu, oracle):
+    """Distance arrays off the 8-B grid (and reference / row pointers off 16 B) take the lane-group
+    kernel; the results are the same as the streaming kernels'."""
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import lib
+    rng = np.random.default_rng(77)
+    for L in (32, 96, 512):
+        n = 3001
+        a = _rand_reads(rng, n, L)
+        wa = B.encode(torch.from_numpy(a).to(gpu).view(n, L), L)
+        wpr = wa.shape[1]
+        ref = wa[n // 3].clone()
+        want = oracle.hamming_ref_batch(_u64(wa), n, L, _u64(ref.view(1, -1))[0])
+        buf = torch.zeros(n + 1, dtype=torch.int32, device=gpu)
+        out = buf[1:]                                   # 4-B aligned, not 8-B
+        s = torch.cuda.current_stream(gpu).cuda_stream
+        assert lib().ss_hamming_ref(wa.data_ptr(), n, L, wpr, ref.data_ptr(), out.data_ptr(), s) == 0
+        assert np.array_equal(out.cpu().numpy().astype(np.uint32), want), L
+        pair = torch.zeros(n + 1, dtype=torch.int32, device=gpu)[1:]
+        assert lib().ss_hamming_pair(wa.data_ptr(), wa.data_ptr(), n, L, wpr, pair.data_ptr(), s) == 0
+        assert int(pair.abs().sum()) == 0, L
+
+
 def test_synth_matches_oracle_generator(gpu, oracle):
     import shortseq_amd.batch as B
     for L in [1, 16, 31, 32, 33, 96, 100, 512, 1024]:
