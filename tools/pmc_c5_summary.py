@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Summarise scripts/pmc_c5.sh (rocprofv3 --pmc passes over tools/c5_only.py) per C5 kernel: HBM read
+= FETCH_SIZE KB x 2 (gfx950 wide-read correction) x 1024, write = WRITE_SIZE KB x 1024, and the 8
+SQ counters; the median over that kernel's launches.
+
+usage: pmc_c5_summary.py <gpurun_out/pmc_c5> > profiles/r1/pmc_c5_<tag>.txt
+"""
+import csv
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+KERNELS = ["k_pf_coarse", "k_pf_count", "k_pf_scatter", "k_pc_aggregate_slice"]
+
+
+def per_dispatch(path):
+    """{kernel: {counter: [value per dispatch]}} for the C5 kernels."""
+    acc = defaultdict(float)
+    names = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            k = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
+            if k is None:
+                continue
+            key = (r["Dispatch_Id"], r["Counter_Name"])
+            acc[key] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = (k, r["Kernel_Name"])
+    out = defaultdict(lambda: defaultdict(list))
+    for (d, c), v in acc.items():
+        out[names[d][0]][c].append(v)
+    full = {k: n for (k, n) in names.values()}
+    return out, full
+
+
+def main():
+    root = sys.argv[1]
+    fetch, full = per_dispatch(os.path.join(root, "fetch", "run_counter_collection.csv"))
+    write, _ = per_dispatch(os.path.join(root, "write", "run_counter_collection.csv"))
+    sq, _ = per_dispatch(os.path.join(root, "sq", "run_counter_collection.csv"))
+    print("C5 counter kernels (tools/c5_only.py: 125M x 32-nt reads, pool 2^24, lazy reset), rocprofv3 --pmc,")
+    print("three separate passes (FETCH_SIZE | WRITE_SIZE | 8 SQ counters), median over launches.")
+    print("HBM read = FETCH_SIZE KB x2 (gfx950 wide-read correction) x1024; write = WRITE_SIZE KB x1024.")
+    print("Algorithmic per launch: coarse 4.0 GB in / 1.5 GB out; count 1.0 GB in; scatter 1.5 / 1.5 GB;")
+    print("aggregate 1.5 GB in + whole 1-GB table written (fresh slices).\n")
+    for k in KERNELS:
+        if k not in fetch:
+            continue
+        rd = statistics.median(fetch[k]["FETCH_SIZE"]) * 2 * 1024 / 1e9
+        wr = statistics.median(write[k]["WRITE_SIZE"]) * 1024 / 1e9 if k in write else float("nan")
+        name = full[k].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+        print(f"{name}: HBM read {rd:.3f} GB, write {wr:.3f} GB")
+        for c in sorted(sq.get(k, {})):
+            print(f"   {c:24s} {statistics.median(sq[k][c]):.4g}")
+        print()
+
+
+if __name__ == "__main__":
+    main()
