@@ -255,13 +255,16 @@ def bench_roundtrip(B, lib, dev, rank, world, n, L, steps, warmup, seed=3):
     return el, t_enc.mean_ms(), t_dec.mean_ms(), tr.region_ms / steps
 
 
-def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool_seed=77):
-    """C5: per rank n reads drawn from a pool of U 32-mers (shard = contiguous read-index range);
-    shortseq_amd.dist.ShardedCounter: local HBM table -> partition by owner -> RCCL all-to-all of
-    (key, count, first) -> owners merge."""
+def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool_seed=77, zipf=None):
+    """C5: per rank n reads drawn from a pool of U 32-mers (uniform, or Zipf(zipf) when given; shard =
+    contiguous read-index range); shortseq_amd.dist.ShardedCounter: local HBM table -> partition by
+    owner -> RCCL all-to-all of (key, count, first) -> owners merge."""
     from shortseq_amd.dist import ShardedCounter
     i0 = rank * n
-    ascii = B.synth_pool_reads(n, L, seed, pool_seed, U, i0=i0, device=dev)
+    if zipf:
+        ascii = B.synth_zipf_reads(n, L, seed, pool_seed, B.zipf_cdf(U, zipf), i0=i0, device=dev)
+    else:
+        ascii = B.synth_pool_reads(n, L, seed, pool_seed, U, i0=i0, device=dev)
     cap = 1 << max(10, int(np.ceil(np.log2(2 * U))))
     sc = ShardedCounter(cap, device=dev)
 
@@ -658,6 +661,15 @@ def main():
             "merge": (f"all_to_all_single of (key, count, first) by owner over {dist.get_backend()}"
                       f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
                      if world > 1 else "none (1 GPU)"}
+        # SURVEY §8(d) C5 variants: the smaller pool and Zipf s = 1.1 skew (same shard size)
+        for name, U_, zs in (("C5_counter_32_U20", 1 << 20, None), ("C5_counter_32_zipf1.1_U24", 1 << 24, 1.1),
+                             ("C5_counter_32_zipf1.1_U20", 1 << 20, 1.1)):
+            log(f"C5 counter {n5} x 32 per GPU, pool {U_}, {'zipf ' + str(zs) if zs else 'uniform'}")
+            el_, d_, u_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
+            extra[name] = {"reads_per_s": n5 * world / (el_ / s5), "ms_per_step": el_ / s5 * 1e3,
+                           "device_ms_per_step": d_, "reads_per_gpu": n5, "pool": U_, "zipf_s": zs, "unique": u_,
+                           "vs_uniform_U24": d_ / d5,
+                           "floor_frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS}
         if rank == 0 or world == 1:
             # rank-local extras (no collective): an error is recorded in its entry instead of costing
             # the run its JSON line; parity failures (SystemExit) still end the run

@@ -149,6 +149,8 @@ int ss_hamming_all_pairs(const uint64_t* d_words, uint64_t n, uint32_t L, uint32
  * handle; all keys of one handle share one length L <= 1024 (the length is part of the key).
  * L <= 32: the slot key is the packed word.  L > 32: W = ceil(L/32) words per key, kept beside the
  * slots; the slot holds a 64-bit fingerprint of the words and equality is decided on the words.
+ * A slot is 16 B (key u64, count u32, first index u32): global read indices of one handle stay below
+ * 2^32 - 1 (inserts past that return SS_EARG) and a key counts at most 2^32 - 1 copies.
  * ---------------------------------------------------------------------------------------------- */
 typedef struct ss_counter ss_counter;
 
@@ -157,12 +159,14 @@ int ss_counter_destroy(ss_counter* c);
 int ss_counter_reset(ss_counter* c, void* stream);
 uint64_t ss_counter_capacity(const ss_counter* c);
 
-/* Reserve workspace (20 B per read + a small per-region table) so inserts of up to max_reads
+/* Reserve workspace (~72 B per read + a small per-region table) so inserts of up to max_reads
  * reads take the partitioned path: reads are bucketed by table region and each region is
  * aggregated by one workgroup in LDS (no per-read global atomics).  Host call (allocates).  L 16/32
- * with 16-B aligned rows encode inside the first partition pass; any other L <= 32 / layout is
- * packed into the workspace first.  Inserts larger than the reservation use the direct
- * atomic-insert kernels.  Requires capacity <= 2^26 (16384 regions).  max_reads < 2^32. */
+ * with 16-B aligned rows encode inside the first partition pass (a key repeated within a 4096-read
+ * tile leaves it as one weighted record when its bin is heavy, so skewed inputs keep the partition
+ * balanced; records finding their bucket full are counted by a direct insert afterwards); any other
+ * L <= 32 / layout is packed into the workspace first.  Inserts larger than the reservation use the
+ * direct atomic-insert kernels.  Requires capacity <= 2^26 (32768 regions).  max_reads < 2^31. */
 int ss_counter_reserve(ss_counter* c, uint64_t max_reads);
 uint64_t ss_counter_reserved(const ss_counter* c);
 int ss_counter_release(ss_counter* c);       /* free the workspace (inserts take the direct path) */
@@ -185,7 +189,8 @@ int ss_counter_set_length(ss_counter* c, uint32_t L);
 int ss_counter_length(const ss_counter* c);
 
 /* Copy the handle's overflow word to *d_flag (device u64): bit 0 = table full during an insert or
- * merge, bit 1 = an extract found more entries than `cap`.  Nonzero means the result is invalid. */
+ * merge, bit 1 = an extract found more entries than `cap`, bit 2 = a merged count did not fit 32
+ * bits, bit 3 = a read index did not fit 32 bits.  Nonzero means the result is invalid. */
 int ss_counter_overflow(ss_counter* c, uint64_t* d_flag, void* stream);
 
 /* Number of occupied slots -> *d_size (device u64). */
@@ -295,10 +300,16 @@ int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):
  * read i word w: r = splitmix64(seed + i*W + w) masked to its nts, byte j = "ACTG"[(r >> 2j) & 3].
  * Pool variant: read i is pool item splitmix64(pool_seed ^ (i * 0xD1B54A32D192ED03)) % U.
+ * Zipf variant (SURVEY §8(d) C5 skew): read i is pool item rank = #{k : d_cdf[k] <= u63}, u63 =
+ * splitmix64(pool_seed ^ (i * 0xD1B54A32D192ED03)) >> 1, for a device table d_cdf[U] of the Zipf
+ * CDF scaled to 2^63 (d_cdf[k] = floor(2^63 * P(rank <= k)), d_cdf[U-1] = 2^63; built on the host by
+ * shortseq_amd.batch.zipf_cdf).  Item 0 is the most frequent.
  * ---------------------------------------------------------------------------------------------- */
 int ss_synth_reads(uint8_t* d_ascii, uint64_t seed, uint64_t i0, uint64_t n, uint32_t L,
                    uint64_t stride, void* stream);
 int ss_synth_pool_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, uint64_t U,
+                        uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream);
+int ss_synth_zipf_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, const uint64_t* d_cdf, uint64_t U,
                         uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream);
 
 /* ------------------------------------------------------------------------------------------------

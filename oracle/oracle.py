@@ -59,6 +59,9 @@ def lib():
         L.ora_pool_index.argtypes = [U64, U64, U64]
         L.ora_pool_index.restype = U64
         L.ora_gen_pool_reads.argtypes = [U64, U64, U64, U64, U64, U32, U64, P]
+        L.ora_zipf_index.argtypes = [U64, U64, P, U64]
+        L.ora_zipf_index.restype = U64
+        L.ora_gen_zipf_reads.argtypes = [U64, U64, P, U64, U64, U64, U32, U64, P]
         L.ora_count.argtypes = [P, P, P, U64, P, P, P, P, C.POINTER(OraErr)]
         L.ora_count.restype = I64
         L.ora_fastq_index.argtypes = [P, U64, P, P, U64]
@@ -163,6 +166,69 @@ def gen_pool_reads(seed: int, pool_seed: int, U: int, i0: int, n: int, L: int) -
     out = np.zeros(max(1, n * L), dtype=np.uint8)
     lib().ora_gen_pool_reads(seed, pool_seed, U, i0, n, L, L, _p(out))
     return out[: n * L]
+
+
+def gen_zipf_reads(seed: int, pool_seed: int, cdf: np.ndarray, i0: int, n: int, L: int) -> np.ndarray:
+    out = np.zeros(max(1, n * L), dtype=np.uint8)
+    c = np.ascontiguousarray(cdf, dtype=np.uint64)
+    lib().ora_gen_zipf_reads(seed, pool_seed, _p(c), len(c), i0, n, L, L, _p(out))
+    return out[: n * L]
+
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64_np(x: np.ndarray) -> np.ndarray:
+    """Vectorised ora_splitmix64 (uint64 wrap-around arithmetic)."""
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def pool_ids(pool_seed: int, i0: int, n: int, U: int, cdf: np.ndarray | None = None) -> np.ndarray:
+    """Pool item of reads i0 .. i0+n-1 (ora_pool_index, or ora_zipf_index when cdf is given), vectorised."""
+    i = np.arange(i0, i0 + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        r = splitmix64_np(np.uint64(pool_seed) ^ (i * np.uint64(0xD1B54A32D192ED03)))
+    if cdf is None:
+        return r % np.uint64(U)
+    ids = np.searchsorted(np.asarray(cdf, dtype=np.uint64), r >> np.uint64(1), side="right").astype(np.uint64)
+    return np.minimum(ids, np.uint64(U - 1))
+
+
+def pool_counter_table(seed: int, pool_seed: int, U: int, n: int, L: int = 32, i0: int = 0,
+                       cdf: np.ndarray | None = None, chunk: int = 1 << 23):
+    """The counter result of n pool-drawn L <= 32 reads, derived from the generator alone: keys = the
+    generator word of each drawn pool item, counts = bincount of the draw indices, first = global
+    index of the first draw.  Returns (keys, counts, first) uint64 arrays sorted by key."""
+    assert L <= 32
+    counts = np.zeros(U, dtype=np.uint64)
+    first = np.full(U, np.iinfo(np.uint64).max, dtype=np.uint64)
+    for s0 in range(0, n, chunk):
+        m = min(chunk, n - s0)
+        ids = pool_ids(pool_seed, i0 + s0, m, U, cdf)
+        counts += np.bincount(ids.astype(np.int64), minlength=U).astype(np.uint64)
+        u, pos = np.unique(ids, return_index=True)
+        new = first[u] == np.iinfo(np.uint64).max
+        first[u[new]] = np.uint64(i0 + s0) + pos[new].astype(np.uint64)
+    used = np.nonzero(counts)[0].astype(np.uint64)
+    with np.errstate(over="ignore"):
+        keys = splitmix64_np(np.uint64(seed) + used)
+    if L < 32:
+        keys &= np.uint64((1 << (2 * L)) - 1)
+    o = np.argsort(keys, kind="stable")
+    return keys[o], counts[used.astype(np.int64)][o], first[used.astype(np.int64)][o]
+
+
+def table_digest(keys: np.ndarray, counts: np.ndarray, first: np.ndarray) -> str:
+    """SHA-256 of the (key, count, first) rows sorted by key (all uint64)."""
+    import hashlib
+    o = np.argsort(np.asarray(keys, dtype=np.uint64), kind="stable")
+    rows = np.stack([np.asarray(keys, dtype=np.uint64)[o], np.asarray(counts, dtype=np.uint64)[o],
+                     np.asarray(first, dtype=np.uint64)[o]], 1)
+    return hashlib.sha256(np.ascontiguousarray(rows).tobytes()).hexdigest()
 
 
 def count(reads):

@@ -213,6 +213,25 @@ void ora_gen_pool_reads(uint64_t seed, uint64_t pool_seed, uint64_t U, uint64_t 
         ora_gen_reads(seed, ora_pool_index(pool_seed, i0 + k, U), 1, L, stride, ascii + k * stride);
 }
 
+/* Zipf-drawn pool reads (SURVEY §8(d) C5 skew): read i is pool item rank = #{k : cdf[k] <= u63},
+ * u63 = splitmix64(pool_seed ^ (i * 0xD1B54A32D192ED03)) >> 1, cdf = the Zipf CDF scaled to 2^63
+ * (cdf[U-1] = 2^63; the table is an input, built once on the host). */
+uint64_t ora_zipf_index(uint64_t pool_seed, uint64_t i, const uint64_t* cdf, uint64_t U) {
+    const uint64_t u63 = ora_splitmix64(pool_seed ^ (i * 0xD1B54A32D192ED03ull)) >> 1;
+    uint64_t lo = 0, hi = U;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (cdf[mid] <= u63) lo = mid + 1; else hi = mid;
+    }
+    return lo < U ? lo : U - 1;
+}
+
+void ora_gen_zipf_reads(uint64_t seed, uint64_t pool_seed, const uint64_t* cdf, uint64_t U, uint64_t i0,
+                        uint64_t n, uint32_t L, uint64_t stride, uint8_t* ascii) {
+    for (uint64_t k = 0; k < n; ++k)
+        ora_gen_reads(seed, ora_zipf_index(pool_seed, i0 + k, cdf, U), 1, L, stride, ascii + k * stride);
+}
+
 /* ---------------------------------------------------------------------------------------------
  * Counter (counter.pyx:41-54): dict keyed on (length, packed words) — ShortSeq64.__eq__ compares
  * (length, packed) (short_seq_64.pyx:41-44), ShortSeq192/Var compare length + memcmp of ceil(L/32)

@@ -1,11 +1,16 @@
 #!/usr/bin/env bash
-# A/B the counter tuner binaries given as arguments: rocprofv3 kernel-trace stats per binary, twice.
+# A/B the counter tuner binaries tools/tune_counter_<v> given as arguments, same box, interleaved:
+# uniform 2^24 and Zipf 1.1 2^24 (and 2^20 uniform), 3 rounds.  Prints one line per run.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
+mkdir -p gpurun_out/ab
 for rep in 1 2 3; do
-  for v in "$@"; do
-    timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/ab/$v.$rep -o run --output-format csv -- tools/tune_counter_$v 125000000 15 > gpurun_out/ab/$v.$rep.log 2>&1 || exit 1
+  for cfg in "24 0" "24 1.1" "20 0"; do
+    for v in "$@"; do
+      echo -n "$v $rep: "
+      timeout -k 10 120 tools/tune_counter_$v 125000000 15 $cfg || exit 1
+    done
   done
-done
+done 2>&1 | tee gpurun_out/ab/ab.log
 echo DONE

@@ -28,7 +28,8 @@ MAX_NT = 1024
 _NO_BAD = -1  # UINT64_MAX viewed as int64
 
 __all__ = ["words_for", "wpr_for", "encode", "encode_var", "decode", "decode_var", "hamming_ref",
-           "hamming_pair", "encode_hamming_ref", "synth_reads", "synth_pool_reads", "GpuCounter",
+           "hamming_pair", "encode_hamming_ref", "synth_reads", "synth_pool_reads", "synth_zipf_reads", "zipf_cdf",
+           "GpuCounter",
            "raise_read_error", "first_bad_buffer", "fastq_index", "gather_rows", "slice_fixed",
            "slice_var", "hamming_all_pairs", "HostStager", "host_stager", "encode_host", "decode_host"]
 
@@ -392,6 +393,31 @@ def synth_pool_reads(n: int, L: int, seed: int, pool_seed: int, U: int, *, i0: i
         out = torch.empty((n, L), dtype=torch.uint8, device=dev)
     check(lib().ss_synth_pool_reads(out.data_ptr(), seed, pool_seed, U, i0, n, L, L, _stream(dev)),
           "ss_synth_pool_reads")
+    return out
+
+
+def zipf_cdf(U: int, s: float = 1.1) -> np.ndarray:
+    """Zipf(s) CDF over pool ranks 0..U-1 scaled to 2^63 (uint64 [U]; the last entry is 2^63), the
+    table ss_synth_zipf_reads draws from (include/shortseq_amd.h).  Rank k has weight (k+1)^-s."""
+    w = np.arange(1, U + 1, dtype=np.float64) ** (-float(s))
+    c = np.cumsum(w)
+    c /= c[-1]
+    cdf = np.floor(c * 2.0 ** 63).astype(np.uint64)
+    cdf[-1] = np.uint64(1 << 63)
+    return cdf
+
+
+def synth_zipf_reads(n: int, L: int, seed: int, pool_seed: int, cdf, *, i0: int = 0, device=None,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Reads drawn from a Zipf-distributed pool (SURVEY §8(d) C5 skew): read i = pool item
+    rank(i) of the ss_synth_zipf_reads rule; `cdf` = zipf_cdf(U, s) (numpy) or its device copy."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if isinstance(cdf, np.ndarray):
+        cdf = torch.from_numpy(cdf.view(np.int64)).to(dev)
+    if out is None:
+        out = torch.empty((n, L), dtype=torch.uint8, device=dev)
+    check(lib().ss_synth_zipf_reads(out.data_ptr(), seed, pool_seed, cdf.data_ptr(), cdf.numel(), i0, n, L, L,
+                                    _stream(dev)), "ss_synth_zipf_reads")
     return out
 
 

@@ -540,10 +540,22 @@ __global__ __launch_bounds__(kThreads) void k_slice(const uint64_t* __restrict__
 // ------------------------------------------------------------------------------------------------
 // Synthetic reads; lane per (read, word).
 // ------------------------------------------------------------------------------------------------
-template <bool POOL>
+// Zipf pool draw: rank = #{k : cdf[k] <= u63} for the read's 63-bit uniform u63 (cdf[U-1] = 2^63,
+// so the rank is < U); pool id = rank (id 0 the most frequent).
+__device__ __forceinline__ uint64_t zipf_rank(const uint64_t* __restrict__ cdf, uint64_t U, uint64_t u63) {
+    uint64_t lo = 0, hi = U;           // first k with cdf[k] > u63 lies in [lo, hi]
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (cdf[mid] <= u63) lo = mid + 1; else hi = mid;
+    }
+    return lo < U ? lo : U - 1;
+}
+
+// POOL: 0 = read i is generator read i; 1 = pool read drawn uniformly from U; 2 = Zipf draw (cdf)
+template <int POOL>
 __global__ __launch_bounds__(kThreads) void k_synth(uint8_t* out, uint64_t seed, uint64_t pool_seed,
                                                     uint64_t U, uint64_t i0, uint64_t n, uint32_t L,
-                                                    uint64_t stride) {
+                                                    uint64_t stride, const uint64_t* __restrict__ cdf = nullptr) {
     const uint32_t W = words_for(L);
     const uint64_t total = n * W;
     for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total;
@@ -551,7 +563,8 @@ __global__ __launch_bounds__(kThreads) void k_synth(uint8_t* out, uint64_t seed,
         const uint64_t k = g / W;
         const uint32_t w = (uint32_t)(g - k * W);
         uint64_t id = i0 + k;
-        if (POOL) id = splitmix64(pool_seed ^ (id * 0xD1B54A32D192ED03ull)) % U;
+        if (POOL == 1) id = splitmix64(pool_seed ^ (id * 0xD1B54A32D192ED03ull)) % U;
+        if (POOL == 2) id = zipf_rank(cdf, U, splitmix64(pool_seed ^ (id * 0xD1B54A32D192ED03ull)) >> 1);
         const uint32_t nb = min(32u, L - 32u * w);
         uint64_t r = splitmix64(seed + id * W + w);
         if (nb < 32u) r &= (1ull << (2 * nb)) - 1ull;
@@ -851,7 +864,7 @@ int ss_synth_reads(uint8_t* d_ascii, uint64_t seed, uint64_t i0, uint64_t n, uin
     if (n == 0) return SS_OK;
     if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
     const unsigned grid = grid_for(n * words_for(L), kThreads, kGenGridCap);
-    hipLaunchKernelGGL((k_synth<false>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
+    hipLaunchKernelGGL((k_synth<0>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
                        (uint64_t)0, (uint64_t)1, i0, n, L, stride);
     return ss_check(hipGetLastError(), "k_synth");
 }
@@ -862,9 +875,20 @@ int ss_synth_pool_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, uin
     if (n == 0) return SS_OK;
     if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
     const unsigned grid = grid_for(n * words_for(L), kThreads, kGenGridCap);
-    hipLaunchKernelGGL((k_synth<true>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
-                       pool_seed, U, i0, n, L, stride);
+    hipLaunchKernelGGL((k_synth<1>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
+                       pool_seed, U, i0, n, L, stride, (const uint64_t*)nullptr);
     return ss_check(hipGetLastError(), "k_synth<pool>");
+}
+
+int ss_synth_zipf_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, const uint64_t* d_cdf, uint64_t U,
+                        uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream) {
+    if (L == 0 || L > SS_MAX_NT || stride < L || U == 0) return ss_fail(SS_EARG, "bad L/stride/U");
+    if (n == 0) return SS_OK;
+    if (!d_ascii || !d_cdf) return ss_fail(SS_EARG, "null buffer");
+    const unsigned grid = grid_for(n * words_for(L), kThreads, kGenGridCap);
+    hipLaunchKernelGGL((k_synth<2>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
+                       pool_seed, U, i0, n, L, stride, d_cdf);
+    return ss_check(hipGetLastError(), "k_synth<zipf>");
 }
 
 }  // extern "C"

@@ -1,13 +1,16 @@
 // ss_counter.hip — ShortSeqCounter on the GPU: fused encode -> open-addressing hash table in HBM
 // with atomic counts and first-occurrence indices (counter.pyx:41-54 semantics).
 //
-// Table: C = 2^k slots of 32 B (array of structs, one slot per 32-B sector) plus one sentinel slot:
+// Table: C = 2^k slots of 16 B (array of structs, one dwordx4 per slot) plus one sentinel slot:
 //   key    u64 packed word; EMPTY = ~0.  Claimed once by atomicCAS EMPTY -> key, never changed.
-//   ncount u64 = ~count (so a single 0xFF memset resets key, count and first together);
+//   ncount u32 = ~count (so a single 0xFF memset resets key, count and first together);
 //          incremented with atomicAdd(-1).
-//   first  u64 atomicMin of the global read index (~0 = unset).
-// One slot = one sector: the probe load, the count atomic and the first-index check touch the same
-// 32 B, instead of three random lines for three separate arrays.
+//   first  u32 atomicMin of the global read index (0xFFFFFFFF = unset).
+// A handle therefore counts reads with global indices below 2^32 - 1 (the 1B-read C5 job uses
+// 0..1e9); an index past that raises overflow bit 3 (ss_counter_overflow) and the insert is
+// refused up front when base_index + n says so.
+// One slot = one dwordx4: the probe load, the count atomic and the first-index check touch the same
+// 16 B, and a fresh slice is written back as one dwordx4 store per slot.
 // The packed word ~0 ("G" * 32) collides with EMPTY and lives in the sentinel slot C.
 // Every key of one handle has the same length L <= 32 (the host groups a mixed batch by length, so
 // the dict key (length, packed) of short_seq_64.pyx:41-44 is (handle, word) here).
@@ -21,12 +24,15 @@
 using namespace ssd;
 
 namespace {
-struct alignas(32) Slot {
+struct alignas(16) Slot {
     unsigned long long key;
-    unsigned long long ncount;
-    unsigned long long first;
-    unsigned long long pad;
+    uint32_t ncount;
+    uint32_t first;
 };
+static_assert(sizeof(Slot) == 16, "one slot = one dwordx4");
+constexpr uint32_t kNoFirst = 0xFFFFFFFFu;     // first index of an unused slot
+constexpr uint64_t kMaxIndex = 0xFFFFFFFEull;  // largest global read index a slot can hold
+constexpr unsigned long long kOvfTable = 1ull, kOvfExtract = 2ull, kOvfField = 4ull, kOvfIndex = 8ull;
 constexpr int kThreads = 256;
 constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
 constexpr uint32_t kExtractBlocks = 4096;  // extract passes: fixed grid, contiguous slot ranges
@@ -56,16 +62,21 @@ struct ss_counter {
     uint64_t* ws_keys = nullptr;           // [ws_reads] packed key of read i; later bucketed by region
     uint64_t* ws_akey = nullptr;           // [ws_reads] keys bucketed by coarse bin
     uint32_t* ws_aidx = nullptr;           // [ws_reads] batch-local read index, same order
+    uint32_t* ws_acnt = nullptr;           // weighted records' counts, coarse order (same size as ws_aidx)
     uint32_t* ws_bidx = nullptr;           // [ws_reads] batch-local read index, region order
+    uint32_t* ws_bcnt = nullptr;           // [ws_reads] weighted records' counts, region order
+    uint4* ws_spill = nullptr;             // [ws_reads] records past a full sub-bin
     uint32_t* ws_hist = nullptr;           // [kPartBlocks * regions] per-(block, bin) counts -> offsets
     uint32_t* ws_rstart = nullptr;         // [regions + 1] region start in the bucket arrays
+    uint32_t* ws_order = nullptr;          // [kNFill] sub-bins by descending fill (k_pf_order)
+    uint32_t* ws_segend = nullptr;         // [regions x kFinePerBin] end of each (sub-bin, region) fine segment
     uint32_t* ws_tot = nullptr;            // [regions + 1] scratch (bin totals / coarse starts)
     // optimistic coarse partition (k_pf_coarse): ws_akey / ws_aidx hold 128 bins of ws_cap1 slots
     uint64_t ws_cap1 = 0;
-    uint32_t* ws_fill = nullptr;           // bin fill counters + overflow flag, kFillStride apart
-    // per-region occupancy (used slots of each slice), written by the single-word aggregate; lets
-    // ss_counter_pack_ranges skip its counting pass.  occ_src: 0 = stale, 1 = valid, 2 = valid
-    // unless the optimistic partition overflowed (the ws_fill overflow flag: the direct insert ran instead)
+    uint32_t* ws_fill = nullptr;           // sub-bin fill counters + the spill counter, kFillStride apart
+    // per-region occupancy (used slots of each slice), written by the single-word aggregate (and
+    // kept by the spill insert); lets ss_counter_pack_ranges skip its counting pass.
+    // occ_src: 0 = stale, 1 = valid
     uint32_t* occ = nullptr;               // [R]
     unsigned long long* roff = nullptr;    // [R + 2] pack scratch: region offsets, sentinel position
     uint64_t occ_R = 0;
@@ -106,8 +117,10 @@ __device__ __forceinline__ uint64_t slot_top(const Tbl& t, uint64_t key) {
     return t.shift >= 64 ? 0 : slot_hash(key, t.shift);
 }
 
-__device__ __forceinline__ void tbl_add(const Tbl& t, uint64_t key, unsigned long long cnt,
-                                        unsigned long long idx) {
+// Insert / count `cnt` copies of `key` first seen at global read index `idx`.  Returns true when this
+// call claimed a new slot (the spill pass keeps the region occupancy current with it).
+__device__ __forceinline__ bool tbl_add(const Tbl& t, uint64_t key, uint32_t cnt, unsigned long long idx) {
+    bool claimed = false;
     uint64_t s;
     if (key == kEmpty) {
         s = t.mask + 1;  // sentinel slot
@@ -127,20 +140,26 @@ __device__ __forceinline__ void tbl_add(const Tbl& t, uint64_t key, unsigned lon
                 const unsigned long long prev = atomicCAS(&t.slots[h].key, (unsigned long long)kEmpty,
                                                           (unsigned long long)key);
                 if (prev == kEmpty || prev == key) {
+                    claimed = prev == kEmpty;
                     s = h;
                     break;
                 }
             }
             off = (off + 1) & t.slice_mask;
             if (++probes > t.slice_mask) {
-                atomicOr(t.overflow, 1ull);
-                return;
+                atomicOr(t.overflow, kOvfTable);
+                return false;
             }
         }
     }
+    if (idx > kMaxIndex) {
+        atomicOr(t.overflow, kOvfIndex);
+        idx = kMaxIndex;
+    }
     Slot* sl = &t.slots[s];
-    atomicAdd(&sl->ncount, 0ull - cnt);
-    if (sl->first > idx) atomicMin(&sl->first, idx);
+    atomicAdd(&sl->ncount, 0u - cnt);
+    if (sl->first > (uint32_t)idx) atomicMin(&sl->first, (uint32_t)idx);
+    return claimed;
 }
 
 // Fast path, L in {16, 32}, 16-B aligned rows: two lanes per read (lane pair = one packed word,
@@ -175,7 +194,7 @@ __global__ __launch_bounds__(kThreads) void k_count_g16(Tbl t, const uint4* __re
         const uint32_t bad_pair = e.bad | swap_pair(e.bad);
         const bool live = r < n && k == 0;
         report_bad(live && bad_pair != 0u, r, first_bad);
-        if (live && bad_pair == 0u) tbl_add(t, (uint64_t)v | ((uint64_t)hi << 32), 1ull, base_index + r);
+        if (live && bad_pair == 0u) tbl_add(t, (uint64_t)v | ((uint64_t)hi << 32), 1u, base_index + r);
     }
     }
 }
@@ -193,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void k_count_gen(Tbl t, const uint8_t* in
             atomicMin(first_bad, (unsigned long long)r);
             continue;
         }
-        tbl_add(t, key, 1ull, base_index + r);
+        tbl_add(t, key, 1u, base_index + r);
     }
 }
 
@@ -228,7 +247,10 @@ __device__ __forceinline__ uint64_t load_word_general(const uint8_t* p, uint32_t
 __global__ __launch_bounds__(kThreads) void k_merge(Tbl t, const uint64_t* keys, const uint64_t* counts,
                                                     const uint64_t* first, uint64_t m) {
     for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kThreads)
-        tbl_add(t, keys[i], counts[i], first[i]);
+    {
+        if (counts[i] >> 32) atomicOr(t.overflow, kOvfField);   // a slot counts up to 2^32 - 1
+        tbl_add(t, keys[i], (uint32_t)counts[i], first[i]);
+    }
 }
 
 __device__ __forceinline__ bool slot_used(const Tbl& t, uint64_t s, uint64_t& key) {
@@ -238,7 +260,7 @@ __device__ __forceinline__ bool slot_used(const Tbl& t, uint64_t s, uint64_t& ke
         return key != kEmpty;
     }
     key = kEmpty;
-    return sl.ncount != ~0ull;   // sentinel slot: used iff its count is nonzero
+    return sl.ncount != 0xFFFFFFFFu;   // sentinel slot: used iff its count is nonzero
 }
 
 __global__ __launch_bounds__(kThreads) void k_size(Tbl t, unsigned long long* out) {
@@ -361,7 +383,7 @@ __global__ __launch_bounds__(kExtractT) void k_part_scatter(Tbl t, uint32_t npar
         const unsigned long long pos = wave_reserve(used, used ? part_of(t, s, key, nparts, ranges) : 0u, cursor);
         if (!used) continue;
         if (pos >= cap_out) {
-            atomicOr(overflow, 2ull);
+            atomicOr(overflow, kOvfExtract);
             continue;
         }
         const Slot& sl = t.slots[s];
@@ -375,7 +397,7 @@ __global__ __launch_bounds__(kExtractT) void k_part_scatter(Tbl t, uint32_t npar
         }
         okeys[pos] = key;
         olens[pos] = (uint32_t)L;
-        ocounts[pos] = ~sl.ncount;
+        ocounts[pos] = (uint32_t)~sl.ncount;
         ofirst[pos] = sl.first;
     }
 }
@@ -399,11 +421,22 @@ __global__ __launch_bounds__(kExtractT) void k_part_scatter(Tbl t, uint32_t npar
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kCoarseBits = 7;    // 128 coarse bins for the first partition pass
 
+// Weighted partition record: read index | kWeighted means the record stands for several copies of
+// its key (deduplicated inside one coarse tile); its count sits in the parallel count array (acnt
+// in coarse order, bcnt in region order).  Batch-local indices are < 2^31 (ss_counter_reserve).
+constexpr uint32_t kWeighted = 0x80000000u;
+
 struct PartWs {
     uint64_t* keys;    // P1 output; P3 second-pass output (bucketed by region)
     uint64_t* akey;    // first-pass output (bucketed by coarse bin)
     uint32_t* aidx;
+    uint32_t* acnt;    // weighted records' counts, coarse order (sparse: weighted positions only)
     uint32_t* bidx;    // second-pass output indices
+    uint32_t* bcnt;    // weighted records' counts, region order (sparse)
+    uint4* spill;      // records past a full sub-bin: {key lo, key hi, count, batch index}
+    uint64_t spill_cap;
+    uint32_t* seg_end; // optimistic path: end of each (sub-bin, region) segment written by the fine
+                       // scatter (hist holds the starts); null on the exact paths (rstart ranges)
     const uint64_t* bkey;  // the region-bucketed keys the aggregate reads (keys or akey)
     uint32_t* hist;    // [kPartBlocks][bins] per-(block, bin) counts -> offsets
     uint32_t* rstart;  // [R + 1] region start in the bucketed arrays
@@ -739,11 +772,17 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
 // serialize: 128 shared counters cost ~0.57 ms of the pass at 125M reads, 8 x 128 cost the pass
 // 1.54 -> 1.28 ms, profiles/r1/r1k/c5_coarse_probes.txt), while the 64 blocks that share a
 // sub-bin still fill its lines back to back.  Sub-bin f = (bin, sub) owns slots [f * cap1,
-// (f + 1) * cap1) of the coarse arrays (cap1 = 1.25 x the mean sub-bin load + 1024).  Order inside
+// (f + 1) * cap1) of the coarse arrays (cap1 = 2.5 x the mean sub-bin load + 1024).  Order inside
 // a sub-bin is arbitrary, which the aggregation does not care about (count = sum, first = min of
-// the carried read index).  A sub-bin that would overflow raises the overflow word: every later
-// pass then idles and k_count_g16 inserts the batch directly (adversarial inputs that pile one
-// bin, e.g. a few keys repeated, still count exactly).
+// the carried read index).
+// Skew (counter.pyx:41-54 counts every duplicate; real read sets and Zipf pools repeat a few keys
+// very often): a bin holding more than kHeavy reads of a tile (2x the mean of 32) is deduplicated in
+// LDS before its reservation: every distinct key of the bin leaves the tile as ONE record, with its
+// copy count (a weighted record, kWeighted) when it occurred more than once, and the minimum read
+// index.  A hot key therefore costs one record per tile, and a bin that was not deduplicated holds at
+// most 2x the mean per tile, which the 2.5x sub-bin capacity absorbs.  Records that still find their
+// sub-bin full (crafted inputs: thousands of distinct keys in one bin) go to the spill list, which
+// k_spill_insert counts into the table after the aggregate (exact; no whole-batch fallback).
 // Fine pass: block f takes sub-bin f whole; all of its keys lie in the bin's 2^(rbits - 7)
 // regions, so the histogram and the LDS staging use that window.
 // ------------------------------------------------------------------------------------------------
@@ -760,8 +799,8 @@ constexpr uint32_t kFillStride = SS_FILL_STRIDE;
 #endif
 constexpr uint32_t kFinePerBin = SS_FINE_PER_BIN;    // fine-pass blocks per coarse bin = sub-bins per bin
 constexpr uint32_t kNFill = kCB * kFinePerBin;       // sub-bin fill counters
-constexpr uint32_t kOvf = kNFill;                    // the overflow flag's index
-constexpr uint32_t kFillWords = (kNFill + 1) * kFillStride;   // counters + the overflow flag
+constexpr uint32_t kSpillCtr = kNFill;               // the spill list's record counter
+constexpr uint32_t kFillWords = (kNFill + 1) * kFillStride;   // counters + the spill counter
 __host__ __device__ __forceinline__ uint32_t fill_at(uint32_t b) { return b * kFillStride; }
 #ifndef SS_PF_RPL
 #define SS_PF_RPL 16
@@ -769,19 +808,94 @@ __host__ __device__ __forceinline__ uint32_t fill_at(uint32_t b) { return b * kF
 #ifndef SS_PF_T
 #define SS_PF_T 256      // 256 x 16 reads per tile: ~5 % faster than 512 x 8 over 9 same-box samples each
 #endif
+#ifndef SS_PF_HEAVY
+#define SS_PF_HEAVY 64   // reads of one bin in one tile above which the bin is deduplicated (2x the mean)
+#endif
 constexpr uint32_t kPfT = SS_PF_T, kPfRPL = SS_PF_RPL;   // k_pf_coarse: kPfT * kPfRPL-read tiles
+constexpr uint32_t kHeavy = SS_PF_HEAVY;
+
+// sub-bin capacity of the optimistic partition for a batch of n reads (host and device agree)
+__host__ __device__ __forceinline__ uint64_t pf_cap1(uint64_t n) {
+    return (5 * n / 2 + kNFill - 1) / kNFill + 1024;
+}
+
+// 64-bit lane broadcast
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int lane) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, lane), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Wave-level fold of lanes that share a key (hot keys fill whole waves of a skewed bucket): up to
+// PEELS times, the active lanes whose key equals the key of the lowest active lane not yet folded
+// into are folded into that lane (count summed, index min); the folded lanes turn inactive.  A peel
+// costs one ballot + broadcast, and a 6-step sum / min only when at least two lanes match.  All 64
+// lanes must call it (uniform control flow); returns with the surviving lanes active.
+template <int PEELS>
+__device__ __forceinline__ void wave_fold(bool& act, uint64_t key, uint32_t& cnt, uint32_t& idx) {
+    const int lane = (int)(threadIdx.x & 63);
+    bool led = false;
+#pragma unroll
+    for (int peel = 0; peel < PEELS; ++peel) {
+        const uint64_t cand = __ballot(act && !led);
+        if (!cand) break;
+        const int leader = __ffsll((long long)cand) - 1;
+        const uint64_t lk = shfl64(key, leader);
+        const bool m = act && key == lk;
+        const uint64_t mm = __ballot(m);
+        if (__popcll(mm) < 2) break;
+        uint32_t cs = m ? cnt : 0u, mi = m ? idx : 0xFFFFFFFFu;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            cs += (uint32_t)__shfl_xor((int)cs, off);
+            const uint32_t o = (uint32_t)__shfl_xor((int)mi, off);
+            mi = o < mi ? o : mi;
+        }
+        if (m) {
+            if (lane == leader) {
+                cnt = cs;
+                idx = mi;
+                led = true;
+            } else {
+                act = false;
+            }
+        }
+    }
+}
+
+// wave_fold peels in the coarse dedup, the fine dedup and the aggregate (0 = off).  Same-box A/B
+// (tools/tune_counter.hip, 125M reads, 3 rounds): coarse 2 peels Zipf 3.67 -> 3.83 ms, fine 2 peels
+// no change, aggregate 2 peels 3.59 -> 3.67 ms Zipf and +0.03 ms uniform (the fine dedup already
+// bounds a region's copies of one key to ~1 per tile), so all are off; kept as knobs.
+#ifndef SS_COARSE_FOLD
+#define SS_COARSE_FOLD 0
+#endif
+#ifndef SS_FINE_FOLD
+#define SS_FINE_FOLD 0
+#endif
+#ifndef SS_AGG_FOLD
+#define SS_AGG_FOLD 0
+#endif
+
+// LDS dedup table of one tile: entry = (staged element + 1) | count << 16, 0 = free
+__device__ __forceinline__ uint32_t dedup_home(uint64_t key, uint32_t log2n) {
+    return (uint32_t)((key * 0xD6E8FEB86659FD93ull) >> (64 - log2n));
+}
 
 template <int T, int RPL>
 __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
                                                  uint64_t n, uint32_t cpr, uint64_t cap1, uint32_t* fill,
                                                  unsigned long long* first_bad) {
     constexpr uint32_t TILE = T * RPL;
-    // (two blocks per CU by LDS: a 3-block variant without the staged bin array measured 4 % slower)
-    __shared__ uint32_t lcount[kCB], lstart[kCB], gbase[kCB];
+    constexpr uint32_t kHtLog = TILE == 4096 ? 12 : TILE == 2048 ? 11 : 13;
+    static_assert((1u << kHtLog) == TILE, "tile must be 2048, 4096 or 8192 reads");
+    __shared__ uint32_t lcount[kCB], lstart[kCB], gbase[kCB], hcnt[kCB], sbase[kCB];
+    __shared__ uint8_t hflag[kCB];
+    __shared__ uint32_t any_heavy;
     __shared__ uint64_t skey[TILE];
     __shared__ uint32_t sidx[TILE];
     __shared__ uint8_t sbin[TILE];
-    uint32_t* ovf = fill + fill_at(kOvf);
+    __shared__ uint32_t ht[TILE];
+    uint32_t* spill_ctr = fill + fill_at(kSpillCtr);
     const uint32_t shift = w.rbits - kCoarseBits;
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t sub = blockIdx.x % kFinePerBin;   // this block's sub-bin of every bin
@@ -796,26 +910,23 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                                       : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
         }
     };
-#ifndef SS_PF_PREFETCH
-#define SS_PF_PREFETCH 0   // register double buffer off: 190 -> fewer VGPRs, 2 blocks per CU (tune_counter A/B: -5 %)
-#endif
+    // wave 0, one bin: reserve c slots of sub-bin (b, sub); the part past cap1 reserves spill records
+    auto reserve = [&](uint32_t b, uint32_t c) {
+        const uint32_t g = c ? atomicAdd(&fill[fill_at(b * kFinePerBin + sub)], c) : 0u;
+        gbase[b] = g;
+        const uint64_t end = (uint64_t)g + c, from = max((uint64_t)g, cap1);
+        sbase[b] = end > from ? atomicAdd(spill_ctr, (uint32_t)(end - from)) : 0u;
+    };
     static_assert(kCB == 128, "wave 0 scans two bins per lane");
     for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
     __syncthreads();
-    if (SS_PF_PREFETCH && blockIdx.x < tiles) load_tile(blockIdx.x);
     // three barriers per tile: (A) ranks counted, (B) wave 0 has scanned the bins, reserved the
     // tile's runs in the global bins and zeroed the counters for the next tile, (C) tile staged in
     // LDS.  The next tile's rank atomics only touch lcount (zeroed before B) and its staging waits
-    // for its own barrier B, which every wave reaches only after this tile's write-out.
+    // for its own barrier B, which every wave reaches only after this tile's write-out.  A tile with
+    // a heavy bin adds three: (D) deduplicated, (E) survivors counted, (F) heavy bins reserved.
     for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        if (!SS_PF_PREFETCH) load_tile(tile);
-        uint4 x[RPL][2];
-#pragma unroll
-        for (int j = 0; j < RPL; ++j) {
-            x[j][0] = nx[j][0];
-            x[j][1] = nx[j][1];
-        }
-        if (SS_PF_PREFETCH && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
+        load_tile(tile);
         uint64_t key[RPL];
         uint32_t bin[RPL], rank[RPL];
         const uint64_t t0 = tile * TILE;
@@ -824,8 +935,8 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
         for (int j = 0; j < RPL; ++j) {
             const uint64_t r = t0 + j * T + threadIdx.x;
             // table path for both chunks (L <= 32); the low chunk's alias carry into the high half
-            const Enc32 a = encode16(x[j][0].x, x[j][0].y, x[j][0].z, x[j][0].w, true);
-            const Enc32 b = encode16(x[j][1].x, x[j][1].y, x[j][1].z, x[j][1].w, true);
+            const Enc32 a = encode16(nx[j][0].x, nx[j][0].y, nx[j][0].z, nx[j][0].w, true);
+            const Enc32 b = encode16(nx[j][1].x, nx[j][1].y, nx[j][1].z, nx[j][1].w, true);
             const bool live = r < n;
             report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
             key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
@@ -846,12 +957,20 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             const uint32_t excl = incl - c0 - c1;
             lstart[b0] = excl;
             lstart[b0 + 1] = excl + c0;
-            gbase[b0] = c0 ? atomicAdd(&fill[fill_at(b0 * kFinePerBin + sub)], c0) : 0u;
-            gbase[b0 + 1] = c1 ? atomicAdd(&fill[fill_at((b0 + 1) * kFinePerBin + sub)], c1) : 0u;
+            const bool h0 = c0 > kHeavy, h1 = c1 > kHeavy;
+            hflag[b0] = h0;
+            hflag[b0 + 1] = h1;
+            if (!h0) reserve(b0, c0);
+            if (!h1) reserve(b0 + 1, c1);
+            const uint64_t hv = __ballot(h0 || h1);
+            if (lane == 0) any_heavy = hv != 0;
             lcount[b0] = 0;
             lcount[b0 + 1] = 0;
+            hcnt[b0] = 0;
+            hcnt[b0 + 1] = 0;
         }
         __syncthreads();                                                  // (B)
+        const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
             const uint32_t e = j * T + threadIdx.x;
@@ -862,16 +981,85 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                 sbin[sp] = (uint8_t)bin[j];
             }
         }
+        if (heavy_tile)
+            for (uint32_t i = threadIdx.x; i < TILE; i += T) ht[i] = 0;
         __syncthreads();                                                  // (C)
+        if (heavy_tile) {
+            // (D) every element of a heavy bin claims its key's entry or folds into the claimer's:
+            // count += c in the entry, read index min into the claimer's sidx, element marked dead.
+            // Staged elements are bin-sorted, so a wave's lanes often share a hot key: those fold
+            // in registers first (one LDS atomic per wave instead of 64 on one address).
+            for (uint32_t i0 = 0; i0 < cnt; i0 += T) {
+                const uint32_t i = i0 + threadIdx.x;
+                bool act = i < cnt && hflag[sbin[i]];
+                const uint64_t k = act ? skey[i] : 0ull;
+                uint32_t c = 1, mi = act ? sidx[i] : 0xFFFFFFFFu;
+                const bool was = act;
+                wave_fold<SS_COARSE_FOLD>(act, k, c, mi);
+                if (was && !act) sbin[i] = 0xFF;                          // folded into its wave leader
+                if (!act) continue;
+                sidx[i] = mi;
+                uint32_t h = dedup_home(k, kHtLog);
+                for (;;) {
+                    uint32_t e = ht[h];
+                    if (e == 0) {
+                        e = atomicCAS(&ht[h], 0u, (i + 1) | (c << 16));
+                        if (e == 0) break;
+                    }
+                    const uint32_t j = (e & 0xFFFFu) - 1;
+                    if (skey[j] == k) {
+                        atomicAdd(&ht[h], c << 16);
+                        atomicMin(&sidx[j], mi);
+                        sbin[i] = 0xFF;
+                        break;
+                    }
+                    h = (h + 1) & (TILE - 1);
+                }
+            }
+            __syncthreads();                                              // (D)
+            for (uint32_t i = threadIdx.x; i < cnt; i += T) {
+                const uint32_t b = sbin[i];
+                if (b != 0xFF && hflag[b]) atomicAdd(&hcnt[b], 1u);
+            }
+            __syncthreads();                                              // (E)
+            if (threadIdx.x < 64) {
+                const uint32_t b0 = 2 * threadIdx.x;
+                if (hflag[b0]) reserve(b0, hcnt[b0]);
+                if (hflag[b0 + 1]) reserve(b0 + 1, hcnt[b0 + 1]);
+                hcnt[b0] = 0;     // now the heavy bins' write cursors
+                hcnt[b0 + 1] = 0;
+            }
+            __syncthreads();                                              // (F)
+        }
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
             const uint32_t b = sbin[i];
-            const uint64_t pos = (uint64_t)gbase[b] + (i - lstart[b]);
+            if (b == 0xFF) continue;                                      // folded into its claimer
+            uint32_t local, c = 1;
+            if (heavy_tile && hflag[b]) {
+                local = atomicAdd(&hcnt[b], 1u);
+                uint32_t h = dedup_home(skey[i], kHtLog);
+                while ((ht[h] & 0xFFFFu) != i + 1) h = (h + 1) & (TILE - 1);
+                c = ht[h] >> 16;
+            } else {
+                local = i - lstart[b];
+            }
+            const uint64_t pos = (uint64_t)gbase[b] + local;
+            const uint64_t k = skey[i];
             if (pos < cap1) {
                 const uint64_t at = (uint64_t)(b * kFinePerBin + sub) * cap1 + pos;
-                w.akey[at] = skey[i];
-                w.aidx[at] = sidx[i];
+                w.akey[at] = k;
+                if (c > 1) {
+                    w.aidx[at] = sidx[i] | kWeighted;
+                    w.acnt[at] = c;
+                } else {
+                    w.aidx[at] = sidx[i];
+                }
             } else {
-                *ovf = 1u;
+                const uint64_t sp = (uint64_t)sbase[b] + (pos - max((uint64_t)gbase[b], cap1));
+                if (sp < w.spill_cap)
+                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), c, sidx[i]);
+                else
+                    atomicOr(t.overflow, kOvfTable);
             }
         }
     }
@@ -889,7 +1077,6 @@ __device__ __forceinline__ void fine_range(uint32_t fb, const uint32_t* fill, ui
 template <int T>
 __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
     __shared__ uint32_t h[kMaxLocalBins];
-    if (fill[fill_at(kOvf)]) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits);
     uint32_t bin;
     uint64_t lo, hi;
@@ -905,8 +1092,7 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
 
 // region totals over the bin's 8 fine blocks (thread per region) -> w.tot; then k_pc_scan (one
 // block) -> rstart; then k_pf_offsets (thread per region) -> each fine block's write cursors
-__global__ __launch_bounds__(256) void k_pf_tot(PartWs w, const uint32_t* fill) {
-    if (fill[fill_at(kOvf)]) return;
+__global__ __launch_bounds__(256) void k_pf_tot(PartWs w) {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= w.R) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
@@ -916,8 +1102,7 @@ __global__ __launch_bounds__(256) void k_pf_tot(PartWs w, const uint32_t* fill) 
     w.tot[r] = tot;
 }
 
-__global__ __launch_bounds__(256) void k_pf_offsets(PartWs w, const uint32_t* fill) {
-    if (fill[fill_at(kOvf)]) return;
+__global__ __launch_bounds__(256) void k_pf_offsets(PartWs w) {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= w.R) return;
     const uint32_t rpb = 1u << (w.rbits - kCoarseBits), bin = r / rpb, j = r % rpb;
@@ -931,28 +1116,74 @@ __global__ __launch_bounds__(256) void k_pf_offsets(PartWs w, const uint32_t* fi
     }
 }
 
+// Largest sub-bin first: order[k] = the sub-bin with the k-th largest fill (ties by index), so the
+// fine scatter's blocks (dispatched in blockIdx order) start the long ones first and the pass does
+// not end on a skewed sub-bin that started last.  One block: bitonic sort of (~fill, index) in LDS.
+__global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ fill, uint64_t cap1,
+                                                  uint32_t* __restrict__ order) {
+    static_assert(kNFill == 1024, "one 512-thread block sorts 1024 sub-bins");
+    __shared__ uint64_t v[kNFill];
+    for (uint32_t i = threadIdx.x; i < kNFill; i += 512) {
+        const uint32_t f = (uint32_t)min((uint64_t)fill[fill_at(i)], cap1);
+        v[i] = ((uint64_t)~f << 32) | i;      // ascending = fill descending, then index
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= kNFill; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t t = threadIdx.x;
+            const uint32_t i = 2 * j * (t / j) + (t % j), l = i + j;   // the pair (i, l), i < l
+            const bool up = (i & k) == 0;
+            const uint64_t a = v[i], b = v[l];
+            if ((a > b) == up) {
+                v[i] = b;
+                v[l] = a;
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < kNFill; i += 512) order[i] = (uint32_t)v[i];
+}
+
 // fine scatter: coarse bin slice -> (key, read index) grouped by region, LDS-staged like
-// k_pc_scatter_lds (local bins = the coarse bin's regions)
-__global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
+// k_pc_scatter_lds (local bins = the coarse bin's regions).  A weighted record is staged with its
+// position in the sub-bin instead of its read index; the write-out fetches its index and count.
+// Region-level skew (a key too rare to make its coarse bin heavy can still hold a large share of its
+// region: Zipf rank 13 is 0.7 % of all reads = 110x a region's mean): a region holding more than
+// kHeavyFine records of a 4096-record tile is deduplicated like the coarse pass's heavy bins
+// (unweighted records only; each distinct key leaves as one record, weighted when repeated).  The
+// (sub-bin, region) segments then end before their reserved size; the end of each is written to
+// w.seg_end and the aggregate reads only the written part.
+#ifndef SS_HEAVY_FINE
+#define SS_HEAVY_FINE 2   // x the mean records per region per tile
+#endif
+__global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill,
+                                                    const uint32_t* __restrict__ order) {
     constexpr int T = 512;
-    // <= 256 regions per coarse bin on this path (rbits - 7 <= 8); LDS under 53 KB (no stored bin:
-    // recomputed from the key) so three 512-thread blocks fit a CU
+    constexpr uint32_t kHtLog = 12;
+    static_assert(kTile == (1u << kHtLog), "fine tile = dedup table size");
+    constexpr uint32_t kDead = 0xFFFFFFFFu;
+    // <= 256 regions per coarse bin on this path (rbits - 7 <= 8)
     constexpr uint32_t kNB = 256;
     __shared__ uint32_t cursor[kNB];
     __shared__ uint32_t lstart[kNB];
     __shared__ uint32_t lcount[kNB];
+    __shared__ uint32_t hcnt[kNB];
     __shared__ uint64_t skey[kTile];
     __shared__ uint32_t sidx[kTile];
+    __shared__ uint32_t ht[kTile];
     __shared__ uint32_t wsum[17];
-    if (fill[fill_at(kOvf)]) return;
+    __shared__ uint32_t any_heavy;
     const uint32_t nb = 1u << (w.rbits - kCoarseBits);
+    const uint32_t heavy_at = max(64u, SS_HEAVY_FINE * (kTile / nb));
     uint32_t bin;
     uint64_t lo, hi;
-    fine_range(blockIdx.x, fill, cap1, bin, lo, hi);
+    const uint32_t fb = order[blockIdx.x];     // this block's sub-bin
+    fine_range(fb, fill, cap1, bin, lo, hi);
     const uint32_t r0 = bin * nb;
-    const uint64_t* src = w.akey + (uint64_t)blockIdx.x * cap1;
-    const uint32_t* src_idx = w.aidx + (uint64_t)blockIdx.x * cap1;
-    for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] = w.hist[(uint64_t)blockIdx.x * nb + i];
+    const uint64_t* src = w.akey + (uint64_t)fb * cap1;
+    const uint32_t* src_idx = w.aidx + (uint64_t)fb * cap1;
+    const uint32_t* src_cnt = w.acnt + (uint64_t)fb * cap1;
+    for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] = w.hist[(uint64_t)fb * nb + i];
     __syncthreads();
     uint64_t nkey[kTile / T];
     uint32_t nidx[kTile / T];
@@ -963,7 +1194,8 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
             const uint32_t e = j * T + threadIdx.x;
             if (e < cnt) {
                 nkey[j] = src[t0 + e];
-                nidx[j] = src_idx[t0 + e];
+                const uint32_t x = src_idx[t0 + e];
+                nidx[j] = (x & kWeighted) ? kWeighted | (uint32_t)(t0 + e) : x;
             }
         }
     };
@@ -971,6 +1203,7 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
     for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
         const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
         for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
+        if (threadIdx.x == 0) any_heavy = 0;
         __syncthreads();
         uint64_t key[kTile / T];
         uint32_t idx[kTile / T], lb[kTile / T], rank[kTile / T];
@@ -989,9 +1222,14 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
             }
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nb; i += T) lstart[i] = lcount[i];
+        for (uint32_t i = threadIdx.x; i < nb; i += T) {
+            lstart[i] = lcount[i];
+            hcnt[i] = 0;
+            if (lcount[i] > heavy_at) any_heavy = 1;
+        }
         __syncthreads();
         block_scan_512(lstart, nb, wsum);
+        const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
             const uint32_t e = j * T + threadIdx.x;
@@ -1001,17 +1239,93 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
                 sidx[sp] = idx[j];
             }
         }
+        if (heavy_tile)
+            for (uint32_t i = threadIdx.x; i < kTile; i += T) ht[i] = 0;
         __syncthreads();
+        if (heavy_tile) {
+            for (uint32_t i0 = 0; i0 < cnt; i0 += T) {
+                const uint32_t i = i0 + threadIdx.x;
+                const uint64_t k = i < cnt ? skey[i] : 0ull;
+                const uint32_t x = i < cnt ? sidx[i] : kWeighted;
+                bool act = i < cnt && lcount[region_of(t, k) - r0] > heavy_at && !(x & kWeighted);
+                uint32_t c = 1, mi = x;
+                const bool was = act;
+                wave_fold<SS_FINE_FOLD>(act, k, c, mi);
+                if (was && !act) sidx[i] = kDead;                         // folded into its wave leader
+                if (!act) continue;
+                sidx[i] = mi;
+                uint32_t h = dedup_home(k, kHtLog);
+                for (;;) {
+                    uint32_t e = ht[h];
+                    if (e == 0) {
+                        e = atomicCAS(&ht[h], 0u, (i + 1) | (c << 16));
+                        if (e == 0) break;
+                    }
+                    const uint32_t j = (e & 0xFFFFu) - 1;
+                    if (skey[j] == k) {
+                        atomicAdd(&ht[h], c << 16);
+                        atomicMin(&sidx[j], mi);
+                        sidx[i] = kDead;
+                        break;
+                    }
+                    h = (h + 1) & (kTile - 1);
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < cnt; i += T) {
+                const uint32_t b = region_of(t, skey[i]) - r0;
+                if (lcount[b] > heavy_at && sidx[i] != kDead) atomicAdd(&hcnt[b], 1u);
+            }
+            for (uint32_t i = threadIdx.x; i < nb; i += T)
+                if (lcount[i] > heavy_at) lstart[i] = 0;    // now the heavy region's write cursor
+            __syncthreads();
+        }
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
             const uint64_t k = skey[i];
+            const uint32_t x = sidx[i];
+            if (x == kDead) continue;
             const uint32_t b = region_of(t, k) - r0;
-            const uint32_t gpos = cursor[b] + (i - lstart[b]);
+            uint32_t local, c = 1;
+            if (heavy_tile && lcount[b] > heavy_at) {
+                local = atomicAdd(&lstart[b], 1u);
+                if (!(x & kWeighted)) {
+                    uint32_t h = dedup_home(k, kHtLog);
+                    while ((ht[h] & 0xFFFFu) != i + 1) h = (h + 1) & (kTile - 1);
+                    c = ht[h] >> 16;
+                }
+            } else {
+                local = i - lstart[b];
+            }
+            const uint32_t gpos = cursor[b] + local;
             w.keys[gpos] = k;
-            w.bidx[gpos] = sidx[i];
+            if (x & kWeighted) {
+                const uint32_t p = x & ~kWeighted;
+                w.bidx[gpos] = src_idx[p];          // the read index, flag kept
+                w.bcnt[gpos] = src_cnt[p];
+            } else if (c > 1) {
+                w.bidx[gpos] = x | kWeighted;
+                w.bcnt[gpos] = c;
+            } else {
+                w.bidx[gpos] = x;
+            }
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] += lcount[i];
+        for (uint32_t i = threadIdx.x; i < nb; i += T)
+            cursor[i] += (heavy_tile && lcount[i] > heavy_at) ? hcnt[i] : lcount[i];
         __syncthreads();
+    }
+    for (uint32_t i = threadIdx.x; i < nb; i += T) w.seg_end[(uint64_t)fb * nb + i] = cursor[i];
+}
+
+// Spilled records (sub-bin full) into the table with the direct insert, after the aggregate; a slot
+// claimed here is added to its region's occupancy (ss_counter_pack_ranges reads it).
+__global__ __launch_bounds__(256) void k_spill_insert(Tbl t, PartWs w, const uint32_t* __restrict__ fill,
+                                                      uint64_t base_index) {
+    const uint64_t m = min((uint64_t)fill[fill_at(kSpillCtr)], w.spill_cap);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+        const uint4 r = w.spill[i];
+        const uint64_t k = ((uint64_t)r.y << 32) | r.x;
+        if (tbl_add(t, k, r.z, base_index + r.w) && t.occ && k != kEmpty) atomicAdd(&t.occ[region_of(t, k)], 1u);
     }
 }
 
@@ -1021,27 +1335,21 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
 #endif
 constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools/tune_counter.hip)
 
+
 // P4, slice-direct form: the region's slice itself is the LDS hash table.  Keys are copied into LDS
 // (16 KB for 2048 slots) next to two per-batch u32 arrays (count, first read index); every bucket
 // element probes the slice from its home slot (a new key claims an EMPTY slot with one LDS CAS),
 // then one LDS add and one LDS min.  The whole slice is written back coalesced (key, count, first
-// combined with the slot's old values).  32 KB of LDS per workgroup instead of 80 KB, one phase.
+// combined with the slot's old values; one dwordx4 per slot).  32 KB of LDS per workgroup.
+// Skewed regions: the fine scatter's dedup leaves at most ~one record per (tile, hot key), and
+// weighted records carry their counts (one LDS add of c); SS_AGG_FOLD > 0 would also fold lanes that
+// share a key before the LDS atomics (measured slower, see wave_fold).
 // fresh: the table was reset and the reset is still pending (ss_counter_reset is lazy): the slice is
 // taken as empty instead of loaded, and written back whole (empty slots as the 0xFF reset pattern),
-// which replaces the 1-GB reset memset and the slice read.  With skip_if set (the optimistic
-// partition overflowed) a fresh aggregate only performs its slice's reset.
+// which replaces the table-sized reset memset and the slice read.
 template <int T>
-__global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index,
-                                                          const uint32_t* skip_if = nullptr, bool fresh = false) {
+__global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index, bool fresh = false) {
     const uint32_t S = (uint32_t)t.slice_mask + 1;
-    if (skip_if && *skip_if) {
-        if (fresh) {
-            uint4* sl = (uint4*)&t.slots[(uint64_t)blockIdx.x << t.slice_log];
-            const uint4 ff = make_uint4(~0u, ~0u, ~0u, ~0u);
-            for (uint32_t i = threadIdx.x; i < 2 * S; i += T) sl[i] = ff;
-        }
-        return;
-    }
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* skey = (unsigned long long*)smem;   // [S]
     uint32_t* bcnt = (uint32_t*)(skey + S);                   // [S] this batch's count
@@ -1060,25 +1368,72 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         sent[2] = 0;
     }
     __syncthreads();
-    const uint32_t b0 = w.rstart[region], b1 = w.rstart[region + 1];
     constexpr int kP = 4;
-    for (uint32_t e0 = b0; e0 < b1; e0 += kP * T) {
-        uint64_t key[kP];
-        uint32_t idx[kP];
+    // the region's records: one range (exact paths) or its kFinePerBin fine-scatter segments,
+    // walked as one flat index space (segment s covers flat [pre[s], pre[s + 1])) so every
+    // iteration issues kP loads per thread whatever the segment lengths
+    static_assert(kFinePerBin <= 16, "segment table");
+    uint32_t seg0[kFinePerBin], pre[kFinePerBin + 1];
+    pre[0] = 0;
+    if (w.seg_end) {
+        const uint32_t rpb = 1u << (w.rbits - kCoarseBits);
 #pragma unroll
-        for (int q = 0; q < kP; ++q) {
-            const uint32_t e = e0 + q * T + threadIdx.x;
-            key[q] = e < b1 ? w.bkey[e] : kEmpty;
-            idx[q] = e < b1 ? w.bidx[e] : 0xFFFFFFFFu;
+        for (uint32_t sg = 0; sg < kFinePerBin; ++sg) {
+            const uint64_t at = (uint64_t)((region / rpb) * kFinePerBin + sg) * rpb + region % rpb;
+            seg0[sg] = w.hist[at];
+            pre[sg + 1] = pre[sg] + (w.seg_end[at] - seg0[sg]);
         }
+    } else {
+        seg0[0] = w.rstart[region];
+#pragma unroll
+        for (uint32_t sg = 0; sg < kFinePerBin; ++sg) pre[sg + 1] = w.rstart[region + 1] - seg0[0];
+    }
+    const uint32_t total = pre[kFinePerBin];
+    auto flat_at = [&](uint32_t f) -> uint32_t {   // element index of flat position f < total
+        uint32_t e = seg0[0] + f;
+#pragma unroll
+        for (uint32_t sg = 1; sg < kFinePerBin; ++sg)
+            if (f >= pre[sg]) e = seg0[sg] + (f - pre[sg]);
+        return e;
+    };
+    // software-pipelined: the next step's loads are in flight while this step's records are folded
+    uint64_t nkey[kP];
+    uint32_t nidx[kP], nel[kP];
+    auto load_step = [&](uint32_t e0) {
 #pragma unroll
         for (int q = 0; q < kP; ++q) {
-            if (idx[q] == 0xFFFFFFFFu && key[q] == kEmpty) continue;   // past the bucket
-            if (key[q] == kEmpty) {
-                atomicAdd(&sent[0], 1u);
-                atomicMin(&sent[1], idx[q]);
-                continue;
+            const uint32_t f = e0 + q * T + threadIdx.x;
+            nel[q] = f < total ? flat_at(f) : 0u;
+            nkey[q] = f < total ? w.bkey[nel[q]] : kEmpty;
+            nidx[q] = f < total ? w.bidx[nel[q]] : 0u;
+        }
+    };
+    if (total) load_step(0);
+    for (uint32_t e0 = 0; e0 < total; e0 += kP * T) {
+        uint64_t key[kP];
+        uint32_t idx[kP], el[kP];
+#pragma unroll
+        for (int q = 0; q < kP; ++q) {
+            key[q] = nkey[q];
+            idx[q] = nidx[q];
+            el[q] = nel[q];
+        }
+        if (e0 + kP * T < total) load_step(e0 + kP * T);
+#pragma unroll
+        for (int q = 0; q < kP; ++q) {
+            const bool valid = e0 + q * T + threadIdx.x < total;
+            uint32_t c = 1, ix = idx[q];
+            if (valid && (ix & kWeighted)) {
+                c = w.bcnt[el[q]];
+                ix &= ~kWeighted;
             }
+            if (valid && key[q] == kEmpty) {
+                atomicAdd(&sent[0], c);
+                atomicMin(&sent[1], ix);
+            }
+            bool act = valid && key[q] != kEmpty;
+            wave_fold<SS_AGG_FOLD>(act, key[q], c, ix);
+            if (!act) continue;
             uint32_t off = (uint32_t)(slot_top(t, key[q]) & t.slice_mask);
             uint32_t probe = 0;
             for (; probe < S; ++probe) {
@@ -1092,39 +1447,28 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
                 off = (off + 1) & (uint32_t)t.slice_mask;
             }
             if (probe == S) {
-                atomicOr(t.overflow, 1ull);
+                atomicOr(t.overflow, kOvfTable);
                 continue;
             }
-            atomicAdd(&bcnt[off], 1u);
-            atomicMin(&bfst[off], idx[q]);
+            atomicAdd(&bcnt[off], c);
+            atomicMin(&bfst[off], ix);
         }
     }
     __syncthreads();
     uint32_t used = 0;
-    if (fresh) {   // whole slots, two dwordx4 stores each (lane pairs cover one 32-B slot)
-        uint4* sl = (uint4*)&t.slots[slice_base];
-        for (uint32_t h = threadIdx.x; h < 2 * S; h += T) {
-            const uint32_t i = h >> 1;
-            const bool hit = bcnt[i] != 0;
-            if ((h & 1u) == 0) {
-                used += skey[i] != kEmpty ? 1u : 0u;
-                const unsigned long long k = skey[i], nc = ~(unsigned long long)bcnt[i];
-                sl[h] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)nc, (uint32_t)(nc >> 32));
-            } else {
-                const unsigned long long f = hit ? base_index + bfst[i] : ~0ull;
-                sl[h] = make_uint4((uint32_t)f, (uint32_t)(f >> 32), ~0u, ~0u);
-            }
+    uint4* sl = (uint4*)&t.slots[slice_base];
+    for (uint32_t i = threadIdx.x; i < S; i += T) {
+        const unsigned long long k = skey[i];
+        used += k != kEmpty ? 1u : 0u;
+        const uint32_t bc = bcnt[i];
+        if (fresh) {   // every slot, one dwordx4 each (empty slots as the reset pattern)
+            sl[i] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), ~bc,
+                               bc ? (uint32_t)(base_index + bfst[i]) : kNoFirst);
+        } else if (bc) {
+            const uint4 old = sl[i];
+            const uint32_t f = (uint32_t)(base_index + bfst[i]);
+            sl[i] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), old.z - bc, f < old.w ? f : old.w);
         }
-    }
-    for (uint32_t i = threadIdx.x; !fresh && i < S; i += T) {
-        used += skey[i] != kEmpty ? 1u : 0u;
-        if (!bcnt[i]) continue;
-        Slot* sl = &t.slots[slice_base + i];
-        const unsigned long long nc = sl->ncount, fs = sl->first;
-        const unsigned long long f = base_index + bfst[i];
-        sl->key = skey[i];
-        sl->ncount = nc - bcnt[i];
-        sl->first = f < fs ? f : fs;
     }
     if (t.occ) {   // the slice's occupancy after this batch (ss_counter_pack_ranges)
         if (used) atomicAdd(&sent[2], used);
@@ -1132,9 +1476,9 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         if (threadIdx.x == 0) t.occ[region] = sent[2];
     }
     if (threadIdx.x == 0 && sent[0]) {
-        Slot* sl = &t.slots[t.mask + 1];
-        atomicAdd(&sl->ncount, 0ull - (unsigned long long)sent[0]);
-        atomicMin(&sl->first, base_index + sent[1]);
+        Slot* ss = &t.slots[t.mask + 1];
+        atomicAdd(&ss->ncount, 0u - sent[0]);
+        atomicMin(&ss->first, (uint32_t)(base_index + sent[1]));
     }
 }
 
@@ -1215,15 +1559,16 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t S = (uint32_t)t.slice_mask + 1;
     unsigned long long* skey = (unsigned long long*)smem;     // [S]
-    unsigned long long* scnt = skey + S;                       // [S] counts (not complemented)
-    unsigned long long* sfst = scnt + S;                       // [S]
+    uint32_t* scnt = (uint32_t*)(skey + S);                    // [S] counts (not complemented)
+    uint32_t* sfst = scnt + S;                                 // [S]
     const uint32_t j = blockIdx.x;                             // owned region reg_lo + j
     const uint64_t base = (uint64_t)(reg_lo + j) << t.slice_log;
+    uint4* sl = (uint4*)&t.slots[base];
     for (uint32_t q = threadIdx.x; q < S; q += kMergeT) {
-        const Slot& sl = t.slots[base + q];
-        skey[q] = sl.key;
-        scnt[q] = ~sl.ncount;
-        sfst[q] = sl.first;
+        const uint4 v = sl[q];
+        skey[q] = ((uint64_t)v.y << 32) | v.x;
+        scnt[q] = ~v.z;
+        sfst[q] = v.w;
     }
     __syncthreads();
     for (uint32_t run = 0; run < n_runs; ++run) {
@@ -1248,19 +1593,18 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
                 off = (off + 1) & (uint32_t)t.slice_mask;
             }
             if (probe == S) {
-                atomicOr(t.overflow, 1ull);
+                atomicOr(t.overflow, kOvfTable);
                 continue;
             }
-            atomicAdd(&scnt[off], c);
-            atomicMin(&sfst[off], f);
+            if ((c >> 32) || f > kMaxIndex) atomicOr(t.overflow, f > kMaxIndex ? kOvfIndex : kOvfField);
+            atomicAdd(&scnt[off], (uint32_t)c);
+            atomicMin(&sfst[off], (uint32_t)min((unsigned long long)kMaxIndex, f));
         }
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < S; q += kMergeT) {
-        Slot* sl = &t.slots[base + q];
-        sl->key = skey[q];
-        sl->ncount = ~scnt[q];
-        sl->first = sfst[q];
+        const unsigned long long k = skey[q];
+        sl[q] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), ~scnt[q], sfst[q]);
     }
 }
 
@@ -1275,8 +1619,9 @@ __global__ void k_merge_sentinel(Tbl t, Recs recs, const uint64_t* run_off, uint
             unsigned long long c, f;
             recs.load(end - 1, run, k, c, f);
             Slot* sl = &t.slots[t.mask + 1];
-            atomicAdd(&sl->ncount, 0ull - c);
-            atomicMin(&sl->first, f);
+            if ((c >> 32) || f > kMaxIndex) atomicOr(t.overflow, f > kMaxIndex ? kOvfIndex : kOvfField);
+            atomicAdd(&sl->ncount, 0u - (uint32_t)c);
+            atomicMin(&sl->first, (uint32_t)min((unsigned long long)kMaxIndex, f));
         }
     }
 }
@@ -1297,8 +1642,7 @@ __device__ __forceinline__ uint32_t part_of_region(uint64_t region, uint64_t R, 
     return (uint32_t)(region * nparts / R);
 }
 
-__global__ __launch_bounds__(kPackT) void k_region_occ(Tbl t, const uint32_t* skip_if) {
-    if (skip_if && *skip_if == 0) return;          // the aggregate's occupancy is valid
+__global__ __launch_bounds__(kPackT) void k_region_occ(Tbl t) {
     __shared__ uint32_t sum;
     if (threadIdx.x == 0) sum = 0;
     __syncthreads();
@@ -1363,12 +1707,12 @@ __global__ __launch_bounds__(kPackT) void k_region_pack(Tbl t, uint32_t R, uint3
     __shared__ unsigned long long cursor;
     if (r == 0 && threadIdx.x == 0 && roff[R] != ~0ull) {   // the sentinel record
         const Slot& sl = t.slots[t.mask + 1];
-        const unsigned long long c = ~sl.ncount, f = sl.first - first_base;
-        if (c >> 32 || f >> 32 || sl.first < first_base) atomicOr(flags, 4ull);
+        const unsigned long long c = (uint32_t)~sl.ncount, f = sl.first - first_base;
+        if (f >> 32 || sl.first < first_base) atomicOr(flags, kOvfField);
         if (roff[R] < cap)
             rec[roff[R]] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, (uint32_t)c, (uint32_t)f);
         else
-            atomicOr(flags, 2ull);
+            atomicOr(flags, kOvfExtract);
     }
     if ((int32_t)part_of_region(r, R, nparts) == skip) return;
     if (threadIdx.x == 0) cursor = roff[r];
@@ -1376,33 +1720,25 @@ __global__ __launch_bounds__(kPackT) void k_region_pack(Tbl t, uint32_t R, uint3
     const uint32_t S = (uint32_t)t.slice_mask + 1;
     const uint64_t base = (uint64_t)r << t.slice_log;
     constexpr int kU = 4;
+    const uint4* slots = (const uint4*)&t.slots[base];
     for (uint32_t i0 = 0; i0 < S; i0 += kU * kPackT) {
         uint4 a[kU];
-        uint64_t fs[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const uint32_t i = i0 + u * kPackT + threadIdx.x;
-            if (i < S) {
-                const uint4* p = (const uint4*)&t.slots[base + i];
-                a[u] = p[0];
-                fs[u] = t.slots[base + i].first;
-            } else {
-                a[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-                fs[u] = 0;
-            }
+            a[u] = i < S ? slots[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const bool used = !(a[u].x == 0xFFFFFFFFu && a[u].y == 0xFFFFFFFFu);
             const unsigned long long pos = wave_reserve(used, 0u, &cursor);
             if (!used) continue;
-            const unsigned long long c = ~(((unsigned long long)a[u].w << 32) | a[u].z);
-            const unsigned long long f = fs[u] - first_base;
-            if (c >> 32 || f >> 32 || fs[u] < first_base) atomicOr(flags, 4ull);
+            const uint32_t c = ~a[u].z;
+            if (a[u].w < first_base) atomicOr(flags, kOvfField);
             if (pos < cap)
-                rec[pos] = make_uint4(a[u].x, a[u].y, (uint32_t)c, (uint32_t)f);
+                rec[pos] = make_uint4(a[u].x, a[u].y, c, (uint32_t)(a[u].w - first_base));
             else
-                atomicOr(flags, 2ull);
+                atomicOr(flags, kOvfExtract);
         }
     }
 }
@@ -1541,7 +1877,7 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
             }
             off = (off + 1) & (uint32_t)t.slice_mask;
         }
-        if (slot[j] == 0xFFFFFFFFu) atomicOr(t.overflow, 1ull);
+        if (slot[j] == 0xFFFFFFFFu) atomicOr(t.overflow, kOvfTable);
     }
     // phase 3: slot read-modify-writes (the workgroup owns the slice) and key words of new slots
 #pragma unroll
@@ -1555,11 +1891,11 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
             uint64_t* dst = t.keywords + (slice_base + slot[j]) * W;
             for (uint32_t q = 0; q < W; ++q) dst[q] = kw[q];
             sl->key = fps[j];
-            sl->ncount = ~(unsigned long long)lcnt[ls];
-            sl->first = f;
+            sl->ncount = ~lcnt[ls];
+            sl->first = (uint32_t)f;
         } else {
             sl->ncount -= lcnt[ls];
-            if (f < sl->first) sl->first = f;
+            if ((uint32_t)f < sl->first) sl->first = (uint32_t)f;
         }
     }
 }
@@ -1601,7 +1937,7 @@ int launch_merge(ss_counter* c, Recs recs, const uint64_t* d_run_offsets, uint32
     hipLaunchKernelGGL((k_run_bounds<Recs>), dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, t, recs,
                        d_run_offsets, n_runs, reg_lo, nreg, d_bounds);
     if (nreg) {
-        const size_t lds = (size_t)3 * ((size_t)1 << c->slice_log) * 8;
+        const size_t lds = ((size_t)1 << c->slice_log) * 16;
         hipLaunchKernelGGL((k_merge_runs<Recs>), dim3(nreg), dim3(kMergeT), lds, s, t, recs, d_run_offsets, n_runs,
                            reg_lo, nreg, (const uint32_t*)d_bounds);
     }
@@ -1658,6 +1994,8 @@ int ss_counter_destroy(ss_counter* c) {
     ss_counter_release(c);
     if (c->ws_hist) (void)hipFree(c->ws_hist);
     if (c->ws_rstart) (void)hipFree(c->ws_rstart);
+    if (c->ws_segend) (void)hipFree(c->ws_segend);
+    if (c->ws_order) (void)hipFree(c->ws_order);
     if (c->ws_tot) (void)hipFree(c->ws_tot);
     if (c->ws_fill) (void)hipFree(c->ws_fill);
     delete c;
@@ -1703,21 +2041,27 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     if (!c) return ss_fail(SS_EARG, "null counter");
     const uint64_t R = c->cap >> c->slice_log;
     if (R > kMaxRegions) return ss_fail(SS_EARG, "capacity too large for the partitioned insert");
-    if (max_reads >= (1ull << 32)) return ss_fail(SS_EARG, "max_reads must be < 2^32 per insert");
+    if (max_reads >= (1ull << 31)) return ss_fail(SS_EARG, "max_reads must be < 2^31 per insert");
     if (max_reads <= c->ws_reads) return SS_OK;
     ss_counter_release(c);
     // coarse arrays: room for the exact passes (max_reads) and for the optimistic partition's
-    // 128 x 8 sub-bins of cap1 = 1.25 x the mean sub-bin load + 1024 slots
-    const uint64_t cap1 = (max_reads + max_reads / 4 + kNFill - 1) / kNFill + 8192 / kFinePerBin;
+    // 128 x 8 sub-bins of cap1 = 2.5 x the mean sub-bin load + 1024 slots (pf_cap1)
+    const uint64_t cap1 = pf_cap1(max_reads);
     const uint64_t acap = kNFill * cap1 > max_reads ? kNFill * cap1 : max_reads;
     hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_acnt, acap * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, kFillWords * sizeof(uint32_t));
     c->ws_cap1 = cap1;
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bcnt, max_reads * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_spill, max_reads * sizeof(uint4));
     if (e == hipSuccess && !c->ws_hist) e = hipMalloc((void**)&c->ws_hist, (size_t)kPartBlocks * R * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_rstart) e = hipMalloc((void**)&c->ws_rstart, (R + 1) * sizeof(uint32_t));
+    // one entry per (sub-bin, region of its bin): kNFill x (R / 128) = R x kFinePerBin
+    if (e == hipSuccess && !c->ws_order) e = hipMalloc((void**)&c->ws_order, kNFill * sizeof(uint32_t));
+    if (e == hipSuccess && !c->ws_segend) e = hipMalloc((void**)&c->ws_segend, R * kFinePerBin * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_tot) e = hipMalloc((void**)&c->ws_tot, (R + 1) * sizeof(uint32_t));
     if (e != hipSuccess) {
         ss_counter_release(c);
@@ -1735,14 +2079,20 @@ int ss_counter_release(ss_counter* c) {
     if (c->ws_keys) (void)hipFree(c->ws_keys);
     if (c->ws_akey) (void)hipFree(c->ws_akey);
     if (c->ws_aidx) (void)hipFree(c->ws_aidx);
+    if (c->ws_acnt) (void)hipFree(c->ws_acnt);
     if (c->ws_bidx) (void)hipFree(c->ws_bidx);
+    if (c->ws_bcnt) (void)hipFree(c->ws_bcnt);
+    if (c->ws_spill) (void)hipFree(c->ws_spill);
     if (c->ws_words) (void)hipFree(c->ws_words);
     c->ws_words = nullptr;
     c->ws_words_cap = 0;
     c->ws_keys = nullptr;
     c->ws_akey = nullptr;
     c->ws_aidx = nullptr;
+    c->ws_acnt = nullptr;
     c->ws_bidx = nullptr;
+    c->ws_bcnt = nullptr;
+    c->ws_spill = nullptr;
     c->ws_reads = 0;
     return SS_OK;
 }
@@ -1758,6 +2108,8 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
     rc = ss_check(hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s), "reset first_bad");
     if (rc || n == 0) return rc;
     if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
+    if (base_index > kMaxIndex || n - 1 > kMaxIndex - base_index)
+        return ss_fail(SS_EARG, "global read indices of a counter handle must stay below 2^32 - 1");
     c->occ_src = 0;   // set again below by the paths whose aggregate records the region occupancy
     Tbl t = tbl_of(c);
     const bool multi = c->W > 1;
@@ -1800,7 +2152,12 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         w.keys = c->ws_keys;
         w.akey = c->ws_akey;
         w.aidx = c->ws_aidx;
+        w.acnt = c->ws_acnt;
         w.bidx = c->ws_bidx;
+        w.bcnt = c->ws_bcnt;
+        w.spill = c->ws_spill;
+        w.spill_cap = c->ws_reads;
+        w.seg_end = nullptr;
         w.hist = c->ws_hist;
         w.rstart = c->ws_rstart;
         w.tot = c->ws_tot;
@@ -1857,24 +2214,23 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
                                (unsigned long long*)d_first_bad);
             const unsigned fine_blocks = kCB * kFinePerBin;
-            const uint32_t* ovf = (const uint32_t*)(c->ws_fill + fill_at(kOvf));
             hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill);
             const unsigned rg = (w.R + 255) / 256;
-            hipLaunchKernelGGL(k_pf_tot, dim3(rg), dim3(256), 0, s, w, (const uint32_t*)c->ws_fill);
-            hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, w.R, w.rstart, ovf);
-            hipLaunchKernelGGL(k_pf_offsets, dim3(rg), dim3(256), 0, s, w, (const uint32_t*)c->ws_fill);
+            hipLaunchKernelGGL(k_pf_tot, dim3(rg), dim3(256), 0, s, w);
+            hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, w.R, w.rstart, (const uint32_t*)nullptr);
+            hipLaunchKernelGGL(k_pf_offsets, dim3(rg), dim3(256), 0, s, w);
+            w.seg_end = c->ws_segend;
+            hipLaunchKernelGGL(k_pf_order, dim3(1), dim3(512), 0, s, (const uint32_t*)c->ws_fill, cap1, c->ws_order);
             hipLaunchKernelGGL(k_pf_scatter, dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
-                               (const uint32_t*)c->ws_fill);
+                               (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
             w.bkey = w.keys;
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
-                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, ovf, fresh);
-            // overflow (a bin past cap1): the passes above idled; insert the batch directly
-            constexpr int U = 4;
-            const unsigned grid = grid_for(2 * n, (uint64_t)U * kThreads, 256 * 16);
-            hipLaunchKernelGGL((k_count_g16<U>), dim3(grid), dim3(kThreads), 0, s, t, (const uint4*)d_ascii,
-                               stride / 16, n, L / 16, base_index, (unsigned long long*)d_first_bad, ovf);
-            c->occ_src = 2;   // valid unless the fallback ran (ws_fill overflow flag set)
+                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
+            // records that found their sub-bin full (none unless many distinct keys pile into a bin)
+            hipLaunchKernelGGL(k_spill_insert, dim3(1024), dim3(256), 0, s, t, w, (const uint32_t*)c->ws_fill,
+                               base_index);
+            c->occ_src = 1;
             return ss_check(hipGetLastError(), "optimistic partitioned insert");
         }
         if (multi) {
@@ -1909,8 +2265,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint64_t*)c->ws_words, base_index);
         else
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
-                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, (const uint32_t*)nullptr,
-                               fresh);
+                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
         if (!multi) c->occ_src = 1;
         return ss_check(hipGetLastError(), "partitioned insert");
     }
@@ -2042,9 +2397,7 @@ int ss_counter_pack_ranges(ss_counter* c, uint32_t n_parts, int32_t skip_part, u
     if (rc) return rc;
     Tbl t = tbl_of(c);
     const uint32_t R = (uint32_t)c->occ_R;
-    if (c->occ_src != 1)
-        hipLaunchKernelGGL(k_region_occ, dim3(R), dim3(kPackT), 0, s, t,
-                           c->occ_src == 2 ? (const uint32_t*)(c->ws_fill + fill_at(kOvf)) : (const uint32_t*)nullptr);
+    if (c->occ_src != 1) hipLaunchKernelGGL(k_region_occ, dim3(R), dim3(kPackT), 0, s, t);
     hipLaunchKernelGGL(k_region_scan, dim3(1), dim3(1024), 0, s, t, R, n_parts, skip_part, c->roff,
                        (unsigned long long*)d_part_counts);
     hipLaunchKernelGGL(k_region_pack, dim3(R), dim3(kPackT), 0, s, t, R, n_parts, skip_part,

@@ -140,3 +140,39 @@ def test_fuzz_against_reference_kernels(oracle):
         ora, rc, _ = oracle.encode_batch(a, n, L)
         assert rc == 0
         assert np.array_equal(ref, ora), L
+
+
+def test_pool_counter_table_matches_reference_digest(oracle, digests):
+    """The generator-derived counter (keys from the pool generator, counts = bincount of the draw
+    indices, first = first draw; what tests/golden/c5_digests.json is built from) reproduces the
+    reference ShortSeqCounter's own digest of the 1M x 32 pool-65536 list (dict order = first draw)."""
+    d = digests["counter_1000000x32_pool65536"]
+    k, c, f = oracle.pool_counter_table(d["seed"], d["pool_seed"], d["U"], d["n"], d["L"])
+    assert len(k) == d["unique"] and int(c.max()) == d["max_count"]
+    o = np.argsort(f, kind="stable")
+    ordered = np.stack([k[o], np.full(len(k), d["L"], np.uint64), c[o]], 1).astype(np.uint64)
+    assert _sha(ordered) == d["ordered_sha256"]
+
+
+@pytest.mark.parametrize("s", [None, 1.1])
+def test_pool_counter_table_matches_oracle_count(oracle, s):
+    """Uniform and Zipf pools: the vectorised construction equals oracle.count over the same reads,
+    at shard offsets, so the full-shard C5 digests (tests/test_c5_full.py) are pinned to the oracle."""
+    U, n, i0 = 1 << 13, 300_000, 123_456_789
+    cdf = None
+    if s:
+        w = np.arange(1, U + 1, dtype=np.float64) ** -s
+        cc = np.cumsum(w) / w.sum()
+        cdf = np.floor(cc * 2.0 ** 63).astype(np.uint64)
+        cdf[-1] = np.uint64(1 << 63)
+        a = oracle.gen_zipf_reads(5, 77, cdf, i0, n, 32)
+        assert np.array_equal(oracle.pool_ids(77, i0, 64, U, cdf),
+                              [oracle.lib().ora_zipf_index(77, i0 + j, cdf.ctypes.data, U) for j in range(64)])
+    else:
+        a = oracle.gen_pool_reads(5, 77, U, i0, n, 32)
+    exp = oracle.count([a[i * 32:(i + 1) * 32].tobytes() for i in range(n)])
+    k, c, f = oracle.pool_counter_table(5, 77, U, n, 32, i0=i0, cdf=cdf, chunk=1 << 16)
+    ek = np.array([w[0] for (w, _l, _c, _f) in exp], np.uint64)
+    ec = np.array([x[2] for x in exp], np.uint64)
+    ef = np.array([x[3] for x in exp], np.uint64) + np.uint64(i0)
+    assert oracle.table_digest(k, c, f) == oracle.table_digest(ek, ec, ef)

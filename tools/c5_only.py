@@ -1,5 +1,8 @@
 #!/usr/bin/env python3
-"""Run only the C5 counter step (bench.py's bench_counter) for profiling."""
+"""Run only the C5 counter step (bench.py's bench_counter) for profiling.
+
+    python3 tools/c5_only.py [U_log2=24] [zipf_s=0 (uniform)] [steps=10]
+"""
 import os
 import sys
 
@@ -10,29 +13,10 @@ import bench  # noqa: E402
 import shortseq_amd.batch as B  # noqa: E402
 from shortseq_amd._native import lib  # noqa: E402
 
+ulog = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+zs = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-el, d, u = bench.bench_counter(B, lib(), dev, 0, 1, 125_000_000, 32, 1 << 24, 10, 3)
-print(f"C5: {el / 10 * 1e3:.3f} ms/step wall, {d:.3f} ms device, unique {u}")
-
-# A/B in the same process: lazy reset (fresh aggregate) vs an eager reset (memset + slice read)
-from shortseq_amd.dist import ShardedCounter  # noqa: E402
-ascii = B.synth_pool_reads(125_000_000, 32, 5, 77, 1 << 24, device=dev)
-sc = ShardedCounter(1 << 25, device=dev)
-t = sc.local
-for name in ("lazy", "eager", "lazy", "eager"):
-    def step():
-        t.reset()
-        if name == "eager":
-            t.size()                 # flushes the pending reset: memset, then a non-fresh insert
-        t.insert(ascii, 32, base_index=0, check_errors=False)
-    for _ in range(3):
-        step()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        step()
-    e1.record()
-    torch.cuda.synchronize()
-    print(f"{name}: {e0.elapsed_time(e1) / 10:.3f} ms/step (device)", flush=True)
+el, d, u = bench.bench_counter(B, lib(), dev, 0, 1, 125_000_000, 32, 1 << ulog, steps, 3, zipf=zs or None)
+print(f"C5 U=2^{ulog} zipf={zs}: {el / steps * 1e3:.3f} ms/step wall, {d:.3f} ms device, unique {u}", flush=True)

@@ -9,22 +9,44 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 #define CS(x) do { int r_ = (x); if (r_) { printf("ss error %d: %s @%d\n", r_, ss_last_error_string(), __LINE__); exit(1); } } while (0)
 
 int main(int argc, char** argv) {
+    // tune_counter [n=125M] [reps=10] [U_log2=24] [zipf_s=0 (uniform)]
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 125000000ull;
     const int reps = argc > 2 ? atoi(argv[2]) : 10;
+    const int ulog = argc > 3 ? atoi(argv[3]) : 24;
+    const double zs = argc > 4 ? atof(argv[4]) : 0.0;
+    const uint64_t U = 1ull << ulog;
     const uint32_t L = 32;
     uint8_t* ascii;
     uint64_t *fb, *size;
     CK(hipMalloc(&ascii, n * L));
     CK(hipMalloc(&fb, 8));
     CK(hipMalloc(&size, 8));
-    CS(ss_synth_pool_reads(ascii, 5, 77, 1ull << 24, 0, n, L, L, nullptr));
+    if (zs > 0) {   // the table of shortseq_amd.batch.zipf_cdf
+        uint64_t* h = (uint64_t*)malloc(U * 8);
+        double* c = (double*)malloc(U * 8);
+        double acc = 0;
+        for (uint64_t k = 0; k < U; ++k) c[k] = (acc += pow((double)(k + 1), -zs));
+        for (uint64_t k = 0; k < U; ++k) h[k] = (uint64_t)floor(c[k] / acc * 9223372036854775808.0);
+        h[U - 1] = 1ull << 63;
+        uint64_t* d;
+        CK(hipMalloc(&d, U * 8));
+        CK(hipMemcpy(d, h, U * 8, hipMemcpyHostToDevice));
+        CS(ss_synth_zipf_reads(ascii, 5, 77, d, U, 0, n, L, L, nullptr));
+        CK(hipDeviceSynchronize());
+        CK(hipFree(d));
+        free(h);
+        free(c);
+    } else {
+        CS(ss_synth_pool_reads(ascii, 5, 77, U, 0, n, L, L, nullptr));
+    }
     ss_counter* c;
-    CS(ss_counter_create(1ull << 25, &c));
+    CS(ss_counter_create(2 * U, &c));
     CS(ss_counter_reserve(c, n));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -47,7 +69,7 @@ int main(int argc, char** argv) {
     uint64_t hs, hfb;
     CK(hipMemcpy(&hs, size, 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(&hfb, fb, 8, hipMemcpyDeviceToHost));
-    printf("tile %d: insert avg %.3f ms min %.3f ms  (%.1f G reads/s)  unique %llu first_bad %llx\n", (int)SS_PC_TILE,
+    printf("U=2^%d zipf=%.2f: insert avg %.3f ms min %.3f ms  (%.1f G reads/s)  unique %llu first_bad %llx\n", ulog, zs,
            tot / reps, mn, n / (tot / reps) / 1e6, (unsigned long long)hs, (unsigned long long)hfb);
     return 0;
 }
