@@ -1,7 +1,14 @@
+#!/usr/bin/env bash
+# C5 counter PMC passes (one counter group per rocprofv3 run) over tools/c5_only.py (uniform 2^24),
+# summarised by tools/pmc_c5_summary.py.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_c5/fetch -o run --output-format csv -- python3 tools/c5_only.py > gpurun_out/pmc_c5_fetch.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_c5/write -o run --output-format csv -- python3 tools/c5_only.py > gpurun_out/pmc_c5_write.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR -d gpurun_out/pmc_c5/sq -o run --output-format csv -- python3 tools/c5_only.py > gpurun_out/pmc_c5_sq.log 2>&1 || exit 1
+P=gpurun_out/pmc_c5
+run() { name=$1; shift; timeout -s KILL 90 rocprofv3 --pmc "$@" -d $P/$name -o run --output-format csv -- python3 tools/c5_only.py 24 0 3 > $P.$name.log 2>&1 || { echo "pass $name failed"; exit 1; }; }
+mkdir -p $P
+run fetch FETCH_SIZE
+run write WRITE_SIZE
+run sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR
+run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
 echo DONE

@@ -63,6 +63,7 @@ struct ss_counter {
     uint64_t* ws_akey = nullptr;           // [ws_reads] keys bucketed by coarse bin
     uint32_t* ws_aidx = nullptr;           // [ws_reads] batch-local read index, same order
     uint32_t* ws_acnt = nullptr;           // weighted records' counts, coarse order (same size as ws_aidx)
+    uint8_t* ws_areg = nullptr;            // region-in-bin byte per coarse record (same size as ws_aidx)
     uint32_t* ws_bidx = nullptr;           // [ws_reads] batch-local read index, region order
     uint32_t* ws_bcnt = nullptr;           // [ws_reads] weighted records' counts, region order
     uint4* ws_spill = nullptr;             // [ws_reads] records past a full sub-bin
@@ -431,6 +432,7 @@ struct PartWs {
     uint64_t* akey;    // first-pass output (bucketed by coarse bin)
     uint32_t* aidx;
     uint32_t* acnt;    // weighted records' counts, coarse order (sparse: weighted positions only)
+    uint8_t* areg;     // optimistic path: each coarse record's region within its bin (k_pf_count)
     uint32_t* bidx;    // second-pass output indices
     uint32_t* bcnt;    // weighted records' counts, region order (sparse)
     uint4* spill;      // records past a full sub-bin: {key lo, key hi, count, batch index}
@@ -813,10 +815,13 @@ __host__ __device__ __forceinline__ uint32_t fill_at(uint32_t b) { return b * kF
 #endif
 constexpr uint32_t kPfT = SS_PF_T, kPfRPL = SS_PF_RPL;   // k_pf_coarse: kPfT * kPfRPL-read tiles
 constexpr uint32_t kHeavy = SS_PF_HEAVY;
+#ifndef SS_PF_DET
+#define SS_PF_DET 0
+#endif
 
 // sub-bin capacity of the optimistic partition for a batch of n reads (host and device agree)
 __host__ __device__ __forceinline__ uint64_t pf_cap1(uint64_t n) {
-    return (5 * n / 2 + kNFill - 1) / kNFill + 1024;
+    return ((5 * n / 2 + kNFill - 1) / kNFill + 1024 + 15) & ~15ull;   // x16: k_pf_count's dwordx4 loads
 }
 
 // 64-bit lane broadcast
@@ -912,7 +917,12 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
     };
     // wave 0, one bin: reserve c slots of sub-bin (b, sub); the part past cap1 reserves spill records
     auto reserve = [&](uint32_t b, uint32_t c) {
+#if SS_PF_DET   // measurement only: tile-local positions, no reservation atomics (results invalid)
+        const uint32_t g = 0;
+        (void)c;
+#else
         const uint32_t g = c ? atomicAdd(&fill[fill_at(b * kFinePerBin + sub)], c) : 0u;
+#endif
         gbase[b] = g;
         const uint64_t end = (uint64_t)g + c, from = max((uint64_t)g, cap1);
         sbase[b] = end > from ? atomicAdd(spill_ctr, (uint32_t)(end - from)) : 0u;
@@ -1046,8 +1056,13 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             const uint64_t pos = (uint64_t)gbase[b] + local;
             const uint64_t k = skey[i];
             if (pos < cap1) {
+#if SS_PF_DET
+                const uint64_t at = t0 + lstart[b] + local;
+#else
                 const uint64_t at = (uint64_t)(b * kFinePerBin + sub) * cap1 + pos;
+#endif
                 w.akey[at] = k;
+                w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
                 if (c > 1) {
                     w.aidx[at] = sidx[i] | kWeighted;
                     w.acnt[at] = c;
@@ -1083,9 +1098,17 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
     fine_range(blockIdx.x, fill, cap1, bin, lo, hi);
     for (uint32_t i = threadIdx.x; i < rpb; i += T) h[i] = 0;
     __syncthreads();
-    const uint64_t* src = w.akey + (uint64_t)blockIdx.x * cap1;
-    const uint32_t r0 = bin * rpb;
-    for (uint64_t e = lo + threadIdx.x; e < hi; e += T) atomicAdd(&h[region_of(t, src[e]) - r0], 1u);
+    // the coarse pass wrote each record's region-in-bin byte (1 B per record instead of the 8-B key)
+    const uint4* src = (const uint4*)(w.areg + (uint64_t)blockIdx.x * cap1);
+    const uint64_t n16 = (hi - lo + 15) / 16;
+    for (uint64_t q = threadIdx.x; q < n16; q += T) {
+        const uint4 v = src[q];
+        const uint32_t m = (uint32_t)min((uint64_t)16, hi - 16 * q);
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j)
+            if (j < m) atomicAdd(&h[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < rpb; i += T) w.hist[(uint64_t)blockIdx.x * rpb + i] = h[i];
 }
@@ -1334,6 +1357,9 @@ __global__ __launch_bounds__(256) void k_spill_insert(Tbl t, PartWs w, const uin
 #define SS_AGG_SLICE_T 512
 #endif
 constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools/tune_counter.hip)
+#ifndef SS_AGG_P
+#define SS_AGG_P 4         // records per thread per aggregate step (loads in flight)
+#endif
 
 
 // P4, slice-direct form: the region's slice itself is the LDS hash table.  Keys are copied into LDS
@@ -1368,7 +1394,7 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         sent[2] = 0;
     }
     __syncthreads();
-    constexpr int kP = 4;
+    constexpr int kP = SS_AGG_P;
     // the region's records: one range (exact paths) or its kFinePerBin fine-scatter segments,
     // walked as one flat index space (segment s covers flat [pre[s], pre[s + 1])) so every
     // iteration issues kP loads per thread whatever the segment lengths
@@ -2052,6 +2078,7 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_acnt, acap * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_areg, acap);
     if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, kFillWords * sizeof(uint32_t));
     c->ws_cap1 = cap1;
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
@@ -2080,6 +2107,7 @@ int ss_counter_release(ss_counter* c) {
     if (c->ws_akey) (void)hipFree(c->ws_akey);
     if (c->ws_aidx) (void)hipFree(c->ws_aidx);
     if (c->ws_acnt) (void)hipFree(c->ws_acnt);
+    if (c->ws_areg) (void)hipFree(c->ws_areg);
     if (c->ws_bidx) (void)hipFree(c->ws_bidx);
     if (c->ws_bcnt) (void)hipFree(c->ws_bcnt);
     if (c->ws_spill) (void)hipFree(c->ws_spill);
@@ -2090,6 +2118,7 @@ int ss_counter_release(ss_counter* c) {
     c->ws_akey = nullptr;
     c->ws_aidx = nullptr;
     c->ws_acnt = nullptr;
+    c->ws_areg = nullptr;
     c->ws_bidx = nullptr;
     c->ws_bcnt = nullptr;
     c->ws_spill = nullptr;
@@ -2153,6 +2182,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         w.akey = c->ws_akey;
         w.aidx = c->ws_aidx;
         w.acnt = c->ws_acnt;
+        w.areg = c->ws_areg;
         w.bidx = c->ws_bidx;
         w.bcnt = c->ws_bcnt;
         w.spill = c->ws_spill;

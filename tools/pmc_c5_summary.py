@@ -11,7 +11,7 @@ import statistics
 import sys
 from collections import defaultdict
 
-KERNELS = ["k_pf_coarse", "k_pf_count", "k_pf_scatter", "k_pc_aggregate_slice"]
+KERNELS = ["k_pf_coarse", "k_pf_count", "k_pf_scatter", "k_pc_aggregate_slice", "k_spill_insert", "k_pf_order"]
 
 
 def per_dispatch(path):
@@ -38,11 +38,16 @@ def main():
     fetch, full = per_dispatch(os.path.join(root, "fetch", "run_counter_collection.csv"))
     write, _ = per_dispatch(os.path.join(root, "write", "run_counter_collection.csv"))
     sq, _ = per_dispatch(os.path.join(root, "sq", "run_counter_collection.csv"))
-    print("C5 counter kernels (tools/c5_only.py: 125M x 32-nt reads, pool 2^24, lazy reset), rocprofv3 --pmc,")
-    print("three separate passes (FETCH_SIZE | WRITE_SIZE | 8 SQ counters), median over launches.")
+    p2 = os.path.join(root, "sq2", "run_counter_collection.csv")
+    if os.path.exists(p2):
+        sq2, _ = per_dispatch(p2)
+        for k, v in sq2.items():
+            sq.setdefault(k, {}).update(v)
+    print("C5 counter kernels (tools/c5_only.py: 125M x 32-nt reads, pool 2^24 uniform, lazy reset), rocprofv3 --pmc,")
+    print("separate passes (FETCH_SIZE | WRITE_SIZE | 8 SQ counters | 8 SQ counters), median over launches.")
     print("HBM read = FETCH_SIZE KB x2 (gfx950 wide-read correction) x1024; write = WRITE_SIZE KB x1024.")
     print("Algorithmic per launch: coarse 4.0 GB in / 1.5 GB out; count 1.0 GB in; scatter 1.5 / 1.5 GB;")
-    print("aggregate 1.5 GB in + whole 1-GB table written (fresh slices).\n")
+    print("aggregate 1.5 GB in + whole 0.5-GB table written (fresh slices, 16-B slots).\n")
     for k in KERNELS:
         if k not in fetch:
             continue
@@ -52,6 +57,9 @@ def main():
         print(f"{name}: HBM read {rd:.3f} GB, write {wr:.3f} GB")
         for c in sorted(sq.get(k, {})):
             print(f"   {c:24s} {statistics.median(sq[k][c]):.4g}")
+        d = {c: statistics.median(v) for c, v in sq.get(k, {}).items()}
+        if d.get("SQ_INSTS_LDS"):
+            print(f"   -> LDS bank-conflict cycles per LDS instruction {d.get('SQ_LDS_BANK_CONFLICT', 0) / d['SQ_INSTS_LDS']:.2f}")
         print()
 
 
