@@ -11,7 +11,8 @@ index ranges (weak scaling, no data-path collective).  `value` = all ranks' nt /
 time.  The same JSON line carries the other BASELINE configs as `extra` (C3 fused encode+hamming,
 C4 encode+decode round trip, C5 sharded counter with an RCCL all-to-all merge), the `roofline` of
 the dominant kernel (algorithmic bytes / HIP-event kernel time vs 8 TB/s) and the `cpu_baseline`
-(the reference's own compiled _marshall_bytes_64 kernel, oracle/_ref, timed on 1 host core).
+(the reference's CPU algorithms restated in oracle/cpu_baseline.cpp, timed on 1 host core and on all
+usable cores for C2-C5; the reference itself never runs on the GPU box).
 """
 from __future__ import annotations
 
@@ -407,7 +408,8 @@ def _median_time(fn, reps=3):
 def bench_c1_dropin(n=1_000_000, L=32):
     """BASELINE configs[0] (C1): 1M x 32-nt synthetic reads through the drop-in Python API —
     sq.pack() per object (host codec) and ShortSeqCounter(list) (GPU batch path); median of 3
-    calls each (the reference in cpu_baseline_c1 is timed the same way)."""
+    calls each (the reference's API was timed the same way in the build container,
+    oracle/calibrate_cpu_baseline.py)."""
     import shortseq_amd as sq
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # the generator only (same synthetic reads as the CPU baseline)
@@ -463,87 +465,34 @@ def bench_fastq_dropin(path, n):
                                       "(page-cached), incl. building the 65,536-entry dict"}
 
 
-def cpu_baseline_fastq(path, n):
-    """The reference's own read_and_count_fastq (oracle/_ref, 1 host core) on the same file."""
-    import contextlib
-    import io
+def cpu_baseline(target_s=2.0):
+    """The reference's per-read CPU algorithms (oracle/cpu_baseline.cpp, kind "port": table loop for
+    L <= 32, PEXT blocks beyond, XOR-collapse-popcount hamming, charmap decode, a hash map for the
+    counter) timed on this host over bounded samples of C2-C5: 1 core (the reference is
+    single-threaded) and all the cores this process may use (OpenMP).  The reference itself never runs
+    here; its own numbers (the kernels' calibration ratios, and its Python API for C1 / a18) were
+    measured in the build container by oracle/calibrate_cpu_baseline.py and are attached, labelled."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle
-    if not oracle.ref_available():
-        return None
-    if oracle.REF_DIR not in sys.path:
-        sys.path.insert(0, oracle.REF_DIR)
-    import shortseq.counter as ref_counter
-    with contextlib.redirect_stdout(io.StringIO()):
-        t0 = time.perf_counter()
-        c = ref_counter.read_and_count_fastq(path)
-        t = time.perf_counter() - t0
-    return {"s_per_call": t, "records_per_s": n / t, "unique": len(c), "cores": 1, "kind": "reference",
-            "sample": f"{n} records, shortseq.counter.read_and_count_fastq from oracle/_ref"}
-
-
-def cpu_baseline_c1(n=1_000_000, L=32):
-    """The reference's own Python API on the same C1 reads (oracle/_ref, 1 host core): pack per
-    object and ShortSeqCounter(list)."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle
-    if not oracle.ref_available():
-        return None
-    if oracle.REF_DIR not in sys.path:
-        sys.path.insert(0, oracle.REF_DIR)
-    import shortseq.counter as ref_counter      # the reference, built from its sources (oracle/_ref)
-    import shortseq.short_seq as ref_sq
-    a = oracle.gen_reads(11, 0, n, L)
-    reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
-    t_pack, _ = _median_time(lambda: [ref_sq.pack(r) for r in reads])
-    t_cnt, _ = _median_time(lambda: ref_counter.ShortSeqCounter(reads))
-    pa = oracle.gen_pool_reads(12, 13, 1 << 14, 0, n, L)
-    preads = [pa[i * L:(i + 1) * L].tobytes() for i in range(n)]
-    t_pool, _ = _median_time(lambda: ref_counter.ShortSeqCounter(preads))
-    return {"pack_per_s": n / t_pack, "counter_reads_per_s": n / t_cnt, "counter_pool16k_reads_per_s": n / t_pool,
-            "cores": 1, "kind": "reference",
-            "sample": f"{n} x {L}-nt reads, shortseq.pack / ShortSeqCounter from oracle/_ref, median of 3"}
-
-
-# ------------------------------------------------------------------------------------------------
-def cpu_baseline(L=32, target_s=10.0):
-    """The reference's compiled _marshall_bytes_64 (oracle/_ref) on 1 host core over a bounded
-    sample of the same workload; falls back to the C restatement (kind "port") if _ref is absent."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle  # test/baseline infrastructure only — never the measured GPU path
-    n = 4_000_000
-    ascii = oracle.gen_reads(1, 0, n, L)
-    kind = "reference" if oracle.ref_available() else "port"
-    if kind == "reference":
-        def run():
-            return oracle.ref_encode_batch(ascii, n, L)
-    else:
-        def run():
-            return oracle.encode_batch(ascii, n, L)[0]
-    out = run()  # warm
-    if not np.array_equal(out[:16], oracle.gen_words(1, 0, 16, L)):
-        raise SystemExit("cpu baseline produced wrong words")
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= target_s:
-            break
-    nt = passes * n * L
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": nt / el, "unit": "nt/s", "cores": 1, "kind": kind,
-            "sample": f"{passes} passes x {n} reads x {L} nt ({el:.1f} s), "
-                      f"{'shortseq.short_seq_64._marshall_bytes_64 (reference, -O3 -mbmi2)' if kind == 'reference' else 'oracle C restatement'}"
-                      f"; host cpu: {cpu}, nproc {os.cpu_count()}"}
+    import cpu_baseline as cb  # test/baseline infrastructure only — never the measured GPU path
+    res = cb.run_all(target_s)
+    th = res["threads_all"]
+    c2 = res["C2_encode_32"]
+    out = {"value": c2["1_core"], "unit": "nt/s", "cores": 1, "kind": "port",
+           "value_all_cores": c2[f"{th}_cores"], "cores_all": th,
+           "sample": f"C2: {c2['sample_1_core']} (1 core); {c2[f'sample_{th}_cores']} ({th} cores); "
+                     f"oracle/cpu_baseline.cpp; host cpu: {res['cpu']}, nproc {res['nproc']}, "
+                     f"threads used for all-core legs {th} (OMP_NUM_THREADS / affinity)",
+           "configs": {k: v for k, v in res.items() if k.startswith("C")}}
+    cal = os.path.join(REPO, "profiles", "r2", "cpu_baseline_calibration.json")
+    if os.path.exists(cal):
+        with open(cal) as f:
+            c = json.load(f)
+        out["calibration_vs_reference"] = {
+            "where": f"build container ({c.get('cpu')}), 1 core, same inputs; ratio = port speed / reference speed",
+            **{k: round(v["ratio"], 3) for k, v in c.items() if isinstance(v, dict) and "ratio" in v}}
+        out["c1_reference_api_container"] = c.get("C1_reference_api")
+        out["a18_reference_read_and_count_fastq_container"] = c.get("a18_reference_read_and_count_fastq")
+    return out
 
 
 def main():
@@ -556,7 +505,7 @@ def main():
     ap.add_argument("--reads-per-gpu", type=int, default=100_000_000, help="reads per GPU (C2, C3; C4 uses half)")
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="timed seconds per CPU-baseline leg (8 legs)")
     ap.add_argument("--dist-backend", default=os.environ.get("SHORTSEQ_DIST_BACKEND", "nccl"),
                     help="nccl (= RCCL over xGMI, default) or gloo (rehearsal: several ranks on one GPU)")
     ap.add_argument("--same-device", action="store_true",
@@ -695,10 +644,7 @@ def main():
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline ...")
-            result["cpu_baseline"] = cpu_baseline(32, args.cpu_seconds)
-            if not args.no_extras:
-                result["cpu_baseline"]["c1_reference_api"] = cpu_baseline_c1()
-                result["cpu_baseline"]["a18_reference_read_and_count_fastq"] = cpu_baseline_fastq(fq_path, fq_n)
+            result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
