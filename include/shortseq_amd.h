@@ -297,6 +297,39 @@ int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_
                             uint32_t n_parts, uint32_t L, uint32_t* d_bounds, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
+ * Ragged read streams counted on the GPU — the batch engine behind the drop-in ShortSeqCounter(list)
+ * (counter.pyx:22-39: _count_py_bytes_list -> _from_py_bytes -> _count_sequence) and
+ * read_and_count_fastq (counter.pyx:57-70 + fast_read.pyx:3-20).  Host calls, synchronous, one
+ * engine per thread; the engine owns its stream, pinned staging and per-length counter tables.
+ *   ss_ingest_staging:  a pinned buffer of >= nbytes the caller fills with the reads back to back
+ *                       (valid until the next staging / add call).
+ *   ss_ingest_add_blob: count n reads of h_blob (read i = the next h_lens[i] bytes); global indices
+ *                       continue across calls.
+ *   ss_ingest_add_fastq: the sequence lines of a FASTQ file (the fast_read.pyx rule; lengths as
+ *                       ss_fastq_index), read in chunks of chunk_bytes (0 = 1 GiB); *h_nseqs = lines.
+ *   ss_ingest_error:    the first rejected read in input order: *h_index (UINT64_MAX = none), *h_kind
+ *                       (SS_EINVALID_BASE, its bytes -> h_read[0..cap), *h_len; or SS_ETOO_LONG).  The
+ *                       caller raises the reference's exception for it (ss_host_encode gives the
+ *                       message of an invalid base); nothing after that read is counted.
+ *   ss_ingest_finish:   orders the distinct keys by first occurrence (dict insertion order);
+ *                       *h_nkeys entries, *h_nwords packed words in total.
+ *   ss_ingest_results:  pinned arrays valid until the next reset: lengths u32 [nkeys], counts u64
+ *                       [nkeys], words u64 (entry k's max(0, ceil(L/32)) words follow entry k-1's; a
+ *                       length-0 entry is the empty read and has none).
+ *   ss_ingest_reset:    drop the counts (tables are pooled for the next call).
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct ss_ingest ss_ingest;
+int ss_ingest_create(int device, ss_ingest** h_out);
+int ss_ingest_destroy(ss_ingest* g);
+int ss_ingest_reset(ss_ingest* g);
+int ss_ingest_staging(ss_ingest* g, uint64_t nbytes, uint8_t** h_ptr);
+int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_lens, uint64_t n);
+int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, uint64_t* h_nseqs);
+int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_read, uint64_t cap, uint64_t* h_len);
+int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords);
+int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words);
+
+/* ------------------------------------------------------------------------------------------------
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):
  * read i word w: r = splitmix64(seed + i*W + w) masked to its nts, byte j = "ACTG"[(r >> 2j) & 3].
  * Pool variant: read i is pool item splitmix64(pool_seed ^ (i * 0xD1B54A32D192ED03)) % U.

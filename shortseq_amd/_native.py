@@ -76,6 +76,15 @@ SIGNATURES = [
     ("ss_fastq_onepass_ws_bytes", _U64, [_U64, _U64]),
     ("ss_fastq_index_onepass", C.c_int, [_P, _U64, _U64, C.c_int, _P, _U64, _P, _P, _P, _U64, _P, _P]),
     ("ss_gather_rows", C.c_int, [_P, _U64, _P, _P, _U64, _U32, _P, _U64, _P]),
+    ("ss_ingest_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("ss_ingest_destroy", C.c_int, [_P]),
+    ("ss_ingest_reset", C.c_int, [_P]),
+    ("ss_ingest_staging", C.c_int, [_P, _U64, C.POINTER(C.c_void_p)]),
+    ("ss_ingest_add_blob", C.c_int, [_P, _P, _P, _U64]),
+    ("ss_ingest_add_fastq", C.c_int, [_P, C.c_char_p, _U64, C.POINTER(C.c_uint64)]),
+    ("ss_ingest_error", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int), _P, _U64, C.POINTER(C.c_uint64)]),
+    ("ss_ingest_finish", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("ss_ingest_results", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("ss_stager_create", C.c_int, [C.c_int, _U64, _U32, _U32, C.POINTER(C.c_void_p)]),
     ("ss_stager_destroy", C.c_int, [_P]),
     ("ss_encode_host", C.c_int, [_P, _P, _U64, _U32, _U64, _P, _U32, C.POINTER(C.c_uint64)]),

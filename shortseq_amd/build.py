@@ -1,7 +1,8 @@
 """In-tree build of the native pieces (no pip install; the built files travel with the repo).
 
   lib/libshortseq_amd.so   hipcc --offload-arch=gfx950: kernels + C ABI (include/shortseq_amd.h)
-  _shortseq*.so            Cython front (per-object drop-in types), host C++ codec compiled in
+  _shortseq*.so            Cython front (per-object drop-in types, host C++ codec compiled in); binds
+                           lib/libshortseq_amd.so's batch engine (ss_ingest_*) at the first batch call
 
 `python -m shortseq_amd.build` rebuilds whatever is stale.
 """
@@ -17,7 +18,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIB = os.path.join(PKG, "lib", "libshortseq_amd.so")
-HIP_SOURCES = ["ss_codec.hip", "ss_counter.hip", "ss_fastq.hip", "ss_allpairs.hip", "ss_runtime.hip",
+HIP_SOURCES = ["ss_codec.hip", "ss_counter.hip", "ss_fastq.hip", "ss_allpairs.hip", "ss_runtime.hip", "ss_ingest.hip",
                "ss_stage.hip"]
 HIP_DEPS = HIP_SOURCES + ["ss_device.h", "ss_internal.h", "host_codec.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -53,7 +54,7 @@ def _ext_path(name: str) -> str:
 def build_cython(force: bool = False, verbose: bool = False) -> str:
     pyx = os.path.join(CSRC, "_shortseq.pyx")
     out = _ext_path("_shortseq")
-    deps = [pyx, os.path.join(CSRC, "host_codec.h"), os.path.join(INCLUDE, "shortseq_amd.h")]
+    deps = [pyx, os.path.join(CSRC, "host_codec.h"), os.path.join(INCLUDE, "shortseq_amd.h"), LIB]
     if not os.path.exists(pyx):
         return out
     if force or _stale(out, deps):
@@ -65,8 +66,9 @@ def build_cython(force: bool = False, verbose: bool = False) -> str:
                        check=True, stdout=None if verbose else subprocess.DEVNULL)
         inc = sysconfig.get_paths()["include"]
         tmp = out + ".tmp"
+        # the HIP C ABI library (ss_ingest_* batch engine) is dlopen'ed at the first batch call
         cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-mbmi2", "-mpopcnt", "-march=x86-64-v3",
-               "-fno-strict-aliasing", "-w", "-I" + inc, "-I" + CSRC, "-I" + INCLUDE, cpp, "-o", tmp]
+               "-fno-strict-aliasing", "-w", "-I" + inc, "-I" + CSRC, "-I" + INCLUDE, cpp, "-ldl", "-o", tmp]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

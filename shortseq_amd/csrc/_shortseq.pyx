@@ -3,9 +3,12 @@
 
 Per-object operations (pack / str / ^ / == / [] on single reads) run on the host C++ codec
 (csrc/host_codec.h): one read is ~tens of ns of work, a kernel launch is microseconds (SURVEY §7).
-Batch operations — ShortSeqCounter over a large list, read_and_count_fastq — stage the reads in a
-contiguous buffer and run on the GPU through the C ABI (shortseq_amd.batch -> libshortseq_amd.so);
-the GPU path raises if the HIP library cannot be used, it never degrades silently.
+Batch operations — ShortSeqCounter over a large list, read_and_count_fastq — call the C ABI of
+libshortseq_amd.so directly (include/shortseq_amd.h ss_ingest_*, bound with dlopen at the first batch call; no Python
+layer, no torch): the reads are copied into the engine's pinned staging buffer (or the FASTQ file is
+named), counted on the GPU, and the dict is rebuilt from the (length, words, count) rows the engine
+returns in first-occurrence order.  The GPU path raises if the HIP library cannot be used, it never
+degrades silently.
 
 Object layouts match the reference so sys.getsizeof agrees (short_seq_64.pxd:11-14,
 short_seq_192.pxd:11-14, short_seq_var.pxd:14-17): 32 / 48 / 32 + 8*ceil(L/32) bytes.
@@ -14,7 +17,7 @@ Documented deviations (DESIGN.md §6): hash() and the counter agree for every ke
 inserts with the raw word, so counts[pack("G"*32)] raises KeyError there); ShortSeqVar keys are
 deduplicated by content (reference Q6 keys them by heap pointer).
 """
-from libc.stdint cimport uint8_t, uint64_t, int64_t, int32_t, int16_t
+from libc.stdint cimport uint8_t, uint32_t, uint64_t, int64_t, int32_t, int16_t
 from libc.string cimport memcmp, memcpy, memset, strlen
 from libc.stdio cimport FILE, fopen, fclose
 from libc.stdlib cimport free, malloc, calloc
@@ -39,6 +42,79 @@ cdef extern from "Python.h":
 
 cdef extern from "stdio.h":
     ssize_t getline(char** lineptr, size_t* n, FILE* stream) nogil
+
+cdef extern from "shortseq_amd.h":
+    ctypedef struct ss_ingest:
+        pass
+    enum:
+        SS_ETOO_LONG
+
+cdef extern from "dlfcn.h":
+    void* dlopen(const char* filename, int flag) nogil
+    void* dlsym(void* handle, const char* symbol) nogil
+    char* dlerror() nogil
+    int RTLD_NOW
+    int RTLD_GLOBAL
+
+# The C ABI (include/shortseq_amd.h) bound at the first batch call, not at import: libshortseq_amd
+# links the HIP runtime, and a process that imports this module before torch would otherwise map
+# the system runtime first and torch its own bundled copy (two runtimes, the second sees no device).
+# Loaded lazily it joins whichever runtime is already there (torch's, when torch came first).
+ctypedef int (*f_device_count)(int*) noexcept nogil
+ctypedef const char* (*f_last_error)() noexcept nogil
+ctypedef int (*f_create)(int, ss_ingest**) noexcept nogil
+ctypedef int (*f_handle)(ss_ingest*) noexcept nogil
+ctypedef int (*f_staging)(ss_ingest*, uint64_t, uint8_t**) noexcept nogil
+ctypedef int (*f_add_blob)(ss_ingest*, const uint8_t*, const uint32_t*, uint64_t) noexcept nogil
+ctypedef int (*f_add_fastq)(ss_ingest*, const char*, uint64_t, uint64_t*) noexcept nogil
+ctypedef int (*f_error)(ss_ingest*, uint64_t*, int*, uint8_t*, uint64_t, uint64_t*) noexcept nogil
+ctypedef int (*f_finish)(ss_ingest*, uint64_t*, uint64_t*) noexcept nogil
+ctypedef int (*f_results)(ss_ingest*, const uint32_t**, const uint64_t**, const uint64_t**) noexcept nogil
+
+cdef struct _Abi:
+    f_device_count device_count
+    f_last_error last_error
+    f_create create
+    f_handle reset
+    f_staging staging
+    f_add_blob add_blob
+    f_add_fastq add_fastq
+    f_error error
+    f_finish finish
+    f_results results
+
+cdef _Abi _abi
+cdef bint _abi_ready = False
+
+
+cdef void* _sym(void* h, const char* name) except NULL:
+    cdef void* p = dlsym(h, name)
+    if p == NULL:
+        raise ImportError(f"libshortseq_amd: missing symbol {name.decode()}")
+    return p
+
+
+cdef int _bind_abi() except -1:
+    global _abi_ready
+    if _abi_ready:
+        return 0
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libshortseq_amd.so").encode()
+    cdef void* h = dlopen(path, RTLD_NOW | RTLD_GLOBAL)
+    if h == NULL:
+        raise ImportError(f"cannot load the HIP library {path.decode()}: {dlerror().decode(errors='replace')}")
+    _abi.device_count = <f_device_count>_sym(h, b"ss_device_count")
+    _abi.last_error = <f_last_error>_sym(h, b"ss_last_error_string")
+    _abi.create = <f_create>_sym(h, b"ss_ingest_create")
+    _abi.reset = <f_handle>_sym(h, b"ss_ingest_reset")
+    _abi.staging = <f_staging>_sym(h, b"ss_ingest_staging")
+    _abi.add_blob = <f_add_blob>_sym(h, b"ss_ingest_add_blob")
+    _abi.add_fastq = <f_add_fastq>_sym(h, b"ss_ingest_add_fastq")
+    _abi.error = <f_error>_sym(h, b"ss_ingest_error")
+    _abi.finish = <f_finish>_sym(h, b"ss_ingest_finish")
+    _abi.results = <f_results>_sym(h, b"ss_ingest_results")
+    _abi_ready = True
+    return 0
 
 cdef extern from "host_codec.h":
     ctypedef struct ss_err:
@@ -397,8 +473,8 @@ cdef class ShortSeqCounter(dict):
     """dict subclass {ShortSeq: count} in first-occurrence order (counter.pyx:10-54).
 
     ShortSeqCounter(list_of_bytes, device="auto"): lists of >= GPU_MIN_READS reads are encoded and
-    counted on the GPU (one hash-and-atomic-count kernel per read length <= 32); device="host"
-    forces the per-object host path, device="cuda"/"cuda:N" forces the GPU.
+    counted on the GPU (ss_ingest: split by length on the device, one counter table per length);
+    device="host" forces the per-object host path, device="cuda"/"cuda:N" forces the GPU.
     """
 
     def __init__(self, source=None, device="auto"):
@@ -413,15 +489,11 @@ cdef class ShortSeqCounter(dict):
 
     cdef _count_list(self, list it, device):
         cdef Py_ssize_t n = PyList_GET_SIZE(it)
-        use_gpu = False
+        dev = -1
         if device != "host" and n >= (GPU_MIN_READS if device == "auto" else 0):
-            if device == "auto":
-                import torch
-                use_gpu = torch.cuda.is_available()
-            else:
-                use_gpu = True
-        if use_gpu:
-            _count_batch_gpu(self, it, device)
+            dev = _resolve_device(device)
+        if dev >= 0:
+            _count_batch_gpu(self, it, dev)
         else:
             self._count_host(it)
 
@@ -437,147 +509,147 @@ cdef class ShortSeqCounter(dict):
 
 
 def _resolve_device(device):
-    import torch
-    if device in ("auto", "cuda"):
-        return torch.device("cuda", torch.cuda.current_device())
-    return torch.device(device)
+    """device argument -> HIP device index, or -1 for the host path: "auto" = device 0 when the HIP
+    runtime sees one, "cuda" = device 0, "cuda:N" = N (a torch.device-like object works too)."""
+    cdef int count = 0
+    if device == "host":
+        return -1
+    _bind_abi()
+    if device == "auto":
+        if _abi.device_count(&count) != 0 or count <= 0:
+            return -1
+        return 0
+    name = str(device)
+    if name == "cuda":
+        return 0
+    if name.startswith("cuda:"):
+        return int(name[5:])
+    raise ValueError(f"unknown device {device!r} (use 'auto', 'host', 'cuda' or 'cuda:N')")
 
 
-def _count_batch_gpu(ShortSeqCounter self, list reads, device):
-    """Batch path (shortseq_amd/ingest.py): the reads are joined into one pinned buffer, copied up
-    once, split by length on the device (the length is part of the key, short_seq_64.pyx:41-44),
-    each length group gathered densely and counted by one GPU table; the dict is rebuilt in
-    first-occurrence order.  The first rejected read in list order raises the reference's error."""
-    import numpy as np
-    from . import ingest
-
-    cdef Py_ssize_t i, n = PyList_GET_SIZE(reads), ln
-    cdef size_t total = 0
-    cdef object item
-    cdef char* dst
-    lens_np = np.empty(n, dtype=np.int64)
-    cdef int64_t[:] lens = lens_np
-    for i in range(n):
-        item = <object>PyList_GET_ITEM(reads, i)
-        if not PyBytes_CheckExact(item):
-            # the host loop would raise here unless an earlier read is invalid: find out first
-            _raise_first_error(reads, i)
-            raise TypeError(f"expected bytes, {type(item).__name__} found")
-        lens[i] = PyBytes_GET_SIZE(item)
-        total += lens[i]
-    # concatenate straight into the pinned staging buffer (no intermediate joined bytes object)
-    dst = <char*><size_t>ingest._staging(total).data_ptr()
-    for i in range(n):
-        ln = lens[i]
-        memcpy(dst, PyBytes_AS_STRING(<object>PyList_GET_ITEM(reads, i)), ln)
-        dst += ln
-    gc = ingest.count_list(reads, lens_np, _resolve_device(device), staged=True)
-    _fill_from_groups(self, gc)
+cdef dict _engines = {}
 
 
-def _order_groups_host(groups):
-    """finish() groups in any row order -> (groups sorted by first index, group sequence or None);
-    the host-side equivalent of LengthGroupCounter.finish_ordered's device sort."""
-    import numpy as np
-    out, firsts = [], []
-    for (Lg, w, c, f) in groups:
-        f = np.asarray(f, dtype=np.int64)
-        o = np.argsort(f, kind="stable")
-        out.append((Lg, np.ascontiguousarray(np.asarray(w, dtype=np.uint64)[o]), np.asarray(c, dtype=np.int64)[o],
-                    f[o]))
-        firsts.append(f[o])
-    if len(out) <= 1:
-        return out, None
-    allf = np.concatenate(firsts)
-    allg = np.repeat(np.arange(len(out), dtype=np.int16), [len(f) for f in firsts])
-    return out, allg[np.argsort(allf, kind="stable")]
-
-
-cdef _fill_from_groups(ShortSeqCounter self, gc):
-    """Insert the per-length GPU results into the dict in first-occurrence (= reference) order.
-    The order comes from the device (gc.finish_ordered: every group sorted by first index plus the
-    group of each key in global order), so this loop reads every array front to back, builds each
-    key object and inserts it with its known hash: no per-key __hash__ call, tuple or sort.  (A
-    presized scratch dict merged into self measured slower: the merge re-touches every key.)"""
-    import numpy as np
-    cdef int16_t[::1] gseq_v
-    cdef Py_ssize_t i, m = 0, ng, g = 0
-    cdef int64_t ef = 0
-    cdef bint empty_pending, one = True
-    cdef Py_hash_t h
-    cdef const uint64_t* wp
-    cdef int64_t[::1] cv
-    cdef int64_t[::1] fv
-    if hasattr(gc, "finish_ordered"):
-        groups, (ecount, efirst), gseq = gc.finish_ordered()
+cdef ss_ingest* _engine(int dev) except NULL:
+    """The ingest engine of a device (created once per process, reset per call)."""
+    cdef ss_ingest* g = NULL
+    cdef size_t h
+    cdef int rc
+    if dev in _engines:
+        h = _engines[dev]
+        g = <ss_ingest*>h
+        rc = _abi.reset(g)
     else:
-        groups, (ecount, efirst) = gc.finish()
-        groups, gseq = _order_groups_host(groups)
-    if not groups:
-        if ecount:
-            dict.__setitem__(self, empty, ecount)
+        rc = _abi.create(dev, &g)
+        if rc == 0:
+            _engines[dev] = <size_t>g
+    if rc != 0:
+        raise RuntimeError(f"shortseq_amd GPU engine: {_abi.last_error().decode(errors='replace')} (rc {rc})")
+    return g
+
+
+cdef _ingest_check(int rc, what):
+    if rc != 0:
+        raise RuntimeError(f"shortseq_amd {what}: {_abi.last_error().decode(errors='replace')} (rc {rc})")
+
+
+cdef _raise_ingest_error(ss_ingest* g):
+    """The first rejected read, as the reference raises it (the host codec re-encodes its bytes)."""
+    cdef uint64_t idx = 0, ln = 0
+    cdef int kind = 0
+    _ingest_check(_abi.error(g, &idx, &kind, NULL, 0, &ln), "ingest error")
+    if idx == <uint64_t>-1:
         return
-    ng = len(groups)
-    # per-group cursors over C pointers (the groups' arrays stay referenced by `keep`)
-    keep = []
-    cdef uint64_t** wps = <uint64_t**>malloc(ng * sizeof(uint64_t*))
-    cdef int64_t** cps = <int64_t**>malloc(ng * sizeof(int64_t*))
-    cdef int64_t** fps = <int64_t**>malloc(ng * sizeof(int64_t*))
-    cdef size_t* lens = <size_t*>malloc(ng * sizeof(size_t))
-    cdef size_t* wstride = <size_t*>malloc(ng * sizeof(size_t))
-    cdef Py_ssize_t* cur = <Py_ssize_t*>calloc(ng, sizeof(Py_ssize_t))
-    cdef uint64_t[:, ::1] kv
-    if wps == NULL or cps == NULL or fps == NULL or lens == NULL or wstride == NULL or cur == NULL:
-        free(wps); free(cps); free(fps); free(lens); free(wstride); free(cur)
+    if kind == SS_ETOO_LONG:
+        raise Exception(f"Sequences longer than {MAX_VAR_NT} bases are not supported.")
+    buf = PyBytes_FromStringAndSize(NULL, ln)
+    _ingest_check(_abi.error(g, &idx, &kind, <uint8_t*>PyBytes_AS_STRING(buf), ln, &ln), "ingest error")
+    _from_py_bytes(buf)          # raises the reference's exception for this read
+    raise RuntimeError("ingest flagged a read the host codec accepts")   # not reached
+
+
+cdef _fill_rows(ShortSeqCounter self, uint64_t K, const uint32_t* lens, const uint64_t* counts,
+                const uint64_t* words):
+    """Insert the engine's rows (first-occurrence order) into the dict: one key object per row,
+    inserted with its known hash (the objects' own __hash__ = packed word 0, -1 -> -2; counter.pyx
+    :44-50 inserts the same way), so the loop walks the arrays front to back with no per-key
+    __hash__ call, tuple or sort."""
+    cdef uint64_t k, woff = 0
+    cdef uint32_t L
+    cdef Py_hash_t h
+    for k in range(K):
+        L = lens[k]
+        if L == 0:
+            dict.__setitem__(self, empty, counts[k])
+            continue
+        h = <Py_hash_t>words[woff]
+        if h == -1:
+            h = -2
+        _PyDict_SetItem_KnownHash(self, _from_words(words + woff, L), counts[k], h)
+        woff += _nwords(L)
+
+
+def _fill_from_arrays(ShortSeqCounter counter, lens, counts, words):
+    """Host-side test hook for the dict rebuild: numpy arrays in the ss_ingest_results layout."""
+    import numpy as np
+    cdef uint32_t[::1] lv = np.ascontiguousarray(lens, dtype=np.uint32)
+    cdef uint64_t[::1] cv = np.ascontiguousarray(counts, dtype=np.uint64)
+    cdef uint64_t[::1] wv = np.ascontiguousarray(np.concatenate([np.asarray(words, np.uint64), np.zeros(1, np.uint64)]))
+    _fill_rows(counter, lv.shape[0], &lv[0] if lv.shape[0] else NULL, &cv[0] if cv.shape[0] else NULL, &wv[0])
+
+
+cdef _fill_from_engine(ShortSeqCounter self, ss_ingest* g):
+    cdef uint64_t K = 0, NW = 0
+    cdef const uint32_t* lens
+    cdef const uint64_t* counts
+    cdef const uint64_t* words
+    cdef int rc
+    _raise_ingest_error(g)
+    with nogil:
+        rc = _abi.finish(g, &K, &NW)
+    _ingest_check(rc, "ingest finish")
+    _ingest_check(_abi.results(g, &lens, &counts, &words), "ingest results")
+    _fill_rows(self, K, lens, counts, words)
+
+
+def _count_batch_gpu(ShortSeqCounter self, list reads, int dev):
+    """Batch path (counter.pyx:22-39 over a whole list): the bytes objects are copied back to back
+    into the engine's pinned staging buffer, counted on the GPU (split by length on the device, one
+    table per length: the length is part of the key, short_seq_64.pyx:41-44) and the dict is
+    rebuilt in first-occurrence order.  The first rejected read in list order raises the reference's
+    error."""
+    cdef Py_ssize_t i, n = PyList_GET_SIZE(reads), ln
+    cdef uint64_t total = 0
+    cdef object item
+    cdef uint8_t* dst
+    cdef uint32_t* lens = <uint32_t*>malloc(max(1, n) * sizeof(uint32_t))
+    cdef ss_ingest* g
+    cdef int rc
+    if lens == NULL:
         raise MemoryError()
     try:
-        for g in range(ng):
-            Lg, w, c, f = groups[g]
-            w = np.ascontiguousarray(w, dtype=np.uint64)
-            if w.ndim == 1:
-                w = w.reshape(-1, 1)
-            c = np.ascontiguousarray(c, dtype=np.int64)
-            f = np.ascontiguousarray(f, dtype=np.int64)
-            keep.append((w, c, f))
-            kv = w
-            cv = c
-            fv = f
-            wps[g] = &kv[0, 0] if kv.shape[0] else NULL
-            cps[g] = &cv[0] if cv.shape[0] else NULL
-            fps[g] = &fv[0] if fv.shape[0] else NULL
-            lens[g] = Lg
-            wstride[g] = kv.shape[1]
-            m += kv.shape[0]
-        if gseq is not None:
-            one = False
-            gseq_v = np.ascontiguousarray(gseq, dtype=np.int16)
-        empty_pending = ecount > 0
-        if empty_pending:
-            ef = efirst
-        for i in range(m):
-            if not one:
-                g = gseq_v[i]
-            if empty_pending and fps[g][cur[g]] > ef:
-                dict.__setitem__(self, empty, ecount)
-                empty_pending = False
-            wp = wps[g] + cur[g] * wstride[g]
-            # the objects' own __hash__ (packed word 0; CPython maps -1 to -2), given to the dict
-            # directly as the reference's counter does (counter.pyx:44-50)
-            h = <Py_hash_t>wp[0]
-            if h == -1:
-                h = -2
-            _PyDict_SetItem_KnownHash(self, _from_words(wp, lens[g]), cps[g][cur[g]], h)
-            cur[g] += 1
-        if empty_pending:
-            dict.__setitem__(self, empty, ecount)
+        for i in range(n):
+            item = <object>PyList_GET_ITEM(reads, i)
+            if not PyBytes_CheckExact(item):
+                # the host loop would raise here unless an earlier read is invalid: find out first
+                _raise_first_error(reads, i)
+                raise TypeError(f"expected bytes, {type(item).__name__} found")
+            ln = PyBytes_GET_SIZE(item)
+            lens[i] = <uint32_t>ln if ln < 0xFFFFFFFF else <uint32_t>0xFFFFFFFF
+            total += ln
+        g = _engine(dev)
+        _ingest_check(_abi.staging(g, total, &dst), "ingest staging")
+        for i in range(n):
+            ln = lens[i]
+            memcpy(dst, PyBytes_AS_STRING(<object>PyList_GET_ITEM(reads, i)), ln)
+            dst += ln
+        _ingest_check(_abi.staging(g, total, &dst), "ingest staging")   # base pointer again
+        with nogil:
+            rc = _abi.add_blob(g, dst, lens, n)
+        _ingest_check(rc, "ingest")
+        _fill_from_engine(self, g)
     finally:
-        free(wps); free(cps); free(fps); free(lens); free(wstride); free(cur)
-
-
-def _fill_groups(ShortSeqCounter counter, gc):
-    """Fill `counter` from an object with finish() -> (groups, (empty_count, empty_first)) in the
-    ingest.LengthGroupCounter format (host-side; used by the GPU paths and by the CPU tests)."""
-    _fill_from_groups(counter, gc)
+        free(lens)
 
 
 def _raise_first_error(list reads, Py_ssize_t upto):
@@ -592,19 +664,15 @@ def _raise_first_error(list reads, Py_ssize_t upto):
         _from_py_bytes(item)
 
 
-def read_and_count_fastq(filename, device="auto"):
+def read_and_count_fastq(filename, device="auto", *, _chunk_bytes=0):
     """counter.pyx:57-70 + fast_read.pyx:3-20: keep line 2 of every 4 lines; each kept line loses
     exactly its last character (strlen - 1, short_seq.pyx:50-52); prints the reference's timings.
     device "auto" (a GPU when present) / "cuda[:N]": the file is streamed to HBM in pinned chunks
-    and indexed, split by length and counted there (shortseq_amd/ingest.py); "host": the
+    and indexed, split by length and counted there (ss_ingest_add_fastq); "host": the
     reference's per-line loop."""
-    if device != "host":
-        use_gpu = True
-        if device == "auto":
-            import torch
-            use_gpu = torch.cuda.is_available()
-        if use_gpu:
-            return _read_and_count_fastq_gpu(filename, device)
+    dev = _resolve_device(device)
+    if dev >= 0:
+        return _read_and_count_fastq_gpu(filename, dev, _chunk_bytes)
     cdef FILE* f
     cdef char* line = NULL
     cdef size_t cap = 0
@@ -638,17 +706,25 @@ def read_and_count_fastq(filename, device="auto"):
     return counts
 
 
-def _read_and_count_fastq_gpu(filename, device):
+def _read_and_count_fastq_gpu(filename, int dev, uint64_t chunk_bytes=0):
+    """The file streamed through the engine (parallel preads into pinned staging, chunks ending
+    after a newline, one-read FASTQ index, split by length and counted on the device)."""
     import os
-    from . import ingest
+    cdef uint64_t nseqs = 0
+    cdef int rc
+    cdef ss_ingest* g
     fname = filename.encode("utf-8")
     if not os.path.isfile(filename):
         raise Exception(f"{str(fname)}: Something went wrong while reading this file.")
+    cdef const char* cpath = fname
     t1 = time.time()
-    gc, nseqs = ingest.count_fastq(filename, _resolve_device(device))
+    g = _engine(dev)
+    with nogil:
+        rc = _abi.add_fastq(g, cpath, chunk_bytes, &nseqs)
+    _ingest_check(rc, "ingest fastq")
     t2 = time.time()
     counts = ShortSeqCounter()
-    _fill_from_groups(counts, gc)
+    _fill_from_engine(counts, g)
     t3 = time.time()
     print(f"{t2-t1:.2f}s to read {nseqs} total seqs, and {t3 - t2:.2f}s to count {len(counts)} unique sequences")
     return counts

@@ -1,0 +1,920 @@
+// ss_ingest.hip — ragged read streams counted on the GPU behind the C ABI: the batch side of
+// ShortSeqCounter(list) (counter.pyx:22-39) and read_and_count_fastq (counter.pyx:57-70 +
+// fast_read.pyx:3-20).  The Cython front calls these entry points directly (no Python or torch in
+// between): it stages a list's bytes in the engine's pinned buffer, or names a FASTQ file, and walks
+// the returned (length, words, count) rows in first-occurrence order to rebuild the dict.
+//
+// Per chunk of reads (a staged list, or a FASTQ chunk ending after a newline):
+//   1. d_lens (u32 per read; FASTQ: ss_fastq_index_onepass, 0xFFFFFFFF = the reference's strlen
+//      underflow) -> stable split by length: k_len_count (per-block length histograms),
+//      k_len_binscan (block per length: offsets inside the length, its total and first read),
+//      k_len_binstart (one block: where each length starts), k_len_scatter
+//      (one wave per block, input order kept: a wave peels its distinct lengths with ballots, ranks by
+//      popcount) -> d_order = read indices grouped by length.  One 16-KB copy back (histogram + first).
+//   2. each length L in 1..1024: ss_gather_rows (dense rows) -> ss_counter_insert_fixed into the
+//      table of length L (the length is part of the dict key, short_seq_64.pyx:41-44); the rows'
+//      global read indices are appended to the table's row map (k_rowmap).  Length 0 is the empty
+//      ShortSeq (counted on the host side of the split); length > 1024 is the too-long error.
+//   3. first bad read: the inserts' first-bad words come back in one copy; the smallest global index
+//      of a rejected read is kept (and its bytes) — the reference raises at the first one in input
+//      order, so nothing after the chunk that holds it is read.
+// Finish: every table's entries are placed at their global first index (k_place into a per-read
+// slot array), compacted in read order (k_flag_count / k_scan_* / k_compact: a stable stream
+// compaction), and gathered into (length u32, count u64, words u64[ceil(L/32)]) rows (k_gather_out,
+// word offsets by the same scan), copied into engine-owned pinned buffers.
+//
+// Tables: one ss_counter per length, pooled across calls (reset is lazy).  Each starts at
+// 2 x the rows its length brings in the first chunk and, for single-word keys, grows (extract ->
+// merge into a table of twice the needed size) when the rows counted could push it past half full
+// (an exact size query decides; the query costs one sync and is skipped while rows <= capacity / 2).
+// Multi-word tables (L > 32) cannot merge; they start at 2 x the length's rows scaled by the file's
+// remaining size.  (table sizes follow each length's own share, not the whole file.)
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ss_internal.h"
+
+namespace {
+
+constexpr uint32_t kLenBins = SS_MAX_NT + 2;        // lengths 0..1024, and 1025 = rejected (too long)
+constexpr uint32_t kSplitBlocks = 2048;             // k_len_count / k_len_scatter: one wave per block
+constexpr uint32_t kEmptyGroup = 0xFFFFFFFFu;       // slot marker of the empty read's entry
+constexpr uint64_t kNoSlot = ~0ull;
+
+__device__ __forceinline__ uint32_t len_bin(uint32_t L) { return L > SS_MAX_NT ? SS_MAX_NT + 1 : L; }
+
+__global__ __launch_bounds__(64) void k_len_count(const uint32_t* __restrict__ lens, uint64_t n,
+                                                  uint32_t* __restrict__ blkhist, uint32_t* __restrict__ blkfirst) {
+    __shared__ uint32_t h[kLenBins], f[kLenBins];
+    for (uint32_t b = threadIdx.x; b < kLenBins; b += 64) {
+        h[b] = 0;
+        f[b] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 64) {
+        const uint32_t b = len_bin(lens[i]);
+        atomicAdd(&h[b], 1u);
+        atomicMin(&f[b], (uint32_t)i);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < kLenBins; b += 64) {
+        blkhist[(uint64_t)b * gridDim.x + blockIdx.x] = h[b];
+        blkfirst[(uint64_t)b * gridDim.x + blockIdx.x] = f[b];
+    }
+}
+
+// one block per length bin: exclusive scan of the bin's per-block counts (bin-major rows of blkhist,
+// in place) -> offsets inside the bin; out[b] = bin total, out[kLenBins + b] = first read of the bin
+__global__ __launch_bounds__(256) void k_len_binscan(uint32_t nblk, uint32_t* __restrict__ blkhist,
+                                                     const uint32_t* __restrict__ blkfirst, uint64_t* __restrict__ out) {
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t run, fmin;
+    const uint32_t b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t* row = blkhist + (uint64_t)b * nblk;
+    const uint32_t* frow = blkfirst + (uint64_t)b * nblk;
+    if (threadIdx.x == 0) {
+        run = 0;
+        fmin = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint32_t f = 0xFFFFFFFFu;
+    for (uint32_t k0 = 0; k0 < nblk; k0 += 256) {
+        const uint32_t k = k0 + threadIdx.x;
+        const uint32_t v = k < nblk ? row[k] : 0u;
+        if (k < nblk) f = min(f, frow[k]);
+        uint32_t incl = v;
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t before = run;
+        for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
+        if (k < nblk) row[k] = before + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 0) run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+    if (f != 0xFFFFFFFFu) atomicMin(&fmin, f);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[b] = run;
+        out[kLenBins + b] = fmin == 0xFFFFFFFFu ? kNoSlot : fmin;
+    }
+}
+
+// one block: out[2 kLenBins + b] = start of bin b in d_order (exclusive scan of the bin totals)
+__global__ __launch_bounds__(1024) void k_len_binstart(uint64_t* __restrict__ out) {
+    __shared__ uint64_t s[2048];
+    for (uint32_t b = threadIdx.x; b < 2048; b += 1024) s[b] = b < kLenBins ? out[b] : 0ull;
+    __syncthreads();
+    for (uint32_t off = 1; off < 2048; off <<= 1) {
+        uint64_t y0 = 0, y1 = 0;
+        const uint32_t i0 = threadIdx.x, i1 = threadIdx.x + 1024;
+        if (i0 >= off) y0 = s[i0 - off];
+        if (i1 >= off) y1 = s[i1 - off];
+        __syncthreads();
+        s[i0] += y0;
+        s[i1] += y1;
+        __syncthreads();
+    }
+    for (uint32_t b = threadIdx.x; b < kLenBins; b += 1024) out[2 * kLenBins + b] = s[b] - out[b];
+}
+
+// stable scatter: block k walks its range in input order, 64 reads per step; the wave peels the
+// distinct lengths of the step (readfirstlane + ballot), ranks lanes by popcount below them and
+// advances that length's LDS cursor
+__global__ __launch_bounds__(64) void k_len_scatter(const uint32_t* __restrict__ lens, uint64_t n,
+                                                    const uint32_t* __restrict__ blkoff, const uint64_t* __restrict__ split,
+                                                    uint64_t* __restrict__ order) {
+    __shared__ uint32_t cur[kLenBins];
+    for (uint32_t b = threadIdx.x; b < kLenBins; b += 64)
+        cur[b] = (uint32_t)split[2 * kLenBins + b] + blkoff[(uint64_t)b * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
+    const uint32_t lane = threadIdx.x;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint64_t i0 = lo; i0 < hi; i0 += 64) {
+        const uint64_t i = i0 + lane;
+        const bool live = i < hi;
+        const uint32_t b = live ? len_bin(lens[i]) : 0u;
+        uint64_t pending = __ballot(live);
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const uint32_t b0 = (uint32_t)__shfl((int)b, leader);
+            const uint64_t mine = __ballot(live && b == b0);
+            const uint32_t base = cur[b0];
+            if (live && b == b0) order[base + __popcll(mine & lt)] = i;
+            __syncthreads();   // one wave: orders the cursor read before the update
+            if (lane == (uint32_t)leader) cur[b0] = base + (uint32_t)__popcll(mine);
+            __syncthreads();
+            pending &= ~mine;
+        }
+    }
+}
+
+// row map of an insert: dst[r] = global index of row r (base + sel[r], or base + r when sel is null)
+__global__ __launch_bounds__(256) void k_rowmap(const uint64_t* __restrict__ sel, uint64_t m, uint64_t base,
+                                                uint32_t* __restrict__ dst) {
+    for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (uint64_t)gridDim.x * 256)
+        dst[r] = (uint32_t)(base + (sel ? sel[r] : r));
+}
+
+// table entry e of group g -> the slot of its global first read
+__global__ __launch_bounds__(256) void k_place(const uint64_t* __restrict__ first, uint64_t m,
+                                               const uint32_t* __restrict__ rowmap, uint32_t g,
+                                               uint64_t* __restrict__ slot) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
+        slot[rowmap[first[e]]] = ((uint64_t)g << 32) | e;
+}
+
+// ---- stable compaction / exclusive scan over n items in 1024 contiguous block ranges -------------
+constexpr uint32_t kScanBlocks = 1024;
+
+struct GDesc {
+    const uint64_t* words;   // [m * W]
+    const uint64_t* counts;  // [m]
+    uint32_t W;
+    uint32_t L;
+};
+
+// item value for the two scans: MODE 0 = slot used (1/0), MODE 1 = words of ordered entry i
+template <int MODE>
+__device__ __forceinline__ uint32_t item_val(const uint64_t* src, uint64_t i, const GDesc* gd) {
+    const uint64_t v = src[i];
+    if (MODE == 0) return v != kNoSlot ? 1u : 0u;
+    const uint32_t g = (uint32_t)(v >> 32);
+    return g == kEmptyGroup ? 0u : gd[g].W;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_scan_count(const uint64_t* __restrict__ src, uint64_t n, const GDesc* gd,
+                                                    uint64_t* __restrict__ blksum) {
+    __shared__ uint64_t s[256];
+    const uint64_t per = (n + kScanBlocks - 1) / kScanBlocks;
+    const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
+    uint64_t c = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += 256) c += item_val<MODE>(src, i, gd);
+    s[threadIdx.x] = c;
+    __syncthreads();
+    for (uint32_t off = 128; off; off >>= 1) {
+        if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) blksum[blockIdx.x] = s[0];
+}
+
+// exclusive scan of kScanBlocks block sums (one block); blksum[kScanBlocks] = total
+__global__ __launch_bounds__(1024) void k_scan_top(uint64_t* __restrict__ blksum) {
+    __shared__ uint64_t s[1024];
+    const uint64_t v = blksum[threadIdx.x];
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint64_t y = threadIdx.x >= off ? s[threadIdx.x - off] : 0ull;
+        __syncthreads();
+        s[threadIdx.x] += y;
+        __syncthreads();
+    }
+    blksum[threadIdx.x] = s[threadIdx.x] - v;
+    if (threadIdx.x == 1023) blksum[1024] = s[1023];
+}
+
+// block-local ordered walk (256 items per step, wave ballots + a 4-wave prefix): MODE 0 writes the
+// used slots in read order to dst; MODE 1 writes each ordered entry's word offset to woff
+template <int MODE>
+__global__ __launch_bounds__(256) void k_scan_apply(const uint64_t* __restrict__ src, uint64_t n, const GDesc* gd,
+                                                    const uint64_t* __restrict__ blksum, uint64_t* __restrict__ dst) {
+    __shared__ uint64_t wsum[4];
+    __shared__ uint64_t run;
+    const uint64_t per = (n + kScanBlocks - 1) / kScanBlocks;
+    const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
+    if (threadIdx.x == 0) run = blksum[blockIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t i0 = lo; i0 < hi; i0 += 256) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint32_t v = i < hi ? item_val<MODE>(src, i, gd) : 0u;
+        // inclusive wave scan of v
+        uint32_t incl = v;
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint64_t before = run;
+        for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
+        const uint64_t pos = before + incl - v;
+        if (i < hi) {
+            if (MODE == 0) {
+                if (v) dst[pos] = src[i];
+            } else {
+                dst[i] = pos;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+}
+
+// ordered entry k -> (length, count, words at woff[k])
+__global__ __launch_bounds__(256) void k_gather_out(const uint64_t* __restrict__ ordered, uint64_t K,
+                                                    const GDesc* __restrict__ gd, const uint64_t* __restrict__ woff,
+                                                    uint64_t empty_count, uint32_t* __restrict__ out_len,
+                                                    uint64_t* __restrict__ out_cnt, uint64_t* __restrict__ out_words) {
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < K; k += (uint64_t)gridDim.x * 256) {
+        const uint64_t v = ordered[k];
+        const uint32_t g = (uint32_t)(v >> 32);
+        if (g == kEmptyGroup) {
+            out_len[k] = 0;
+            out_cnt[k] = empty_count;
+            continue;
+        }
+        const uint64_t e = (uint32_t)v;
+        const GDesc d = gd[g];
+        out_len[k] = d.L;
+        out_cnt[k] = d.counts[e];
+        for (uint32_t q = 0; q < d.W; ++q) out_words[woff[k] + q] = d.words[e * d.W + q];
+    }
+}
+
+inline unsigned grid_of(uint64_t items, uint32_t per_block, unsigned cap = 4096) {
+    uint64_t b = (items + per_block - 1) / per_block;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, cap));
+}
+
+uint64_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1024;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// grow-only device buffer
+template <typename T>
+struct DBuf {
+    T* p = nullptr;
+    uint64_t cap = 0;
+    int ensure(uint64_t n) {
+        if (n <= cap) return SS_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const uint64_t want = std::max<uint64_t>(n, 1024);
+        if (hipMalloc((void**)&p, want * sizeof(T)) != hipSuccess) {
+            (void)hipGetLastError();
+            return ss_fail(SS_ENOMEM, "ingest: out of device memory");
+        }
+        cap = want;
+        return SS_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// grow-only pinned host buffer
+struct HBuf {
+    uint8_t* p = nullptr;
+    uint64_t cap = 0;
+    int ensure(uint64_t n) {
+        if (n <= cap) return SS_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const uint64_t want = std::max<uint64_t>(n, 1 << 20);
+        if (hipHostMalloc((void**)&p, want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return ss_fail(SS_ENOMEM, "ingest: out of pinned host memory");
+        }
+        cap = want;
+        return SS_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Group {
+    uint32_t L = 0;
+    ss_counter* table = nullptr;
+    uint64_t cap = 0;
+    uint64_t rows = 0;            // rows inserted (= the table's first index space)
+    DBuf<uint32_t> rowmap;        // row -> global read index
+    // finish(): the extracted entries
+    DBuf<uint64_t> fps, words, counts, first;
+    DBuf<uint32_t> lens;
+    uint64_t m = 0;
+};
+
+}  // namespace
+
+struct ss_ingest {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    HBuf stage;                    // list bytes / FASTQ chunks (pinned)
+    HBuf out_host;                 // results: lens | counts | words (pinned)
+    DBuf<uint8_t> dbuf;            // the chunk on the device
+    DBuf<uint64_t> offs;           // per read: offset in the chunk
+    DBuf<uint32_t> dlens;          // per read: length (0xFFFFFFFF = strlen underflow)
+    DBuf<uint64_t> order;          // split output
+    DBuf<uint32_t> blkhist, blkfirst;
+    DBuf<uint64_t> split_out;      // [3 * kLenBins]
+    uint64_t* h_split = nullptr;   // pinned [3 * kLenBins]
+    DBuf<uint8_t> rows;            // gathered dense rows
+    DBuf<uint64_t> first_bad;      // one u64 per length of the chunk
+    uint64_t* h_bad = nullptr;     // pinned [kLenBins + 2]
+    DBuf<uint64_t> fq_ws, fq_aux, fq_counts;
+    std::map<uint32_t, Group> groups;
+    std::vector<std::pair<uint64_t, ss_counter*>> pool;    // idle tables (capacity, handle)
+    uint64_t nreads = 0;           // global read index of the next read
+    uint64_t empty_count = 0, empty_first = kNoSlot;
+    // first rejected read (input order)
+    uint64_t bad_index = kNoSlot;
+    int bad_kind = 0;
+    std::string bad_bytes;
+    double est_scale = 1.0;        // FASTQ: file bytes / bytes seen (multi-word table sizing)
+    // finish() results
+    uint64_t nkeys = 0, nwords = 0;
+    DBuf<uint64_t> slot, ordered, woff, scan;
+    DBuf<uint32_t> out_len;
+    DBuf<uint64_t> out_cnt, out_words;
+    DBuf<GDesc> gdesc;
+};
+
+namespace {
+
+int table_get(ss_ingest* g, uint64_t cap, ss_counter** out) {
+    for (size_t i = g->pool.size(); i-- > 0;) {
+        if (g->pool[i].first == cap) {
+            *out = g->pool[i].second;
+            g->pool.erase(g->pool.begin() + (long)i);
+            return ss_counter_reset(*out, g->stream);
+        }
+    }
+    return ss_counter_create(cap, out);
+}
+
+// device bytes a pooled table holds: its slots and its partition workspace (~72 B per reserved read)
+uint64_t table_bytes(ss_counter* t) { return ss_counter_capacity(t) * 16 + ss_counter_reserved(t) * 72; }
+
+void table_put(ss_ingest* g, ss_counter* t) {
+    if (!t) return;
+    g->pool.emplace_back(ss_counter_capacity(t), t);   // workspace kept: the next call reuses it
+    uint64_t total = 0;
+    for (auto& p : g->pool) total += table_bytes(p.second);
+    while (!g->pool.empty() && total > (6ull << 30)) {
+        total -= table_bytes(g->pool.front().second);
+        ss_counter_destroy(g->pool.front().second);
+        g->pool.erase(g->pool.begin());
+    }
+}
+
+// size query (one sync): occupied slots of a table
+int table_size(ss_ingest* g, ss_counter* t, uint64_t* out) {
+    DBuf<uint64_t>& s = g->scan;
+    int rc = s.ensure(kScanBlocks + 8);
+    if (rc) return rc;
+    rc = ss_counter_size(t, s.p + kScanBlocks + 2, g->stream);
+    if (rc) return rc;
+    rc = ss_check(hipMemcpyAsync(g->h_bad + kLenBins, s.p + kScanBlocks + 2, 8, hipMemcpyDeviceToHost, g->stream),
+                  "ingest size copy");
+    if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest sync");
+    *out = g->h_bad[kLenBins];
+    return rc;
+}
+
+// make room for m more rows in group gr (single-word keys grow by extract + merge)
+int group_room(ss_ingest* g, Group& gr, uint64_t m) {
+    if (gr.table && gr.rows + m <= gr.cap / 2) return SS_OK;
+    if (!gr.table) {
+        const double scale = gr.L > 32 ? g->est_scale : 1.0;
+        gr.cap = std::min<uint64_t>(1ull << 32, pow2_at_least((uint64_t)(2.0 * (double)m * scale) + 2));
+        return table_get(g, gr.cap, &gr.table);
+    }
+    if (gr.L > 32) return SS_OK;      // multi-word tables do not merge: sized up front
+    uint64_t size = 0;
+    int rc = table_size(g, gr.table, &size);
+    if (rc) return rc;
+    if (size + m <= gr.cap / 2) return SS_OK;
+    const uint64_t ncap = pow2_at_least(2 * (size + m));
+    ss_counter* nt = nullptr;
+    if ((rc = table_get(g, ncap, &nt)) != SS_OK) return rc;
+    if ((rc = ss_counter_set_length(nt, gr.L)) != SS_OK) return rc;
+    const uint64_t cap = gr.cap + 1;
+    DBuf<uint64_t> k, c, f, pc;
+    DBuf<uint32_t> l;
+    if ((rc = k.ensure(cap)) || (rc = c.ensure(cap)) || (rc = f.ensure(cap)) || (rc = l.ensure(cap)) ||
+        (rc = pc.ensure(1)))
+        return rc;
+    rc = ss_counter_extract(gr.table, 1, k.p, l.p, c.p, f.p, cap, pc.p, g->stream);
+    if (!rc) rc = ss_counter_merge(nt, k.p, l.p, c.p, f.p, size, g->stream);
+    if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest grow");
+    k.release(), c.release(), f.release(), l.release(), pc.release();
+    if (rc) return rc;
+    table_put(g, gr.table);
+    gr.table = nt;
+    gr.cap = ss_counter_capacity(nt);
+    return SS_OK;
+}
+
+// The chunk's reads: d_buf[offs[i], + lens[i]) for i < n (global index base + i).  dense: reads are
+// back to back (offs = exclusive prefix of lens) and all have length dense_L (no split, no gather).
+int process_chunk(ss_ingest* g, uint64_t nbytes, uint64_t n, uint32_t dense_L,
+                  const std::vector<uint64_t>* h_offs, const uint8_t* h_chunk) {
+    if (n == 0) return SS_OK;
+    if (n >= (1ull << 32)) return ss_fail(SS_EARG, "ingest: a chunk holds < 2^32 reads");
+    hipStream_t s = g->stream;
+    const uint64_t base = g->nreads;
+    int rc = SS_OK;
+    struct Job {
+        uint32_t L;
+        uint64_t m, start, first;
+    };
+    std::vector<Job> jobs;
+    if (dense_L) {
+        jobs.push_back({dense_L, n, 0, 0});
+    } else {
+        if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
+            (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins)))
+            return rc;
+        hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, g->dlens.p, n, g->blkhist.p, g->blkfirst.p);
+        hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(256), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
+                           g->split_out.p);
+        hipLaunchKernelGGL(k_len_binstart, dim3(1), dim3(1024), 0, s, g->split_out.p);
+        hipLaunchKernelGGL(k_len_scatter, dim3(kSplitBlocks), dim3(64), 0, s, g->dlens.p, n, g->blkhist.p,
+                           (const uint64_t*)g->split_out.p, g->order.p);
+        rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, 3 * kLenBins * 8, hipMemcpyDeviceToHost, s),
+                      "ingest split copy");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest split");
+        if (rc) return rc;
+        const uint64_t* hh = g->h_split;
+        for (uint32_t L = 0; L < kLenBins; ++L) {
+            const uint64_t m = hh[L];
+            if (!m) continue;
+            const uint64_t f = hh[kLenBins + L];
+            if (L == 0) {
+                g->empty_count += m;
+                g->empty_first = std::min(g->empty_first, base + f);
+            } else if (L > SS_MAX_NT) {
+                if (base + f < g->bad_index) {
+                    g->bad_index = base + f;
+                    g->bad_kind = SS_ETOO_LONG;
+                    g->bad_bytes.clear();
+                }
+            } else {
+                jobs.push_back({L, m, hh[2 * kLenBins + L], f});
+            }
+        }
+    }
+    if ((rc = g->first_bad.ensure(jobs.size() + 1))) return rc;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        const Job& jb = jobs[j];
+        if (base + jb.first > g->bad_index) continue;       // cannot hold the first error any more
+        Group& gr = g->groups[jb.L];
+        gr.L = jb.L;
+        if ((rc = group_room(g, gr, jb.m))) return rc;
+        if ((rc = gr.rowmap.ensure(gr.rows + jb.m))) return rc;
+        const uint8_t* src;
+        uint64_t stride;
+        const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
+        if (dense_L) {
+            src = g->dbuf.p;
+            stride = dense_L;
+        } else {
+            stride = (jb.L + 15) / 16 * 16;
+            if ((rc = g->rows.ensure(jb.m * stride))) return rc;
+            rc = ss_gather_rows(g->dbuf.p, nbytes, g->offs.p, sel, jb.m, jb.L, g->rows.p, stride, s);
+            if (rc) return rc;
+            src = g->rows.p;
+        }
+        if (jb.m >= (1u << 16) && jb.m < (1ull << 31) && jb.L <= 32) (void)ss_counter_reserve(gr.table, jb.m);
+        rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.L, stride, gr.rows, g->first_bad.p + j, s);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, s, sel, jb.m, base, gr.rowmap.p + gr.rows);
+        gr.rows += jb.m;
+    }
+    if (jobs.empty()) {
+        g->nreads += n;
+        return SS_OK;
+    }
+    rc = ss_check(hipMemcpyAsync(g->h_bad, g->first_bad.p, jobs.size() * 8, hipMemcpyDeviceToHost, s), "ingest bad copy");
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest chunk");
+    if (rc) return rc;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        const uint64_t fb = g->h_bad[j];
+        if (fb == kNoSlot || base + jobs[j].first > g->bad_index) continue;
+        uint64_t idx = fb;           // row of the insert -> read of the chunk
+        if (!dense_L) {
+            rc = ss_check(hipMemcpy(&idx, g->order.p + jobs[j].start + fb, 8, hipMemcpyDeviceToHost), "ingest bad row");
+            if (rc) return rc;
+        }
+        if (base + idx < g->bad_index) {
+            g->bad_index = base + idx;
+            g->bad_kind = SS_EINVALID_BASE;
+            uint64_t off = 0;
+            if (h_offs) {
+                off = (*h_offs)[idx];
+            } else if ((rc = ss_check(hipMemcpy(&off, g->offs.p + idx, 8, hipMemcpyDeviceToHost), "ingest bad off"))) {
+                return rc;
+            }
+            g->bad_bytes.assign((const char*)h_chunk + off, jobs[j].L);
+        }
+    }
+    // a too-long read's bytes (the message does not quote them) are not needed
+    g->nreads += n;
+    return SS_OK;
+}
+
+// ---- FASTQ file reading (parallel preads into the pinned staging buffer) ---------------------------
+uint64_t pread_full(int fd, uint8_t* dst, uint64_t len, uint64_t pos) {
+    uint64_t got = 0;
+    while (got < len) {
+        const ssize_t k = pread(fd, dst + got, len - got, (off_t)(pos + got));
+        if (k <= 0) break;
+        got += (uint64_t)k;
+    }
+    return got;
+}
+
+uint64_t read_parallel(int fd, uint8_t* dst, uint64_t len, uint64_t pos, unsigned threads) {
+    if (len < (32ull << 20) || threads <= 1) return pread_full(fd, dst, len, pos);
+    const uint64_t per = ((len + threads - 1) / threads + (1 << 20) - 1) & ~((uint64_t)(1 << 20) - 1);
+    std::vector<std::thread> ts;
+    std::vector<uint64_t> got(threads, 0);
+    for (unsigned t = 0; t < threads; ++t) {
+        const uint64_t a = (uint64_t)t * per;
+        if (a >= len) break;
+        const uint64_t b = std::min(len, a + per);
+        ts.emplace_back([&, t, a, b] { got[t] = pread_full(fd, dst + a, b - a, pos + a); });
+    }
+    uint64_t sum = 0;
+    for (size_t t = 0; t < ts.size(); ++t) {
+        ts[t].join();
+        sum += got[t];
+    }
+    return sum;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ss_ingest_create(int device, ss_ingest** h_out) {
+    if (!h_out) return ss_fail(SS_EARG, "null h_out");
+    int rc = ss_check(hipSetDevice(device), "ingest hipSetDevice");
+    if (rc) return rc;
+    ss_ingest* g = new ss_ingest();
+    g->device = device;
+    rc = ss_check(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking), "ingest stream");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_split, 3 * kLenBins * 8, hipHostMallocDefault), "ingest pinned");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_bad, (kLenBins + 2) * 8, hipHostMallocDefault), "ingest pinned");
+    if (rc) {
+        ss_ingest_destroy(g);
+        return rc;
+    }
+    *h_out = g;
+    return SS_OK;
+}
+
+int ss_ingest_reset(ss_ingest* g) {
+    if (!g) return ss_fail(SS_EARG, "null ingest");
+    (void)hipSetDevice(g->device);
+    // tables go back to the pool; a length's row map and extraction buffers stay (grow-only) for the
+    // next call (a fresh hipMalloc per call and length costs more than the counting)
+    for (auto& kv : g->groups) {
+        table_put(g, kv.second.table);
+        kv.second.table = nullptr;
+        kv.second.cap = 0;
+        kv.second.rows = 0;
+        kv.second.m = 0;
+    }
+    g->nreads = 0;
+    g->empty_count = 0;
+    g->empty_first = kNoSlot;
+    g->bad_index = kNoSlot;
+    g->bad_kind = 0;
+    g->bad_bytes.clear();
+    g->est_scale = 1.0;
+    g->nkeys = g->nwords = 0;
+    return SS_OK;
+}
+
+int ss_ingest_destroy(ss_ingest* g) {
+    if (!g) return SS_OK;
+    ss_ingest_reset(g);
+    for (auto& kv : g->groups) {
+        kv.second.rowmap.release();
+        kv.second.fps.release(), kv.second.words.release(), kv.second.counts.release(), kv.second.first.release();
+        kv.second.lens.release();
+    }
+    g->groups.clear();
+    for (auto& p : g->pool) ss_counter_destroy(p.second);
+    g->pool.clear();
+    g->stage.release();
+    g->out_host.release();
+    g->dbuf.release(), g->offs.release(), g->dlens.release(), g->order.release(), g->blkhist.release();
+    g->blkfirst.release(), g->split_out.release(), g->rows.release(), g->first_bad.release();
+    g->fq_ws.release(), g->fq_aux.release(), g->fq_counts.release();
+    g->slot.release(), g->ordered.release(), g->woff.release(), g->scan.release(), g->out_len.release();
+    g->out_cnt.release(), g->out_words.release(), g->gdesc.release();
+    if (g->h_split) (void)hipHostFree(g->h_split);
+    if (g->h_bad) (void)hipHostFree(g->h_bad);
+    if (g->stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+    return SS_OK;
+}
+
+int ss_ingest_staging(ss_ingest* g, uint64_t nbytes, uint8_t** h_ptr) {
+    if (!g || !h_ptr) return ss_fail(SS_EARG, "null argument");
+    int rc = g->stage.ensure(nbytes + 16);
+    *h_ptr = rc ? nullptr : g->stage.p;
+    return rc;
+}
+
+int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_lens, uint64_t n) {
+    if (!g || (n && (!h_blob || !h_lens))) return ss_fail(SS_EARG, "null argument");
+    if (n == 0 || g->bad_index != kNoSlot) return SS_OK;
+    (void)hipSetDevice(g->device);
+    std::vector<uint64_t> offs(n);
+    uint64_t total = 0;
+    bool same = true;
+    for (uint64_t i = 0; i < n; ++i) {
+        offs[i] = total;
+        total += h_lens[i];
+        same &= h_lens[i] == h_lens[0];
+    }
+    hipStream_t s = g->stream;
+    int rc;
+    if ((rc = g->dbuf.ensure(total + 16)) || (rc = g->offs.ensure(n)) || (rc = g->dlens.ensure(n))) return rc;
+    rc = ss_check(hipMemcpyAsync(g->dbuf.p, h_blob, total ? total : 1, hipMemcpyHostToDevice, s), "ingest H2D");
+    const uint32_t dense = (same && h_lens[0] > 0 && h_lens[0] <= SS_MAX_NT) ? h_lens[0] : 0u;
+    if (!rc && !dense) {
+        rc = ss_check(hipMemcpyAsync(g->offs.p, offs.data(), n * 8, hipMemcpyHostToDevice, s), "ingest H2D");
+        if (!rc) rc = ss_check(hipMemcpyAsync(g->dlens.p, h_lens, n * 4, hipMemcpyHostToDevice, s), "ingest H2D");
+    }
+    if (!rc) rc = process_chunk(g, total, n, dense, &offs, h_blob);
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest blob");   // staging reusable after return
+    return rc;
+}
+
+int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, uint64_t* h_nseqs) {
+    if (!g || !path) return ss_fail(SS_EARG, "null argument");
+    (void)hipSetDevice(g->device);
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return ss_fail(SS_EARG, "cannot open the FASTQ file");
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        return ss_fail(SS_EARG, "cannot stat the FASTQ file");
+    }
+    const uint64_t size = (uint64_t)st.st_size;
+    if (chunk_bytes == 0) chunk_bytes = 1ull << 30;
+    uint64_t cap = std::max<uint64_t>(16, std::min<uint64_t>(chunk_bytes, size + 16));
+    hipStream_t s = g->stream;
+    int rc = g->stage.ensure(cap);
+    uint64_t line0 = 0, carry = 0, pos = 0, seqs0 = g->nreads;
+    unsigned threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    while (!rc) {
+        if (cap >= (1ull << 32)) {
+            rc = ss_fail(SS_EARG, "a FASTQ line is longer than 2 GiB");
+            break;
+        }
+        uint8_t* hv = g->stage.p;
+        const uint64_t want = std::min(cap - carry, size - std::min(size, pos));
+        const uint64_t got = read_parallel(fd, hv + carry, want, pos, threads);
+        if (got != want) {
+            rc = ss_fail(SS_EHIP, "short read of the FASTQ file");
+            break;
+        }
+        pos += got;
+        const uint64_t n = carry + got;
+        const bool at_eof = pos >= size;
+        if (n == 0) break;
+        uint64_t use = n;
+        if (!at_eof) {
+            use = 0;
+            for (uint64_t k = n; k > 0; --k)
+                if (hv[k - 1] == '\n') {
+                    use = k;
+                    break;
+                }
+            if (use == 0) {     // one line fills the chunk: grow the staging buffer, keep its bytes
+                HBuf grown;
+                if ((rc = grown.ensure(2 * cap))) break;
+                memcpy(grown.p, hv, n);
+                g->stage.release();
+                g->stage = grown;
+                cap *= 2;
+                carry = n;
+                continue;
+            }
+        }
+        // index the chunk on the device
+        if ((rc = g->dbuf.ensure(use + 16))) break;
+        rc = ss_check(hipMemcpyAsync(g->dbuf.p, hv, use, hipMemcpyHostToDevice, s), "ingest H2D");
+        uint64_t maxr = use / 16 + 2;
+        uint64_t nl = 0, nrec = 0;
+        while (!rc) {
+            const uint64_t wsb = ss_fastq_onepass_ws_bytes(use, maxr);
+            if ((rc = g->fq_ws.ensure(wsb / 8 + 1)) || (rc = g->offs.ensure(maxr)) || (rc = g->dlens.ensure(maxr)) ||
+                (rc = g->fq_aux.ensure(maxr)) || (rc = g->fq_counts.ensure(3)))
+                break;
+            rc = ss_fastq_index_onepass(g->dbuf.p, use, line0, at_eof ? 1 : 0, g->fq_ws.p, wsb, g->offs.p, g->dlens.p,
+                                        g->fq_aux.p, maxr, g->fq_counts.p, s);
+            if (!rc) rc = ss_check(hipMemcpyAsync(g->h_bad, g->fq_counts.p, 24, hipMemcpyDeviceToHost, s), "ingest fq");
+            if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest fq");
+            if (rc) break;
+            nl = g->h_bad[0];
+            nrec = g->h_bad[1];
+            if (g->h_bad[2]) {
+                maxr *= 2;
+                continue;
+            }
+            if (nrec <= maxr) break;
+            maxr = nrec;
+        }
+        if (rc) break;
+        if (!at_eof && g->est_scale == 1.0 && use) g->est_scale = (double)size / (double)use;
+        rc = process_chunk(g, use, nrec, 0, nullptr, hv);
+        if (rc) break;
+        line0 += nl;
+        if (at_eof || g->bad_index != kNoSlot) break;
+        rc = ss_check(hipStreamSynchronize(s), "ingest chunk");
+        carry = n - use;
+        memmove(hv, hv + use, carry);
+    }
+    close(fd);
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest fastq");
+    if (h_nseqs) *h_nseqs = g->nreads - seqs0;
+    return rc;
+}
+
+int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_read, uint64_t cap, uint64_t* h_len) {
+    if (!g || !h_index || !h_kind) return ss_fail(SS_EARG, "null argument");
+    *h_index = g->bad_index;
+    *h_kind = g->bad_kind;
+    if (h_len) *h_len = g->bad_bytes.size();
+    if (h_read && cap) memcpy(h_read, g->bad_bytes.data(), std::min<uint64_t>(cap, g->bad_bytes.size()));
+    return SS_OK;
+}
+
+int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
+    if (!g || !h_nkeys || !h_nwords) return ss_fail(SS_EARG, "null argument");
+    (void)hipSetDevice(g->device);
+    hipStream_t s = g->stream;
+    const uint64_t N = g->nreads;
+    int rc = SS_OK;
+    *h_nkeys = *h_nwords = 0;
+    if (N == 0) return SS_OK;
+    if ((rc = g->slot.ensure(N))) return rc;
+    rc = ss_check(hipMemsetAsync(g->slot.p, 0xFF, N * 8, s), "ingest slot reset");
+    std::vector<GDesc> desc;
+    uint32_t gi = 0;
+    for (auto& kv : g->groups) {
+        Group& gr = kv.second;
+        if (rc) break;
+        if (!gr.table) continue;      // a length of an earlier call
+        const uint32_t W = gr.L <= 32 ? 1u : (gr.L + 31) / 32;
+        const uint64_t cap = gr.cap + 1;
+        if ((rc = gr.fps.ensure(cap)) || (rc = gr.words.ensure(cap * W)) || (rc = gr.counts.ensure(cap)) ||
+            (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)) || (rc = g->scan.ensure(kScanBlocks + 8)))
+            break;
+        rc = ss_counter_extract_words(gr.table, 1, gr.fps.p, gr.lens.p, gr.words.p, gr.counts.p, gr.first.p, cap,
+                                      g->scan.p + kScanBlocks + 2, s);
+        if (!rc) rc = ss_counter_overflow(gr.table, g->scan.p + kScanBlocks + 3, s);
+        if (!rc) rc = ss_check(hipMemcpyAsync(g->h_bad, g->scan.p + kScanBlocks + 2, 16, hipMemcpyDeviceToHost, s), "ingest");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest extract");
+        if (rc) break;
+        if (g->h_bad[1]) {
+            rc = ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
+            break;
+        }
+        gr.m = g->h_bad[0];
+        hipLaunchKernelGGL(k_place, dim3(grid_of(gr.m, 256)), dim3(256), 0, s, gr.first.p, gr.m, gr.rowmap.p, gi,
+                           g->slot.p);
+        desc.push_back({gr.words.p, gr.counts.p, W, gr.L});
+        ++gi;
+    }
+    if (rc) return rc;
+    if (g->empty_count) {
+        const uint64_t v = ((uint64_t)kEmptyGroup << 32);
+        rc = ss_check(hipMemcpyAsync(g->slot.p + g->empty_first, &v, 8, hipMemcpyHostToDevice, s), "ingest empty");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest empty");   // v lives on this stack frame
+        if (rc) return rc;
+    }
+    if ((rc = g->gdesc.ensure(desc.size() + 1))) return rc;
+    if (!desc.empty())
+        rc = ss_check(hipMemcpyAsync(g->gdesc.p, desc.data(), desc.size() * sizeof(GDesc), hipMemcpyHostToDevice, s),
+                      "ingest desc");
+    // stable compaction of the used slots (read order = dict order)
+    if (!rc) {
+        hipLaunchKernelGGL((k_scan_count<0>), dim3(kScanBlocks), dim3(256), 0, s, g->slot.p, N, (const GDesc*)g->gdesc.p,
+                           g->scan.p);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
+        rc = ss_check(hipMemcpyAsync(g->h_bad, g->scan.p + kScanBlocks, 8, hipMemcpyDeviceToHost, s), "ingest");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest count");
+    }
+    if (rc) return rc;
+    const uint64_t K = g->h_bad[0];
+    if ((rc = g->ordered.ensure(K + 1)) || (rc = g->woff.ensure(K + 1))) return rc;
+    hipLaunchKernelGGL((k_scan_apply<0>), dim3(kScanBlocks), dim3(256), 0, s, g->slot.p, N, (const GDesc*)g->gdesc.p,
+                       g->scan.p, g->ordered.p);
+    // word offsets of the ordered entries
+    hipLaunchKernelGGL((k_scan_count<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
+                       g->scan.p);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
+    hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
+                       g->scan.p, g->woff.p);
+    rc = ss_check(hipMemcpyAsync(g->h_bad, g->scan.p + kScanBlocks, 8, hipMemcpyDeviceToHost, s), "ingest");
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest words");
+    if (rc) return rc;
+    const uint64_t NW = g->h_bad[0];
+    if ((rc = g->out_len.ensure(K + 1)) || (rc = g->out_cnt.ensure(K + 1)) || (rc = g->out_words.ensure(NW + 1)))
+        return rc;
+    hipLaunchKernelGGL(k_gather_out, dim3(grid_of(K, 256)), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
+                       g->woff.p, g->empty_count, g->out_len.p, g->out_cnt.p, g->out_words.p);
+    // results -> pinned host: lens [K] u32 | pad | counts [K] u64 | words [NW] u64
+    const uint64_t lb = (K * 4 + 15) & ~15ull, cb = K * 8, wb = NW * 8;
+    if ((rc = g->out_host.ensure(lb + cb + wb + 16))) return rc;
+    rc = ss_check(hipMemcpyAsync(g->out_host.p, g->out_len.p, K * 4, hipMemcpyDeviceToHost, s), "ingest out");
+    if (!rc) rc = ss_check(hipMemcpyAsync(g->out_host.p + lb, g->out_cnt.p, cb, hipMemcpyDeviceToHost, s), "ingest out");
+    if (!rc && wb) rc = ss_check(hipMemcpyAsync(g->out_host.p + lb + cb, g->out_words.p, wb, hipMemcpyDeviceToHost, s), "ingest out");
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest out");
+    if (rc) return rc;
+    g->nkeys = K;
+    g->nwords = NW;
+    *h_nkeys = K;
+    *h_nwords = NW;
+    return SS_OK;
+}
+
+int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words) {
+    if (!g || !h_lens || !h_counts || !h_words) return ss_fail(SS_EARG, "null argument");
+    const uint64_t lb = (g->nkeys * 4 + 15) & ~15ull;
+    *h_lens = (const uint32_t*)g->out_host.p;
+    *h_counts = (const uint64_t*)(g->out_host.p + lb);
+    *h_words = (const uint64_t*)(g->out_host.p + lb + g->nkeys * 8);
+    return SS_OK;
+}
+
+}  // extern "C"

@@ -34,7 +34,8 @@ def test_no_device_is_an_error_not_a_fallback():
     n = C.c_int(-1)
     rc = lib.ss_device_count(C.byref(n))
     if n.value > 0:
-        return  # on a GPU box this test has nothing to say
+        import pytest
+        pytest.skip("a HIP device is present: this checks the CPU-only failure mode")
     fb = C.c_uint64(0)
     rc = lib.ss_encode_fixed(None, 10, 32, 32, None, 1, C.addressof(fb), None)
     assert rc != 0

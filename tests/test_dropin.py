@@ -8,10 +8,13 @@ singleton :21-30, single bases :34-49, class switch :54-59, invalid chars :63-69
 hamming every length :159-166 and :456-463, slices :170-240 and :310-452, README :465-491),
 restated here with a seeded RNG.  Host path only (CPU); the GPU counter path is in test_gpu_*.
 """
+import os
 import random
 import sys
 
 import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 import shortseq_amd as sq
 from shortseq_amd import (MAX_64_NT, MAX_192_NT, MAX_VAR_NT, MIN_64_NT, MIN_192_NT, MIN_VAR_NT,
@@ -245,28 +248,32 @@ def test_read_and_count_fastq(tmp_path, capsys):
     assert "total seqs" in capsys.readouterr().out
 
 
-def test_fill_groups_order_and_empty():
-    """The GPU paths' dict rebuild (host side): keys from several length groups and the empty read
-    come out in first-occurrence order with their counts and hashes (dict lookups work)."""
+def test_fill_rows_order_and_empty():
+    """The GPU paths' dict rebuild (host side) from the engine's rows (ss_ingest_results layout):
+    keys of several lengths and the empty read, in the given (first-occurrence) order, with their
+    counts and hashes (dict lookups work, incl. "G" * 32 whose word is ~0: hash -1 -> -2)."""
     import numpy as np
     from shortseq_amd import _shortseq as S
 
-    def words_of(s):
-        return [int(x) for x in sq.pack(s).packed]
-    g32 = ["A" * 32, "G" * 32, "ACGT" * 8]            # "G" * 32 packs to ~0: hash -1 -> -2
-    g40 = ["C" * 40, "T" * 40]
-    w32 = np.array([words_of(s) for s in g32], dtype=np.uint64)
-    w40 = np.array([words_of(s) + [0] * (2 - len(words_of(s))) for s in g40], dtype=np.uint64)
-
-    class G:
-        def finish(self):
-            return ([(32, w32, np.array([3, 1, 2]), np.array([7, 2, 9])),
-                     (40, w40, np.array([5, 4]), np.array([0, 8]))], (6, 4))
+    keys = ["C" * 40, "G" * 32, "", "A" * 32, "T" * 40, "ACGT" * 8, "A" * 100]
+    counts = [5, 1, 6, 3, 4, 2, 7]
+    words = [int(x) for k in keys if k for x in sq.pack(k).packed[:(len(k) + 31) // 32]]
     c = ShortSeqCounter()
-    S._fill_groups(c, G())
-    assert [(str(k), v) for k, v in c.items()] == [
-        ("C" * 40, 5), ("G" * 32, 1), ("", 6), ("A" * 32, 3), ("T" * 40, 4), ("ACGT" * 8, 2)]
+    S._fill_from_arrays(c, np.array([len(k) for k in keys], np.uint32), np.array(counts, np.uint64),
+                        np.array(words, np.uint64))
+    assert [(str(k), v) for k, v in c.items()] == list(zip(keys, counts))
     assert c[sq.pack("G" * 32)] == 1 and c[sq.pack("ACGT" * 8)] == 2 and c[sq.pack("")] == 6
+    assert c[sq.pack("A" * 100)] == 7
+
+
+def test_import_does_not_load_torch():
+    """The drop-in (per-object API and the GPU batch engine) goes Cython -> C ABI: importing it, and
+    counting on the host, never imports torch."""
+    import subprocess
+    import sys
+    code = ("import sys, shortseq_amd as sq; sq.ShortSeqCounter([b'ACGT'] * 3, device='host'); "
+            "sq.pack('ACGT'); assert 'torch' not in sys.modules, 'torch imported'")
+    subprocess.run([sys.executable, "-c", code], check=True, cwd=REPO)
 
 
 def test_pack_every_byte_value_in_every_block_position(oracle):

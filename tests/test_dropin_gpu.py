@@ -84,3 +84,51 @@ def test_fastq_gpu(gpu, tmp_path):
     d = sq.read_and_count_fastq(str(p), device="cuda")
     assert _items(d) == _items(h)
     assert sum(d.values()) == 80_000
+
+
+def test_c1_dropin_reference_digest(gpu, digests, oracle):
+    """BASELINE configs[0] (C1) through the drop-in API on the GPU: ShortSeqCounter(list) of the 1M x
+    32-nt pool-65536 reads reproduces the reference ShortSeqCounter's own ordered digest (keys, length,
+    count in dict order; tests/golden/golden_digests.json, captured from the compiled reference)."""
+    import hashlib
+    import numpy as np
+    d = digests["counter_1000000x32_pool65536"]
+    n, L = d["n"], d["L"]
+    a = oracle.gen_pool_reads(d["seed"], d["pool_seed"], d["U"], 0, n, L)
+    reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    c = ShortSeqCounter(reads, device="cuda")
+    assert len(c) == d["unique"]
+    rows = np.array([(k.packed[0], len(k), v) for k, v in c.items()], dtype=np.uint64)
+    assert hashlib.sha256(np.ascontiguousarray(rows).tobytes()).hexdigest() == d["ordered_sha256"]
+
+
+def test_gpu_batch_path_without_torch(gpu, tmp_path):
+    """ShortSeqCounter(list) and read_and_count_fastq on the GPU go Cython -> C ABI: a fresh
+    interpreter runs both on the device and never imports torch; results equal the host path."""
+    import subprocess
+    import sys
+    code = r'''
+import random, sys
+import shortseq_amd as sq
+rng = random.Random(7)
+pool = [bytes(rng.choice(b"ACGT") for _ in range(rng.choice([0, 12, 32, 33, 100]))) for _ in range(300)]
+reads = [rng.choice(pool) for _ in range(120_000)]
+d = sq.ShortSeqCounter(reads, device="cuda")
+h = sq.ShortSeqCounter(reads, device="host")
+assert [(str(k), v) for k, v in d.items()] == [(str(k), v) for k, v in h.items()]
+p = sys.argv[1]
+with open(p, "w") as f:
+    for i, r in enumerate(reads[:50_000]):
+        f.write(f"@r{i}\n{r.decode()}A\n+\n{'I' * (len(r) + 1)}\n")
+fd = sq.read_and_count_fastq(p, device="cuda")
+fh = sq.read_and_count_fastq(p, device="host")
+assert [(str(k), v) for k, v in fd.items()] == [(str(k), v) for k, v in fh.items()]
+assert "torch" not in sys.modules, "torch imported"
+print("ok")
+'''
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code, str(tmp_path / "x.fq")], cwd=repo, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "ok" in out.stdout

@@ -223,28 +223,19 @@ def test_gather_rows_gpu(gpu):
 
 @pytest.mark.gpu
 def test_fastq_golden_gpu(gpu, golden, tmp_path, capsys):
-    from shortseq_amd import ingest
     for name, case in _cases(golden):
         p = tmp_path / (name + ".fq")
         p.write_bytes(bytes.fromhex(case["file_hex"]))
-        if case["raises"]:
-            with pytest.raises(Exception) as ei:
-                sq.read_and_count_fastq(str(p), device="cuda")
-            assert str(ei.value) == case["message"], name
-            continue
-        c = sq.read_and_count_fastq(str(p), device="cuda")
-        assert _items(c) == _merged_golden(case), name
-        # the same through tiny ingest chunks (every chunk boundary path)
-        if len(case["file_hex"]) > 200:
-            gc, n = ingest.count_fastq(str(p), gpu, chunk_bytes=96)
-            c2 = sq.ShortSeqCounter()
-            groups, (ec, ef) = gc.finish()
-            ent = [(ef, sq.pack(""), ec)] if ec else []
-            for L, words, counts, firsts in groups:
-                for k in range(words.shape[0]):
-                    ent.append((int(firsts[k]), sq.from_words([int(x) for x in words[k]], L), int(counts[k])))
-            ent.sort(key=lambda e: e[0])
-            assert [(type(k).__name__, str(k), len(k), v) for _f, k, v in ent] == _merged_golden(case), name
+        for chunk in (0, 96):              # default chunks, and tiny ones (every chunk-boundary path)
+            if chunk and len(case["file_hex"]) <= 200:
+                continue
+            if case["raises"]:
+                with pytest.raises(Exception) as ei:
+                    sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=chunk)
+                assert str(ei.value) == case["message"], (name, chunk)
+                continue
+            c = sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=chunk)
+            assert _items(c) == _merged_golden(case), (name, chunk)
     assert "total seqs" in capsys.readouterr().out
 
 
