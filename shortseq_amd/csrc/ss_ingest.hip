@@ -312,7 +312,10 @@ struct DBuf {
     uint64_t cap = 0;
     int ensure(uint64_t n) {
         if (n <= cap) return SS_OK;
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipDeviceSynchronize();   // queued work may still read the old buffer
+            (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
         const uint64_t want = std::max<uint64_t>(n, 1024);
@@ -322,6 +325,23 @@ struct DBuf {
         }
         cap = want;
         return SS_OK;
+    }
+    // grow keeping the first `used` elements (geometric: appended-to buffers such as row maps)
+    int ensure_keep(uint64_t n, uint64_t used, hipStream_t s) {
+        if (n <= cap) return SS_OK;
+        T* q = nullptr;
+        const uint64_t want = std::max<uint64_t>(n, 2 * cap);
+        if (hipMalloc((void**)&q, want * sizeof(T)) != hipSuccess) {
+            (void)hipGetLastError();
+            return ss_fail(SS_ENOMEM, "ingest: out of device memory");
+        }
+        int rc = SS_OK;
+        if (used) rc = ss_check(hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, s), "ingest grow copy");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest grow copy");
+        if (p) (void)hipFree(p);
+        p = q;
+        cap = want;
+        return rc;
     }
     void release() {
         if (p) (void)hipFree(p);
@@ -533,7 +553,7 @@ int process_chunk(ss_ingest* g, uint64_t nbytes, uint64_t n, uint32_t dense_L,
         Group& gr = g->groups[jb.L];
         gr.L = jb.L;
         if ((rc = group_room(g, gr, jb.m))) return rc;
-        if ((rc = gr.rowmap.ensure(gr.rows + jb.m))) return rc;
+        if ((rc = gr.rowmap.ensure_keep(gr.rows + jb.m, gr.rows, s))) return rc;
         const uint8_t* src;
         uint64_t stride;
         const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;

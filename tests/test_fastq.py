@@ -271,3 +271,37 @@ def test_counter_packed_keys_partitioned(gpu, oracle, L):
     assert [int(x) for x in k] == [w[0] for (w, _L, _c, _f) in exp]
     assert [int(x) for x in cnt] == [cc for (_w, _L, cc, _f) in exp]
     assert [int(x) for x in f] == [ff for (_w, _L, _c, ff) in exp]
+
+
+@pytest.mark.gpu
+def test_fastq_gpu_many_lengths_many_chunks(gpu, tmp_path):
+    """a multi-chunk FASTQ with many read lengths (1..300 nt, every chunk a mix) counted
+    through small chunks: equals the host path; per-length tables follow each length's own share."""
+    rng = random.Random(21)
+    recs = []
+    for i in range(30_000):
+        L = rng.randint(1, 300)
+        s = "".join(rng.choice("ACGT") for _ in range(L)) if rng.random() < 0.5 else "ACGT" * (L // 4) + "A" * (L % 4)
+        recs.append(f"@r{i}\n{s}A\n+\n{'I' * (L + 1)}\n")
+    p = tmp_path / "mix.fq"
+    p.write_text("".join(recs))
+    h = sq.read_and_count_fastq(str(p), device="host")
+    for chunk in (1 << 16, 1 << 20):
+        d = sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=chunk)
+        assert _items(d) == _items(h), chunk
+
+
+@pytest.mark.gpu
+def test_fastq_gpu_table_growth(gpu, tmp_path):
+    """A length whose distinct keys keep arriving after the first chunk: its table (sized from the first
+    chunk's rows) grows by extract + merge and keeps every count and first occurrence."""
+    rng = random.Random(22)
+    pool = ["".join(rng.choice("ACGT") for _ in range(20)) for _ in range(200)]
+    recs = [f"@a{i}\n{rng.choice(pool)}A\n+\n{'I' * 21}\n" for i in range(3000)]          # few keys first
+    recs += [f"@b{i}\n{''.join(rng.choice('ACGT') for _ in range(20))}A\n+\n{'I' * 21}\n" for i in range(150_000)]
+    recs += [f"@c{i}\n{rng.choice(pool)}A\n+\n{'I' * 21}\n" for i in range(3000)]
+    p = tmp_path / "grow.fq"
+    p.write_text("".join(recs))
+    h = sq.read_and_count_fastq(str(p), device="host")
+    d = sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=1 << 17)
+    assert _items(d) == _items(h)
