@@ -256,6 +256,26 @@ def bench_roundtrip(B, lib, dev, rank, world, n, L, steps, warmup, seed=3):
     return el, t_enc.mean_ms(), t_dec.mean_ms(), tr.region_ms / steps
 
 
+def table_digest(keys, counts, first) -> str:
+    """SHA-256 of the (key, count, first) uint64 rows sorted by key (tests/golden/gen_c5_digests.py)."""
+    import hashlib
+    k = np.asarray(keys, dtype=np.uint64)
+    o = np.argsort(k, kind="stable")
+    rows = np.stack([k[o], np.asarray(counts, dtype=np.uint64)[o], np.asarray(first, dtype=np.uint64)[o]], 1)
+    return hashlib.sha256(np.ascontiguousarray(rows).tobytes()).hexdigest()
+
+
+def c5_digest_name(U, zipf, world, n):
+    """The c5_digests.json entry for this C5 run (125M reads per rank, seeds 5 / 77), or None."""
+    if n != 125_000_000:
+        return None
+    if world == 1:
+        return (f"zipf{zipf}" if zipf else "uniform") + f"_U{U.bit_length() - 1}_shard0"
+    if not zipf and U == 1 << 24 and world in (2, 4, 8):
+        return f"uniform_U24_job{world}"
+    return None
+
+
 def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool_seed=77, zipf=None):
     """C5: per rank n reads drawn from a pool of U 32-mers (uniform, or Zipf(zipf) when given; shard =
     contiguous read-index range); shortseq_amd.dist.ShardedCounter: local HBM table -> partition by
@@ -273,17 +293,27 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
         sc.count(ascii, L, base_index=i0, check_errors=False)
 
     el, tr = timed_loop(step, steps, warmup, world)
-    k, c, f = sc.owned_items()
-    tot = torch.tensor([int(c.sum().item()), k.numel()], dtype=torch.int64,
-                       device=dev if world == 1 or dist.get_backend() == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(tot)
-    if int(tot[0]) != n * world:
-        raise SystemExit(f"PARITY FAILURE: counter total {int(tot[0])} != {n * world}")
-    uniq = int(tot[1])
-    sc.close()
     del ascii
-    return el, tr.region_ms / steps, uniq
+    # parity after timing: the whole job's table gathered to rank 0 (all owners' regions), its
+    # (key, count, first) rows sorted by key hashed and compared with the generator-derived digest of
+    # the same job (tests/golden/c5_digests.json) when one exists for this (U, skew, world), else
+    # the total count
+    res = sc.gather_items(dst=0)
+    sc.close()
+    uniq, check = 0, "total count"
+    if rank == 0:
+        keys, counts, first = res
+        uniq = len(keys)
+        if int(counts.sum()) != n * world:
+            raise SystemExit(f"PARITY FAILURE: counter total {int(counts.sum())} != {n * world}")
+        name = c5_digest_name(U, zipf, world, n)
+        if name is not None:
+            with open(os.path.join(REPO, "tests", "golden", "c5_digests.json")) as fh:
+                want = json.load(fh)[name]
+            if (uniq, table_digest(keys, counts, first)) != (want["unique"], want["digest"]):
+                raise SystemExit(f"PARITY FAILURE: counter table != {name}")
+            check = f"digest {name}"
+    return el, tr.region_ms / steps, uniq, check
 
 
 def bench_fastq_index(B, lib, dev, n_rec=8 << 20, L=100, reps=10):
@@ -411,9 +441,9 @@ def bench_c1_dropin(n=1_000_000, L=32):
     calls each (the reference's API was timed the same way in the build container,
     oracle/calibrate_cpu_baseline.py)."""
     import shortseq_amd as sq
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle  # the generator only (same synthetic reads as the CPU baseline)
-    a = oracle.gen_reads(11, 0, n, L)
+    import shortseq_amd.batch as B
+    # the SURVEY §8(d) generator on the device, copied to host bytes objects (the API's input shape)
+    a = B.synth_reads(n, L, seed=11, device="cuda").cpu().numpy().reshape(-1)
     reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
     t_pack, objs = _median_time(lambda: [sq.pack(r) for r in reads])
     sq.ShortSeqCounter(reads[:100_000])                    # warm the GPU path
@@ -422,7 +452,7 @@ def bench_c1_dropin(n=1_000_000, L=32):
     if len(c) != len(set(reads)) or sum(c.values()) != n or str(objs[7]) != reads[7].decode():
         raise SystemExit("PARITY FAILURE: C1 drop-in")
     # the same API on a duplicate-heavy list (2^14-read pool): the dict the API must return is small
-    pa = oracle.gen_pool_reads(12, 13, 1 << 14, 0, n, L)
+    pa = B.synth_pool_reads(n, L, 12, 13, 1 << 14, device="cuda").cpu().numpy().reshape(-1)
     preads = [pa[i * L:(i + 1) * L].tobytes() for i in range(n)]
     t_pool, pc = _median_time(lambda: sq.ShortSeqCounter(preads))
     if sum(pc.values()) != n:
@@ -565,7 +595,7 @@ def main():
             "ms_per_step": el3 / args.steps * 1e3, "kernel_ms_events": k3, "device_ms_per_step": d3,
             "roofline": {"kernel": "k_encode_ham_dense", "achieved": b3 / (k3 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": b3 / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "algo_bytes_per_launch": b3, "kernel_ms": k3,
+                         "algo_bytes_per_launch": b3, "kernel_ms": k3, "traffic": load_traffic("encode_hamming96", n3),
                          "note": "HIP events around the fused launch; device_ms_per_step also holds the "
                                  "1-read reference encode each step"}}
         for Lh, nh in ((32, args.reads_per_gpu), (96, args.reads_per_gpu), (512, args.reads_per_gpu // 2)):
@@ -577,7 +607,8 @@ def main():
                 "device_ms_per_step": dh, "reads": nh,
                 "roofline": {"kernel": "k_ham_dense3" if Lh == 96 else "k_ham_dense",
                              "achieved": bh / (dh * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": bh / (dh * 1e-3) / 1e9 / HBM_PEAK_GBS, "algo_bytes_per_step": bh}}
+                             "frac": bh / (dh * 1e-3) / 1e9 / HBM_PEAK_GBS, "algo_bytes_per_step": bh,
+                             "traffic": load_traffic(f"hamming_ref_{Lh}", nh)}}
         L4, n4 = 512, args.reads_per_gpu // 2
         log(f"C4 encode+decode {n4} x {L4}")
         s4 = max(5, args.steps // 2)
@@ -588,35 +619,40 @@ def main():
             "encode_kernel_ms_events": ke, "decode_kernel_ms_events": kd, "device_ms_per_step": d4,
             "roofline": {"kernel": "k_encode_g16<pext> + k_decode_g16", "achieved": (b4e + b4d) / (d4 * 1e-3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": (b4e + b4d) / (d4 * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "algo_bytes_per_step": b4e + b4d}}
+                         "algo_bytes_per_step": b4e + b4d,
+                         "traffic": (None if load_traffic("encode512", n4) is None or load_traffic("decode512", n4) is None
+                                     else load_traffic("encode512", n4) + load_traffic("decode512", n4))}}
         n5, U5 = 125_000_000, 1 << 24
         log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
         s5 = max(3, args.steps // 4)
-        el5, d5, uniq = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
-        # per-read bytes of the partitioned pipeline: coarse pass 32 in + 12 out,
-        # fine count 8, fine scatter 12 + 12, aggregate 12 + the table slices (2 x 32 B per unique
-        # slot, amortised over the reads); the floor of the problem is the 32 B of ASCII per read
-        table_b = 2 * 32 * min(U5, n5) / n5
-        pipe_b = 32 + 12 + 8 + 24 + 12 + table_b
+        el5, d5, uniq, chk5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
+        # per-read bytes of the partitioned pipeline: coarse pass 32 in + 13 out (key,
+        # read index, region byte), fine count 1, fine scatter 12 + 12, aggregate 12 + the whole
+        # table written once (fresh slices: 16 B x 2^25 slots, amortised over the reads); the floor of
+        # the problem is the 32 B of ASCII per read
+        table_b = 16 * (2 * U5) / n5
+        pipe_b = 32 + 13 + 1 + 24 + 12 + table_b
         extra["C5_counter_32"] = {
             "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
-            "reads_per_gpu": n5, "pool": U5, "unique": uniq,
+            "reads_per_gpu": n5, "pool": U5, "unique": uniq, "parity": chk5,
             "roofline": {"bound": "hbm", "kernel": "partitioned insert (k_pf_coarse, k_pf_count, k_pf_scatter, "
                                                     "k_pc_aggregate)",
                          "achieved": n5 * pipe_b / (d5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": n5 * pipe_b / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_read": pipe_b,
                          "floor_frac": n5 * 32 / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": load_traffic("counter32_insert", n5),
                          "note": "frac: the pipeline's own pass bytes; floor_frac: 32 B of ASCII per read"},
-            "merge": (f"all_to_all_single of (key, count, first) by owner over {dist.get_backend()}"
+            "merge": (f"all_to_all_single of 16-B (key, count, first) records by owner over {dist.get_backend()}"
                       f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
                      if world > 1 else "none (1 GPU)"}
         # SURVEY §8(d) C5 variants: the smaller pool and Zipf s = 1.1 skew (same shard size)
         for name, U_, zs in (("C5_counter_32_U20", 1 << 20, None), ("C5_counter_32_zipf1.1_U24", 1 << 24, 1.1),
                              ("C5_counter_32_zipf1.1_U20", 1 << 20, 1.1)):
             log(f"C5 counter {n5} x 32 per GPU, pool {U_}, {'zipf ' + str(zs) if zs else 'uniform'}")
-            el_, d_, u_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
+            el_, d_, u_, chk_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
             extra[name] = {"reads_per_s": n5 * world / (el_ / s5), "ms_per_step": el_ / s5 * 1e3,
                            "device_ms_per_step": d_, "reads_per_gpu": n5, "pool": U_, "zipf_s": zs, "unique": u_,
+                           "parity": chk_,
                            "vs_uniform_U24": d_ / d5,
                            "floor_frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS}
         if rank == 0 or world == 1:

@@ -629,10 +629,14 @@ class GpuCounter:
         check(lib().ss_counter_size(self._h, self._scratch.data_ptr(), _stream(self.device)), "ss_counter_size")
         return int(self._scratch[0].item())
 
-    def overflowed(self) -> bool:
+    def overflow_word(self) -> torch.Tensor:
+        """The handle's overflow word as a 1-element device tensor (no host sync)."""
         check(lib().ss_counter_overflow(self._h, self._scratch[1:].data_ptr(), _stream(self.device)),
               "ss_counter_overflow")
-        return int(self._scratch[1].item()) != 0
+        return self._scratch[1:2]
+
+    def overflowed(self) -> bool:
+        return int(self.overflow_word().item()) != 0
 
     def extract(self, n_parts: int = 1, cap: Optional[int] = None):
         """Occupied slots grouped by owner part -> (keys, lens, counts, first, part_counts), all on

@@ -78,29 +78,36 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, part
     return out + (rc_l,) if with_sizes else out
 
 
-def exchange_packed(rec: torch.Tensor, part_counts: torch.Tensor, first_base: int, group=None):
+def exchange_packed(rec: torch.Tensor, part_counts: torch.Tensor, first_base: int, group=None,
+                    extra: torch.Tensor = None):
     """All-to-all of owner-grouped packed records (int64 [m, 2] = 16 B each, ss_counter_pack_ranges).
 
-    One small all-to-all carries (records for you, my first_base) per peer, then one all-to-all
-    moves the records.  Returns (received records in source-rank order, per-source sizes,
-    per-source first_base)."""
+    One small all-to-all carries (records for you, my first_base) per peer; then ONE host sync reads
+    this rank's send sizes, the received metadata and `extra` (e.g. the table's overflow word)
+    together, and one all-to-all moves the records (RCCL needs the split sizes on the host; a
+    fixed-capacity exchange would avoid the sync but move the whole region range, 2x the records at
+    the table's 0.5 load factor).  Returns (received records in source-rank order, per-source sizes,
+    per-source first_base, host copy of extra or None)."""
     world = dist.get_world_size(group)
     dev = rec.device
     if dev.type != "cpu" and dist.get_backend(group) == "gloo":
-        out = exchange_packed(rec.cpu(), part_counts.cpu(), first_base, group)
+        out = exchange_packed(rec.cpu(), part_counts.cpu(), first_base, group,
+                              None if extra is None else extra.cpu())
         return (out[0].to(dev),) + tuple(out[1:])
     meta = torch.stack([part_counts.to(torch.int64),
                         torch.full((world,), first_base, dtype=torch.int64, device=dev)], 1)
     rmeta = torch.empty_like(meta)
     dist.all_to_all_single(rmeta, meta, group=group)
-    sc_l = [int(x) for x in part_counts.tolist()]
-    rm = rmeta.tolist()
-    rc_l = [int(r[0]) for r in rm]
-    bases = [int(r[1]) for r in rm]
+    parts = [meta[:, 0], rmeta.reshape(-1)] + ([extra.reshape(-1).to(torch.int64)] if extra is not None else [])
+    host = torch.cat(parts).cpu().tolist()                               # the one host sync
+    sc_l = [int(x) for x in host[:world]]
+    rc_l = [int(host[world + 2 * p]) for p in range(world)]
+    bases = [int(host[world + 2 * p + 1]) for p in range(world)]
+    ex = host[3 * world:] if extra is not None else None
     m = sum(sc_l)
     recv = torch.empty((sum(rc_l), 2), dtype=torch.int64, device=dev)
     dist.all_to_all_single(recv, rec[:m], output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
-    return recv, rc_l, bases
+    return recv, rc_l, bases, ex
 
 
 class ShardedCounter:
@@ -134,9 +141,11 @@ class ShardedCounter:
             return self.local
         # the other owners' regions as 16-B records (the rank's own part stays in its table)
         rec, parts = self.local.pack_ranges(self.world, skip=self.rank, first_base=base_index)
-        if self.local.overflowed():
+        # the table's overflow word rides along the exchange's one host sync
+        recv, rsizes, rbases, ovf = exchange_packed(rec, parts, base_index, group=self.group,
+                                                     extra=self.local.overflow_word())
+        if ovf[0]:
             raise RuntimeError("counter pack overflow (a count or first index past 32 bits, or the table)")
-        recv, rsizes, rbases = exchange_packed(rec, parts, base_index, group=self.group)
         runs, pos = [], 0
         for src, n in enumerate(rsizes):
             if n:

@@ -65,13 +65,17 @@ def main():
                      "max_count": int(c.max()), "digest": oracle.table_digest(k, c, f)}
         print(name, out[name], f"{time.time() - t:.0f} s", flush=True)
         json.dump(out, open(path, "w"), indent=1)
-    # the whole 1B-read job over 8 shards (8-rank rehearsal): union of the shard tables
-    if not only or "uniform_U24_job8" in only:
+    # whole jobs over W shards of N reads (the multi-GPU C5: rank r counts reads [r N, (r + 1) N)):
+    # the union of the shard tables, for the 8-rank rehearsal test and bench.py's world > 1 check
+    for W in (2, 4, 8):
+        name = f"uniform_U24_job{W}"
+        if only and name not in only:
+            continue
         t = time.time()
         U = 1 << 24
         counts = np.zeros(U, dtype=np.uint64)
         first = np.full(U, np.iinfo(np.uint64).max, dtype=np.uint64)
-        for r in range(8):
+        for r in range(W):
             for s0 in range(0, N, 1 << 23):
                 m = min(1 << 23, N - s0)
                 ids = oracle.pool_ids(POOL_SEED, r * N + s0, m, U)
@@ -81,12 +85,11 @@ def main():
                 first[u[new]] = np.uint64(r * N + s0) + pos[new].astype(np.uint64)
         used = np.nonzero(counts)[0]
         keys = oracle.splitmix64_np(np.uint64(SEED) + used.astype(np.uint64))
-        out["uniform_U24_job8"] = {"U": U, "zipf_s": None, "i0": 0, "n": 8 * N, "shards": 8,
-                                   "unique": int(len(used)), "max_count": int(counts.max()),
-                                   "digest": oracle.table_digest(keys, counts[used], first[used])}
-        print("uniform_U24_job8", out["uniform_U24_job8"], f"{time.time() - t:.0f} s", flush=True)
+        out[name] = {"U": U, "zipf_s": None, "i0": 0, "n": W * N, "shards": W,
+                     "unique": int(len(used)), "max_count": int(counts.max()),
+                     "digest": oracle.table_digest(keys, counts[used], first[used])}
+        print(name, out[name], f"{time.time() - t:.0f} s", flush=True)
         json.dump(out, open(path, "w"), indent=1)
-
 
 if __name__ == "__main__":
     main()

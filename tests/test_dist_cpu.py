@@ -72,6 +72,9 @@ class HostTable:
         own = owner_of_region_np(ks, n_parts, self.log2cap, self.slice_log) if len(ks) else np.zeros(0, np.int64)
         return self._rows(ks, own, n_parts)
 
+    def overflow_word(self):
+        return torch.zeros(1, dtype=torch.int64)
+
     def overflowed(self):
         return False
 

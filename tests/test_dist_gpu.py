@@ -59,3 +59,59 @@ def test_sharded_counter_two_ranks_one_gpu(oracle):
     assert [int(k) for k in keys] == [w[0] for (w, _L, _c, _f) in exp]
     assert counts == [c for (_w, _L, c, _f) in exp]
     assert first == [f for (_w, _L, _c, f) in exp]
+
+
+def _worker_c5(rank, world, port, n, U, q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import shortseq_amd.batch as B
+        from shortseq_amd.dist import ShardedCounter
+        dev = torch.device("cuda", 0)
+        ascii = B.synth_pool_reads(n, 32, 5, 77, U, i0=rank * n, device=dev)
+        sc = ShardedCounter(2 * U, device=dev)
+        sc.local.reserve(n)
+        sc.count(ascii, 32, base_index=rank * n, check_errors=False)
+        del ascii
+        torch.cuda.empty_cache()
+        res = sc.gather_items(dst=0)
+        sc.close()
+        if rank == 0:
+            import oracle
+            k, c, f = res
+            q.put((len(k), int(c.sum()), oracle.table_digest(k, c, f)))
+    except Exception as e:  # noqa: BLE001
+        q.put(("error", rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_sharded_counter_8_ranks_c5_shards():
+    """SURVEY §8(e) C5 rehearsal without an 8-GPU node: 8 ranks (one process each, all on this GPU,
+    gloo staging the exchange through host memory where the node uses RCCL) each count a full
+    125M-read shard of the 1B-read job in its own HBM table, exchange the other owners' regions and
+    fold them in; the union gathered on rank 0 equals the generator-derived digest of the whole job
+    (tests/golden/c5_digests.json uniform_U24_job8: content, not just the total)."""
+    import json
+    d = json.load(open(os.path.join(REPO, "tests", "golden", "c5_digests.json")))["uniform_U24_job8"]
+    world, n = d["shards"], d["n"] // d["shards"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_c5, args=(r, world, port, n, d["U"], q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=800)
+    for p in procs:
+        p.join(timeout=120)
+    assert got[0] != "error", got
+    assert all(p.exitcode == 0 for p in procs)
+    assert got == (d["unique"], d["n"], d["digest"])

@@ -35,6 +35,7 @@ def per_dispatch(path):
 
 def main():
     root = sys.argv[1]
+    save = "--save-traffic" in sys.argv
     fetch, full = per_dispatch(os.path.join(root, "fetch", "run_counter_collection.csv"))
     write, _ = per_dispatch(os.path.join(root, "write", "run_counter_collection.csv"))
     sq, _ = per_dispatch(os.path.join(root, "sq", "run_counter_collection.csv"))
@@ -48,6 +49,7 @@ def main():
     print("HBM read = FETCH_SIZE KB x2 (gfx950 wide-read correction) x1024; write = WRITE_SIZE KB x1024.")
     print("Algorithmic per launch: coarse 4.0 GB in / 1.5 GB out; count 1.0 GB in; scatter 1.5 / 1.5 GB;")
     print("aggregate 1.5 GB in + whole 0.5-GB table written (fresh slices, 16-B slots).\n")
+    per_kernel = {}
     for k in KERNELS:
         if k not in fetch:
             continue
@@ -60,6 +62,20 @@ def main():
         d = {c: statistics.median(v) for c, v in sq.get(k, {}).items()}
         if d.get("SQ_INSTS_LDS"):
             print(f"   -> LDS bank-conflict cycles per LDS instruction {d.get('SQ_LDS_BANK_CONFLICT', 0) / d['SQ_INSTS_LDS']:.2f}")
+        per_kernel[k] = rd + wr
+    total = sum(per_kernel.values())
+    print(f"per insert: {total:.3f} GB HBM ({total * 1e9 / 125e6:.1f} B per read)")
+    if save:
+        import json
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+        t = json.load(open(path)) if os.path.exists(path) else {}
+        t["counter32_insert"] = {"kernels": {k: v * 1e9 for k, v in per_kernel.items()},
+                                 "hbm_bytes_per_launch": total * 1e9, "reads": 125_000_000,
+                                 "hbm_bytes_per_read": total * 1e9 / 125e6, "source": sys.argv[2] if len(sys.argv) > 2 else root,
+                                 "method": "scripts/pmc_c5.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                                           "tools/c5_only.py (125M x 32 nt, pool 2^24 uniform); FETCH x2 (gfx950), x1024"}
+        with open(path, "w") as f:
+            json.dump(t, f, indent=1)
         print()
 
 

@@ -40,37 +40,48 @@ def main():
             summ[name] = json.load(f)
     if len(sys.argv) > 3 and os.path.exists(sys.argv[3]):
         shutil.copy(sys.argv[3], os.path.join(dst, "bench.log"))
-    # roofline-kernel traffic table for bench.py
+    # roofline-kernel traffic table for bench.py: HBM bytes per launch of every bench line's kernel,
+    # with the launch's read count so bench.py scales it to its own launch (bytes per read x reads)
     traffic = {}
+    method = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; FETCH_SIZE x2 (gfx950 wide-read "
+              "correction), x1024 (KB)")
+
+    def put(name, e, reads, note=None):
+        traffic[name] = {"kernel": e["kernel"], "grid": e["grid"], "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
+                         "reads": reads, "hbm_bytes_per_read": e["hbm_bytes_per_launch"] / reads,
+                         "fetch_kb_raw": e.get("fetch_kb_raw"), "write_kb_raw": e.get("write_kb_raw"),
+                         "avg_ms_rocprof": e["avg_ms"], "source": os.path.relpath(dst, REPO), "method": method}
+        if note:
+            traffic[name]["note"] = note
+
     for e in summ.get("c2", []):
         if e["kernel"].startswith("void k_encode_g16<false, true, 1") and "hbm_bytes_per_launch" in e:
-            traffic["encode32"] = {"kernel": e["kernel"], "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
-                                   "reads": READS, "hbm_bytes_per_read": e["hbm_bytes_per_launch"] / READS,
-                                   "fetch_kb_raw": e.get("fetch_kb_raw"), "write_kb_raw": e.get("write_kb_raw"),
-                                   "avg_ms_rocprof": e["avg_ms"], "source": os.path.relpath(dst, REPO),
-                                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes; "
-                                             "FETCH_SIZE x2 (gfx950 wide-read correction), x1024 (KB)"}
+            put("encode32", e, READS)
+    big = lambda e: e["grid"] >= 1_000_000   # noqa: E731  (the bench's launches, not the 1-read reference encode)
     for e in summ.get("all", []):
         k = e["kernel"]
-        if "hbm_bytes_per_launch" not in e:
+        if "hbm_bytes_per_launch" not in e or not big(e):
             continue
         if k.startswith("void k_encode_ham_dense"):
-            traffic["encode_hamming96"] = {"kernel": k, "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
-                                           "avg_ms_rocprof": e["avg_ms"]}
-        elif k.startswith("void k_decode_g16") and e["grid"] >= 400000000:
-            traffic["decode512"] = {"kernel": k, "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
-                                    "avg_ms_rocprof": e["avg_ms"]}
-        elif k.startswith("void k_encode_g16<false, true, 2") and e["grid"] >= 400000000:
-            traffic["encode512"] = {"kernel": k, "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
-                                    "avg_ms_rocprof": e["avg_ms"]}
-        elif k.startswith("void k_count_g16"):
-            traffic["counter32_insert"] = {"kernel": k, "hbm_bytes_per_launch": e["hbm_bytes_per_launch"],
-                                           "avg_ms_rocprof": e["avg_ms"],
-                                           "note": "random 32-B slot traffic; the x2 FETCH correction is calibrated "
-                                                   "for wide streaming reads only"}
+            put("encode_hamming96", e, READS)
+        elif k.startswith("void k_ham_dense3"):
+            put("hamming_ref_96", e, READS)
+        elif k.startswith("void k_ham_dense<"):
+            # C3' 32 nt: 100M pairs, 2048 per 256-thread block; 512 nt: 50M pairs, 128 per block
+            if e["grid"] < 50_000_000:
+                put("hamming_ref_32", e, READS)
+            else:
+                put("hamming_ref_512", e, READS // 2)
+        elif k.startswith("void k_decode_g16"):
+            put("decode512", e, READS // 2)
+        elif k.startswith("void k_encode_g16<false, true, 2"):
+            put("encode512", e, READS // 2)
     if traffic:
-        with open(os.path.join(REPO, "profiles", "pmc_traffic.json"), "w") as f:
-            json.dump(traffic, f, indent=1)
+        path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        old = json.load(open(path)) if os.path.exists(path) else {}
+        keep = {k: v for k, v in old.items() if k.startswith("counter32")}   # from tools/pmc_c5_summary.py
+        with open(path, "w") as f:
+            json.dump({**traffic, **keep}, f, indent=1)
     print("saved", dst, sorted(traffic))
 
 
