@@ -7,7 +7,10 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")
-for p in (REPO, os.path.join(REPO, "oracle")):
+# SHORTSEQ_TEST_ROOT: import the package and the oracle from another build of them (scripts/
+# sanitize_cpu.sh points it at build/asan); data files still come from this checkout
+_ROOT = os.environ.get("SHORTSEQ_TEST_ROOT", REPO)
+for p in (_ROOT, os.path.join(_ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
