@@ -517,9 +517,21 @@ def cpu_baseline(target_s=2.0):
     if os.path.exists(cal):
         with open(cal) as f:
             c = json.load(f)
+        ratios = {k: v["ratio"] for k, v in c.items() if isinstance(v, dict) and "ratio" in v}
         out["calibration_vs_reference"] = {
             "where": f"build container ({c.get('cpu')}), 1 core, same inputs; ratio = port speed / reference speed",
-            **{k: round(v["ratio"], 3) for k, v in c.items() if isinstance(v, dict) and "ratio" in v}}
+            **{k: round(v, 3) for k, v in ratios.items()},
+            "why": "L > 32: the reference's compiled _marshall_bytes_array checks __Pyx_ErrOccurredWithGIL() "
+                   "after _divmod and _marshall_full_blocks for every read (Cython exception propagation of "
+                   "util.pyx:88-90), which the port does not restate; counter: the reference builds a "
+                   "ShortSeq object per read into a CPython dict, the port a std::unordered_map node"}
+        # the port's 1-core numbers scaled by the calibration: the reference's expected speed on this host
+        pick = {"C2_encode_32": "encode_32", "C3_encode_hamming_96": "encode_96",
+                "C4_roundtrip_512": "encode_512", "C5_counter_32": "counter_32_pool2^24"}
+        for cfg, key in pick.items():
+            if cfg in out["configs"] and key in ratios:
+                out["configs"][cfg]["reference_equiv_1_core"] = out["configs"][cfg]["1_core"] / ratios[key]
+                out["configs"][cfg]["calibrated_by"] = key
         out["c1_reference_api_container"] = c.get("C1_reference_api")
         out["a18_reference_read_and_count_fastq_container"] = c.get("a18_reference_read_and_count_fastq")
     return out

@@ -818,6 +818,17 @@ constexpr uint32_t kHeavy = SS_PF_HEAVY;
 #ifndef SS_PF_DET
 #define SS_PF_DET 0
 #endif
+// measurement only (results invalid when not 7): which record streams the coarse / fine write-outs
+// store, bit 0 keys, bit 1 region bytes (coarse) / counts (fine), bit 2 read indices
+#ifndef SS_PF_WRITE
+#define SS_PF_WRITE 7
+#endif
+#ifndef SS_FS_WRITE
+#define SS_FS_WRITE 7
+#endif
+#ifndef SS_PF_STOP
+#define SS_PF_STOP 0
+#endif
 
 // sub-bin capacity of the optimistic partition for a batch of n reads (host and device agree)
 __host__ __device__ __forceinline__ uint64_t pf_cap1(uint64_t n) {
@@ -1061,12 +1072,12 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
 #else
                 const uint64_t at = (uint64_t)(b * kFinePerBin + sub) * cap1 + pos;
 #endif
-                w.akey[at] = k;
-                w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
+                if (SS_PF_WRITE & 1) w.akey[at] = k;
+                if (SS_PF_WRITE & 2) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
                 if (c > 1) {
                     w.aidx[at] = sidx[i] | kWeighted;
                     w.acnt[at] = c;
-                } else {
+                } else if (SS_PF_WRITE & 4) {
                     w.aidx[at] = sidx[i];
                 }
             } else {
@@ -1182,7 +1193,7 @@ __global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ f
 __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill,
                                                     const uint32_t* __restrict__ order) {
     constexpr int T = 512;
-    constexpr uint32_t kHtLog = 12;
+    constexpr uint32_t kHtLog = kTile == 2048 ? 11 : kTile == 4096 ? 12 : 13;
     static_assert(kTile == (1u << kHtLog), "fine tile = dedup table size");
     constexpr uint32_t kDead = 0xFFFFFFFFu;
     // <= 256 regions per coarse bin on this path (rbits - 7 <= 8)
@@ -1320,7 +1331,8 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
                 local = i - lstart[b];
             }
             const uint32_t gpos = cursor[b] + local;
-            w.keys[gpos] = k;
+            if (SS_FS_WRITE & 1) w.keys[gpos] = k;
+            if (!(SS_FS_WRITE & 4)) continue;
             if (x & kWeighted) {
                 const uint32_t p = x & ~kWeighted;
                 w.bidx[gpos] = src_idx[p];          // the read index, flag kept
@@ -2243,6 +2255,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
                                (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
                                (unsigned long long*)d_first_bad);
+            // SS_PF_STOP (measurement only, results invalid): 1 = end after the coarse pass, 2 = after
+            // the fine scatter
+            if (SS_PF_STOP == 1) return ss_check(hipGetLastError(), "coarse pass");
             const unsigned fine_blocks = kCB * kFinePerBin;
             hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill);
@@ -2254,6 +2269,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL(k_pf_order, dim3(1), dim3(512), 0, s, (const uint32_t*)c->ws_fill, cap1, c->ws_order);
             hipLaunchKernelGGL(k_pf_scatter, dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
+            if (SS_PF_STOP == 2) return ss_check(hipGetLastError(), "fine scatter");
             w.bkey = w.keys;
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
