@@ -27,18 +27,37 @@ def test_header_symbols_exported():
     assert lib.ss_abi_version() == 1
 
 
+_NO_DEVICE_CHILD = r"""
+import ctypes as C, sys
+sys.path.insert(0, sys.argv[1])
+from shortseq_amd import _native
+lib = _native.lib()
+n = C.c_int(-1)
+lib.ss_device_count(C.byref(n))
+assert n.value == 0, ("device visible", n.value)
+fb = C.c_uint64(0)
+assert lib.ss_encode_fixed(None, 10, 32, 32, None, 1, C.addressof(fb), None) != 0
+import shortseq_amd as sq
+try:
+    sq.ShortSeqCounter([b"ACGT"] * 10, device="cuda")
+except Exception as e:
+    print("RAISED", type(e).__name__)
+else:
+    raise SystemExit("counted a batch without a device")
+"""
+
+
 def test_no_device_is_an_error_not_a_fallback():
-    """Without a GPU the device entry points fail loudly (SS_EHIP/EARG), they never compute."""
-    from shortseq_amd import _native
-    lib = _native.lib()
-    n = C.c_int(-1)
-    rc = lib.ss_device_count(C.byref(n))
-    if n.value > 0:
-        import pytest
-        pytest.skip("a HIP device is present: this checks the CPU-only failure mode")
-    fb = C.c_uint64(0)
-    rc = lib.ss_encode_fixed(None, 10, 32, 32, None, 1, C.addressof(fb), None)
-    assert rc != 0
+    """Without a GPU the device entry points fail loudly (SS_EHIP/EARG) and a batch forced onto the
+    GPU raises: nothing computes on a silent fallback.  Runs in a child that sees no device
+    (HIP_VISIBLE_DEVICES=-1), so it checks the same thing on a GPU box as on a CPU-only host."""
+    import subprocess
+    import sys
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1")
+    r = subprocess.run([sys.executable, "-c", _NO_DEVICE_CHILD, REPO], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "RAISED" in r.stdout, r.stdout
 
 
 def test_product_does_not_import_oracle():
