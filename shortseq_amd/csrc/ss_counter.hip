@@ -37,7 +37,11 @@ constexpr int kThreads = 256;
 constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
 constexpr uint32_t kExtractBlocks = 4096;  // extract passes: fixed grid, contiguous slot ranges
 constexpr uint32_t kExtractT = 64;         // ONE wave per extract block: slot order is output order
-constexpr uint32_t kSliceLogMax = 11;      // region slice: 2048 slots (one LDS-resident aggregation)
+#ifndef SS_SLICE_LOG_MAX
+#define SS_SLICE_LOG_MAX 11
+#endif
+constexpr uint32_t kSliceLogMax = SS_SLICE_LOG_MAX;   // region slice: 2048 slots (one LDS-resident aggregation)
+constexpr uint32_t kMwSliceLog = 11;                  // multi-word tables: the k_mw_aggregate LDS bound
 #ifndef SS_PC_BLOCKS
 #define SS_PC_BLOCKS 1024
 #endif
@@ -829,6 +833,20 @@ constexpr uint32_t kHeavy = SS_PF_HEAVY;
 #ifndef SS_PF_STOP
 #define SS_PF_STOP 0
 #endif
+// k_pf_coarse: issue the next tile's loads right after this tile's encode (1) or at the top of
+// each tile (0)
+#ifndef SS_PF_PREFETCH
+#define SS_PF_PREFETCH 0
+#endif
+// nontemporal loads of the record streams read exactly once (fine count / scatter, aggregate)
+#ifndef SS_NT_LOADS
+#define SS_NT_LOADS 0
+#endif
+template <typename V>
+__device__ __forceinline__ V ld_once(const V* p) {
+    if constexpr (SS_NT_LOADS != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
 
 // sub-bin capacity of the optimistic partition for a batch of n reads (host and device agree)
 __host__ __device__ __forceinline__ uint64_t pf_cap1(uint64_t n) {
@@ -946,8 +964,9 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
     // LDS.  The next tile's rank atomics only touch lcount (zeroed before B) and its staging waits
     // for its own barrier B, which every wave reaches only after this tile's write-out.  A tile with
     // a heavy bin adds three: (D) deduplicated, (E) survivors counted, (F) heavy bins reserved.
+    if (SS_PF_PREFETCH && blockIdx.x < tiles) load_tile(blockIdx.x);
     for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        load_tile(tile);
+        if (!SS_PF_PREFETCH) load_tile(tile);
         uint64_t key[RPL];
         uint32_t bin[RPL], rank[RPL];
         const uint64_t t0 = tile * TILE;
@@ -966,6 +985,7 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                 rank[j] = atomicAdd(&lcount[bin[j]], 1u);
             }
         }
+        if (SS_PF_PREFETCH && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
         __syncthreads();                                                  // (A)
         if (threadIdx.x < 64) {
             const uint32_t lane = threadIdx.x, b0 = 2 * lane;
@@ -1113,7 +1133,7 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
     const uint4* src = (const uint4*)(w.areg + (uint64_t)blockIdx.x * cap1);
     const uint64_t n16 = (hi - lo + 15) / 16;
     for (uint64_t q = threadIdx.x; q < n16; q += T) {
-        const uint4 v = src[q];
+        const uint4 v = SS_NT_LOADS ? ld_stream(&src[q]) : src[q];
         const uint32_t m = (uint32_t)min((uint64_t)16, hi - 16 * q);
         const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1227,8 +1247,8 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
         for (int j = 0; j < (int)(kTile / T); ++j) {
             const uint32_t e = j * T + threadIdx.x;
             if (e < cnt) {
-                nkey[j] = src[t0 + e];
-                const uint32_t x = src_idx[t0 + e];
+                nkey[j] = ld_once(&src[t0 + e]);
+                const uint32_t x = ld_once(&src_idx[t0 + e]);
                 nidx[j] = (x & kWeighted) ? kWeighted | (uint32_t)(t0 + e) : x;
             }
         }
@@ -1442,8 +1462,8 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         for (int q = 0; q < kP; ++q) {
             const uint32_t f = e0 + q * T + threadIdx.x;
             nel[q] = f < total ? flat_at(f) : 0u;
-            nkey[q] = f < total ? w.bkey[nel[q]] : kEmpty;
-            nidx[q] = f < total ? w.bidx[nel[q]] : 0u;
+            nkey[q] = f < total ? (uint64_t)ld_once(&w.bkey[nel[q]]) : kEmpty;
+            nidx[q] = f < total ? ld_once(&w.bidx[nel[q]]) : 0u;
         }
     };
     if (total) load_step(0);
@@ -1827,7 +1847,7 @@ __global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, con
 }
 
 constexpr uint32_t kMwT = 1024;
-constexpr uint32_t kMwPerThread = (2u << kSliceLogMax) / kMwT;
+constexpr uint32_t kMwPerThread = (2u << kMwSliceLog) / kMwT;
 
 template <int T>
 __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint64_t* __restrict__ words,
@@ -2217,7 +2237,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         // dynamic LDS above the 64 KB default: opt in once per kernel (host-side attribute)
         static bool attrs_set = false;
         if (!attrs_set) {
-            const int agg_max = (int)(2 * (1u << kSliceLogMax) * 16 + (1u << kSliceLogMax) * 8 + 8);
+            const int agg_max = (int)(2 * (1u << kMwSliceLog) * 16 + (1u << kMwSliceLog) * 8 + 8);
             hipError_t ea = hipFuncSetAttribute((const void*)k_pc_keys<T1, U1>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kMaxRegions * 4);
             if (ea == hipSuccess)
@@ -2229,6 +2249,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_mw_aggregate<kMwT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          agg_max);
+            if (ea == hipSuccess && kSliceLogMax > 11)
+                ea = hipFuncSetAttribute((const void*)k_pc_aggregate_slice<kAggSliceT>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (1u << kSliceLogMax) * 16);
             if (ea != hipSuccess) return ss_check(ea, "hipFuncSetAttribute (dynamic LDS)");
             attrs_set = true;
         }

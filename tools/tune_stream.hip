@@ -16,6 +16,62 @@
 #include "../shortseq_amd/csrc/ss_codec.hip"
 #include "../shortseq_amd/csrc/ss_runtime.hip"
 
+namespace {
+// (measured slower than k_encode_ham_dense: 2.32-2.45 vs 1.87-1.94 ms, gpurun_out/tune_c3.log)
+// Dense fused encode + hamming for 96-nt reads (3 PEXT words, no alias carries) without LDS or a
+// barrier: a lane owns one 32-nt word (its two dwordx4 chunks), a wave streams 63 consecutive words =
+// 21 whole reads (lane 63 idles, 1.6 % of the lanes), and the three lanes of a read add their
+// distances with two shuffles; the read's first lane stores the sum.  Word chunk c of the block =
+// j * (T / 64) + wave, so at each j the block's waves read one contiguous span.
+template <int T, int U, bool NTST>
+__global__ __launch_bounds__(T) void k_encode_ham_w3(G16Args a) {
+    constexpr uint32_t NWV = T / 64, RPC = 21, QPC = 63, RPB = RPC * NWV * U;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t m = lane / 3u, p = lane - 3u * m;
+    const uint64_t r0 = (uint64_t)blockIdx.x * RPB;
+    const uint32_t nr = (uint32_t)min((uint64_t)RPB, a.n - r0);
+    const uint32_t nw = 3u * nr;
+    const uint64_t q0 = r0 * 3u;
+    uint4 x[U][2];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t ql = (j * NWV + wv) * QPC + lane;
+        const bool live = lane < QPC && ql < nw;
+        x[j][0] = live ? ld_stream(&a.in[2 * (q0 + ql)]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+        x[j][1] = live ? ld_stream(&a.in[2 * (q0 + ql) + 1])
+                       : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    }
+    const uint64_t ref = ((uint64_t)a.ref32[2 * p + 1] << 32) | a.ref32[2 * p];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t ql = (j * NWV + wv) * QPC + lane;
+        const uint32_t rb = (j * NWV + wv) * RPC + m;                      // block-local read
+        const bool live = lane < QPC && ql < nw;
+        const Enc32 lo = encode16(x[j][0].x, x[j][0].y, x[j][0].z, x[j][0].w, false);
+        const Enc32 hi = encode16(x[j][1].x, x[j][1].y, x[j][1].z, x[j][1].w, false);
+        report_bad(live && (lo.bad | hi.bad) != 0u, r0 + rb, a.first_bad);
+        const uint64_t v = ((uint64_t)hi.v << 32) | lo.v;
+        if (live && a.out32) {
+            uint64_t* dst = (uint64_t*)a.out32 + q0 + ql;
+            if constexpr (NTST) __builtin_nontemporal_store(v, dst);
+            else *dst = v;
+        }
+        const uint32_t d = live ? ham64(v ^ ref) : 0u;
+        const uint32_t d1 = __shfl(d, (int)min(lane + 1u, 63u)), d2 = __shfl(d, (int)min(lane + 2u, 63u));
+        if (live && p == 0) {
+            if constexpr (NTST) __builtin_nontemporal_store(d + d1 + d2, &a.counts[r0 + rb]);
+            else a.counts[r0 + rb] = d + d1 + d2;
+        }
+    }
+}
+
+template <int T, int U, bool NTST>
+void launch_ham_w3(const G16Args& a, hipStream_t s) {
+    const uint64_t rpb = 21ull * (T / 64) * U;
+    hipLaunchKernelGGL((k_encode_ham_w3<T, U, NTST>), dim3(grid_for(a.n, rpb)), dim3(T), 0, s, a);
+}
+}  // namespace
+
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -283,6 +339,7 @@ static bool same(const void* d_a, const void* d_b, size_t bytes, const char* wha
 
 int main(int argc, char** argv) {
     g_reps = argc > 1 ? atoi(argv[1]) : 20;
+    const bool only_c3 = argc > 2 && strcmp(argv[2], "c3") == 0;
     const uint64_t n2 = 100000000ull;              // C2 reads
     const uint64_t n3 = 100000000ull;              // C3 reads
     uint8_t* in;
@@ -324,7 +381,7 @@ int main(int argc, char** argv) {
     }
     for (int pass = 0; pass < 2; ++pass) {
     // ---------------- C2 ----------------
-    {
+    if (!only_c3) {
         const uint32_t L = 32;
         const double bytes = (double)n2 * 40;
         G16Args a = make_args(in, n2, L, w_ref, nullptr, nullptr, fb);
@@ -373,15 +430,37 @@ int main(int argc, char** argv) {
             launch_ham_dense<kPathPext, 256, 4, true>(b, 0);
             same(c_ref, c_var, n3 * 4, "ham_dense T256 U4 distances");
         }
+        if (pass == 0) {
+            G16Args b = make_args(in, n3, L, w_var, ref, c_var, fb);
+            CK(hipMemset(w_var, 0, n3 * 24));
+            CK(hipMemset(c_var, 0, n3 * 4));
+            launch_ham_w3<256, 4, true>(b, 0);
+            same(w_ref, w_var, n3 * 24, "ham_w3 T256 U4 words");
+            same(c_ref, c_var, n3 * 4, "ham_w3 T256 U4 distances");
+            CK(hipMemset(w_var, 0, n3 * 24));
+            CK(hipMemset(c_var, 0, n3 * 4));
+            hipLaunchKernelGGL((k_ham_wave<6, 8>), dim3((unsigned)((n3 + 511) / 512)), dim3(512), 0, 0, (const uint4*)in,
+                               (uint32_t*)w_var, (const uint32_t*)ref, c_var, n3, fb);
+            same(w_ref, w_var, n3 * 24, "wave WPB8 words");
+            same(c_ref, c_var, n3 * 4, "wave WPB8 distances");
+        }
         printf("C3 96-nt fused encode + hamming, %llu reads (pass %d)\n", (unsigned long long)n3, pass);
+        timeit("C3 ham_w3 T256 U2", bytes, [&] { launch_ham_w3<256, 2, true>(a, 0); });
+        timeit("C3 wave WPB4", bytes, [&] {
+            hipLaunchKernelGGL((k_ham_wave<6, 4>), dim3((unsigned)((n3 + 255) / 256)), dim3(256), 0, 0, (const uint4*)in,
+                               (uint32_t*)w_var, (const uint32_t*)ref, c_var, n3, fb); });
+        timeit("C3 wave WPB2", bytes, [&] {
+            hipLaunchKernelGGL((k_ham_wave<6, 2>), dim3((unsigned)((n3 + 127) / 128)), dim3(128), 0, 0, (const uint4*)in,
+                               (uint32_t*)w_var, (const uint32_t*)ref, c_var, n3, fb); });
+        timeit("C3 wave WPB16", bytes, [&] {
+            hipLaunchKernelGGL((k_ham_wave<6, 16>), dim3((unsigned)((n3 + 1023) / 1024)), dim3(1024), 0, 0, (const uint4*)in,
+                               (uint32_t*)w_var, (const uint32_t*)ref, c_var, n3, fb); });
         timeit("C3 ham_dense T768 U2 (r1 production)", bytes, [&] { launch_ham_dense<kPathPext, 768, 2, true>(a, 0); });
         timeit("C3 ham_dense T256 U3", bytes, [&] { launch_ham_dense<kPathPext, 256, 3, true>(a, 0); });
         timeit("C3 ham_dense T128 U6", bytes, [&] { launch_ham_dense<kPathPext, 128, 6, true>(a, 0); });
         timeit("C3 ham_dense T384 U2", bytes, [&] { launch_ham_dense<kPathPext, 384, 2, true>(a, 0); });
         timeit("C3 ham_dense T512 U3", bytes, [&] { launch_ham_dense<kPathPext, 512, 3, true>(a, 0); });
         timeit("C3 ham_dense T192 U4", bytes, [&] { launch_ham_dense<kPathPext, 192, 4, true>(a, 0); });
-        timeit("C3 ham_dense T256 U6", bytes, [&] { launch_ham_dense<kPathPext, 256, 6, true>(a, 0); });
-        timeit("C3 ham_dense T256 U4", bytes, [&] { launch_ham_dense<kPathPext, 256, 4, true>(a, 0); });
         timeit("C3 ham_dense T128 U3", bytes, [&] { launch_ham_dense<kPathPext, 128, 3, true>(a, 0); });
         timeit("C3 wave WPB8", bytes, [&] {
             hipLaunchKernelGGL((k_ham_wave<6, 8>), dim3((unsigned)((n3 + 511) / 512)), dim3(512), 0, 0, (const uint4*)in,
