@@ -833,8 +833,8 @@ constexpr uint32_t kHeavy = SS_PF_HEAVY;
 #ifndef SS_PF_STOP
 #define SS_PF_STOP 0
 #endif
-// k_pf_coarse: issue the next tile's loads right after this tile's encode (1) or at the top of
-// each tile (0)
+// k_pf_coarse: issue the next tile's loads right after this tile's encode (1), after the tile's
+// reservation barrier (2), or at the top of each tile (0)
 #ifndef SS_PF_PREFETCH
 #define SS_PF_PREFETCH 0
 #endif
@@ -985,7 +985,7 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
                 rank[j] = atomicAdd(&lcount[bin[j]], 1u);
             }
         }
-        if (SS_PF_PREFETCH && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
+        if (SS_PF_PREFETCH == 1 && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
         __syncthreads();                                                  // (A)
         if (threadIdx.x < 64) {
             const uint32_t lane = threadIdx.x, b0 = 2 * lane;
@@ -1011,6 +1011,9 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             hcnt[b0 + 1] = 0;
         }
         __syncthreads();                                                  // (B)
+        // prefetch form 2: the next tile's loads go out after the reservation, so wave 0's wait for
+        // its atomics' return values (vmcnt counts in issue order) does not also wait for them
+        if (SS_PF_PREFETCH == 2 && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
         const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
