@@ -431,7 +431,19 @@ constexpr uint32_t kCoarseBits = 7;    // 128 coarse bins for the first partitio
 // in coarse order, bcnt in region order).  Batch-local indices are < 2^31 (ss_counter_reserve).
 constexpr uint32_t kWeighted = 0x80000000u;
 
+// Fine-scatter output record: key and read index in one 12-B dwordx3 (SS_FS_AOS 1).  Against two
+// streams (u64 keys + u32 indices): the scatter 2.54 -> 2.21-2.37 ms at its end, the insert -0.01 to
+// -0.14 ms uniform 2^24 over 3 same-box rounds (the aggregate's dwordx3 loads give part of it back);
+// a 16-B record with the count inside measured no better (scripts/ab_counter.sh, gpurun_out/ab).
+struct __attribute__((packed, aligned(4))) Rec12 {
+    uint32_t klo, khi, idx;
+};
+#ifndef SS_FS_AOS
+#define SS_FS_AOS 1
+#endif
+
 struct PartWs {
+    const Rec12* brec; // optimistic path with SS_FS_AOS: the region-ordered records (else null)
     uint64_t* keys;    // P1 output; P3 second-pass output (bucketed by region)
     uint64_t* akey;    // first-pass output (bucketed by coarse bin)
     uint32_t* aidx;
@@ -1354,6 +1366,23 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
                 local = i - lstart[b];
             }
             const uint32_t gpos = cursor[b] + local;
+            if constexpr (SS_FS_AOS != 0) {
+                uint32_t xi = x;
+                if (x & kWeighted) {
+                    const uint32_t p = x & ~kWeighted;
+                    xi = src_idx[p];                // the read index, flag kept
+                    w.bcnt[gpos] = src_cnt[p];
+                } else if (c > 1) {
+                    xi = x | kWeighted;
+                    w.bcnt[gpos] = c;
+                }
+                Rec12 r;
+                r.klo = (uint32_t)k;
+                r.khi = (uint32_t)(k >> 32);
+                r.idx = xi;
+                ((Rec12*)w.keys)[gpos] = r;
+                continue;
+            }
             if (SS_FS_WRITE & 1) w.keys[gpos] = k;
             if (!(SS_FS_WRITE & 4)) continue;
             if (x & kWeighted) {
@@ -1465,6 +1494,17 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         for (int q = 0; q < kP; ++q) {
             const uint32_t f = e0 + q * T + threadIdx.x;
             nel[q] = f < total ? flat_at(f) : 0u;
+            if (SS_FS_AOS != 0 && w.brec) {
+                if (f < total) {
+                    const Rec12 r = w.brec[nel[q]];
+                    nkey[q] = ((uint64_t)r.khi << 32) | r.klo;
+                    nidx[q] = r.idx;
+                } else {
+                    nkey[q] = kEmpty;
+                    nidx[q] = 0u;
+                }
+                continue;
+            }
             nkey[q] = f < total ? (uint64_t)ld_once(&w.bkey[nel[q]]) : kEmpty;
             nidx[q] = f < total ? ld_once(&w.bidx[nel[q]]) : 0u;
         }
@@ -2109,7 +2149,7 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     // 128 x 8 sub-bins of cap1 = 2.5 x the mean sub-bin load + 1024 slots (pf_cap1)
     const uint64_t cap1 = pf_cap1(max_reads);
     const uint64_t acap = kNFill * cap1 > max_reads ? kNFill * cap1 : max_reads;
-    hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * sizeof(uint64_t));
+    hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * (SS_FS_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(uint64_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_acnt, acap * sizeof(uint32_t));
@@ -2227,6 +2267,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         w.rstart = c->ws_rstart;
         w.tot = c->ws_tot;
         w.bkey = nullptr;
+        w.brec = nullptr;
         w.R = (uint32_t)(c->cap >> c->slice_log);
         w.rbits = c->log2cap - c->slice_log;
         const uint32_t S = 1u << c->slice_log;
@@ -2297,6 +2338,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
             if (SS_PF_STOP == 2) return ss_check(hipGetLastError(), "fine scatter");
             w.bkey = w.keys;
+            if (SS_FS_AOS) w.brec = (const Rec12*)w.keys;
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
             // records that found their sub-bin full (none unless many distinct keys pile into a bin)
