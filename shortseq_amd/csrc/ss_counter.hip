@@ -441,6 +441,10 @@ struct __attribute__((packed, aligned(4))) Rec12 {
 #ifndef SS_FS_AOS
 #define SS_FS_AOS 1
 #endif
+// coarse records as the same 12-B {key, read index} (areg and the sparse counts stay apart)
+#ifndef SS_PF_AOS
+#define SS_PF_AOS 0
+#endif
 
 struct PartWs {
     const Rec12* brec; // optimistic path with SS_FS_AOS: the region-ordered records (else null)
@@ -1107,6 +1111,16 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
 #else
                 const uint64_t at = (uint64_t)(b * kFinePerBin + sub) * cap1 + pos;
 #endif
+                if constexpr (SS_PF_AOS != 0) {
+                    Rec12 r;
+                    r.klo = (uint32_t)k;
+                    r.khi = (uint32_t)(k >> 32);
+                    r.idx = c > 1 ? (sidx[i] | kWeighted) : sidx[i];
+                    ((Rec12*)w.akey)[at] = r;
+                    w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
+                    if (c > 1) w.acnt[at] = c;
+                    continue;
+                }
                 if (SS_PF_WRITE & 1) w.akey[at] = k;
                 if (SS_PF_WRITE & 2) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
                 if (c > 1) {
@@ -1250,7 +1264,9 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
     fine_range(fb, fill, cap1, bin, lo, hi);
     const uint32_t r0 = bin * nb;
     const uint64_t* src = w.akey + (uint64_t)fb * cap1;
+    const Rec12* srec = (const Rec12*)w.akey + (uint64_t)fb * cap1;     // SS_PF_AOS layout
     const uint32_t* src_idx = w.aidx + (uint64_t)fb * cap1;
+    auto rec_idx = [&](uint32_t p) -> uint32_t { return SS_PF_AOS ? srec[p].idx : src_idx[p]; };
     const uint32_t* src_cnt = w.acnt + (uint64_t)fb * cap1;
     for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] = w.hist[(uint64_t)fb * nb + i];
     __syncthreads();
@@ -1262,8 +1278,15 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
         for (int j = 0; j < (int)(kTile / T); ++j) {
             const uint32_t e = j * T + threadIdx.x;
             if (e < cnt) {
-                nkey[j] = ld_once(&src[t0 + e]);
-                const uint32_t x = ld_once(&src_idx[t0 + e]);
+                uint32_t x;
+                if constexpr (SS_PF_AOS != 0) {
+                    const Rec12 r = srec[t0 + e];
+                    nkey[j] = ((uint64_t)r.khi << 32) | r.klo;
+                    x = r.idx;
+                } else {
+                    nkey[j] = ld_once(&src[t0 + e]);
+                    x = ld_once(&src_idx[t0 + e]);
+                }
                 nidx[j] = (x & kWeighted) ? kWeighted | (uint32_t)(t0 + e) : x;
             }
         }
@@ -1370,7 +1393,7 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
                 uint32_t xi = x;
                 if (x & kWeighted) {
                     const uint32_t p = x & ~kWeighted;
-                    xi = src_idx[p];                // the read index, flag kept
+                    xi = rec_idx(p);                // the read index, flag kept
                     w.bcnt[gpos] = src_cnt[p];
                 } else if (c > 1) {
                     xi = x | kWeighted;
@@ -1387,7 +1410,7 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
             if (!(SS_FS_WRITE & 4)) continue;
             if (x & kWeighted) {
                 const uint32_t p = x & ~kWeighted;
-                w.bidx[gpos] = src_idx[p];          // the read index, flag kept
+                w.bidx[gpos] = rec_idx(p);          // the read index, flag kept
                 w.bcnt[gpos] = src_cnt[p];
             } else if (c > 1) {
                 w.bidx[gpos] = x | kWeighted;
@@ -2150,7 +2173,7 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     const uint64_t cap1 = pf_cap1(max_reads);
     const uint64_t acap = kNFill * cap1 > max_reads ? kNFill * cap1 : max_reads;
     hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * (SS_FS_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(uint64_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * (SS_PF_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_acnt, acap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_areg, acap);
