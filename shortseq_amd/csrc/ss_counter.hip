@@ -950,14 +950,15 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t sub = blockIdx.x % kFinePerBin;   // this block's sub-bin of every bin
     uint4 nx[RPL][2];
+    // branch-free loads (read index clamped to the last read; lanes past n are never live): the
+    // compiler then waits for each chunk just before its encode instead of for all 2 * RPL loads
+    const uint32_t hi16 = cpr > 1 ? 1u : 0u;    // L = 16: one chunk (the high half reads 'A's below)
     auto load_tile = [&](uint64_t tile) {
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
-            const uint64_t r = tile * TILE + j * T + threadIdx.x;
-            const bool ok = r < n;
-            nx[j][0] = ok ? ld_stream(&in[r * stride16]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
-            nx[j][1] = (ok && cpr > 1) ? ld_stream(&in[r * stride16 + 1])
-                                      : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+            const uint64_t r = min(tile * TILE + j * T + threadIdx.x, n - 1);
+            nx[j][0] = ld_stream(&in[r * stride16]);
+            nx[j][1] = ld_stream(&in[r * stride16 + hi16]);
         }
     };
     // wave 0, one bin: reserve c slots of sub-bin (b, sub); the part past cap1 reserves spill records
@@ -992,7 +993,8 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             const uint64_t r = t0 + j * T + threadIdx.x;
             // table path for both chunks (L <= 32); the low chunk's alias carry into the high half
             const Enc32 a = encode16(nx[j][0].x, nx[j][0].y, nx[j][0].z, nx[j][0].w, true);
-            const Enc32 b = encode16(nx[j][1].x, nx[j][1].y, nx[j][1].z, nx[j][1].w, true);
+            const uint4 h = hi16 ? nx[j][1] : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+            const Enc32 b = encode16(h.x, h.y, h.z, h.w, true);
             const bool live = r < n;
             report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
             key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
@@ -1161,13 +1163,22 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
     // the coarse pass wrote each record's region-in-bin byte (1 B per record instead of the 8-B key)
     const uint4* src = (const uint4*)(w.areg + (uint64_t)blockIdx.x * cap1);
     const uint64_t n16 = (hi - lo + 15) / 16;
-    for (uint64_t q = threadIdx.x; q < n16; q += T) {
-        const uint4 v = SS_NT_LOADS ? ld_stream(&src[q]) : src[q];
-        const uint32_t m = (uint32_t)min((uint64_t)16, hi - 16 * q);
-        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    // four dwordx4 per thread per step, loaded branch-free (clamped) before any is counted
+    constexpr int kQ = 4;
+    for (uint64_t q0 = threadIdx.x; q0 < n16; q0 += (uint64_t)kQ * T) {
+        uint4 v[kQ];
 #pragma unroll
-        for (uint32_t j = 0; j < 16; ++j)
-            if (j < m) atomicAdd(&h[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+        for (int u = 0; u < kQ; ++u) v[u] = src[min(q0 + (uint64_t)u * T, n16 - 1)];
+#pragma unroll
+        for (int u = 0; u < kQ; ++u) {
+            const uint64_t q = q0 + (uint64_t)u * T;
+            if (q >= n16) break;
+            const uint32_t m = (uint32_t)min((uint64_t)16, hi - 16 * q);
+            const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (j < m) atomicAdd(&h[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < rpb; i += T) w.hist[(uint64_t)blockIdx.x * rpb + i] = h[i];
@@ -1272,22 +1283,21 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
     __syncthreads();
     uint64_t nkey[kTile / T];
     uint32_t nidx[kTile / T];
+    // Unconditional loads (index clamped to the sub-bin's last record; lanes past the tile are never
+    // used) with the raw index word kept: no branch and no use of a loaded value between the loads,
+    // so a tile's loads all go out back to back (a conditional load, or transforming the index right
+    // after loading it, makes the compiler wait for each load before issuing the next).
     auto load_tile = [&](uint64_t t0) {
-        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
-            const uint32_t e = j * T + threadIdx.x;
-            if (e < cnt) {
-                uint32_t x;
-                if constexpr (SS_PF_AOS != 0) {
-                    const Rec12 r = srec[t0 + e];
-                    nkey[j] = ((uint64_t)r.khi << 32) | r.klo;
-                    x = r.idx;
-                } else {
-                    nkey[j] = ld_once(&src[t0 + e]);
-                    x = ld_once(&src_idx[t0 + e]);
-                }
-                nidx[j] = (x & kWeighted) ? kWeighted | (uint32_t)(t0 + e) : x;
+            const uint64_t at = min(t0 + j * T + threadIdx.x, hi - 1);
+            if constexpr (SS_PF_AOS != 0) {
+                const Rec12 r = srec[at];
+                nkey[j] = ((uint64_t)r.khi << 32) | r.klo;
+                nidx[j] = r.idx;
+            } else {
+                nkey[j] = ld_once(&src[at]);
+                nidx[j] = ld_once(&src_idx[at]);
             }
         }
     };
@@ -1302,9 +1312,11 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
             key[j] = nkey[j];
-            idx[j] = nidx[j];
+            // a weighted coarse record is staged with its position in the sub-bin (its index and
+            // count are fetched at the write-out)
+            idx[j] = (nidx[j] & kWeighted) ? kWeighted | (uint32_t)(t0 + j * T + threadIdx.x) : nidx[j];
         }
-        if (t0 + kTile < hi) load_tile(t0 + kTile);
+        load_tile(t0 + kTile);
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
             const uint32_t e = j * T + threadIdx.x;
@@ -1460,7 +1472,7 @@ constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools
 // fresh: the table was reset and the reset is still pending (ss_counter_reset is lazy): the slice is
 // taken as empty instead of loaded, and written back whole (empty slots as the 0xFF reset pattern),
 // which replaces the table-sized reset memset and the slice read.
-template <int T>
+template <int T, bool REC12>
 __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index, bool fresh = false) {
     const uint32_t S = (uint32_t)t.slice_mask + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1509,27 +1521,26 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
             if (f >= pre[sg]) e = seg0[sg] + (f - pre[sg]);
         return e;
     };
-    // software-pipelined: the next step's loads are in flight while this step's records are folded
+    // software-pipelined: the next step's loads are in flight while this step's records are folded.
+    // Every lane loads unconditionally (index clamped to the last record; lanes past the end are
+    // masked by `valid` when folding) and the next step is always prefetched: with no branch around
+    // a load the kP loads go out back to back, where a conditional load makes the compiler wait for
+    // each one before the next (vmcnt(0) at every join).
     uint64_t nkey[kP];
     uint32_t nidx[kP], nel[kP];
     auto load_step = [&](uint32_t e0) {
 #pragma unroll
         for (int q = 0; q < kP; ++q) {
-            const uint32_t f = e0 + q * T + threadIdx.x;
-            nel[q] = f < total ? flat_at(f) : 0u;
-            if (SS_FS_AOS != 0 && w.brec) {
-                if (f < total) {
-                    const Rec12 r = w.brec[nel[q]];
-                    nkey[q] = ((uint64_t)r.khi << 32) | r.klo;
-                    nidx[q] = r.idx;
-                } else {
-                    nkey[q] = kEmpty;
-                    nidx[q] = 0u;
-                }
-                continue;
+            const uint32_t f = min(e0 + q * T + threadIdx.x, total - 1u);
+            nel[q] = flat_at(f);
+            if constexpr (REC12) {
+                const Rec12 r = w.brec[nel[q]];
+                nkey[q] = ((uint64_t)r.khi << 32) | r.klo;
+                nidx[q] = r.idx;
+            } else {
+                nkey[q] = ld_once(&w.bkey[nel[q]]);
+                nidx[q] = ld_once(&w.bidx[nel[q]]);
             }
-            nkey[q] = f < total ? (uint64_t)ld_once(&w.bkey[nel[q]]) : kEmpty;
-            nidx[q] = f < total ? ld_once(&w.bidx[nel[q]]) : 0u;
         }
     };
     if (total) load_step(0);
@@ -1542,15 +1553,19 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
             idx[q] = nidx[q];
             el[q] = nel[q];
         }
-        if (e0 + kP * T < total) load_step(e0 + kP * T);
+        // weighted records' counts (a conditional load) before the prefetch: waiting for them then
+        // does not wait for the next step's loads as well (vmcnt counts in issue order)
+        uint32_t cw[kP];
 #pragma unroll
         for (int q = 0; q < kP; ++q) {
             const bool valid = e0 + q * T + threadIdx.x < total;
-            uint32_t c = 1, ix = idx[q];
-            if (valid && (ix & kWeighted)) {
-                c = w.bcnt[el[q]];
-                ix &= ~kWeighted;
-            }
+            cw[q] = (valid && (idx[q] & kWeighted)) ? w.bcnt[el[q]] : 1u;
+        }
+        load_step(e0 + kP * T);
+#pragma unroll
+        for (int q = 0; q < kP; ++q) {
+            const bool valid = e0 + q * T + threadIdx.x < total;
+            uint32_t c = cw[q], ix = idx[q] & ~kWeighted;
             if (valid && key[q] == kEmpty) {
                 atomicAdd(&sent[0], c);
                 atomicMin(&sent[1], ix);
@@ -2317,7 +2332,10 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                 ea = hipFuncSetAttribute((const void*)k_mw_aggregate<kMwT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          agg_max);
             if (ea == hipSuccess && kSliceLogMax > 11)
-                ea = hipFuncSetAttribute((const void*)k_pc_aggregate_slice<kAggSliceT>,
+                ea = hipFuncSetAttribute((const void*)k_pc_aggregate_slice<kAggSliceT, true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (1u << kSliceLogMax) * 16);
+            if (ea == hipSuccess && kSliceLogMax > 11)
+                ea = hipFuncSetAttribute((const void*)k_pc_aggregate_slice<kAggSliceT, false>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (1u << kSliceLogMax) * 16);
             if (ea != hipSuccess) return ss_check(ea, "hipFuncSetAttribute (dynamic LDS)");
             attrs_set = true;
@@ -2361,9 +2379,14 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
             if (SS_PF_STOP == 2) return ss_check(hipGetLastError(), "fine scatter");
             w.bkey = w.keys;
-            if (SS_FS_AOS) w.brec = (const Rec12*)w.keys;
-            hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
-                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
+            if (SS_FS_AOS) {
+                w.brec = (const Rec12*)w.keys;
+                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, true>), dim3(w.R), dim3(kAggSliceT),
+                                   ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
+            } else {
+                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(w.R), dim3(kAggSliceT),
+                                   ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
+            }
             // records that found their sub-bin full (none unless many distinct keys pile into a bin)
             hipLaunchKernelGGL(k_spill_insert, dim3(1024), dim3(256), 0, s, t, w, (const uint32_t*)c->ws_fill,
                                base_index);
@@ -2401,7 +2424,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL((k_mw_aggregate<kMwT>), dim3(w.R), dim3(kMwT), mw_lds, s, t, w,
                                (const uint64_t*)c->ws_words, base_index);
         else
-            hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT>), dim3(w.R), dim3(kAggSliceT),
+            hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
         if (!multi) c->occ_src = 1;
         return ss_check(hipGetLastError(), "partitioned insert");
