@@ -823,7 +823,14 @@ constexpr uint32_t kFinePerBin = SS_FINE_PER_BIN;    // fine-pass blocks per coa
 constexpr uint32_t kNFill = kCB * kFinePerBin;       // sub-bin fill counters
 constexpr uint32_t kSpillCtr = kNFill;               // the spill list's record counter
 constexpr uint32_t kFillWords = (kNFill + 1) * kFillStride;   // counters + the spill counter
-__host__ __device__ __forceinline__ uint32_t fill_at(uint32_t b) { return b * kFillStride; }
+// Sub-bins (2p, s) and (2p + 1, s) of a coarse bin pair share one 64-bit word (low / high half), so
+// the coarse pass reserves both bins a wave-0 lane scans with ONE 64-bit atomic (a sub-bin's fill
+// stays below 2^31: no carry into the high half).  fb = bin * kFinePerBin + sub.
+static_assert(kFillStride == 1, "paired fill counters");
+__host__ __device__ __forceinline__ uint32_t fill_at(uint32_t fb) {
+    const uint32_t bin = fb / kFinePerBin, sub = fb % kFinePerBin;
+    return (((bin >> 1) * kFinePerBin + sub) << 1) | (bin & 1u);
+}
 #ifndef SS_PF_RPL
 #define SS_PF_RPL 16
 #endif
@@ -961,17 +968,27 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             nx[j][1] = ld_stream(&in[r * stride16 + hi16]);
         }
     };
-    // wave 0, one bin: reserve c slots of sub-bin (b, sub); the part past cap1 reserves spill records
-    auto reserve = [&](uint32_t b, uint32_t c) {
+    // wave 0 lane, bins b0 = 2 lane and b0 + 1: reserve c0 / c1 slots of their sub-bins (b, sub) with
+    // one 64-bit atomic on the pair's word (only the bins flagged in `mask`: bit 0 = b0, bit 1 =
+    // b0 + 1); the part past cap1 reserves spill records (a second atomic, rare)
+    auto reserve = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) {
+        const uint64_t add = ((mask & 1u) ? (uint64_t)c0 : 0ull) | ((mask & 2u) ? (uint64_t)c1 << 32 : 0ull);
 #if SS_PF_DET   // measurement only: tile-local positions, no reservation atomics (results invalid)
-        const uint32_t g = 0;
-        (void)c;
+        const uint64_t g2 = 0;
+        (void)add;
 #else
-        const uint32_t g = c ? atomicAdd(&fill[fill_at(b * kFinePerBin + sub)], c) : 0u;
+        const uint64_t g2 = add ? atomicAdd((unsigned long long*)&fill[fill_at(b0 * kFinePerBin + sub)],
+                                            (unsigned long long)add)
+                                : 0ull;
 #endif
-        gbase[b] = g;
-        const uint64_t end = (uint64_t)g + c, from = max((uint64_t)g, cap1);
-        sbase[b] = end > from ? atomicAdd(spill_ctr, (uint32_t)(end - from)) : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) {
+            if (!(mask & (1u << k))) continue;
+            const uint32_t g = (uint32_t)(g2 >> (32 * k)), c = k ? c1 : c0;
+            gbase[b0 + k] = g;
+            const uint64_t end = (uint64_t)g + c, from = max((uint64_t)g, cap1);
+            sbase[b0 + k] = end > from ? atomicAdd(spill_ctr, (uint32_t)(end - from)) : 0u;
+        }
     };
     static_assert(kCB == 128, "wave 0 scans two bins per lane");
     for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
@@ -1019,8 +1036,7 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             const bool h0 = c0 > kHeavy, h1 = c1 > kHeavy;
             hflag[b0] = h0;
             hflag[b0 + 1] = h1;
-            if (!h0) reserve(b0, c0);
-            if (!h1) reserve(b0 + 1, c1);
+            reserve(b0, c0, c1, (h0 ? 0u : 1u) | (h1 ? 0u : 2u));
             const uint64_t hv = __ballot(h0 || h1);
             if (lane == 0) any_heavy = hv != 0;
             lcount[b0] = 0;
@@ -1086,8 +1102,7 @@ __global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* _
             __syncthreads();                                              // (E)
             if (threadIdx.x < 64) {
                 const uint32_t b0 = 2 * threadIdx.x;
-                if (hflag[b0]) reserve(b0, hcnt[b0]);
-                if (hflag[b0 + 1]) reserve(b0 + 1, hcnt[b0 + 1]);
+                reserve(b0, hcnt[b0], hcnt[b0 + 1], (hflag[b0] ? 1u : 0u) | (hflag[b0 + 1] ? 2u : 0u));
                 hcnt[b0] = 0;     // now the heavy bins' write cursors
                 hcnt[b0 + 1] = 0;
             }
