@@ -831,11 +831,15 @@ __host__ __device__ __forceinline__ uint32_t fill_at(uint32_t fb) {
     const uint32_t bin = fb / kFinePerBin, sub = fb % kFinePerBin;
     return (((bin >> 1) * kFinePerBin + sub) << 1) | (bin & 1u);
 }
+// k_pf_coarse shape: 512 threads x 8 reads per 4096-read tile, capped at 128 VGPRs (4 waves per
+// SIMD: two 72-KB-LDS blocks per CU, 16 waves).  Against 256 x 16 at 230 VGPRs (8 waves per CU):
+// coarse 1.30 -> 1.19 ms uniform, 1.87 -> 1.40 ms Zipf 1.1 (its dedup phases are latency-bound);
+// insert medians 2.87 -> 2.83 / 3.28 -> 2.80 ms (scripts/ab_many.sh).  1024 x 4: 1.38 / 1.86 ms.
 #ifndef SS_PF_RPL
-#define SS_PF_RPL 16
+#define SS_PF_RPL 8
 #endif
 #ifndef SS_PF_T
-#define SS_PF_T 256      // 256 x 16 reads per tile: ~5 % faster than 512 x 8 over 9 same-box samples each
+#define SS_PF_T 512
 #endif
 #ifndef SS_PF_HEAVY
 #define SS_PF_HEAVY 64   // reads of one bin in one tile above which the bin is deduplicated (2x the mean)
@@ -939,7 +943,10 @@ __device__ __forceinline__ uint32_t dedup_home(uint64_t key, uint32_t log2n) {
 }
 
 template <int T, int RPL>
-__global__ __launch_bounds__(T) void k_pf_coarse(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
+#ifndef SS_PF_WPE
+#define SS_PF_WPE 4     // amdgpu_waves_per_eu floor of k_pf_coarse (see SS_PF_T)
+#endif
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) void k_pf_coarse(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
                                                  uint64_t n, uint32_t cpr, uint64_t cap1, uint32_t* fill,
                                                  unsigned long long* first_bad) {
     constexpr uint32_t TILE = T * RPL;
