@@ -652,7 +652,10 @@ constexpr uint32_t kTile = SS_PC_TILE;
 constexpr uint32_t kMaxLocalBins = 1024;
 
 // exclusive scan of data[0..n) (n <= 1024) by a 512-thread block; returns the total
-__device__ __forceinline__ uint32_t block_scan_512(uint32_t* data, uint32_t n, uint32_t* wsum) {
+// exclusive scan of data[0, n) (n <= 2 T) by a block of T threads; wsum holds 2 T / 64 + 1 words
+template <int T = 512>
+__device__ __forceinline__ uint32_t block_scan(uint32_t* data, uint32_t n, uint32_t* wsum) {
+    constexpr uint32_t NW = T / 64;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t i0 = 2 * tid, i1 = 2 * tid + 1;
     const uint32_t a = i0 < n ? data[i0] : 0u, b = i1 < n ? data[i1] : 0u;
@@ -663,20 +666,20 @@ __device__ __forceinline__ uint32_t block_scan_512(uint32_t* data, uint32_t n, u
     }
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    if (tid < 8) {
+    if (tid < NW) {
         uint32_t run = 0;
-        for (uint32_t w = 0; w < 8; ++w) {
+        for (uint32_t w = 0; w < NW; ++w) {
             const uint32_t t = wsum[w];
-            if (w == tid) wsum[8 + w] = run;
+            if (w == tid) wsum[NW + w] = run;
             run += t;
         }
-        if (tid == 0) wsum[16] = run;
+        if (tid == 0) wsum[2 * NW] = run;
     }
     __syncthreads();
-    const uint32_t excl = incl - v + wsum[8 + wave];
+    const uint32_t excl = incl - v + wsum[NW + wave];
     if (i0 < n) data[i0] = excl;
     if (i1 < n) data[i1] = excl + a;
-    const uint32_t total = wsum[16];
+    const uint32_t total = wsum[2 * NW];
     __syncthreads();
     return total;
 }
@@ -760,7 +763,7 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < nb; i += T) lstart[i] = lcount[i];
         __syncthreads();
-        block_scan_512(lstart, nb, wsum);
+        block_scan<T>(lstart, nb, wsum);
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
             const uint32_t e = j * T + threadIdx.x;
@@ -1272,9 +1275,15 @@ __global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ f
 #ifndef SS_HEAVY_FINE
 #define SS_HEAVY_FINE 2   // x the mean records per region per tile
 #endif
-__global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill,
-                                                    const uint32_t* __restrict__ order) {
-    constexpr int T = 512;
+#ifndef SS_FS_T
+#define SS_FS_T 512
+#endif
+#ifndef SS_FS_TILE
+#define SS_FS_TILE 4096
+#endif
+template <int T, uint32_t kTile>
+__global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill,
+                                                  const uint32_t* __restrict__ order) {
     constexpr uint32_t kHtLog = kTile == 2048 ? 11 : kTile == 4096 ? 12 : 13;
     static_assert(kTile == (1u << kHtLog), "fine tile = dedup table size");
     constexpr uint32_t kDead = 0xFFFFFFFFu;
@@ -1287,7 +1296,7 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
     __shared__ uint64_t skey[kTile];
     __shared__ uint32_t sidx[kTile];
     __shared__ uint32_t ht[kTile];
-    __shared__ uint32_t wsum[17];
+    __shared__ uint32_t wsum[2 * (T / 64) + 1];
     __shared__ uint32_t any_heavy;
     const uint32_t nb = 1u << (w.rbits - kCoarseBits);
     const uint32_t heavy_at = max(64u, SS_HEAVY_FINE * (kTile / nb));
@@ -1354,7 +1363,7 @@ __global__ __launch_bounds__(512) void k_pf_scatter(Tbl t, PartWs w, uint64_t ca
             if (lcount[i] > heavy_at) any_heavy = 1;
         }
         __syncthreads();
-        block_scan_512(lstart, nb, wsum);
+        block_scan<T>(lstart, nb, wsum);
         const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
@@ -2419,7 +2428,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             hipLaunchKernelGGL(k_pf_offsets, dim3(rg), dim3(256), 0, s, w);
             w.seg_end = c->ws_segend;
             hipLaunchKernelGGL(k_pf_order, dim3(1), dim3(512), 0, s, (const uint32_t*)c->ws_fill, cap1, c->ws_order);
-            hipLaunchKernelGGL(k_pf_scatter, dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
+            hipLaunchKernelGGL((k_pf_scatter<SS_FS_T, SS_FS_TILE>), dim3(fine_blocks), dim3(SS_FS_T), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
             if (SS_PF_STOP == 2) return ss_check(hipGetLastError(), "fine scatter");
             w.bkey = w.keys;
