@@ -662,11 +662,19 @@ def main():
                              ("C5_counter_32_zipf1.1_U20", 1 << 20, 1.1)):
             log(f"C5 counter {n5} x 32 per GPU, pool {U_}, {'zipf ' + str(zs) if zs else 'uniform'}")
             el_, d_, u_, chk_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
+            # the same pipeline bytes model with this pool's table (a skewed batch moves fewer records
+            # through the fine passes after deduplication: the model is then an upper bound)
+            pb_ = 32 + 13 + 1 + 24 + 12 + 16 * (2 * U_) / n5
             extra[name] = {"reads_per_s": n5 * world / (el_ / s5), "ms_per_step": el_ / s5 * 1e3,
                            "device_ms_per_step": d_, "reads_per_gpu": n5, "pool": U_, "zipf_s": zs, "unique": u_,
                            "parity": chk_,
                            "vs_uniform_U24": d_ / d5,
-                           "floor_frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                           "roofline": {"bound": "hbm", "kernel": "partitioned insert",
+                                        "achieved": n5 * pb_ / (d_ * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                        "unit": "GB/s", "frac": n5 * pb_ / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                        "bytes_per_read": pb_,
+                                        "floor_frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                        "traffic": load_traffic("counter32_insert_" + name[len("C5_counter_32_"):], n5)}}
         if rank == 0 or world == 1:
             # rank-local extras (no collective): an error is recorded in its entry instead of costing
             # the run its JSON line; parity failures (SystemExit) still end the run

@@ -443,7 +443,7 @@ struct __attribute__((packed, aligned(4))) Rec12 {
 #endif
 // coarse records as the same 12-B {key, read index} (areg and the sparse counts stay apart)
 #ifndef SS_PF_AOS
-#define SS_PF_AOS 0
+#define SS_PF_AOS 1
 #endif
 
 struct PartWs {

@@ -74,6 +74,21 @@ def main():
                                  "hbm_bytes_per_read": total * 1e9 / 125e6, "source": sys.argv[2] if len(sys.argv) > 2 else root,
                                  "method": "scripts/pmc_c5.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
                                            "tools/c5_only.py (125M x 32 nt, pool 2^24 uniform); FETCH x2 (gfx950), x1024"}
+        # the variants' passes (scripts/pmc_c5.sh: var_<name>/fetch, var_<name>/write)
+        for d in sorted(os.listdir(root)):
+            if not d.startswith("var_") or not os.path.isdir(os.path.join(root, d, "write")):
+                continue
+            vf, _ = per_dispatch(os.path.join(root, d, "fetch", "run_counter_collection.csv"))
+            vw, _ = per_dispatch(os.path.join(root, d, "write", "run_counter_collection.csv"))
+            vk = {k: statistics.median(vf[k]["FETCH_SIZE"]) * 2 * 1024 + statistics.median(vw[k]["WRITE_SIZE"]) * 1024
+                  for k in KERNELS if k in vf and k in vw}
+            vt = sum(vk.values())
+            print(f"variant {d[4:]}: {vt / 1e9:.3f} GB HBM per insert ({vt / 125e6:.1f} B per read)")
+            t["counter32_insert_" + d[4:]] = {"kernels": vk, "hbm_bytes_per_launch": vt, "reads": 125_000_000,
+                                              "hbm_bytes_per_read": vt / 125e6,
+                                              "source": sys.argv[2] if len(sys.argv) > 2 else root,
+                                              "method": t["counter32_insert"]["method"].replace(
+                                                  "pool 2^24 uniform", d[4:])}
         with open(path, "w") as f:
             json.dump(t, f, indent=1)
         print()
