@@ -929,9 +929,10 @@ __device__ __forceinline__ void wave_fold(bool& act, uint64_t key, uint32_t& cnt
 // wave_fold peels in the coarse dedup, the fine dedup and the aggregate (0 = off).  Same-box A/B
 // (tools/tune_counter.hip, 125M reads, 3 rounds): coarse 2 peels Zipf 3.67 -> 3.83 ms, fine 2 peels
 // no change, aggregate 2 peels 3.59 -> 3.67 ms Zipf and +0.03 ms uniform (the fine dedup already
-// bounds a region's copies of one key to ~1 per tile), so all are off; kept as knobs.
+// bounds a region's copies of one key to ~1 per tile), so all were off.  With the 512 x 8 coarse
+// tiles one coarse peel pays (below); a fine peel still costs (Zipf scatter 0.90 -> 1.22 ms).
 #ifndef SS_COARSE_FOLD
-#define SS_COARSE_FOLD 0
+#define SS_COARSE_FOLD 1   // 512 x 8 coarse tiles: 1 peel, Zipf coarse 1.40 -> 1.35 ms (2 peels: no better)
 #endif
 #ifndef SS_FINE_FOLD
 #define SS_FINE_FOLD 0
@@ -1175,6 +1176,11 @@ __device__ __forceinline__ void fine_range(uint32_t fb, const uint32_t* fill, ui
     hi = min((uint64_t)fill[fill_at(fb)], cap1);
 }
 
+// k_pf_count: add the first active lane's region for all lanes holding it with one atomic (Zipf
+// count 0.154 -> 0.116 ms, uniform 0.049 -> 0.100 ms: off)
+#ifndef SS_CNT_PEEL
+#define SS_CNT_PEEL 0
+#endif
 // fine histogram: block fb counts the regions of its slice of coarse bin fb / 8 -> hist[fb][rpb]
 template <int T>
 __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
@@ -1201,8 +1207,25 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
             const uint32_t m = (uint32_t)min((uint64_t)16, hi - 16 * q);
             const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-            for (uint32_t j = 0; j < 16; ++j)
-                if (j < m) atomicAdd(&h[(wd[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+            for (uint32_t j = 0; j < 16; ++j) {
+                const bool valid = j < m;
+                const uint32_t r = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                if constexpr (SS_CNT_PEEL != 0) {
+                    // the lanes holding the first active lane's region add together: a hot region of
+                    // a skewed sub-bin costs one LDS atomic per wave instead of up to 64 on one word
+                    const uint32_t r0 = __builtin_amdgcn_readfirstlane(valid ? r : 0x100u);
+                    const bool same = valid && r == r0;
+                    const uint64_t mm = __ballot(same);
+                    if (same) {
+                        if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)mm) - 1))
+                            atomicAdd(&h[r0], (uint32_t)__popcll(mm));
+                    } else if (valid) {
+                        atomicAdd(&h[r], 1u);
+                    }
+                } else if (valid) {
+                    atomicAdd(&h[r], 1u);
+                }
+            }
         }
     }
     __syncthreads();
