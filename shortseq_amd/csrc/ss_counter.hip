@@ -591,12 +591,19 @@ __global__ __launch_bounds__(T) void k_pc_count(Tbl t, PartWs w, const uint64_t*
 }
 
 // bin totals (thread per bin; coalesced over bins)
+// bin totals: one block per bin, its threads over the kPartBlocks partition blocks' counts (a
+// thread per bin looping over all blocks was a 1024-long serial chain: 40-65 us per call on the
+// small per-length tables of a FASTQ file)
 __global__ __launch_bounds__(256) void k_pc_tot(PartWs w, uint32_t bins) {
-    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= bins) return;
+    __shared__ uint32_t red[4];
+    const uint32_t r = blockIdx.x;
     uint32_t sum = 0;
-    for (uint32_t b = 0; b < kPartBlocks; ++b) sum += w.hist[(uint64_t)b * bins + r];
-    w.tot[r] = sum;
+    for (uint32_t b = threadIdx.x; b < kPartBlocks; b += 256) sum += w.hist[(uint64_t)b * bins + r];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) sum += (uint32_t)__shfl_xor((int)sum, off);
+    if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) w.tot[r] = red[0] + red[1] + red[2] + red[3];
 }
 
 // exclusive scan of bin totals (one block of 1024) -> start[bins + 1]
@@ -625,17 +632,26 @@ __global__ __launch_bounds__(1024) void k_pc_scan(PartWs w, uint32_t bins, uint3
     if (threadIdx.x == 1023) start[bins] = sums[1023];
 }
 
-// per-(block, bin) write offsets = bin start + counts of earlier blocks (thread per bin)
-__global__ __launch_bounds__(256) void k_pc_offsets(PartWs w, uint32_t bins, const uint32_t* start) {
-    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= bins) return;
-    uint32_t run = start[r];
-    for (uint32_t b = 0; b < kPartBlocks; ++b) {
-        const uint64_t i = (uint64_t)b * bins + r;
-        const uint32_t c = w.hist[i];
-        w.hist[i] = run;
-        run += c;
+// per-(block, bin) write offsets = bin start + counts of earlier blocks: one block per bin, a thread
+// per partition block, block-wide exclusive scan
+static_assert(kPartBlocks == 1024, "k_pc_offsets: one thread per partition block");
+__global__ __launch_bounds__(1024) void k_pc_offsets(PartWs w, uint32_t bins, const uint32_t* start) {
+    __shared__ uint32_t wtot[16];
+    const uint32_t r = blockIdx.x, b = threadIdx.x, lane = b & 63u, wave = b >> 6;
+    const uint64_t i = (uint64_t)b * bins + r;
+    const uint32_t c = w.hist[i];
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+        if (lane >= (uint32_t)off) incl += y;
     }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < 16; ++v) before += v < wave ? wtot[v] : 0u;
+    w.hist[i] = start[r] + before + incl - c;
 }
 
 // LDS-staged scatter (both partition passes).  Per tile of kTile elements: local histogram of the
@@ -2417,10 +2433,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             attrs_set = true;
         }
         auto scan = [&](uint32_t bins, uint32_t* start) {
-            const unsigned g = (bins + 255) / 256;
-            hipLaunchKernelGGL(k_pc_tot, dim3(g), dim3(256), 0, s, w, bins);
+            hipLaunchKernelGGL(k_pc_tot, dim3(bins), dim3(256), 0, s, w, bins);
             hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, bins, start);
-            hipLaunchKernelGGL(k_pc_offsets, dim3(g), dim3(256), 0, s, w, bins, (const uint32_t*)start);
+            hipLaunchKernelGGL(k_pc_offsets, dim3(bins), dim3(1024), 0, s, w, bins, (const uint32_t*)start);
         };
         if (!multi && !packed_keys && two_pass && w.rbits - kCoarseBits <= 8) {
             // optimistic coarse partition: encode + coarse scatter in one pass, fine pass by bin
