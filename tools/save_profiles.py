@@ -80,6 +80,21 @@ def main():
             put("decode512", e, READS // 2)
         elif k.startswith("void k_encode_g16<false, true, 2"):
             put("encode512", e, READS // 2)
+    # F1: the one-pass FASTQ index (k_fq_nlpos + k_fq_place per call; 8 Mi records of the bench's
+    # synthetic 100-nt file)
+    fq = []
+    for kname in ("k_fq_nlpos", "k_fq_place"):      # the bench's launch: the one repeated most
+        cand = [e for e in summ.get("all", []) if "hbm_bytes_per_launch" in e and e["kernel"].startswith(kname)]
+        if cand:
+            fq.append(max(cand, key=lambda e: e.get("calls", 0)))
+    if len(fq) == 2:
+        nrec = 8 << 20
+        tot = sum(e["hbm_bytes_per_launch"] for e in fq)
+        traffic["fastq_index_onepass"] = {"kernel": "k_fq_nlpos + k_fq_place", "grid": None, "calls": None,
+                                          "hbm_bytes_per_launch": tot, "reads": nrec,
+                                          "hbm_bytes_per_read": tot / nrec,
+                                          "avg_ms_rocprof": sum(e["avg_ms"] for e in fq),
+                                          "source": os.path.relpath(dst, REPO), "method": method}
     if traffic:
         path = os.path.join(REPO, "profiles", "pmc_traffic.json")
         old = json.load(open(path)) if os.path.exists(path) else {}
