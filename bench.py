@@ -528,10 +528,10 @@ def cpu_baseline(target_s=2.0):
         out["calibration_vs_reference"] = {
             "where": f"build container ({c.get('cpu')}), 1 core, same inputs; ratio = port speed / reference speed",
             **{k: round(v, 3) for k, v in ratios.items()},
-            "why": "L > 32: the reference's compiled _marshall_bytes_array checks __Pyx_ErrOccurredWithGIL() "
-                   "after _divmod and _marshall_full_blocks for every read (Cython exception propagation of "
-                   "util.pyx:88-90), which the port does not restate; counter: the reference builds a "
-                   "ShortSeq object per read into a CPython dict, the port a std::unordered_map node"}
+            "how": "median of 5 interleaved rounds (the build container's CPU timings wander by up to "
+                   "+-20 % between runs); the port restates the reference's per-read GIL error checks "
+                   "of _marshall_bytes_array (util.pyx:88-90); counter: the reference builds a ShortSeq "
+                   "object per read into a CPython dict, the port a std::unordered_map node"}
         # the port's 1-core numbers scaled by the calibration: the reference's expected speed on this host
         pick = {"C2_encode_32": "encode_32", "C3_encode_hamming_96": "encode_96",
                 "C4_roundtrip_512": "encode_512", "C5_counter_32": "counter_32_pool2^24"}

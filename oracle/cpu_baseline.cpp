@@ -16,16 +16,55 @@
 //                    (one length per batch; std::unordered_map, count += 1, first index kept)
 // Calibrated against the reference's own compiled kernels in the container
 // (oracle/calibrate_cpu_baseline.py -> profiles/r2/cpu_baseline_calibration.json).
+#include <dlfcn.h>
 #include <immintrin.h>
 #include <omp.h>
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
 #include <unordered_map>
 #include <utility>
 #include <vector>
 
 namespace {
+
+// The reference's compiled _marshall_bytes_array (Cython's exception propagation for util.pyx:88-90)
+// calls __Pyx_ErrOccurredWithGIL() -- PyGILState_Ensure, PyErr_Occurred, PyGILState_Release --
+// after _divmod and after _marshall_full_blocks, i.e. twice per read of L > 32 (the L <= 32 path,
+// _marshall_bytes_64, has no such check).  Inside a Python process (bench.py, the calibration) the
+// port makes the same three C-API calls per check, resolved from the process; on the multi-thread
+// legs (each core stands for a separate single-threaded reference process with its own GIL) and
+// outside Python an uncontended thread-local mutex stands in.
+struct PyApi {
+    typedef int (*ensure_t)();
+    typedef void (*release_t)(int);
+    typedef void* (*occurred_t)();
+    ensure_t ensure = nullptr;
+    release_t release = nullptr;
+    occurred_t occurred = nullptr;
+    PyApi() {
+        ensure = (ensure_t)dlsym(RTLD_DEFAULT, "PyGILState_Ensure");
+        release = (release_t)dlsym(RTLD_DEFAULT, "PyGILState_Release");
+        occurred = (occurred_t)dlsym(RTLD_DEFAULT, "PyErr_Occurred");
+        if (!ensure || !release || !occurred) ensure = nullptr;
+    }
+};
+const PyApi kPy;
+int g_gil_checks = 1;   // cb_set_gil_checks(0) turns the emulation off (the pure algorithm)
+
+inline void err_check(bool single) {
+    if (!g_gil_checks) return;
+    if (single && kPy.ensure) {
+        const int st = kPy.ensure();
+        (void)kPy.occurred();
+        kPy.release(st);
+    } else {
+        thread_local std::mutex m;
+        m.lock();
+        m.unlock();
+    }
+}
 
 constexpr uint64_t kBloom = 0xFFFFFFFFFFEFFF75ull;   // util.pyx:75
 constexpr uint64_t kPextMask = 0x0606060606060606ull;  // util.pyx:39
@@ -81,10 +120,13 @@ inline bool marshall_array(const uint8_t* seq, uint32_t L, uint64_t* dst) {
     return true;
 }
 
-inline bool encode_read(const uint8_t* seq, uint32_t L, uint64_t* w, uint32_t wpr) {
+inline bool encode_read(const uint8_t* seq, uint32_t L, uint64_t* w, uint32_t wpr, bool single) {
     for (uint32_t k = 0; k < wpr; ++k) w[k] = 0;
     if (L <= 32) return marshall_64(seq, L, w[0]);
-    return marshall_array(seq, L, w);
+    err_check(single);                    // after _divmod (util.pyx:88)
+    const bool ok = marshall_array(seq, L, w);
+    err_check(single);                    // after _marshall_full_blocks (util.pyx:90)
+    return ok;
 }
 
 inline uint32_t hamming(const uint64_t* a, const uint64_t* b, uint32_t nw) {
@@ -116,13 +158,15 @@ inline uint32_t words_for(uint32_t L) { return L <= 32 ? 1u : (L + 31) / 32; }
 extern "C" {
 
 int cb_max_threads(void) { return omp_get_max_threads(); }
+void cb_set_gil_checks(int on) { g_gil_checks = on; }
+int cb_gil_api(void) { return kPy.ensure != nullptr; }
 
 // encode n reads (row i at ascii + i * L) -> words [n * wpr]; returns the number of invalid reads
 uint64_t cb_encode(const uint8_t* ascii, uint64_t n, uint32_t L, uint64_t* words, uint32_t wpr, int threads) {
     uint64_t bad = 0;
 #pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : bad)
     for (int64_t i = 0; i < (int64_t)n; ++i)
-        bad += encode_read(ascii + (uint64_t)i * L, L, words + (uint64_t)i * wpr, wpr) ? 0 : 1;
+        bad += encode_read(ascii + (uint64_t)i * L, L, words + (uint64_t)i * wpr, wpr, threads <= 1) ? 0 : 1;
     return bad;
 }
 
@@ -134,7 +178,7 @@ uint64_t cb_encode_hamming(const uint8_t* ascii, uint64_t n, uint32_t L, uint64_
 #pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : bad)
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         uint64_t* w = words + (uint64_t)i * wpr;
-        bad += encode_read(ascii + (uint64_t)i * L, L, w, wpr) ? 0 : 1;
+        bad += encode_read(ascii + (uint64_t)i * L, L, w, wpr, threads <= 1) ? 0 : 1;
         dist[i] = hamming(w, ref, nw);
     }
     return bad;
@@ -147,7 +191,7 @@ uint64_t cb_roundtrip(const uint8_t* ascii, uint64_t n, uint32_t L, uint64_t* wo
 #pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : bad)
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         uint64_t* w = words + (uint64_t)i * wpr;
-        bad += encode_read(ascii + (uint64_t)i * L, L, w, wpr) ? 0 : 1;
+        bad += encode_read(ascii + (uint64_t)i * L, L, w, wpr, threads <= 1) ? 0 : 1;
         decode_read(w, L, back + (uint64_t)i * L);
     }
     return bad;

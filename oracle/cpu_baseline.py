@@ -18,24 +18,41 @@ LIB_PATH = os.path.join(HERE, "libcpubaseline.so")
 _lib = None
 
 
-def lib():
-    global _lib
+_lib1 = None
+
+
+def lib(threads: int = 0):
+    """The port.  threads == 1: a PyDLL handle (the GIL stays held, as when Python calls the
+    reference's kernels), so the port's per-read error checks (cpu_baseline.cpp err_check) take the
+    GIL the way the compiled reference does; otherwise a CDLL handle (GIL released for the OpenMP
+    legs)."""
+    global _lib, _lib1
+    if threads == 1:
+        if _lib1 is None:
+            lib()
+            _lib1 = _bind(C.PyDLL(LIB_PATH))
+        return _lib1
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             oracle.build()
-        L = C.CDLL(LIB_PATH)
-        P, U64, U32, I = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
-        L.cb_encode.argtypes = [P, U64, U32, P, U32, I]
-        L.cb_encode.restype = U64
-        L.cb_encode_hamming.argtypes = [P, U64, U32, P, U32, P, P, I]
-        L.cb_encode_hamming.restype = U64
-        L.cb_roundtrip.argtypes = [P, U64, U32, P, U32, P, I]
-        L.cb_roundtrip.restype = U64
-        L.cb_count.argtypes = [P, U64, U32, I, C.POINTER(U64), C.POINTER(U64)]
-        L.cb_count.restype = U64
-        L.cb_max_threads.restype = I
-        _lib = L
+        _lib = _bind(C.CDLL(LIB_PATH))
     return _lib
+
+
+def _bind(L):
+    P, U64, U32, I = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+    L.cb_encode.argtypes = [P, U64, U32, P, U32, I]
+    L.cb_encode.restype = U64
+    L.cb_encode_hamming.argtypes = [P, U64, U32, P, U32, P, P, I]
+    L.cb_encode_hamming.restype = U64
+    L.cb_roundtrip.argtypes = [P, U64, U32, P, U32, P, I]
+    L.cb_roundtrip.restype = U64
+    L.cb_count.argtypes = [P, U64, U32, I, C.POINTER(U64), C.POINTER(U64)]
+    L.cb_count.restype = U64
+    L.cb_max_threads.restype = I
+    L.cb_set_gil_checks.argtypes = [I]
+    L.cb_gil_api.restype = I
+    return L
 
 
 def host_threads() -> int:
@@ -80,9 +97,9 @@ def bench_encode(L: int, n: int, threads: int, target_s: float, seed: int = 1) -
     ascii = oracle.gen_reads(seed, 0, n, L)
     wpr = max(1, (L + 31) // 32)
     words = np.zeros(n * wpr, np.uint64)
-    assert lib().cb_encode(_p(ascii), n, L, _p(words), wpr, threads) == 0
+    assert lib(threads).cb_encode(_p(ascii), n, L, _p(words), wpr, threads) == 0
     assert np.array_equal(words.reshape(n, wpr)[:64], oracle.gen_words(seed, 0, 64, L))
-    passes, el = _time(lambda: lib().cb_encode(_p(ascii), n, L, _p(words), wpr, threads), target_s)
+    passes, el = _time(lambda: lib(threads).cb_encode(_p(ascii), n, L, _p(words), wpr, threads), target_s)
     return {"nt_per_s": passes * n * L / el, "reads_per_s": passes * n / el, "sample": f"{passes} x {n} reads x {L} nt"}
 
 
@@ -93,10 +110,10 @@ def bench_encode_hamming(L: int, n: int, threads: int, target_s: float, seed: in
     dist = np.zeros(n, np.uint32)
     ref = oracle.gen_words(seed, 0, 1, L)[0].astype(np.uint64)
     ref = np.ascontiguousarray(np.concatenate([ref, np.zeros(wpr - len(ref), np.uint64)]))
-    assert lib().cb_encode_hamming(_p(ascii), n, L, _p(words), wpr, _p(ref), _p(dist), threads) == 0
+    assert lib(threads).cb_encode_hamming(_p(ascii), n, L, _p(words), wpr, _p(ref), _p(dist), threads) == 0
     exp = oracle.hamming_ref_batch(words.reshape(n, wpr)[:4096], 4096, L, ref)
     assert np.array_equal(dist[:4096], exp)
-    passes, el = _time(lambda: lib().cb_encode_hamming(_p(ascii), n, L, _p(words), wpr, _p(ref), _p(dist), threads),
+    passes, el = _time(lambda: lib(threads).cb_encode_hamming(_p(ascii), n, L, _p(words), wpr, _p(ref), _p(dist), threads),
                        target_s)
     return {"pairs_per_s": passes * n / el, "nt_per_s": passes * n * L / el, "sample": f"{passes} x {n} reads x {L} nt"}
 
@@ -106,9 +123,9 @@ def bench_roundtrip(L: int, n: int, threads: int, target_s: float, seed: int = 3
     wpr = max(1, (L + 31) // 32)
     words = np.zeros(n * wpr, np.uint64)
     back = np.zeros(n * L, np.uint8)
-    assert lib().cb_roundtrip(_p(ascii), n, L, _p(words), wpr, _p(back), threads) == 0
+    assert lib(threads).cb_roundtrip(_p(ascii), n, L, _p(words), wpr, _p(back), threads) == 0
     assert np.array_equal(back, ascii)
-    passes, el = _time(lambda: lib().cb_roundtrip(_p(ascii), n, L, _p(words), wpr, _p(back), threads), target_s)
+    passes, el = _time(lambda: lib(threads).cb_roundtrip(_p(ascii), n, L, _p(words), wpr, _p(back), threads), target_s)
     return {"nt_per_s": passes * n * L / el, "reads_per_s": passes * n / el, "sample": f"{passes} x {n} reads x {L} nt"}
 
 
@@ -116,10 +133,10 @@ def bench_count(n: int, U: int, threads: int, target_s: float, seed: int = 5, po
     L = 32
     ascii = oracle.gen_pool_reads(seed, pool_seed, U, 0, n, L)
     tot, fs = C.c_uint64(), C.c_uint64()
-    uniq = lib().cb_count(_p(ascii), n, L, threads, C.byref(tot), C.byref(fs))
+    uniq = lib(threads).cb_count(_p(ascii), n, L, threads, C.byref(tot), C.byref(fs))
     k, c, f = oracle.pool_counter_table(seed, pool_seed, U, n, L)
     assert uniq == len(k) and tot.value == n and fs.value == int(f.sum()), (uniq, len(k))
-    passes, el = _time(lambda: lib().cb_count(_p(ascii), n, L, threads, C.byref(tot), C.byref(fs)), target_s)
+    passes, el = _time(lambda: lib(threads).cb_count(_p(ascii), n, L, threads, C.byref(tot), C.byref(fs)), target_s)
     return {"reads_per_s": passes * n / el, "unique": int(uniq), "sample": f"{passes} x {n} reads (pool {U})"}
 
 
