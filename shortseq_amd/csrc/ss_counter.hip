@@ -73,11 +73,13 @@ struct ss_counter {
     uint4* ws_spill = nullptr;             // [ws_reads] records past a full sub-bin
     uint32_t* ws_hist = nullptr;           // [kPartBlocks * regions] per-(block, bin) counts -> offsets
     uint32_t* ws_rstart = nullptr;         // [regions + 1] region start in the bucket arrays
-    uint32_t* ws_order = nullptr;          // [kNFill] sub-bins by descending fill (k_pf_order)
+    uint32_t* ws_order = nullptr;          // [3 kNFill] sub-bins by descending fill, slab bases, slab sizes (k_pf_order)
     uint32_t* ws_segend = nullptr;         // [regions x kFinePerBin] end of each (sub-bin, region) fine segment
     uint32_t* ws_tot = nullptr;            // [regions + 1] scratch (bin totals / coarse starts)
     // optimistic coarse partition (k_pf_coarse): ws_akey / ws_aidx hold 128 bins of ws_cap1 slots
     uint64_t ws_cap1 = 0;
+    uint64_t ws_slab = 0;                  // 1 = fine-scatter slabs per (sub-bin, region), 0 = counted cursors
+    uint64_t ws_brecs = 0;                 // fine-record slots (ws_keys / ws_bidx / ws_bcnt)
     uint32_t* ws_fill = nullptr;           // sub-bin fill counters + the spill counter, kFillStride apart
     // per-region occupancy (used slots of each slice), written by the single-word aggregate (and
     // kept by the spill insert); lets ss_counter_pack_ranges skip its counting pass.
@@ -441,6 +443,23 @@ struct __attribute__((packed, aligned(4))) Rec12 {
 #ifndef SS_FS_AOS
 #define SS_FS_AOS 1
 #endif
+// fine-pass slabs instead of counted cursors (ss_counter_reserve decides per reservation)
+#ifndef SS_PF_SLABS
+#define SS_PF_SLABS 1
+#endif
+constexpr uint64_t kSlabMinMean = 256;
+#ifndef SS_SLAB_MUL
+#define SS_SLAB_MUL 4   // a slab holds SS_SLAB_MUL / 2 x its region's mean share of the sub-bin ...
+#endif
+#ifndef SS_SLAB_PAD
+#define SS_SLAB_PAD 256 // ... + SS_SLAB_PAD records, rounded up to 16
+#endif
+// slab size of a sub-bin holding f coarse records over nb regions.  The fine scatter's heavy-region
+// dedup keeps a region at <= 2 x the mean records per tile unless it holds that many distinct keys,
+// so 2 x (f / nb) + a partial tile's slack is overrun only by crafted inputs (those spill).
+__host__ __device__ __forceinline__ uint32_t slab_size(uint32_t f, uint32_t nb) {
+    return ((SS_SLAB_MUL * ((f + nb - 1) / nb)) / 2 + SS_SLAB_PAD + 15) & ~15u;
+}
 // coarse records as the same 12-B {key, read index} (areg and the sparse counts stay apart)
 #ifndef SS_PF_AOS
 #define SS_PF_AOS 1
@@ -448,6 +467,11 @@ struct __attribute__((packed, aligned(4))) Rec12 {
 
 struct PartWs {
     const Rec12* brec; // optimistic path with SS_FS_AOS: the region-ordered records (else null)
+    uint32_t slab;     // optimistic path: 1 = fine records of (sub-bin f, region j) live in slab
+                       // [slabs[f] + j slabs[kNFill + f], + slabs[kNFill + f]) (no count pass);
+                       // 0 = counted cursors (hist)
+    const uint32_t* slabs; // [2 kNFill] per sub-bin slab base and slab size (k_pf_order)
+    uint32_t* spill_ctr;   // the spill list's record counter (shared with the coarse pass's overflow)
     uint64_t* keys;    // P1 output; P3 second-pass output (bucketed by region)
     uint64_t* akey;    // first-pass output (bucketed by coarse bin)
     uint32_t* aidx;
@@ -909,8 +933,9 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int lane) {
 // PEELS times, the active lanes whose key equals the key of the lowest active lane not yet folded
 // into are folded into that lane (count summed, index min); the folded lanes turn inactive.  A peel
 // costs one ballot + broadcast, and a 6-step sum / min only when at least two lanes match.  All 64
-// lanes must call it (uniform control flow); returns with the surviving lanes active.
-template <int PEELS>
+// lanes must call it (uniform control flow); returns with the surviving lanes active.  A peel whose
+// key is unique in the wave ends the fold, or with kPastSingles passes over that lane.
+template <int PEELS, bool kPastSingles = false>
 __device__ __forceinline__ void wave_fold(bool& act, uint64_t key, uint32_t& cnt, uint32_t& idx) {
     const int lane = (int)(threadIdx.x & 63);
     bool led = false;
@@ -922,7 +947,11 @@ __device__ __forceinline__ void wave_fold(bool& act, uint64_t key, uint32_t& cnt
         const uint64_t lk = shfl64(key, leader);
         const bool m = act && key == lk;
         const uint64_t mm = __ballot(m);
-        if (__popcll(mm) < 2) break;
+        if (__popcll(mm) < 2) {   // the lowest candidate's key is unique in the wave
+            if (!kPastSingles) break;
+            led = led || lane == leader;
+            continue;
+        }
         uint32_t cs = m ? cnt : 0u, mi = m ? idx : 0xFFFFFFFFu;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
@@ -949,6 +978,9 @@ __device__ __forceinline__ void wave_fold(bool& act, uint64_t key, uint32_t& cnt
 // tiles one coarse peel pays (below); a fine peel still costs (Zipf scatter 0.90 -> 1.22 ms).
 #ifndef SS_COARSE_FOLD
 #define SS_COARSE_FOLD 1   // 512 x 8 coarse tiles: 1 peel, Zipf coarse 1.40 -> 1.35 ms (2 peels: no better)
+#endif
+#ifndef SS_SPILL_FOLD
+#define SS_SPILL_FOLD 8   // Zipf 1.1 over 2^24: 278k spilled records, insert 0.30 -> 0.12 (4 peels) -> 0.09 ms (8)
 #endif
 #ifndef SS_FINE_FOLD
 #define SS_FINE_FOLD 0
@@ -1161,12 +1193,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
                     r.khi = (uint32_t)(k >> 32);
                     r.idx = c > 1 ? (sidx[i] | kWeighted) : sidx[i];
                     ((Rec12*)w.akey)[at] = r;
-                    w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
+                    if (!w.slab) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
                     if (c > 1) w.acnt[at] = c;
                     continue;
                 }
                 if (SS_PF_WRITE & 1) w.akey[at] = k;
-                if (SS_PF_WRITE & 2) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
+                if ((SS_PF_WRITE & 2) && !w.slab) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
                 if (c > 1) {
                     w.aidx[at] = sidx[i] | kWeighted;
                     w.acnt[at] = c;
@@ -1278,14 +1310,26 @@ __global__ __launch_bounds__(256) void k_pf_offsets(PartWs w) {
 // fine scatter's blocks (dispatched in blockIdx order) start the long ones first and the pass does
 // not end on a skewed sub-bin that started last.  One block: bitonic sort of (~fill, index) in LDS.
 __global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ fill, uint64_t cap1,
-                                                  uint32_t* __restrict__ order) {
+                                                  uint32_t* __restrict__ order, uint32_t nb,
+                                                  uint32_t* __restrict__ slabs) {
     static_assert(kNFill == 1024, "one 512-thread block sorts 1024 sub-bins");
     __shared__ uint64_t v[kNFill];
+    __shared__ uint32_t base[kNFill];
+    __shared__ uint32_t wsum[2 * (512 / 64) + 1];
     for (uint32_t i = threadIdx.x; i < kNFill; i += 512) {
         const uint32_t f = (uint32_t)min((uint64_t)fill[fill_at(i)], cap1);
         v[i] = ((uint64_t)~f << 32) | i;      // ascending = fill descending, then index
+        if (slabs) base[i] = nb * slab_size(f, nb);
     }
     __syncthreads();
+    if (slabs) {   // slab bases: sub-bins back to back in index order, each nb slabs of its size
+        block_scan<512>(base, kNFill, wsum);
+        for (uint32_t i = threadIdx.x; i < kNFill; i += 512) {
+            slabs[i] = base[i];
+            slabs[kNFill + i] = slab_size((uint32_t)~(v[i] >> 32), nb);
+        }
+        __syncthreads();
+    }
     for (uint32_t k = 2; k <= kNFill; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             const uint32_t t = threadIdx.x;
@@ -1349,7 +1393,11 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
     const uint32_t* src_idx = w.aidx + (uint64_t)fb * cap1;
     auto rec_idx = [&](uint32_t p) -> uint32_t { return SS_PF_AOS ? srec[p].idx : src_idx[p]; };
     const uint32_t* src_cnt = w.acnt + (uint64_t)fb * cap1;
-    for (uint32_t i = threadIdx.x; i < nb; i += T) cursor[i] = w.hist[(uint64_t)fb * nb + i];
+    const uint32_t sbase = w.slab ? w.slabs[fb] : 0u, ssize = w.slab ? w.slabs[kNFill + fb] : 0u;
+    for (uint32_t i = threadIdx.x; i < nb; i += T) {
+        cursor[i] = w.slab ? sbase + i * ssize : w.hist[(uint64_t)fb * nb + i];
+        if (w.slab) w.hist[(uint64_t)fb * nb + i] = sbase + i * ssize;   // the aggregate's segment start
+    }
     __syncthreads();
     uint64_t nkey[kTile / T];
     uint32_t nidx[kTile / T];
@@ -1471,6 +1519,22 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
                 local = i - lstart[b];
             }
             const uint32_t gpos = cursor[b] + local;
+            if (w.slab && gpos >= sbase + (b + 1) * ssize) {
+                // the region's slab of this sub-bin is full: the record goes to the spill list
+                // (counted by k_spill_insert after the aggregate)
+                uint32_t xi = x, cc = c;
+                if (x & kWeighted) {
+                    const uint32_t p = x & ~kWeighted;
+                    xi = rec_idx(p);
+                    cc = src_cnt[p];
+                }
+                const uint64_t sp = atomicAdd(w.spill_ctr, 1u);
+                if (sp < w.spill_cap)
+                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), cc, xi & ~kWeighted);
+                else
+                    atomicOr(t.overflow, kOvfTable);
+                continue;
+            }
             if constexpr (SS_FS_AOS != 0) {
                 uint32_t xi = x;
                 if (x & kWeighted) {
@@ -1506,7 +1570,8 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
             cursor[i] += (heavy_tile && lcount[i] > heavy_at) ? hcnt[i] : lcount[i];
         __syncthreads();
     }
-    for (uint32_t i = threadIdx.x; i < nb; i += T) w.seg_end[(uint64_t)fb * nb + i] = cursor[i];
+    for (uint32_t i = threadIdx.x; i < nb; i += T)
+        w.seg_end[(uint64_t)fb * nb + i] = w.slab ? min(cursor[i], sbase + (i + 1) * ssize) : cursor[i];
 }
 
 // Spilled records (sub-bin full) into the table with the direct insert, after the aggregate; a slot
@@ -1514,10 +1579,17 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
 __global__ __launch_bounds__(256) void k_spill_insert(Tbl t, PartWs w, const uint32_t* __restrict__ fill,
                                                       uint64_t base_index) {
     const uint64_t m = min((uint64_t)fill[fill_at(kSpillCtr)], w.spill_cap);
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
-        const uint4 r = w.spill[i];
+    // wave-uniform trip count (the folds below are wave operations)
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < m; i0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint4 r = w.spill[min(i, m - 1)];
         const uint64_t k = ((uint64_t)r.y << 32) | r.x;
-        if (tbl_add(t, k, r.z, base_index + r.w) && t.occ && k != kEmpty) atomicAdd(&t.occ[region_of(t, k)], 1u);
+        // a full slab spills a run of one region's records, mostly copies of its heavy keys (one
+        // weighted record per coarse tile): fold a wave's copies before the global atomics
+        bool act = i < m;
+        uint32_t c = r.z, idx = r.w;
+        wave_fold<SS_SPILL_FOLD, true>(act, k, c, idx);
+        if (act && tbl_add(t, k, c, base_index + idx) && t.occ && k != kEmpty) atomicAdd(&t.occ[region_of(t, k)], 1u);
     }
 }
 
@@ -2279,20 +2351,38 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     // 128 x 8 sub-bins of cap1 = 2.5 x the mean sub-bin load + 1024 slots (pf_cap1)
     const uint64_t cap1 = pf_cap1(max_reads);
     const uint64_t acap = kNFill * cap1 > max_reads ? kNFill * cap1 : max_reads;
-    hipError_t e = hipMalloc((void**)&c->ws_keys, max_reads * (SS_FS_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
+    // fine-pass slabs (optimistic path, R > 128 regions): every (sub-bin, region of its bin) gets
+    // slab_size(sub-bin fill) record slots (2 x its mean share + 256; k_pf_order lays them out once
+    // the coarse fills are known), so the fine scatter needs no count pass; a slab that runs full
+    // sends the rest to the spill list.  Only where the mean share is >= kSlabMinMean (the per-slab
+    // slack would dominate small reservations) and the slots index in 32 bits.
+    c->ws_slab = 0;
+    c->ws_brecs = max_reads;
+    if (SS_PF_SLABS && R > (1u << kCoarseBits) && R <= (1u << (kCoarseBits + 8))) {
+        const uint64_t nslab = (uint64_t)kNFill * (R >> kCoarseBits);
+        const uint64_t mean = max_reads / nslab;
+        // sum over sub-bins of nb x slab_size(fill, nb), fills summing to <= max_reads
+        const uint64_t brecs = (SS_SLAB_MUL * max_reads) / 2 + nslab * (SS_SLAB_MUL / 2 + SS_SLAB_PAD + 15);
+        if (mean >= kSlabMinMean && brecs < (1ull << 32)) {
+            c->ws_slab = 1;
+            c->ws_brecs = brecs > max_reads ? brecs : max_reads;
+        }
+    }
+    const uint64_t brecs = c->ws_brecs;
+    hipError_t e = hipMalloc((void**)&c->ws_keys, brecs * (SS_FS_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * (SS_PF_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_acnt, acap * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_areg, acap);
+    if (e == hipSuccess && !c->ws_slab) e = hipMalloc((void**)&c->ws_areg, acap);   // counted cursors only
     if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, kFillWords * sizeof(uint32_t));
     c->ws_cap1 = cap1;
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bcnt, max_reads * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, (SS_FS_AOS ? max_reads : brecs) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bcnt, brecs * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_spill, max_reads * sizeof(uint4));
     if (e == hipSuccess && !c->ws_hist) e = hipMalloc((void**)&c->ws_hist, (size_t)kPartBlocks * R * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_rstart) e = hipMalloc((void**)&c->ws_rstart, (R + 1) * sizeof(uint32_t));
     // one entry per (sub-bin, region of its bin): kNFill x (R / 128) = R x kFinePerBin
-    if (e == hipSuccess && !c->ws_order) e = hipMalloc((void**)&c->ws_order, kNFill * sizeof(uint32_t));
+    if (e == hipSuccess && !c->ws_order) e = hipMalloc((void**)&c->ws_order, 3 * kNFill * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_segend) e = hipMalloc((void**)&c->ws_segend, R * kFinePerBin * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_tot) e = hipMalloc((void**)&c->ws_tot, (R + 1) * sizeof(uint32_t));
     if (e != hipSuccess) {
@@ -2328,6 +2418,8 @@ int ss_counter_release(ss_counter* c) {
     c->ws_bcnt = nullptr;
     c->ws_spill = nullptr;
     c->ws_reads = 0;
+    c->ws_slab = 0;
+    c->ws_brecs = 0;
     return SS_OK;
 }
 
@@ -2398,6 +2490,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         w.tot = c->ws_tot;
         w.bkey = nullptr;
         w.brec = nullptr;
+        w.slab = 0;
+        w.slabs = nullptr;
+        w.spill_ctr = nullptr;
         w.R = (uint32_t)(c->cap >> c->slice_log);
         w.rbits = c->log2cap - c->slice_log;
         const uint32_t S = 1u << c->slice_log;
@@ -2440,6 +2535,8 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         if (!multi && !packed_keys && two_pass && w.rbits - kCoarseBits <= 8) {
             // optimistic coarse partition: encode + coarse scatter in one pass, fine pass by bin
             const uint64_t cap1 = c->ws_cap1;
+            w.slab = (uint32_t)c->ws_slab;
+            w.spill_ctr = c->ws_fill + fill_at(kSpillCtr);
             rc = ss_check(hipMemsetAsync(c->ws_fill, 0, kFillWords * sizeof(uint32_t), s), "fill reset");
             if (rc) return rc;
             // grid-stride over tiles: exactly the resident blocks (no second, partial round)
@@ -2458,14 +2555,18 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             // the fine scatter
             if (SS_PF_STOP == 1) return ss_check(hipGetLastError(), "coarse pass");
             const unsigned fine_blocks = kCB * kFinePerBin;
-            hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
-                               (const uint32_t*)c->ws_fill);
-            const unsigned rg = (w.R + 255) / 256;
-            hipLaunchKernelGGL(k_pf_tot, dim3(rg), dim3(256), 0, s, w);
-            hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, w.R, w.rstart, (const uint32_t*)nullptr);
-            hipLaunchKernelGGL(k_pf_offsets, dim3(rg), dim3(256), 0, s, w);
+            if (!w.slab) {   // counted cursors: region histogram per sub-bin, then the scans
+                hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
+                                   (const uint32_t*)c->ws_fill);
+                const unsigned rg = (w.R + 255) / 256;
+                hipLaunchKernelGGL(k_pf_tot, dim3(rg), dim3(256), 0, s, w);
+                hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, w.R, w.rstart, (const uint32_t*)nullptr);
+                hipLaunchKernelGGL(k_pf_offsets, dim3(rg), dim3(256), 0, s, w);
+            }
             w.seg_end = c->ws_segend;
-            hipLaunchKernelGGL(k_pf_order, dim3(1), dim3(512), 0, s, (const uint32_t*)c->ws_fill, cap1, c->ws_order);
+            w.slabs = w.slab ? c->ws_order + kNFill : nullptr;
+            hipLaunchKernelGGL(k_pf_order, dim3(1), dim3(512), 0, s, (const uint32_t*)c->ws_fill, cap1, c->ws_order,
+                               1u << (w.rbits - kCoarseBits), w.slab ? c->ws_order + kNFill : nullptr);
             hipLaunchKernelGGL((k_pf_scatter<SS_FS_T, SS_FS_TILE>), dim3(fine_blocks), dim3(SS_FS_T), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
             if (SS_PF_STOP == 2) return ss_check(hipGetLastError(), "fine scatter");

@@ -10,6 +10,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <math.h>
+#include <vector>
+#include <unordered_map>
+#include <algorithm>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 #define CS(x) do { int r_ = (x); if (r_) { printf("ss error %d: %s @%d\n", r_, ss_last_error_string(), __LINE__); exit(1); } } while (0)
@@ -69,7 +72,35 @@ int main(int argc, char** argv) {
     uint64_t hs, hfb;
     CK(hipMemcpy(&hs, size, 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(&hfb, fb, 8, hipMemcpyDeviceToHost));
-    printf("U=2^%d zipf=%.2f: insert avg %.3f ms min %.3f ms  (%.1f G reads/s)  unique %llu first_bad %llx\n", ulog, zs,
-           tot / reps, mn, n / (tot / reps) / 1e6, (unsigned long long)hs, (unsigned long long)hfb);
+    uint32_t hspill = 0;
+    CK(hipMemcpy(&hspill, c->ws_fill + fill_at(kSpillCtr), 4, hipMemcpyDeviceToHost));
+    if (getenv("SS_DIAG") && c->ws_slab && hspill) {   // where do the spills come from
+        const uint32_t nb = (uint32_t)((c->cap >> c->slice_log) >> kCoarseBits);
+        std::vector<uint32_t> sl(2 * kNFill), hist((size_t)kNFill * nb), se((size_t)kNFill * nb), fl(kFillWords);
+        CK(hipMemcpy(sl.data(), c->ws_order + kNFill, sl.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hist.data(), c->ws_hist, hist.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(se.data(), c->ws_segend, se.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(fl.data(), c->ws_fill, fl.size() * 4, hipMemcpyDeviceToHost));
+        uint64_t full = 0, fullfb = 0;
+        for (uint32_t f = 0; f < kNFill; ++f) {
+            uint32_t nf = 0;
+            for (uint32_t i = 0; i < nb; ++i) nf += se[(size_t)f * nb + i] - hist[(size_t)f * nb + i] >= sl[kNFill + f];
+            full += nf;
+            fullfb += nf > 0;
+            if (nf && fullfb <= 6) printf("  fb %u fill %u slab %u full regions %u\n", f, fl[fill_at(f)], sl[kNFill + f], nf);
+        }
+        std::vector<uint4> sp(std::min<uint64_t>(hspill, c->ws_reads));
+        CK(hipMemcpy(sp.data(), c->ws_spill, sp.size() * 16, hipMemcpyDeviceToHost));
+        std::unordered_map<uint64_t, uint64_t> kc;
+        uint64_t weighted = 0;
+        for (auto& r : sp) { kc[((uint64_t)r.y << 32) | r.x] += 1; weighted += r.z > 1; }
+        uint64_t mx = 0;
+        for (auto& e : kc) mx = std::max(mx, e.second);
+        printf("  full slabs %llu in %llu sub-bins; spill records %zu distinct keys %zu weighted %llu max per key %llu\n",
+               (unsigned long long)full, (unsigned long long)fullfb, sp.size(), kc.size(), (unsigned long long)weighted,
+               (unsigned long long)mx);
+    }
+    printf("U=2^%d zipf=%.2f: insert avg %.3f ms min %.3f ms  (%.1f G reads/s)  unique %llu first_bad %llx  spill %u\n", ulog, zs,
+           tot / reps, mn, n / (tot / reps) / 1e6, (unsigned long long)hs, (unsigned long long)hfb, hspill);
     return 0;
 }
