@@ -645,17 +645,17 @@ def main():
         log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
         s5 = max(3, args.steps // 4)
         el5, d5, uniq, chk5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
-        # per-read bytes of the partitioned pipeline: coarse pass 32 in + 13 out (key,
-        # read index, region byte), fine count 1, fine scatter 12 + 12, aggregate 12 + the whole
-        # table written once (fresh slices: 16 B x 2^25 slots, amortised over the reads); the floor of
-        # the problem is the 32 B of ASCII per read
+        # per-read bytes of the partitioned pipeline: coarse pass 32 in + 12 out (key,
+        # read index), fine scatter 12 + 12 (into per-sub-bin slabs: no count pass), aggregate 12 +
+        # the whole table written once (fresh slices: 16 B x 2^25 slots, amortised over the reads);
+        # the floor of the problem is the 32 B of ASCII per read
         table_b = 16 * (2 * U5) / n5
-        pipe_b = 32 + 13 + 1 + 24 + 12 + table_b
+        pipe_b = 32 + 12 + 24 + 12 + table_b
         extra["C5_counter_32"] = {
             "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
             "reads_per_gpu": n5, "pool": U5, "unique": uniq, "parity": chk5,
-            "roofline": {"bound": "hbm", "kernel": "partitioned insert (k_pf_coarse, k_pf_count, k_pf_scatter, "
-                                                    "k_pc_aggregate)",
+            "roofline": {"bound": "hbm", "kernel": "partitioned insert (k_pf_coarse, k_pf_scatter, "
+                                                    "k_pc_aggregate_slice)",
                          "achieved": n5 * pipe_b / (d5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": n5 * pipe_b / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_read": pipe_b,
                          "floor_frac": n5 * 32 / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -671,7 +671,7 @@ def main():
             el_, d_, u_, chk_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
             # the same pipeline bytes model with this pool's table (a skewed batch moves fewer records
             # through the fine passes after deduplication: the model is then an upper bound)
-            pb_ = 32 + 13 + 1 + 24 + 12 + 16 * (2 * U_) / n5
+            pb_ = 32 + 12 + 24 + 12 + 16 * (2 * U_) / n5
             extra[name] = {"reads_per_s": n5 * world / (el_ / s5), "ms_per_step": el_ / s5 * 1e3,
                            "device_ms_per_step": d_, "reads_per_gpu": n5, "pool": U_, "zipf_s": zs, "unique": u_,
                            "parity": chk_,
