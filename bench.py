@@ -641,47 +641,58 @@ def main():
                          "algo_bytes_per_step": b4e + b4d,
                          "traffic": (None if load_traffic("encode512", n4) is None or load_traffic("decode512", n4) is None
                                      else load_traffic("encode512", n4) + load_traffic("decode512", n4))}}
-        n5, U5 = 125_000_000, 1 << 24
-        log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
-        s5 = max(3, args.steps // 4)
-        el5, d5, uniq, chk5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
-        # per-read bytes of the partitioned pipeline: coarse pass 32 in + 12 out (key,
-        # read index), fine scatter 12 + 12 (into per-sub-bin slabs: no count pass), aggregate 12 +
-        # the whole table written once (fresh slices: 16 B x 2^25 slots, amortised over the reads);
-        # the floor of the problem is the 32 B of ASCII per read
-        table_b = 16 * (2 * U5) / n5
-        pipe_b = 32 + 12 + 24 + 12 + table_b
-        extra["C5_counter_32"] = {
-            "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
-            "reads_per_gpu": n5, "pool": U5, "unique": uniq, "parity": chk5,
-            "roofline": {"bound": "hbm", "kernel": "partitioned insert (k_pf_coarse, k_pf_scatter, "
-                                                    "k_pc_aggregate_slice)",
-                         "achieved": n5 * pipe_b / (d5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": n5 * pipe_b / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_read": pipe_b,
-                         "floor_frac": n5 * 32 / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "traffic": load_traffic("counter32_insert", n5),
-                         "note": "frac: the pipeline's own pass bytes; floor_frac: 32 B of ASCII per read"},
-            "merge": (f"all_to_all_single of 16-B (key, count, first) records by owner over {dist.get_backend()}"
-                      f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
-                     if world > 1 else "none (1 GPU)"}
-        # SURVEY §8(d) C5 variants: the smaller pool and Zipf s = 1.1 skew (same shard size)
-        for name, U_, zs in (("C5_counter_32_U20", 1 << 20, None), ("C5_counter_32_zipf1.1_U24", 1 << 24, 1.1),
-                             ("C5_counter_32_zipf1.1_U20", 1 << 20, 1.1)):
-            log(f"C5 counter {n5} x 32 per GPU, pool {U_}, {'zipf ' + str(zs) if zs else 'uniform'}")
-            el_, d_, u_, chk_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
-            # the same pipeline bytes model with this pool's table (a skewed batch moves fewer records
-            # through the fine passes after deduplication: the model is then an upper bound)
-            pb_ = 32 + 12 + 24 + 12 + 16 * (2 * U_) / n5
-            extra[name] = {"reads_per_s": n5 * world / (el_ / s5), "ms_per_step": el_ / s5 * 1e3,
-                           "device_ms_per_step": d_, "reads_per_gpu": n5, "pool": U_, "zipf_s": zs, "unique": u_,
-                           "parity": chk_,
-                           "vs_uniform_U24": d_ / d5,
-                           "roofline": {"bound": "hbm", "kernel": "partitioned insert",
-                                        "achieved": n5 * pb_ / (d_ * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                                        "unit": "GB/s", "frac": n5 * pb_ / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                        "bytes_per_read": pb_,
-                                        "floor_frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                        "traffic": load_traffic("counter32_insert_" + name[len("C5_counter_32_"):], n5)}}
+
+        def c5_extras():
+            n5, U5 = 125_000_000, 1 << 24
+            log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
+            s5 = max(3, args.steps // 4)
+            el5, d5, uniq, chk5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
+            # per-read bytes of the partitioned pipeline: coarse pass 32 in + 12 out (key,
+            # read index), fine scatter 12 + 12 (into per-sub-bin slabs: no count pass), aggregate 12 +
+            # the whole table written once (fresh slices: 16 B x 2^25 slots, amortised over the reads);
+            # the floor of the problem is the 32 B of ASCII per read
+            table_b = 16 * (2 * U5) / n5
+            pipe_b = 32 + 12 + 24 + 12 + table_b
+            extra["C5_counter_32"] = {
+                "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
+                "reads_per_gpu": n5, "pool": U5, "unique": uniq, "parity": chk5,
+                "roofline": {"bound": "hbm", "kernel": "partitioned insert (k_pf_coarse, k_pf_scatter, "
+                                                        "k_pc_aggregate_slice)",
+                             "achieved": n5 * pipe_b / (d5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": n5 * pipe_b / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_read": pipe_b,
+                             "floor_frac": n5 * 32 / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "traffic": load_traffic("counter32_insert", n5),
+                             "note": "frac: the pipeline's own pass bytes; floor_frac: 32 B of ASCII per read"},
+                "merge": (f"all_to_all_single of 16-B (key, count, first) records by owner over {dist.get_backend()}"
+                          f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
+                         if world > 1 else "none (1 GPU)"}
+            # SURVEY §8(d) C5 variants: the smaller pool and Zipf s = 1.1 skew (same shard size)
+            for name, U_, zs in (("C5_counter_32_U20", 1 << 20, None), ("C5_counter_32_zipf1.1_U24", 1 << 24, 1.1),
+                                 ("C5_counter_32_zipf1.1_U20", 1 << 20, 1.1)):
+                log(f"C5 counter {n5} x 32 per GPU, pool {U_}, {'zipf ' + str(zs) if zs else 'uniform'}")
+                el_, d_, u_, chk_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
+                # the same pipeline bytes model with this pool's table (a skewed batch moves fewer records
+                # through the fine passes after deduplication: the model is then an upper bound)
+                pb_ = 32 + 12 + 24 + 12 + 16 * (2 * U_) / n5
+                extra[name] = {"reads_per_s": n5 * world / (el_ / s5), "ms_per_step": el_ / s5 * 1e3,
+                               "device_ms_per_step": d_, "reads_per_gpu": n5, "pool": U_, "zipf_s": zs, "unique": u_,
+                               "parity": chk_,
+                               "vs_uniform_U24": d_ / d5,
+                               "roofline": {"bound": "hbm", "kernel": "partitioned insert",
+                                            "achieved": n5 * pb_ / (d_ * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                            "unit": "GB/s", "frac": n5 * pb_ / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                            "bytes_per_read": pb_,
+                                            "floor_frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                            "traffic": load_traffic("counter32_insert_" + name[len("C5_counter_32_"):], n5)}}
+
+        # C5 (and at world > 1 its RCCL exchange): an exception every rank raises alike (e.g. a backend
+        # without all_to_all) is recorded in the entry instead of costing the run its JSON line;
+        # parity failures (SystemExit) still end the run
+        try:
+            c5_extras()
+        except Exception as e:  # noqa: BLE001
+            log(f"C5: {type(e).__name__}: {e}")
+            extra.setdefault("C5_counter_32", {"error": f"{type(e).__name__}: {e}"})
         if rank == 0 or world == 1:
             # rank-local extras (no collective): an error is recorded in its entry instead of costing
             # the run its JSON line; parity failures (SystemExit) still end the run

@@ -159,7 +159,7 @@ int ss_counter_destroy(ss_counter* c);
 int ss_counter_reset(ss_counter* c, void* stream);
 uint64_t ss_counter_capacity(const ss_counter* c);
 
-/* Reserve workspace (~76 B per read + a small per-region table) so inserts of up to max_reads
+/* Reserve workspace (~100 B per read + a small per-region table) so inserts of up to max_reads
  * reads take the partitioned path: reads are bucketed by table region and each region is
  * aggregated by one workgroup in LDS (no per-read global atomics).  Host call (allocates).  L 16/32
  * with 16-B aligned rows encode inside the first partition pass (a key repeated within a 4096-read

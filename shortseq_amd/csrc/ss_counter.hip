@@ -2371,7 +2371,8 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     const uint64_t brecs = c->ws_brecs;
     hipError_t e = hipMalloc((void**)&c->ws_keys, brecs * (SS_FS_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * (SS_PF_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, acap * sizeof(uint32_t));
+    // coarse read indices live in the 12-B records with SS_PF_AOS (aidx then serves the exact paths)
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, (SS_PF_AOS ? max_reads : acap) * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_acnt, acap * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_slab) e = hipMalloc((void**)&c->ws_areg, acap);   // counted cursors only
     if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, kFillWords * sizeof(uint32_t));

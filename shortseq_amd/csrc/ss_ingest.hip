@@ -434,8 +434,8 @@ int table_get(ss_ingest* g, uint64_t cap, ss_counter** out) {
     return ss_counter_create(cap, out);
 }
 
-// device bytes a pooled table holds: its slots and its partition workspace (~72 B per reserved read)
-uint64_t table_bytes(ss_counter* t) { return ss_counter_capacity(t) * 16 + ss_counter_reserved(t) * 72; }
+// device bytes a pooled table holds: its slots and its partition workspace (~100 B per reserved read)
+uint64_t table_bytes(ss_counter* t) { return ss_counter_capacity(t) * 16 + ss_counter_reserved(t) * 100; }
 
 void table_put(ss_ingest* g, ss_counter* t) {
     if (!t) return;
