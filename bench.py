@@ -89,8 +89,18 @@ def timed_loop(step, steps, warmup, world):
     # clock settle: the MI355X needs ~20-30 ms of sustained load before its clocks stop ramping
     # (tools/tune_stream.hip ramp trace: first ~30 back-to-back 0.6-ms launches 2-6 % slower), so
     # untimed steps continue until SETTLE_S of load has passed, whatever W is
+    # With world > 1 the ranks agree on every settle step (a step may hold collectives, e.g. the C5
+    # exchange: ranks running different numbers of steps would pair one rank's exchange with another's
+    # barrier and hang)
     t_s = time.perf_counter()
-    while time.perf_counter() - t_s < SETTLE_S:
+    while True:
+        more = time.perf_counter() - t_s < SETTLE_S
+        if world > 1:
+            f = torch.tensor([int(more)], dtype=torch.int32, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(f, op=dist.ReduceOp.MAX)
+            more = bool(f.item())
+        if not more:
+            break
         step(None)
         torch.cuda.synchronize()
     if world > 1:

@@ -115,3 +115,30 @@ def test_sharded_counter_8_ranks_c5_shards():
     assert got[0] != "error", got
     assert all(p.exitcode == 0 for p in procs)
     assert got == (d["unique"], d["n"], d["digest"])
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_rehearsal():
+    """bench.py as the driver launches it for N > 1 (torch.distributed.run, one process per rank),
+    rehearsed with 2 gloo ranks on this GPU: the ranks agree on every settle step (a C5 step holds the
+    exchange), rank 0 prints ONE JSON line with the whole-job value, and the C5 line's table equals
+    the 2-shard job digest (tests/golden/c5_digests.json uniform_U24_job2)."""
+    import json
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--dist-backend", "gloo", "--same-device"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=540)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 2 * r["config"]["reads_per_gpu"]
+    assert r["extra"]["C5_counter_32"]["parity"] == "digest uniform_U24_job2"
+    for k, v in r["extra"].items():
+        assert "error" not in v, (k, v)
