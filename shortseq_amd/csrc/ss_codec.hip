@@ -7,7 +7,7 @@
 //                  __shfl_xor and per-read sums (fused hamming) reduce inside the group.
 //   k_encode_gen   any L / stride / variable lengths: one lane per output word, aligned dword
 //                  loads + v_alignbyte; the general and ragged path.
-//   k_ham_dense / k_ham_dense3  hamming on dense packed rows (dwordx4 streams; k_ham_group otherwise)
+//   k_ham_dense / k_ham_dense3w hamming on dense packed rows (dwordx4 streams; k_ham_group otherwise)
 //   k_decode_g16 / k_decode_gen, k_ham_group, k_synth_*.
 #include "ss_device.h"
 #include "ss_internal.h"
@@ -342,58 +342,97 @@ __device__ __forceinline__ void ham_store2(uint32_t* p, uint32_t lo, uint32_t hi
     else *(uint64_t*)p = v;
 }
 
-// Dense hamming for W = 3 (96-nt reads) without LDS: every wave streams chunks of 63 consecutive
-// dwordx4 (lane 63 idles, 1.6 % of the lanes), so a chunk is 21 lane triples = 42 whole reads and a
-// triple (p = 0, 1, 2) holds words 6m .. 6m+5: read 2m = p0.lo + p0.hi + p1.lo, read 2m+1 = p1.hi +
-// p2.lo + p2.hi.  Two shuffles move p1's halves to p0 and p2, which store the two distances.  Chunk c
-// = j * (T / 64) + wave, so at each j the block's waves read one contiguous span.
-template <bool PAIR, int T, int U>
-__global__ __launch_bounds__(T) void k_ham_dense3(const uint4* __restrict__ a, const uint4* __restrict__ b,
-                                                  const uint64_t* __restrict__ ref, uint64_t n,
-                                                  uint32_t* __restrict__ out) {
-    constexpr uint32_t NWV = T / 64, RPC = 42, QPC = 63;
-    constexpr uint32_t RPB = RPC * NWV * U;          // reads per block (even)
+// Dense hamming for W = 3 with every lane busy and line-aligned loads: a wave takes groups of 3
+// whole 1-KiB chunks (192 dwordx4 = 384 words = 128 reads, so a group starts on a read boundary).
+// Global lane L = 64 j + l of a group holds words 2L, 2L+1; the lane triple (3m, 3m+1, 3m+2) holds
+// reads 2m = words 6m..6m+2 and 2m+1 = words 6m+3..6m+5, and lane 3m gathers its neighbours'
+// per-word distances by shuffle and stores both read distances (one 8-B store).  Two
+// triples straddle a chunk boundary (L = 63..65, 126..128): their p0 lane takes the next chunk's
+// lane-0/1 values by readlane.  Group index = (block G + g) NWV + wave, so at each g the block's
+// waves read one contiguous span.
+template <bool PAIR, int T, int G>
+__global__ __launch_bounds__(T) void k_ham_dense3w(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                   const uint64_t* __restrict__ ref, uint64_t n,
+                                                   uint32_t* __restrict__ out) {
+    constexpr uint32_t NWV = T / 64;
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t m = lane / 3u, p = lane - 3u * m;
-    const uint64_t r0 = (uint64_t)blockIdx.x * RPB;
-    const uint32_t nr = (uint32_t)min((uint64_t)RPB, n - r0);
-    const uint32_t nw = 3u * nr, nfull = nw / 2;
-    const uint64_t q0 = r0 * 3u / 2u;
-    auto load = [&](const uint4* src, uint32_t ql) -> uint4 {
-        if (lane < QPC && ql < nfull) return ld_stream(&src[q0 + ql]);
-        if (lane < QPC && ql * 2 < nw) {
-            const uint64_t v = ((const uint64_t*)src)[2 * (q0 + ql)];
+    const uint64_t nw = 3 * n, nfull = nw / 2;                      // whole dwordx4 of the rows
+    const uint64_t blk_q1 = ((uint64_t)blockIdx.x + 1) * G * NWV * 192;   // past the block's last dwordx4
+    const bool whole = blk_q1 <= nfull;
+    auto load = [&](const uint4* src, uint64_t q) -> uint4 {
+        if (q < nfull) return ld_stream(&src[q]);
+        if (2 * q < nw) {
+            const uint64_t v = ((const uint64_t*)src)[2 * q];
             return make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
         }
         return make_uint4(0u, 0u, 0u, 0u);
     };
-    uint4 x[U], y[U];
+    uint4 x[G][3], y[G][3];
+    if (whole) {   // block-uniform: unconditional loads, all issued back to back
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-        const uint32_t ql = (j * NWV + wv) * QPC + lane;
-        x[j] = load(a, ql);
-        if constexpr (PAIR) y[j] = load(b, ql);
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint64_t q = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 192 + j * 64 + lane;
+                x[g][j] = ld_stream(&a[q]);
+                if constexpr (PAIR) y[g][j] = ld_stream(&b[q]);
+            }
+    } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint64_t q = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 192 + j * 64 + lane;
+                x[g][j] = load(a, q);
+                if constexpr (PAIR) y[g][j] = load(b, q);
+            }
     }
-    uint64_t rl = 0, rh = 0;   // reference words at this lane's two positions: (2p) % 3, (2p + 1) % 3
+    uint64_t rw[3] = {0, 0, 0};
     if constexpr (!PAIR) {
-        rl = ref[p == 0 ? 0 : (p == 1 ? 2 : 1)];
-        rh = ref[p == 0 ? 1 : (p == 1 ? 0 : 2)];
+        rw[0] = ref[0];
+        rw[1] = ref[1];
+        rw[2] = ref[2];
     }
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-        const uint64_t wlo = ((uint64_t)x[j].y << 32) | x[j].x, whi = ((uint64_t)x[j].w << 32) | x[j].z;
-        uint64_t clo = rl, chi = rh;
-        if constexpr (PAIR) {
-            clo = ((uint64_t)y[j].y << 32) | y[j].x;
-            chi = ((uint64_t)y[j].w << 32) | y[j].z;
+    for (int g = 0; g < G; ++g) {
+        uint32_t dl[3], dh[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t wlo = ((uint64_t)x[g][j].y << 32) | x[g][j].x, whi = ((uint64_t)x[g][j].w << 32) | x[g][j].z;
+            uint64_t clo, chi;
+            if constexpr (PAIR) {
+                clo = ((uint64_t)y[g][j].y << 32) | y[g][j].x;
+                chi = ((uint64_t)y[g][j].w << 32) | y[g][j].z;
+            } else {   // word 2L sits at position (2L) % 3 of its read; 64 = 1 (mod 3)
+                const uint32_t pos = (2u * ((uint32_t)j + lane)) % 3u;
+                clo = pos == 0 ? rw[0] : (pos == 1 ? rw[1] : rw[2]);
+                chi = pos == 0 ? rw[1] : (pos == 1 ? rw[2] : rw[0]);
+            }
+            dl[j] = ham64(wlo ^ clo);
+            dh[j] = ham64(whi ^ chi);
         }
-        const uint32_t dl = ham64(wlo ^ clo), dh = ham64(whi ^ chi);
-        const uint32_t from_next = __shfl(dl, (int)min(lane + 1u, 63u));   // p0 <- p1.lo
-        const uint32_t from_prev = __shfl(dh, (int)(lane == 0 ? 0u : lane - 1u));   // p2 <- p1.hi
-        const uint32_t rb = (j * NWV + wv) * RPC + 2u * m;                   // block-local read of p0
-        if (lane < QPC) {
-            if (p == 0 && rb < nr) ham_store(&out[r0 + rb], dl + dh + from_next);
-            if (p == 2 && rb + 1 < nr) ham_store(&out[r0 + rb + 1], from_prev + dl + dh);
+        const uint64_t grp = ((uint64_t)blockIdx.x * G + g) * NWV + wv;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t sm = dl[j] + dh[j];
+            uint32_t n1l = __shfl(dl[j], (int)min(lane + 1u, 63u)), n1h = __shfl(dh[j], (int)min(lane + 1u, 63u));
+            uint32_t n2 = __shfl(sm, (int)min(lane + 2u, 63u));
+            if (j < 2) {   // triples across the chunk boundary take the next chunk's lanes 0 / 1
+                const uint32_t l0 = __builtin_amdgcn_readlane(dl[j + 1], 0), h0 = __builtin_amdgcn_readlane(dh[j + 1], 0);
+                const uint32_t s1 = __builtin_amdgcn_readlane(dl[j + 1] + dh[j + 1], 1);
+                if (lane == 62) n2 = l0 + h0;
+                if (lane == 63) {
+                    n1l = l0;
+                    n1h = h0;
+                    n2 = s1;
+                }
+            }
+            const uint32_t L = 64u * j + lane;
+            if (L % 3u == 0) {
+                const uint64_t r = grp * 128 + 2 * (L / 3u);
+                if (r + 1 < n) ham_store2(&out[r], sm + n1l, n1h + n2);
+                else if (r < n) ham_store(&out[r], sm + n1l);
+            }
         }
     }
 }
@@ -799,13 +838,15 @@ static int launch_ham(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t
     const bool aligned = (((uintptr_t)a | (uintptr_t)(pair ? b : a)) & 15u) == 0 && (((uintptr_t)out) & 7u) == 0;
     if (wpr == W && aligned && W <= 32) {   // dense rows: the streaming kernel (W <= 32 keeps wl < 4096 exact)
         hipStream_t s = (hipStream_t)stream;
-        if (W == 3) {   // 96 nt (C3): lane triples, no LDS (0.63 -> 0.68 of HBM peak, same-box A/B)
-            constexpr int T = 256, U = 4;
-            const unsigned grid = grid_for(n, (uint64_t)42 * (T / 64) * U);
+        if (W == 3) {   // 96 nt (C3'): lane triples over whole 1-KiB chunks, no LDS (tools/tune_ham3.hip,
+                        // same box: 63-lane chunks 0.718, + one 8-B store per triple 0.750, 3-chunk
+                        // groups 0.779 of the 8-TB/s peak)
+            constexpr int T = 256, G = 1;
+            const unsigned grid = grid_for(n, (uint64_t)128 * (T / 64) * G);
             const uint4 *a4 = (const uint4*)a, *b4 = (const uint4*)b;
-            if (pair) hipLaunchKernelGGL((k_ham_dense3<true, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
-            else hipLaunchKernelGGL((k_ham_dense3<false, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
-            return ss_check(hipGetLastError(), "k_ham_dense3");
+            if (pair) hipLaunchKernelGGL((k_ham_dense3w<true, T, G>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
+            else hipLaunchKernelGGL((k_ham_dense3w<false, T, G>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
+            return ss_check(hipGetLastError(), "k_ham_dense3w");
         }
         launch_ham_dense_k<kHamDT, kHamDU>(a, b, n, W, out, pair, s);
         return ss_check(hipGetLastError(), "k_ham_dense");
