@@ -1361,6 +1361,9 @@ __global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ f
 #ifndef SS_FS_T
 #define SS_FS_T 512
 #endif
+#ifndef SS_FS_EARLY_WAIT
+#define SS_FS_EARLY_WAIT 1
+#endif
 #ifndef SS_FS_TILE
 #define SS_FS_TILE 4096
 #endif
@@ -1502,6 +1505,13 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
                 if (lcount[i] > heavy_at) lstart[i] = 0;    // now the heavy region's write cursor
             __syncthreads();
         }
+        // Wait for the next tile's loads here, before this tile's record stores are issued: vmcnt
+        // counts loads and stores in issue order, and with a data-dependent number of stores in
+        // between, the wait at the next tile's first use would also drain this tile's stores
+        if (SS_FS_EARLY_WAIT) {
+#pragma unroll
+            for (int j = 0; j < (int)(kTile / T); ++j) asm volatile("" ::"v"(nkey[j]), "v"(nidx[j]));
+        }
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
             const uint64_t k = skey[i];
             const uint32_t x = sidx[i];
@@ -1549,7 +1559,7 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
                 r.klo = (uint32_t)k;
                 r.khi = (uint32_t)(k >> 32);
                 r.idx = xi;
-                ((Rec12*)w.keys)[gpos] = r;
+                if (SS_FS_WRITE & 1) ((Rec12*)w.keys)[gpos] = r;   // (measurement knob: 0 = no record writes)
                 continue;
             }
             if (SS_FS_WRITE & 1) w.keys[gpos] = k;
