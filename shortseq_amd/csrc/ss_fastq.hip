@@ -51,6 +51,25 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* buf, uint64_t off, ui
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// U chunks per thread of the tile at t0 (chunk j of thread t at t0 + 16 (j kFqT + t)).  A whole tile
+// (block-uniform test) loads unconditionally, so the U loads go out back to back; a guarded load per
+// chunk (the tile holding the end of the chunk) puts each load in its own branch, and the compiler
+// then waits for each one before issuing the next.
+template <int U>
+__device__ __forceinline__ void load_chunks(const uint8_t* buf, uint64_t nbytes, uint64_t t0, uint4 (&x)[U]) {
+    if (t0 + 16ull * U * kFqT <= nbytes) {
+#pragma unroll
+        for (int j = 0; j < U; ++j) x[j] = ld_stream((const uint4*)(buf + t0 + 16ull * (j * kFqT + threadIdx.x)));
+    } else {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
+            x[j] = off < nbytes ? load_chunk(buf, off, nbytes)
+                                : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t count_nl(const uint4& x) {
     return __popc(eq_bytes(x.x, 0x0A0A0A0Au)) + __popc(eq_bytes(x.y, 0x0A0A0A0Au)) +
            __popc(eq_bytes(x.z, 0x0A0A0A0Au)) + __popc(eq_bytes(x.w, 0x0A0A0A0Au));
@@ -61,11 +80,7 @@ __global__ __launch_bounds__(kFqT) void k_fq_count(const uint8_t* __restrict__ b
     __shared__ uint32_t part[kFqT / 64];
     const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile;
     uint4 x[kFqU];
-#pragma unroll
-    for (int j = 0; j < kFqU; ++j) {
-        const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
-        x[j] = off < nbytes ? load_chunk(buf, off, nbytes) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-    }
+    load_chunks<kFqU>(buf, nbytes, t0, x);
     uint32_t c = 0;
 #pragma unroll
     for (int j = 0; j < kFqU; ++j) c += count_nl(x[j]);
@@ -274,11 +289,7 @@ __device__ __forceinline__ void emit_tile(const FqOut& o, const uint4 (&x)[U], u
 template <int U>
 __device__ __forceinline__ void load_tile(const uint8_t* buf, uint64_t nbytes, uint64_t t0, uint4 (&x)[U],
                                           uint64_t (&packed)[U / 4]) {
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-        const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
-        x[j] = off < nbytes ? load_chunk(buf, off, nbytes) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-    }
+    load_chunks<U>(buf, nbytes, t0, x);
 #pragma unroll
     for (int k = 0; k < U / 4; ++k) packed[k] = 0;   // 16-bit newline count of chunk j at bits 16 (j % 4)
 #pragma unroll
@@ -338,11 +349,7 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
     bool nul = false;
     {
         uint4 x[kFqU1];
-#pragma unroll
-        for (int j = 0; j < kFqU1; ++j) {
-            const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
-            x[j] = off < nbytes ? load_chunk(buf, off, nbytes) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-        }
+        load_chunks<kFqU1>(buf, nbytes, t0, x);
 #pragma unroll
         for (int j = 0; j < kFqU1; j += 2) {
             mk[j / 2] = nl_mask16(x[j]) | nl_mask16(x[j + 1]) << 16;
