@@ -143,3 +143,42 @@ def test_counter_index_limit(gpu):
     with pytest.raises(NativeError):
         c.insert(a, 32, base_index=(1 << 32) - 100)
     c.close()
+
+
+def test_counter_slabs_multi_batch(gpu, oracle):
+    """Fine-pass slabs (a 42M-read reservation on a 2^25-slot table: 320 reads per (sub-bin, region)
+    on average, so the slab layout is on) with three 14M-read batches into ONE table: the second and
+    third merge into already-written slices (no fresh reset).  Compared with the generator-derived
+    table of all 42M draws."""
+    import shortseq_amd.batch as B
+    U, nb, nbat = 1 << 24, 14_000_000, 3
+    c = B.GpuCounter(1 << 25, device=gpu)
+    assert c.reserve(nb * nbat)
+    for b in range(nbat):
+        a = B.synth_pool_reads(nb, 32, 5, 77, U, i0=b * nb, device=gpu)
+        c.insert(a, 32, base_index=b * nb, partitioned=True)
+        del a
+    k, cnt, f = _table_rows(c)
+    c.close()
+    torch.cuda.empty_cache()
+    ek, ec, ef = oracle.pool_counter_table(5, 77, U, nb * nbat, 32)
+    assert len(k) == len(ek)
+    assert oracle.table_digest(k, cnt, f) == oracle.table_digest(ek, ec, ef)
+
+
+def test_counter_slabs_zipf_spill(gpu, oracle):
+    """Slab layout under Zipf s = 1.1 over 2^24 (40M reads, one batch, 128 regions per coarse bin): a
+    region's copies of a heavy key arrive as one weighted record per coarse tile and overrun its slab,
+    so records take the spill list (folded per wave, then inserted directly) -- still exact."""
+    import shortseq_amd.batch as B
+    U, n = 1 << 24, 40_000_000
+    cdf = B.zipf_cdf(U, 1.1)
+    a = B.synth_zipf_reads(n, 32, 5, 77, cdf, device=gpu)
+    c = B.GpuCounter(1 << 25, device=gpu)
+    c.insert(a, 32, base_index=7, partitioned=True)
+    del a
+    k, cnt, f = _table_rows(c)
+    c.close()
+    torch.cuda.empty_cache()
+    ek, ec, ef = oracle.pool_counter_table(5, 77, U, n, 32, cdf=cdf)
+    assert oracle.table_digest(k, cnt, f) == oracle.table_digest(ek, ec, ef + np.uint64(7))
