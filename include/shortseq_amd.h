@@ -104,7 +104,7 @@ int ss_decode_var(const uint64_t* d_words, const uint32_t* d_lens, uint64_t n, u
  * short_seq_var.pyx:64-81): sum over W = (L <= 32 ? 1 : ceil(L/32)) words of
  * popcount(((x >> 1) | x) & 0x5555555555555555), x = a ^ b.  Whole-word, like the reference.
  * Dense rows (wpr == W) with 16-B aligned word arrays and an 8-B aligned d_out take the streaming
- * kernels (k_ham_dense / k_ham_dense3); any other layout the lane-group kernel.  Same results.
+ * kernels (k_ham_dense / k_ham_dense3w); any other layout the lane-group kernel.  Same results.
  * ---------------------------------------------------------------------------------------------- */
 int ss_hamming_ref(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr,
                    const uint64_t* d_ref, uint32_t* d_out, void* stream);
