@@ -2,9 +2,12 @@
 
 Bit-exact for everything (integer work).  Small/medium sizes compare element-wise with the oracle;
 full BASELINE sizes are checked through size-independent properties (known-answer generator words,
-encode -> decode round trip, checksum of per-read distances).
+encode -> decode round trip) and whole-batch digests of the words and distances derived from the
+generator (tests/golden/stream_digests.json).
 """
 import hashlib
+import json
+import os
 
 import numpy as np
 import pytest
@@ -13,6 +16,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 ALIASES = np.array([1, 3, 7, 20], np.uint8)
+
+
+STREAM = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "stream_digests.json")))
 
 
 def _sha(a):
@@ -269,12 +275,18 @@ def test_full_size_properties(gpu, oracle, L, n):
     samp = _u64(words[torch.from_numpy(idx).to(gpu)])
     exp = np.stack([oracle.gen_words(1, int(i), 1, L)[0] for i in idx])
     assert np.array_equal(samp, exp)
+    # whole-batch digests derived from the generator (tests/golden/gen_stream_digests.py, pinned to
+    # the oracle on CPU by tests/test_oracle_golden.py::test_stream_digest_construction)
+    d = STREAM[f"{'C2' if L == 32 else 'C3' if L == 96 else 'C4'}_{n}x{L}"]
+    assert d["seed"] == 1
+    assert _sha(_u64(words)) == d["words_sha256"]
+    # hamming vs read 0: the dense kernel on the packed words, and for C3 the fused encode+hamming
+    d2 = B.hamming_ref(words, L, words[0])
+    assert _sha(d2.cpu().numpy().astype(np.uint32)) == d["hamming_vs_read0_sha256"]
     if L == 96:
         _, dist = B.encode_hamming_ref(ascii, L, words[0], store_words=False)
-        dsum = int(dist.to(torch.int64).sum().item())
-        d2 = B.hamming_ref(words, L, words[0])
-        assert int(d2.to(torch.int64).sum().item()) == dsum
         assert torch.equal(dist, d2)
+    del d2
     del ascii, words
     torch.cuda.empty_cache()
 

@@ -176,3 +176,27 @@ def test_pool_counter_table_matches_oracle_count(oracle, s):
     ec = np.array([x[2] for x in exp], np.uint64)
     ef = np.array([x[3] for x in exp], np.uint64) + np.uint64(i0)
     assert oracle.table_digest(k, c, f) == oracle.table_digest(ek, ec, ef)
+
+
+@pytest.mark.parametrize("L,i0", [(32, 0), (96, 0), (96, 77_777_777), (512, 0), (512, 49_990_000)])
+def test_stream_digest_construction(oracle, L, i0):
+    """The numpy construction behind tests/golden/stream_digests.json (generator words, distances to
+    read 0) equals the oracle's encode / hamming of the generator's ASCII, at offsets into the batch."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "gen_stream_digests", os.path.join(os.path.dirname(__file__), "golden", "gen_stream_digests.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    n = 3000
+    ascii = oracle.gen_reads(1, i0, n, L)
+    words, rc, _ = oracle.encode_batch(ascii, n, L)
+    assert rc == 0
+    mine = g.gen_words(1, i0, n, L)
+    assert np.array_equal(words, mine)
+    ref = g.gen_words(1, 0, 1, L)[0]
+    assert np.array_equal(g.hamming_ref(mine, ref), oracle.hamming_ref_batch(words, n, L, ref))
+    if i0 == 0:   # the chunked digest of a prefix equals the SHA of the oracle's arrays
+        ws, ds = g.digests(n, L, 1, chunk=700)
+        assert ws == _sha(words)
+        assert ds == _sha(oracle.hamming_ref_batch(words, n, L, words[0]))

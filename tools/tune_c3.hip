@@ -1,0 +1,187 @@
+// tools/tune_c3.hip — C3 fused encode + hamming (96 nt, dense) : the LDS-sum kernel k_encode_ham_dense
+// (production) against a no-LDS lane-row form k_encode_ham6w in block shapes (measured slower:
+// 0.772 vs 0.784 of 8 TB/s for the best shape, T256 G1, same box, gpurun_out/tune_c3_6w.log).  Every
+// variant's packed words, distances and first-bad read are checked against the production launch
+// (ss_encode_hamming_ref) on a tail-heavy small batch with an invalid byte and on the timed batch.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include tools/tune_c3.hip -o tools/tune_c3
+#include "../shortseq_amd/csrc/ss_codec.hip"
+#include "../shortseq_amd/csrc/ss_runtime.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+namespace {
+// Dense fused encode + hamming for 96-nt reads (6 chunks = 3 words) with no LDS and no barrier, in
+// k_ham_dense3w's layout: a wave streams groups of 3 whole 1-KiB rows of chunks (192 dwordx4 =
+// 32 reads, line-aligned, every lane busy).  Group lane Lg = 64 j + lane holds chunk Lg (chunk
+// k = Lg % 6 of read Lg / 6; 64 = 4 mod 6).  Per-chunk distances are summed over lane pairs by one
+// DPP op, lane 6m adds the pairs at 6m + 2 and 6m + 4 by shuffle (the two reads that straddle a
+// row boundary, Lg = 60..65 and 126..131, take the next row's lanes 0 / 2 by readlane) and stores
+// read m's distance.  Loads are unconditional from a clamped chunk index (no per-load branch).
+template <int T, int G>
+__global__ __launch_bounds__(T) void k_encode_ham6w(G16Args a) {
+    constexpr uint32_t NWV = T / 64;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t nq = a.n * 6, qmax = nq - 1;
+    uint4 x[G][3];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t q = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 192 + j * 64 + lane;
+            x[g][j] = ld_stream(&a.in[min(q, qmax)]);
+        }
+    uint32_t rf[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) rf[k] = a.ref32[k];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint64_t grp = ((uint64_t)blockIdx.x * G + g) * NWV + wv;
+        uint32_t p[3], kk[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t q = grp * 192 + j * 64 + lane;
+            const bool live = q < nq;
+            kk[j] = (lane + 4u * j) % 6u;
+            uint32_t bad;
+            const uint32_t v = encode_chunk<kPathPext>(x[g][j], kk[j], a, bad);
+            report_bad_div(live && bad != 0u, q, 6, a.first_bad);
+            if (live && a.out32) st_stream(&a.out32[q], v);
+            const uint32_t r = kk[j] == 0 ? rf[0] : kk[j] == 1 ? rf[1] : kk[j] == 2 ? rf[2]
+                             : kk[j] == 3 ? rf[3] : kk[j] == 4 ? rf[4] : rf[5];
+            const uint32_t d = live ? ham32(v ^ r) : 0u;
+            p[j] = d + swap_pair(d);                   // even lanes: chunks Lg, Lg + 1
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            uint32_t p2 = __shfl(p[j], (int)min(lane + 2u, 63u));
+            uint32_t p4 = __shfl(p[j], (int)min(lane + 4u, 63u));
+            if (j == 0) {           // Lg = 60: chunks 64, 65 are row 1's lanes 0, 1
+                const uint32_t n0 = __builtin_amdgcn_readlane(p[1], 0);
+                if (lane == 60) p4 = n0;
+            } else if (j == 1) {    // Lg = 126: chunks 128..131 are row 2's lanes 0..3
+                const uint32_t n0 = __builtin_amdgcn_readlane(p[2], 0), n2 = __builtin_amdgcn_readlane(p[2], 2);
+                if (lane == 62) {
+                    p2 = n0;
+                    p4 = n2;
+                }
+            }
+            if (kk[j] == 0) {
+                const uint64_t r = grp * 32 + (64u * j + lane) / 6u;
+                if (r < a.n) st_stream(&a.counts[r], p[j] + p2 + p4);
+            }
+        }
+    }
+}
+}  // namespace
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+static G16Args args(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
+    G16Args a;
+    a.in = (const uint4*)in;
+    a.in_stride16 = 6;
+    a.out32 = (uint32_t*)words;
+    a.wpr2 = 6;
+    a.n = n;
+    a.cpr = 6;
+    a.full2 = 6;
+    a.all_table = 0;
+    a.logG = 3;
+    a.ref32 = (const uint32_t*)ref;
+    a.ham2 = 6;
+    a.counts = out;
+    a.first_bad = (unsigned long long*)fb;
+    return a;
+}
+
+template <int T, int G>
+static void v6w(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
+    reset_first_bad(fb, 0);
+    const uint64_t per = (uint64_t)32 * (T / 64) * G;
+    hipLaunchKernelGGL((k_encode_ham6w<T, G>), dim3((unsigned)((n + per - 1) / per)), dim3(T), 0, 0,
+                       args(in, n, words, ref, out, fb));
+}
+
+static void prod(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
+    if (ss_encode_hamming_ref(in, n, 96, 96, words, 3, ref, out, fb, 0)) { printf("prod failed\n"); exit(1); }
+}
+
+typedef void (*Fn)(const uint8_t*, uint64_t, uint64_t*, const uint64_t*, uint32_t*, uint64_t*);
+
+int main(int argc, char** argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 30;
+    const uint64_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 100000000ull;
+    const uint64_t ns = 1000003;   // small check batch: tails, an invalid byte
+    uint8_t* in;
+    uint64_t *w0, *w1, *ref, *fb;
+    uint32_t *d0, *d1;
+    CK(hipMalloc(&in, n * 96));
+    CK(hipMalloc(&w0, n * 24));
+    CK(hipMalloc(&w1, n * 24));
+    CK(hipMalloc(&ref, 24));
+    CK(hipMalloc(&fb, 8));
+    CK(hipMalloc(&d0, n * 4));
+    CK(hipMalloc(&d1, n * 4));
+    if (ss_synth_reads(in, 7, 0, n, 96, 96, 0)) { printf("synth failed\n"); exit(1); }
+    prod(in, n, w0, w0, d0, fb);           // words of read 12345 as the reference
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref, w0 + 3 * 12345, 24, hipMemcpyDeviceToDevice));
+    const struct { const char* name; Fn f; } vs[] = {
+        {"prod k_encode_ham_dense<192,4>", prod},
+        {"6w T256 G1", v6w<256, 1>}, {"6w T256 G2", v6w<256, 2>}, {"6w T512 G1", v6w<512, 1>},
+        {"6w T512 G2", v6w<512, 2>}, {"6w T128 G2", v6w<128, 2>}, {"6w T1024 G1", v6w<1024, 1>},
+    };
+    const int nv = sizeof(vs) / sizeof(vs[0]);
+    // correctness: small batch with an invalid byte in read 777777 (chunk 4), then the full batch
+    std::vector<uint8_t> hb(1);
+    bool all_ok = true;
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint64_t m = pass == 0 ? ns : n;
+        if (pass == 0) { uint8_t nb = 'N'; CK(hipMemcpy(in + 777777ull * 96 + 70, &nb, 1, hipMemcpyHostToDevice)); }
+        std::vector<uint32_t> hd0(m), hd1(m);
+        std::vector<uint64_t> hw0(m * 3), hw1(m * 3);
+        uint64_t f0, f1;
+        prod(in, m, w0, ref, d0, fb);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(hd0.data(), d0, m * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hw0.data(), w0, m * 24, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&f0, fb, 8, hipMemcpyDeviceToHost));
+        for (int v = 1; v < nv; ++v) {
+            CK(hipMemset(d1, 0xAB, m * 4));
+            CK(hipMemset(w1, 0xAB, m * 24));
+            vs[v].f(in, m, w1, ref, d1, fb);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(hd1.data(), d1, m * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(hw1.data(), w1, m * 24, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(&f1, fb, 8, hipMemcpyDeviceToHost));
+            const bool ok = hd0 == hd1 && hw0 == hw1 && f0 == f1;
+            all_ok &= ok;
+            printf("check n=%llu %-32s %s (first_bad %llu vs %llu)\n", (unsigned long long)m, vs[v].name,
+                   ok ? "OK" : "MISMATCH", (unsigned long long)f1, (unsigned long long)f0);
+        }
+        if (pass == 0) { uint8_t ab = 'A'; CK(hipMemcpy(in + 777777ull * 96 + 70, &ab, 1, hipMemcpyHostToDevice)); }
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double bytes = 124.0 * (double)n;
+    for (int round = 0; round < 3; ++round) {
+        for (int v = 0; v < nv; ++v) {
+            for (int i = 0; i < 5; ++i) vs[v].f(in, n, w1, ref, d1, fb);
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < reps; ++i) vs[v].f(in, n, w1, ref, d1, fb);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= reps;
+            printf("round %d %-32s %.4f ms  %.0f GB/s  frac %.3f\n", round, vs[v].name, ms, bytes / ms / 1e6,
+                   bytes / ms / 1e6 / 8000.0);
+        }
+    }
+    printf(all_ok ? "ALL OK\n" : "SOME MISMATCH\n");
+    return all_ok ? 0 : 2;
+}
