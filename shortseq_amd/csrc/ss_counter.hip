@@ -905,6 +905,10 @@ constexpr uint32_t kHeavy = SS_PF_HEAVY;
 #endif
 // k_pf_coarse: issue the next tile's loads right after this tile's encode (1), after the tile's
 // reservation barrier (2), or at the top of each tile (0)
+#ifndef SS_PF_LATE
+#define SS_PF_LATE 0   // 1: wave 0 consumes the coarse reservation after its staging writes (same-box
+                       // medians uniform 2.536 -> 2.587, Zipf 2.605 -> 2.567 ms: within the spread, off)
+#endif
 #ifndef SS_PF_PREFETCH
 #define SS_PF_PREFETCH 0
 #endif
@@ -1030,16 +1034,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
     // wave 0 lane, bins b0 = 2 lane and b0 + 1: reserve c0 / c1 slots of their sub-bins (b, sub) with
     // one 64-bit atomic on the pair's word (only the bins flagged in `mask`: bit 0 = b0, bit 1 =
     // b0 + 1); the part past cap1 reserves spill records (a second atomic, rare)
-    auto reserve = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) {
+    auto reserve_issue = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) -> uint64_t {
         const uint64_t add = ((mask & 1u) ? (uint64_t)c0 : 0ull) | ((mask & 2u) ? (uint64_t)c1 << 32 : 0ull);
 #if SS_PF_DET   // measurement only: tile-local positions, no reservation atomics (results invalid)
-        const uint64_t g2 = 0;
         (void)add;
+        return 0;
 #else
-        const uint64_t g2 = add ? atomicAdd((unsigned long long*)&fill[fill_at(b0 * kFinePerBin + sub)],
-                                            (unsigned long long)add)
-                                : 0ull;
+        return add ? atomicAdd((unsigned long long*)&fill[fill_at(b0 * kFinePerBin + sub)], (unsigned long long)add)
+                   : 0ull;
 #endif
+    };
+    // the reservation's bases (gbase) and spill runs (sbase) from the atomic's return value
+    auto reserve_finish = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask, uint64_t g2) {
 #pragma unroll
         for (uint32_t k = 0; k < 2; ++k) {
             if (!(mask & (1u << k))) continue;
@@ -1048,6 +1054,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             const uint64_t end = (uint64_t)g + c, from = max((uint64_t)g, cap1);
             sbase[b0 + k] = end > from ? atomicAdd(spill_ctr, (uint32_t)(end - from)) : 0u;
         }
+    };
+    auto reserve = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) {
+        reserve_finish(b0, c0, c1, mask, reserve_issue(b0, c0, c1, mask));
     };
     static_assert(kCB == 128, "wave 0 scans two bins per lane");
     for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
@@ -1081,9 +1090,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
         }
         if (SS_PF_PREFETCH == 1 && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
         __syncthreads();                                                  // (A)
+        // wave 0: the reservation atomic of bins b0 = 2 lane, b0 + 1 (SS_PF_LATE: its return value is
+        // consumed after this wave's staging, so the round trip overlaps the staging phase)
+        uint32_t c0 = 0, c1 = 0, rmask = 0;
+        uint64_t g2 = 0;
         if (threadIdx.x < 64) {
             const uint32_t lane = threadIdx.x, b0 = 2 * lane;
-            const uint32_t c0 = lcount[b0], c1 = lcount[b0 + 1];
+            c0 = lcount[b0];
+            c1 = lcount[b0 + 1];
             uint32_t incl = c0 + c1;
             for (uint32_t off = 1; off < 64; off <<= 1) {
                 const uint32_t y = __shfl_up(incl, off);
@@ -1095,7 +1109,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             const bool h0 = c0 > kHeavy, h1 = c1 > kHeavy;
             hflag[b0] = h0;
             hflag[b0 + 1] = h1;
-            reserve(b0, c0, c1, (h0 ? 0u : 1u) | (h1 ? 0u : 2u));
+            rmask = (h0 ? 0u : 1u) | (h1 ? 0u : 2u);
+            if (SS_PF_LATE) g2 = reserve_issue(b0, c0, c1, rmask);
+            else reserve(b0, c0, c1, rmask);
             const uint64_t hv = __ballot(h0 || h1);
             if (lane == 0) any_heavy = hv != 0;
             lcount[b0] = 0;
@@ -1118,6 +1134,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
                 sbin[sp] = (uint8_t)bin[j];
             }
         }
+        if (SS_PF_LATE && threadIdx.x < 64) reserve_finish(2 * threadIdx.x, c0, c1, rmask, g2);
         if (heavy_tile)
             for (uint32_t i = threadIdx.x; i < TILE; i += T) ht[i] = 0;
         __syncthreads();                                                  // (C)
