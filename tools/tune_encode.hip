@@ -157,6 +157,122 @@ void run(const char* name, Buf& b, int reps, int blocks_per_cu) {
     fflush(stdout);
 }
 
+// Wide-store form: a block owns T*U contiguous chunks; lane t loads chunks j*T + t (coalesced), its
+// u32 results go to LDS in chunk order and come back as one dwordx4 (U = 4) or two (U = 8) per lane,
+// stored contiguously (1 KiB per wave store instruction instead of 256 B).
+template <int T, int U, int MODE>
+__global__ __launch_bounds__(T) void k_w4(const uint4* __restrict__ in, uint32_t* __restrict__ out,
+                                          uint64_t nchunks, unsigned long long* fb) {
+    static_assert(U == 4 || U == 8, "U = 4 or 8");
+    __shared__ uint32_t s[T * U];
+    const uint64_t base = (uint64_t)blockIdx.x * T * U;
+    uint4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * T + threadIdx.x;
+        x[j] = g < nchunks ? ld_stream(&in[g]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * T + threadIdx.x;
+        uint32_t v;
+        if constexpr (MODE == ENC) {
+            Enc32 e = encode16(x[j].x, x[j].y, x[j].z, x[j].w, true);
+            v = e.v | ((threadIdx.x & 1u) ? swap_pair(e.cout) : 0u);
+            report_bad(g < nchunks && e.bad != 0u, g >> 1, fb);
+        } else {
+            v = x[j].x ^ x[j].y ^ x[j].z ^ x[j].w;
+        }
+        s[j * T + threadIdx.x] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < U / 4; ++h) {
+        const uint32_t q = h * T + threadIdx.x;                 // dwordx4 index within the block
+        const uint64_t g = base + 4ull * q;
+        const uint4 o = *(const uint4*)&s[4 * q];
+        if (g + 3 < nchunks) {
+            const u32x4 v = {o.x, o.y, o.z, o.w};
+            __builtin_nontemporal_store(v, (u32x4*)&out[g]);
+        } else {
+            const uint32_t a[4] = {o.x, o.y, o.z, o.w};
+            for (int k = 0; k < 4; ++k) if (g + k < nchunks) out[g + k] = a[k];
+        }
+    }
+}
+
+template <int T, int U, int MODE>
+void run_w4(const char* name, Buf& b, int reps) {
+    const unsigned grid = (unsigned)((b.nchunks + (uint64_t)T * U - 1) / ((uint64_t)T * U));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_w4<T, U, MODE>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
+    CK(hipDeviceSynchronize());
+    double s = 0, mn = 1e9;
+    for (int r = 0; r < reps; ++r) {
+        float ms;
+        CK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL((k_w4<T, U, MODE>), dim3(grid), dim3(T), 0, 0, b.in, b.out, b.nchunks, b.fb);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        s += ms;
+        mn = std::min<double>(mn, ms);
+    }
+    const double bytes = (double)b.nreads * 40.0;
+    printf("%-44s grid %7u  avg %.4f ms  min %.4f ms  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", name, grid, s / reps, mn,
+           bytes / (s / reps) / 1e6, bytes / mn / 1e6);
+    fflush(stdout);
+}
+
+// decode, wide loads: lane t loads one dwordx4 = 4 half-words, LDS, then a coalesced 16-B store per chunk
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_dec_w4(const uint32_t* __restrict__ w, uint4* __restrict__ out, uint64_t nchunks) {
+    __shared__ uint32_t s[T * U];
+    const uint64_t base = (uint64_t)blockIdx.x * T * U;
+#pragma unroll
+    for (int h = 0; h < U / 4; ++h) {
+        const uint32_t q = h * T + threadIdx.x;
+        const uint64_t g = base + 4ull * q;
+        uint4 v;
+        if (g + 3 < nchunks) v = *(const uint4*)&w[g];
+        else v = make_uint4(g < nchunks ? w[g] : 0u, g + 1 < nchunks ? w[g + 1] : 0u, g + 2 < nchunks ? w[g + 2] : 0u, 0u);
+        *(uint4*)&s[4 * q] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t g = base + (uint64_t)j * T + threadIdx.x;
+        if (g < nchunks) out[g] = decode16(s[j * T + threadIdx.x]);
+    }
+}
+
+template <int T, int U>
+void run_dec_w4(const char* name, uint32_t* w, uint4* out, uint64_t nchunks, int reps) {
+    unsigned grid = (unsigned)((nchunks + (uint64_t)T * U - 1) / ((uint64_t)T * U));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_dec_w4<T, U>), dim3(grid), dim3(T), 0, 0, w, out, nchunks);
+    CK(hipDeviceSynchronize());
+    double s = 0, mn = 1e9;
+    for (int r = 0; r < reps; ++r) {
+        float ms;
+        CK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL((k_dec_w4<T, U>), dim3(grid), dim3(T), 0, 0, w, out, nchunks);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        s += ms;
+        mn = std::min<double>(mn, ms);
+    }
+    double bytes = (double)nchunks * 20.0;
+    printf("%-44s grid %7u  avg %.4f ms  min %.4f ms  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", name, grid, s / reps, mn,
+           bytes / (s / reps) / 1e6, bytes / mn / 1e6);
+    fflush(stdout);
+}
+
 int main(int argc, char** argv) {
     uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 100000000ull;
     int reps = argc > 2 ? atoi(argv[2]) : 20;
@@ -173,6 +289,28 @@ int main(int argc, char** argv) {
     // ceilings
     run<1024, 2, true, false, false, COPY, false, true>("copy4to1 T1024 U2 nt ntstore", b, reps, 0);
     run<256, 4, true, false, false, READ>("readonly T256 U4 nt", b, reps, 0);
+    // wide-store forms (verified against the production-shape kernel's output below)
+    run<768, 2, true, false, false, ENC, false, true>("enc T768 U2 nt ntstore (production)", b, reps, 0);
+    std::vector<uint32_t> h0(b.nchunks), h1(b.nchunks);
+    CK(hipMemcpy(h0.data(), b.out, b.nchunks * 4, hipMemcpyDeviceToHost));
+    run_w4<256, 4, ENC>("enc-w4 T256 U4", b, reps);
+    CK(hipMemcpy(h1.data(), b.out, b.nchunks * 4, hipMemcpyDeviceToHost));
+    printf("enc-w4 T256 U4 output %s\n", h0 == h1 ? "OK" : "MISMATCH");
+    run_w4<512, 4, ENC>("enc-w4 T512 U4", b, reps);
+    run_w4<256, 8, ENC>("enc-w4 T256 U8", b, reps);
+    CK(hipMemcpy(h1.data(), b.out, b.nchunks * 4, hipMemcpyDeviceToHost));
+    printf("enc-w4 T256 U8 output %s\n", h0 == h1 ? "OK" : "MISMATCH");
+    run_w4<512, 8, ENC>("enc-w4 T512 U8", b, reps);
+    run_w4<1024, 4, ENC>("enc-w4 T1024 U4", b, reps);
+    run_w4<256, 4, COPY>("copy-w4 T256 U4", b, reps);
+    run_w4<512, 8, COPY>("copy-w4 T512 U8", b, reps);
+    run<768, 2, true, false, false, ENC, false, true>("enc T768 U2 nt ntstore (production, repeat)", b, reps, 0);
+    run_dec<256, 2, false, false>("dec T256 U2 (production)", b.out, b.in, b.nchunks, reps);
+    run_dec_w4<256, 4>("dec-w4 T256 U4", b.out, b.in, b.nchunks, reps);
+    run_dec_w4<256, 8>("dec-w4 T256 U8", b.out, b.in, b.nchunks, reps);
+    run_dec_w4<512, 4>("dec-w4 T512 U4", b.out, b.in, b.nchunks, reps);
+    run_dec<256, 2, false, false>("dec T256 U2 (production, repeat)", b.out, b.in, b.nchunks, reps);
+    if (argc > 3) return 0;
     // encode variants around the round-2 winner
     run<1024, 2, true, false, false, ENC, false, true>("enc T1024 U2 nt ntstore (production r1b)", b, reps, 0);
     run<1024, 2, true, false, false, ENC, true, true>("enc T1024 U2 nt ntstore xcd", b, reps, 0);
