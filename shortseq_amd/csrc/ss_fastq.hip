@@ -327,9 +327,15 @@ constexpr uint64_t kFqTile1 = (uint64_t)kFqT * kFqU1 * 16;     // 32 KiB per til
 
 constexpr uint32_t kStageShards = 64, kShardStride = 32;       // counters 128 B apart
 constexpr uint32_t kLdsPos = 4096;                             // newline positions gathered in LDS
+// SS_FQ_TILE_CAP > 0: every tile also owns a fixed run of that many staging words (after the
+// shards' regions); a tile with at most that many newlines stages there with no reservation atomic
+#ifndef SS_FQ_TILE_CAP
+#define SS_FQ_TILE_CAP 0   // same-box A/B (tools/tune_f1.hip): 1024 / 4096 within the run-to-run spread, off
+#endif
+constexpr uint32_t kTileCap = SS_FQ_TILE_CAP;
 
 struct FqStage {
-    uint32_t* pos;        // [kStageShards * region] staged newline positions
+    uint32_t* pos;        // [kStageShards * region (+ tiles * kTileCap)] staged newline positions
     uint64_t region;      // staging words per shard
     uint32_t* used;       // [kStageShards * kShardStride] run reservations per shard
     uint32_t* ovf;        // a shard's region ran full
@@ -373,7 +379,9 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
         const uint32_t sh = blockIdx.x % kStageShards;
         uint64_t run = (uint64_t)sh * st.region;
         uint32_t c = cnt;
-        if (c) {
+        if (kTileCap && c <= kTileCap) {
+            run = (uint64_t)kStageShards * st.region + (uint64_t)blockIdx.x * kTileCap;
+        } else if (c) {
             const uint32_t r = atomicAdd(&st.used[sh * kShardStride], c);
             if (r + (uint64_t)c > st.region) {
                 atomicExch(st.ovf, 1u);
@@ -718,7 +726,7 @@ inline uint64_t fq_region(uint64_t max_reads) {
 uint64_t ss_fastq_onepass_ws_bytes(uint64_t nbytes, uint64_t max_reads) {
     const uint64_t t = fq_tiles1(nbytes);
     return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 8 + 4ull * kNulCap + 8 * t +
-           4 * kStageShards * fq_region(max_reads) + 16;
+           4 * kStageShards * fq_region(max_reads) + 4ull * kTileCap * t + 16;
 }
 
 int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, void* d_ws,
@@ -727,7 +735,8 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     int rc = fq_check(d_buf, nbytes, d_ws, d_counts, max_reads, d_offsets, d_lens, d_aux);
     if (rc) return rc;
     if (ws_bytes < ss_fastq_onepass_ws_bytes(nbytes, max_reads)) return ss_fail(SS_EARG, "workspace too small");
-    if (kStageShards * fq_region(max_reads) >= (1ull << 32)) return ss_fail(SS_EARG, "max_reads too large");
+    if (kStageShards * fq_region(max_reads) + (uint64_t)kTileCap * fq_tiles1(nbytes) >= (1ull << 32))
+        return ss_fail(SS_EARG, "max_reads too large");
     hipStream_t s = (hipStream_t)stream;
     const uint64_t t = fq_tiles1(nbytes), g = fq_groups(t);
     uint64_t* tile_base = (uint64_t*)d_ws;
