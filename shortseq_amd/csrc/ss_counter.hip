@@ -1683,6 +1683,11 @@ __device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t
     return S;
 }
 
+// SS_AGG_PERSIST: a grid of the resident blocks walks the regions (region += gridDim.x) instead of
+// one block per region
+#ifndef SS_AGG_PERSIST
+#define SS_AGG_PERSIST 0   // 1 measured slower: aggregate 0.63 -> 0.87 ms, insert 2.74 -> 2.91 ms (same box, gpurun_out/ab_apers.log)
+#endif
 template <int T, bool REC12>
 __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index, bool fresh = false) {
     const uint32_t S = (uint32_t)t.slice_mask + 1;
@@ -1691,7 +1696,8 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     uint32_t* bcnt = (uint32_t*)(skey + S);                   // [S] this batch's count
     uint32_t* bfst = bcnt + S;                                // [S] this batch's first read index
     __shared__ uint32_t sent[3];   // sentinel count, sentinel first, slice occupancy
-    const uint32_t region = blockIdx.x;
+    const uint32_t nreg = SS_AGG_PERSIST ? w.R : gridDim.x;
+    for (uint32_t region = blockIdx.x; region < nreg; region += gridDim.x) {
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
     for (uint32_t i = threadIdx.x; i < S; i += T) {
         skey[i] = fresh ? kEmpty : t.slots[slice_base + i].key;
@@ -1819,6 +1825,8 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         Slot* ss = &t.slots[t.mask + 1];
         atomicAdd(&ss->ncount, 0u - sent[0]);
         atomicMin(&ss->first, (uint32_t)(base_index + sent[1]));
+    }
+    if (SS_AGG_PERSIST) __syncthreads();   // the next region re-initialises the LDS slice and sent[]
     }
 }
 
@@ -2599,12 +2607,25 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
             if (SS_PF_STOP == 2) return ss_check(hipGetLastError(), "fine scatter");
             w.bkey = w.keys;
+            unsigned agg_grid = w.R;
+            if (SS_AGG_PERSIST) {
+                static int agg_res = 0;
+                if (!agg_res) {
+                    int dev = 0, cus = 0, per = 0;
+                    (void)hipGetDevice(&dev);
+                    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &per, (const void*)k_pc_aggregate_slice<kAggSliceT, true>, kAggSliceT, ((size_t)1 << kSliceLogMax) * 16);
+                    agg_res = (cus > 0 && per > 0) ? cus * per : 1024;
+                }
+                agg_grid = w.R < (unsigned)agg_res ? w.R : (unsigned)agg_res;
+            }
             if (SS_FS_AOS) {
                 w.brec = (const Rec12*)w.keys;
-                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, true>), dim3(w.R), dim3(kAggSliceT),
+                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, true>), dim3(agg_grid), dim3(kAggSliceT),
                                    ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
             } else {
-                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(w.R), dim3(kAggSliceT),
+                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(agg_grid), dim3(kAggSliceT),
                                    ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
             }
             // records that found their sub-bin full (none unless many distinct keys pile into a bin)
