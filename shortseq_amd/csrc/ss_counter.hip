@@ -1686,7 +1686,7 @@ __device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t
 // SS_AGG_PERSIST: a grid of the resident blocks walks the regions (region += gridDim.x) instead of
 // one block per region
 #ifndef SS_AGG_PERSIST
-#define SS_AGG_PERSIST 0   // 1 measured slower: aggregate 0.63 -> 0.87 ms, insert 2.74 -> 2.91 ms (same box, gpurun_out/ab_apers.log)
+#define SS_AGG_PERSIST 0   // 1 measured slower: aggregate 0.63 -> 0.87 ms, insert 2.74 -> 2.91 ms (same box, profiles/r2/r2f/ab_apers.log)
 #endif
 template <int T, bool REC12>
 __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index, bool fresh = false) {

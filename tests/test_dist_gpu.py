@@ -142,3 +142,50 @@ def test_bench_two_ranks_rehearsal():
     assert r["extra"]["C5_counter_32"]["parity"] == "digest uniform_U24_job2"
     for k, v in r["extra"].items():
         assert "error" not in v, (k, v)
+
+
+def _rccl_worker(port, q):
+    """One rank on the nccl backend (RCCL): the exchange helpers with device tensors, as the
+    multi-GPU bench calls them (a 1-rank all-to-all is a copy to itself)."""
+    sys.path[:0] = [REPO]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from shortseq_amd.dist import exchange, exchange_packed
+        assert dist.get_backend() == "nccl"
+        g = torch.Generator().manual_seed(3)
+        m = 100_003
+        rec = torch.randint(-2 ** 62, 2 ** 62, (m + 17, 2), generator=g, dtype=torch.int64).to(dev)
+        recv, sizes, bases, ex = exchange_packed(rec, torch.tensor([m], device=dev), 12345,
+                                                 extra=torch.tensor([7], dtype=torch.int32, device=dev))
+        ok = torch.equal(recv, rec[:m]) and sizes == [m] and bases == [12345] and ex == [7]
+        k = rec[:, 0].contiguous()
+        kk, cc, ff, rs = exchange(k, k + 1, k + 2, torch.tensor([m], device=dev), with_sizes=True)
+        ok = ok and torch.equal(kk, k[:m]) and torch.equal(cc, k[:m] + 1) and torch.equal(ff, k[:m] + 2) and rs == [m]
+        f = torch.tensor([1], dtype=torch.int32, device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        q.put(bool(ok) and int(f.item()) == 1)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_helpers_world1():
+    """The RCCL path of the exchange (backend nccl, device tensors, uneven split sizes passed from
+    the host) at world size 1: the only RCCL configuration a 1-GPU box can form."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    ok = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert ok
