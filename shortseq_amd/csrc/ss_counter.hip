@@ -1686,7 +1686,8 @@ __device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t
 // SS_AGG_PERSIST: a grid of the resident blocks walks the regions (region += gridDim.x) instead of
 // one block per region
 #ifndef SS_AGG_PERSIST
-#define SS_AGG_PERSIST 0   // 1 measured slower: aggregate 0.63 -> 0.87 ms, insert 2.74 -> 2.91 ms (same box, profiles/r2/r2f/ab_apers.log)
+#define SS_AGG_PERSIST 0   // 1 measured slower: aggregate 0.63 -> 0.87 ms, insert 2.74 -> 2.91 ms (same box, both
+                           // builds with the loop's 80 VGPRs; profiles/r2/r2f/ab_apers.log)
 #endif
 template <int T, bool REC12>
 __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index, bool fresh = false) {
@@ -1696,8 +1697,12 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     uint32_t* bcnt = (uint32_t*)(skey + S);                   // [S] this batch's count
     uint32_t* bfst = bcnt + S;                                // [S] this batch's first read index
     __shared__ uint32_t sent[3];   // sentinel count, sentinel first, slice occupancy
-    const uint32_t nreg = SS_AGG_PERSIST ? w.R : gridDim.x;
-    for (uint32_t region = blockIdx.x; region < nreg; region += gridDim.x) {
+#if SS_AGG_PERSIST
+    for (uint32_t region = blockIdx.x; region < w.R; region += gridDim.x) {
+#else
+    {
+    const uint32_t region = blockIdx.x;   // (the loop form costs 58 -> 80 VGPRs even when it runs once)
+#endif
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
     for (uint32_t i = threadIdx.x; i < S; i += T) {
         skey[i] = fresh ? kEmpty : t.slots[slice_base + i].key;
