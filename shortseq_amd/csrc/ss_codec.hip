@@ -129,22 +129,31 @@ __global__ __launch_bounds__(T) void k_encode_g16(G16Args a) {
 
 // Dense fused encode + hamming for any even chunks-per-read (e.g. 96 nt: 6 chunks = 3 words): the
 // block owns rpb whole reads = rpb*cpr consecutive chunks (dense, coalesced loads/stores as in the
-// DENSE encode); per-read sums go through LDS atomics, then one coalesced u32 store per read.
+// DENSE encode); per-chunk distances (<= 16) go to LDS bytes, then one thread per read sums them and
+// stores the read's distance (the reads of a block are contiguous: coalesced u32 stores).
+// PAD8 (cpr <= 8): a read's bytes are padded to 8 (byte 8 rl + k), so the sum is one 8-B LDS read
+// and two v_sad_u8 instead of cpr byte reads (96 nt: 0.775-0.784 -> 0.790-0.795 of peak, same box,
+// tools/tune_c3.hip); otherwise byte cl of the block's chunk order.
 // Local read index = floor((cl + 0.5) * (1/cpr)) in f32 (exact for cl < 4096, cpr <= 64; checked
 // exhaustively, and written with _rn intrinsics so no FMA contraction changes the rounding).
-template <int PATH, int T, int U, bool NTST>
+template <int PATH, int T, int U, bool NTST, bool PAD8>
 __global__ __launch_bounds__(T) void k_encode_ham_dense(G16Args a, uint32_t rpb, float inv_cpr) {
-    __shared__ uint8_t part[T * U];                  // per-chunk distance (<= 16), chunk order
+    constexpr int kPartWords = PAD8 ? T * U / 2 : T * U / 8;   // PAD8: rpb <= T U / 2 reads (cpr >= 2)
+    __shared__ uint64_t part8[kPartWords];
+    uint8_t* part = (uint8_t*)part8;
     const uint64_t r0 = (uint64_t)blockIdx.x * rpb;
     const uint32_t nr = (uint32_t)min((uint64_t)rpb, a.n - r0);
     const uint32_t nloc = nr * a.cpr;
     const uint64_t c0 = r0 * a.cpr;
+    if constexpr (PAD8)
+        for (uint32_t i = threadIdx.x; i < rpb; i += T) part8[i] = 0;   // bytes cpr..7 of each read stay 0
     uint4 x[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const uint32_t cl = j * T + threadIdx.x;
         x[j] = cl < nloc ? ld_stream(&a.in[c0 + cl]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
     }
+    if constexpr (PAD8) __syncthreads();            // the zeroed reads before any byte lands
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const uint32_t cl = j * T + threadIdx.x;
@@ -158,13 +167,23 @@ __global__ __launch_bounds__(T) void k_encode_ham_dense(G16Args a, uint32_t rpb,
             if constexpr (NTST) st_stream(&a.out32[c0 + cl], v);
             else a.out32[c0 + cl] = v;
         }
-        part[cl] = (uint8_t)((live && k < a.ham2) ? ham32(v ^ a.ref32[k]) : 0u);
+        const uint8_t d = (uint8_t)((live && k < a.ham2) ? ham32(v ^ a.ref32[k]) : 0u);
+        if constexpr (PAD8) {
+            if (live) part[8 * rl + k] = d;
+        } else {
+            part[cl] = d;
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nr; i += T) {
         uint32_t sum = 0;
-        for (uint32_t k = 0; k < a.cpr; ++k) sum += part[i * a.cpr + k];
-        a.counts[r0 + i] = sum;
+        if constexpr (PAD8) {
+            const uint64_t p = part8[i];
+            sum = __builtin_amdgcn_sad_u8((uint32_t)p, 0u, 0u) + __builtin_amdgcn_sad_u8((uint32_t)(p >> 32), 0u, 0u);
+        } else {
+            for (uint32_t k = 0; k < a.cpr; ++k) sum += part[i * a.cpr + k];
+        }
+        st_stream(&a.counts[r0 + i], sum);
     }
 }
 
@@ -645,8 +664,12 @@ void launch_g16(const G16Args& a, hipStream_t s) {
 template <int PATH, int T, int U, bool NTST>
 void launch_ham_dense(const G16Args& a, hipStream_t s) {
     const uint32_t rpb = (U * T) / a.cpr;
-    hipLaunchKernelGGL((k_encode_ham_dense<PATH, T, U, NTST>), dim3(grid_for(a.n, rpb)), dim3(T), 0, s, a, rpb,
-                       1.0f / (float)a.cpr);
+    if (a.cpr <= 8)
+        hipLaunchKernelGGL((k_encode_ham_dense<PATH, T, U, NTST, true>), dim3(grid_for(a.n, rpb)), dim3(T), 0, s, a,
+                           rpb, 1.0f / (float)a.cpr);
+    else
+        hipLaunchKernelGGL((k_encode_ham_dense<PATH, T, U, NTST, false>), dim3(grid_for(a.n, rpb)), dim3(T), 0, s, a,
+                           rpb, 1.0f / (float)a.cpr);
 }
 
 template <int T, int U, bool NTLD, bool NTST>

@@ -1,4 +1,4 @@
-// tools/tune_c3.hip — C3 fused encode + hamming (96 nt, dense) : the LDS-sum kernel k_encode_ham_dense
+// tools/tune_c3.hip — C3 fused encode + hamming (96 nt, dense): the production kernel k_encode_ham_dense
 // (production) against a no-LDS lane-row form k_encode_ham6w in block shapes (measured slower:
 // 0.772 vs 0.784 of 8 TB/s for the best shape, T256 G1, same box, gpurun_out/tune_c3_6w.log).  Every
 // variant's packed words, distances and first-bad read are checked against the production launch
@@ -75,6 +75,44 @@ __global__ __launch_bounds__(T) void k_encode_ham6w(G16Args a) {
         }
     }
 }
+
+// LDS-sum kernel with each read's per-chunk distances padded to 8 bytes: the tail sums a read with
+// one 8-B LDS read and two v_sad_u8 instead of cpr byte reads (cpr <= 8)
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_encode_ham_dense8(G16Args a, uint32_t rpb, float inv_cpr) {
+    __shared__ uint64_t part8[T * U / 4];              // >= rpb reads (rpb = T U / cpr, cpr >= 4)
+    uint8_t* part = (uint8_t*)part8;
+    const uint64_t r0 = (uint64_t)blockIdx.x * rpb;
+    const uint32_t nr = (uint32_t)min((uint64_t)rpb, a.n - r0);
+    const uint32_t nloc = nr * a.cpr;
+    const uint64_t c0 = r0 * a.cpr;
+    for (uint32_t i = threadIdx.x; i < rpb; i += T) part8[i] = 0;
+    uint4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t cl = j * T + threadIdx.x;
+        x[j] = cl < nloc ? ld_stream(&a.in[c0 + cl]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t cl = j * T + threadIdx.x;
+        const uint32_t rl = (uint32_t)__fmul_rn(__fadd_rn((float)cl, 0.5f), inv_cpr);
+        const uint32_t k = cl - rl * a.cpr;
+        uint32_t bad;
+        const uint32_t v = encode_chunk<kPathPext>(x[j], k, a, bad);
+        const bool live = cl < nloc;
+        report_bad(live && bad != 0u, r0 + rl, a.first_bad);
+        if (live && a.out32) st_stream(&a.out32[c0 + cl], v);
+        if (live && k < a.ham2) part[8 * rl + k] = (uint8_t)ham32(v ^ a.ref32[k]);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nr; i += T) {
+        const uint64_t p = part8[i];
+        const uint32_t s = __builtin_amdgcn_sad_u8((uint32_t)p, 0u, 0u) + __builtin_amdgcn_sad_u8((uint32_t)(p >> 32), 0u, 0u);
+        st_stream(&a.counts[r0 + i], s);
+    }
+}
 }  // namespace
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -95,6 +133,14 @@ static G16Args args(const uint8_t* in, uint64_t n, uint64_t* words, const uint64
     a.counts = out;
     a.first_bad = (unsigned long long*)fb;
     return a;
+}
+
+template <int T, int U>
+static void v8(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
+    reset_first_bad(fb, 0);
+    const uint32_t rpb = (U * T) / 6;
+    hipLaunchKernelGGL((k_encode_ham_dense8<T, U>), dim3((unsigned)((n + rpb - 1) / rpb)), dim3(T), 0, 0,
+                       args(in, n, words, ref, out, fb), rpb, 1.0f / 6.0f);
 }
 
 template <int T, int G>
@@ -131,8 +177,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(ref, w0 + 3 * 12345, 24, hipMemcpyDeviceToDevice));
     const struct { const char* name; Fn f; } vs[] = {
         {"prod k_encode_ham_dense<192,4>", prod},
-        {"6w T256 G1", v6w<256, 1>}, {"6w T256 G2", v6w<256, 2>}, {"6w T512 G1", v6w<512, 1>},
-        {"6w T512 G2", v6w<512, 2>}, {"6w T128 G2", v6w<128, 2>}, {"6w T1024 G1", v6w<1024, 1>},
+        {"6w T256 G1", v6w<256, 1>}, {"sad8 T192 U4", v8<192, 4>}, {"sad8 T384 U2", v8<384, 2>},
+        {"sad8 T192 U8", v8<192, 8>}, {"sad8 T96 U8", v8<96, 8>}, {"sad8 T384 U4", v8<384, 4>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // correctness: small batch with an invalid byte in read 777777 (chunk 4), then the full batch
