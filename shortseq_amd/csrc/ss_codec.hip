@@ -131,9 +131,10 @@ __global__ __launch_bounds__(T) void k_encode_g16(G16Args a) {
 // block owns rpb whole reads = rpb*cpr consecutive chunks (dense, coalesced loads/stores as in the
 // DENSE encode); per-chunk distances (<= 16) go to LDS bytes, then one thread per read sums them and
 // stores the read's distance (the reads of a block are contiguous: coalesced u32 stores).
-// PAD8 (cpr <= 8): a read's bytes are padded to 8 (byte 8 rl + k), so the sum is one 8-B LDS read
-// and two v_sad_u8 instead of cpr byte reads (96 nt: 0.775-0.784 -> 0.790-0.795 of peak, same box,
-// tools/tune_c3.hip); otherwise byte cl of the block's chunk order.
+// PAD8 (cpr <= 8): a read's bytes are padded to 8 (byte 8 rl + k; the unwritten bytes cpr..7 are
+// masked off), so the sum is one 8-B LDS read and two v_sad_u8 instead of cpr byte reads (96 nt:
+// 0.775-0.784 -> 0.790-0.795 of peak, same box, tools/tune_c3.hip); otherwise byte cl of the block's
+// chunk order.
 // Local read index = floor((cl + 0.5) * (1/cpr)) in f32 (exact for cl < 4096, cpr <= 64; checked
 // exhaustively, and written with _rn intrinsics so no FMA contraction changes the rounding).
 template <int PATH, int T, int U, bool NTST, bool PAD8>
@@ -145,15 +146,12 @@ __global__ __launch_bounds__(T) void k_encode_ham_dense(G16Args a, uint32_t rpb,
     const uint32_t nr = (uint32_t)min((uint64_t)rpb, a.n - r0);
     const uint32_t nloc = nr * a.cpr;
     const uint64_t c0 = r0 * a.cpr;
-    if constexpr (PAD8)
-        for (uint32_t i = threadIdx.x; i < rpb; i += T) part8[i] = 0;   // bytes cpr..7 of each read stay 0
     uint4 x[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const uint32_t cl = j * T + threadIdx.x;
         x[j] = cl < nloc ? ld_stream(&a.in[c0 + cl]) : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
     }
-    if constexpr (PAD8) __syncthreads();            // the zeroed reads before any byte lands
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const uint32_t cl = j * T + threadIdx.x;
@@ -178,7 +176,7 @@ __global__ __launch_bounds__(T) void k_encode_ham_dense(G16Args a, uint32_t rpb,
     for (uint32_t i = threadIdx.x; i < nr; i += T) {
         uint32_t sum = 0;
         if constexpr (PAD8) {
-            const uint64_t p = part8[i];
+            const uint64_t p = part8[i] & (~0ull >> (64 - 8 * a.cpr));   // bytes cpr..7 are never written
             sum = __builtin_amdgcn_sad_u8((uint32_t)p, 0u, 0u) + __builtin_amdgcn_sad_u8((uint32_t)(p >> 32), 0u, 0u);
         } else {
             for (uint32_t k = 0; k < a.cpr; ++k) sum += part[i * a.cpr + k];
