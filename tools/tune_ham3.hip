@@ -30,6 +30,56 @@ static void launch_w(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_
                        (const uint4*)a, (const uint4*)a, ref, n, out);
 }
 
+// LDS-sum form with each read's per-word distances padded to 8 bytes (byte 8 rl + k), summed with one
+// 8-B LDS read and one v_sad_u8 (the C3 fused kernel's tail): block = rpb whole reads as dwordx4
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_ham3_pad8(const uint4* __restrict__ a, const uint64_t* __restrict__ ref,
+                                                 uint64_t n, uint32_t rpb, uint32_t* __restrict__ out) {
+    __shared__ uint64_t part8[2 * T * U / 3 + 2];
+    uint8_t* part = (uint8_t*)part8;
+    const uint64_t r0 = (uint64_t)blockIdx.x * rpb;
+    const uint32_t nr = (uint32_t)min((uint64_t)rpb, n - r0);
+    const uint32_t nw = nr * 3, nfull = nw / 2;
+    const uint64_t q0 = r0 * 3 / 2;
+    const uint64_t rf0 = ref[0], rf1 = ref[1], rf2 = ref[2];
+    uint4 x[U];
+    if (nr == rpb) {   // whole block (rpb even: whole dwordx4): clamped unconditional loads
+#pragma unroll
+        for (int j = 0; j < U; ++j) x[j] = ld_stream(&a[q0 + min((uint32_t)(j * T + threadIdx.x), nfull - 1)]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t ql = j * T + threadIdx.x;
+            if (ql < nfull) x[j] = ld_stream(&a[q0 + ql]);
+            else if (2 * ql < nw) { const uint64_t v = ((const uint64_t*)a)[2 * (q0 + ql)]; x[j] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u); }
+            else x[j] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t ql = j * T + threadIdx.x;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t w = 2 * ql + h;
+            const uint32_t rl = (uint32_t)__fmul_rn(__fadd_rn((float)w, 0.5f), 1.0f / 3.0f);
+            const uint32_t k = w - 3 * rl;
+            const uint64_t v = h ? (((uint64_t)x[j].w << 32) | x[j].z) : (((uint64_t)x[j].y << 32) | x[j].x);
+            const uint64_t rv = k == 0 ? rf0 : (k == 1 ? rf1 : rf2);
+            if (w < nw) part[8 * rl + k] = (uint8_t)ham64(v ^ rv);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nr; i += T)
+        __builtin_nontemporal_store(__builtin_amdgcn_sad_u8((uint32_t)part8[i] & 0xFFFFFFu, 0u, 0u), &out[r0 + i]);
+}
+
+template <int T, int U>
+static void launch_p8(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
+    const uint32_t rpb = ((2u * T * U) / 3u) & ~1u;
+    hipLaunchKernelGGL((k_ham3_pad8<T, U>), dim3((unsigned)((n + rpb - 1) / rpb)), dim3(T), 0, 0, (const uint4*)a, ref, n,
+                       rpb, out);
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 30;
     const uint64_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 100000000ull;
@@ -64,12 +114,15 @@ int main(int argc, char** argv) {
         ms /= reps;
         printf("%-28s %s  %.4f ms  %.3f of 8 TB/s\n", name, ok ? "OK " : "BAD", ms, n * 28.0 / (ms * 1e-3) / 8e12);
     };
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < 3; ++pass) {
         run("prod T256 G1", launch_w<256, 1>);
-        run("T256 G2", launch_w<256, 2>);
-        run("T512 G1", launch_w<512, 1>);
-        run("T128 G2", launch_w<128, 2>);
         run("T1024 G1", launch_w<1024, 1>);
+        run("pad8 T512 U2", launch_p8<512, 2>);
+        run("pad8 T768 U2", launch_p8<768, 2>);
+        run("pad8 T1024 U2", launch_p8<1024, 2>);
+        run("pad8 T1024 U1", launch_p8<1024, 1>);
+        run("pad8 T384 U2", launch_p8<384, 2>);
+        run("pad8 T512 U3", launch_p8<512, 3>);
     }
     return 0;
 }
