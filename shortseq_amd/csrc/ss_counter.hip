@@ -1384,6 +1384,10 @@ __global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ f
 #ifndef SS_FS_TILE
 #define SS_FS_TILE 4096
 #endif
+#ifndef SS_FS_W0SCAN
+#define SS_FS_W0SCAN 0   // 1: per-tile region scan by wave 0 alone (2 barriers instead of 5): measured slower,
+                         // scatter 0.72 -> 0.82 ms same box (profiles/r2/r2f/ab_w0.log)
+#endif
 template <int T, uint32_t kTile>
 __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill,
                                                   const uint32_t* __restrict__ order) {
@@ -1440,11 +1444,18 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
         }
     };
     if (lo < hi) load_tile(lo);
-    for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
-        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
+    if (SS_FS_W0SCAN) {   // the counters start zeroed; each tile's cursor step zeroes them for the next
         for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
         if (threadIdx.x == 0) any_heavy = 0;
         __syncthreads();
+    }
+    for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
+        if (!SS_FS_W0SCAN) {
+            for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
+            if (threadIdx.x == 0) any_heavy = 0;
+            __syncthreads();
+        }
         uint64_t key[kTile / T];
         uint32_t idx[kTile / T], lb[kTile / T], rank[kTile / T];
 #pragma unroll
@@ -1464,13 +1475,47 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
             }
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nb; i += T) {
-            lstart[i] = lcount[i];
-            hcnt[i] = 0;
-            if (lcount[i] > heavy_at) any_heavy = 1;
+        if (SS_FS_W0SCAN) {
+            // wave 0 alone: each lane scans E = nb / 64 consecutive regions (nb <= 256), flags the
+            // heavy ones and zeroes their dedup counters; one barrier publishes lstart / any_heavy
+            if (threadIdx.x < 64) {
+                const uint32_t lane = threadIdx.x;
+                const uint32_t E = nb >= 64 ? nb / 64 : 1u, i0 = lane * E;
+                uint32_t c[4], sum = 0;
+                bool heavy = false;
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    c[e] = (e < E && i0 + e < nb) ? lcount[i0 + e] : 0u;
+                    sum += c[e];
+                    heavy |= c[e] > heavy_at;
+                }
+                uint32_t incl = sum;
+                for (uint32_t off = 1; off < 64; off <<= 1) {
+                    const uint32_t y = __shfl_up(incl, off);
+                    if (lane >= off) incl += y;
+                }
+                uint32_t run = incl - sum;
+#pragma unroll
+                for (uint32_t e = 0; e < 4; ++e) {
+                    if (e < E && i0 + e < nb) {
+                        lstart[i0 + e] = run;
+                        hcnt[i0 + e] = 0;
+                        run += c[e];
+                    }
+                }
+                const uint64_t hv = __ballot(heavy);
+                if (lane == 0) any_heavy = hv != 0;
+            }
+            __syncthreads();
+        } else {
+            for (uint32_t i = threadIdx.x; i < nb; i += T) {
+                lstart[i] = lcount[i];
+                hcnt[i] = 0;
+                if (lcount[i] > heavy_at) any_heavy = 1;
+            }
+            __syncthreads();
+            block_scan<T>(lstart, nb, wsum);
         }
-        __syncthreads();
-        block_scan<T>(lstart, nb, wsum);
         const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
@@ -1593,8 +1638,11 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
             }
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nb; i += T)
+        for (uint32_t i = threadIdx.x; i < nb; i += T) {
             cursor[i] += (heavy_tile && lcount[i] > heavy_at) ? hcnt[i] : lcount[i];
+            if (SS_FS_W0SCAN) lcount[i] = 0;                  // the next tile's counters
+        }
+        if (SS_FS_W0SCAN && threadIdx.x == 0) any_heavy = 0;  // read into heavy_tile before (B)
         __syncthreads();
     }
     for (uint32_t i = threadIdx.x; i < nb; i += T)
