@@ -869,7 +869,14 @@ static int launch_ham(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t
             else hipLaunchKernelGGL((k_ham_dense3w<false, T, G>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
             return ss_check(hipGetLastError(), "k_ham_dense3w");
         }
-        launch_ham_dense_k<kHamDT, kHamDU>(a, b, n, W, out, pair, s);
+        // hamming vs one read on power-of-two W: small blocks (4-8 KiB of rows each) stream best
+        // (tools/tune_ham.hip, same box: W 1 0.786 -> 0.850, 2 0.779 -> 0.844, 4 0.775 -> 0.801,
+        // 8 0.756 -> 0.789, 16 0.747 -> 0.777 of 8 TB/s; W 32 level)
+        const bool pow2 = (W & (W - 1u)) == 0;
+        if (!pair && pow2 && W <= 2) launch_ham_dense_k<128, 2>(a, b, n, W, out, pair, s);
+        else if (!pair && pow2 && (W == 8 || W == 16)) launch_ham_dense_k<64, 4>(a, b, n, W, out, pair, s);
+        else if (!pair && pow2) launch_ham_dense_k<128, 4>(a, b, n, W, out, pair, s);
+        else launch_ham_dense_k<kHamDT, kHamDU>(a, b, n, W, out, pair, s);
         return ss_check(hipGetLastError(), "k_ham_dense");
     }
     const uint32_t logG = log2_ceil(W);
