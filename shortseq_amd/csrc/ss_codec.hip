@@ -679,7 +679,10 @@ void launch_decode_g16(const uint32_t* w32, uint32_t wpr2, uint64_t n, uint32_t 
 }
 
 // Production shapes
-constexpr int kEncT = 768, kEncU = 2;        // dense encode (32 / 64.. / 512 / 1024 nt)
+// dense encode: table path (L <= 32) 384 x 2, PEXT path (L % 32 == 0, L >= 64) 128 x 2 (same box,
+// three interleaved rounds: 32 nt 0.6018 -> 0.5978 ms, 512 nt 4.975 -> 4.819 ms against 768 x 2;
+// tools/tune_kernels.hip, profiles/r2/r2f/tune_encode_shapes.log)
+constexpr int kEncT = 384, kEncU = 2, kEncTP = 128;
 constexpr bool kEncXcd = false, kEncNtSt = true;
 constexpr int kHamT = 192, kHamU = 4;        // fused encode + hamming (dense, LDS reduction): 768-chunk
                                              // blocks, 128 whole 96-nt reads (tools/tune_stream.hip)
@@ -716,7 +719,7 @@ void launch_encode_fast(const G16Args& a, bool dense, bool ham, uint32_t L, hipS
         launch_g16<true, false, kPathMixed, 256, 4, false, true>(a, s);
     } else if (dense) {
         if (path == kPathTable) launch_g16<false, true, kPathTable, kEncT, kEncU, kEncXcd, kEncNtSt>(a, s);
-        else launch_g16<false, true, kPathPext, kEncT, kEncU, kEncXcd, kEncNtSt>(a, s);
+        else launch_g16<false, true, kPathPext, kEncTP, kEncU, kEncXcd, kEncNtSt>(a, s);
     } else {
         launch_g16<false, false, kPathMixed, 256, 4, false, true>(a, s);
     }

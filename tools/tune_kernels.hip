@@ -95,42 +95,18 @@ int main(int argc, char** argv) {
         G16Args a = make_args(in, n, L, words, ref, counts, fb);
         const double bytes = n * 40.0;
         printf("== C2 encode 100M x 32 nt\n");
-        ENC(kPathTable, 256, 4, false, true, "32");
-        ENC(kPathTable, 512, 2, false, true, "32");
-        ENC(kPathTable, 640, 2, false, true, "32");
-        ENC(kPathTable, 768, 2, false, true, "32");
-        ENC(kPathTable, 768, 2, true, true, "32");
-        ENC(kPathTable, 768, 1, false, true, "32");
-        ENC(kPathTable, 768, 3, false, true, "32");
-        ENC(kPathTable, 896, 2, false, true, "32");
-        ENC(kPathTable, 1024, 2, false, true, "32");
-        ENC(kPathTable, 1024, 2, true, true, "32");
-        ENC(kPathTable, 768, 2, false, false, "32");
-        ENC(kPathTable, 768, 2, false, true, "32 (repeat)");
+        ENC(kPathTable, 768, 2, false, true, "32 (warm-up)");
+        for (int round = 0; round < 3; ++round) {
+            ENC(kPathTable, 768, 2, false, true, "32 (production)");
+            ENC(kPathTable, 128, 2, false, true, "32");
+            ENC(kPathTable, 384, 2, false, true, "32");
+            ENC(kPathTable, 256, 2, false, true, "32");
+        }
         printf("== decode 100M x 32 nt\n");
-        DEC(256, 2, false, false, "32");
-        DEC(256, 4, false, false, "32");
-        DEC(768, 2, false, false, "32");
-        DEC(1024, 2, true, true, "32");
-    }
-    {   // ---- C3: 100M x 96 nt fused encode + hamming
-        const uint64_t n = 100000000;
-        const uint32_t L = 96;
-        CK((hipError_t)(ss_synth_reads(in, 2, 0, n, L, L, nullptr) == 0 ? hipSuccess : hipErrorUnknown));
-        CK(hipMemset(ref, 0, 256));
-        G16Args a = make_args(in, n, L, words, ref, counts, fb);
-        const double bytes = n * 124.0;
-        printf("== C3 encode+hamming 100M x 96 nt\n");
-        HAMD(kPathPext, 256, 4, "96");
-        HAMD(kPathPext, 256, 2, "96");
-        HAMD(kPathPext, 512, 2, "96");
-        HAMD(kPathPext, 512, 4, "96");
-        HAMD(kPathPext, 768, 2, "96");
-        HAMD(kPathPext, 1024, 2, "96");
-        timeit("ham-group96 G8 T256 U4", bytes, [&] { launch_g16<true, false, kPathMixed, 256, 4, false, true>(a, 0); });
-        timeit("ham-group96 G8 T512 U2", bytes, [&] { launch_g16<true, false, kPathMixed, 512, 2, false, true>(a, 0); });
-        const double bytes_e = n * 120.0;
-        timeit("enc96 (no hamming) T768 U2 ntst", bytes_e, [&] { launch_g16<false, true, kPathPext, 768, 2, false, true>(a, 0); });
+        for (int round = 0; round < 2; ++round) {
+            DEC(256, 2, false, false, "32 (production)");
+            DEC(128, 2, false, false, "32");
+        }
     }
     {   // ---- C4: 50M x 512 nt
         const uint64_t n = 50000000;
@@ -139,22 +115,17 @@ int main(int argc, char** argv) {
         G16Args a = make_args(in, n, L, words, ref, counts, fb);
         double bytes = n * 640.0;
         printf("== C4 encode 50M x 512 nt\n");
-        ENC(kPathPext, 256, 4, false, true, "512");
-        ENC(kPathPext, 512, 2, false, true, "512");
-        ENC(kPathPext, 768, 2, false, true, "512");
-        ENC(kPathPext, 768, 2, true, true, "512");
-        ENC(kPathPext, 1024, 2, false, true, "512");
-        ENC(kPathPext, 768, 2, false, false, "512");
+        for (int round = 0; round < 3; ++round) {
+            ENC(kPathPext, 768, 2, false, true, "512 (production)");
+            ENC(kPathPext, 128, 2, false, true, "512");
+            ENC(kPathPext, 384, 2, false, true, "512");
+        }
         printf("== C4 decode 50M x 512 nt\n");
-        DEC(256, 2, false, false, "512");
-        DEC(256, 4, false, false, "512");
-        DEC(512, 2, false, false, "512");
-        DEC(768, 2, false, false, "512");
-        DEC(1024, 2, false, false, "512");
-        DEC(256, 2, true, false, "512");
-        DEC(256, 2, false, true, "512");
-        DEC(1024, 2, true, true, "512");
-        DEC(256, 2, false, false, "512 (repeat)");
+        for (int round = 0; round < 3; ++round) {
+            DEC(256, 2, false, false, "512 (production)");
+            DEC(128, 2, false, false, "512");
+            DEC(192, 2, false, false, "512");
+        }
     }
     return 0;
 }
