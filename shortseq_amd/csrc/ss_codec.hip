@@ -864,8 +864,8 @@ static int launch_ham(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t
         hipStream_t s = (hipStream_t)stream;
         if (W == 3) {   // 96 nt (C3'): lane triples over whole 1-KiB chunks, no LDS (tools/tune_ham3.hip,
                         // same box: 63-lane chunks 0.718, + one 8-B store per triple 0.750, 3-chunk
-                        // groups 0.779 of the 8-TB/s peak)
-            constexpr int T = 256, G = 1;
+                        // groups 0.779 of the 8-TB/s peak; one-wave blocks 0.761-0.779 -> 0.782-0.785)
+            constexpr int T = 64, G = 1;
             const unsigned grid = grid_for(n, (uint64_t)128 * (T / 64) * G);
             const uint4 *a4 = (const uint4*)a, *b4 = (const uint4*)b;
             if (pair) hipLaunchKernelGGL((k_ham_dense3w<true, T, G>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);

@@ -143,6 +143,12 @@ static void v8(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* r
                        args(in, n, words, ref, out, fb), rpb, 1.0f / 6.0f);
 }
 
+template <int T, int U>
+static void vp(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
+    reset_first_bad(fb, 0);
+    launch_ham_dense<kPathPext, T, U, true>(args(in, n, words, ref, out, fb), 0);
+}
+
 template <int T, int G>
 static void v6w(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
     reset_first_bad(fb, 0);
@@ -177,8 +183,9 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(ref, w0 + 3 * 12345, 24, hipMemcpyDeviceToDevice));
     const struct { const char* name; Fn f; } vs[] = {
         {"prod k_encode_ham_dense<192,4>", prod},
-        {"6w T256 G1", v6w<256, 1>}, {"sad8 T192 U4", v8<192, 4>}, {"sad8 T384 U2", v8<384, 2>},
-        {"sad8 T192 U8", v8<192, 8>}, {"sad8 T96 U8", v8<96, 8>}, {"sad8 T384 U4", v8<384, 4>},
+        {"prod T128 U3", vp<128, 3>}, {"prod T96 U4", vp<96, 4>}, {"prod T192 U2", vp<192, 2>},
+        {"prod T64 U6", vp<64, 6>}, {"prod T128 U6", vp<128, 6>}, {"prod T256 U3", vp<256, 3>},
+        {"prod T64 U3", vp<64, 3>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // correctness: small batch with an invalid byte in read 777777 (chunk 4), then the full batch

@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d1, n * 4));
     hipLaunchKernelGGL(k_fill_words, dim3(8192), dim3(256), 0, 0, w, n * 3);
     CK(hipMemcpy(ref, w + 3 * 12345, 24, hipMemcpyDeviceToDevice));
-    launch_w<256, 1>(w, ref, n, d0);
+    launch_w<64, 1>(w, ref, n, d0);
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> h0(n), h1(n);
     CK(hipMemcpy(h0.data(), d0, n * 4, hipMemcpyDeviceToHost));
@@ -115,14 +115,10 @@ int main(int argc, char** argv) {
         printf("%-28s %s  %.4f ms  %.3f of 8 TB/s\n", name, ok ? "OK " : "BAD", ms, n * 28.0 / (ms * 1e-3) / 8e12);
     };
     for (int pass = 0; pass < 3; ++pass) {
-        run("prod T256 G1", launch_w<256, 1>);
-        run("T1024 G1", launch_w<1024, 1>);
-        run("pad8 T512 U2", launch_p8<512, 2>);
-        run("pad8 T768 U2", launch_p8<768, 2>);
-        run("pad8 T1024 U2", launch_p8<1024, 2>);
-        run("pad8 T1024 U1", launch_p8<1024, 1>);
-        run("pad8 T384 U2", launch_p8<384, 2>);
-        run("pad8 T512 U3", launch_p8<512, 3>);
+        run("prod T64 G1", launch_w<64, 1>);
+        run("T256 G1 (before)", launch_w<256, 1>);
+        run("T128 G1", launch_w<128, 1>);
+        run("T64 G2", launch_w<64, 2>);
     }
     return 0;
 }
