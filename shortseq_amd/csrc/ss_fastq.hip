@@ -322,7 +322,10 @@ __global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ bu
 //   k_fq_place : tile-wise, the staged positions with their line numbers -> offsets / lens
 //   k_fq_nulfix: sequence lines holding a NUL byte re-measured
 // HBM: the file once + 4 B per line written and read back + 12 B per sequence line of output.
-constexpr int kFqU1 = 8;                                       // 16-B chunks per thread
+#ifndef SS_FQ_U1
+#define SS_FQ_U1 8   // 16-KiB tiles (4) 0.525 ms, 64-KiB tiles (16) level with 32 KiB (tools/tune_f1.hip)
+#endif
+constexpr int kFqU1 = SS_FQ_U1;                                // 16-B chunks per thread
 constexpr uint64_t kFqTile1 = (uint64_t)kFqT * kFqU1 * 16;     // 32 KiB per tile
 
 constexpr uint32_t kStageShards = 64, kShardStride = 32;       // counters 128 B apart
