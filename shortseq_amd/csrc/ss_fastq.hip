@@ -28,7 +28,10 @@ namespace {
 
 using namespace ssd;
 
-constexpr int kFqT = 256;                                   // threads per block
+#ifndef SS_FQ_T
+#define SS_FQ_T 256   // 512 x 4 / 512 x 8 / 128 x 8 / 128 x 16 measured slower or level (profiles/r2/r2f/tune_f1_t.log)
+#endif
+constexpr int kFqT = SS_FQ_T;                               // threads per block
 constexpr int kFqU = 4;                                     // 16-B chunks per thread
 constexpr uint64_t kFqTile = (uint64_t)kFqT * kFqU * 16;    // 16 KiB per block
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
