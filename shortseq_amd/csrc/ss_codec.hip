@@ -460,12 +460,16 @@ __global__ __launch_bounds__(T) void k_ham_dense3w(const uint4* __restrict__ a, 
 //   W = 1:        a lane's pair of words is two reads -> one 8-B store of two distances
 //   W = 2^k >= 2: a read is W/2 consecutive lanes -> shfl_xor sum, the group's first lane stores
 //   other W:      per-word distances (<= 32) as bytes in LDS, then one thread per read sums its W
-//                 bytes and the block stores its distances coalesced
-template <bool PAIR, bool POW2, int T, int U>
+//                 bytes and the block stores its distances coalesced (W <= 8: bytes padded to 8
+//                 per read, one 8-B LDS read + v_sad_u8)
+// PAD8 (other W <= 8): a read's distance bytes sit at 8 rl + k and one 8-B LDS read + two v_sad_u8
+// sum them (the fused C3 kernel's tail); otherwise byte w of the block's word order
+template <bool PAIR, bool POW2, int T, int U, bool PAD8 = false>
 __global__ __launch_bounds__(T) void k_ham_dense(const uint4* __restrict__ a, const uint4* __restrict__ b,
                                                  const uint64_t* __restrict__ ref, uint64_t n, uint32_t W,
                                                  uint32_t rpb, float inv_w, uint32_t* __restrict__ out) {
-    __shared__ uint8_t part[POW2 ? 1 : 2 * T * U];
+    __shared__ uint64_t part8[POW2 ? 1 : (PAD8 ? (2 * T * U) / 3 + 1 : (2 * T * U) / 8)];   // PAD8: W >= 3
+    uint8_t* part = (uint8_t*)part8;
     __shared__ uint64_t sref[PAIR || POW2 ? 1 : 32];   // the reference read (W <= 32 words)
     if constexpr (!PAIR && !POW2) {
         if (threadIdx.x < W) sref[threadIdx.x] = ref[threadIdx.x];
@@ -536,7 +540,11 @@ __global__ __launch_bounds__(T) void k_ham_dense(const uint4* __restrict__ a, co
                 uint64_t rv;
                 if constexpr (PAIR) rv = h ? r_hi : r_lo;
                 else rv = sref[k];
-                part[w] = (uint8_t)(w < nw ? ham64(v ^ rv) : 0u);
+                if constexpr (PAD8) {
+                    if (w < nw) part[8 * rl + k] = (uint8_t)ham64(v ^ rv);
+                } else {
+                    part[w] = (uint8_t)(w < nw ? ham64(v ^ rv) : 0u);
+                }
             }
         }
     }
@@ -544,7 +552,12 @@ __global__ __launch_bounds__(T) void k_ham_dense(const uint4* __restrict__ a, co
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < nr; i += T) {
             uint32_t sum = 0;
-            for (uint32_t k = 0; k < W; ++k) sum += part[i * W + k];
+            if constexpr (PAD8) {
+                const uint64_t p = part8[i] & (~0ull >> (64 - 8 * W));        // bytes W..7 never written
+                sum = __builtin_amdgcn_sad_u8((uint32_t)p, 0u, 0u) + __builtin_amdgcn_sad_u8((uint32_t)(p >> 32), 0u, 0u);
+            } else {
+                for (uint32_t k = 0; k < W; ++k) sum += part[i * W + k];
+            }
             ham_store(&out[r0 + i], sum);
         }
     }
@@ -698,12 +711,17 @@ void launch_ham_dense_k(const uint64_t* a, const uint64_t* b, uint64_t n, uint32
     const bool pow2 = (W & (W - 1u)) == 0;
     const float inv_w = 1.0f / (float)W;
     const uint4 *a4 = (const uint4*)a, *b4 = (const uint4*)b;
+    const bool pad8 = !pow2 && W <= 8;
     if (pair && pow2)
         hipLaunchKernelGGL((k_ham_dense<true, true, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
+    else if (pair && pad8)
+        hipLaunchKernelGGL((k_ham_dense<true, false, T, U, true>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
     else if (pair)
         hipLaunchKernelGGL((k_ham_dense<true, false, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
     else if (pow2)
         hipLaunchKernelGGL((k_ham_dense<false, true, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
+    else if (pad8)
+        hipLaunchKernelGGL((k_ham_dense<false, false, T, U, true>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
     else
         hipLaunchKernelGGL((k_ham_dense<false, false, T, U>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, W, rpb, inv_w, out);
 }

@@ -186,7 +186,7 @@ def test_hamming(gpu, oracle):
         assert np.array_equal(dist2.cpu().numpy().astype(np.uint32), ref), L
 
 
-@pytest.mark.parametrize("L", [1, 31, 32, 33, 64, 96, 100, 128, 200, 256, 500, 512, 1000, 1024])
+@pytest.mark.parametrize("L", [1, 31, 32, 33, 64, 96, 100, 128, 150, 176, 200, 224, 256, 300, 500, 512, 1000, 1024])
 def test_hamming_dense_multiblock(gpu, oracle, L):
     """k_ham_dense (packed rows, wpr == words): batches spanning several blocks, odd word counts
     ending on a half pair, and row views off the 16-B grid (those take k_ham_group)."""
