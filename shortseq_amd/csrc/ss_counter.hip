@@ -905,6 +905,10 @@ constexpr uint32_t kHeavy = SS_PF_HEAVY;
 #endif
 // k_pf_coarse: issue the next tile's loads right after this tile's encode (1), after the tile's
 // reservation barrier (2), or at the top of each tile (0)
+#ifndef SS_PF_NOSBIN
+#define SS_PF_NOSBIN 0   // 1: no staged bin byte per element (recomputed from the key; dead = read index ~0):
+                         // same box uniform 2.510 -> 2.513, Zipf 2.598 -> 2.683 ms (profiles/r2/r2f/ab_nosbin.log), off
+#endif
 #ifndef SS_PF_LATE
 #define SS_PF_LATE 0   // 1: wave 0 consumes the coarse reservation after its staging writes (same-box
                        // medians uniform 2.536 -> 2.587, Zipf 2.605 -> 2.567 ms: within the spread, off)
@@ -1013,8 +1017,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
     __shared__ uint32_t any_heavy;
     __shared__ uint64_t skey[TILE];
     __shared__ uint32_t sidx[TILE];
-    __shared__ uint8_t sbin[TILE];
+    __shared__ uint8_t sbin[SS_PF_NOSBIN ? 1 : TILE];
     __shared__ uint32_t ht[TILE];
+    constexpr uint32_t kDeadIdx = 0xFFFFFFFFu;   // SS_PF_NOSBIN: a folded element's read index
     uint32_t* spill_ctr = fill + fill_at(kSpillCtr);
     const uint32_t shift = w.rbits - kCoarseBits;
     const uint64_t tiles = (n + TILE - 1) / TILE;
@@ -1131,7 +1136,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
                 const uint32_t sp = lstart[bin[j]] + rank[j];
                 skey[sp] = key[j];
                 sidx[sp] = (uint32_t)(t0 + e);
-                sbin[sp] = (uint8_t)bin[j];
+                if (!SS_PF_NOSBIN) sbin[sp] = (uint8_t)bin[j];
             }
         }
         if (SS_PF_LATE && threadIdx.x < 64) reserve_finish(2 * threadIdx.x, c0, c1, rmask, g2);
@@ -1145,12 +1150,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             // in registers first (one LDS atomic per wave instead of 64 on one address).
             for (uint32_t i0 = 0; i0 < cnt; i0 += T) {
                 const uint32_t i = i0 + threadIdx.x;
+#if SS_PF_NOSBIN
+                const uint64_t k0 = i < cnt ? skey[i] : 0ull;
+                bool act = i < cnt && hflag[region_of(t, k0) >> shift];
+                const uint64_t k = act ? k0 : 0ull;
+#else
                 bool act = i < cnt && hflag[sbin[i]];
                 const uint64_t k = act ? skey[i] : 0ull;
+#endif
                 uint32_t c = 1, mi = act ? sidx[i] : 0xFFFFFFFFu;
                 const bool was = act;
                 wave_fold<SS_COARSE_FOLD>(act, k, c, mi);
-                if (was && !act) sbin[i] = 0xFF;                          // folded into its wave leader
+                if (was && !act) {                                        // folded into its wave leader
+                    if (SS_PF_NOSBIN) sidx[i] = kDeadIdx;
+                    else sbin[i] = 0xFF;
+                }
                 if (!act) continue;
                 sidx[i] = mi;
                 uint32_t h = dedup_home(k, kHtLog);
@@ -1164,7 +1178,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
                     if (skey[j] == k) {
                         atomicAdd(&ht[h], c << 16);
                         atomicMin(&sidx[j], mi);
-                        sbin[i] = 0xFF;
+                        if (SS_PF_NOSBIN) sidx[i] = kDeadIdx;
+                        else sbin[i] = 0xFF;
                         break;
                     }
                     h = (h + 1) & (TILE - 1);
@@ -1172,8 +1187,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             }
             __syncthreads();                                              // (D)
             for (uint32_t i = threadIdx.x; i < cnt; i += T) {
+#if SS_PF_NOSBIN
+                if (sidx[i] == kDeadIdx) continue;
+                const uint32_t b = region_of(t, skey[i]) >> shift;
+                if (hflag[b]) atomicAdd(&hcnt[b], 1u);
+#else
                 const uint32_t b = sbin[i];
                 if (b != 0xFF && hflag[b]) atomicAdd(&hcnt[b], 1u);
+#endif
             }
             __syncthreads();                                              // (E)
             if (threadIdx.x < 64) {
@@ -1185,8 +1206,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             __syncthreads();                                              // (F)
         }
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
+#if SS_PF_NOSBIN
+            if (sidx[i] == kDeadIdx) continue;                            // folded into its claimer
+            const uint32_t b = region_of(t, skey[i]) >> shift;
+#else
             const uint32_t b = sbin[i];
             if (b == 0xFF) continue;                                      // folded into its claimer
+#endif
             uint32_t local, c = 1;
             if (heavy_tile && hflag[b]) {
                 local = atomicAdd(&hcnt[b], 1u);
