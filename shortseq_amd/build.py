@@ -33,11 +33,14 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_hip(force: bool = False, verbose: bool = False) -> str:
-    deps = [os.path.join(CSRC, f) for f in HIP_DEPS] + [os.path.join(INCLUDE, "shortseq_amd.h")]
+    deps = [os.path.join(CSRC, f) for f in HIP_DEPS] + [os.path.join(INCLUDE, "shortseq_amd.h"), os.path.abspath(__file__)]
     if force or _stale(LIB, deps):
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
         tmp = LIB + ".tmp"
+        # -amdgpu-mfma-vgpr-form: MFMA results in VGPRs (no v_accvgpr_read before the all-pairs hit
+        # test; tools/tune_allpairs.hip, 100k-200k x 12 nt: 14.1 -> 14.6 T pairs/s, same hits)
         cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
+               "-mllvm", "-amdgpu-mfma-vgpr-form=1",
                "-Xarch_host", "-mbmi2", "-Xarch_host", "-mpopcnt", "-I" + INCLUDE,
                *[os.path.join(CSRC, f) for f in HIP_SOURCES], "-o", tmp]
         if verbose:
