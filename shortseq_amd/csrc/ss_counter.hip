@@ -2419,14 +2419,24 @@ int ss_counter_destroy(ss_counter* c) {
     return SS_OK;
 }
 
+// 8-B device words set by a stream write packet (no fill-kernel dispatch; the streamed C5 step ran
+// four fills before its first pass); hipMemsetAsync where the runtime refuses the packet
+static hipError_t set_u64(uint64_t* p, bool ones, hipStream_t s) {
+    if (hipStreamWriteValue64(s, p, ones ? ~0ull : 0ull, 0) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+    return hipMemsetAsync(p, ones ? 0xFF : 0, sizeof(uint64_t), s);
+}
+
 int ss_counter_reset(ss_counter* c, void* stream) {
     if (!c) return ss_fail(SS_EARG, "null counter");
     hipStream_t s = (hipStream_t)stream;
     c->L = -1;
     c->occ_src = 0;
     c->reset_pending = true;    // the slots [0, cap): flush_reset or a fresh aggregate
-    hipError_t e = hipMemsetAsync(c->slots + c->cap, 0xFF, sizeof(Slot), s);   // the sentinel slot
-    if (e == hipSuccess) e = hipMemsetAsync(c->work, 0, sizeof(unsigned long long), s);
+    uint64_t* sent = (uint64_t*)(c->slots + c->cap);                        // the sentinel slot
+    hipError_t e = set_u64(sent, true, s);
+    if (e == hipSuccess) e = set_u64(sent + 1, true, s);
+    if (e == hipSuccess) e = set_u64((uint64_t*)c->work, false, s);
     return ss_check(e, "ss_counter_reset");
 }
 
@@ -2546,7 +2556,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
     int rc = fix_length(c, L);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    rc = ss_check(hipMemsetAsync(d_first_bad, 0xFF, sizeof(uint64_t), s), "reset first_bad");
+    rc = ss_check(set_u64(d_first_bad, true, s), "reset first_bad");
     if (rc || n == 0) return rc;
     if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
     if (base_index > kMaxIndex || n - 1 > kMaxIndex - base_index)
