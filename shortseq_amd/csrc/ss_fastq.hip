@@ -516,6 +516,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
         const uint64_t nl = *d_nl;
         bool partial;
         *d_nreads = fq_nsel(buf, o, line0, at_eof, nl, partial);
+        d_nreads[1] = *st.ovf;                             // status word (a staging region ran full)
         const uint64_t last = line0 + nl;                  // the unterminated final line, if any
         if (partial && (last & 3u) == 1u) {
             const uint64_t i = (last >> 2) - o.sel0;
@@ -773,9 +774,8 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
                            (const uint64_t*)d_counts, d_lens);
     }
     rc = ss_check(hipGetLastError(), "k_fq_nlpos/k_fq_place/k_fq_nulfix");
-    if (!rc && t == 0) rc = ss_check(hipMemsetAsync(d_counts + 1, 0, 8, s), "fastq read count");   // empty chunk
-    if (!rc) rc = ss_check(hipMemsetAsync(d_counts + 2, 0, 8, s), "fastq status");
-    if (!rc) rc = ss_check(hipMemcpyAsync(d_counts + 2, st.ovf, 4, hipMemcpyDeviceToDevice, s), "fastq status");
+    // k_fq_place's last block wrote the read count and the status word; an empty chunk has no tiles
+    if (!rc && t == 0) rc = ss_check(hipMemsetAsync(d_counts + 1, 0, 16, s), "fastq read count / status");
     return rc;
 }
 
