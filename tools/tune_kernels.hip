@@ -95,12 +95,12 @@ int main(int argc, char** argv) {
         G16Args a = make_args(in, n, L, words, ref, counts, fb);
         const double bytes = n * 40.0;
         printf("== C2 encode 100M x 32 nt\n");
-        ENC(kPathTable, 768, 2, false, true, "32 (warm-up)");
+        ENC(kPathTable, 384, 2, false, true, "32 (warm-up)");
         for (int round = 0; round < 3; ++round) {
-            ENC(kPathTable, 768, 2, false, true, "32 (production)");
-            ENC(kPathTable, 128, 2, false, true, "32");
-            ENC(kPathTable, 384, 2, false, true, "32");
-            ENC(kPathTable, 256, 2, false, true, "32");
+            ENC(kPathTable, 384, 2, false, true, "32 (production)");
+            ENC(kPathTable, 384, 2, true, true, "32");
+            ENC(kPathTable, 320, 2, false, true, "32");
+            ENC(kPathTable, 448, 2, false, true, "32");
         }
         printf("== decode 100M x 32 nt\n");
         for (int round = 0; round < 2; ++round) {
@@ -116,9 +116,10 @@ int main(int argc, char** argv) {
         double bytes = n * 640.0;
         printf("== C4 encode 50M x 512 nt\n");
         for (int round = 0; round < 3; ++round) {
-            ENC(kPathPext, 768, 2, false, true, "512 (production)");
-            ENC(kPathPext, 128, 2, false, true, "512");
-            ENC(kPathPext, 384, 2, false, true, "512");
+            ENC(kPathPext, 128, 2, false, true, "512 (production)");
+            ENC(kPathPext, 128, 2, true, true, "512");
+            ENC(kPathPext, 96, 2, false, true, "512");
+            ENC(kPathPext, 160, 2, false, true, "512");
         }
         printf("== C4 decode 50M x 512 nt\n");
         for (int round = 0; round < 3; ++round) {
