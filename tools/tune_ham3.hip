@@ -119,6 +119,11 @@ int main(int argc, char** argv) {
         run("T256 G1 (before)", launch_w<256, 1>);
         run("T128 G1", launch_w<128, 1>);
         run("T64 G2", launch_w<64, 2>);
+        run("pad8 T64 U4", launch_p8<64, 4>);
+        run("pad8 T64 U8", launch_p8<64, 8>);
+        run("pad8 T128 U2", launch_p8<128, 2>);
+        run("pad8 T128 U4", launch_p8<128, 4>);
+        run("pad8 T64 U2", launch_p8<64, 2>);
     }
     return 0;
 }
