@@ -38,6 +38,18 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def compact(x, sig: int = 4):
+    """The JSON line the driver keeps is the tail of stdout (~8.8 KB): floats to `sig` significant
+    digits, explanatory strings (note / how / where) dropped -- DESIGN.md section 5 holds them."""
+    if isinstance(x, float):
+        return float(f"{x:.{sig}g}") if x == x else None
+    if isinstance(x, dict):
+        return {k: compact(v, sig) for k, v in x.items() if k not in ("note", "how", "where")}
+    if isinstance(x, (list, tuple)):
+        return [compact(v, sig) for v in x]
+    return x
+
+
 def splitmix64(x: int) -> int:
     M = (1 << 64) - 1
     z = (x + 0x9E3779B97F4A7C15) & M
@@ -409,11 +421,15 @@ def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):
     # issued i8 MACs: one-hot codes, 8 positions (32 MACs) per k-step, ceil(min(L + 1, 32) / 8) steps
     ks = (min(L + 1, 32) + 7) // 8
     tops = pairs * 2 * 32 * ks / (ms * 1e-3) / 1e12
+    # algorithmic work: L position compares per pair (one MAC each, x2 ops) against the same peak
+    algo_tops = pairs * 2 * L / (ms * 1e-3) / 1e12
     return {"n": n, "read_len": L, "max_dist": k, "pairs": pairs, "ms_per_step": ms,
             "pairs_per_s": pairs / ms * 1e3, "hits": int(tot.item()),
             "roofline": {"bound": "mfma", "kernel": "k_allpairs_mfma (v_mfma_i32_32x32x32_i8)", "achieved": tops,
                          "peak": I8_PEAK_TOPS, "unit": "TOP/s", "frac": tops / I8_PEAK_TOPS,
-                         "note": "issued i8 MAC ops x2 (one-hot K padded to whole k-steps); dense i8 peak = 2x bf16"}}
+                         "frac_algorithmic": algo_tops / I8_PEAK_TOPS,
+                         "note": "frac: issued i8 MAC ops x2 (one-hot codes, 4 MACs per position, K padded to "
+                                 "whole k-steps); frac_algorithmic: L compares per pair x2; dense i8 peak = 2x bf16"}}
 
 
 def bench_host_staged(B, dev, n=32_000_000, L=32, reps=5):
@@ -515,42 +531,45 @@ def bench_fastq_dropin(path, n):
 def cpu_baseline(target_s=2.0):
     """The reference's per-read CPU algorithms (oracle/cpu_baseline.cpp, kind "port": table loop for
     L <= 32, PEXT blocks beyond, XOR-collapse-popcount hamming, charmap decode, a hash map for the
-    counter) timed on this host over bounded samples of C2-C5: 1 core (the reference is
+    counter) timed on this host over bounded samples of C2-C5 and C3': 1 core (the reference is
     single-threaded) and all the cores this process may use (OpenMP).  The reference itself never runs
-    here; its own numbers (the kernels' calibration ratios, and its Python API for C1 / a18) were
-    measured in the build container by oracle/calibrate_cpu_baseline.py and are attached, labelled."""
+    here; its own numbers (the kernels' calibration ratios, and its Python API for C1 / a18 / C3') were
+    measured in the build container by oracle/calibrate_cpu_baseline.py
+    (profiles/r3/cpu_baseline_calibration.json) and are attached, labelled."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import cpu_baseline as cb  # test/baseline infrastructure only — never the measured GPU path
     res = cb.run_all(target_s)
     th = res["threads_all"]
     c2 = res["C2_encode_32"]
+    cfgs = {k: {"unit": v["unit"], "1_core": v["1_core"], "all_cores": v[f"{th}_cores"]}
+            for k, v in res.items() if k.startswith("C")}
     out = {"value": c2["1_core"], "unit": "nt/s", "cores": 1, "kind": "port",
            "value_all_cores": c2[f"{th}_cores"], "cores_all": th,
-           "sample": f"C2: {c2['sample_1_core']} (1 core); {c2[f'sample_{th}_cores']} ({th} cores); "
-                     f"oracle/cpu_baseline.cpp; host cpu: {res['cpu']}, nproc {res['nproc']}, "
-                     f"threads used for all-core legs {th} (OMP_NUM_THREADS / affinity)",
-           "configs": {k: v for k, v in res.items() if k.startswith("C")}}
-    cal = os.path.join(REPO, "profiles", "r2", "cpu_baseline_calibration.json")
+           "sample": f"C2 {c2['sample_1_core']} (1 core); oracle/cpu_baseline.cpp on {res['cpu']}, "
+                     f"nproc {res['nproc']}, {th} threads for all_cores",
+           "configs": cfgs}
+    cal = os.path.join(REPO, "profiles", "r3", "cpu_baseline_calibration.json")
     if os.path.exists(cal):
         with open(cal) as f:
             c = json.load(f)
-        ratios = {k: v["ratio"] for k, v in c.items() if isinstance(v, dict) and "ratio" in v}
-        out["calibration_vs_reference"] = {
-            "where": f"build container ({c.get('cpu')}), 1 core, same inputs; ratio = port speed / reference speed",
-            **{k: round(v, 3) for k, v in ratios.items()},
-            "how": "median of 5 interleaved rounds (the build container's CPU timings wander by up to "
-                   "+-20 % between runs); the port restates the reference's per-read GIL error checks "
-                   "of _marshall_bytes_array (util.pyx:88-90); counter: the reference builds a ShortSeq "
-                   "object per read into a CPython dict, the port a std::unordered_map node"}
-        # the port's 1-core numbers scaled by the calibration: the reference's expected speed on this host
+        # port speed / reference speed, 1 pinned core, median of 9 interleaved rounds (min..max)
+        out["calibration"] = {k: [v["ratio"], v.get("ratio_min"), v.get("ratio_max")] if "ratio_min" in v else v["ratio"]
+                              for k, v in c.items() if isinstance(v, dict) and "ratio" in v}
         pick = {"C2_encode_32": "encode_32", "C3_encode_hamming_96": "encode_96",
                 "C4_roundtrip_512": "encode_512", "C5_counter_32": "counter_32_pool2^24"}
         for cfg, key in pick.items():
-            if cfg in out["configs"] and key in ratios:
-                out["configs"][cfg]["reference_equiv_1_core"] = out["configs"][cfg]["1_core"] / ratios[key]
-                out["configs"][cfg]["calibrated_by"] = key
-        out["c1_reference_api_container"] = c.get("C1_reference_api")
-        out["a18_reference_read_and_count_fastq_container"] = c.get("a18_reference_read_and_count_fastq")
+            if cfg in cfgs and key in c:
+                cfgs[cfg]["ref_equiv_1_core"] = cfgs[cfg]["1_core"] / c[key]["ratio"]
+        api = {}
+        if c.get("C1_reference_api"):
+            api["C1_counter_reads_per_s"] = c["C1_reference_api"]["counter_reads_per_s"]
+            api["C1_pack_per_s"] = c["C1_reference_api"]["pack_per_s"]
+        if c.get("a18_reference_read_and_count_fastq"):
+            api["a18_records_per_s"] = c["a18_reference_read_and_count_fastq"]["records_per_s"]
+        for L in (32, 96, 512):
+            if c.get(f"hamming_{L}"):
+                api[f"C3p_xor_api_{L}_pairs_per_s"] = c[f"hamming_{L}"]["reference_api_pairs_per_s"]
+        out["reference_api_container"] = api
     return out
 
 
@@ -731,7 +750,11 @@ def main():
             result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         else:
             result["cpu_baseline"] = None
-        print(json.dumps(result), flush=True)
+        # cpu_baseline before extra, and the line compacted: the driver keeps only stdout's tail
+        ex = result.pop("extra", None)
+        if ex is not None:
+            result["extra"] = ex
+        print(json.dumps(compact(result), separators=(",", ":")), flush=True)
     if fq_path is not None:
         import shutil
         shutil.rmtree(os.path.dirname(fq_path), ignore_errors=True)

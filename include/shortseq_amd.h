@@ -64,6 +64,7 @@ int ss_abi_version(void);
 const char* ss_last_error_string(void);          /* thread-local message of the last SS_EHIP/EARG */
 int ss_device_count(int* h_count);
 int ss_set_device(int device);
+int ss_get_device(int* h_device);                   /* the calling thread's current device */
 
 /* Pinned host staging buffers (hipHostMalloc / hipHostFree) for H2D batch staging. */
 int ss_pinned_alloc(void** h_ptr, size_t bytes);
@@ -182,6 +183,14 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
 /* Merge already-counted entries (e.g. received from other GPUs): counts add, first index = min. */
 int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_lens,
                      const uint64_t* d_counts, const uint64_t* d_first, uint64_t m, void* stream);
+
+/* Merge already-counted multi-word entries (L > 32): d_words[m * W] the key words of entry i (row
+ * i), counts add, first index = min.  The m entries must be distinct keys (e.g. the extraction of
+ * another handle of the same length, ss_counter_extract_words); keys already in the table are
+ * found by their words.  Used to grow a per-length table (ss_ingest).  New in this ABI version;
+ * replaces no reference interface (the reference's dict grows by itself, counter.pyx:41-54). */
+int ss_counter_merge_words(ss_counter* c, const uint64_t* d_words, const uint64_t* d_counts,
+                           const uint64_t* d_first, uint64_t m, void* stream);
 
 /* Fix the key length of an empty handle (also done by the first insert); -1 from ss_counter_length
  * means not fixed yet. */
@@ -325,6 +334,22 @@ int ss_ingest_reset(ss_ingest* g);
 int ss_ingest_staging(ss_ingest* g, uint64_t nbytes, uint8_t** h_ptr);
 int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_lens, uint64_t n);
 int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, uint64_t* h_nseqs);
+/* Multi-GPU FASTQ (counter.pyx:57-70 over one file, split across devices): ss_fastq_split cuts the
+ * file into nparts byte ranges h_begin[p] .. h_begin[p + 1] (h_begin has nparts + 1 entries), each
+ * starting at a line start and ending after a newline or at the end of the file, and gives the
+ * lines before each range (h_line0[p]).  ss_ingest_add_fastq_range counts one range (line0 = the
+ * lines before it, so the j % 4 == 1 selection of fast_read.pyx:13 stays global); the ranges'
+ * results, taken in range order, are the file's counter (first-occurrence order kept: every read of
+ * range p precedes every read of range p + 1).  Host calls. */
+int ss_fastq_split(const char* path, uint32_t nparts, uint64_t* h_begin, uint64_t* h_line0);
+int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, uint64_t end, uint64_t line0,
+                              uint64_t chunk_bytes, uint64_t* h_nseqs);
+/* A ragged batch already on this engine's device: read i = d_blob[d_offsets[i], + d_lens[i]) of an
+ * nbytes-byte blob (e.g. the output of ss_fastq_index_onepass, or a device-generated batch); counted
+ * as ss_ingest_add_blob counts a staged list (same length split, tables and first-occurrence order).
+ * Synchronous; the caller's buffers are not kept. */
+int ss_ingest_add_device(ss_ingest* g, const uint8_t* d_blob, uint64_t nbytes, const uint64_t* d_offsets,
+                         const uint32_t* d_lens, uint64_t n);
 int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_read, uint64_t cap, uint64_t* h_len);
 int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords);
 int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words);

@@ -5,7 +5,11 @@ against the reference's own compiled kernels (oracle/_ref, built by oracle/build
 same process, same inputs; and measures the reference's Python API (C1: sq.pack / ShortSeqCounter,
 a18: read_and_count_fastq) here, so bench.py can report those numbers labelled as container-measured.
 
-    python3 oracle/calibrate_cpu_baseline.py   ->  profiles/r2/cpu_baseline_calibration.json
+    python3 oracle/calibrate_cpu_baseline.py   ->  profiles/r3/cpu_baseline_calibration.json
+
+The process is pinned to one core; each kernel ratio is the median of ROUNDS interleaved rounds
+(reference, then port, best of 3 each), and the speeds reported beside it are the ones of that
+median round (not independently minimised), with the spread of all rounds.
 """
 import contextlib
 import io
@@ -34,13 +38,19 @@ def best_of(fn, reps=5):
     return min(ts)
 
 
+ROUNDS = 9
+
+
 def main():
     assert oracle.ref_available(), "build the reference first (oracle/build_ref.sh)"
-    out = {"cpu": cb.cpu_model(), "nproc": os.cpu_count(),
-           "note": "1 core, same process and inputs; ratio = port / reference (1.0 = same speed)"}
+    core = sorted(os.sched_getaffinity(0))[-1]
+    os.sched_setaffinity(0, {core})
+    out = {"cpu": cb.cpu_model(), "nproc": os.cpu_count(), "pinned_core": core, "rounds": ROUNDS,
+           "note": "1 pinned core, same process and inputs; ratio = port / reference (1.0 = same speed); "
+                   "speeds are those of the median-ratio round"}
     p64, par = oracle.ref_kernel_ptrs()
-    # this container's CPU timings wander by up to +-20 % between runs (a shared host): 5 rounds,
-    # reference and port interleaved, the median ratio reported with all rounds
+    # this container's CPU timings wander between runs (a shared host): ROUNDS rounds, reference
+    # and port interleaved; the median round is reported with the spread of all rounds
     for L, n in ((32, 4_000_000), (96, 1_500_000), (512, 300_000)):
         a = oracle.gen_reads(1, 0, n, L)
         wpr = max(1, (L + 31) // 32)
@@ -49,15 +59,15 @@ def main():
         cb.lib(1).cb_encode(a.ctypes.data, n, L, words.ctypes.data, wpr, 1)
         assert np.array_equal(ref_out.reshape(-1), words)
         rounds = []
-        for _ in range(5):
+        for _ in range(ROUNDS):
             t_ref = best_of(lambda: oracle.ref_encode_batch(a, n, L), reps=3)
             t_port = best_of(lambda: cb.lib(1).cb_encode(a.ctypes.data, n, L, words.ctypes.data, wpr, 1), reps=3)
-            rounds.append((t_ref, t_port))
-        ratios = sorted(tr / tp for tr, tp in rounds)
-        med = ratios[len(ratios) // 2]
-        t_ref, t_port = min(r[0] for r in rounds), min(r[1] for r in rounds)
+            rounds.append((t_ref / t_port, t_ref, t_port))
+        rounds.sort()
+        med, t_ref, t_port = rounds[len(rounds) // 2]
         out[f"encode_{L}"] = {"reference_nt_per_s": n * L / t_ref, "port_nt_per_s": n * L / t_port,
-                              "ratio": med, "ratio_rounds": ratios,
+                              "ratio": med, "ratio_min": rounds[0][0], "ratio_max": rounds[-1][0],
+                              "ratio_rounds": [r[0] for r in rounds],
                               "kernel": "_marshall_bytes_64" if L <= 32 else "_marshall_bytes_array"}
         print(L, out[f"encode_{L}"], flush=True)
     sys.path.insert(0, oracle.REF_DIR)
@@ -76,6 +86,19 @@ def main():
                                   "note": "reference: ShortSeqCounter(list of bytes) incl. object creation; "
                                           "port: encode + std::unordered_map on the packed word"}
     print(out["counter_32_pool2^24"], flush=True)
+    # C3' (hamming on packed objects): the reference's hamming has no batch kernel to call -- the
+    # XOR-collapse-popcount loop is inlined in each __xor__ dunder -- so its own number is the
+    # per-object Python API (a ^ b over pre-built objects), beside the port's batch loop
+    for L, n in ((32, 1_000_000), (96, 1_000_000), (512, 300_000)):
+        a = oracle.gen_reads(6, 0, n, L)
+        objs = [ref_sq.pack(a[i * L:(i + 1) * L].tobytes()) for i in range(n)]
+        r0 = objs[0]
+        t_ref = best_of(lambda: [r0 ^ o for o in objs], reps=3)
+        pr = cb.bench_hamming_only(L, n, 1, 1.0)
+        out[f"hamming_{L}"] = {"reference_api_pairs_per_s": n / t_ref, "port_pairs_per_s": pr["pairs_per_s"],
+                               "note": "reference: r0 ^ obj per object (Python API; no batch kernel exists); "
+                                       "port: the same loop over a packed batch (oracle/cpu_baseline.cpp cb_hamming_ref)"}
+        print(out[f"hamming_{L}"], flush=True)
     # C1 (BASELINE configs[0]): the reference's own Python API on 1M x 32-nt reads, as bench.py's
     # C1 drop-in line measures the drop-in (median of 3)
     n = 1_000_000
@@ -101,8 +124,8 @@ def main():
                                                  "s_per_call": t, "records_per_s": nrec / t}
     print(out["a18_reference_read_and_count_fastq"], flush=True)
     os.remove(path)
-    os.makedirs(os.path.join(REPO, "profiles", "r2"), exist_ok=True)
-    with open(os.path.join(REPO, "profiles", "r2", "cpu_baseline_calibration.json"), "w") as f:
+    os.makedirs(os.path.join(REPO, "profiles", "r3"), exist_ok=True)
+    with open(os.path.join(REPO, "profiles", "r3", "cpu_baseline_calibration.json"), "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -184,6 +184,16 @@ uint64_t cb_encode_hamming(const uint8_t* ascii, uint64_t n, uint32_t L, uint64_
     return bad;
 }
 
+// C3': hamming of every pre-packed read (wpr words, the first nw used) against `ref` -> dist [n]
+// (the __xor__ kernel of short_seq_64.pyx:77-84 / short_seq_192.pyx:74-91 / short_seq_var.pyx:64-81
+// over a batch, without the per-object Python call)
+void cb_hamming_ref(const uint64_t* words, uint64_t n, uint32_t L, uint32_t wpr, const uint64_t* ref, uint32_t* dist,
+                    int threads) {
+    const uint32_t nw = words_for(L);
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) dist[i] = hamming(words + (uint64_t)i * wpr, ref, nw);
+}
+
 // C4: encode + decode round trip -> back [n * L]
 uint64_t cb_roundtrip(const uint8_t* ascii, uint64_t n, uint32_t L, uint64_t* words, uint32_t wpr, uint8_t* back,
                       int threads) {

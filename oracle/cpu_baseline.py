@@ -45,6 +45,8 @@ def _bind(L):
     L.cb_encode.restype = U64
     L.cb_encode_hamming.argtypes = [P, U64, U32, P, U32, P, P, I]
     L.cb_encode_hamming.restype = U64
+    L.cb_hamming_ref.argtypes = [P, U64, U32, U32, P, P, I]
+    L.cb_hamming_ref.restype = None
     L.cb_roundtrip.argtypes = [P, U64, U32, P, U32, P, I]
     L.cb_roundtrip.restype = U64
     L.cb_count.argtypes = [P, U64, U32, I, C.POINTER(U64), C.POINTER(U64)]
@@ -118,6 +120,22 @@ def bench_encode_hamming(L: int, n: int, threads: int, target_s: float, seed: in
     return {"pairs_per_s": passes * n / el, "nt_per_s": passes * n * L / el, "sample": f"{passes} x {n} reads x {L} nt"}
 
 
+def bench_hamming_only(L: int, n: int, threads: int, target_s: float, seed: int = 6) -> dict:
+    """C3': hamming vs read 0 on pre-packed words (the XOR-collapse-popcount loop alone)."""
+    W = (L + 31) // 32
+    words = oracle.splitmix64_np(np.uint64(seed) + np.arange(n * W, dtype=np.uint64)).reshape(n, W)
+    if L % 32:
+        words[:, -1] &= np.uint64((1 << (2 * (L % 32))) - 1)
+    assert np.array_equal(words[:4], oracle.gen_words(seed, 0, 4, L))   # the generator's known answer
+    wpr = words.shape[1]
+    ref = np.ascontiguousarray(words[0].copy())
+    dist = np.zeros(n, np.uint32)
+    lib(threads).cb_hamming_ref(_p(words), n, L, wpr, _p(ref), _p(dist), threads)
+    assert np.array_equal(dist[:4096], oracle.hamming_ref_batch(words[:4096], 4096, L, ref))
+    passes, el = _time(lambda: lib(threads).cb_hamming_ref(_p(words), n, L, wpr, _p(ref), _p(dist), threads), target_s)
+    return {"pairs_per_s": passes * n / el, "sample": f"{passes} x {n} pairs x {L} nt"}
+
+
 def bench_roundtrip(L: int, n: int, threads: int, target_s: float, seed: int = 3) -> dict:
     ascii = oracle.gen_reads(seed, 0, n, L)
     wpr = max(1, (L + 31) // 32)
@@ -144,6 +162,9 @@ WORKLOADS = {
     # name: (callable(threads, target_s), unit key)
     "C2_encode_32": (lambda th, s: bench_encode(32, 4_000_000, th, s), "nt_per_s"),
     "C3_encode_hamming_96": (lambda th, s: bench_encode_hamming(96, 2_000_000, th, s), "pairs_per_s"),
+    "C3p_hamming_ref_32": (lambda th, s: bench_hamming_only(32, 8_000_000, th, s), "pairs_per_s"),
+    "C3p_hamming_ref_96": (lambda th, s: bench_hamming_only(96, 4_000_000, th, s), "pairs_per_s"),
+    "C3p_hamming_ref_512": (lambda th, s: bench_hamming_only(512, 1_000_000, th, s), "pairs_per_s"),
     "C4_roundtrip_512": (lambda th, s: bench_roundtrip(512, 400_000, th, s), "nt_per_s"),
     "C5_counter_32": (lambda th, s: bench_count(8_000_000, 1 << 24, th, s), "reads_per_s"),
 }

@@ -270,6 +270,10 @@ def ref_kernel_ptrs():
         sys.path.insert(0, REF_DIR)
     m64 = importlib.import_module("shortseq.short_seq_64")
     util = importlib.import_module("shortseq.util")
+    # the repository's own `shortseq` alias package (the drop-in under the reference's name) must
+    # never stand in for the reference here
+    if not os.path.abspath(m64.__file__).startswith(os.path.abspath(REF_DIR)):
+        raise RuntimeError(f"'shortseq' resolved to {m64.__file__}, not the reference build in {REF_DIR}")
     get = C.pythonapi.PyCapsule_GetPointer
     get.restype = C.c_void_p
     get.argtypes = [C.py_object, C.c_char_p]

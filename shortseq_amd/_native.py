@@ -34,6 +34,7 @@ SIGNATURES = [
     ("ss_last_error_string", C.c_char_p, []),
     ("ss_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("ss_set_device", C.c_int, [C.c_int]),
+    ("ss_get_device", C.c_int, [C.POINTER(C.c_int)]),
     ("ss_pinned_alloc", C.c_int, [C.POINTER(C.c_void_p), _SZ]),
     ("ss_pinned_free", C.c_int, [_P]),
     ("ss_encode_fixed", C.c_int, [_P, _U64, _U32, _U64, _P, _U32, _P, _P]),
@@ -52,6 +53,7 @@ SIGNATURES = [
     ("ss_counter_release", C.c_int, [_P]),
     ("ss_counter_insert_fixed", C.c_int, [_P, _P, _U64, _U32, _U64, _U64, _P, _P]),
     ("ss_counter_merge", C.c_int, [_P, _P, _P, _P, _P, _U64, _P]),
+    ("ss_counter_merge_words", C.c_int, [_P, _P, _P, _P, _U64, _P]),
     ("ss_counter_set_length", C.c_int, [_P, _U32]),
     ("ss_counter_length", C.c_int, [_P]),
     ("ss_counter_overflow", C.c_int, [_P, _P, _P]),
@@ -82,6 +84,9 @@ SIGNATURES = [
     ("ss_ingest_staging", C.c_int, [_P, _U64, C.POINTER(C.c_void_p)]),
     ("ss_ingest_add_blob", C.c_int, [_P, _P, _P, _U64]),
     ("ss_ingest_add_fastq", C.c_int, [_P, C.c_char_p, _U64, C.POINTER(C.c_uint64)]),
+    ("ss_fastq_split", C.c_int, [C.c_char_p, C.c_uint32, _P, _P]),
+    ("ss_ingest_add_fastq_range", C.c_int, [_P, C.c_char_p, _U64, _U64, _U64, _U64, C.POINTER(C.c_uint64)]),
+    ("ss_ingest_add_device", C.c_int, [_P, _P, _U64, _P, _P, _U64]),
     ("ss_ingest_error", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int), _P, _U64, C.POINTER(C.c_uint64)]),
     ("ss_ingest_finish", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("ss_ingest_results", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),

@@ -32,6 +32,7 @@ import time
 cdef extern from "Python.h":
     ctypedef Py_ssize_t Py_hash_t
     int _PyDict_SetItem_KnownHash(object mp, object key, object item, Py_hash_t hash) except -1
+    PyObject* _PyDict_GetItem_KnownHash(object mp, object key, Py_hash_t hash)
     object PyUnicode_New(Py_ssize_t size, Py_UCS4 maxchar)
     void* PyUnicode_1BYTE_DATA(object o)
     void* PyUnicode_DATA(object o)
@@ -70,6 +71,9 @@ ctypedef int (*f_add_fastq)(ss_ingest*, const char*, uint64_t, uint64_t*) noexce
 ctypedef int (*f_error)(ss_ingest*, uint64_t*, int*, uint8_t*, uint64_t, uint64_t*) noexcept nogil
 ctypedef int (*f_finish)(ss_ingest*, uint64_t*, uint64_t*) noexcept nogil
 ctypedef int (*f_results)(ss_ingest*, const uint32_t**, const uint64_t**, const uint64_t**) noexcept nogil
+ctypedef int (*f_get_device)(int*) noexcept nogil
+ctypedef int (*f_fastq_split)(const char*, uint32_t, uint64_t*, uint64_t*) noexcept nogil
+ctypedef int (*f_add_fastq_range)(ss_ingest*, const char*, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t*) noexcept nogil
 
 cdef struct _Abi:
     f_device_count device_count
@@ -82,6 +86,9 @@ cdef struct _Abi:
     f_error error
     f_finish finish
     f_results results
+    f_get_device get_device
+    f_fastq_split fastq_split
+    f_add_fastq_range add_fastq_range
 
 cdef _Abi _abi
 cdef bint _abi_ready = False
@@ -113,6 +120,9 @@ cdef int _bind_abi() except -1:
     _abi.error = <f_error>_sym(h, b"ss_ingest_error")
     _abi.finish = <f_finish>_sym(h, b"ss_ingest_finish")
     _abi.results = <f_results>_sym(h, b"ss_ingest_results")
+    _abi.get_device = <f_get_device>_sym(h, b"ss_get_device")
+    _abi.fastq_split = <f_fastq_split>_sym(h, b"ss_fastq_split")
+    _abi.add_fastq_range = <f_add_fastq_range>_sym(h, b"ss_ingest_add_fastq_range")
     _abi_ready = True
     return 0
 
@@ -489,11 +499,11 @@ cdef class ShortSeqCounter(dict):
 
     cdef _count_list(self, list it, device):
         cdef Py_ssize_t n = PyList_GET_SIZE(it)
-        dev = -1
+        devs = []
         if device != "host" and n >= (GPU_MIN_READS if device == "auto" else 0):
-            dev = _resolve_device(device)
-        if dev >= 0:
-            _count_batch_gpu(self, it, dev)
+            devs = _resolve_devices(device, n)
+        if devs:
+            _count_batch_gpu(self, it, devs)
         else:
             self._count_host(it)
 
@@ -508,44 +518,109 @@ cdef class ShortSeqCounter(dict):
             dict.__setitem__(self, seq, dict.get(self, seq, 0) + 1)
 
 
-def _resolve_device(device):
-    """device argument -> HIP device index, or -1 for the host path: "auto" = device 0 when the HIP
-    runtime sees one, "cuda" = device 0, "cuda:N" = N (a torch.device-like object works too)."""
+GPU_MIN_READS_PER_DEVICE = 1 << 20   # "auto" adds a device per this many reads (list) / 256 MB (FASTQ)
+
+
+def _current_device():
+    """The caller's current device: torch's when torch has initialised HIP (its current device is
+    what a multi-rank job sets per rank), else the HIP runtime's for this thread."""
+    import sys
+    cdef int d = 0
+    t = sys.modules.get("torch")
+    if t is not None:
+        try:
+            if t.cuda.is_initialized():
+                return int(t.cuda.current_device())
+        except Exception:  # noqa: BLE001
+            pass
+    if _abi.get_device(&d) != 0:
+        return 0
+    return d
+
+
+def _resolve_devices(device, Py_ssize_t work=0, Py_ssize_t per_device=GPU_MIN_READS_PER_DEVICE):
+    """device argument -> the HIP devices a batch call shards over (contiguous read ranges, in
+    order), or [] for the host path.
+      "host"                 the reference's per-object loop
+      "auto"                 every visible device (one per `per_device` units of work, at least one);
+                             only the current device inside a multi-rank job (LOCAL_RANK set); the
+                             host path when no HIP runtime / device is usable
+      "cuda"                 the current device
+      "cuda:N" / torch.device("cuda", N) / N      device N
+      "all"                  every visible device
+      a list / tuple of the above                 those devices, in that order (one engine each; a
+                                                  device may repeat)"""
+    import os
     cdef int count = 0
-    if device == "host":
-        return -1
-    _bind_abi()
-    if device == "auto":
+    if isinstance(device, str) and device == "host":
+        return []
+    if isinstance(device, str) and device == "auto":
+        try:
+            _bind_abi()
+        except ImportError:
+            return []
         if _abi.device_count(&count) != 0 or count <= 0:
-            return -1
-        return 0
-    name = str(device)
-    if name == "cuda":
-        return 0
-    if name.startswith("cuda:"):
-        return int(name[5:])
-    raise ValueError(f"unknown device {device!r} (use 'auto', 'host', 'cuda' or 'cuda:N')")
+            return []
+        if os.environ.get("LOCAL_RANK") is not None or int(os.environ.get("WORLD_SIZE", "1") or 1) > 1:
+            return [_current_device()]
+        want = max(1, min(count, work // max(1, per_device)))
+        return list(range(want))
+    _bind_abi()
+    if _abi.device_count(&count) != 0 or count <= 0:
+        raise RuntimeError(f"shortseq_amd: device {device!r} requested but no HIP device is visible")
+    if isinstance(device, (list, tuple)):
+        out = []
+        for d in device:
+            out.extend(_resolve_devices(d, work, per_device))
+        if not out:
+            raise ValueError("empty device list")
+        return out
+    if isinstance(device, int):
+        idx = device
+    else:
+        name = str(device)
+        if name == "cuda":
+            return [_current_device()]
+        if name == "all":
+            return list(range(count))
+        if not name.startswith("cuda:"):
+            raise ValueError(f"unknown device {device!r} (use 'auto', 'host', 'cuda', 'cuda:N', 'all' or a list)")
+        idx = int(name[5:])
+    if idx < 0 or idx >= count:
+        raise ValueError(f"device {device!r}: {count} HIP device(s) visible")
+    return [idx]
 
 
-cdef dict _engines = {}
+# Ingest engines: a pool of idle engines per device.  A call takes one engine per shard and gives
+# them back when its dict is built, so concurrent calls from several Python threads (the GIL is
+# released while they count) never share an engine, its pinned staging or its result buffers.
+import threading
+_pool_lock = threading.Lock()
+cdef dict _idle_engines = {}
 
 
 cdef ss_ingest* _engine(int dev) except NULL:
-    """The ingest engine of a device (created once per process, reset per call)."""
+    """An idle engine of device `dev` (reset), or a new one."""
     cdef ss_ingest* g = NULL
-    cdef size_t h
+    cdef size_t h = 0
     cdef int rc
-    if dev in _engines:
-        h = _engines[dev]
+    with _pool_lock:
+        lst = _idle_engines.get(dev)
+        if lst:
+            h = lst.pop()
+    if h:
         g = <ss_ingest*>h
         rc = _abi.reset(g)
     else:
         rc = _abi.create(dev, &g)
-        if rc == 0:
-            _engines[dev] = <size_t>g
     if rc != 0:
         raise RuntimeError(f"shortseq_amd GPU engine: {_abi.last_error().decode(errors='replace')} (rc {rc})")
     return g
+
+
+cdef _engine_release(int dev, ss_ingest* g):
+    with _pool_lock:
+        _idle_engines.setdefault(dev, []).append(<size_t>g)
 
 
 cdef _ingest_check(int rc, what):
@@ -569,23 +644,33 @@ cdef _raise_ingest_error(ss_ingest* g):
 
 
 cdef _fill_rows(ShortSeqCounter self, uint64_t K, const uint32_t* lens, const uint64_t* counts,
-                const uint64_t* words):
+                const uint64_t* words, bint add=False):
     """Insert the engine's rows (first-occurrence order) into the dict: one key object per row,
     inserted with its known hash (the objects' own __hash__ = packed word 0, -1 -> -2; counter.pyx
     :44-50 inserts the same way), so the loop walks the arrays front to back with no per-key
-    __hash__ call, tuple or sort."""
+    __hash__ call, tuple or sort.  add: the rows of a later shard (every read of it comes after the
+    dict's reads): a key already present adds its count and keeps its place, a new key goes last --
+    the first-occurrence order of the whole list."""
     cdef uint64_t k, woff = 0
     cdef uint32_t L
     cdef Py_hash_t h
+    cdef PyObject* old
     for k in range(K):
         L = lens[k]
         if L == 0:
-            dict.__setitem__(self, empty, counts[k])
+            dict.__setitem__(self, empty, (dict.get(self, empty, 0) + counts[k]) if add else counts[k])
             continue
         h = <Py_hash_t>words[woff]
         if h == -1:
             h = -2
-        _PyDict_SetItem_KnownHash(self, _from_words(words + woff, L), counts[k], h)
+        key = _from_words(words + woff, L)
+        if add:
+            old = _PyDict_GetItem_KnownHash(self, key, h)
+            if old != NULL:
+                _PyDict_SetItem_KnownHash(self, key, <object>old + counts[k], h)
+                woff += _nwords(L)
+                continue
+        _PyDict_SetItem_KnownHash(self, key, counts[k], h)
         woff += _nwords(L)
 
 
@@ -598,35 +683,87 @@ def _fill_from_arrays(ShortSeqCounter counter, lens, counts, words):
     _fill_rows(counter, lv.shape[0], &lv[0] if lv.shape[0] else NULL, &cv[0] if cv.shape[0] else NULL, &wv[0])
 
 
-cdef _fill_from_engine(ShortSeqCounter self, ss_ingest* g):
-    cdef uint64_t K = 0, NW = 0
+cdef _fill_from_engine(ShortSeqCounter self, ss_ingest* g, bint add=False):
+    """The rows of a finished shard (its first rejected read raises instead)."""
     cdef const uint32_t* lens
     cdef const uint64_t* counts
     cdef const uint64_t* words
-    cdef int rc
     _raise_ingest_error(g)
-    with nogil:
-        rc = _abi.finish(g, &K, &NW)
-    _ingest_check(rc, "ingest finish")
     _ingest_check(_abi.results(g, &lens, &counts, &words), "ingest results")
-    _fill_rows(self, K, lens, counts, words)
+    _fill_rows(self, _engine_keys(g), lens, counts, words, add)
 
 
-def _count_batch_gpu(ShortSeqCounter self, list reads, int dev):
-    """Batch path (counter.pyx:22-39 over a whole list): the bytes objects are copied back to back
-    into the engine's pinned staging buffer, counted on the GPU (split by length on the device, one
-    table per length: the length is part of the key, short_seq_64.pyx:41-44) and the dict is
-    rebuilt in first-occurrence order.  The first rejected read in list order raises the reference's
-    error."""
+cdef dict _engine_nkeys = {}
+
+
+cdef uint64_t _engine_keys(ss_ingest* g):
+    return _engine_nkeys.get(<size_t>g, 0)
+
+
+def _shard_work(size_t gh, int kind, size_t blob, size_t lens, uint64_t n, bytes path, uint64_t begin,
+                uint64_t end, uint64_t line0, uint64_t chunk, size_t nseqs_p):
+    """One shard on its engine, GIL released: count (a staged list slice, or a FASTQ byte range),
+    then -- unless it holds a rejected read -- finish (its rows into the engine's pinned results)."""
+    cdef ss_ingest* g = <ss_ingest*>gh
+    cdef int rc, bad_kind = 0
+    cdef uint64_t bad_idx = 0, K = 0, NW = 0
+    cdef uint64_t* nseqs = <uint64_t*>nseqs_p
+    cdef const char* cpath = NULL
+    if kind == 1:
+        cpath = path
+    with nogil:
+        if kind == 0:
+            rc = _abi.add_blob(g, <const uint8_t*>blob, <const uint32_t*>lens, n)
+        else:
+            rc = _abi.add_fastq_range(g, cpath, begin, end, line0, chunk, nseqs)
+        if rc == 0:
+            rc = _abi.error(g, &bad_idx, &bad_kind, NULL, 0, NULL)
+        if rc == 0 and bad_idx == <uint64_t>-1:
+            rc = _abi.finish(g, &K, &NW)
+    _ingest_check(rc, "ingest")
+    _engine_nkeys[gh] = K
+
+
+def _run_shards(jobs):
+    """jobs: argument tuples of _shard_work, one per engine; all but the first run in threads."""
+    errs = [None] * len(jobs)
+
+    def run(i):
+        try:
+            _shard_work(*jobs[i])
+        except BaseException as e:  # noqa: BLE001
+            errs[i] = e
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(1, len(jobs))]
+    for t in ts:
+        t.start()
+    run(0)
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+def _count_batch_gpu(ShortSeqCounter self, list reads, devs):
+    """Batch path (counter.pyx:22-39 over a whole list): the list is cut into len(devs) contiguous
+    shards; each shard's bytes objects are copied back to back into its engine's pinned staging
+    buffer and counted on that engine's device (split by length on the device, one table per length:
+    the length is part of the key, short_seq_64.pyx:41-44), the shards concurrently.  The dict is
+    built from the shards' rows in shard order (each shard's rows in first-occurrence order), which
+    is the first-occurrence order of the whole list.  The first rejected read in list order raises
+    the reference's error."""
     cdef Py_ssize_t i, n = PyList_GET_SIZE(reads), ln
-    cdef uint64_t total = 0
+    cdef uint64_t total = 0, sub
     cdef object item
     cdef uint8_t* dst
+    cdef uint8_t* base
     cdef uint32_t* lens = <uint32_t*>malloc(max(1, n) * sizeof(uint32_t))
     cdef ss_ingest* g
-    cdef int rc
+    cdef Py_ssize_t D, k, lo, hi
+    cdef uint64_t nseq = 0
     if lens == NULL:
         raise MemoryError()
+    engines = []
     try:
         for i in range(n):
             item = <object>PyList_GET_ITEM(reads, i)
@@ -637,19 +774,47 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, int dev):
             ln = PyBytes_GET_SIZE(item)
             lens[i] = <uint32_t>ln if ln < 0xFFFFFFFF else <uint32_t>0xFFFFFFFF
             total += ln
-        g = _engine(dev)
-        _ingest_check(_abi.staging(g, total, &dst), "ingest staging")
-        for i in range(n):
-            ln = lens[i]
-            memcpy(dst, PyBytes_AS_STRING(<object>PyList_GET_ITEM(reads, i)), ln)
-            dst += ln
-        _ingest_check(_abi.staging(g, total, &dst), "ingest staging")   # base pointer again
-        with nogil:
-            rc = _abi.add_blob(g, dst, lens, n)
-        _ingest_check(rc, "ingest")
-        _fill_from_engine(self, g)
+        D = max(1, min(len(devs), n))
+        jobs = []
+        for k in range(D):
+            lo, hi = n * k // D, n * (k + 1) // D
+            g = _engine(devs[k])
+            engines.append((devs[k], <size_t>g))
+            sub = 0
+            for i in range(lo, hi):
+                sub += lens[i]
+            _ingest_check(_abi.staging(g, sub, &base), "ingest staging")
+            dst = base
+            for i in range(lo, hi):
+                ln = lens[i]
+                memcpy(dst, PyBytes_AS_STRING(<object>PyList_GET_ITEM(reads, i)), ln)
+                dst += ln
+            jobs.append((<size_t>g, 0, <size_t>base, <size_t>(lens + lo), <uint64_t>(hi - lo), b"", 0, 0, 0, 0, None))
+        _run_shard_jobs(jobs)
+        for k in range(D):
+            _fill_from_engine(self, <ss_ingest*><size_t>engines[k][1], k > 0)
     finally:
         free(lens)
+        for d, h in engines:
+            _engine_nkeys.pop(h, None)
+            _engine_release(d, <ss_ingest*><size_t>h)
+
+
+def _run_shard_jobs(jobs):
+    """_run_shards with the nseqs out-pointer of every FASTQ job owned here."""
+    cdef uint64_t* ns = <uint64_t*>calloc(max(1, len(jobs)), sizeof(uint64_t))
+    if ns == NULL:
+        raise MemoryError()
+    cdef Py_ssize_t i
+    cdef size_t base = <size_t>ns
+    try:
+        full = []
+        for i in range(len(jobs)):
+            full.append((*jobs[i][:10], base + 8 * i))
+        _run_shards(full)
+        return [ns[i] for i in range(len(jobs))]
+    finally:
+        free(ns)
 
 
 def _raise_first_error(list reads, Py_ssize_t upto):
@@ -667,12 +832,16 @@ def _raise_first_error(list reads, Py_ssize_t upto):
 def read_and_count_fastq(filename, device="auto", *, _chunk_bytes=0):
     """counter.pyx:57-70 + fast_read.pyx:3-20: keep line 2 of every 4 lines; each kept line loses
     exactly its last character (strlen - 1, short_seq.pyx:50-52); prints the reference's timings.
-    device "auto" (a GPU when present) / "cuda[:N]": the file is streamed to HBM in pinned chunks
-    and indexed, split by length and counted there (ss_ingest_add_fastq); "host": the
+    device "auto" (the visible GPUs) / "cuda[:N]" / "all" / a list: the file is cut into one byte
+    range per device at line boundaries (ss_fastq_split), each range streamed to its device in
+    pinned chunks and indexed, split by length and counted there (ss_ingest_add_fastq_range), the
+    ranges concurrently, and the dict built from the ranges' rows in file order; "host": the
     reference's per-line loop."""
-    dev = _resolve_device(device)
-    if dev >= 0:
-        return _read_and_count_fastq_gpu(filename, dev, _chunk_bytes)
+    import os
+    work = os.path.getsize(filename) if os.path.isfile(filename) else 0
+    devs = _resolve_devices(device, work, 256 << 20)
+    if devs:
+        return _read_and_count_fastq_gpu(filename, devs, _chunk_bytes)
     cdef FILE* f
     cdef char* line = NULL
     cdef size_t cap = 0
@@ -706,25 +875,45 @@ def read_and_count_fastq(filename, device="auto", *, _chunk_bytes=0):
     return counts
 
 
-def _read_and_count_fastq_gpu(filename, int dev, uint64_t chunk_bytes=0):
-    """The file streamed through the engine (parallel preads into pinned staging, chunks ending
-    after a newline, one-read FASTQ index, split by length and counted on the device)."""
+def _read_and_count_fastq_gpu(filename, devs, uint64_t chunk_bytes=0):
+    """The file streamed through one engine per device: range k of ss_fastq_split on devs[k]
+    (parallel preads into pinned staging, chunks ending after a newline, one-read FASTQ index, split
+    by length and counted on the device); rows merged in range order."""
     import os
-    cdef uint64_t nseqs = 0
     cdef int rc
-    cdef ss_ingest* g
+    cdef Py_ssize_t D = len(devs), k
     fname = filename.encode("utf-8")
     if not os.path.isfile(filename):
         raise Exception(f"{str(fname)}: Something went wrong while reading this file.")
-    cdef const char* cpath = fname
+    cdef uint64_t* begin = <uint64_t*>calloc(D + 1, sizeof(uint64_t))
+    cdef uint64_t* line0 = <uint64_t*>calloc(D + 1, sizeof(uint64_t))
+    if begin == NULL or line0 == NULL:
+        free(begin)
+        free(line0)
+        raise MemoryError()
+    engines = []
     t1 = time.time()
-    g = _engine(dev)
-    with nogil:
-        rc = _abi.add_fastq(g, cpath, chunk_bytes, &nseqs)
-    _ingest_check(rc, "ingest fastq")
-    t2 = time.time()
-    counts = ShortSeqCounter()
-    _fill_from_engine(counts, g)
-    t3 = time.time()
+    try:
+        if D > 1:
+            _ingest_check(_abi.fastq_split(fname, <uint32_t>D, begin, line0), "fastq split")
+        else:
+            begin[1] = <uint64_t>-1
+        jobs = []
+        for k in range(D):
+            g = <size_t>_engine(devs[k])
+            engines.append((devs[k], g))
+            jobs.append((g, 1, 0, 0, 0, fname, begin[k], begin[k + 1], line0[k], chunk_bytes, None))
+        nseqs = sum(_run_shard_jobs(jobs))
+        t2 = time.time()
+        counts = ShortSeqCounter()
+        for k in range(D):
+            _fill_from_engine(counts, <ss_ingest*><size_t>engines[k][1], k > 0)
+        t3 = time.time()
+    finally:
+        free(begin)
+        free(line0)
+        for d, h in engines:
+            _engine_nkeys.pop(h, None)
+            _engine_release(d, <ss_ingest*><size_t>h)
     print(f"{t2-t1:.2f}s to read {nseqs} total seqs, and {t3 - t2:.2f}s to count {len(counts)} unique sequences")
     return counts

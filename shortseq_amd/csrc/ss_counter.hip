@@ -2317,6 +2317,73 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
     }
 }
 
+// Merge of already-counted multi-word entries (distinct keys: e.g. the extraction of another
+// table when a per-length table grows): phase 1 finds each entry's key among the slots that existed
+// before the merge (the table is stable during the pass, so the key words are complete); phase 2
+// gives the rest a fresh slot (a CAS on the fingerprint; a slot another entry claims is never this
+// entry's key, the entries being distinct, so claimed slots are skipped without comparing words)
+// and writes their key words, count and first index.  Found keys add count / min first.
+__global__ __launch_bounds__(256) void k_mw_merge_find(Tbl t, const uint64_t* __restrict__ words, uint64_t m,
+                                                       uint64_t* __restrict__ found) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
+        const uint64_t* kw = words + e * t.W;
+        const uint64_t fp = words_fp(kw, t.W);
+        const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
+        uint64_t off = top & t.slice_mask, at = kEmpty;
+        for (uint64_t probe = 0; probe <= t.slice_mask; ++probe) {
+            const uint64_t k = t.slots[base + off].key;
+            if (k == kEmpty) break;
+            if (k == fp && words_eq(t.keywords + (base + off) * t.W, kw, t.W)) {
+                at = base + off;
+                break;
+            }
+            off = (off + 1) & t.slice_mask;
+        }
+        found[e] = at;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mw_merge_claim(Tbl t, const uint64_t* __restrict__ words,
+                                                        const uint64_t* __restrict__ counts,
+                                                        const uint64_t* __restrict__ first, uint64_t m,
+                                                        const uint64_t* __restrict__ found) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
+        const uint64_t* kw = words + e * t.W;
+        if (counts[e] >> 32) atomicOr(t.overflow, kOvfField);
+        const uint32_t c = (uint32_t)counts[e];
+        uint64_t f = first[e];
+        if (f > kMaxIndex) {
+            atomicOr(t.overflow, kOvfIndex);
+            f = kMaxIndex;
+        }
+        uint64_t at = found[e];
+        if (at == kEmpty) {
+            const uint64_t fp = words_fp(kw, t.W);
+            const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
+            uint64_t off = top & t.slice_mask;
+            for (uint64_t probe = 0; probe <= t.slice_mask; ++probe) {
+                if (t.slots[base + off].key == kEmpty &&
+                    atomicCAS(&t.slots[base + off].key, (unsigned long long)kEmpty, (unsigned long long)fp) == kEmpty) {
+                    at = base + off;
+                    break;
+                }
+                off = (off + 1) & t.slice_mask;
+            }
+            if (at == kEmpty) {
+                atomicOr(t.overflow, kOvfTable);
+                continue;
+            }
+            uint64_t* dst = t.keywords + at * t.W;
+            for (uint32_t q = 0; q < t.W; ++q) dst[q] = kw[q];
+            t.slots[at].ncount = ~c;
+            t.slots[at].first = (uint32_t)f;
+            continue;
+        }
+        atomicAdd(&t.slots[at].ncount, 0u - c);
+        if (t.slots[at].first > (uint32_t)f) atomicMin(&t.slots[at].first, (uint32_t)f);
+    }
+}
+
 Tbl tbl_of(const ss_counter* c) {
     Tbl t;
     t.slots = c->slots;
@@ -2786,6 +2853,28 @@ int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_le
     hipLaunchKernelGGL(k_merge, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, tbl_of(c), d_keys, d_counts,
                        d_first, m);
     return ss_check(hipGetLastError(), "k_merge");
+}
+
+int ss_counter_merge_words(ss_counter* c, const uint64_t* d_words, const uint64_t* d_counts,
+                           const uint64_t* d_first, uint64_t m, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (m == 0) return SS_OK;
+    if (!d_words || !d_counts || !d_first) return ss_fail(SS_EARG, "null buffer");
+    if (c->W < 2) return ss_fail(SS_EARG, "ss_counter_merge_words takes multi-word keys (L > 32): use ss_counter_merge");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = flush_reset(c, s);
+    if (rc) return rc;
+    uint64_t* found = nullptr;
+    rc = ss_check(hipMallocAsync((void**)&found, m * sizeof(uint64_t), s), "merge_words scratch");
+    if (rc) return rc;
+    const unsigned grid = grid_for(m, 256, 256 * 16);
+    const Tbl t = tbl_of(c);
+    hipLaunchKernelGGL(k_mw_merge_find, dim3(grid), dim3(256), 0, s, t, d_words, m, found);
+    hipLaunchKernelGGL(k_mw_merge_claim, dim3(grid), dim3(256), 0, s, t, d_words, d_counts, d_first, m,
+                       (const uint64_t*)found);
+    rc = ss_check(hipGetLastError(), "ss_counter_merge_words");
+    const int rf = ss_check(hipFreeAsync(found, s), "merge_words scratch free");
+    return rc ? rc : rf;
 }
 
 int ss_counter_set_length(ss_counter* c, uint32_t L) {

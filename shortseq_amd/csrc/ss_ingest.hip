@@ -27,8 +27,9 @@
 // 2 x the rows its length brings in the first chunk and, for single-word keys, grows (extract ->
 // merge into a table of twice the needed size) when the rows counted could push it past half full
 // (an exact size query decides; the query costs one sync and is skipped while rows <= capacity / 2).
-// Multi-word tables (L > 32) cannot merge; they start at 2 x the length's rows scaled by the file's
-// remaining size.  (table sizes follow each length's own share, not the whole file.)
+// Multi-word tables (L > 32) grow the same way through ss_counter_extract_words +
+// ss_counter_merge_words (a length rare in the first chunk and common later); they start
+// at 2 x the length's rows scaled by the file's remaining size.
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -471,7 +472,6 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m) {
         gr.cap = std::min<uint64_t>(1ull << 32, pow2_at_least((uint64_t)(2.0 * (double)m * scale) + 2));
         return table_get(g, gr.cap, &gr.table);
     }
-    if (gr.L > 32) return SS_OK;      // multi-word tables do not merge: sized up front
     uint64_t size = 0;
     int rc = table_size(g, gr.table, &size);
     if (rc) return rc;
@@ -481,15 +481,21 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m) {
     if ((rc = table_get(g, ncap, &nt)) != SS_OK) return rc;
     if ((rc = ss_counter_set_length(nt, gr.L)) != SS_OK) return rc;
     const uint64_t cap = gr.cap + 1;
-    DBuf<uint64_t> k, c, f, pc;
+    const uint32_t W = gr.L <= 32 ? 1u : (gr.L + 31) / 32;
+    DBuf<uint64_t> k, c, f, pc, wd;
     DBuf<uint32_t> l;
     if ((rc = k.ensure(cap)) || (rc = c.ensure(cap)) || (rc = f.ensure(cap)) || (rc = l.ensure(cap)) ||
-        (rc = pc.ensure(1)))
+        (rc = pc.ensure(1)) || (W > 1 && (rc = wd.ensure(cap * W))))
         return rc;
-    rc = ss_counter_extract(gr.table, 1, k.p, l.p, c.p, f.p, cap, pc.p, g->stream);
-    if (!rc) rc = ss_counter_merge(nt, k.p, l.p, c.p, f.p, size, g->stream);
+    if (W == 1) {
+        rc = ss_counter_extract(gr.table, 1, k.p, l.p, c.p, f.p, cap, pc.p, g->stream);
+        if (!rc) rc = ss_counter_merge(nt, k.p, l.p, c.p, f.p, size, g->stream);
+    } else {     // multi-word keys: the entries' words travel (equality is decided on them)
+        rc = ss_counter_extract_words(gr.table, 1, k.p, l.p, wd.p, c.p, f.p, cap, pc.p, g->stream);
+        if (!rc) rc = ss_counter_merge_words(nt, wd.p, c.p, f.p, size, g->stream);
+    }
     if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest grow");
-    k.release(), c.release(), f.release(), l.release(), pc.release();
+    k.release(), c.release(), f.release(), l.release(), pc.release(), wd.release();
     if (rc) return rc;
     table_put(g, gr.table);
     gr.table = nt;
@@ -499,10 +505,16 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m) {
 
 // The chunk's reads: d_buf[offs[i], + lens[i]) for i < n (global index base + i).  dense: reads are
 // back to back (offs = exclusive prefix of lens) and all have length dense_L (no split, no gather).
-int process_chunk(ss_ingest* g, uint64_t nbytes, uint64_t n, uint32_t dense_L,
-                  const std::vector<uint64_t>* h_offs, const uint8_t* h_chunk) {
+// d_buf / d_offs / d_lens: the chunk on the device (the engine's own buffers, or the caller's for
+// ss_ingest_add_device); h_chunk / h_offs: the same bytes on the host when there (the first rejected
+// read's bytes are then taken from there, else copied back).
+int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t nbytes,
+                  uint64_t n, uint32_t dense_L, const std::vector<uint64_t>* h_offs, const uint8_t* h_chunk) {
     if (n == 0) return SS_OK;
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "ingest: a chunk holds < 2^32 reads");
+    // the row maps and first indices hold global read indices as u32
+    if (g->nreads + n > 0xFFFFFFFEull)
+        return ss_fail(SS_EARG, "ingest: one call counts fewer than 2^32 - 1 reads");
     hipStream_t s = g->stream;
     const uint64_t base = g->nreads;
     int rc = SS_OK;
@@ -517,11 +529,11 @@ int process_chunk(ss_ingest* g, uint64_t nbytes, uint64_t n, uint32_t dense_L,
         if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins)))
             return rc;
-        hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, g->dlens.p, n, g->blkhist.p, g->blkfirst.p);
+        hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p, g->blkfirst.p);
         hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(256), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
                            g->split_out.p);
         hipLaunchKernelGGL(k_len_binstart, dim3(1), dim3(1024), 0, s, g->split_out.p);
-        hipLaunchKernelGGL(k_len_scatter, dim3(kSplitBlocks), dim3(64), 0, s, g->dlens.p, n, g->blkhist.p,
+        hipLaunchKernelGGL(k_len_scatter, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p,
                            (const uint64_t*)g->split_out.p, g->order.p);
         rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, 3 * kLenBins * 8, hipMemcpyDeviceToHost, s),
                       "ingest split copy");
@@ -558,12 +570,12 @@ int process_chunk(ss_ingest* g, uint64_t nbytes, uint64_t n, uint32_t dense_L,
         uint64_t stride;
         const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
         if (dense_L) {
-            src = g->dbuf.p;
+            src = d_buf;
             stride = dense_L;
         } else {
             stride = (jb.L + 15) / 16 * 16;
             if ((rc = g->rows.ensure(jb.m * stride))) return rc;
-            rc = ss_gather_rows(g->dbuf.p, nbytes, g->offs.p, sel, jb.m, jb.L, g->rows.p, stride, s);
+            rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.L, g->rows.p, stride, s);
             if (rc) return rc;
             src = g->rows.p;
         }
@@ -591,13 +603,20 @@ int process_chunk(ss_ingest* g, uint64_t nbytes, uint64_t n, uint32_t dense_L,
         if (base + idx < g->bad_index) {
             g->bad_index = base + idx;
             g->bad_kind = SS_EINVALID_BASE;
-            uint64_t off = 0;
+            uint64_t off = dense_L ? idx * dense_L : 0;
             if (h_offs) {
                 off = (*h_offs)[idx];
-            } else if ((rc = ss_check(hipMemcpy(&off, g->offs.p + idx, 8, hipMemcpyDeviceToHost), "ingest bad off"))) {
+            } else if (!dense_L &&
+                       (rc = ss_check(hipMemcpy(&off, d_offs + idx, 8, hipMemcpyDeviceToHost), "ingest bad off"))) {
                 return rc;
             }
-            g->bad_bytes.assign((const char*)h_chunk + off, jobs[j].L);
+            if (h_chunk) {
+                g->bad_bytes.assign((const char*)h_chunk + off, jobs[j].L);
+            } else {
+                g->bad_bytes.assign(jobs[j].L, '\0');
+                rc = ss_check(hipMemcpy(&g->bad_bytes[0], d_buf + off, jobs[j].L, hipMemcpyDeviceToHost), "ingest bad read");
+                if (rc) return rc;
+            }
         }
     }
     // a too-long read's bytes (the message does not quote them) are not needed
@@ -732,12 +751,80 @@ int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_le
         rc = ss_check(hipMemcpyAsync(g->offs.p, offs.data(), n * 8, hipMemcpyHostToDevice, s), "ingest H2D");
         if (!rc) rc = ss_check(hipMemcpyAsync(g->dlens.p, h_lens, n * 4, hipMemcpyHostToDevice, s), "ingest H2D");
     }
-    if (!rc) rc = process_chunk(g, total, n, dense, &offs, h_blob);
+    if (!rc) rc = process_chunk(g, g->dbuf.p, g->offs.p, g->dlens.p, total, n, dense, &offs, h_blob);
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest blob");   // staging reusable after return
     return rc;
 }
 
+int ss_ingest_add_device(ss_ingest* g, const uint8_t* d_blob, uint64_t nbytes, const uint64_t* d_offsets,
+                         const uint32_t* d_lens, uint64_t n) {
+    if (!g || (n && (!d_blob || !d_offsets || !d_lens))) return ss_fail(SS_EARG, "null argument");
+    if (n == 0 || g->bad_index != kNoSlot) return SS_OK;
+    (void)hipSetDevice(g->device);
+    int rc = process_chunk(g, d_blob, d_offsets, d_lens, nbytes, n, 0, nullptr, nullptr);
+    if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest device blob");
+    return rc;
+}
+
 int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, uint64_t* h_nseqs) {
+    return ss_ingest_add_fastq_range(g, path, 0, ~0ull, 0, chunk_bytes, h_nseqs);
+}
+
+int ss_fastq_split(const char* path, uint32_t nparts, uint64_t* h_begin, uint64_t* h_line0) {
+    if (!path || !nparts || !h_begin || !h_line0) return ss_fail(SS_EARG, "null argument");
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return ss_fail(SS_EARG, "cannot open the FASTQ file");
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        return ss_fail(SS_EARG, "cannot stat the FASTQ file");
+    }
+    const uint64_t size = (uint64_t)st.st_size;
+    // part p starts right after the first newline at or past p * size / nparts (part 0 at 0); parts
+    // may come out empty (begin[p] == begin[p + 1]) when lines are long
+    std::vector<uint64_t> b(nparts + 1, size);
+    b[0] = 0;
+    std::vector<uint8_t> buf(1 << 16);
+    for (uint32_t p = 1; p < nparts; ++p) {
+        uint64_t pos = std::max(b[p - 1], size * p / nparts), at = size;
+        while (pos < size && at == size) {
+            const uint64_t got = pread_full(fd, buf.data(), std::min<uint64_t>(buf.size(), size - pos), pos);
+            if (got == 0) break;
+            const void* nl = memchr(buf.data(), '\n', got);
+            if (nl) at = pos + (uint64_t)((const uint8_t*)nl - buf.data()) + 1;
+            pos += got;
+        }
+        b[p] = at;
+    }
+    // newlines before each part: the parts' newline counts (one thread per part), prefix-summed
+    std::vector<uint64_t> nl(nparts, 0);
+    std::vector<std::thread> ts;
+    for (uint32_t p = 0; p + 1 < nparts; ++p)
+        ts.emplace_back([&, p] {
+            std::vector<uint8_t> tb(1 << 20);
+            uint64_t cnt = 0;
+            for (uint64_t pos = b[p]; pos < b[p + 1];) {
+                const uint64_t got = pread_full(fd, tb.data(), std::min<uint64_t>(tb.size(), b[p + 1] - pos), pos);
+                if (got == 0) break;
+                for (uint64_t k = 0; k < got; ++k) cnt += tb[k] == '\n';
+                pos += got;
+            }
+            nl[p] = cnt;
+        });
+    for (auto& t : ts) t.join();
+    close(fd);
+    uint64_t run = 0;
+    for (uint32_t p = 0; p < nparts; ++p) {
+        h_begin[p] = b[p];
+        h_line0[p] = run;
+        run += nl[p];
+    }
+    h_begin[nparts] = size;
+    return SS_OK;
+}
+
+int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, uint64_t end, uint64_t line0,
+                              uint64_t chunk_bytes, uint64_t* h_nseqs) {
     if (!g || !path) return ss_fail(SS_EARG, "null argument");
     (void)hipSetDevice(g->device);
     const int fd = open(path, O_RDONLY);
@@ -747,12 +834,20 @@ int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, ui
         close(fd);
         return ss_fail(SS_EARG, "cannot stat the FASTQ file");
     }
-    const uint64_t size = (uint64_t)st.st_size;
+    // the range [begin, end) of the file: it starts at a line boundary and ends at the file's end or
+    // right after a newline, so its last line is complete (the strlen - 1 rule of a final line with no
+    // newline applies only at the file's end)
+    const uint64_t size = std::min<uint64_t>((uint64_t)st.st_size, end);
+    if (h_nseqs) *h_nseqs = 0;
+    if (begin >= size) {
+        close(fd);
+        return SS_OK;
+    }
     if (chunk_bytes == 0) chunk_bytes = 1ull << 30;
-    uint64_t cap = std::max<uint64_t>(16, std::min<uint64_t>(chunk_bytes, size + 16));
+    uint64_t cap = std::max<uint64_t>(16, std::min<uint64_t>(chunk_bytes, size - begin + 16));
     hipStream_t s = g->stream;
     int rc = g->stage.ensure(cap);
-    uint64_t line0 = 0, carry = 0, pos = 0, seqs0 = g->nreads;
+    uint64_t carry = 0, pos = begin, seqs0 = g->nreads;
     unsigned threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     while (!rc) {
         if (cap >= (1ull << 32)) {
@@ -814,8 +909,8 @@ int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, ui
             maxr = nrec;
         }
         if (rc) break;
-        if (!at_eof && g->est_scale == 1.0 && use) g->est_scale = (double)size / (double)use;
-        rc = process_chunk(g, use, nrec, 0, nullptr, hv);
+        if (!at_eof && g->est_scale == 1.0 && use) g->est_scale = (double)(size - begin) / (double)use;
+        rc = process_chunk(g, g->dbuf.p, g->offs.p, g->dlens.p, use, nrec, 0, nullptr, hv);
         if (rc) break;
         line0 += nl;
         if (at_eof || g->bad_index != kNoSlot) break;

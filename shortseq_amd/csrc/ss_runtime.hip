@@ -41,6 +41,11 @@ int ss_device_count(int* h_count) {
 
 int ss_set_device(int device) { return ss_check(hipSetDevice(device), "hipSetDevice"); }
 
+int ss_get_device(int* h_device) {
+    if (!h_device) return ss_fail(SS_EARG, "null h_device");
+    return ss_check(hipGetDevice(h_device), "hipGetDevice");
+}
+
 int ss_pinned_alloc(void** h_ptr, size_t bytes) {
     if (!h_ptr) return ss_fail(SS_EARG, "null h_ptr");
     return ss_check(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault), "hipHostMalloc");

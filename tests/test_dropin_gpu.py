@@ -132,3 +132,97 @@ print("ok")
                          text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ok" in out.stdout
+
+
+@pytest.mark.parametrize("ndev", [2, 8])
+def test_c1_dropin_reference_digest_multi_engine(gpu, digests, oracle, ndev):
+    """The multi-GPU drop-in (counter.pyx:10-54 over a list sharded by contiguous read ranges, one
+    ingest engine per device, rows merged in shard order) rehearsed with `ndev` engines on device 0:
+    the reference's ordered digest of the 1M x 32 pool-65536 list, exactly as with one engine."""
+    import hashlib
+    import numpy as np
+    d = digests["counter_1000000x32_pool65536"]
+    n, L = d["n"], d["L"]
+    a = oracle.gen_pool_reads(d["seed"], d["pool_seed"], d["U"], 0, n, L)
+    reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    c = ShortSeqCounter(reads, device=[0] * ndev)
+    assert len(c) == d["unique"]
+    rows = np.array([(k.packed[0], len(k), v) for k, v in c.items()], dtype=np.uint64)
+    assert hashlib.sha256(np.ascontiguousarray(rows).tobytes()).hexdigest() == d["ordered_sha256"]
+
+
+@pytest.mark.parametrize("ndev", [2, 3, 8])
+def test_multi_engine_golden_and_mixed(gpu, golden, ndev):
+    """Golden counter cases (errors too) and a mixed-length list through `ndev` engines: identical
+    to the single-device and host paths (dict order across shard boundaries, the first error in list
+    order)."""
+    devs = [0] * ndev
+    for case in golden["counter"]:
+        if "reads_str" in case:
+            continue
+        reads = [bytes.fromhex(h) for h in case["reads_hex"]]
+        if "raises" in case:
+            with pytest.raises(Exception) as ei:
+                ShortSeqCounter(reads, device=devs)
+            assert str(ei.value) == case["message"]
+            continue
+        c = ShortSeqCounter(reads, device=devs)
+        assert _items(c) == [(it["class"], it["str"], it["length"], it["count"]) for it in case["items"]]
+    rng = random.Random(31)
+    pool = [bytes(rng.choice(b"ACGT") for _ in range(L)) for L in (0, 3, 16, 32, 33, 64, 96, 97, 300, 1024)
+            for _ in range(5)]
+    reads = [rng.choice(pool) for _ in range(90_000)]
+    assert _items(ShortSeqCounter(reads, device=devs)) == _items(ShortSeqCounter(reads, device="host"))
+    reads[70_000] = b"ACGTX"
+    reads[80_000] = b"ACGTN"
+    with pytest.raises(Exception) as ei:
+        ShortSeqCounter(reads, device=devs)
+    assert str(ei.value) == "Unsupported base character: X"
+
+
+@pytest.mark.parametrize("ndev", [2, 8])
+def test_fastq_multi_engine(gpu, golden, tmp_path, ndev):
+    """read_and_count_fastq split into `ndev` byte ranges at line boundaries (ss_fastq_split: the
+    lines before each range keep the j % 4 == 1 selection global), one engine each: the reference's
+    FASTQ fixtures and a random file equal the host path."""
+    devs = [0] * ndev
+    for name, case in sorted(golden["fastq"].items()):
+        p = tmp_path / (name + ".fq")
+        p.write_bytes(bytes.fromhex(case["file_hex"]))
+        if case["raises"]:
+            with pytest.raises(Exception) as ei:
+                sq.read_and_count_fastq(str(p), device=devs)
+            assert str(ei.value) == case["message"], name
+            continue
+        c = sq.read_and_count_fastq(str(p), device=devs)
+        h = sq.read_and_count_fastq(str(p), device="host")
+        assert _items(c) == _items(h), name
+    rng = random.Random(32)
+    pool = [bytes(rng.choice(b"ACGT") for _ in range(rng.choice([18, 32, 33, 75, 151]))) for _ in range(700)]
+    lines = [f"@r{i}\n{rng.choice(pool).decode()}\n+\n{'I' * 10}\n" for i in range(60_000)]
+    p = tmp_path / "multi.fq"
+    p.write_text("".join(lines))
+    assert _items(sq.read_and_count_fastq(str(p), device=devs)) == _items(sq.read_and_count_fastq(str(p), device="host"))
+
+
+def test_engines_thread_safe(gpu):
+    """concurrent ShortSeqCounter calls from several Python threads (the GIL is released
+    while they count) each get their own engine: every thread's dict is exact."""
+    import threading
+    rng = random.Random(33)
+    lists = []
+    for t in range(4):
+        pool = [bytes(rng.choice(b"ACGT") for _ in range(rng.choice([12, 32, 40]))) for _ in range(400)]
+        lists.append([rng.choice(pool) for _ in range(80_000)])
+    want = [_items(ShortSeqCounter(r, device="host")) for r in lists]
+    got = [None] * len(lists)
+
+    def run(i):
+        for _ in range(3):
+            got[i] = _items(ShortSeqCounter(lists[i], device="cuda"))
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(lists))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert got == want

@@ -305,3 +305,46 @@ def test_fastq_gpu_table_growth(gpu, tmp_path):
     h = sq.read_and_count_fastq(str(p), device="host")
     d = sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=1 << 17)
     assert _items(d) == _items(h)
+
+
+@pytest.mark.gpu
+def test_fastq_gpu_table_growth_multiword(gpu, tmp_path):
+    """an L > 32 length with a few reads near the end of the first chunk, then many
+    distinct keys in later chunks: its multi-word table grows (extract_words + merge_words) instead of
+    overflowing, and the dict equals the host path."""
+    rng = random.Random(23)
+    recs = [f"@a{i}\n{''.join(rng.choice('ACGT') for _ in range(20))}A\n+\nI\n" for i in range(2000)]
+    for L in (40, 150):
+        recs += [f"@x{L}_{i}\n{''.join(rng.choice('ACGT') for _ in range(L))}A\n+\nI\n" for i in range(3)]
+    for L in (40, 150):
+        recs += [f"@y{L}_{i}\n{''.join(rng.choice('ACGT') for _ in range(L))}A\n+\nI\n" for i in range(40_000)]
+    p = tmp_path / "growmw.fq"
+    p.write_text("".join(recs))
+    h = sq.read_and_count_fastq(str(p), device="host")
+    d = sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=1 << 16)
+    assert _items(d) == _items(h)
+
+
+def test_fastq_split_host(tmp_path):
+    """ss_fastq_split (host): every range starts at the file start or right after a newline, the
+    ranges tile the file, and line0 = the newlines before each range."""
+    import ctypes as C
+    from shortseq_amd import _native
+    lib = _native.lib()
+    rng = random.Random(24)
+    for trial in range(6):
+        data = b"".join(b"@r%d\n%s\n+\n%s\n" % (i, b"ACGT" * rng.randint(0, 60), b"I" * rng.randint(0, 3))
+                        for i in range(rng.choice([0, 1, 5, 2000])))
+        if trial == 5:
+            data += b"@last\nACG"           # no trailing newline
+        p = tmp_path / f"s{trial}.fq"
+        p.write_bytes(data)
+        for parts in (1, 2, 3, 8, 17):
+            b = (C.c_uint64 * (parts + 1))()
+            l0 = (C.c_uint64 * (parts + 1))()
+            assert lib.ss_fastq_split(str(p).encode(), parts, C.addressof(b), C.addressof(l0)) == 0
+            bs = list(b)
+            assert bs[0] == 0 and bs[-1] == len(data) and bs == sorted(bs)
+            for k in range(parts):
+                assert bs[k] in (0, len(data)) or data[bs[k] - 1:bs[k]] == b"\n", (trial, parts, k)
+                assert l0[k] == data[:bs[k]].count(b"\n"), (trial, parts, k)
