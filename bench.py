@@ -432,6 +432,64 @@ def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):
                                  "whole k-steps); frac_algorithmic: L compares per pair x2; dense i8 peak = 2x bf16"}}
 
 
+def bench_ragged(B, lib, dev, reps=5):
+    """50M ragged reads of 50-150 nt drawn from a 2^20-item pool, device-resident
+    (ss_synth_ragged_*: blob + offsets + lengths).  (a) ss_encode_var over the batch (wpr 5); (b) the
+    drop-in counter engine fed from device memory, ss_ingest_add_device + ss_ingest_finish: the
+    length split, one table per length (multi-word keys for L > 32: k_mw_*), the first-occurrence
+    rows copied back -- checked against the generator-derived digest (tests/golden/ragged_digests.json)."""
+    from shortseq_amd._native import check
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    with open(os.path.join(REPO, "tests", "golden", "ragged_digests.json")) as f:
+        d = json.load(f)["ragged_50M_L50-150_U20"]
+    n = d["n"]
+    blob, offs, lens = B.synth_ragged_pool_reads(n, d["seed"], d["pool_seed"], d["U"], d["Lmin"], d["Lmax"], device=dev)
+    nt = int(lens.sum().item())
+    wpr = B.wpr_for(d["Lmax"])
+    words = torch.empty((n, wpr), dtype=torch.int64, device=dev)
+    fb = B.first_bad_buffer(dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+
+    def enc(_t):
+        check(lib.ss_encode_var(blob.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, words.data_ptr(), wpr,
+                                fb.data_ptr(), s), "encode_var")
+    _el, tr = timed_loop(enc, reps, 2, 1)
+    if int(fb.item()) != -1:
+        raise SystemExit("PARITY FAILURE: ragged encode flagged a read")
+    enc_ms = tr.region_ms / reps
+    enc_bytes = nt + n * (8 + 4) + n * wpr * 8        # ASCII + offset + length in, wpr words out
+    del words
+    eng = B.DeviceIngest(dev)
+    ts = []
+    try:
+        for r in range(reps + 1):
+            eng.reset()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.count(blob, offs, lens)
+            gl, gc, gw = eng.results()
+            if r:
+                ts.append(time.perf_counter() - t0)
+    finally:
+        eng.close()
+    import oracle as _o   # the digest helper only (numpy), after timing
+    if len(gl) != d["unique"] or _o.rows_digest(gl, gc, gw) != d["digest"]:
+        raise SystemExit("PARITY FAILURE: ragged counter rows != ragged_50M_L50-150_U20")
+    t = float(np.median(ts))
+    floor = nt + n * 12
+    return {"reads": n, "nt": nt, "len_range": [d["Lmin"], d["Lmax"]], "pool": d["U"], "unique": len(gl),
+            "encode_var": {"ms_per_step": enc_ms, "nt_per_s": nt / enc_ms * 1e3,
+                           "roofline": {"bound": "hbm", "kernel": "k_encode_gen<var>", "achieved": enc_bytes / enc_ms / 1e6,
+                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": enc_bytes / enc_ms / 1e6 / HBM_PEAK_GBS,
+                                        "traffic": load_traffic("encode_var_ragged", n)}},
+            "count": {"s_per_call": t, "reads_per_s": n / t, "nt_per_s": nt / t,
+                      "floor_frac": floor / t / 1e9 / HBM_PEAK_GBS, "parity": "digest ragged_50M_L50-150_U20",
+                      "note": "ss_ingest_add_device + ss_ingest_finish wall time (host-synchronous engine: length "
+                              "split, per-length gathers and tables, rows copied back); floor_frac = one read of "
+                              "the blob + offsets + lengths at 8 TB/s"}}
+
+
 def bench_host_staged(B, dev, n=32_000_000, L=32, reps=5):
     """PCIe-inclusive C2: the reads in pageable host memory, packed words back to host memory
     (ss_encode_host: pinned ring + H2D / kernel / D2H streams).  Never `value`: the device-resident
@@ -735,6 +793,8 @@ def main():
             log("F1 FASTQ index / F4 all-pairs")
             local_extra("F1_fastq_index_100nt", lambda: bench_fastq_index(B, lib, dev))
             local_extra("F4_all_pairs_umi12", lambda: bench_all_pairs(B, lib, dev))
+            log("F2 ragged 50-150 nt")
+            local_extra("F2_ragged_50_150", lambda: bench_ragged(B, lib, dev))
             log("C2 host-staged (PCIe-inclusive)")
             local_extra("C2_host_staged_32", lambda: bench_host_staged(B, dev))
             log("C1 drop-in API")

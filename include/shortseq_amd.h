@@ -369,6 +369,15 @@ int ss_synth_pool_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, uin
                         uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream);
 int ss_synth_zipf_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, const uint64_t* d_cdf, uint64_t U,
                         uint64_t i0, uint64_t n, uint32_t L, uint64_t stride, void* stream);
+/* Ragged pool reads (mixed lengths): read i draws pool item
+ * p = splitmix64(pool_seed ^ i * 0xD1B54A32D192ED03) % U of length
+ * Lmin + splitmix64(seed ^ 0x6A09E667F3BCC909 ^ p) % (Lmax - Lmin + 1), word w = splitmix64(seed + 32 p + w)
+ * masked.  ss_synth_ragged_lens writes the n lengths; the caller lays the blob out (d_offsets, e.g.
+ * an exclusive prefix sum of the lengths) and ss_synth_ragged_reads writes the ASCII there. */
+int ss_synth_ragged_lens(uint32_t* d_lens, uint64_t seed, uint64_t pool_seed, uint64_t U, uint64_t i0, uint64_t n,
+                         uint32_t Lmin, uint32_t Lmax, void* stream);
+int ss_synth_ragged_reads(uint8_t* d_blob, const uint64_t* d_offsets, uint64_t seed, uint64_t pool_seed, uint64_t U,
+                          uint64_t i0, uint64_t n, uint32_t Lmin, uint32_t Lmax, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Host-resident batches (the host side stages read batches in pinned

@@ -222,6 +222,104 @@ def pool_counter_table(seed: int, pool_seed: int, U: int, n: int, L: int = 32, i
     return keys[o], counts[used.astype(np.int64)][o], first[used.astype(np.int64)][o]
 
 
+RAGGED_LEN_SALT = 0x6A09E667F3BCC909
+
+
+def ragged_item_lens(seed: int, items: np.ndarray, Lmin: int, Lmax: int) -> np.ndarray:
+    """Length of ragged pool items (the ss_synth_ragged_* rule, include/shortseq_amd.h)."""
+    with np.errstate(over="ignore"):
+        r = splitmix64_np(np.uint64(seed) ^ np.uint64(RAGGED_LEN_SALT) ^ np.asarray(items, np.uint64))
+    return (np.uint64(Lmin) + r % np.uint64(Lmax - Lmin + 1)).astype(np.uint32)
+
+
+def ragged_item_words(seed: int, item: int, L: int) -> list:
+    """The packed words of ragged pool item `item` of length L (= the encode of its ASCII)."""
+    out = []
+    for w in range((L + 31) // 32):
+        nb = min(32, L - 32 * w)
+        with np.errstate(over="ignore"):
+            r = int(splitmix64_np(np.array([seed + 32 * item + w], dtype=np.uint64))[0])
+        out.append(r if nb == 32 else r & ((1 << (2 * nb)) - 1))
+    return out
+
+
+def ragged_pool_reads(seed: int, pool_seed: int, U: int, i0: int, n: int, Lmin: int, Lmax: int) -> list:
+    """The reads (bytes) of ss_synth_ragged_* for a small n (host restatement)."""
+    items = pool_ids(pool_seed, i0, n, U)
+    lens = ragged_item_lens(seed, items, Lmin, Lmax)
+    out = []
+    for p, L in zip(items.tolist(), lens.tolist()):
+        ws = ragged_item_words(seed, p, L)
+        out.append(bytes(b"ACTG"[(ws[j // 32] >> (2 * (j % 32))) & 3] for j in range(L)))
+    return out
+
+
+def ragged_pool_rows(seed: int, pool_seed: int, U: int, n: int, Lmin: int, Lmax: int, chunk: int = 1 << 23):
+    """The drop-in counter's rows for n ragged pool reads, from the generator alone: the drawn items
+    in first-occurrence order, each (length, count, words), items of equal content merged.  Returns
+    (lens u32 [K], counts u64 [K], words u64 [sum ceil(L/32)]) -- the ss_ingest_results layout."""
+    counts = np.zeros(U, dtype=np.uint64)
+    first = np.full(U, np.iinfo(np.uint64).max, dtype=np.uint64)
+    for s0 in range(0, n, chunk):
+        m = min(chunk, n - s0)
+        ids = pool_ids(pool_seed, s0, m, U)
+        counts += np.bincount(ids.astype(np.int64), minlength=U).astype(np.uint64)
+        u, pos = np.unique(ids, return_index=True)
+        new = first[u] == np.iinfo(np.uint64).max
+        first[u[new]] = np.uint64(s0) + pos[new].astype(np.uint64)
+    used = np.nonzero(counts)[0]
+    used = used[np.argsort(first[used], kind="stable")]
+    lens = ragged_item_lens(seed, used.astype(np.uint64), Lmin, Lmax)
+    W = ((lens.astype(np.int64) + 31) // 32)
+    woff = np.concatenate([[0], np.cumsum(W)])
+    words = np.zeros(int(woff[-1]), dtype=np.uint64)
+    for w in range(int(W.max()) if len(W) else 0):
+        sel = np.nonzero(W > w)[0]
+        with np.errstate(over="ignore"):
+            r = splitmix64_np(np.uint64(seed) + np.uint64(32) * used[sel].astype(np.uint64) + np.uint64(w))
+        nb = np.minimum(32, lens[sel].astype(np.int64) - 32 * w)
+        mask = np.where(nb >= 32, np.uint64(0xFFFFFFFFFFFFFFFF),
+                        (np.uint64(1) << (np.uint64(2) * nb.astype(np.uint64))) - np.uint64(1))
+        words[woff[sel] + w] = r & mask
+    # items of equal content (short lengths repeat: 4^L distinct reads) are one key: merged into the
+    # row of their first occurrence (rows are already in first-occurrence order)
+    cnt = counts[used].copy()
+    keep = np.ones(len(used), dtype=bool)
+    seen = {}
+    wl = words.tolist()
+    for k in range(len(used)):
+        key = (int(lens[k]),) + tuple(wl[woff[k]:woff[k + 1]])
+        j = seen.get(key)
+        if j is None:
+            seen[key] = k
+        else:
+            cnt[j] += cnt[k]
+            keep[k] = False
+    if keep.all():
+        return lens, cnt, words
+    wkeep = np.repeat(keep, W)
+    return lens[keep], cnt[keep], words[wkeep]
+
+
+def rows_digest(lens: np.ndarray, counts: np.ndarray, words: np.ndarray) -> str:
+    """SHA-256 of the counter rows in order: per row the uint64s [length, count, words...] (the
+    ss_ingest_results layout: ceil(L / 32) words per row)."""
+    import hashlib
+    lens = np.asarray(lens, np.uint64)
+    W = (lens.astype(np.int64) + 31) // 32          # ceil(L / 32) words per row (none for L = 0)
+    rl = 2 + W
+    off = np.concatenate([[0], np.cumsum(rl)])
+    flat = np.zeros(int(off[-1]), dtype=np.uint64)
+    flat[off[:-1]] = lens
+    flat[off[:-1] + 1] = np.asarray(counts, np.uint64)
+    woff = np.concatenate([[0], np.cumsum(W)])
+    src = np.asarray(words, np.uint64)
+    for w in range(int(W.max()) if len(W) else 0):
+        sel = np.nonzero(W > w)[0]
+        flat[off[sel] + 2 + w] = src[woff[sel] + w]
+    return hashlib.sha256(flat.tobytes()).hexdigest()
+
+
 def table_digest(keys: np.ndarray, counts: np.ndarray, first: np.ndarray) -> str:
     """SHA-256 of the (key, count, first) rows sorted by key (all uint64)."""
     import hashlib

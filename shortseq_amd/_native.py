@@ -69,6 +69,8 @@ SIGNATURES = [
     ("ss_synth_reads", C.c_int, [_P, _U64, _U64, _U64, _U32, _U64, _P]),
     ("ss_synth_pool_reads", C.c_int, [_P, _U64, _U64, _U64, _U64, _U64, _U32, _U64, _P]),
     ("ss_synth_zipf_reads", C.c_int, [_P, _U64, _U64, _P, _U64, _U64, _U64, _U32, _U64, _P]),
+    ("ss_synth_ragged_lens", C.c_int, [_P, _U64, _U64, _U64, _U64, _U64, C.c_uint32, C.c_uint32, _P]),
+    ("ss_synth_ragged_reads", C.c_int, [_P, _P, _U64, _U64, _U64, _U64, _U64, C.c_uint32, C.c_uint32, _P]),
     ("ss_slice_fixed", C.c_int, [_P, _U64, _U32, _U32, _U32, _U32, _P, _U32, _P]),
     ("ss_slice_var", C.c_int, [_P, _U64, _U32, _P, _P, _P, _P, _U32, _P]),
     ("ss_hamming_all_pairs", C.c_int, [_P, _U64, _U32, _U32, _U32, _P, _P, _U64, _P, _P]),

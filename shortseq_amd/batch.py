@@ -421,6 +421,80 @@ def synth_zipf_reads(n: int, L: int, seed: int, pool_seed: int, cdf, *, i0: int 
     return out
 
 
+def synth_ragged_pool_reads(n: int, seed: int, pool_seed: int, U: int, Lmin: int, Lmax: int, *, i0: int = 0,
+                            device=None):
+    """Device-side ragged reads drawn from a pool of U items of lengths Lmin..Lmax (the
+    ss_synth_ragged_* rule, include/shortseq_amd.h): returns (blob u8 [total + 16], offsets i64 [n],
+    lens i32 [n]) with the reads back to back."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    s = _stream(dev)
+    check(lib().ss_synth_ragged_lens(lens.data_ptr(), seed, pool_seed, U, i0, n, Lmin, Lmax, s), "ss_synth_ragged_lens")
+    offs = torch.cumsum(lens, 0, dtype=torch.int64) - lens.to(torch.int64)   # layout only (exclusive prefix)
+    total = int(offs[-1].item() + lens[-1].item()) if n else 0
+    blob = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    check(lib().ss_synth_ragged_reads(blob.data_ptr(), offs.data_ptr(), seed, pool_seed, U, i0, n, Lmin, Lmax, s),
+          "ss_synth_ragged_reads")
+    return blob, offs, lens
+
+
+class DeviceIngest:
+    """The drop-in counter's engine (ss_ingest_*) fed from device memory: count(blob, offsets, lens)
+    any number of times (global read indices continue), then results() -> (lens u32, counts u64,
+    words u64) numpy arrays in first-occurrence order (the ShortSeqCounter dict order: row k has
+    ceil(lens[k] / 32) words, one for lengths 0..32).  A rejected read raises like ShortSeqCounter."""
+
+    def __init__(self, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        h = C.c_void_p()
+        check(lib().ss_ingest_create(dev.index or 0, C.byref(h)), "ss_ingest_create")
+        self._h = h
+
+    def count(self, blob: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor) -> None:
+        for t, name in ((blob, "blob"), (offsets, "offsets"), (lens, "lens")):
+            _require_cuda(t, name)
+        if offsets.dtype != torch.int64 or lens.dtype not in (torch.int32, torch.uint32) or blob.dtype != torch.uint8:
+            raise TypeError("blob u8, offsets int64, lens int32")
+        torch.cuda.current_stream(self.device).synchronize()   # the engine runs on its own stream
+        check(lib().ss_ingest_add_device(self._h, blob.data_ptr(), blob.numel(), offsets.data_ptr(), lens.data_ptr(),
+                                         lens.numel()), "ss_ingest_add_device")
+        idx, kind, ln = C.c_uint64(), C.c_int(), C.c_uint64()
+        check(lib().ss_ingest_error(self._h, C.byref(idx), C.byref(kind), None, 0, C.byref(ln)), "ss_ingest_error")
+        if idx.value != (1 << 64) - 1:
+            if kind.value == 2:
+                raise Exception("Sequences longer than 1024 bases are not supported.")
+            buf = (C.c_uint8 * max(1, ln.value))()
+            check(lib().ss_ingest_error(self._h, C.byref(idx), C.byref(kind), buf, ln.value, C.byref(ln)),
+                  "ss_ingest_error")
+            raise_read_error(bytes(buf)[:ln.value], idx.value)
+
+    def results(self):
+        K, NW = C.c_uint64(), C.c_uint64()
+        check(lib().ss_ingest_finish(self._h, C.byref(K), C.byref(NW)), "ss_ingest_finish")
+        pl, pc, pw = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        check(lib().ss_ingest_results(self._h, C.byref(pl), C.byref(pc), C.byref(pw)), "ss_ingest_results")
+        k, nw = K.value, NW.value
+        lens = np.ctypeslib.as_array((C.c_uint32 * max(1, k)).from_address(pl.value))[:k].copy() if k else np.zeros(0, np.uint32)
+        cnts = np.ctypeslib.as_array((C.c_uint64 * max(1, k)).from_address(pc.value))[:k].copy() if k else np.zeros(0, np.uint64)
+        wds = np.ctypeslib.as_array((C.c_uint64 * max(1, nw)).from_address(pw.value))[:nw].copy() if nw else np.zeros(0, np.uint64)
+        return lens, cnts, wds
+
+    def reset(self) -> None:
+        check(lib().ss_ingest_reset(self._h), "ss_ingest_reset")
+
+    def close(self) -> None:
+        if self._h:
+            lib().ss_ingest_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 def slice_fixed(words: torch.Tensor, L: int, start: Optional[int] = None, stop: Optional[int] = None,
                 *, out: Optional[torch.Tensor] = None):
     """reads[start:stop] for every read of a fixed-length packed batch (Python slice bounds, step 1,

@@ -647,6 +647,44 @@ __global__ __launch_bounds__(kThreads) void k_synth(uint8_t* out, uint64_t seed,
     }
 }
 
+// Ragged pool reads (the f2 workload): read i draws pool item
+// p = splitmix64(pool_seed ^ i * 0xD1B54A32D192ED03) % U (the uniform pool draw of k_synth<1>); item
+// p has length Lmin + splitmix64(seed ^ kLenSalt ^ p) % (Lmax - Lmin + 1) and word w
+// splitmix64(seed + 32 p + w), masked to its nucleotides.  Mirrored by oracle.ragged_pool_*.
+constexpr uint64_t kLenSalt = 0x6A09E667F3BCC909ull;
+
+__device__ __forceinline__ uint64_t ragged_item(uint64_t pool_seed, uint64_t i, uint64_t U) {
+    return splitmix64(pool_seed ^ (i * 0xD1B54A32D192ED03ull)) % U;
+}
+
+__device__ __forceinline__ uint32_t ragged_len(uint64_t seed, uint64_t p, uint32_t Lmin, uint32_t span) {
+    return Lmin + (uint32_t)(splitmix64(seed ^ kLenSalt ^ p) % span);
+}
+
+__global__ __launch_bounds__(kThreads) void k_synth_ragged_lens(uint32_t* __restrict__ lens, uint64_t seed,
+                                                                uint64_t pool_seed, uint64_t U, uint64_t i0,
+                                                                uint64_t n, uint32_t Lmin, uint32_t span) {
+    for (uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kThreads)
+        lens[k] = ragged_len(seed, ragged_item(pool_seed, i0 + k, U), Lmin, span);
+}
+
+// one lane per (read, 32-nt word slot); slots past a read's length idle
+__global__ __launch_bounds__(kThreads) void k_synth_ragged(uint8_t* __restrict__ out, const uint64_t* __restrict__ offs,
+                                                           uint64_t seed, uint64_t pool_seed, uint64_t U, uint64_t i0,
+                                                           uint64_t n, uint32_t Lmin, uint32_t span, uint32_t wmax) {
+    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < n * wmax; g += (uint64_t)gridDim.x * kThreads) {
+        const uint64_t k = g / wmax;
+        const uint32_t w = (uint32_t)(g - k * wmax);
+        const uint64_t p = ragged_item(pool_seed, i0 + k, U);
+        const uint32_t L = ragged_len(seed, p, Lmin, span);
+        if (32u * w >= L) continue;
+        const uint32_t nb = min(32u, L - 32u * w);
+        uint64_t r = splitmix64(seed + 32ull * p + w);
+        if (nb < 32u) r &= (1ull << (2 * nb)) - 1ull;
+        store_chars(out + offs[k] + 32u * w, r, nb);
+    }
+}
+
 inline unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap = 0) {
     uint64_t b = (items + per_block - 1) / per_block;
     if (b == 0) b = 1;
@@ -968,6 +1006,27 @@ int ss_synth_pool_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, uin
     hipLaunchKernelGGL((k_synth<1>), dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_ascii, seed,
                        pool_seed, U, i0, n, L, stride, (const uint64_t*)nullptr);
     return ss_check(hipGetLastError(), "k_synth<pool>");
+}
+
+int ss_synth_ragged_lens(uint32_t* d_lens, uint64_t seed, uint64_t pool_seed, uint64_t U, uint64_t i0, uint64_t n,
+                         uint32_t Lmin, uint32_t Lmax, void* stream) {
+    if (Lmin > Lmax || Lmax > SS_MAX_NT || U == 0) return ss_fail(SS_EARG, "bad Lmin/Lmax/U");
+    if (n == 0) return SS_OK;
+    if (!d_lens) return ss_fail(SS_EARG, "null buffer");
+    hipLaunchKernelGGL(k_synth_ragged_lens, dim3(grid_for(n, kThreads, kGenGridCap)), dim3(kThreads), 0,
+                       (hipStream_t)stream, d_lens, seed, pool_seed, U, i0, n, Lmin, Lmax - Lmin + 1);
+    return ss_check(hipGetLastError(), "k_synth_ragged_lens");
+}
+
+int ss_synth_ragged_reads(uint8_t* d_blob, const uint64_t* d_offsets, uint64_t seed, uint64_t pool_seed, uint64_t U,
+                          uint64_t i0, uint64_t n, uint32_t Lmin, uint32_t Lmax, void* stream) {
+    if (Lmin > Lmax || Lmax > SS_MAX_NT || U == 0) return ss_fail(SS_EARG, "bad Lmin/Lmax/U");
+    if (n == 0) return SS_OK;
+    if (!d_blob || !d_offsets) return ss_fail(SS_EARG, "null buffer");
+    const uint32_t wmax = words_for(Lmax ? Lmax : 1);
+    hipLaunchKernelGGL(k_synth_ragged, dim3(grid_for(n * wmax, kThreads, kGenGridCap)), dim3(kThreads), 0,
+                       (hipStream_t)stream, d_blob, d_offsets, seed, pool_seed, U, i0, n, Lmin, Lmax - Lmin + 1, wmax);
+    return ss_check(hipGetLastError(), "k_synth_ragged");
 }
 
 int ss_synth_zipf_reads(uint8_t* d_ascii, uint64_t seed, uint64_t pool_seed, const uint64_t* d_cdf, uint64_t U,

@@ -37,15 +37,9 @@ constexpr int kThreads = 256;
 constexpr uint32_t kMaxParts = 64;         // owners (GPUs) a table can be partitioned for
 constexpr uint32_t kExtractBlocks = 4096;  // extract passes: fixed grid, contiguous slot ranges
 constexpr uint32_t kExtractT = 64;         // ONE wave per extract block: slot order is output order
-#ifndef SS_SLICE_LOG_MAX
-#define SS_SLICE_LOG_MAX 11
-#endif
-constexpr uint32_t kSliceLogMax = SS_SLICE_LOG_MAX;   // region slice: 2048 slots (one LDS-resident aggregation)
+constexpr uint32_t kSliceLogMax = 11;                 // region slice: 2048 slots (one LDS-resident aggregation)
 constexpr uint32_t kMwSliceLog = 11;                  // multi-word tables: the k_mw_aggregate LDS bound
-#ifndef SS_PC_BLOCKS
-#define SS_PC_BLOCKS 1024
-#endif
-constexpr uint32_t kPartBlocks = SS_PC_BLOCKS;  // partition passes: fixed grid, contiguous read ranges
+constexpr uint32_t kPartBlocks = 1024;      // partition passes: fixed grid, contiguous read ranges
 constexpr uint32_t kMaxRegions = 32768;    // per-block region histogram in LDS (128 KB)
 }  // namespace
 
@@ -433,40 +427,26 @@ constexpr uint32_t kCoarseBits = 7;    // 128 coarse bins for the first partitio
 // in coarse order, bcnt in region order).  Batch-local indices are < 2^31 (ss_counter_reserve).
 constexpr uint32_t kWeighted = 0x80000000u;
 
-// Fine-scatter output record: key and read index in one 12-B dwordx3 (SS_FS_AOS 1).  Against two
-// streams (u64 keys + u32 indices): the scatter 2.54 -> 2.21-2.37 ms at its end, the insert -0.01 to
-// -0.14 ms uniform 2^24 over 3 same-box rounds (the aggregate's dwordx3 loads give part of it back);
-// a 16-B record with the count inside measured no better (scripts/ab_counter.sh, gpurun_out/ab).
+// Partition record: key and read index in one 12-B dwordx3, for the coarse and the fine records
+// (the region bytes and the sparse counts stay apart).  Against two streams (u64 keys + u32
+// indices): the scatter 2.54 -> 2.21-2.37 ms at its end, the insert -0.01 to -0.14 ms uniform 2^24
+// over 3 same-box rounds; a 16-B record with the count inside measured no better.
 struct __attribute__((packed, aligned(4))) Rec12 {
     uint32_t klo, khi, idx;
 };
-#ifndef SS_FS_AOS
-#define SS_FS_AOS 1
-#endif
-// fine-pass slabs instead of counted cursors (ss_counter_reserve decides per reservation)
-#ifndef SS_PF_SLABS
-#define SS_PF_SLABS 1
-#endif
+// fine-pass slabs instead of counted cursors (ss_counter_reserve decides per reservation): a slab
+// holds 2 x its region's mean share of the sub-bin + kSlabPad records, rounded up to 16
 constexpr uint64_t kSlabMinMean = 256;
-#ifndef SS_SLAB_MUL
-#define SS_SLAB_MUL 4   // a slab holds SS_SLAB_MUL / 2 x its region's mean share of the sub-bin ...
-#endif
-#ifndef SS_SLAB_PAD
-#define SS_SLAB_PAD 256 // ... + SS_SLAB_PAD records, rounded up to 16
-#endif
+constexpr uint32_t kSlabPad = 256;
 // slab size of a sub-bin holding f coarse records over nb regions.  The fine scatter's heavy-region
 // dedup keeps a region at <= 2 x the mean records per tile unless it holds that many distinct keys,
 // so 2 x (f / nb) + a partial tile's slack is overrun only by crafted inputs (those spill).
 __host__ __device__ __forceinline__ uint32_t slab_size(uint32_t f, uint32_t nb) {
-    return ((SS_SLAB_MUL * ((f + nb - 1) / nb)) / 2 + SS_SLAB_PAD + 15) & ~15u;
+    return (2 * ((f + nb - 1) / nb) + kSlabPad + 15) & ~15u;
 }
-// coarse records as the same 12-B {key, read index} (areg and the sparse counts stay apart)
-#ifndef SS_PF_AOS
-#define SS_PF_AOS 1
-#endif
 
 struct PartWs {
-    const Rec12* brec; // optimistic path with SS_FS_AOS: the region-ordered records (else null)
+    const Rec12* brec; // optimistic path: the region-ordered records (else null)
     uint32_t slab;     // optimistic path: 1 = fine records of (sub-bin f, region j) live in slab
                        // [slabs[f] + j slabs[kNFill + f], + slabs[kNFill + f]) (no count pass);
                        // 0 = counted cursors (hist)
@@ -685,10 +665,7 @@ __global__ __launch_bounds__(1024) void k_pc_offsets(PartWs w, uint32_t bins, co
 // the regions of the (1-2) coarse buckets the block's range spans (range-sorted input), mapped to
 // local bins region - lo_region; a block spanning more than kMaxLocalBins falls back to direct
 // (unstaged) stores through the same cursors.
-#ifndef SS_PC_TILE
-#define SS_PC_TILE 4096     // elements per LDS-staged scatter tile (tools/tune_counter.hip sweeps it)
-#endif
-constexpr uint32_t kTile = SS_PC_TILE;
+constexpr uint32_t kTile = 4096;      // elements per LDS-staged scatter tile
 constexpr uint32_t kMaxLocalBins = 1024;
 
 // exclusive scan of data[0..n) (n <= 1024) by a 512-thread block; returns the total
@@ -852,24 +829,15 @@ __global__ __launch_bounds__(512) void k_pc_scatter_lds(Tbl t, PartWs w, uint32_
 // regions, so the histogram and the LDS staging use that window.
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kCB = 1u << kCoarseBits;          // 128 coarse bins
-// The fill counters take one atomicAdd per (4096-read tile, bin), ~3.9M device-scope atomics per
-// 125M reads.  kFillStride spaces them (u32 units); 64 and 1024 (128 counters) and 32 (8 x 128)
-// measured no different from 1 (tools/tune_counter.hip, scripts/ab_counter.sh): they stay packed.
-#ifndef SS_FILL_STRIDE
-#define SS_FILL_STRIDE 1
-#endif
-constexpr uint32_t kFillStride = SS_FILL_STRIDE;
-#ifndef SS_FINE_PER_BIN
-#define SS_FINE_PER_BIN 8
-#endif
-constexpr uint32_t kFinePerBin = SS_FINE_PER_BIN;    // fine-pass blocks per coarse bin = sub-bins per bin
+// The fill counters take one atomicAdd per (4096-read tile, bin pair), ~2M device-scope atomics per
+// 125M reads; spacing them apart measured no different from packing them.
+constexpr uint32_t kFinePerBin = 8;                  // fine-pass blocks per coarse bin = sub-bins per bin
 constexpr uint32_t kNFill = kCB * kFinePerBin;       // sub-bin fill counters
 constexpr uint32_t kSpillCtr = kNFill;               // the spill list's record counter
-constexpr uint32_t kFillWords = (kNFill + 1) * kFillStride;   // counters + the spill counter
+constexpr uint32_t kFillWords = kNFill + 1;          // counters + the spill counter
 // Sub-bins (2p, s) and (2p + 1, s) of a coarse bin pair share one 64-bit word (low / high half), so
 // the coarse pass reserves both bins a wave-0 lane scans with ONE 64-bit atomic (a sub-bin's fill
 // stays below 2^31: no carry into the high half).  fb = bin * kFinePerBin + sub.
-static_assert(kFillStride == 1, "paired fill counters");
 __host__ __device__ __forceinline__ uint32_t fill_at(uint32_t fb) {
     const uint32_t bin = fb / kFinePerBin, sub = fb % kFinePerBin;
     return (((bin >> 1) * kFinePerBin + sub) << 1) | (bin & 1u);
@@ -877,54 +845,11 @@ __host__ __device__ __forceinline__ uint32_t fill_at(uint32_t fb) {
 // k_pf_coarse shape: 512 threads x 8 reads per 4096-read tile, capped at 128 VGPRs (4 waves per
 // SIMD: two 72-KB-LDS blocks per CU, 16 waves).  Against 256 x 16 at 230 VGPRs (8 waves per CU):
 // coarse 1.30 -> 1.19 ms uniform, 1.87 -> 1.40 ms Zipf 1.1 (its dedup phases are latency-bound);
-// insert medians 2.87 -> 2.83 / 3.28 -> 2.80 ms (scripts/ab_many.sh).  1024 x 4: 1.38 / 1.86 ms.
-#ifndef SS_PF_RPL
-#define SS_PF_RPL 8
-#endif
-#ifndef SS_PF_T
-#define SS_PF_T 512
-#endif
-#ifndef SS_PF_HEAVY
-#define SS_PF_HEAVY 64   // reads of one bin in one tile above which the bin is deduplicated (2x the mean)
-#endif
-constexpr uint32_t kPfT = SS_PF_T, kPfRPL = SS_PF_RPL;   // k_pf_coarse: kPfT * kPfRPL-read tiles
-constexpr uint32_t kHeavy = SS_PF_HEAVY;
-#ifndef SS_PF_DET
-#define SS_PF_DET 0
-#endif
-// measurement only (results invalid when not 7): which record streams the coarse / fine write-outs
-// store, bit 0 keys, bit 1 region bytes (coarse) / counts (fine), bit 2 read indices
-#ifndef SS_PF_WRITE
-#define SS_PF_WRITE 7
-#endif
-#ifndef SS_FS_WRITE
-#define SS_FS_WRITE 7
-#endif
-#ifndef SS_PF_STOP
-#define SS_PF_STOP 0
-#endif
-// k_pf_coarse: issue the next tile's loads right after this tile's encode (1), after the tile's
-// reservation barrier (2), or at the top of each tile (0)
-#ifndef SS_PF_NOSBIN
-#define SS_PF_NOSBIN 0   // 1: no staged bin byte per element (recomputed from the key; dead = read index ~0):
-                         // same box uniform 2.510 -> 2.513, Zipf 2.598 -> 2.683 ms (profiles/r2/r2f/ab_nosbin.log), off
-#endif
-#ifndef SS_PF_LATE
-#define SS_PF_LATE 0   // 1: wave 0 consumes the coarse reservation after its staging writes (same-box
-                       // medians uniform 2.536 -> 2.587, Zipf 2.605 -> 2.567 ms: within the spread, off)
-#endif
-#ifndef SS_PF_PREFETCH
-#define SS_PF_PREFETCH 0
-#endif
-// nontemporal loads of the record streams read exactly once (fine count / scatter, aggregate)
-#ifndef SS_NT_LOADS
-#define SS_NT_LOADS 0
-#endif
-template <typename V>
-__device__ __forceinline__ V ld_once(const V* p) {
-    if constexpr (SS_NT_LOADS != 0) return __builtin_nontemporal_load(p);
-    else return *p;
-}
+// insert medians 2.87 -> 2.83 / 3.28 -> 2.80 ms.  1024 x 4: 1.38 / 1.86 ms.  Measured and not kept
+// (DESIGN.md §4): the next tile's loads issued early, the reservation consumed after staging, the
+// bin recomputed instead of staged, nontemporal record loads.
+constexpr uint32_t kPfT = 512, kPfRPL = 8;   // k_pf_coarse: kPfT * kPfRPL-read tiles
+constexpr uint32_t kHeavy = 64;              // reads of one bin in one tile above which the bin is deduplicated (2x the mean)
 
 // sub-bin capacity of the optimistic partition for a batch of n reads (host and device agree)
 __host__ __device__ __forceinline__ uint64_t pf_cap1(uint64_t n) {
@@ -979,23 +904,12 @@ __device__ __forceinline__ void wave_fold(bool& act, uint64_t key, uint32_t& cnt
     }
 }
 
-// wave_fold peels in the coarse dedup, the fine dedup and the aggregate (0 = off).  Same-box A/B
-// (tools/tune_counter.hip, 125M reads, 3 rounds): coarse 2 peels Zipf 3.67 -> 3.83 ms, fine 2 peels
-// no change, aggregate 2 peels 3.59 -> 3.67 ms Zipf and +0.03 ms uniform (the fine dedup already
-// bounds a region's copies of one key to ~1 per tile), so all were off.  With the 512 x 8 coarse
-// tiles one coarse peel pays (below); a fine peel still costs (Zipf scatter 0.90 -> 1.22 ms).
-#ifndef SS_COARSE_FOLD
-#define SS_COARSE_FOLD 1   // 512 x 8 coarse tiles: 1 peel, Zipf coarse 1.40 -> 1.35 ms (2 peels: no better)
-#endif
-#ifndef SS_SPILL_FOLD
-#define SS_SPILL_FOLD 8   // Zipf 1.1 over 2^24: 278k spilled records, insert 0.30 -> 0.12 (4 peels) -> 0.09 ms (8)
-#endif
-#ifndef SS_FINE_FOLD
-#define SS_FINE_FOLD 0
-#endif
-#ifndef SS_AGG_FOLD
-#define SS_AGG_FOLD 0
-#endif
+// wave_fold peels in the coarse dedup and the spill insert.  Same-box A/B (125M reads, 3 rounds):
+// a fine-dedup peel costs (Zipf scatter 0.90 -> 1.22 ms), aggregate peels cost (Zipf 3.59 -> 3.67 ms,
+// uniform +0.03 ms: the fine dedup already bounds a region's copies of one key to ~1 per tile), so
+// those have none.
+constexpr int kCoarseFold = 1;   // 512 x 8 coarse tiles: 1 peel, Zipf coarse 1.40 -> 1.35 ms (2 peels: no better)
+constexpr int kSpillFold = 8;    // Zipf 1.1 over 2^24: 278k spilled records, insert 0.30 -> 0.12 (4 peels) -> 0.09 ms (8)
 
 // LDS dedup table of one tile: entry = (staged element + 1) | count << 16, 0 = free
 __device__ __forceinline__ uint32_t dedup_home(uint64_t key, uint32_t log2n) {
@@ -1003,12 +917,9 @@ __device__ __forceinline__ uint32_t dedup_home(uint64_t key, uint32_t log2n) {
 }
 
 template <int T, int RPL>
-#ifndef SS_PF_WPE
-#define SS_PF_WPE 4     // amdgpu_waves_per_eu floor of k_pf_coarse (see SS_PF_T)
-#endif
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) void k_pf_coarse(Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16,
-                                                 uint64_t n, uint32_t cpr, uint64_t cap1, uint32_t* fill,
-                                                 unsigned long long* first_bad) {
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_coarse(
+        Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16, uint64_t n, uint32_t cpr, uint64_t cap1,
+        uint32_t* fill, unsigned long long* first_bad) {
     constexpr uint32_t TILE = T * RPL;
     constexpr uint32_t kHtLog = TILE == 4096 ? 12 : TILE == 2048 ? 11 : 13;
     static_assert((1u << kHtLog) == TILE, "tile must be 2048, 4096 or 8192 reads");
@@ -1017,9 +928,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
     __shared__ uint32_t any_heavy;
     __shared__ uint64_t skey[TILE];
     __shared__ uint32_t sidx[TILE];
-    __shared__ uint8_t sbin[SS_PF_NOSBIN ? 1 : TILE];
+    __shared__ uint8_t sbin[TILE];
     __shared__ uint32_t ht[TILE];
-    constexpr uint32_t kDeadIdx = 0xFFFFFFFFu;   // SS_PF_NOSBIN: a folded element's read index
     uint32_t* spill_ctr = fill + fill_at(kSpillCtr);
     const uint32_t shift = w.rbits - kCoarseBits;
     const uint64_t tiles = (n + TILE - 1) / TILE;
@@ -1038,19 +948,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
     };
     // wave 0 lane, bins b0 = 2 lane and b0 + 1: reserve c0 / c1 slots of their sub-bins (b, sub) with
     // one 64-bit atomic on the pair's word (only the bins flagged in `mask`: bit 0 = b0, bit 1 =
-    // b0 + 1); the part past cap1 reserves spill records (a second atomic, rare)
-    auto reserve_issue = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) -> uint64_t {
+    // b0 + 1); the part past cap1 reserves spill records (a second atomic, rare).  Sets the bins'
+    // bases (gbase) and spill runs (sbase).
+    auto reserve = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) {
         const uint64_t add = ((mask & 1u) ? (uint64_t)c0 : 0ull) | ((mask & 2u) ? (uint64_t)c1 << 32 : 0ull);
-#if SS_PF_DET   // measurement only: tile-local positions, no reservation atomics (results invalid)
-        (void)add;
-        return 0;
-#else
-        return add ? atomicAdd((unsigned long long*)&fill[fill_at(b0 * kFinePerBin + sub)], (unsigned long long)add)
-                   : 0ull;
-#endif
-    };
-    // the reservation's bases (gbase) and spill runs (sbase) from the atomic's return value
-    auto reserve_finish = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask, uint64_t g2) {
+        const uint64_t g2 = add ? atomicAdd((unsigned long long*)&fill[fill_at(b0 * kFinePerBin + sub)],
+                                            (unsigned long long)add)
+                                : 0ull;
 #pragma unroll
         for (uint32_t k = 0; k < 2; ++k) {
             if (!(mask & (1u << k))) continue;
@@ -1060,9 +964,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             sbase[b0 + k] = end > from ? atomicAdd(spill_ctr, (uint32_t)(end - from)) : 0u;
         }
     };
-    auto reserve = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) {
-        reserve_finish(b0, c0, c1, mask, reserve_issue(b0, c0, c1, mask));
-    };
     static_assert(kCB == 128, "wave 0 scans two bins per lane");
     for (uint32_t i = threadIdx.x; i < kCB; i += T) lcount[i] = 0;
     __syncthreads();
@@ -1071,9 +972,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
     // LDS.  The next tile's rank atomics only touch lcount (zeroed before B) and its staging waits
     // for its own barrier B, which every wave reaches only after this tile's write-out.  A tile with
     // a heavy bin adds three: (D) deduplicated, (E) survivors counted, (F) heavy bins reserved.
-    if (SS_PF_PREFETCH && blockIdx.x < tiles) load_tile(blockIdx.x);
     for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        if (!SS_PF_PREFETCH) load_tile(tile);
+        load_tile(tile);
         uint64_t key[RPL];
         uint32_t bin[RPL], rank[RPL];
         const uint64_t t0 = tile * TILE;
@@ -1093,16 +993,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
                 rank[j] = atomicAdd(&lcount[bin[j]], 1u);
             }
         }
-        if (SS_PF_PREFETCH == 1 && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
         __syncthreads();                                                  // (A)
-        // wave 0: the reservation atomic of bins b0 = 2 lane, b0 + 1 (SS_PF_LATE: its return value is
-        // consumed after this wave's staging, so the round trip overlaps the staging phase)
-        uint32_t c0 = 0, c1 = 0, rmask = 0;
-        uint64_t g2 = 0;
-        if (threadIdx.x < 64) {
+        if (threadIdx.x < 64) {       // wave 0: scan, heavy flags, the reservation atomic of bins 2 lane, 2 lane + 1
             const uint32_t lane = threadIdx.x, b0 = 2 * lane;
-            c0 = lcount[b0];
-            c1 = lcount[b0 + 1];
+            const uint32_t c0 = lcount[b0], c1 = lcount[b0 + 1];
             uint32_t incl = c0 + c1;
             for (uint32_t off = 1; off < 64; off <<= 1) {
                 const uint32_t y = __shfl_up(incl, off);
@@ -1114,9 +1008,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             const bool h0 = c0 > kHeavy, h1 = c1 > kHeavy;
             hflag[b0] = h0;
             hflag[b0 + 1] = h1;
-            rmask = (h0 ? 0u : 1u) | (h1 ? 0u : 2u);
-            if (SS_PF_LATE) g2 = reserve_issue(b0, c0, c1, rmask);
-            else reserve(b0, c0, c1, rmask);
+            reserve(b0, c0, c1, (h0 ? 0u : 1u) | (h1 ? 0u : 2u));
             const uint64_t hv = __ballot(h0 || h1);
             if (lane == 0) any_heavy = hv != 0;
             lcount[b0] = 0;
@@ -1125,9 +1017,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             hcnt[b0 + 1] = 0;
         }
         __syncthreads();                                                  // (B)
-        // prefetch form 2: the next tile's loads go out after the reservation, so wave 0's wait for
-        // its atomics' return values (vmcnt counts in issue order) does not also wait for them
-        if (SS_PF_PREFETCH == 2 && tile + gridDim.x < tiles) load_tile(tile + gridDim.x);
         const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
@@ -1136,10 +1025,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
                 const uint32_t sp = lstart[bin[j]] + rank[j];
                 skey[sp] = key[j];
                 sidx[sp] = (uint32_t)(t0 + e);
-                if (!SS_PF_NOSBIN) sbin[sp] = (uint8_t)bin[j];
+                sbin[sp] = (uint8_t)bin[j];
             }
         }
-        if (SS_PF_LATE && threadIdx.x < 64) reserve_finish(2 * threadIdx.x, c0, c1, rmask, g2);
         if (heavy_tile)
             for (uint32_t i = threadIdx.x; i < TILE; i += T) ht[i] = 0;
         __syncthreads();                                                  // (C)
@@ -1150,21 +1038,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             // in registers first (one LDS atomic per wave instead of 64 on one address).
             for (uint32_t i0 = 0; i0 < cnt; i0 += T) {
                 const uint32_t i = i0 + threadIdx.x;
-#if SS_PF_NOSBIN
-                const uint64_t k0 = i < cnt ? skey[i] : 0ull;
-                bool act = i < cnt && hflag[region_of(t, k0) >> shift];
-                const uint64_t k = act ? k0 : 0ull;
-#else
                 bool act = i < cnt && hflag[sbin[i]];
                 const uint64_t k = act ? skey[i] : 0ull;
-#endif
                 uint32_t c = 1, mi = act ? sidx[i] : 0xFFFFFFFFu;
                 const bool was = act;
-                wave_fold<SS_COARSE_FOLD>(act, k, c, mi);
-                if (was && !act) {                                        // folded into its wave leader
-                    if (SS_PF_NOSBIN) sidx[i] = kDeadIdx;
-                    else sbin[i] = 0xFF;
-                }
+                wave_fold<kCoarseFold>(act, k, c, mi);
+                if (was && !act) sbin[i] = 0xFF;                          // folded into its wave leader
                 if (!act) continue;
                 sidx[i] = mi;
                 uint32_t h = dedup_home(k, kHtLog);
@@ -1178,8 +1057,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
                     if (skey[j] == k) {
                         atomicAdd(&ht[h], c << 16);
                         atomicMin(&sidx[j], mi);
-                        if (SS_PF_NOSBIN) sidx[i] = kDeadIdx;
-                        else sbin[i] = 0xFF;
+                        sbin[i] = 0xFF;
                         break;
                     }
                     h = (h + 1) & (TILE - 1);
@@ -1187,14 +1065,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             }
             __syncthreads();                                              // (D)
             for (uint32_t i = threadIdx.x; i < cnt; i += T) {
-#if SS_PF_NOSBIN
-                if (sidx[i] == kDeadIdx) continue;
-                const uint32_t b = region_of(t, skey[i]) >> shift;
-                if (hflag[b]) atomicAdd(&hcnt[b], 1u);
-#else
                 const uint32_t b = sbin[i];
                 if (b != 0xFF && hflag[b]) atomicAdd(&hcnt[b], 1u);
-#endif
             }
             __syncthreads();                                              // (E)
             if (threadIdx.x < 64) {
@@ -1206,13 +1078,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             __syncthreads();                                              // (F)
         }
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
-#if SS_PF_NOSBIN
-            if (sidx[i] == kDeadIdx) continue;                            // folded into its claimer
-            const uint32_t b = region_of(t, skey[i]) >> shift;
-#else
             const uint32_t b = sbin[i];
             if (b == 0xFF) continue;                                      // folded into its claimer
-#endif
             uint32_t local, c = 1;
             if (heavy_tile && hflag[b]) {
                 local = atomicAdd(&hcnt[b], 1u);
@@ -1225,29 +1092,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(SS_PF_WPE))) 
             const uint64_t pos = (uint64_t)gbase[b] + local;
             const uint64_t k = skey[i];
             if (pos < cap1) {
-#if SS_PF_DET
-                const uint64_t at = t0 + lstart[b] + local;
-#else
                 const uint64_t at = (uint64_t)(b * kFinePerBin + sub) * cap1 + pos;
-#endif
-                if constexpr (SS_PF_AOS != 0) {
-                    Rec12 r;
-                    r.klo = (uint32_t)k;
-                    r.khi = (uint32_t)(k >> 32);
-                    r.idx = c > 1 ? (sidx[i] | kWeighted) : sidx[i];
-                    ((Rec12*)w.akey)[at] = r;
-                    if (!w.slab) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
-                    if (c > 1) w.acnt[at] = c;
-                    continue;
-                }
-                if (SS_PF_WRITE & 1) w.akey[at] = k;
-                if ((SS_PF_WRITE & 2) && !w.slab) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
-                if (c > 1) {
-                    w.aidx[at] = sidx[i] | kWeighted;
-                    w.acnt[at] = c;
-                } else if (SS_PF_WRITE & 4) {
-                    w.aidx[at] = sidx[i];
-                }
+                Rec12 r;
+                r.klo = (uint32_t)k;
+                r.khi = (uint32_t)(k >> 32);
+                r.idx = c > 1 ? (sidx[i] | kWeighted) : sidx[i];
+                ((Rec12*)w.akey)[at] = r;
+                if (!w.slab) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
+                if (c > 1) w.acnt[at] = c;
             } else {
                 const uint64_t sp = (uint64_t)sbase[b] + (pos - max((uint64_t)gbase[b], cap1));
                 if (sp < w.spill_cap)
@@ -1267,11 +1119,6 @@ __device__ __forceinline__ void fine_range(uint32_t fb, const uint32_t* fill, ui
     hi = min((uint64_t)fill[fill_at(fb)], cap1);
 }
 
-// k_pf_count: add the first active lane's region for all lanes holding it with one atomic (Zipf
-// count 0.154 -> 0.116 ms, uniform 0.049 -> 0.100 ms: off)
-#ifndef SS_CNT_PEEL
-#define SS_CNT_PEEL 0
-#endif
 // fine histogram: block fb counts the regions of its slice of coarse bin fb / 8 -> hist[fb][rpb]
 template <int T>
 __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill) {
@@ -1299,23 +1146,8 @@ __global__ __launch_bounds__(T) void k_pf_count(Tbl t, PartWs w, uint64_t cap1, 
             const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
             for (uint32_t j = 0; j < 16; ++j) {
-                const bool valid = j < m;
                 const uint32_t r = (wd[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                if constexpr (SS_CNT_PEEL != 0) {
-                    // the lanes holding the first active lane's region add together: a hot region of
-                    // a skewed sub-bin costs one LDS atomic per wave instead of up to 64 on one word
-                    const uint32_t r0 = __builtin_amdgcn_readfirstlane(valid ? r : 0x100u);
-                    const bool same = valid && r == r0;
-                    const uint64_t mm = __ballot(same);
-                    if (same) {
-                        if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)mm) - 1))
-                            atomicAdd(&h[r0], (uint32_t)__popcll(mm));
-                    } else if (valid) {
-                        atomicAdd(&h[r], 1u);
-                    }
-                } else if (valid) {
-                    atomicAdd(&h[r], 1u);
-                }
+                if (j < m) atomicAdd(&h[r], 1u);
             }
         }
     }
@@ -1398,22 +1230,8 @@ __global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ f
 // (unweighted records only; each distinct key leaves as one record, weighted when repeated).  The
 // (sub-bin, region) segments then end before their reserved size; the end of each is written to
 // w.seg_end and the aggregate reads only the written part.
-#ifndef SS_HEAVY_FINE
-#define SS_HEAVY_FINE 2   // x the mean records per region per tile
-#endif
-#ifndef SS_FS_T
-#define SS_FS_T 512
-#endif
-#ifndef SS_FS_EARLY_WAIT
-#define SS_FS_EARLY_WAIT 1
-#endif
-#ifndef SS_FS_TILE
-#define SS_FS_TILE 4096
-#endif
-#ifndef SS_FS_W0SCAN
-#define SS_FS_W0SCAN 0   // 1: per-tile region scan by wave 0 alone (2 barriers instead of 5): measured slower,
-                         // scatter 0.72 -> 0.82 ms same box (profiles/r2/r2f/ab_w0.log)
-#endif
+constexpr uint32_t kHeavyFine = 2;    // x the mean records per region per tile
+constexpr uint32_t kFsT = 512, kFsTile = 4096;   // k_pf_scatter block and tile
 template <int T, uint32_t kTile>
 __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill,
                                                   const uint32_t* __restrict__ order) {
@@ -1432,16 +1250,13 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
     __shared__ uint32_t wsum[2 * (T / 64) + 1];
     __shared__ uint32_t any_heavy;
     const uint32_t nb = 1u << (w.rbits - kCoarseBits);
-    const uint32_t heavy_at = max(64u, SS_HEAVY_FINE * (kTile / nb));
+    const uint32_t heavy_at = max(64u, kHeavyFine * (kTile / nb));
     uint32_t bin;
     uint64_t lo, hi;
     const uint32_t fb = order[blockIdx.x];     // this block's sub-bin
     fine_range(fb, fill, cap1, bin, lo, hi);
     const uint32_t r0 = bin * nb;
-    const uint64_t* src = w.akey + (uint64_t)fb * cap1;
-    const Rec12* srec = (const Rec12*)w.akey + (uint64_t)fb * cap1;     // SS_PF_AOS layout
-    const uint32_t* src_idx = w.aidx + (uint64_t)fb * cap1;
-    auto rec_idx = [&](uint32_t p) -> uint32_t { return SS_PF_AOS ? srec[p].idx : src_idx[p]; };
+    const Rec12* srec = (const Rec12*)w.akey + (uint64_t)fb * cap1;
     const uint32_t* src_cnt = w.acnt + (uint64_t)fb * cap1;
     const uint32_t sbase = w.slab ? w.slabs[fb] : 0u, ssize = w.slab ? w.slabs[kNFill + fb] : 0u;
     for (uint32_t i = threadIdx.x; i < nb; i += T) {
@@ -1458,30 +1273,17 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
     auto load_tile = [&](uint64_t t0) {
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
-            const uint64_t at = min(t0 + j * T + threadIdx.x, hi - 1);
-            if constexpr (SS_PF_AOS != 0) {
-                const Rec12 r = srec[at];
-                nkey[j] = ((uint64_t)r.khi << 32) | r.klo;
-                nidx[j] = r.idx;
-            } else {
-                nkey[j] = ld_once(&src[at]);
-                nidx[j] = ld_once(&src_idx[at]);
-            }
+            const Rec12 r = srec[min(t0 + j * T + threadIdx.x, hi - 1)];
+            nkey[j] = ((uint64_t)r.khi << 32) | r.klo;
+            nidx[j] = r.idx;
         }
     };
     if (lo < hi) load_tile(lo);
-    if (SS_FS_W0SCAN) {   // the counters start zeroed; each tile's cursor step zeroes them for the next
+    for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
+        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
         for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
         if (threadIdx.x == 0) any_heavy = 0;
         __syncthreads();
-    }
-    for (uint64_t t0 = lo; t0 < hi; t0 += kTile) {
-        const uint32_t cnt = (uint32_t)min((uint64_t)kTile, hi - t0);
-        if (!SS_FS_W0SCAN) {
-            for (uint32_t i = threadIdx.x; i < nb; i += T) lcount[i] = 0;
-            if (threadIdx.x == 0) any_heavy = 0;
-            __syncthreads();
-        }
         uint64_t key[kTile / T];
         uint32_t idx[kTile / T], lb[kTile / T], rank[kTile / T];
 #pragma unroll
@@ -1501,47 +1303,13 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
             }
         }
         __syncthreads();
-        if (SS_FS_W0SCAN) {
-            // wave 0 alone: each lane scans E = nb / 64 consecutive regions (nb <= 256), flags the
-            // heavy ones and zeroes their dedup counters; one barrier publishes lstart / any_heavy
-            if (threadIdx.x < 64) {
-                const uint32_t lane = threadIdx.x;
-                const uint32_t E = nb >= 64 ? nb / 64 : 1u, i0 = lane * E;
-                uint32_t c[4], sum = 0;
-                bool heavy = false;
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    c[e] = (e < E && i0 + e < nb) ? lcount[i0 + e] : 0u;
-                    sum += c[e];
-                    heavy |= c[e] > heavy_at;
-                }
-                uint32_t incl = sum;
-                for (uint32_t off = 1; off < 64; off <<= 1) {
-                    const uint32_t y = __shfl_up(incl, off);
-                    if (lane >= off) incl += y;
-                }
-                uint32_t run = incl - sum;
-#pragma unroll
-                for (uint32_t e = 0; e < 4; ++e) {
-                    if (e < E && i0 + e < nb) {
-                        lstart[i0 + e] = run;
-                        hcnt[i0 + e] = 0;
-                        run += c[e];
-                    }
-                }
-                const uint64_t hv = __ballot(heavy);
-                if (lane == 0) any_heavy = hv != 0;
-            }
-            __syncthreads();
-        } else {
-            for (uint32_t i = threadIdx.x; i < nb; i += T) {
-                lstart[i] = lcount[i];
-                hcnt[i] = 0;
-                if (lcount[i] > heavy_at) any_heavy = 1;
-            }
-            __syncthreads();
-            block_scan<T>(lstart, nb, wsum);
+        for (uint32_t i = threadIdx.x; i < nb; i += T) {
+            lstart[i] = lcount[i];
+            hcnt[i] = 0;
+            if (lcount[i] > heavy_at) any_heavy = 1;
         }
+        __syncthreads();
+        block_scan<T>(lstart, nb, wsum);
         const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < (int)(kTile / T); ++j) {
@@ -1560,24 +1328,19 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
                 const uint32_t i = i0 + threadIdx.x;
                 const uint64_t k = i < cnt ? skey[i] : 0ull;
                 const uint32_t x = i < cnt ? sidx[i] : kWeighted;
-                bool act = i < cnt && lcount[region_of(t, k) - r0] > heavy_at && !(x & kWeighted);
-                uint32_t c = 1, mi = x;
-                const bool was = act;
-                wave_fold<SS_FINE_FOLD>(act, k, c, mi);
-                if (was && !act) sidx[i] = kDead;                         // folded into its wave leader
+                const bool act = i < cnt && lcount[region_of(t, k) - r0] > heavy_at && !(x & kWeighted);
                 if (!act) continue;
-                sidx[i] = mi;
                 uint32_t h = dedup_home(k, kHtLog);
                 for (;;) {
                     uint32_t e = ht[h];
                     if (e == 0) {
-                        e = atomicCAS(&ht[h], 0u, (i + 1) | (c << 16));
+                        e = atomicCAS(&ht[h], 0u, (i + 1) | (1u << 16));
                         if (e == 0) break;
                     }
                     const uint32_t j = (e & 0xFFFFu) - 1;
                     if (skey[j] == k) {
-                        atomicAdd(&ht[h], c << 16);
-                        atomicMin(&sidx[j], mi);
+                        atomicAdd(&ht[h], 1u << 16);
+                        atomicMin(&sidx[j], x);
                         sidx[i] = kDead;
                         break;
                     }
@@ -1596,10 +1359,8 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
         // Wait for the next tile's loads here, before this tile's record stores are issued: vmcnt
         // counts loads and stores in issue order, and with a data-dependent number of stores in
         // between, the wait at the next tile's first use would also drain this tile's stores
-        if (SS_FS_EARLY_WAIT) {
 #pragma unroll
-            for (int j = 0; j < (int)(kTile / T); ++j) asm volatile("" ::"v"(nkey[j]), "v"(nidx[j]));
-        }
+        for (int j = 0; j < (int)(kTile / T); ++j) asm volatile("" ::"v"(nkey[j]), "v"(nidx[j]));
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
             const uint64_t k = skey[i];
             const uint32_t x = sidx[i];
@@ -1616,59 +1377,35 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
             } else {
                 local = i - lstart[b];
             }
+            uint32_t xi = x;          // the read index (weighted flag kept) and the count
+            if (x & kWeighted) {
+                const uint32_t p = x & ~kWeighted;
+                xi = srec[p].idx;
+                c = src_cnt[p];
+            } else if (c > 1) {
+                xi = x | kWeighted;
+            }
             const uint32_t gpos = cursor[b] + local;
             if (w.slab && gpos >= sbase + (b + 1) * ssize) {
                 // the region's slab of this sub-bin is full: the record goes to the spill list
                 // (counted by k_spill_insert after the aggregate)
-                uint32_t xi = x, cc = c;
-                if (x & kWeighted) {
-                    const uint32_t p = x & ~kWeighted;
-                    xi = rec_idx(p);
-                    cc = src_cnt[p];
-                }
                 const uint64_t sp = atomicAdd(w.spill_ctr, 1u);
                 if (sp < w.spill_cap)
-                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), cc, xi & ~kWeighted);
+                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), c, xi & ~kWeighted);
                 else
                     atomicOr(t.overflow, kOvfTable);
                 continue;
             }
-            if constexpr (SS_FS_AOS != 0) {
-                uint32_t xi = x;
-                if (x & kWeighted) {
-                    const uint32_t p = x & ~kWeighted;
-                    xi = rec_idx(p);                // the read index, flag kept
-                    w.bcnt[gpos] = src_cnt[p];
-                } else if (c > 1) {
-                    xi = x | kWeighted;
-                    w.bcnt[gpos] = c;
-                }
-                Rec12 r;
-                r.klo = (uint32_t)k;
-                r.khi = (uint32_t)(k >> 32);
-                r.idx = xi;
-                if (SS_FS_WRITE & 1) ((Rec12*)w.keys)[gpos] = r;   // (measurement knob: 0 = no record writes)
-                continue;
-            }
-            if (SS_FS_WRITE & 1) w.keys[gpos] = k;
-            if (!(SS_FS_WRITE & 4)) continue;
-            if (x & kWeighted) {
-                const uint32_t p = x & ~kWeighted;
-                w.bidx[gpos] = rec_idx(p);          // the read index, flag kept
-                w.bcnt[gpos] = src_cnt[p];
-            } else if (c > 1) {
-                w.bidx[gpos] = x | kWeighted;
-                w.bcnt[gpos] = c;
-            } else {
-                w.bidx[gpos] = x;
-            }
+            if (c > 1) w.bcnt[gpos] = c;
+            Rec12 r;
+            r.klo = (uint32_t)k;
+            r.khi = (uint32_t)(k >> 32);
+            r.idx = xi;
+            ((Rec12*)w.keys)[gpos] = r;
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nb; i += T) {
+        for (uint32_t i = threadIdx.x; i < nb; i += T)
             cursor[i] += (heavy_tile && lcount[i] > heavy_at) ? hcnt[i] : lcount[i];
-            if (SS_FS_W0SCAN) lcount[i] = 0;                  // the next tile's counters
-        }
-        if (SS_FS_W0SCAN && threadIdx.x == 0) any_heavy = 0;  // read into heavy_tile before (B)
         __syncthreads();
     }
     for (uint32_t i = threadIdx.x; i < nb; i += T)
@@ -1689,19 +1426,14 @@ __global__ __launch_bounds__(256) void k_spill_insert(Tbl t, PartWs w, const uin
         // weighted record per coarse tile): fold a wave's copies before the global atomics
         bool act = i < m;
         uint32_t c = r.z, idx = r.w;
-        wave_fold<SS_SPILL_FOLD, true>(act, k, c, idx);
+        wave_fold<kSpillFold, true>(act, k, c, idx);
         if (act && tbl_add(t, k, c, base_index + idx) && t.occ && k != kEmpty) atomicAdd(&t.occ[region_of(t, k)], 1u);
     }
 }
 
 
-#ifndef SS_AGG_SLICE_T
-#define SS_AGG_SLICE_T 512
-#endif
-constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools/tune_counter.hip)
-#ifndef SS_AGG_P
-#define SS_AGG_P 4         // records per thread per aggregate step (loads in flight)
-#endif
+constexpr uint32_t kAggSliceT = 512;   // P4 threads per region (256 / 1024: slower)
+constexpr int kAggP = 4;               // records per thread per aggregate step (loads in flight)
 
 
 // P4, slice-direct form: the region's slice itself is the LDS hash table.  Keys are copied into LDS
@@ -1710,8 +1442,8 @@ constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools
 // then one LDS add and one LDS min.  The whole slice is written back coalesced (key, count, first
 // combined with the slot's old values; one dwordx4 per slot).  32 KB of LDS per workgroup.
 // Skewed regions: the fine scatter's dedup leaves at most ~one record per (tile, hot key), and
-// weighted records carry their counts (one LDS add of c); SS_AGG_FOLD > 0 would also fold lanes that
-// share a key before the LDS atomics (measured slower, see wave_fold).
+// weighted records carry their counts (one LDS add of c); folding lanes that share a key before the
+// LDS atomics measured slower (see wave_fold).
 // fresh: the table was reset and the reset is still pending (ss_counter_reset is lazy): the slice is
 // taken as empty instead of loaded, and written back whole (empty slots as the 0xFF reset pattern),
 // which replaces the table-sized reset memset and the slice read.
@@ -1720,9 +1452,7 @@ constexpr uint32_t kAggSliceT = SS_AGG_SLICE_T;  // P4 threads per region (tools
 // for a different key first moves the probe on past it) -- the same slot sequential linear probing
 // gives.  G slots are read per round (G independent LDS reads, one wait), so a wave's probe loop
 // runs ceil(longest probe / G) rounds instead of the longest probe.  Returns mask + 1 if full.
-#ifndef SS_AGG_PROBE
-#define SS_AGG_PROBE 2   // probe rounds of 1 / 2 / 4 / 8 slots: aggregate 0.72 / 0.58 / 0.60 / 0.63 ms (U 2^24)
-#endif
+constexpr int kAggProbe = 2;   // probe rounds of 1 / 2 / 4 / 8 slots: aggregate 0.72 / 0.58 / 0.60 / 0.63 ms (U 2^24)
 template <int G>
 __device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t mask, uint32_t off, uint64_t key) {
     const uint32_t S = mask + 1;
@@ -1757,12 +1487,8 @@ __device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t
     return S;
 }
 
-// SS_AGG_PERSIST: a grid of the resident blocks walks the regions (region += gridDim.x) instead of
-// one block per region
-#ifndef SS_AGG_PERSIST
-#define SS_AGG_PERSIST 0   // 1 measured slower: aggregate 0.63 -> 0.87 ms, insert 2.74 -> 2.91 ms (same box, both
-                           // builds with the loop's 80 VGPRs; profiles/r2/r2f/ab_apers.log)
-#endif
+// One block per region (a persistent grid walking the regions measured slower: aggregate 0.63 ->
+// 0.87 ms, the loop form costs 58 -> 80 VGPRs).
 template <int T, bool REC12>
 __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint64_t base_index, bool fresh = false) {
     const uint32_t S = (uint32_t)t.slice_mask + 1;
@@ -1771,12 +1497,7 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     uint32_t* bcnt = (uint32_t*)(skey + S);                   // [S] this batch's count
     uint32_t* bfst = bcnt + S;                                // [S] this batch's first read index
     __shared__ uint32_t sent[3];   // sentinel count, sentinel first, slice occupancy
-#if SS_AGG_PERSIST
-    for (uint32_t region = blockIdx.x; region < w.R; region += gridDim.x) {
-#else
-    {
-    const uint32_t region = blockIdx.x;   // (the loop form costs 58 -> 80 VGPRs even when it runs once)
-#endif
+    const uint32_t region = blockIdx.x;
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
     for (uint32_t i = threadIdx.x; i < S; i += T) {
         skey[i] = fresh ? kEmpty : t.slots[slice_base + i].key;
@@ -1789,7 +1510,7 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         sent[2] = 0;
     }
     __syncthreads();
-    constexpr int kP = SS_AGG_P;
+    constexpr int kP = kAggP;
     // the region's records: one range (exact paths) or its kFinePerBin fine-scatter segments,
     // walked as one flat index space (segment s covers flat [pre[s], pre[s + 1])) so every
     // iteration issues kP loads per thread whatever the segment lengths
@@ -1834,8 +1555,8 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
                 nkey[q] = ((uint64_t)r.khi << 32) | r.klo;
                 nidx[q] = r.idx;
             } else {
-                nkey[q] = ld_once(&w.bkey[nel[q]]);
-                nidx[q] = ld_once(&w.bidx[nel[q]]);
+                nkey[q] = w.bkey[nel[q]];
+                nidx[q] = w.bidx[nel[q]];
             }
         }
     };
@@ -1866,10 +1587,8 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
                 atomicAdd(&sent[0], c);
                 atomicMin(&sent[1], ix);
             }
-            bool act = valid && key[q] != kEmpty;
-            wave_fold<SS_AGG_FOLD>(act, key[q], c, ix);
-            if (!act) continue;
-            const uint32_t off = lds_probe<SS_AGG_PROBE>(skey, (uint32_t)t.slice_mask,
+            if (!valid || key[q] == kEmpty) continue;
+            const uint32_t off = lds_probe<kAggProbe>(skey, (uint32_t)t.slice_mask,
                                                           (uint32_t)(slot_top(t, key[q]) & t.slice_mask), key[q]);
             if (off == S) {
                 atomicOr(t.overflow, kOvfTable);
@@ -1904,8 +1623,6 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         Slot* ss = &t.slots[t.mask + 1];
         atomicAdd(&ss->ncount, 0u - sent[0]);
         atomicMin(&ss->first, (uint32_t)(base_index + sent[1]));
-    }
-    if (SS_AGG_PERSIST) __syncthreads();   // the next region re-initialises the LDS slice and sent[]
     }
 }
 
@@ -2007,7 +1724,7 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
             uint64_t key;
             unsigned long long c, f;
             recs.load(r0 + e, run, key, c, f);
-            const uint32_t off = lds_probe<SS_AGG_PROBE>(skey, (uint32_t)t.slice_mask,
+            const uint32_t off = lds_probe<kAggProbe>(skey, (uint32_t)t.slice_mask,
                                                           (uint32_t)(slot_top(t, key) & t.slice_mask), key);
             if (off == S) {
                 atomicOr(t.overflow, kOvfTable);
@@ -2549,26 +2266,27 @@ int ss_counter_reserve(ss_counter* c, uint64_t max_reads) {
     // slack would dominate small reservations) and the slots index in 32 bits.
     c->ws_slab = 0;
     c->ws_brecs = max_reads;
-    if (SS_PF_SLABS && R > (1u << kCoarseBits) && R <= (1u << (kCoarseBits + 8))) {
+    if (R > (1u << kCoarseBits) && R <= (1u << (kCoarseBits + 8))) {
         const uint64_t nslab = (uint64_t)kNFill * (R >> kCoarseBits);
         const uint64_t mean = max_reads / nslab;
         // sum over sub-bins of nb x slab_size(fill, nb), fills summing to <= max_reads
-        const uint64_t brecs = (SS_SLAB_MUL * max_reads) / 2 + nslab * (SS_SLAB_MUL / 2 + SS_SLAB_PAD + 15);
+        const uint64_t brecs = 2 * max_reads + nslab * (2 + kSlabPad + 15);
         if (mean >= kSlabMinMean && brecs < (1ull << 32)) {
             c->ws_slab = 1;
             c->ws_brecs = brecs > max_reads ? brecs : max_reads;
         }
     }
     const uint64_t brecs = c->ws_brecs;
-    hipError_t e = hipMalloc((void**)&c->ws_keys, brecs * (SS_FS_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * (SS_PF_AOS ? sizeof(Rec12) : sizeof(uint64_t)));
-    // coarse read indices live in the 12-B records with SS_PF_AOS (aidx then serves the exact paths)
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, (SS_PF_AOS ? max_reads : acap) * sizeof(uint32_t));
+    // ws_keys / ws_akey: 12-B records on the optimistic path, u64 keys on the exact paths
+    hipError_t e = hipMalloc((void**)&c->ws_keys, brecs * sizeof(Rec12));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_akey, acap * sizeof(Rec12));
+    // coarse read indices of the exact paths (the optimistic path keeps them in the 12-B records)
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_aidx, max_reads * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_acnt, acap * sizeof(uint32_t));
     if (e == hipSuccess && !c->ws_slab) e = hipMalloc((void**)&c->ws_areg, acap);   // counted cursors only
     if (e == hipSuccess && !c->ws_fill) e = hipMalloc((void**)&c->ws_fill, kFillWords * sizeof(uint32_t));
     c->ws_cap1 = cap1;
-    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, (SS_FS_AOS ? max_reads : brecs) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bidx, max_reads * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_bcnt, brecs * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&c->ws_spill, max_reads * sizeof(uint4));
     if (e == hipSuccess && !c->ws_hist) e = hipMalloc((void**)&c->ws_hist, (size_t)kPartBlocks * R * sizeof(uint32_t));
@@ -2691,13 +2409,10 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         const size_t mw_lds = (size_t)2 * S * 16 + (size_t)S * 8;
         const bool two_pass = w.rbits > kCoarseBits;             // > 64 regions: coarse pass first
         const uint32_t bins1 = two_pass ? (1u << kCoarseBits) : w.R;
-        #ifndef SS_PC_KEYS_U
-#define SS_PC_KEYS_U 2
-#endif
-        constexpr int T1 = 512, U1 = SS_PC_KEYS_U, TS = 512, TF = 512;
-        // dynamic LDS above the 64 KB default: opt in once per kernel (host-side attribute)
-        static bool attrs_set = false;
-        if (!attrs_set) {
+        constexpr int T1 = 512, U1 = 2, TS = 512, TF = 512;
+        // dynamic LDS above the 64 KB default: opt in once per kernel (host-side attribute; a
+        // function-local static is initialised once even with engines on several threads)
+        static const hipError_t attrs = [] {
             const int agg_max = (int)(2 * (1u << kMwSliceLog) * 16 + (1u << kMwSliceLog) * 8 + 8);
             hipError_t ea = hipFuncSetAttribute((const void*)k_pc_keys<T1, U1>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kMaxRegions * 4);
@@ -2710,15 +2425,9 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_mw_aggregate<kMwT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          agg_max);
-            if (ea == hipSuccess && kSliceLogMax > 11)
-                ea = hipFuncSetAttribute((const void*)k_pc_aggregate_slice<kAggSliceT, true>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (1u << kSliceLogMax) * 16);
-            if (ea == hipSuccess && kSliceLogMax > 11)
-                ea = hipFuncSetAttribute((const void*)k_pc_aggregate_slice<kAggSliceT, false>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (1u << kSliceLogMax) * 16);
-            if (ea != hipSuccess) return ss_check(ea, "hipFuncSetAttribute (dynamic LDS)");
-            attrs_set = true;
-        }
+            return ea;
+        }();
+        if (attrs != hipSuccess) return ss_check(attrs, "hipFuncSetAttribute (dynamic LDS)");
         auto scan = [&](uint32_t bins, uint32_t* start) {
             hipLaunchKernelGGL(k_pc_tot, dim3(bins), dim3(256), 0, s, w, bins);
             hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, bins, start);
@@ -2732,20 +2441,16 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             rc = ss_check(hipMemsetAsync(c->ws_fill, 0, kFillWords * sizeof(uint32_t), s), "fill reset");
             if (rc) return rc;
             // grid-stride over tiles: exactly the resident blocks (no second, partial round)
-            static int pf_grid = 0;
-            if (!pf_grid) {
+            static const int pf_grid = [] {
                 int dev = 0, cus = 0, per = 0;
                 (void)hipGetDevice(&dev);
                 (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
                 (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL>, kPfT, 0);
-                pf_grid = (cus > 0 && per > 0) ? cus * per : (int)kPartBlocks;
-            }
+                return (cus > 0 && per > 0) ? cus * per : (int)kPartBlocks;
+            }();
             hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
                                (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
                                (unsigned long long*)d_first_bad);
-            // SS_PF_STOP (measurement only, results invalid): 1 = end after the coarse pass, 2 = after
-            // the fine scatter
-            if (SS_PF_STOP == 1) return ss_check(hipGetLastError(), "coarse pass");
             const unsigned fine_blocks = kCB * kFinePerBin;
             if (!w.slab) {   // counted cursors: region histogram per sub-bin, then the scans
                 hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
@@ -2759,31 +2464,12 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             w.slabs = w.slab ? c->ws_order + kNFill : nullptr;
             hipLaunchKernelGGL(k_pf_order, dim3(1), dim3(512), 0, s, (const uint32_t*)c->ws_fill, cap1, c->ws_order,
                                1u << (w.rbits - kCoarseBits), w.slab ? c->ws_order + kNFill : nullptr);
-            hipLaunchKernelGGL((k_pf_scatter<SS_FS_T, SS_FS_TILE>), dim3(fine_blocks), dim3(SS_FS_T), 0, s, t, w, cap1,
+            hipLaunchKernelGGL((k_pf_scatter<kFsT, kFsTile>), dim3(fine_blocks), dim3(kFsT), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
-            if (SS_PF_STOP == 2) return ss_check(hipGetLastError(), "fine scatter");
             w.bkey = w.keys;
-            unsigned agg_grid = w.R;
-            if (SS_AGG_PERSIST) {
-                static int agg_res = 0;
-                if (!agg_res) {
-                    int dev = 0, cus = 0, per = 0;
-                    (void)hipGetDevice(&dev);
-                    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                        &per, (const void*)k_pc_aggregate_slice<kAggSliceT, true>, kAggSliceT, ((size_t)1 << kSliceLogMax) * 16);
-                    agg_res = (cus > 0 && per > 0) ? cus * per : 1024;
-                }
-                agg_grid = w.R < (unsigned)agg_res ? w.R : (unsigned)agg_res;
-            }
-            if (SS_FS_AOS) {
-                w.brec = (const Rec12*)w.keys;
-                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, true>), dim3(agg_grid), dim3(kAggSliceT),
-                                   ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
-            } else {
-                hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(agg_grid), dim3(kAggSliceT),
-                                   ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
-            }
+            w.brec = (const Rec12*)w.keys;
+            hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, true>), dim3(w.R), dim3(kAggSliceT),
+                               ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
             // records that found their sub-bin full (none unless many distinct keys pile into a bin)
             hipLaunchKernelGGL(k_spill_insert, dim3(1024), dim3(256), 0, s, t, w, (const uint32_t*)c->ws_fill,
                                base_index);

@@ -200,3 +200,24 @@ def test_stream_digest_construction(oracle, L, i0):
         ws, ds = g.digests(n, L, 1, chunk=700)
         assert ws == _sha(words)
         assert ds == _sha(oracle.hamming_ref_batch(words, n, L, words[0]))
+
+
+def test_ragged_pool_rows_match_oracle_count():
+    """The f2 ragged workload's generator-derived rows (oracle.ragged_pool_rows: items in first-draw
+    order, equal contents merged) equal oracle.count over the generated reads (pins
+    tests/golden/ragged_digests.json, tests/golden/gen_ragged_digests.py)."""
+    import oracle
+    for seed, ps, U, n, lo, hi in ((41, 42, 1 << 20, 20_000, 50, 150), (43, 44, 1 << 16, 30_000, 1, 300),
+                                   (45, 46, 400, 5_000, 0, 6)):
+        reads = oracle.ragged_pool_reads(seed, ps, U, 0, n, lo, hi)
+        assert all(lo <= len(r) <= hi for r in reads)
+        exp = oracle.count(reads)
+        lens, counts, words = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+        got, w = [], 0
+        for L, c in zip(lens.tolist(), counts.tolist()):
+            nw = (L + 31) // 32
+            ws = tuple(int(x) for x in words[w:w + nw]) or (0,)
+            w += nw
+            got.append((ws, L, c))
+        assert got == [(ws, L, c) for ws, L, c, _f in exp], (seed, n)
+        assert w == len(words)

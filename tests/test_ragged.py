@@ -1,0 +1,109 @@
+"""f2 — ragged, mixed-length reads (the _new class switch, short_seq.pyx:54-74, over
+a whole batch; counted per length as ShortSeqCounter does, counter.pyx:22-39).
+
+The reads come from the ss_synth_ragged_* generator (pool items of lengths Lmin..Lmax); its host
+restatement (oracle.ragged_pool_reads / ragged_pool_rows) is pinned to oracle.count in
+test_oracle_golden.py.  Checked on the GPU: the generator's bytes, ss_encode_var, and the drop-in
+engine fed from device memory (ss_ingest_add_device) against the oracle at small sizes and against
+the generator-derived digests at the bench's full size (50M reads of 50-150 nt).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _digests():
+    with open(os.path.join(HERE, "golden", "ragged_digests.json")) as f:
+        return json.load(f)
+
+
+def test_synth_ragged_matches_oracle(gpu, oracle):
+    import shortseq_amd.batch as B
+    for seed, ps, U, n, lo, hi in ((41, 42, 1 << 20, 3000, 50, 150), (5, 6, 100, 2000, 0, 70)):
+        blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+        reads = oracle.ragged_pool_reads(seed, ps, U, 0, n, lo, hi)
+        assert lens.cpu().tolist() == [len(r) for r in reads]
+        h = blob.cpu().numpy().tobytes()
+        o = offs.cpu().tolist()
+        assert [h[o[i]:o[i] + len(r)] for i, r in enumerate(reads)] == reads
+
+
+def test_encode_var_ragged_vs_oracle(gpu, oracle):
+    import shortseq_amd.batch as B
+    n = 20_000
+    blob, offs, lens = B.synth_ragged_pool_reads(n, 7, 8, 5000, 1, 300, device=gpu)
+    words = B.encode_var(blob, offs, lens)
+    reads = oracle.ragged_pool_reads(7, 8, 5000, 0, n, 1, 300)
+    got = words.cpu().numpy().view(np.uint64)
+    for i in range(0, n, 97):
+        w, _e = oracle.encode_one(reads[i])
+        nw = max(1, (len(reads[i]) + 31) // 32)
+        assert got[i, :nw].tolist() == [int(x) for x in w[:nw]], i
+        assert not got[i, nw:].any()
+
+
+@pytest.mark.parametrize("case", [(45, 46, 400, 50_000, 0, 6), (43, 44, 1 << 16, 200_000, 1, 300),
+                                  (41, 42, 1 << 20, 300_000, 50, 150)])
+def test_device_ingest_ragged_small(gpu, oracle, case):
+    """ss_ingest_add_device over a ragged device batch (two calls: global read indices continue)
+    == the generator-derived rows (pinned to oracle.count)."""
+    import shortseq_amd.batch as B
+    seed, ps, U, n, lo, hi = case
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    h = n // 3
+    eng = B.DeviceIngest(gpu)
+    try:
+        eng.count(blob, offs[:h], lens[:h])
+        eng.count(blob, offs[h:], lens[h:])
+        gl, gc, gw = eng.results()
+    finally:
+        eng.close()
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    assert gl.tolist() == el.tolist()
+    assert gc.tolist() == ec.tolist()
+    assert np.array_equal(gw, ew)
+
+
+def test_device_ingest_ragged_errors(gpu):
+    """A rejected read in a device batch raises the reference's message (the first in read order)."""
+    import shortseq_amd as sq
+    import shortseq_amd.batch as B
+    blob, offs, lens = B.synth_ragged_pool_reads(100_000, 3, 4, 1000, 20, 120, device=gpu)
+    o, ln = offs.cpu().tolist(), lens.cpu().tolist()
+    blob[o[70_000] + 5] = ord("N")
+    blob[o[90_000] + 1] = ord("x")
+    bad = bytes(blob[o[70_000]:o[70_000] + ln[70_000]].cpu().numpy())
+    with pytest.raises(Exception) as want:          # the reference's message for that read (chunk rule
+        sq.pack(bad)                                # for a full 32-nt block, the byte on the table path)
+    eng = B.DeviceIngest(gpu)
+    try:
+        with pytest.raises(Exception) as ei:
+            eng.count(blob, offs, lens)
+        assert str(ei.value) == str(want.value) and "N" in str(ei.value)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("name", ["ragged_1M_L1-300_U16", "ragged_50M_L50-150_U20"])
+def test_device_ingest_ragged_digest(gpu, oracle, name):
+    """Full size (bench.py F2): the engine's rows (dict order, lengths, counts, words) hash to the
+    generator-derived digest (tests/golden/ragged_digests.json)."""
+    import shortseq_amd.batch as B
+    d = _digests()[name]
+    blob, offs, lens = B.synth_ragged_pool_reads(d["n"], d["seed"], d["pool_seed"], d["U"], d["Lmin"], d["Lmax"],
+                                                 device=gpu)
+    eng = B.DeviceIngest(gpu)
+    try:
+        eng.count(blob, offs, lens)
+        gl, gc, gw = eng.results()
+    finally:
+        eng.close()
+    del blob, offs, lens
+    assert len(gl) == d["unique"] and int((gl.astype(np.uint64) * gc).sum()) == d["nt"]
+    assert oracle.rows_digest(gl, gc, gw) == d["digest"]

@@ -1,6 +1,6 @@
 // tools/tune_counter.hip — time the production partitioned counter insert (C5: 125M x 32 nt from a
 // pool of 2^24, table 2^25) built with compile-time knobs, e.g.
-//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include -DSS_PC_TILE=4096 tools/tune_counter.hip \
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include tools/tune_counter.hip \
 //         shortseq_amd/csrc/ss_codec.hip shortseq_amd/csrc/ss_runtime.hip -o tools/tune_counter_4096
 // prints ms per insert (table reset excluded) and checks the total count and the unique count.
 
