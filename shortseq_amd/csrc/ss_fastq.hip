@@ -35,6 +35,7 @@ constexpr int kFqT = SS_FQ_T;                               // threads per block
 constexpr int kFqU = 4;                                     // 16-B chunks per thread
 constexpr uint64_t kFqTile = (uint64_t)kFqT * kFqU * 16;    // 16 KiB per block
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
+constexpr uint64_t kNone64 = ~0ull;
 
 // 0x80 in every byte of x equal to the byte replicated in pat, 0 elsewhere (exact, no false hits).
 __device__ __forceinline__ uint32_t eq_bytes(uint32_t x, uint32_t pat) {
@@ -333,12 +334,11 @@ constexpr uint64_t kFqTile1 = (uint64_t)kFqT * kFqU1 * 16;     // 32 KiB per til
 
 constexpr uint32_t kStageShards = 64, kShardStride = 32;       // counters 128 B apart
 constexpr uint32_t kLdsPos = 4096;                             // newline positions gathered in LDS
-// SS_FQ_TILE_CAP > 0: every tile also owns a fixed run of that many staging words (after the
-// shards' regions); a tile with at most that many newlines stages there with no reservation atomic
-#ifndef SS_FQ_TILE_CAP
-#define SS_FQ_TILE_CAP 0   // same-box A/B (tools/tune_f1.hip): 1024 / 4096 within the run-to-run spread, off
-#endif
-constexpr uint32_t kTileCap = SS_FQ_TILE_CAP;
+// Every tile owns a fixed run of kTileCap staging words (after the shards' regions, 8 KiB per 32-KiB
+// tile): a tile with at most that many newlines (lines of 16 B or more on average) writes its
+// positions there straight from registers -- no reservation atomic, no LDS staging, no second
+// barrier; a denser tile reserves a run of its shard as before.
+constexpr uint32_t kTileCap = 2048;
 
 struct FqStage {
     uint32_t* pos;        // [kStageShards * region (+ tiles * kTileCap)] staged newline positions
@@ -347,6 +347,7 @@ struct FqStage {
     uint32_t* ovf;        // a shard's region ran full
     uint32_t* tile_cnt;   // [t] newlines per tile
     uint32_t* tile_run;   // [t] start of the tile's run in pos
+    uint32_t* tile_last;  // [t] position of the tile's last newline (kNone32: none staged)
     uint32_t* nul_cnt;    // NUL bytes seen (may exceed kNulCap)
     uint32_t* nul_pos;    // [kNulCap] their positions
 };
@@ -380,12 +381,13 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
     for (int k = 0; k < kFqU1 / 4; ++k)
         cnt += (uint32_t)((total[k] & 0xFFFFu) + ((total[k] >> 16) & 0xFFFFu) + ((total[k] >> 32) & 0xFFFFu) +
                           (total[k] >> 48));
+    const bool fixed = cnt <= kTileCap;    // block-uniform (the scan's totals)
     if (threadIdx.x == 0) {
         // the reservation's round trip overlaps the other waves' LDS staging below
         const uint32_t sh = blockIdx.x % kStageShards;
         uint64_t run = (uint64_t)sh * st.region;
         uint32_t c = cnt;
-        if (kTileCap && c <= kTileCap) {
+        if (fixed) {
             run = (uint64_t)kStageShards * st.region + (uint64_t)blockIdx.x * kTileCap;
         } else if (c) {
             const uint32_t r = atomicAdd(&st.used[sh * kShardStride], c);
@@ -397,10 +399,11 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
         }
         st.tile_cnt[blockIdx.x] = c;
         st.tile_run[blockIdx.x] = (uint32_t)run;
+        if (cnt == 0) st.tile_last[blockIdx.x] = kNone32;
         s_run = (uint32_t)run;
         s_cnt = c;
     }
-    const bool in_lds = cnt <= kLdsPos;   // typical tiles: positions gathered in LDS, stored as one run
+    const bool in_lds = !fixed && cnt <= kLdsPos;   // reserved runs: positions gathered in LDS, stored as one run
     auto put = [&](uint32_t base) {
         uint32_t rows_before = 0;
 #pragma unroll
@@ -414,12 +417,17 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
                 m &= m - 1;
                 if (in_lds) spos[k++] = off + bit;
                 else st.pos[k++] = off + bit;
+                if (k == base + cnt) st.tile_last[blockIdx.x] = off + bit;   // the tile's last newline
             }
         }
     };
-    if (in_lds) put(0);
-    __syncthreads();
-    if (s_cnt) {
+    if (fixed) {
+        put((uint32_t)(kStageShards * st.region + (uint64_t)blockIdx.x * kTileCap));
+    } else {
+        if (in_lds) put(0);
+        __syncthreads();
+    }
+    if (!fixed && s_cnt) {
         if (in_lds) {
             const uint32_t run = s_run;
             for (uint32_t e = threadIdx.x; e < cnt; e += kFqT) st.pos[run + e] = spos[e];
@@ -466,19 +474,21 @@ __device__ __forceinline__ bool fq_has_nl(const FqOut& o, uint64_t line0, uint64
     return !(partial && 4 * (o.sel0 + i) + 1 == line0 + nl);    // the unterminated last line
 }
 
-// one block per tile: staged newline k of the tile closes line lbase + k.  The newline closing a
-// sequence line (line number = 1 mod 4) gives its end; the newline before it (the tile's previous
-// entry, or the last one staged before the tile) gives its start: offsets[i] and lens[i] directly,
-// no end array and no separate length pass.  Block ntiles - 1 also places a final sequence line
-// without '\n' and writes the sequence-line count.
-constexpr int kPlaceR = 4;                                     // staged entries per thread per round
+// One wave per tile (four per block): staged newline k of the tile closes line lbase + k.  The
+// newline closing a sequence line (line number = 1 mod 4) gives its end; the newline before it (the
+// lane below's entry by a shuffle, the previous round's last one, or the previous tile's last newline,
+// tile_last) gives its start: offsets[i] and lens[i] directly, no end array and no separate length
+// pass.  The wave's loads (counts, run, line base, the previous tile's last newline) are independent,
+// so they go out together.  The last tile's wave also places a final sequence line without '\n' and
+// writes the sequence-line count.
 
-// start of the line that follows the last newline staged before `tile` (0: none in the chunk)
+// start of the line that follows the last newline staged before `tile` (0: none in the chunk); a
+// tile that stages none (a line longer than a tile) sends the search further back
 __device__ __forceinline__ uint64_t start_before(const FqStage& st, uint64_t tile) {
     while (tile > 0) {
         --tile;
-        const uint32_t c = st.tile_cnt[tile];
-        if (c) return (uint64_t)st.pos[st.tile_run[tile] + c - 1] + 1;
+        const uint32_t l = st.tile_last[tile];
+        if (l != kNone32) return (uint64_t)l + 1;
     }
     return 0;
 }
@@ -489,30 +499,33 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
                                                   const uint64_t* __restrict__ group_base,
                                                   const uint64_t* __restrict__ d_nl, uint32_t* __restrict__ lens,
                                                   uint64_t* d_nreads) {
-    const uint64_t tile = blockIdx.x;
-    const uint32_t cnt = st.tile_cnt[tile];
-    const uint32_t run = st.tile_run[tile];
-    const uint64_t lbase = line0 + group_base[tile >> 10] + tile_base[tile];
-    for (uint32_t k0 = 0; k0 < cnt; k0 += 256 * kPlaceR) {
-        uint32_t p[kPlaceR];
-#pragma unroll
-        for (int r = 0; r < kPlaceR; ++r) {
-            const uint32_t k = k0 + r * 256 + threadIdx.x;
-            if (k < cnt) p[r] = st.pos[run + k];
-        }
-#pragma unroll
-        for (int r = 0; r < kPlaceR; ++r) {
-            const uint32_t k = k0 + r * 256 + threadIdx.x;
+    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (tile < ntiles) {
+        const uint32_t cnt = st.tile_cnt[tile];
+        const uint32_t run = st.tile_run[tile];
+        const uint64_t lbase = line0 + group_base[tile >> 10] + tile_base[tile];
+        const uint32_t prev = tile ? st.tile_last[tile - 1] : kNone32;
+        // start of the tile's first line: after the previous newline (0 for the chunk's first line)
+        uint64_t carry = lbase == line0 ? 0 : (prev != kNone32 ? (uint64_t)prev + 1 : kNone64);
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const uint32_t p = st.pos[run + min(k, cnt - 1)];
+            const uint32_t below = (uint32_t)__shfl_up((int)p, 1);
             const uint64_t li = lbase + k;
-            if (k >= cnt || (li & 3u) != 1u) continue;
-            const uint64_t i = (li >> 2) - o.sel0;
-            if (i >= o.max_reads) continue;
-            const uint64_t start = k ? (uint64_t)st.pos[run + k - 1] + 1 : (li == line0 ? 0 : start_before(st, tile));
-            o.offsets[i] = start;
-            lens[i] = fq_len((uint64_t)p[r] - start + 1);
+            if (k < cnt && (li & 3u) == 1u) {
+                const uint64_t i = (li >> 2) - o.sel0;
+                if (i < o.max_reads) {
+                    uint64_t start = lane ? (uint64_t)below + 1 : carry;
+                    if (start == kNone64) start = start_before(st, tile);
+                    o.offsets[i] = start;
+                    lens[i] = fq_len((uint64_t)p - start + 1);
+                }
+            }
+            carry = (uint64_t)(uint32_t)__shfl((int)p, 63) + 1;
         }
     }
-    if (tile + 1 == ntiles && threadIdx.x == 0) {
+    if (tile + 1 == ntiles && lane == 0) {
         const uint64_t nl = *d_nl;
         bool partial;
         *d_nreads = fq_nsel(buf, o, line0, at_eof, nl, partial);
@@ -720,7 +733,8 @@ int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at
 }
 
 // one-pass workspace: tile_base u64 [t + 1] | group_base u64 [g + 1] | used u32 [64 x 32] | ovf u32,
-// nul_cnt u32 | nul_pos u32 [kNulCap] | tile_cnt u32 [t] | tile_run u32 [t] | pos u32 [64 x region]
+// nul_cnt u32 | nul_pos u32 [kNulCap] | tile_cnt u32 [t] | tile_run u32 [t] | tile_last u32 [t] |
+// pos u32 [64 x region]
 inline uint64_t fq_tiles1(uint64_t nbytes) { return (nbytes + kFqTile1 - 1) / kFqTile1; }
 
 // staging words per shard: the lines max_reads implies (4 per sequence line) + 25 %, spread over the
@@ -732,7 +746,7 @@ inline uint64_t fq_region(uint64_t max_reads) {
 
 uint64_t ss_fastq_onepass_ws_bytes(uint64_t nbytes, uint64_t max_reads) {
     const uint64_t t = fq_tiles1(nbytes);
-    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 8 + 4ull * kNulCap + 8 * t +
+    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 8 + 4ull * kNulCap + 12 * t +
            4 * kStageShards * fq_region(max_reads) + 4ull * kTileCap * t + 16;
 }
 
@@ -755,7 +769,8 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     st.nul_pos = st.ovf + 2;
     st.tile_cnt = st.nul_pos + kNulCap;
     st.tile_run = st.tile_cnt + t;
-    st.pos = st.tile_run + t;
+    st.tile_last = st.tile_run + t;
+    st.pos = st.tile_last + t;
     st.region = fq_region(max_reads);
     rc = ss_check(hipMemsetAsync(st.used, 0, 4 * (kStageShards * kShardStride + 2), s), "fastq staging reset");
     if (rc) return rc;
@@ -768,7 +783,7 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     }
     hipLaunchKernelGGL(k_fq_scan_groups, dim3(1), dim3(1024), 0, s, group_base, g, t, tile_base, d_counts);
     if (t) {
-        hipLaunchKernelGGL(k_fq_place, dim3((unsigned)t), dim3(256), 0, s, d_buf, o, line0, at_eof, st, t, tile_base,
+        hipLaunchKernelGGL(k_fq_place, dim3((unsigned)((t + 3) / 4)), dim3(256), 0, s, d_buf, o, line0, at_eof, st, t, tile_base,
                            group_base, (const uint64_t*)d_counts, d_lens, d_counts + 1);
         hipLaunchKernelGGL(k_fq_nulfix<false>, dim3(256), dim3(256), 0, s, d_buf, o, line0, at_eof,
                            (const uint64_t*)d_counts, d_lens);

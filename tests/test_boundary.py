@@ -101,3 +101,35 @@ def test_host_codec_matches_oracle(oracle, golden):
         lib.ss_host_decode(wa.ctypes.data, L, out)
         assert out.raw[:L].decode() == v["str_a"]
         assert lib.ss_host_hamming(wa.ctypes.data, wb.ctypes.data, L) == v["hamming"]
+
+
+_AUTO_NO_LIB_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import shortseq_amd as sq
+reads = [b"ACGT" * 8, b"GATTACA"] * 40_000          # >= GPU_MIN_READS: "auto" would pick a GPU
+c = sq.ShortSeqCounter(reads)                        # no HIP library here: the host path, not an error
+assert [(str(k), v) for k, v in c.items()] == [("ACGT" * 8, 40_000), ("GATTACA", 40_000)], list(c.items())
+for dev in ("cuda", "cuda:0", "all", [0, 0]):
+    try:
+        sq.ShortSeqCounter(reads, device=dev)
+    except ImportError:
+        pass
+    else:
+        raise SystemExit(f"device={dev!r} counted without the HIP library")
+print("AUTO OK")
+"""
+
+
+def test_auto_without_hip_library_takes_host_path(tmp_path):
+    """with device="auto" a host without a usable HIP library counts on the host (the
+    reference's behaviour) instead of raising ImportError; explicit GPU choices still raise.  The
+    package is copied without lib/libshortseq_amd.so into a scratch directory."""
+    import shutil
+    import subprocess
+    import sys
+    dst = tmp_path / "shortseq_amd"
+    shutil.copytree(os.path.join(REPO, "shortseq_amd"), dst, ignore=shutil.ignore_patterns("lib", "__pycache__"))
+    r = subprocess.run([sys.executable, "-c", _AUTO_NO_LIB_CHILD, str(tmp_path)], capture_output=True, text=True,
+                       timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0 and "AUTO OK" in r.stdout, r.stdout + r.stderr

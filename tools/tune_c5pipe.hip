@@ -31,12 +31,13 @@ PartWs ws_of(ss_counter* c) {
 }
 
 int g_grid = 0;
+int g_mul = 1;
 
 void coarse(ss_counter* c, const uint8_t* ascii, uint64_t n, uint64_t* fb, hipStream_t s) {
     Tbl t = tbl_of(c);
     PartWs w = ws_of(c);
     CK(hipMemsetAsync(c->ws_fill, 0, kFillWords * sizeof(uint32_t), s));
-    hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(g_grid), dim3(kPfT), 0, s, t, w, (const uint4*)ascii,
+    hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(g_grid * g_mul), dim3(kPfT), 0, s, t, w, (const uint4*)ascii,
                        (uint64_t)2, n, 2u, c->ws_cap1, c->ws_fill, (unsigned long long*)fb);
 }
 
@@ -80,13 +81,14 @@ int main(int argc, char** argv) {
     CK(hipEventCreateWithFlags(&ec0, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&ef0, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&ee1, hipEventDisableTiming));
-    const char* names[4] = {"full", "seq", "pipe", "pipe2"};
-    for (int mode = 0; mode < 4; ++mode) {
+    const char* names[6] = {"full", "seq", "pipe", "pipe2", "fullx2", "fullx3"};
+    for (int mode = 0; mode < 6; ++mode) {
+        g_mul = mode == 4 ? 2 : mode == 5 ? 3 : 1;
         double tot = 0;
         for (int r = -3; r < reps; ++r) {
             CK(hipDeviceSynchronize());
             CK(hipEventRecord(t0, s0));
-            if (mode == 0) {
+            if (mode == 0 || mode >= 4) {
                 coarse(cf, ascii, n, fb, s0);
                 fine(cf, s0);
             } else if (mode == 1) {

@@ -1,6 +1,6 @@
 // tools/tune_f1.hip — F1 one-pass FASTQ index (ss_fastq_index_onepass) on the bench's synthetic file
 // (8.4M records of 100 nt, 20-40-byte headers, 1.98 GB device-resident), built with compile-time knobs:
-//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include [-DSS_FQ_TILE_CAP=1024] tools/tune_f1.hip -o tools/tune_f1_<v>
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include [-D(int)kTileCap=1024] tools/tune_f1.hip -o tools/tune_f1_<v>
 // Checks offsets / lengths / read count against the two-pass index (ss_fastq_scan + ss_fastq_index)
 // and prints the mean time per call over hipEvents.
 #include "../shortseq_amd/csrc/ss_fastq.hip"
@@ -81,7 +81,7 @@ int main(int argc, char** argv) {
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= reps;
-        printf("round %d tile_cap %u: onepass %.4f ms  %.0f GB/s of file\n", round, (unsigned)SS_FQ_TILE_CAP, ms,
+        printf("round %d tile_cap %u: onepass %.4f ms  %.0f GB/s of file\n", round, (unsigned)(int)kTileCap, ms,
                nbytes / ms / 1e6);
     }
     return ok ? 0 : 2;

@@ -80,6 +80,46 @@ static void launch_p8(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32
                        rpb, out);
 }
 
+// glds form: each wave DMAs G whole 3-KiB groups (128 reads) straight into its own LDS region
+// (global_load_lds_dwordx4: coalesced 1-KiB wave-instructions, no VGPRs), waits for its own DMAs
+// (no block barrier: the region is wave-private), then lane l reads reads 2l, 2l+1 of a group as three
+// conflict-free ds_read_b128 (48-B lane stride) and stores both distances with one 8-B store.
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+template <int T, int G>
+__global__ __launch_bounds__(T) void k_ham3_glds(const uint4* __restrict__ a, const uint64_t* __restrict__ ref,
+                                                 uint64_t n, uint32_t* __restrict__ out) {
+    constexpr uint32_t NWV = T / 64;
+    __shared__ uint4 sbuf[NWV][G][192];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t q = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 192 + j * 64 + lane;
+            __builtin_amdgcn_global_load_lds((const void*)&a[q], (lds_void_ptr)&sbuf[wv][g][j * 64], 16, 0, 0);
+        }
+    const uint64_t rf0 = ref[0], rf1 = ref[1], rf2 = ref[2];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint4 u0 = sbuf[wv][g][3 * lane], u1 = sbuf[wv][g][3 * lane + 1], u2 = sbuf[wv][g][3 * lane + 2];
+        const uint64_t w0 = ((uint64_t)u0.y << 32) | u0.x, w1 = ((uint64_t)u0.w << 32) | u0.z;
+        const uint64_t w2 = ((uint64_t)u1.y << 32) | u1.x, w3 = ((uint64_t)u1.w << 32) | u1.z;
+        const uint64_t w4 = ((uint64_t)u2.y << 32) | u2.x, w5 = ((uint64_t)u2.w << 32) | u2.z;
+        const uint32_t d0 = ham64(w0 ^ rf0) + ham64(w1 ^ rf1) + ham64(w2 ^ rf2);
+        const uint32_t d1 = ham64(w3 ^ rf0) + ham64(w4 ^ rf1) + ham64(w5 ^ rf2);
+        const uint64_t r = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 128 + 2 * lane;
+        if (r + 1 < n) ham_store2(&out[r], d0, d1);
+        else if (r < n) ham_store(&out[r], d0);
+    }
+}
+
+template <int T, int G>
+static void launch_glds(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
+    const uint64_t per = (uint64_t)128 * (T / 64) * G;   // whole groups only (n a multiple of per)
+    hipLaunchKernelGGL((k_ham3_glds<T, G>), dim3((unsigned)(n / per)), dim3(T), 0, 0, (const uint4*)a, ref, n, out);
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 30;
     const uint64_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 100000000ull;
@@ -116,14 +156,13 @@ int main(int argc, char** argv) {
     };
     for (int pass = 0; pass < 3; ++pass) {
         run("prod T64 G1", launch_w<64, 1>);
-        run("T256 G1 (before)", launch_w<256, 1>);
         run("T128 G1", launch_w<128, 1>);
-        run("T64 G2", launch_w<64, 2>);
-        run("pad8 T64 U4", launch_p8<64, 4>);
-        run("pad8 T64 U8", launch_p8<64, 8>);
-        run("pad8 T128 U2", launch_p8<128, 2>);
-        run("pad8 T128 U4", launch_p8<128, 4>);
-        run("pad8 T64 U2", launch_p8<64, 2>);
+        run("glds T64 G1", launch_glds<64, 1>);
+        run("glds T64 G2", launch_glds<64, 2>);
+        run("glds T128 G1", launch_glds<128, 1>);
+        run("glds T128 G2", launch_glds<128, 2>);
+        run("glds T256 G1", launch_glds<256, 1>);
+        run("glds T64 G4", launch_glds<64, 4>);
     }
     return 0;
 }
