@@ -479,7 +479,7 @@ def bench_ragged(B, lib, dev, reps=5):
     floor = nt + n * 12
     return {"reads": n, "nt": nt, "len_range": [d["Lmin"], d["Lmax"]], "pool": d["U"], "unique": len(gl),
             "encode_var": {"ms_per_step": enc_ms, "nt_per_s": nt / enc_ms * 1e3,
-                           "roofline": {"bound": "hbm", "kernel": "k_encode_gen<var>", "achieved": enc_bytes / enc_ms / 1e6,
+                           "roofline": {"bound": "hbm", "kernel": "k_encode_var_dense", "achieved": enc_bytes / enc_ms / 1e6,
                                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                         "frac": enc_bytes / enc_ms / 1e6 / HBM_PEAK_GBS,
                                         "traffic": load_traffic("encode_var_ragged", n)}},

@@ -217,6 +217,66 @@ __device__ __forceinline__ uint64_t encode_word_at(const uint8_t* p, uint32_t nb
     return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
 }
 
+// Branch-free form of encode_word_at for the ragged kernel: the dword loads go out unconditionally
+// (the index clamped to the read's last dword: every load stays inside the read, and a clamped
+// duplicate is masked to 'A' below), so the compiler issues them back to back instead of waiting for
+// each conditional load in its own block.
+__device__ __forceinline__ uint64_t encode_word_bf(const uint8_t* p, uint32_t nb, bool table, uint32_t& bad) {
+    const uintptr_t addr = (uintptr_t)p;
+    const uint32_t* d = (const uint32_t*)(addr & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(addr & 3);
+    const uint32_t last = ((sh + nb + 3u) >> 2) - 1u;
+    uint32_t dw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dw[i] = d[min((uint32_t)i, last)];
+    uint32_t xw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t v = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
+        const int m = (int)nb - 4 * i;
+        if (m <= 0) {
+            v = 0x41414141u;
+        } else if (m < 4) {
+            const uint32_t keep = (1u << (8 * m)) - 1u;
+            v = (v & keep) | (0x41414141u & ~keep);
+        }
+        xw[i] = v;
+    }
+    Enc32 lo = encode16(xw[0], xw[1], xw[2], xw[3], table);
+    Enc32 hi = encode16(xw[4], xw[5], xw[6], xw[7], table);
+    bad |= lo.bad | hi.bad;
+    return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
+}
+
+// Ragged batches (ss_encode_var): one lane per output word, dense -- lane g writes out[g], word
+// w = g mod wpr of read r = g / wpr (a double reciprocal, corrected by one step), so no lane idles on
+// power-of-two padding and every wave stores 512 contiguous bytes.  Words at or past a read's length
+// are written as 0 (the row padding).
+__global__ __launch_bounds__(kThreads) void k_encode_var_dense(const uint8_t* in, const uint64_t* __restrict__ offs,
+                                                               const uint32_t* __restrict__ lens, uint64_t n,
+                                                               uint64_t* __restrict__ out, uint32_t wpr,
+                                                               double inv_wpr, unsigned long long* first_bad) {
+    const uint64_t total = n * wpr;
+    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kThreads) {
+        uint64_t r = (uint64_t)((double)g * inv_wpr);
+        if (r * wpr > g) --r;
+        else if ((r + 1) * wpr <= g) ++r;
+        const uint32_t w = (uint32_t)(g - r * wpr);
+        const uint32_t L = lens[r];
+        const uint64_t off = offs[r];
+        uint32_t bad = 0;
+        uint64_t word = 0;
+        if (L > SS_MAX_NT) {
+            bad = (w == 0);                     // short_seq.pyx:74 (too long), reported per read
+        } else if (32u * w < L) {
+            const uint32_t nb = min(32u, L - 32u * w);
+            word = encode_word_bf(in + off + 32u * w, nb, (L <= 32u) || (nb < 32u), bad);
+        }
+        out[g] = word;
+        report_bad(bad != 0u, r, first_bad);
+    }
+}
+
 // Lane slot g -> read r = g >> logG, word w = g & (G-1) (G = next_pow2(wpr)); lanes w >= wpr idle.
 // The grid-stride loop has a uniform trip count so the hamming reduction's shuffles see whole waves.
 template <bool VAR, bool HAM>
@@ -865,14 +925,12 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     hipStream_t s = (hipStream_t)stream;
     int rc = reset_first_bad(d_first_bad, s);
     if (rc || n == 0) return rc;
-    const uint32_t logG = log2_ceil(wpr);
-    // one slot per lane (no grid-stride loop): every lane's two dependent loads (offset / length,
-    // then the bytes) overlap across many resident waves; latency-bound at the capped grid
-    const unsigned grid = grid_for(n << logG, kThreads, 0x7FFFFFFFu);
-    hipLaunchKernelGGL((k_encode_gen<true, false>), dim3(grid), dim3(kThreads), 0, s, d_ascii, (uint64_t)0,
-                       d_offsets, d_lens, 0u, n, d_words, wpr, logG, (const uint64_t*)nullptr, 0u,
-                       (uint32_t*)nullptr, (unsigned long long*)d_first_bad);
-    return ss_check(hipGetLastError(), "k_encode_gen<var>");
+    // one word per lane (no grid-stride round): every lane's two dependent loads (offset / length,
+    // then the bytes) overlap across many resident waves
+    const unsigned grid = grid_for(n * wpr, kThreads, 0x7FFFFFFFu);
+    hipLaunchKernelGGL(k_encode_var_dense, dim3(grid), dim3(kThreads), 0, s, d_ascii, d_offsets, d_lens, n, d_words,
+                       wpr, 1.0 / (double)wpr, (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_encode_var_dense");
 }
 
 int ss_decode_fixed(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr,

@@ -315,9 +315,10 @@ __global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ bu
 // One read of the file (ss_fastq_index_onepass).  A decoupled look-back over tile counts measured
 // 1.25-1.47 ms for 2 GB (every waiting block polls the same status lines; the two-pass form took
 // 0.82), so the line numbers are resolved after the fact instead:
-//   k_fq_nlpos : 32-KiB tiles; each tile reserves a run of the staging array with one atomicAdd and
-//                writes its newline positions there in file order (u32, chunk-relative), plus its
-//                count and run start.  The reservations go to 64 counters (tile % 64), each on its
+//   k_fq_nlpos : 32-KiB tiles; each tile writes its newline positions in file order (u16 offsets in
+//                the tile) to its own fixed run of the staging array, or, past kTileCap newlines,
+//                reserves a run of its shard with one atomicAdd; plus its count, run start and
+//                last newline.  The reservations go to 64 counters (tile % 64), each on its
 //                own 128-B line with its own staging region: one counter word serves ~88
 //                atomics per us, which capped a single shared counter at 0.75 ms per 60k tiles.
 //                A region that runs full raises the overflow word (the caller retries with a larger
@@ -325,7 +326,8 @@ __global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ bu
 //   k_fq_scan_local / k_fq_scan_groups over the tile counts -> each tile's first line number
 //   k_fq_place : tile-wise, the staged positions with their line numbers -> offsets / lens
 //   k_fq_nulfix: sequence lines holding a NUL byte re-measured
-// HBM: the file once + 4 B per line written and read back + 12 B per sequence line of output.
+// HBM: the file once + 2 B per line written and read back (the newline's offset in its 32-KiB tile)
+// + 12 B per sequence line of output.
 #ifndef SS_FQ_U1
 #define SS_FQ_U1 8   // 16-KiB tiles (4) 0.525 ms, 64-KiB tiles (16) level with 32 KiB (tools/tune_f1.hip)
 #endif
@@ -341,7 +343,8 @@ constexpr uint32_t kLdsPos = 4096;                             // newline positi
 constexpr uint32_t kTileCap = 2048;
 
 struct FqStage {
-    uint32_t* pos;        // [kStageShards * region (+ tiles * kTileCap)] staged newline positions
+    uint16_t* pos;        // [kStageShards * region + tiles * kTileCap] staged newline positions, as
+                          // offsets inside their 32-KiB tile
     uint64_t region;      // staging words per shard
     uint32_t* used;       // [kStageShards * kShardStride] run reservations per shard
     uint32_t* ovf;        // a shard's region ran full
@@ -355,7 +358,7 @@ struct FqStage {
 __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ buf, uint64_t nbytes, FqStage st) {
     __shared__ uint64_t wtot[kFqT / 64][kFqU1 / 4];
     __shared__ uint32_t s_run, s_cnt;
-    __shared__ uint32_t spos[kLdsPos];
+    __shared__ uint16_t spos[kLdsPos];
     const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile1;
     // the chunks live only until their newline masks are taken: 16 bits per chunk, two per VGPR
     uint32_t mk[kFqU1 / 2];
@@ -415,8 +418,9 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
             while (m) {
                 const uint32_t bit = __builtin_ctz(m);
                 m &= m - 1;
-                if (in_lds) spos[k++] = off + bit;
-                else st.pos[k++] = off + bit;
+                const uint16_t rel = (uint16_t)(off + bit - (uint32_t)t0);
+                if (in_lds) spos[k++] = rel;
+                else st.pos[k++] = rel;
                 if (k == base + cnt) st.tile_last[blockIdx.x] = off + bit;   // the tile's last newline
             }
         }
@@ -510,7 +514,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
         uint64_t carry = lbase == line0 ? 0 : (prev != kNone32 ? (uint64_t)prev + 1 : kNone64);
         for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
             const uint32_t k = k0 + lane;
-            const uint32_t p = st.pos[run + min(k, cnt - 1)];
+            const uint32_t p = (uint32_t)(tile * kFqTile1) + st.pos[run + min(k, cnt - 1)];
             const uint32_t below = (uint32_t)__shfl_up((int)p, 1);
             const uint64_t li = lbase + k;
             if (k < cnt && (li & 3u) == 1u) {
@@ -747,7 +751,7 @@ inline uint64_t fq_region(uint64_t max_reads) {
 uint64_t ss_fastq_onepass_ws_bytes(uint64_t nbytes, uint64_t max_reads) {
     const uint64_t t = fq_tiles1(nbytes);
     return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 8 + 4ull * kNulCap + 12 * t +
-           4 * kStageShards * fq_region(max_reads) + 4ull * kTileCap * t + 16;
+           2 * kStageShards * fq_region(max_reads) + 2ull * kTileCap * t + 16;
 }
 
 int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, void* d_ws,
@@ -770,7 +774,7 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     st.tile_cnt = st.nul_pos + kNulCap;
     st.tile_run = st.tile_cnt + t;
     st.tile_last = st.tile_run + t;
-    st.pos = st.tile_last + t;
+    st.pos = (uint16_t*)(st.tile_last + t);
     st.region = fq_region(max_reads);
     rc = ss_check(hipMemsetAsync(st.used, 0, 4 * (kStageShards * kShardStride + 2), s), "fastq staging reset");
     if (rc) return rc;

@@ -80,6 +80,8 @@ def main():
             put("decode512", e, READS // 2)
         elif k.startswith("void k_encode_g16<false, true, 2"):
             put("encode512", e, READS // 2)
+        elif k.startswith("k_encode_var_dense") or "k_encode_var_dense" in k:
+            put("encode_var_ragged", e, 50_000_000)   # F2: 50M ragged 50-150-nt reads
     # F1: the one-pass FASTQ index (k_fq_nlpos + k_fq_place per call; 8 Mi records of the bench's
     # synthetic 100-nt file)
     fq = []
