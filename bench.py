@@ -388,9 +388,10 @@ def bench_fastq_index(B, lib, dev, n_rec=8 << 20, L=100, reps=10):
         raise SystemExit("PARITY FAILURE: FASTQ one-pass staging / newline count")
     verify("one-pass", int(cnt[1]))
     ms = tr.region_ms / reps
-    # algorithmic bytes of the one-pass index: the file once, 4 B per line staged and read back (4
-    # lines per record), 12 B per sequence line out (offset u64 + length u32)
-    algo = nbytes + nrec * (4 * 4 * 2 + 12)
+    # algorithmic bytes of the one-pass index: the file once, 2 B per line staged and read back (a
+    # u16 offset in the line's 32-KiB tile; 4 lines per record), 12 B per sequence line out (offset
+    # u64 + length u32)
+    algo = nbytes + nrec * (4 * 2 * 2 + 12)
     return {"file_bytes": nbytes, "records": nrec, "read_len": L, "ms_per_step": ms,
             "file_GB_per_s": nbytes / ms / 1e6, "records_per_s": nrec / ms * 1e3,
             "two_pass_ms_per_step": tr2.region_ms / reps,

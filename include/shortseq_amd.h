@@ -85,7 +85,9 @@ int ss_encode_fixed(const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t str
 
 /* Variable-length batch: read i = d_ascii[d_offsets[i] .. + d_lens[i]), 0 <= len <= 1024
  * (short_seq.pyx:54-74 length-class switch: 0 -> packed 0, <= 32 table path, else array path).
- * Reads longer than 1024 are reported through *d_first_bad like invalid bases. */
+ * Reads longer than 1024 are reported through *d_first_bad like invalid bases.  The kernel reads the
+ * blob in whole 16-B-aligned chunks around each read (device allocations are at least 256-B aligned,
+ * so this never leaves the allocation). */
 int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint32_t* d_lens,
                   uint64_t n, uint64_t* d_words, uint32_t wpr, uint64_t* d_first_bad, void* stream);
 

@@ -217,22 +217,26 @@ __device__ __forceinline__ uint64_t encode_word_at(const uint8_t* p, uint32_t nb
     return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
 }
 
-// Branch-free form of encode_word_at for the ragged kernel: the dword loads go out unconditionally
-// (the index clamped to the read's last dword: every load stays inside the read, and a clamped
-// duplicate is masked to 'A' below), so the compiler issues them back to back instead of waiting for
-// each conditional load in its own block.
-__device__ __forceinline__ uint64_t encode_word_bf(const uint8_t* p, uint32_t nb, bool table, uint32_t& bad) {
+// The ragged kernel's word loader: the 16-B-aligned chunks that hold the word's bytes (three
+// dwordx4 loads, the third clamped to the last chunk holding a byte of the word, so every load stays
+// inside chunks the read touches: no fault past the buffer's last 16-B chunk) realigned by a
+// funnel shift; bytes past nb become 'A'.  Against nine dword loads per lane: a third of the load
+// instructions, each touching half the cache lines.
+__device__ __forceinline__ uint64_t encode_word_q(const uint8_t* p, uint32_t nb, bool table, uint32_t& bad) {
     const uintptr_t addr = (uintptr_t)p;
-    const uint32_t* d = (const uint32_t*)(addr & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(addr & 3);
-    const uint32_t last = ((sh + nb + 3u) >> 2) - 1u;
-    uint32_t dw[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) dw[i] = d[min((uint32_t)i, last)];
+    const uint4* q = (const uint4*)(addr & ~(uintptr_t)15);
+    const uint32_t sh = (uint32_t)(addr & 15);
+    const uint32_t last = (sh + nb - 1u) >> 4;      // 0..2: the chunk holding the word's last byte
+    const uint4 c0 = q[0], c1 = q[min(1u, last)], c2 = q[min(2u, last)];
+    const uint32_t d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+    const uint32_t s4 = sh >> 2, sb = sh & 3u;
     uint32_t xw[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        uint32_t v = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], sh);
+        // dwords i + s4 and i + s4 + 1 of the 12 (s4 < 4): a 4-way select, then the byte shift
+        const uint32_t lo = s4 == 0 ? d[i] : s4 == 1 ? d[i + 1] : s4 == 2 ? d[i + 2] : d[i + 3];
+        const uint32_t hi = s4 == 0 ? d[i + 1] : s4 == 1 ? d[i + 2] : s4 == 2 ? d[i + 3] : d[min(i + 4, 11)];
+        uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sb);
         const int m = (int)nb - 4 * i;
         if (m <= 0) {
             v = 0x41414141u;
@@ -251,7 +255,8 @@ __device__ __forceinline__ uint64_t encode_word_bf(const uint8_t* p, uint32_t nb
 // Ragged batches (ss_encode_var): one lane per output word, dense -- lane g writes out[g], word
 // w = g mod wpr of read r = g / wpr (a double reciprocal, corrected by one step), so no lane idles on
 // power-of-two padding and every wave stores 512 contiguous bytes.  Words at or past a read's length
-// are written as 0 (the row padding).
+// are written as 0 (the row padding).  The blob's 16-B chunks are read whole (encode_word_q): the
+// blob must be readable to the end of its last 16-B chunk (any hipMalloc / torch allocation is).
 __global__ __launch_bounds__(kThreads) void k_encode_var_dense(const uint8_t* in, const uint64_t* __restrict__ offs,
                                                                const uint32_t* __restrict__ lens, uint64_t n,
                                                                uint64_t* __restrict__ out, uint32_t wpr,
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void k_encode_var_dense(const uint8_t* in
             bad = (w == 0);                     // short_seq.pyx:74 (too long), reported per read
         } else if (32u * w < L) {
             const uint32_t nb = min(32u, L - 32u * w);
-            word = encode_word_bf(in + off + 32u * w, nb, (L <= 32u) || (nb < 32u), bad);
+            word = encode_word_q(in + off + 32u * w, nb, (L <= 32u) || (nb < 32u), bad);
         }
         out[g] = word;
         report_bad(bad != 0u, r, first_bad);

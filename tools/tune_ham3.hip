@@ -114,6 +114,112 @@ __global__ __launch_bounds__(T) void k_ham3_glds(const uint4* __restrict__ a, co
     }
 }
 
+// x4-store form: the production lane-triple sums, then the 64 triples' two distances (packed in one
+// u32) are gathered so that lanes 0..31 each store four reads' distances as one dwordx4 (one store
+// instruction per 128-read group instead of three partial ones)
+template <int T, int G>
+__global__ __launch_bounds__(T) void k_ham3_x4(const uint4* __restrict__ a, const uint64_t* __restrict__ ref,
+                                               uint64_t n, uint32_t* __restrict__ out) {
+    constexpr uint32_t NWV = T / 64;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint4 x[G][3];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t q = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 192 + j * 64 + lane;
+            x[g][j] = ld_stream(&a[q]);
+        }
+    const uint64_t rw[3] = {ref[0], ref[1], ref[2]};
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        uint32_t dl[3], dh[3], pk[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t wlo = ((uint64_t)x[g][j].y << 32) | x[g][j].x, whi = ((uint64_t)x[g][j].w << 32) | x[g][j].z;
+            const uint32_t pos = (2u * ((uint32_t)j + lane)) % 3u;
+            const uint64_t clo = pos == 0 ? rw[0] : (pos == 1 ? rw[1] : rw[2]);
+            const uint64_t chi = pos == 0 ? rw[1] : (pos == 1 ? rw[2] : rw[0]);
+            dl[j] = ham64(wlo ^ clo);
+            dh[j] = ham64(whi ^ chi);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t sm = dl[j] + dh[j];
+            uint32_t n1l = __shfl(dl[j], (int)min(lane + 1u, 63u)), n1h = __shfl(dh[j], (int)min(lane + 1u, 63u));
+            uint32_t n2 = __shfl(sm, (int)min(lane + 2u, 63u));
+            if (j < 2) {
+                const uint32_t l0 = __builtin_amdgcn_readlane(dl[j + 1], 0), h0 = __builtin_amdgcn_readlane(dh[j + 1], 0);
+                const uint32_t s1 = __builtin_amdgcn_readlane(dl[j + 1] + dh[j + 1], 1);
+                if (lane == 62) n2 = l0 + h0;
+                if (lane == 63) {
+                    n1l = l0;
+                    n1h = h0;
+                    n2 = s1;
+                }
+            }
+            pk[j] = (sm + n1l) | ((n1h + n2) << 16);    // reads 2m, 2m + 1 of triple lane 3m (valid there)
+        }
+        // output lane q < 32: triples 2q (global lane 6q) and 2q + 1 (6q + 3)
+        const uint32_t L0 = 6u * (lane & 31u), L1 = L0 + 3u;
+        uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t a0 = __shfl(pk[j], (int)(L0 & 63u)), a1 = __shfl(pk[j], (int)(L1 & 63u));
+            if (L0 / 64u == (uint32_t)j) v0 = a0;
+            if (L1 / 64u == (uint32_t)j) v1 = a1;
+        }
+        const uint64_t grp = ((uint64_t)blockIdx.x * G + g) * NWV + wv;
+        const uint64_t r = grp * 128 + 4 * lane;
+        if (lane < 32 && r + 3 < n) {
+            const u32x4 o = {v0 & 0xFFFFu, v0 >> 16, v1 & 0xFFFFu, v1 >> 16};
+            __builtin_nontemporal_store(o, (u32x4*)&out[r]);
+        }
+    }
+}
+
+template <int T, int G>
+static void launch_x4(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
+    const uint64_t per = (uint64_t)128 * (T / 64) * G;   // whole groups only (n a multiple of per)
+    hipLaunchKernelGGL((k_ham3_x4<T, G>), dim3((unsigned)(n / per)), dim3(T), 0, 0, (const uint4*)a, ref, n, out);
+}
+
+// x3 form: a read's 24 B as two dwordx3 halves in a lane pair (lane 2k: dwords 0-2 = word 0 and the
+// low half of word 1; lane 2k+1: dwords 3-5).  A wave-instruction loads 768 contiguous bytes (32
+// reads, six whole lines); the split at bit 32 of word 1 falls on a 2-bit boundary, so each lane's
+// three 32-bit XOR-collapse-popcounts plus one DPP pair swap give the read's distance, and the even
+// lanes store 32 consecutive distances (128 B).
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_ham3_x3(const uint32_t* __restrict__ a32, const uint64_t* __restrict__ ref,
+                                               uint64_t n, uint32_t* __restrict__ out) {
+    constexpr uint32_t NWV = T / 64;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, h = lane & 1u;
+    u32x3 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t g = ((uint64_t)blockIdx.x * NWV + wv) * U + u;    // group of 32 reads
+        x[u] = __builtin_nontemporal_load((const u32x3*)(a32 + g * 192 + 3 * lane));
+    }
+    const uint64_t r0 = ref[0], r1 = ref[1], r2 = ref[2];
+    const uint32_t c0 = h ? (uint32_t)(r1 >> 32) : (uint32_t)r0;
+    const uint32_t c1 = h ? (uint32_t)r2 : (uint32_t)(r0 >> 32);
+    const uint32_t c2 = h ? (uint32_t)(r2 >> 32) : (uint32_t)r1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint32_t d = ham32(x[u].x ^ c0) + ham32(x[u].y ^ c1) + ham32(x[u].z ^ c2);
+        d += swap_pair(d);
+        const uint64_t r = (((uint64_t)blockIdx.x * NWV + wv) * U + u) * 32 + (lane >> 1);
+        if (!h && r < n) ham_store(&out[r], d);
+    }
+}
+
+template <int T, int U>
+static void launch_x3(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
+    const uint64_t per = (uint64_t)32 * (T / 64) * U;   // whole groups only (n a multiple of per)
+    hipLaunchKernelGGL((k_ham3_x3<T, U>), dim3((unsigned)(n / per)), dim3(T), 0, 0, (const uint32_t*)a, ref, n, out);
+}
+
 template <int T, int G>
 static void launch_glds(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
     const uint64_t per = (uint64_t)128 * (T / 64) * G;   // whole groups only (n a multiple of per)
@@ -157,12 +263,13 @@ int main(int argc, char** argv) {
     for (int pass = 0; pass < 3; ++pass) {
         run("prod T64 G1", launch_w<64, 1>);
         run("T128 G1", launch_w<128, 1>);
-        run("glds T64 G1", launch_glds<64, 1>);
-        run("glds T64 G2", launch_glds<64, 2>);
-        run("glds T128 G1", launch_glds<128, 1>);
-        run("glds T128 G2", launch_glds<128, 2>);
-        run("glds T256 G1", launch_glds<256, 1>);
-        run("glds T64 G4", launch_glds<64, 4>);
+        run("x4 T64 G1", launch_x4<64, 1>);
+        run("x3 T64 U4", launch_x3<64, 4>);
+        run("x3 T64 U8", launch_x3<64, 8>);
+        run("x3 T128 U4", launch_x3<128, 4>);
+        run("x3 T128 U2", launch_x3<128, 2>);
+        run("x3 T256 U2", launch_x3<256, 2>);
+        run("x3 T64 U2", launch_x3<64, 2>);
     }
     return 0;
 }
