@@ -712,7 +712,7 @@ def main():
             extra[f"C3p_hamming_ref_{Lh}"] = {
                 "pairs_per_s": nh * world / (elh / args.steps), "ms_per_step": elh / args.steps * 1e3,
                 "device_ms_per_step": dh, "reads": nh,
-                "roofline": {"kernel": "k_ham_dense3w" if Lh == 96 else "k_ham_dense",
+                "roofline": {"kernel": "k_ham_dense3x" if Lh == 96 else "k_ham_dense",
                              "achieved": bh / (dh * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": bh / (dh * 1e-3) / 1e9 / HBM_PEAK_GBS, "algo_bytes_per_step": bh,
                              "traffic": load_traffic(f"hamming_ref_{Lh}", nh)}}

@@ -195,9 +195,21 @@ int ss_counter_merge_words(ss_counter* c, const uint64_t* d_words, const uint64_
                            const uint64_t* d_first, uint64_t m, void* stream);
 
 /* Fix the key length of an empty handle (also done by the first insert); -1 from ss_counter_length
- * means not fixed yet. */
+ * means not fixed yet, -2 a packed-word handle (ss_counter_set_words). */
 int ss_counter_set_length(ss_counter* c, uint32_t L);
 int ss_counter_length(const ss_counter* c);
+
+/* Packed-word keys: an empty handle (or one after ss_counter_reset) set to keys of W = 2..64 words,
+ * compared whole; ss_counter_insert_words counts n rows d_words[n * W] already packed on the device
+ * (row i gets global index base_index + i; partitioned path, workspace grown to n as for multi-word
+ * ss_counter_insert_fixed).  The drop-in engine keys one handle per length class this way: the
+ * ceil(L/32) words of a read of 32(W-2)+1 .. 32(W-1) nt plus its length as the last word, so one
+ * table holds every length of the class (key = (length, words), short_seq_192.pyx:35-41 /
+ * short_seq_var.pyx:22-28).  Extract with ss_counter_extract_words (lens = 0: the length is the
+ * caller's word); grow with ss_counter_merge_words.  New in this ABI version; replaces no
+ * reference interface. */
+int ss_counter_set_words(ss_counter* c, uint32_t W);
+int ss_counter_insert_words(ss_counter* c, const uint64_t* d_words, uint64_t n, uint64_t base_index, void* stream);
 
 /* Copy the handle's overflow word to *d_flag (device u64): bit 0 = table full during an insert or
  * merge, bit 1 = an extract found more entries than `cap`, bit 2 = a merged count did not fit 32

@@ -56,6 +56,8 @@ SIGNATURES = [
     ("ss_counter_merge_words", C.c_int, [_P, _P, _P, _P, _U64, _P]),
     ("ss_counter_set_length", C.c_int, [_P, _U32]),
     ("ss_counter_length", C.c_int, [_P]),
+    ("ss_counter_set_words", C.c_int, [_P, _U32]),
+    ("ss_counter_insert_words", C.c_int, [_P, _P, _U64, _U64, _P]),
     ("ss_counter_overflow", C.c_int, [_P, _P, _P]),
     ("ss_counter_size", C.c_int, [_P, _P, _P]),
     ("ss_counter_extract", C.c_int, [_P, _U32, _P, _P, _P, _P, _U64, _P, _P]),

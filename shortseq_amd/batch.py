@@ -818,6 +818,16 @@ class GpuCounter:
             raise RuntimeError("GPU counter table overflowed; use a larger capacity")
         return words[:m].cpu().numpy().view(np.uint64), counts[:m].cpu().numpy(), first[:m].cpu().numpy()
 
+    def insert_words(self, words: torch.Tensor, base_index: int = 0) -> None:
+        """Count rows of already-packed keys (int64 [n, W], W = 2..64, compared whole;
+        ss_counter_set_words + ss_counter_insert_words).  The first call fixes W."""
+        _require_cuda(words, "words")
+        if words.dim() != 2 or words.dtype != torch.int64 or not words.is_contiguous():
+            raise TypeError("words: contiguous int64 [n, W]")
+        check(lib().ss_counter_set_words(self._h, words.shape[1]), "ss_counter_set_words")
+        check(lib().ss_counter_insert_words(self._h, words.data_ptr(), words.shape[0], base_index,
+                                            _stream(self.device)), "ss_counter_insert_words")
+
     def items_sorted_words(self):
         """Host copy of (words u64 [m, W], counts, first) sorted by first occurrence (= dict order)."""
         _, _, words, counts, first, parts = self.extract_words(1)

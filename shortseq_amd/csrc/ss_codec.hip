@@ -7,7 +7,7 @@
 //                  __shfl_xor and per-read sums (fused hamming) reduce inside the group.
 //   k_encode_gen   any L / stride / variable lengths: one lane per output word, aligned dword
 //                  loads + v_alignbyte; the general and ragged path.
-//   k_ham_dense / k_ham_dense3w hamming on dense packed rows (dwordx4 streams; k_ham_group otherwise)
+//   k_ham_dense / k_ham_dense3x hamming on dense packed rows (dwordx4 streams; k_ham_group otherwise)
 //   k_decode_g16 / k_decode_gen, k_ham_group, k_synth_*.
 #include "ss_device.h"
 #include "ss_internal.h"
@@ -230,13 +230,18 @@ __device__ __forceinline__ uint64_t encode_word_q(const uint8_t* p, uint32_t nb,
     const uint4 c0 = q[0], c1 = q[min(1u, last)], c2 = q[min(2u, last)];
     const uint32_t d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
     const uint32_t s4 = sh >> 2, sb = sh & 3u;
+    // e[k] = d[k + s4] (s4 < 4) by two masked selects on constant indices: written as a ternary on
+    // the index, the compiler turns the 12 dwords into a scratch array indexed at run time
+    const uint32_t m1 = 0u - (s4 & 1u), m2 = 0u - ((s4 >> 1) & 1u);
+    uint32_t a[11], e[9];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) a[k] = d[k] ^ ((d[k] ^ d[k + 1]) & m1);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) e[k] = a[k] ^ ((a[k] ^ a[min(k + 2, 10)]) & m2);
     uint32_t xw[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        // dwords i + s4 and i + s4 + 1 of the 12 (s4 < 4): a 4-way select, then the byte shift
-        const uint32_t lo = s4 == 0 ? d[i] : s4 == 1 ? d[i + 1] : s4 == 2 ? d[i + 2] : d[i + 3];
-        const uint32_t hi = s4 == 0 ? d[i + 1] : s4 == 1 ? d[i + 2] : s4 == 2 ? d[i + 3] : d[min(i + 4, 11)];
-        uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sb);
+        uint32_t v = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
         const int m = (int)nb - 4 * i;
         if (m <= 0) {
             v = 0x41414141u;
@@ -276,6 +281,39 @@ __global__ __launch_bounds__(kThreads) void k_encode_var_dense(const uint8_t* in
         } else if (32u * w < L) {
             const uint32_t nb = min(32u, L - 32u * w);
             word = encode_word_q(in + off + 32u * w, nb, (L <= 32u) || (nb < 32u), bad);
+        }
+        out[g] = word;
+        report_bad(bad != 0u, r, first_bad);
+    }
+}
+
+// Drop-in engine, one multi-word length class (ss_ingest): row i = read sel[i] of the chunk (read i
+// of a dense chunk of fixed length dense_L when sel is null), W words (ss_encode_var's rule) then
+// its length as word W, one lane per output word.  first_bad: the smallest chunk read index that
+// holds a rejected byte (rows are ordered by length, so the row would not give input order).
+__global__ __launch_bounds__(kThreads) void k_encode_class(const uint8_t* in, const uint64_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ lens,
+                                                           const uint64_t* __restrict__ sel, uint32_t dense_L,
+                                                           uint64_t m, uint32_t W, double inv_w1,
+                                                           uint64_t* __restrict__ out, unsigned long long* first_bad) {
+    const uint32_t W1 = W + 1;
+    const uint64_t total = m * W1;
+    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kThreads) {
+        uint64_t i = (uint64_t)((double)g * inv_w1);
+        if (i * W1 > g) --i;
+        else if ((i + 1) * W1 <= g) ++i;
+        const uint32_t w = (uint32_t)(g - i * W1);
+        const uint64_t r = sel ? sel[i] : i;
+        const uint32_t L = dense_L ? dense_L : lens[r];
+        uint32_t bad = 0;
+        uint64_t word = L;
+        if (w < W) {
+            word = 0;
+            if (32u * w < L) {
+                const uint64_t off = dense_L ? r * dense_L : offs[r];
+                const uint32_t nb = min(32u, L - 32u * w);
+                word = encode_word_q(in + off + 32u * w, nb, nb < 32u, bad);
+            }
         }
         out[g] = word;
         report_bad(bad != 0u, r, first_bad);
@@ -424,98 +462,46 @@ __device__ __forceinline__ void ham_store2(uint32_t* p, uint32_t lo, uint32_t hi
     else *(uint64_t*)p = v;
 }
 
-// Dense hamming for W = 3 with every lane busy and line-aligned loads: a wave takes groups of 3
-// whole 1-KiB chunks (192 dwordx4 = 384 words = 128 reads, so a group starts on a read boundary).
-// Global lane L = 64 j + l of a group holds words 2L, 2L+1; the lane triple (3m, 3m+1, 3m+2) holds
-// reads 2m = words 6m..6m+2 and 2m+1 = words 6m+3..6m+5, and lane 3m gathers its neighbours'
-// per-word distances by shuffle and stores both read distances (one 8-B store).  Two
-// triples straddle a chunk boundary (L = 63..65, 126..128): their p0 lane takes the next chunk's
-// lane-0/1 values by readlane.  Group index = (block G + g) NWV + wave, so at each g the block's
-// waves read one contiguous span.
-template <bool PAIR, int T, int G>
-__global__ __launch_bounds__(T) void k_ham_dense3w(const uint4* __restrict__ a, const uint4* __restrict__ b,
+// Dense hamming for W = 3 (96 nt, C3'): a read's 24 B are two dwordx3 halves held by a lane pair
+// (lane 2k: dwords 0-2 = word 0 and the low half of word 1; lane 2k+1: dwords 3-5), so a
+// wave-instruction loads 768 contiguous bytes (32 reads, six whole lines) with no shuffle needed to
+// assemble a read.  The split at bit 32 of word 1 falls on a 2-bit boundary, so each lane's three
+// 32-bit XOR-collapse-popcounts plus one DPP pair swap give the read's distance, and the even lanes
+// store 32 consecutive distances (128 B).  A wave takes U groups of 32 reads.  Lanes past n load the
+// last read again (clamped, branch-free) and store nothing.  Same box (tools/tune_ham3.hip): 0.806
+// of the 8-TB/s peak against 0.776-0.786 for the former lane-triple form over 1-KiB chunks (three
+// shuffles and three partial 8-B stores per 128 reads), 0.791 with that form's distances gathered
+// into dwordx4 stores, 0.73 with the chunks DMA'd into LDS (global_load_lds) and read back per lane.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+template <bool PAIR, int T, int U>
+__global__ __launch_bounds__(T) void k_ham_dense3x(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                                                    const uint64_t* __restrict__ ref, uint64_t n,
                                                    uint32_t* __restrict__ out) {
     constexpr uint32_t NWV = T / 64;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t nw = 3 * n, nfull = nw / 2;                      // whole dwordx4 of the rows
-    const uint64_t blk_q1 = ((uint64_t)blockIdx.x + 1) * G * NWV * 192;   // past the block's last dwordx4
-    const bool whole = blk_q1 <= nfull;
-    auto load = [&](const uint4* src, uint64_t q) -> uint4 {
-        if (q < nfull) return ld_stream(&src[q]);
-        if (2 * q < nw) {
-            const uint64_t v = ((const uint64_t*)src)[2 * q];
-            return make_uint4((uint32_t)v, (uint32_t)(v >> 32), 0u, 0u);
-        }
-        return make_uint4(0u, 0u, 0u, 0u);
-    };
-    uint4 x[G][3], y[G][3];
-    if (whole) {   // block-uniform: unconditional loads, all issued back to back
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, h = lane & 1u;
+    const uint64_t g0 = ((uint64_t)blockIdx.x * NWV + wv) * U;     // the wave's first group of 32 reads
+    u32x3 x[U], y[U];
 #pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const uint64_t q = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 192 + j * 64 + lane;
-                x[g][j] = ld_stream(&a[q]);
-                if constexpr (PAIR) y[g][j] = ld_stream(&b[q]);
-            }
-    } else {
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const uint64_t q = (((uint64_t)blockIdx.x * G + g) * NWV + wv) * 192 + j * 64 + lane;
-                x[g][j] = load(a, q);
-                if constexpr (PAIR) y[g][j] = load(b, q);
-            }
+    for (int u = 0; u < U; ++u) {
+        const uint64_t rc = min((g0 + u) * 32 + (lane >> 1), n - 1);
+        x[u] = __builtin_nontemporal_load((const u32x3*)(a + rc * 6 + 3 * h));
+        if constexpr (PAIR) y[u] = __builtin_nontemporal_load((const u32x3*)(b + rc * 6 + 3 * h));
     }
-    uint64_t rw[3] = {0, 0, 0};
-    if constexpr (!PAIR) {
-        rw[0] = ref[0];
-        rw[1] = ref[1];
-        rw[2] = ref[2];
+    uint32_t c0 = 0, c1 = 0, c2 = 0;
+    if constexpr (!PAIR) {   // the reference's dwords this lane's half meets
+        const uint64_t r0 = ref[0], r1 = ref[1], r2 = ref[2];
+        c0 = h ? (uint32_t)(r1 >> 32) : (uint32_t)r0;
+        c1 = h ? (uint32_t)r2 : (uint32_t)(r0 >> 32);
+        c2 = h ? (uint32_t)(r2 >> 32) : (uint32_t)r1;
     }
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        uint32_t dl[3], dh[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const uint64_t wlo = ((uint64_t)x[g][j].y << 32) | x[g][j].x, whi = ((uint64_t)x[g][j].w << 32) | x[g][j].z;
-            uint64_t clo, chi;
-            if constexpr (PAIR) {
-                clo = ((uint64_t)y[g][j].y << 32) | y[g][j].x;
-                chi = ((uint64_t)y[g][j].w << 32) | y[g][j].z;
-            } else {   // word 2L sits at position (2L) % 3 of its read; 64 = 1 (mod 3)
-                const uint32_t pos = (2u * ((uint32_t)j + lane)) % 3u;
-                clo = pos == 0 ? rw[0] : (pos == 1 ? rw[1] : rw[2]);
-                chi = pos == 0 ? rw[1] : (pos == 1 ? rw[2] : rw[0]);
-            }
-            dl[j] = ham64(wlo ^ clo);
-            dh[j] = ham64(whi ^ chi);
-        }
-        const uint64_t grp = ((uint64_t)blockIdx.x * G + g) * NWV + wv;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const uint32_t sm = dl[j] + dh[j];
-            uint32_t n1l = __shfl(dl[j], (int)min(lane + 1u, 63u)), n1h = __shfl(dh[j], (int)min(lane + 1u, 63u));
-            uint32_t n2 = __shfl(sm, (int)min(lane + 2u, 63u));
-            if (j < 2) {   // triples across the chunk boundary take the next chunk's lanes 0 / 1
-                const uint32_t l0 = __builtin_amdgcn_readlane(dl[j + 1], 0), h0 = __builtin_amdgcn_readlane(dh[j + 1], 0);
-                const uint32_t s1 = __builtin_amdgcn_readlane(dl[j + 1] + dh[j + 1], 1);
-                if (lane == 62) n2 = l0 + h0;
-                if (lane == 63) {
-                    n1l = l0;
-                    n1h = h0;
-                    n2 = s1;
-                }
-            }
-            const uint32_t L = 64u * j + lane;
-            if (L % 3u == 0) {
-                const uint64_t r = grp * 128 + 2 * (L / 3u);
-                if (r + 1 < n) ham_store2(&out[r], sm + n1l, n1h + n2);
-                else if (r < n) ham_store(&out[r], sm + n1l);
-            }
-        }
+    for (int u = 0; u < U; ++u) {
+        uint32_t d;
+        if constexpr (PAIR) d = ham32(x[u].x ^ y[u].x) + ham32(x[u].y ^ y[u].y) + ham32(x[u].z ^ y[u].z);
+        else d = ham32(x[u].x ^ c0) + ham32(x[u].y ^ c1) + ham32(x[u].z ^ c2);
+        d += swap_pair(d);
+        const uint64_t r = (g0 + u) * 32 + (lane >> 1);
+        if (!h && r < n) ham_store(&out[r], d);
     }
 }
 
@@ -938,6 +924,17 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     return ss_check(hipGetLastError(), "k_encode_var_dense");
 }
 
+int ss_encode_class_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, const uint64_t* d_sel,
+                         uint32_t dense_L, uint64_t m, uint32_t W, uint64_t* d_out, uint64_t* d_first_bad,
+                         void* stream) {
+    if (m == 0) return SS_OK;
+    if (W < 2 || W > 32) return ss_fail(SS_EARG, "class words must be in 2..32");
+    const unsigned grid = grid_for(m * (W + 1), kThreads, 0x7FFFFFFFu);
+    hipLaunchKernelGGL(k_encode_class, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, d_buf, d_offs, d_lens, d_sel,
+                       dense_L, m, W, 1.0 / (double)(W + 1), d_out, (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_encode_class");
+}
+
 int ss_decode_fixed(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr,
                     uint8_t* d_ascii, uint64_t stride, void* stream) {
     if (L > SS_MAX_NT) return ss_fail(SS_EARG, "L must be <= 1024");
@@ -981,15 +978,13 @@ static int launch_ham(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t
     const bool aligned = (((uintptr_t)a | (uintptr_t)(pair ? b : a)) & 15u) == 0 && (((uintptr_t)out) & 7u) == 0;
     if (wpr == W && aligned && W <= 32) {   // dense rows: the streaming kernel (W <= 32 keeps wl < 4096 exact)
         hipStream_t s = (hipStream_t)stream;
-        if (W == 3) {   // 96 nt (C3'): lane triples over whole 1-KiB chunks, no LDS (tools/tune_ham3.hip,
-                        // same box: 63-lane chunks 0.718, + one 8-B store per triple 0.750, 3-chunk
-                        // groups 0.779 of the 8-TB/s peak; one-wave blocks 0.761-0.779 -> 0.782-0.785)
-            constexpr int T = 64, G = 1;
-            const unsigned grid = grid_for(n, (uint64_t)128 * (T / 64) * G);
-            const uint4 *a4 = (const uint4*)a, *b4 = (const uint4*)b;
-            if (pair) hipLaunchKernelGGL((k_ham_dense3w<true, T, G>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
-            else hipLaunchKernelGGL((k_ham_dense3w<false, T, G>), dim3(grid), dim3(T), 0, s, a4, b4, b, n, out);
-            return ss_check(hipGetLastError(), "k_ham_dense3w");
+        if (W == 3) {   // 96 nt (C3'): lane pairs of dwordx3 halves, 4 x 32 reads per one-wave block
+            constexpr int T = 64, U = 4;
+            const unsigned grid = grid_for(n, (uint64_t)32 * (T / 64) * U);
+            const uint32_t *a32 = (const uint32_t*)a, *b32 = (const uint32_t*)b;
+            if (pair) hipLaunchKernelGGL((k_ham_dense3x<true, T, U>), dim3(grid), dim3(T), 0, s, a32, b32, b, n, out);
+            else hipLaunchKernelGGL((k_ham_dense3x<false, T, U>), dim3(grid), dim3(T), 0, s, a32, b32, b, n, out);
+            return ss_check(hipGetLastError(), "k_ham_dense3x");
         }
         // hamming vs one read on power-of-two W: small blocks (4-8 KiB of rows each) stream best
         // (tools/tune_ham.hip, same box: W 1 0.786 -> 0.850, 2 0.779 -> 0.844, 4 0.775 -> 0.801,

@@ -43,11 +43,14 @@ constexpr uint32_t kPartBlocks = 1024;      // partition passes: fixed grid, con
 constexpr uint32_t kMaxRegions = 32768;    // per-block region histogram in LDS (128 KB)
 }  // namespace
 
+constexpr int32_t kWordKeys = -2;
+
 struct ss_counter {
     uint64_t cap = 0;
     uint32_t log2cap = 0;
     uint32_t slice_log = 0;                // table = 2^(log2cap - slice_log) regions of 2^slice_log slots
-    int32_t L = -1;                        // length of every key in this handle (-1: not fixed yet)
+    int32_t L = -1;                        // length of every key in this handle (-1: not fixed yet,
+                                           // kWordKeys: packed multi-word keys, ss_counter_set_words)
     uint32_t W = 1;                        // words per key: 1 (L <= 32) or ceil(L/32) (multi-word keys)
     Slot* slots = nullptr;                 // [cap + 1]; multi-word: slot.key = 64-bit fingerprint
     uint64_t* keywords = nullptr;          // multi-word keys: [cap * W] the key words of slot s
@@ -2228,6 +2231,7 @@ uint64_t ss_counter_capacity(const ss_counter* c) { return c ? c->cap : 0; }
 
 static int fix_length(ss_counter* c, uint32_t L) {
     if (L > SS_MAX_NT) return ss_fail(SS_ETOO_LONG, "Sequences longer than 1024 bases are not supported.");
+    if (c->L == kWordKeys) return ss_fail(SS_EARG, "the handle holds packed multi-word keys");
     if (c->L >= 0) {
         if ((uint32_t)c->L != L) return ss_fail(SS_EARG, "all keys of one counter handle must share one length");
         return SS_OK;
@@ -2333,26 +2337,34 @@ int ss_counter_release(ss_counter* c) {
     return SS_OK;
 }
 
-int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L,
-                            uint64_t stride, uint64_t base_index, uint64_t* d_first_bad, void* stream) {
-    if (!c) return ss_fail(SS_EARG, "null counter");
-    if (!d_first_bad) return ss_fail(SS_EARG, "d_first_bad is required");
-    if (stride < L) return ss_fail(SS_EARG, "stride < L");
-    int rc = fix_length(c, L);
-    if (rc) return rc;
+// words_in: pre-packed multi-word rows (ss_counter_insert_words; d_ascii / L / stride / d_first_bad
+// unused), else ASCII reads of length L
+static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
+                       uint64_t base_index, uint64_t* d_first_bad, void* stream, const uint64_t* words_in) {
     hipStream_t s = (hipStream_t)stream;
-    rc = ss_check(set_u64(d_first_bad, true, s), "reset first_bad");
-    if (rc || n == 0) return rc;
-    if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
+    int rc = SS_OK;
+    if (!words_in) {
+        if (!d_first_bad) return ss_fail(SS_EARG, "d_first_bad is required");
+        if (stride < L) return ss_fail(SS_EARG, "stride < L");
+        if ((rc = fix_length(c, L))) return rc;
+        rc = ss_check(set_u64(d_first_bad, true, s), "reset first_bad");
+        if (rc || n == 0) return rc;
+        if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
+    } else if (n == 0) {
+        return SS_OK;
+    }
     if (base_index > kMaxIndex || n - 1 > kMaxIndex - base_index)
         return ss_fail(SS_EARG, "global read indices of a counter handle must stay below 2^32 - 1");
     c->occ_src = 0;   // set again below by the paths whose aggregate records the region occupancy
     Tbl t = tbl_of(c);
     const bool multi = c->W > 1;
-    const bool fast = (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
+    const bool fast = !words_in && (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
+    const uint64_t* mw = words_in;          // the multi-word rows the partition passes read
     if (multi) {
         // multi-word keys: always partitioned; grow the workspace to this batch if needed
         if (n > c->ws_reads && (rc = ss_counter_reserve(c, n)) != SS_OK) return rc;
+    }
+    if (multi && !words_in) {
         const uint64_t need = c->ws_reads * c->W;
         if (c->ws_words_cap < need) {
             if (c->ws_words) (void)hipFree(c->ws_words);
@@ -2366,6 +2378,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         }
         rc = ss_encode_fixed_impl(d_ascii, n, L, stride, c->ws_words, c->W, d_first_bad, nullptr, nullptr, stream);
         if (rc) return rc;
+        mw = c->ws_words;
     }
     // single-word keys of any other length / layout: pack into the key workspace first, then the
     // same partitioned passes (k_pc_hist replaces the fused encode of k_pc_keys)
@@ -2478,8 +2491,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
         }
         if (multi) {
             const size_t fp_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
-            hipLaunchKernelGGL((k_mw_fp<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1,
-                               (const uint64_t*)c->ws_words, n);
+            hipLaunchKernelGGL((k_mw_fp<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, mw, n);
         } else if (packed_keys) {
             const size_t h_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             hipLaunchKernelGGL((k_pc_hist<TF>), dim3(kPartBlocks), dim3(TF), h_lds, s, t, w, bins1, n);
@@ -2504,8 +2516,7 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
             w.bkey = w.akey;
         }
         if (multi)
-            hipLaunchKernelGGL((k_mw_aggregate<kMwT>), dim3(w.R), dim3(kMwT), mw_lds, s, t, w,
-                               (const uint64_t*)c->ws_words, base_index);
+            hipLaunchKernelGGL((k_mw_aggregate<kMwT>), dim3(w.R), dim3(kMwT), mw_lds, s, t, w, mw, base_index);
         else
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
@@ -2523,6 +2534,40 @@ int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, u
     hipLaunchKernelGGL(k_count_gen, dim3(grid), dim3(kThreads), 0, s, t, d_ascii, stride, n, L, base_index,
                        (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_count_gen");
+}
+
+int ss_counter_insert_fixed(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L,
+                            uint64_t stride, uint64_t base_index, uint64_t* d_first_bad, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->L == kWordKeys) return ss_fail(SS_EARG, "the handle holds packed multi-word keys (ss_counter_insert_words)");
+    return insert_impl(c, d_ascii, n, L, stride, base_index, d_first_bad, stream, nullptr);
+}
+
+int ss_counter_set_words(ss_counter* c, uint32_t W) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (W < 2 || W > 64) return ss_fail(SS_EARG, "packed keys of 2..64 words");
+    if (c->L == kWordKeys && c->W == W) return SS_OK;
+    if (c->L != -1) return ss_fail(SS_EARG, "the handle already holds keys of another kind");
+    if (c->keywords_W != W) {
+        if (c->keywords) (void)hipFree(c->keywords);
+        c->keywords = nullptr;
+        c->keywords_W = 0;
+        if (hipMalloc((void**)&c->keywords, c->cap * W * sizeof(uint64_t)) != hipSuccess) {
+            ss_check(hipGetLastError(), "counter key words hipMalloc");
+            return ss_fail(SS_ENOMEM, "counter key words: out of device memory");
+        }
+        c->keywords_W = W;
+    }
+    c->W = W;
+    c->L = kWordKeys;
+    return SS_OK;
+}
+
+int ss_counter_insert_words(ss_counter* c, const uint64_t* d_words, uint64_t n, uint64_t base_index, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->L != kWordKeys) return ss_fail(SS_EARG, "ss_counter_set_words first");
+    if (n && !d_words) return ss_fail(SS_EARG, "null buffer");
+    return insert_impl(c, nullptr, n, 0, 0, base_index, nullptr, stream, d_words);
 }
 
 int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_lens,

@@ -6,30 +6,35 @@
 //
 // Per chunk of reads (a staged list, or a FASTQ chunk ending after a newline):
 //   1. d_lens (u32 per read; FASTQ: ss_fastq_index_onepass, 0xFFFFFFFF = the reference's strlen
-//      underflow) -> stable split by length: k_len_count (per-block length histograms),
-//      k_len_binscan (block per length: offsets inside the length, its total and first read),
-//      k_len_binstart (one block: where each length starts), k_len_scatter
-//      (one wave per block, input order kept: a wave peels its distinct lengths with ballots, ranks by
-//      popcount) -> d_order = read indices grouped by length.  One 16-KB copy back (histogram + first).
-//   2. each length L in 1..1024: ss_gather_rows (dense rows) -> ss_counter_insert_fixed into the
-//      table of length L (the length is part of the dict key, short_seq_64.pyx:41-44); the rows'
-//      global read indices are appended to the table's row map (k_rowmap).  Length 0 is the empty
-//      ShortSeq (counted on the host side of the split); length > 1024 is the too-long error.
-//   3. first bad read: the inserts' first-bad words come back in one copy; the smallest global index
-//      of a rejected read is kept (and its bytes) — the reference raises at the first one in input
-//      order, so nothing after the chunk that holds it is read.
+//      underflow) -> stable split into bins: lengths 0..32 one bin each, lengths 33..1024 one bin per
+//      length class W = ceil(L/32) (2..32), and the too-long bin.  k_len_count (per-block bin
+//      histograms), k_len_binscan (block per bin: offsets inside the bin, its total and first read),
+//      k_len_binstart (one block: where each bin starts), k_len_scatter (one wave per block, input
+//      order kept: a wave peels its distinct bins with ballots, ranks by popcount) -> d_order = read
+//      indices grouped by bin.  One small copy back (totals, first reads, starts).
+//   2. a length L in 1..32: ss_gather_rows (dense rows) -> ss_counter_insert_fixed into the table of
+//      length L (the length is part of the dict key, short_seq_64.pyx:41-44).  A length class:
+//      k_encode_class packs each read straight from the chunk into W words + its length as one more
+//      word, and ss_counter_insert_words counts those rows in the class's table (key = (length,
+//      words), short_seq_192.pyx:35-41, short_seq_var.pyx:22-28): a 50-150 nt batch is 4 tables, not
+//      101.  Each insert's rows get their global read indices appended to the table's row map
+//      (k_rowmap).  Length 0 is the empty ShortSeq (counted on the host side of the split); length >
+//      1024 is the too-long error.
+//   3. first bad read: the inserts' first-bad words come back in one copy (a length's insert reports
+//      its row, a class its read); the smallest global index of a rejected read is kept (and its
+//      bytes) — the reference raises at the first one in input order, so nothing after the chunk
+//      that holds it is read.
 // Finish: every table's entries are placed at their global first index (k_place into a per-read
-// slot array), compacted in read order (k_flag_count / k_scan_* / k_compact: a stable stream
-// compaction), and gathered into (length u32, count u64, words u64[ceil(L/32)]) rows (k_gather_out,
-// word offsets by the same scan), copied into engine-owned pinned buffers.
+// slot array), compacted in read order (k_scan_*: a stable stream compaction), and gathered into
+// (length u32, count u64, words u64[ceil(L/32)]) rows (k_gather_out, word offsets by the same scan),
+// copied into engine-owned pinned buffers.
 //
-// Tables: one ss_counter per length, pooled across calls (reset is lazy).  Each starts at
-// 2 x the rows its length brings in the first chunk and, for single-word keys, grows (extract ->
-// merge into a table of twice the needed size) when the rows counted could push it past half full
-// (an exact size query decides; the query costs one sync and is skipped while rows <= capacity / 2).
-// Multi-word tables (L > 32) grow the same way through ss_counter_extract_words +
-// ss_counter_merge_words (a length rare in the first chunk and common later); they start
-// at 2 x the length's rows scaled by the file's remaining size.
+// Tables: one ss_counter per length (1..32) or length class, pooled across calls (reset is lazy).
+// Each starts at 2 x the rows its bin brings in the first chunk (a class: scaled by the FASTQ file's
+// remaining size) and grows (extract -> merge into a table of twice the needed size) when the rows
+// counted could push it past half full (an exact size query decides; the query costs one sync and is
+// skipped while rows <= capacity / 2); class tables grow through ss_counter_extract_words +
+// ss_counter_merge_words (a length rare in the first chunk and common later).
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -47,12 +52,18 @@
 
 namespace {
 
-constexpr uint32_t kLenBins = SS_MAX_NT + 2;        // lengths 0..1024, and 1025 = rejected (too long)
+// split bins: lengths 0..32 (one table per length), the multi-word length classes W = 2..32 (bins
+// 33..63: lengths 32(W-1)+1 .. 32W share one table), 64 = rejected (too long)
+constexpr uint32_t kClassBin0 = 31;                 // bin of class W = kClassBin0 + W
+constexpr uint32_t kTooLongBin = kClassBin0 + SS_MAX_NT / 32 + 1;
+constexpr uint32_t kLenBins = kTooLongBin + 1;
 constexpr uint32_t kSplitBlocks = 2048;             // k_len_count / k_len_scatter: one wave per block
 constexpr uint32_t kEmptyGroup = 0xFFFFFFFFu;       // slot marker of the empty read's entry
 constexpr uint64_t kNoSlot = ~0ull;
 
-__device__ __forceinline__ uint32_t len_bin(uint32_t L) { return L > SS_MAX_NT ? SS_MAX_NT + 1 : L; }
+__host__ __device__ __forceinline__ uint32_t len_bin(uint32_t L) {
+    return L > SS_MAX_NT ? kTooLongBin : L <= 32 ? L : kClassBin0 + (L + 31) / 32;
+}
 
 __global__ __launch_bounds__(64) void k_len_count(const uint32_t* __restrict__ lens, uint64_t n,
                                                   uint32_t* __restrict__ blkhist, uint32_t* __restrict__ blkfirst) {
@@ -190,8 +201,12 @@ struct GDesc {
     const uint64_t* words;   // [m * W]
     const uint64_t* counts;  // [m]
     uint32_t W;
-    uint32_t L;
+    uint32_t L;              // 0: a length class (entry length = its last word, ceil(L/32) words used)
 };
+
+__device__ __forceinline__ uint32_t entry_len(const GDesc& d, uint64_t e) {
+    return d.L ? d.L : (uint32_t)d.words[e * d.W + d.W - 1];
+}
 
 // item value for the two scans: MODE 0 = slot used (1/0), MODE 1 = words of ordered entry i
 template <int MODE>
@@ -199,7 +214,9 @@ __device__ __forceinline__ uint32_t item_val(const uint64_t* src, uint64_t i, co
     const uint64_t v = src[i];
     if (MODE == 0) return v != kNoSlot ? 1u : 0u;
     const uint32_t g = (uint32_t)(v >> 32);
-    return g == kEmptyGroup ? 0u : gd[g].W;
+    if (g == kEmptyGroup) return 0u;
+    const GDesc d = gd[g];
+    return d.L ? d.W : (entry_len(d, (uint32_t)v) + 31) / 32;
 }
 
 template <int MODE>
@@ -289,9 +306,11 @@ __global__ __launch_bounds__(256) void k_gather_out(const uint64_t* __restrict__
         }
         const uint64_t e = (uint32_t)v;
         const GDesc d = gd[g];
-        out_len[k] = d.L;
+        const uint32_t L = entry_len(d, e);
+        const uint32_t nw = d.L ? d.W : (L + 31) / 32;
+        out_len[k] = L;
         out_cnt[k] = d.counts[e];
-        for (uint32_t q = 0; q < d.W; ++q) out_words[woff[k] + q] = d.words[e * d.W + q];
+        for (uint32_t q = 0; q < nw; ++q) out_words[woff[k] + q] = d.words[e * d.W + q];
     }
 }
 
@@ -376,7 +395,8 @@ struct HBuf {
 };
 
 struct Group {
-    uint32_t L = 0;
+    uint32_t L = 0;               // 1..32: the length of every key; 0: a length class
+    uint32_t W1 = 1;              // words per table key: 1, or a class's ceil(L/32) + 1 (length word)
     ss_counter* table = nullptr;
     uint64_t cap = 0;
     uint64_t rows = 0;            // rows inserted (= the table's first index space)
@@ -401,7 +421,8 @@ struct ss_ingest {
     DBuf<uint32_t> blkhist, blkfirst;
     DBuf<uint64_t> split_out;      // [3 * kLenBins]
     uint64_t* h_split = nullptr;   // pinned [3 * kLenBins]
-    DBuf<uint8_t> rows;            // gathered dense rows
+    DBuf<uint8_t> rows;            // gathered dense rows (lengths <= 32)
+    DBuf<uint64_t> cls_words;      // a length class's packed rows (k_encode_class)
     DBuf<uint64_t> first_bad;      // one u64 per length of the chunk
     uint64_t* h_bad = nullptr;     // pinned [kLenBins + 2]
     DBuf<uint64_t> fq_ws, fq_aux, fq_counts;
@@ -464,13 +485,19 @@ int table_size(ss_ingest* g, ss_counter* t, uint64_t* out) {
     return rc;
 }
 
-// make room for m more rows in group gr (single-word keys grow by extract + merge)
+// key kind of a fresh table: the length (fixed by its first insert) or a class's packed words
+int table_kind(const Group& gr, ss_counter* t) {
+    return gr.L ? ss_counter_set_length(t, gr.L) : ss_counter_set_words(t, gr.W1);
+}
+
+// make room for m more rows in group gr (grow by extract + merge)
 int group_room(ss_ingest* g, Group& gr, uint64_t m) {
     if (gr.table && gr.rows + m <= gr.cap / 2) return SS_OK;
     if (!gr.table) {
-        const double scale = gr.L > 32 ? g->est_scale : 1.0;
+        const double scale = gr.L ? 1.0 : g->est_scale;
         gr.cap = std::min<uint64_t>(1ull << 32, pow2_at_least((uint64_t)(2.0 * (double)m * scale) + 2));
-        return table_get(g, gr.cap, &gr.table);
+        int rc = table_get(g, gr.cap, &gr.table);
+        return rc ? rc : table_kind(gr, gr.table);
     }
     uint64_t size = 0;
     int rc = table_size(g, gr.table, &size);
@@ -479,9 +506,9 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m) {
     const uint64_t ncap = pow2_at_least(2 * (size + m));
     ss_counter* nt = nullptr;
     if ((rc = table_get(g, ncap, &nt)) != SS_OK) return rc;
-    if ((rc = ss_counter_set_length(nt, gr.L)) != SS_OK) return rc;
+    if ((rc = table_kind(gr, nt)) != SS_OK) return rc;
     const uint64_t cap = gr.cap + 1;
-    const uint32_t W = gr.L <= 32 ? 1u : (gr.L + 31) / 32;
+    const uint32_t W = gr.W1;
     DBuf<uint64_t> k, c, f, pc, wd;
     DBuf<uint32_t> l;
     if ((rc = k.ensure(cap)) || (rc = c.ensure(cap)) || (rc = f.ensure(cap)) || (rc = l.ensure(cap)) ||
@@ -490,7 +517,7 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m) {
     if (W == 1) {
         rc = ss_counter_extract(gr.table, 1, k.p, l.p, c.p, f.p, cap, pc.p, g->stream);
         if (!rc) rc = ss_counter_merge(nt, k.p, l.p, c.p, f.p, size, g->stream);
-    } else {     // multi-word keys: the entries' words travel (equality is decided on them)
+    } else {     // packed-word keys: the entries' words travel (equality is decided on them)
         rc = ss_counter_extract_words(gr.table, 1, k.p, l.p, wd.p, c.p, f.p, cap, pc.p, g->stream);
         if (!rc) rc = ss_counter_merge_words(nt, wd.p, c.p, f.p, size, g->stream);
     }
@@ -519,12 +546,13 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     const uint64_t base = g->nreads;
     int rc = SS_OK;
     struct Job {
-        uint32_t L;
+        uint32_t bin;            // len_bin: a length 1..32 or a length class
         uint64_t m, start, first;
     };
     std::vector<Job> jobs;
     if (dense_L) {
-        jobs.push_back({dense_L, n, 0, 0});
+        if (dense_L > SS_MAX_NT) return ss_fail(SS_EARG, "ingest: dense length > 1024");
+        jobs.push_back({len_bin(dense_L), n, 0, 0});
     } else {
         if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins)))
@@ -540,47 +568,56 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest split");
         if (rc) return rc;
         const uint64_t* hh = g->h_split;
-        for (uint32_t L = 0; L < kLenBins; ++L) {
-            const uint64_t m = hh[L];
+        for (uint32_t b = 0; b < kLenBins; ++b) {
+            const uint64_t m = hh[b];
             if (!m) continue;
-            const uint64_t f = hh[kLenBins + L];
-            if (L == 0) {
+            const uint64_t f = hh[kLenBins + b];
+            if (b == 0) {
                 g->empty_count += m;
                 g->empty_first = std::min(g->empty_first, base + f);
-            } else if (L > SS_MAX_NT) {
+            } else if (b == kTooLongBin) {
                 if (base + f < g->bad_index) {
                     g->bad_index = base + f;
                     g->bad_kind = SS_ETOO_LONG;
                     g->bad_bytes.clear();
                 }
             } else {
-                jobs.push_back({L, m, hh[2 * kLenBins + L], f});
+                jobs.push_back({b, m, hh[2 * kLenBins + b], f});
             }
         }
     }
     if ((rc = g->first_bad.ensure(jobs.size() + 1))) return rc;
+    if (!jobs.empty() &&
+        (rc = ss_check(hipMemsetAsync(g->first_bad.p, 0xFF, jobs.size() * 8, s), "ingest first_bad reset")))
+        return rc;
     for (size_t j = 0; j < jobs.size(); ++j) {
         const Job& jb = jobs[j];
         if (base + jb.first > g->bad_index) continue;       // cannot hold the first error any more
-        Group& gr = g->groups[jb.L];
-        gr.L = jb.L;
+        const bool cls = jb.bin > 32;
+        Group& gr = g->groups[jb.bin];
+        gr.L = cls ? 0u : jb.bin;
+        gr.W1 = cls ? jb.bin - kClassBin0 + 1 : 1u;
         if ((rc = group_room(g, gr, jb.m))) return rc;
         if ((rc = gr.rowmap.ensure_keep(gr.rows + jb.m, gr.rows, s))) return rc;
-        const uint8_t* src;
-        uint64_t stride;
         const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
-        if (dense_L) {
-            src = d_buf;
-            stride = dense_L;
+        if (cls) {
+            // the class's rows packed straight from the chunk (no gather): W words + the length
+            if ((rc = g->cls_words.ensure(jb.m * gr.W1))) return rc;
+            rc = ss_encode_class_impl(d_buf, d_offs, d_lens, sel, dense_L, jb.m, gr.W1 - 1, g->cls_words.p,
+                                      g->first_bad.p + j, s);
+            if (!rc) rc = ss_counter_insert_words(gr.table, g->cls_words.p, jb.m, gr.rows, s);
         } else {
-            stride = (jb.L + 15) / 16 * 16;
-            if ((rc = g->rows.ensure(jb.m * stride))) return rc;
-            rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.L, g->rows.p, stride, s);
-            if (rc) return rc;
-            src = g->rows.p;
+            const uint8_t* src = d_buf;
+            uint64_t stride = dense_L;
+            if (!dense_L) {
+                stride = (jb.bin + 15) / 16 * 16;
+                if ((rc = g->rows.ensure(jb.m * stride))) return rc;
+                if ((rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.bin, g->rows.p, stride, s))) return rc;
+                src = g->rows.p;
+            }
+            if (jb.m >= (1u << 16) && jb.m < (1ull << 31)) (void)ss_counter_reserve(gr.table, jb.m);
+            rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, stride, gr.rows, g->first_bad.p + j, s);
         }
-        if (jb.m >= (1u << 16) && jb.m < (1ull << 31) && jb.L <= 32) (void)ss_counter_reserve(gr.table, jb.m);
-        rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.L, stride, gr.rows, g->first_bad.p + j, s);
         if (rc) return rc;
         hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, s, sel, jb.m, base, gr.rowmap.p + gr.rows);
         gr.rows += jb.m;
@@ -595,14 +632,19 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     for (size_t j = 0; j < jobs.size(); ++j) {
         const uint64_t fb = g->h_bad[j];
         if (fb == kNoSlot || base + jobs[j].first > g->bad_index) continue;
-        uint64_t idx = fb;           // row of the insert -> read of the chunk
-        if (!dense_L) {
+        // a length's insert reports its row (rows are in read order); a class reports the read
+        uint64_t idx = fb;
+        if (!dense_L && jobs[j].bin <= 32) {
             rc = ss_check(hipMemcpy(&idx, g->order.p + jobs[j].start + fb, 8, hipMemcpyDeviceToHost), "ingest bad row");
             if (rc) return rc;
         }
         if (base + idx < g->bad_index) {
             g->bad_index = base + idx;
             g->bad_kind = SS_EINVALID_BASE;
+            uint32_t L = dense_L ? dense_L : jobs[j].bin;
+            if (!dense_L && jobs[j].bin > 32 &&
+                (rc = ss_check(hipMemcpy(&L, d_lens + idx, 4, hipMemcpyDeviceToHost), "ingest bad len")))
+                return rc;
             uint64_t off = dense_L ? idx * dense_L : 0;
             if (h_offs) {
                 off = (*h_offs)[idx];
@@ -611,10 +653,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 return rc;
             }
             if (h_chunk) {
-                g->bad_bytes.assign((const char*)h_chunk + off, jobs[j].L);
+                g->bad_bytes.assign((const char*)h_chunk + off, L);
             } else {
-                g->bad_bytes.assign(jobs[j].L, '\0');
-                rc = ss_check(hipMemcpy(&g->bad_bytes[0], d_buf + off, jobs[j].L, hipMemcpyDeviceToHost), "ingest bad read");
+                g->bad_bytes.assign(L, '\0');
+                rc = ss_check(hipMemcpy(&g->bad_bytes[0], d_buf + off, L, hipMemcpyDeviceToHost), "ingest bad read");
                 if (rc) return rc;
             }
         }
@@ -949,7 +991,7 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
         Group& gr = kv.second;
         if (rc) break;
         if (!gr.table) continue;      // a length of an earlier call
-        const uint32_t W = gr.L <= 32 ? 1u : (gr.L + 31) / 32;
+        const uint32_t W = gr.W1;
         const uint64_t cap = gr.cap + 1;
         if ((rc = gr.fps.ensure(cap)) || (rc = gr.words.ensure(cap * W)) || (rc = gr.counts.ensure(cap)) ||
             (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)) || (rc = g->scan.ensure(kScanBlocks + 8)))

@@ -436,6 +436,37 @@ def test_counter_multiword_bad_read(gpu):
     c.close()
 
 
+@pytest.mark.parametrize("W,U,n", [(3, 5000, 200_000), (6, 100_000, 400_000), (33, 300, 20_000)])
+def test_counter_insert_words(gpu, W, U, n):
+    """Packed-word keys (ss_counter_set_words / ss_counter_insert_words, the drop-in engine's
+    length-class tables): rows compared whole, counts and first index against numpy over two
+    inserts; rows one word apart (incl. only the last word, the class's length word) stay apart."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(W)
+    pool = rng.integers(0, 1 << 62, size=(U, W), dtype=np.int64)
+    pool[1] = pool[0]
+    pool[1, W - 1] ^= 1                       # differs in the last word only
+    pool[2] = pool[0]
+    pool[2, 0] ^= 1 << 40                     # differs in the first word only
+    idx = rng.integers(0, U, size=n)
+    idx[:3] = [0, 1, 2]
+    rows = pool[idx]
+    c = B.GpuCounter(1 << max(12, int(2 * U).bit_length()), device=gpu)
+    h = n // 2
+    c.insert_words(torch.from_numpy(rows[:h]).to(gpu))
+    c.insert_words(torch.from_numpy(rows[h:]).to(gpu), base_index=h)
+    assert c.words == W and c.length == -2 and not c.overflowed()
+    words, cnt, f = c.items_sorted_words()
+    _u, first, counts = np.unique(idx, return_index=True, return_counts=True)
+    o = np.argsort(first)
+    assert np.array_equal(f, first[o]) and np.array_equal(cnt, counts[o])
+    assert np.array_equal(words.view(np.int64), rows[first[o]])
+    with pytest.raises(Exception):            # a packed-word handle takes no ASCII inserts
+        c.insert(B.synth_reads(10, 40, seed=1, device=gpu), 40)
+    c.close()
+
+
 @pytest.mark.parametrize("world,cap,U,n", [(3, 1 << 16, 20_000, 300_000), (8, 1 << 22, 500_000, 1_000_000),
                                            (2, 1 << 12, 300, 50_000)])
 def test_counter_region_owner_merge(gpu, oracle, world, cap, U, n):

@@ -70,6 +70,35 @@ def test_device_ingest_ragged_small(gpu, oracle, case):
     assert np.array_equal(gw, ew)
 
 
+def test_device_ingest_class_lengths_apart(gpu, oracle):
+    """One length class (33..64 nt) holds reads that pack to the same words at different lengths
+    (trailing 'A' = code 0): the class key's length word keeps them apart, as the reference's
+    (length, words) key does.  Plus a 96/97 boundary and a bad read inside a class."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(5)
+    s = "".join(rng.choice(list("ACGT"), 60))
+    t = "".join(rng.choice(list("ACGT"), 96))
+    base = [s[:40], s[:40] + "A", s[:40] + "AA", s[:39], s[:40] + "A", s[:64], s[:33], t, t + "A", t[:95],
+            s[:40] + "AA", "A" * 33, "A" * 34, "A" * 64, "A" * 33]
+    reads = [base[i] for i in rng.integers(0, len(base), 5000)] + base
+    enc = [r.encode() for r in reads]
+    lens = torch.tensor([len(r) for r in enc], dtype=torch.int32)
+    offs = torch.zeros(len(enc), dtype=torch.int64)
+    offs[1:] = torch.cumsum(lens.to(torch.int64), 0)[:-1]
+    blob = torch.frombuffer(bytearray(b"".join(enc) + b"\0" * 16), dtype=torch.uint8)
+    eng = B.DeviceIngest(gpu)
+    try:
+        eng.count(blob.to(gpu), offs.to(gpu), lens.to(gpu))
+        gl, gc, gw = eng.results()
+    finally:
+        eng.close()
+    exp = oracle.count(enc)
+    assert gl.tolist() == [L for (_w, L, _c, _f) in exp]
+    assert gc.tolist() == [c for (_w, _L, c, _f) in exp]
+    assert gw.tolist() == [int(x) for (w, _L, _c, _f) in exp for x in w]
+
+
 def test_device_ingest_ragged_errors(gpu):
     """A rejected read in a device batch raises the reference's message (the first in read order)."""
     import shortseq_amd as sq

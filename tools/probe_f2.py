@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""f2 engine probe: where the device-fed drop-in engine's wall time goes on the bench's ragged
+workload (50M reads of 50-150 nt): count (ss_ingest_add_device) vs results (ss_ingest_finish + copy
+back), per rep.  Run under `rocprofv3 --kernel-trace --stats` to set the kernel time beside it.
+
+    python tools/probe_f2.py [reps]
+"""
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO]
+import shortseq_amd.batch as B  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    dev = torch.device("cuda", 0)
+    blob, offs, lens = B.synth_ragged_pool_reads(50_000_000, 41, 42, 1 << 20, 50, 150, device=dev)
+    eng = B.DeviceIngest(dev)
+    for r in range(reps):
+        eng.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.count(blob, offs, lens)
+        t1 = time.perf_counter()
+        gl, _gc, _gw = eng.results()
+        t2 = time.perf_counter()
+        print(f"rep {r}: count {1e3 * (t1 - t0):.2f} ms  results {1e3 * (t2 - t1):.2f} ms  rows {len(gl)}",
+              flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -3,6 +3,7 @@
 // against the production launch before timing.  Same-box history of the kernel: 63-lane chunks with
 // two 4-B stores per triple 0.718 of 8 TB/s, one 8-B store 0.750, whole 1-KiB chunks in 3-chunk
 // groups 0.779.
+// The lane-pair dwordx3 form (k_ham_dense3x) is the production kernel since round 3.
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include tools/tune_ham3.hip -o tools/tune_ham3
 #include "../shortseq_amd/csrc/ss_codec.hip"
 #include "../shortseq_amd/csrc/ss_runtime.hip"
@@ -23,11 +24,11 @@ __global__ void k_fill_words(uint64_t* w, uint64_t n) {
     }
 }
 
-template <int T, int G>
-static void launch_w(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
-    const uint64_t per = (uint64_t)128 * (T / 64) * G;
-    hipLaunchKernelGGL((k_ham_dense3w<false, T, G>), dim3((unsigned)((n + per - 1) / per)), dim3(T), 0, 0,
-                       (const uint4*)a, (const uint4*)a, ref, n, out);
+template <int T, int U>
+static void launch_w(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {   // production
+    const uint64_t per = (uint64_t)32 * (T / 64) * U;
+    hipLaunchKernelGGL((k_ham_dense3x<false, T, U>), dim3((unsigned)((n + per - 1) / per)), dim3(T), 0, 0,
+                       (const uint32_t*)a, (const uint32_t*)a, ref, n, out);
 }
 
 // LDS-sum form with each read's per-word distances padded to 8 bytes (byte 8 rl + k), summed with one
@@ -184,41 +185,8 @@ static void launch_x4(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32
     hipLaunchKernelGGL((k_ham3_x4<T, G>), dim3((unsigned)(n / per)), dim3(T), 0, 0, (const uint4*)a, ref, n, out);
 }
 
-// x3 form: a read's 24 B as two dwordx3 halves in a lane pair (lane 2k: dwords 0-2 = word 0 and the
-// low half of word 1; lane 2k+1: dwords 3-5).  A wave-instruction loads 768 contiguous bytes (32
-// reads, six whole lines); the split at bit 32 of word 1 falls on a 2-bit boundary, so each lane's
-// three 32-bit XOR-collapse-popcounts plus one DPP pair swap give the read's distance, and the even
-// lanes store 32 consecutive distances (128 B).
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 template <int T, int U>
-__global__ __launch_bounds__(T) void k_ham3_x3(const uint32_t* __restrict__ a32, const uint64_t* __restrict__ ref,
-                                               uint64_t n, uint32_t* __restrict__ out) {
-    constexpr uint32_t NWV = T / 64;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, h = lane & 1u;
-    u32x3 x[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t g = ((uint64_t)blockIdx.x * NWV + wv) * U + u;    // group of 32 reads
-        x[u] = __builtin_nontemporal_load((const u32x3*)(a32 + g * 192 + 3 * lane));
-    }
-    const uint64_t r0 = ref[0], r1 = ref[1], r2 = ref[2];
-    const uint32_t c0 = h ? (uint32_t)(r1 >> 32) : (uint32_t)r0;
-    const uint32_t c1 = h ? (uint32_t)r2 : (uint32_t)(r0 >> 32);
-    const uint32_t c2 = h ? (uint32_t)(r2 >> 32) : (uint32_t)r1;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        uint32_t d = ham32(x[u].x ^ c0) + ham32(x[u].y ^ c1) + ham32(x[u].z ^ c2);
-        d += swap_pair(d);
-        const uint64_t r = (((uint64_t)blockIdx.x * NWV + wv) * U + u) * 32 + (lane >> 1);
-        if (!h && r < n) ham_store(&out[r], d);
-    }
-}
-
-template <int T, int U>
-static void launch_x3(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
-    const uint64_t per = (uint64_t)32 * (T / 64) * U;   // whole groups only (n a multiple of per)
-    hipLaunchKernelGGL((k_ham3_x3<T, U>), dim3((unsigned)(n / per)), dim3(T), 0, 0, (const uint32_t*)a, ref, n, out);
-}
+static void launch_x3(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) { launch_w<T, U>(a, ref, n, out); }
 
 template <int T, int G>
 static void launch_glds(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
@@ -237,7 +205,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d1, n * 4));
     hipLaunchKernelGGL(k_fill_words, dim3(8192), dim3(256), 0, 0, w, n * 3);
     CK(hipMemcpy(ref, w + 3 * 12345, 24, hipMemcpyDeviceToDevice));
-    launch_w<64, 1>(w, ref, n, d0);
+    launch_w<64, 4>(w, ref, n, d0);
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> h0(n), h1(n);
     CK(hipMemcpy(h0.data(), d0, n * 4, hipMemcpyDeviceToHost));
@@ -261,8 +229,8 @@ int main(int argc, char** argv) {
         printf("%-28s %s  %.4f ms  %.3f of 8 TB/s\n", name, ok ? "OK " : "BAD", ms, n * 28.0 / (ms * 1e-3) / 8e12);
     };
     for (int pass = 0; pass < 3; ++pass) {
-        run("prod T64 G1", launch_w<64, 1>);
-        run("T128 G1", launch_w<128, 1>);
+        run("prod x3 T64 U4", launch_w<64, 4>);
+        run("prod x3 T128 U2", launch_w<128, 2>);
         run("x4 T64 G1", launch_x4<64, 1>);
         run("x3 T64 U4", launch_x3<64, 4>);
         run("x3 T64 U8", launch_x3<64, 8>);
