@@ -372,6 +372,9 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
             nul |= has_nul(x[j]) | has_nul(x[j + 1]);
         }
     }
+    // the wave's NUL verdict now: left to its use at the end, the compiler keeps the chunks live
+    // through the whole kernel (96 VGPRs, 5 waves per SIMD, instead of 62 and 8)
+    const bool any_nul = __ballot(nul) != 0;
     uint64_t packed[kFqU1 / 4], excl[kFqU1 / 4], total[kFqU1 / 4];
 #pragma unroll
     for (int k = 0; k < kFqU1 / 4; ++k) packed[k] = 0;
@@ -441,7 +444,7 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
             put(s_run);
         }
     }
-    if (__ballot(nul)) {                   // rare: reload the lane's chunks (keeps them out of VGPRs)
+    if (any_nul) {                         // rare: reload the lane's chunks (keeps them out of VGPRs)
 #pragma unroll 1
         for (int j = 0; j < kFqU1; ++j) {
             const uint64_t off = t0 + 16ull * (j * kFqT + threadIdx.x);
@@ -514,9 +517,42 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
         const uint32_t prev = tile ? st.tile_last[tile - 1] : kNone32;
         // start of the tile's first line: after the previous newline (0 for the chunk's first line)
         uint64_t carry = lbase == line0 ? 0 : (prev != kNone32 ? (uint64_t)prev + 1 : kNone64);
-        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+        const uint32_t tb = (uint32_t)(tile * kFqTile1);
+        if (run >= kStageShards * st.region) {
+            // a fixed run (16-B aligned): 8 positions per lane per load, 512 per wave round (a tile's
+            // ~550 newlines in two rounds instead of nine dependent 64-wide ones)
+            for (uint32_t k0 = 0; k0 < cnt; k0 += 512) {
+                const uint32_t kb = k0 + 8u * lane;
+                const uint32_t nv = kb < cnt ? min(8u, cnt - kb) : 0u;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (nv) v = *(const uint4*)(st.pos + run + kb);
+                const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+                uint32_t pp[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) pp[q] = tb + ((vw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
+                uint32_t lastp = pp[7];
+#pragma unroll
+                for (int q = 0; q < 7; ++q)
+                    if ((uint32_t)q + 1 == nv) lastp = pp[q];
+                const uint32_t below = (uint32_t)__shfl_up((int)lastp, 1);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint64_t li = lbase + kb + q;
+                    if ((uint32_t)q < nv && (li & 3u) == 1u) {
+                        const uint64_t i = (li >> 2) - o.sel0;
+                        if (i < o.max_reads) {
+                            uint64_t start = q ? (uint64_t)pp[q - 1] + 1 : (lane ? (uint64_t)below + 1 : carry);
+                            if (start == kNone64) start = start_before(st, tile);
+                            o.offsets[i] = start;
+                            lens[i] = fq_len((uint64_t)pp[q] - start + 1);
+                        }
+                    }
+                }
+                carry = (uint64_t)(uint32_t)__shfl((int)pp[7], 63) + 1;
+            }
+        } else for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
             const uint32_t k = k0 + lane;
-            const uint32_t p = (uint32_t)(tile * kFqTile1) + st.pos[run + min(k, cnt - 1)];
+            const uint32_t p = tb + st.pos[run + min(k, cnt - 1)];
             const uint32_t below = (uint32_t)__shfl_up((int)p, 1);
             const uint64_t li = lbase + k;
             if (k < cnt && (li & 3u) == 1u) {
@@ -739,8 +775,8 @@ int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at
 }
 
 // one-pass workspace: tile_base u64 [t + 1] | group_base u64 [g + 1] | used u32 [64 x 32] | ovf u32,
-// nul_cnt u32 | nul_pos u32 [kNulCap] | tile_cnt u32 [t] | tile_run u32 [t] | tile_last u32 [t] |
-// pos u32 [64 x region]
+// nul_cnt u32, 2 pad u32 | nul_pos u32 [kNulCap] | tile_cnt u32 [t] | tile_run u32 [t] | tile_last u32 [t] |
+// pos u16 [64 x region + t x kTileCap] (256-B aligned)
 inline uint64_t fq_tiles1(uint64_t nbytes) { return (nbytes + kFqTile1 - 1) / kFqTile1; }
 
 // staging words per shard: the lines max_reads implies (4 per sequence line) + 25 %, spread over the
@@ -752,8 +788,8 @@ inline uint64_t fq_region(uint64_t max_reads) {
 
 uint64_t ss_fastq_onepass_ws_bytes(uint64_t nbytes, uint64_t max_reads) {
     const uint64_t t = fq_tiles1(nbytes);
-    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 8 + 4ull * kNulCap + 12 * t +
-           2 * kStageShards * fq_region(max_reads) + 2ull * kTileCap * t + 16;
+    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 16 + 4ull * kNulCap + 12 * t +
+           2 * kStageShards * fq_region(max_reads) + 2ull * kTileCap * t + 256;
 }
 
 int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at_eof, void* d_ws,
@@ -772,13 +808,15 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     st.used = (uint32_t*)(group_base + g + 1);
     st.ovf = st.used + kStageShards * kShardStride;
     st.nul_cnt = st.ovf + 1;
-    st.nul_pos = st.ovf + 2;
+    st.nul_pos = st.ovf + 4;      // two pad words: the reset below is one 16-B-sized fill, not two
     st.tile_cnt = st.nul_pos + kNulCap;
     st.tile_run = st.tile_cnt + t;
     st.tile_last = st.tile_run + t;
-    st.pos = (uint16_t*)(((uintptr_t)(st.tile_last + t) + 7) & ~(uintptr_t)7);   // 8-B aligned (the fixed runs' copies)
+    // 256-B aligned: the fixed runs (4 KiB apart) are then 16-B aligned for k_fq_place's wide loads
+    st.pos = (uint16_t*)(((uintptr_t)(st.tile_last + t) + 255) & ~(uintptr_t)255);
     st.region = fq_region(max_reads);
-    rc = ss_check(hipMemsetAsync(st.used, 0, 4 * (kStageShards * kShardStride + 2), s), "fastq staging reset");
+    static_assert((4 * (kStageShards * kShardStride + 4)) % 16 == 0, "one fill packet");
+    rc = ss_check(hipMemsetAsync(st.used, 0, 4 * (kStageShards * kShardStride + 4), s), "fastq staging reset");
     if (rc) return rc;
     FqOut o = fq_out(d_offsets, d_aux, st.nul_cnt, max_reads, line0, nbytes);
     o.nul_list = st.nul_pos;
