@@ -340,11 +340,18 @@ int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_
  *                       [nkeys], words u64 (entry k's max(0, ceil(L/32)) words follow entry k-1's; a
  *                       length-0 entry is the empty read and has none).
  *   ss_ingest_reset:    drop the counts (tables are pooled for the next call).
+ *   ss_ingest_set_exact: 1 = size every length class's table by its rows (the 2 x rows bound).  By
+ *                       default a class table (lengths 33..1024, one per ceil(L/32)) is sized by a
+ *                       HyperLogLog sketch of its distinct keys over the call (1.2 x the estimate +
+ *                       256, at most half full); a table that still runs full makes the add call
+ *                       return SS_EFULL, and the caller counts again with exact sizing (the drop-in
+ *                       front does).  New in this ABI version; the reference dict has no sizing.
  * ---------------------------------------------------------------------------------------------- */
 typedef struct ss_ingest ss_ingest;
 int ss_ingest_create(int device, ss_ingest** h_out);
 int ss_ingest_destroy(ss_ingest* g);
 int ss_ingest_reset(ss_ingest* g);
+int ss_ingest_set_exact(ss_ingest* g, int exact);
 int ss_ingest_staging(ss_ingest* g, uint64_t nbytes, uint8_t** h_ptr);
 int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_lens, uint64_t n);
 int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, uint64_t* h_nseqs);

@@ -22,7 +22,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ._native import SsErr, check, lib
+from ._native import SS_EFULL, SsErr, check, lib
 
 MAX_NT = 1024
 _NO_BAD = -1  # UINT64_MAX viewed as int64
@@ -444,12 +444,15 @@ class DeviceIngest:
     words u64) numpy arrays in first-occurrence order (the ShortSeqCounter dict order: row k has
     ceil(lens[k] / 32) words, one for lengths 0..32).  A rejected read raises like ShortSeqCounter."""
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, exact: bool = False):
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         h = C.c_void_p()
         check(lib().ss_ingest_create(dev.index or 0, C.byref(h)), "ss_ingest_create")
         self._h = h
+        self._exact = exact
+        self._fresh = True
+        check(lib().ss_ingest_set_exact(h, int(exact)), "ss_ingest_set_exact")
 
     def count(self, blob: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor) -> None:
         for t, name in ((blob, "blob"), (offsets, "offsets"), (lens, "lens")):
@@ -457,8 +460,17 @@ class DeviceIngest:
         if offsets.dtype != torch.int64 or lens.dtype not in (torch.int32, torch.uint32) or blob.dtype != torch.uint8:
             raise TypeError("blob u8, offsets int64, lens int32")
         torch.cuda.current_stream(self.device).synchronize()   # the engine runs on its own stream
-        check(lib().ss_ingest_add_device(self._h, blob.data_ptr(), blob.numel(), offsets.data_ptr(), lens.data_ptr(),
-                                         lens.numel()), "ss_ingest_add_device")
+        args = (self._h, blob.data_ptr(), blob.numel(), offsets.data_ptr(), lens.data_ptr(), lens.numel())
+        rc = lib().ss_ingest_add_device(*args)
+        if rc == SS_EFULL and self._fresh and not self._exact:
+            # a length class's table, sized by its distinct-key sketch, ran full: the first batch of the
+            # count is counted again with tables sized by their rows (later batches cannot be redone)
+            check(lib().ss_ingest_reset(self._h), "ss_ingest_reset")
+            check(lib().ss_ingest_set_exact(self._h, 1), "ss_ingest_set_exact")
+            rc = lib().ss_ingest_add_device(*args)
+            check(lib().ss_ingest_set_exact(self._h, 0), "ss_ingest_set_exact")
+        check(rc, "ss_ingest_add_device")
+        self._fresh = False
         idx, kind, ln = C.c_uint64(), C.c_int(), C.c_uint64()
         check(lib().ss_ingest_error(self._h, C.byref(idx), C.byref(kind), None, 0, C.byref(ln)), "ss_ingest_error")
         if idx.value != (1 << 64) - 1:
@@ -482,6 +494,7 @@ class DeviceIngest:
 
     def reset(self) -> None:
         check(lib().ss_ingest_reset(self._h), "ss_ingest_reset")
+        self._fresh = True
 
     def close(self) -> None:
         if self._h:

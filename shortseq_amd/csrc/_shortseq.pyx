@@ -49,6 +49,7 @@ cdef extern from "shortseq_amd.h":
         pass
     enum:
         SS_ETOO_LONG
+        SS_EFULL
 
 cdef extern from "dlfcn.h":
     void* dlopen(const char* filename, int flag) nogil
@@ -74,6 +75,7 @@ ctypedef int (*f_results)(ss_ingest*, const uint32_t**, const uint64_t**, const 
 ctypedef int (*f_get_device)(int*) noexcept nogil
 ctypedef int (*f_fastq_split)(const char*, uint32_t, uint64_t*, uint64_t*) noexcept nogil
 ctypedef int (*f_add_fastq_range)(ss_ingest*, const char*, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t*) noexcept nogil
+ctypedef int (*f_set_exact)(ss_ingest*, int) noexcept nogil
 
 cdef struct _Abi:
     f_device_count device_count
@@ -89,6 +91,7 @@ cdef struct _Abi:
     f_get_device get_device
     f_fastq_split fastq_split
     f_add_fastq_range add_fastq_range
+    f_set_exact set_exact
 
 cdef _Abi _abi
 cdef bint _abi_ready = False
@@ -123,6 +126,7 @@ cdef int _bind_abi() except -1:
     _abi.get_device = <f_get_device>_sym(h, b"ss_get_device")
     _abi.fastq_split = <f_fastq_split>_sym(h, b"ss_fastq_split")
     _abi.add_fastq_range = <f_add_fastq_range>_sym(h, b"ss_ingest_add_fastq_range")
+    _abi.set_exact = <f_set_exact>_sym(h, b"ss_ingest_set_exact")
     _abi_ready = True
     return 0
 
@@ -716,6 +720,18 @@ def _shard_work(size_t gh, int kind, size_t blob, size_t lens, uint64_t n, bytes
             rc = _abi.add_blob(g, <const uint8_t*>blob, <const uint32_t*>lens, n)
         else:
             rc = _abi.add_fastq_range(g, cpath, begin, end, line0, chunk, nseqs)
+        if rc == SS_EFULL:
+            # a length class's table, sized by its distinct-key sketch, ran full (the sketch
+            # under-estimated): the shard is counted again with tables sized by their rows
+            rc = _abi.reset(g)
+            if rc == 0:
+                rc = _abi.set_exact(g, 1)
+            if rc == 0:
+                if kind == 0:
+                    rc = _abi.add_blob(g, <const uint8_t*>blob, <const uint32_t*>lens, n)
+                else:
+                    rc = _abi.add_fastq_range(g, cpath, begin, end, line0, chunk, nseqs)
+            _abi.set_exact(g, 0)
         if rc == 0:
             rc = _abi.error(g, &bad_idx, &bad_kind, NULL, 0, NULL)
         if rc == 0 and bad_idx == <uint64_t>-1:

@@ -222,14 +222,26 @@ __device__ __forceinline__ uint64_t encode_word_at(const uint8_t* p, uint32_t nb
 // inside chunks the read touches: no fault past the buffer's last 16-B chunk) realigned by a
 // funnel shift; bytes past nb become 'A'.  Against nine dword loads per lane: a third of the load
 // instructions, each touching half the cache lines.
-__device__ __forceinline__ uint64_t encode_word_q(const uint8_t* p, uint32_t nb, bool table, uint32_t& bad) {
+struct Chunks3 {
+    uint4 c0, c1, c2;
+    uint32_t sh;
+};
+
+__device__ __forceinline__ Chunks3 load_word_q(const uint8_t* p, uint32_t nb) {
     const uintptr_t addr = (uintptr_t)p;
     const uint4* q = (const uint4*)(addr & ~(uintptr_t)15);
-    const uint32_t sh = (uint32_t)(addr & 15);
-    const uint32_t last = (sh + nb - 1u) >> 4;      // 0..2: the chunk holding the word's last byte
-    const uint4 c0 = q[0], c1 = q[min(1u, last)], c2 = q[min(2u, last)];
-    const uint32_t d[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
-    const uint32_t s4 = sh >> 2, sb = sh & 3u;
+    Chunks3 c;
+    c.sh = (uint32_t)(addr & 15);
+    const uint32_t last = (c.sh + nb - 1u) >> 4;    // 0..2: the chunk holding the word's last byte
+    c.c0 = q[0];
+    c.c1 = q[min(1u, last)];
+    c.c2 = q[min(2u, last)];
+    return c;
+}
+
+__device__ __forceinline__ uint64_t pack_word_q(const Chunks3& c, uint32_t nb, bool table, uint32_t& bad) {
+    const uint32_t d[12] = {c.c0.x, c.c0.y, c.c0.z, c.c0.w, c.c1.x, c.c1.y, c.c1.z, c.c1.w, c.c2.x, c.c2.y, c.c2.z, c.c2.w};
+    const uint32_t s4 = c.sh >> 2, sb = c.sh & 3u;
     // e[k] = d[k + s4] (s4 < 4) by two masked selects on constant indices: written as a ternary on
     // the index, the compiler turns the 12 dwords into a scratch array indexed at run time
     const uint32_t m1 = 0u - (s4 & 1u), m2 = 0u - ((s4 >> 1) & 1u);
@@ -255,6 +267,10 @@ __device__ __forceinline__ uint64_t encode_word_q(const uint8_t* p, uint32_t nb,
     Enc32 hi = encode16(xw[4], xw[5], xw[6], xw[7], table);
     bad |= lo.bad | hi.bad;
     return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
+}
+
+__device__ __forceinline__ uint64_t encode_word_q(const uint8_t* p, uint32_t nb, bool table, uint32_t& bad) {
+    return pack_word_q(load_word_q(p, nb), nb, table, bad);
 }
 
 // Ragged batches (ss_encode_var): one lane per output word, dense -- lane g writes out[g], word
@@ -317,6 +333,130 @@ __global__ __launch_bounds__(kThreads) void k_encode_class(const uint8_t* in, co
         }
         out[g] = word;
         report_bad(bad != 0u, r, first_bad);
+    }
+}
+
+// Drop-in engine, every multi-word length class of a chunk in one pass, in read order (the blob is
+// read once; per class, k_encode_class re-reads the lines its rows share with other classes').  A
+// block takes kClsTile consecutive reads.  Within the tile the reads of class W hold consecutive rows
+// of W's block (k_len_scatter is stable), so the tile's rows of a class are one contiguous span:
+//   a. per read: class W = ceil(L/32) (L 33..1024), its row (posof[r] - binstart[bin0 + W]); per
+//      class the tile's first row and count (LDS atomics); a scan of W + 1 over the reads
+//   b. lane per word slot in read order (k_encode_var_dense's access pattern: consecutive lanes,
+//      consecutive words of consecutive reads): word w < W packed (encode_word_q), w == W = the
+//      length, into the tile's LDS copy of its class spans; the read's 64-bit hash folded by an LDS
+//      xor (the row's words, mixed)
+//   c. the spans out with dense stores (a per-class run of whole rows), and each read's hash into
+//      class W's HyperLogLog registers (2^kHllLog per class, max of the rank), which the engine
+//      reads to size each class's table by its distinct keys rather than by its reads.
+// (A lane-per-read-slot form with the rows stored straight from registers measured 3.6 ms against
+// 2.75 for the four per-class passes on the f2 batch: its row stores land 24-48 B at a time.)
+struct ClassOut {
+    uint64_t woff[33];
+    uint32_t bin0;
+};
+constexpr uint32_t kClsTile = 256;
+
+template <int MAXW1>
+__global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, const uint64_t* __restrict__ offs,
+                                                             const uint32_t* __restrict__ lens, uint64_t n,
+                                                             const uint32_t* __restrict__ posof,
+                                                             const uint64_t* __restrict__ binstart, ClassOut co,
+                                                             uint64_t* __restrict__ out, uint32_t* hll,
+                                                             unsigned long long* first_bad) {
+    __shared__ uint64_t sw[kClsTile * MAXW1];             // the tile's class spans, class after class
+    __shared__ unsigned long long sfp[kClsTile];
+    __shared__ uint64_t soff[kClsTile];
+    __shared__ uint32_t srow[kClsTile];                   // row within the tile's span of its class
+    __shared__ uint16_t sqoff[kClsTile + 1], sL[kClsTile];
+    __shared__ uint8_t smap[kClsTile * MAXW1];            // word slot -> read of the tile
+    __shared__ uint32_t rmin[33], rcnt[33], cbase[34], wsum[kClsTile / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint64_t r0 = (uint64_t)blockIdx.x * kClsTile, r = r0 + t;
+    if (t < 33) {
+        rmin[t] = 0xFFFFFFFFu;
+        rcnt[t] = 0;
+    }
+    __syncthreads();
+    // a. classes, rows, spans
+    const uint32_t L = r < n ? lens[r] : 0u;
+    const bool cls = L > 32u && L <= SS_MAX_NT;
+    const uint32_t W = cls ? (L + 31u) / 32u : 0u, w1 = cls ? W + 1u : 0u;
+    uint32_t row = 0;
+    if (cls) {
+        row = posof[r] - (uint32_t)binstart[co.bin0 + W];
+        atomicMin(&rmin[W], row);
+        atomicAdd(&rcnt[W], 1u);
+        soff[t] = offs[r];
+    }
+    sL[t] = (uint16_t)(cls ? L : 0u);
+    sfp[t] = 0;
+    uint32_t inc = w1;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d);
+        if (lane >= d) inc += y;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t v = 0; v < wave; ++v) before += wsum[v];
+    const uint32_t q0 = before + inc - w1;
+    sqoff[t] = (uint16_t)q0;
+    if (t == kClsTile - 1) sqoff[kClsTile] = (uint16_t)(q0 + w1);
+    for (uint32_t k = 0; k < w1; ++k) smap[q0 + k] = (uint8_t)t;
+    if (cls) srow[t] = row - rmin[W];
+    if (t == 0) {
+        uint32_t c = 0;
+        for (uint32_t v = 0; v < 33; ++v) {
+            cbase[v] = c;
+            c += v >= 2 ? rcnt[v] * (v + 1u) : 0u;
+        }
+        cbase[33] = c;
+    }
+    __syncthreads();
+    // b. lane per word slot, read order (a form issuing four slots' loads before packing any: 107
+    //    VGPRs, 3.0 vs 2.6 ms on the f2 batch)
+    const uint32_t Q = sqoff[kClsTile];
+    for (uint32_t q = t; q < Q; q += kClsTile) {
+        const uint32_t tt = smap[q];
+        const uint32_t LL = sL[tt], WW = (LL + 31u) / 32u, w = q - sqoff[tt];
+        uint32_t bad = 0;
+        uint64_t word = LL;
+        if (w < WW) {
+            const uint32_t nb = min(32u, LL - 32u * w);
+            word = encode_word_q(in + soff[tt] + 32u * w, nb, nb < 32u, bad);
+        }
+        sw[cbase[WW] + srow[tt] * (WW + 1u) + w] = word;
+        atomicXor(&sfp[tt], (unsigned long long)splitmix64(word ^ (0x9E3779B97F4A7C15ull * (w + 1))));
+        report_bad(bad != 0u, r0 + tt, first_bad);
+    }
+    __syncthreads();
+    // c. the class spans out (dense), the sketches
+    for (uint32_t q = t; q < Q; q += kClsTile) {
+        uint32_t lo = 2, hi = 33;                          // the class whose span holds q: cbase[lo] <= q
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (cbase[mid] <= q) lo = mid; else hi = mid;
+        }
+        out[co.woff[lo] + (uint64_t)rmin[lo] * (lo + 1u) + (q - cbase[lo])] = sw[q];
+    }
+    if (cls) {
+        const uint64_t h = sfp[t];
+        uint32_t* reg = hll + ((uint64_t)W << kHllLog) + (uint32_t)(h >> (64 - kHllLog));
+        const uint32_t rho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
+        if (*reg < rho) atomicMax(reg, rho);    // registers settle early: most reads only load
+    }
+}
+
+// The same registers from rows already packed (k_encode_class's paths): lane per row, the same hash.
+__global__ __launch_bounds__(kThreads) void k_hll_rows(const uint64_t* __restrict__ rows, uint64_t m, uint32_t W1,
+                                                       uint32_t* hll) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kThreads) {
+        uint64_t h = 0;
+        for (uint32_t w = 0; w < W1; ++w) h ^= splitmix64(rows[i * W1 + w] ^ (0x9E3779B97F4A7C15ull * (w + 1)));
+        uint32_t* reg = hll + (uint32_t)(h >> (64 - kHllLog));
+        const uint32_t rho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
+        if (*reg < rho) atomicMax(reg, rho);
     }
 }
 
@@ -922,6 +1062,33 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     hipLaunchKernelGGL(k_encode_var_dense, dim3(grid), dim3(kThreads), 0, s, d_ascii, d_offsets, d_lens, n, d_words,
                        wpr, 1.0 / (double)wpr, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_var_dense");
+}
+
+int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
+                           const uint32_t* d_posof, const uint64_t* d_binstart, const uint64_t* h_woff, uint32_t bin0,
+                           uint32_t w1max, uint64_t* d_out, uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
+    if (n == 0) return SS_OK;
+    if (w1max > 16) return ss_fail(SS_EARG, "k_encode_classes: classes of up to 15 words");
+    ClassOut co;
+    for (int W = 0; W < 33; ++W) co.woff[W] = h_woff[W];
+    co.bin0 = bin0;
+    const uint64_t blocks = (n + kClsTile - 1) / kClsTile;
+    if (blocks > 0x7FFFFFFFull) return ss_fail(SS_EARG, "chunk too large for k_encode_classes");
+    hipStream_t s = (hipStream_t)stream;
+    if (w1max <= 8)
+        hipLaunchKernelGGL((k_encode_classes<8>), dim3((unsigned)blocks), dim3(kClsTile), 0, s, d_buf, d_offs, d_lens, n,
+                           d_posof, d_binstart, co, d_out, d_hll, (unsigned long long*)d_first_bad);
+    else
+        hipLaunchKernelGGL((k_encode_classes<16>), dim3((unsigned)blocks), dim3(kClsTile), 0, s, d_buf, d_offs, d_lens, n,
+                           d_posof, d_binstart, co, d_out, d_hll, (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_encode_classes");
+}
+
+int ss_hll_rows_impl(const uint64_t* d_rows, uint64_t m, uint32_t W1, uint32_t* d_hll, void* stream) {
+    if (m == 0) return SS_OK;
+    hipLaunchKernelGGL(k_hll_rows, dim3(grid_for(m, kThreads, 4096)), dim3(kThreads), 0, (hipStream_t)stream, d_rows, m,
+                       W1, d_hll);
+    return ss_check(hipGetLastError(), "k_hll_rows");
 }
 
 int ss_encode_class_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, const uint64_t* d_sel,

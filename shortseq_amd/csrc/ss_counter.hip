@@ -1955,16 +1955,26 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
         const uint32_t idx = w.bidx[e];
         const uint64_t tag = (fp >> 32) << 32;
         uint32_t ls = (uint32_t)((fp * 0x9E3779B97F4A7C15ull) >> lds_shift) & (LS - 1);
-        for (;;) {
-            unsigned long long cur = lkey[ls];
+        bool placed = false;
+        for (uint32_t probe = 0; probe < LS; ++probe) {   // bounded: a region with > 2S distinct keys
+            unsigned long long cur = lkey[ls];           // (an undersized table) raises the overflow word
             if (cur == kEmpty) {
                 cur = atomicCAS(&lkey[ls], (unsigned long long)kEmpty, (unsigned long long)(tag | idx));
-                if (cur == kEmpty) break;   // claimed, this read is the representative
+                if (cur == kEmpty) {   // claimed, this read is the representative
+                    placed = true;
+                    break;
+                }
             }
             if ((cur & 0xFFFFFFFF00000000ull) == tag &&
-                words_eq(words + (cur & 0xFFFFFFFFull) * W, words + (uint64_t)idx * W, W))
+                words_eq(words + (cur & 0xFFFFFFFFull) * W, words + (uint64_t)idx * W, W)) {
+                placed = true;
                 break;
+            }
             ls = (ls + 1) & (LS - 1);
+        }
+        if (!placed) {
+            atomicOr(t.overflow, kOvfTable);
+            continue;
         }
         atomicAdd(&lcnt[ls], 1u);
         atomicMin(&lfst[ls], idx);

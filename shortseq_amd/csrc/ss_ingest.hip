@@ -42,6 +42,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <map>
 #include <string>
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(1024) void k_len_binstart(uint64_t* __restrict__ ou
 // advances that length's LDS cursor
 __global__ __launch_bounds__(64) void k_len_scatter(const uint32_t* __restrict__ lens, uint64_t n,
                                                     const uint32_t* __restrict__ blkoff, const uint64_t* __restrict__ split,
-                                                    uint64_t* __restrict__ order) {
+                                                    uint64_t* __restrict__ order, uint32_t* __restrict__ posof) {
     __shared__ uint32_t cur[kLenBins];
     for (uint32_t b = threadIdx.x; b < kLenBins; b += 64)
         cur[b] = (uint32_t)split[2 * kLenBins + b] + blkoff[(uint64_t)b * gridDim.x + blockIdx.x];
@@ -170,7 +171,11 @@ __global__ __launch_bounds__(64) void k_len_scatter(const uint32_t* __restrict__
             const uint32_t b0 = (uint32_t)__shfl((int)b, leader);
             const uint64_t mine = __ballot(live && b == b0);
             const uint32_t base = cur[b0];
-            if (live && b == b0) order[base + __popcll(mine & lt)] = i;
+            if (live && b == b0) {
+                const uint32_t pos = base + (uint32_t)__popcll(mine & lt);
+                order[pos] = i;
+                posof[i] = pos;                 // read -> its place in d_order (k_encode_classes)
+            }
             __syncthreads();   // one wave: orders the cursor read before the update
             if (lane == (uint32_t)leader) cur[b0] = base + (uint32_t)__popcll(mine);
             __syncthreads();
@@ -422,9 +427,14 @@ struct ss_ingest {
     DBuf<uint64_t> split_out;      // [3 * kLenBins]
     uint64_t* h_split = nullptr;   // pinned [3 * kLenBins]
     DBuf<uint8_t> rows;            // gathered dense rows (lengths <= 32)
-    DBuf<uint64_t> cls_words;      // a length class's packed rows (k_encode_class)
+    DBuf<uint64_t> cls_words;      // the length classes' packed rows (k_encode_classes / k_encode_class)
+    DBuf<uint32_t> posof;          // per read: its place in d_order (k_len_scatter)
+    DBuf<uint32_t> hll;            // per class W: 2^kHllLog HyperLogLog registers over the call
+    uint32_t* h_hll = nullptr;     // pinned copy
+    DBuf<uint64_t> ovf;            // per job: its table's overflow word after the insert
+    bool exact_sizing = false;     // size class tables by their rows (ss_ingest_set_exact)
     DBuf<uint64_t> first_bad;      // one u64 per length of the chunk
-    uint64_t* h_bad = nullptr;     // pinned [kLenBins + 2]
+    uint64_t* h_bad = nullptr;     // pinned [2 kLenBins + 4]: first-bad and overflow words, a size query
     DBuf<uint64_t> fq_ws, fq_aux, fq_counts;
     std::map<uint32_t, Group> groups;
     std::vector<std::pair<uint64_t, ss_counter*>> pool;    // idle tables (capacity, handle)
@@ -478,11 +488,26 @@ int table_size(ss_ingest* g, ss_counter* t, uint64_t* out) {
     if (rc) return rc;
     rc = ss_counter_size(t, s.p + kScanBlocks + 2, g->stream);
     if (rc) return rc;
-    rc = ss_check(hipMemcpyAsync(g->h_bad + kLenBins, s.p + kScanBlocks + 2, 8, hipMemcpyDeviceToHost, g->stream),
+    rc = ss_check(hipMemcpyAsync(g->h_bad + 2 * kLenBins + 2, s.p + kScanBlocks + 2, 8, hipMemcpyDeviceToHost, g->stream),
                   "ingest size copy");
     if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest sync");
-    *out = g->h_bad[kLenBins];
+    *out = g->h_bad[2 * kLenBins + 2];
     return rc;
+}
+
+// HyperLogLog estimate of the distinct keys behind 2^kHllLog registers (Flajolet et al. 2007, with
+// linear counting below 2.5 m)
+double hll_estimate(const uint32_t* reg) {
+    const double m = (double)(1u << kHllLog);
+    double sum = 0;
+    uint32_t zeros = 0;
+    for (uint32_t j = 0; j < (1u << kHllLog); ++j) {
+        sum += std::ldexp(1.0, -(int)reg[j]);
+        zeros += reg[j] == 0;
+    }
+    double e = 0.7213 / (1.0 + 1.079 / m) * m * m / sum;
+    if (e <= 2.5 * m && zeros) e = m * std::log(m / (double)zeros);
+    return e;
 }
 
 // key kind of a fresh table: the length (fixed by its first insert) or a class's packed words
@@ -490,20 +515,22 @@ int table_kind(const Group& gr, ss_counter* t) {
     return gr.L ? ss_counter_set_length(t, gr.L) : ss_counter_set_words(t, gr.W1);
 }
 
-// make room for m more rows in group gr (grow by extract + merge)
-int group_room(ss_ingest* g, Group& gr, uint64_t m) {
-    if (gr.table && gr.rows + m <= gr.cap / 2) return SS_OK;
+// make room for m more rows in group gr (grow by extract + merge).  need: an upper bound of the
+// table's keys after them -- the rows so far (exact), or a class's distinct-key estimate
+int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
+    if (gr.table && need <= gr.cap / 2) return SS_OK;
     if (!gr.table) {
-        const double scale = gr.L ? 1.0 : g->est_scale;
-        gr.cap = std::min<uint64_t>(1ull << 32, pow2_at_least((uint64_t)(2.0 * (double)m * scale) + 2));
+        const double scale = gr.L || need < m ? 1.0 : g->est_scale;
+        gr.cap = std::min<uint64_t>(1ull << 32, pow2_at_least((uint64_t)(2.0 * (double)need * scale) + 2));
         int rc = table_get(g, gr.cap, &gr.table);
         return rc ? rc : table_kind(gr, gr.table);
     }
     uint64_t size = 0;
     int rc = table_size(g, gr.table, &size);
     if (rc) return rc;
-    if (size + m <= gr.cap / 2) return SS_OK;
-    const uint64_t ncap = pow2_at_least(2 * (size + m));
+    need = std::min(need, size + m);
+    if (need <= gr.cap / 2) return SS_OK;
+    const uint64_t ncap = pow2_at_least(2 * need);
     ss_counter* nt = nullptr;
     if ((rc = table_get(g, ncap, &nt)) != SS_OK) return rc;
     if ((rc = table_kind(gr, nt)) != SS_OK) return rc;
@@ -554,7 +581,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (dense_L > SS_MAX_NT) return ss_fail(SS_EARG, "ingest: dense length > 1024");
         jobs.push_back({len_bin(dense_L), n, 0, 0});
     } else {
-        if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
+        if ((rc = g->order.ensure(n)) || (rc = g->posof.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins)))
             return rc;
         hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p, g->blkfirst.p);
@@ -562,7 +589,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                            g->split_out.p);
         hipLaunchKernelGGL(k_len_binstart, dim3(1), dim3(1024), 0, s, g->split_out.p);
         hipLaunchKernelGGL(k_len_scatter, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p,
-                           (const uint64_t*)g->split_out.p, g->order.p);
+                           (const uint64_t*)g->split_out.p, g->order.p, g->posof.p);
         rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, 3 * kLenBins * 8, hipMemcpyDeviceToHost, s),
                       "ingest split copy");
         if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest split");
@@ -586,26 +613,69 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             }
         }
     }
-    if ((rc = g->first_bad.ensure(jobs.size() + 1))) return rc;
-    if (!jobs.empty() &&
-        (rc = ss_check(hipMemsetAsync(g->first_bad.p, 0xFF, jobs.size() * 8, s), "ingest first_bad reset")))
+    const size_t nj = jobs.size();
+    // first-bad slots: one per job, plus nj for the one-pass class encode (a read index)
+    if ((rc = g->first_bad.ensure(nj + 1)) || (rc = g->ovf.ensure(nj + 1))) return rc;
+    if (nj && (rc = ss_check(hipMemsetAsync(g->first_bad.p, 0xFF, (nj + 1) * 8, s), "ingest first_bad reset")))
         return rc;
-    for (size_t j = 0; j < jobs.size(); ++j) {
+    if (nj && (rc = ss_check(hipMemsetAsync(g->ovf.p, 0, (nj + 1) * 8, s), "ingest overflow reset"))) return rc;
+    auto live = [&](const Job& jb) { return base + jb.first <= g->bad_index; };   // may still hold the first error
+    // ---- the length classes: rows packed (W words + the length) and their distinct keys sketched ----
+    uint64_t woff[33] = {0}, cls_words = 0;
+    uint32_t w1max = 0, wlo = 33, whi = 0;
+    for (const Job& jb : jobs) {
+        if (jb.bin <= 32) continue;
+        const uint32_t W = jb.bin - kClassBin0;
+        woff[W] = cls_words;
+        cls_words += jb.m * (W + 1);
+        w1max = std::max(w1max, W + 1);
+        wlo = std::min(wlo, W);
+        whi = std::max(whi, W);
+    }
+    uint64_t need_cls[33] = {0};
+    if (w1max) {
+        if ((rc = g->cls_words.ensure(cls_words))) return rc;
+        if (!dense_L && w1max <= 16) {      // one read-order pass, the registers updated in it
+            rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->posof.p, g->split_out.p + 2 * kLenBins, woff,
+                                        kClassBin0, w1max, g->cls_words.p, g->hll.p, g->first_bad.p + nj, s);
+        } else {                            // a class per pass (longer reads, or a dense chunk)
+            for (size_t j = 0; j < nj && !rc; ++j) {
+                const Job& jb = jobs[j];
+                if (jb.bin <= 32) continue;
+                const uint32_t W = jb.bin - kClassBin0;
+                const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
+                rc = ss_encode_class_impl(d_buf, d_offs, d_lens, sel, dense_L, jb.m, W, g->cls_words.p + woff[W],
+                                          g->first_bad.p + j, s);
+                if (!rc) rc = ss_hll_rows_impl(g->cls_words.p + woff[W], jb.m, W + 1, g->hll.p + ((uint64_t)W << kHllLog), s);
+            }
+        }
+        // the registers come back (one sync): each class table is sized by its distinct keys so far
+        // (the sketch covers every chunk of the call), not by its rows
+        const uint64_t r0 = (uint64_t)wlo << kHllLog, nr = (uint64_t)(whi - wlo + 1) << kHllLog;
+        if (!rc) rc = ss_check(hipMemcpyAsync(g->h_hll + r0, g->hll.p + r0, nr * 4, hipMemcpyDeviceToHost, s), "ingest sketch copy");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest sketch");
+        if (rc) return rc;
+        for (const Job& jb : jobs) {
+            if (jb.bin <= 32) continue;
+            const uint32_t W = jb.bin - kClassBin0;
+            const double e = hll_estimate(g->h_hll + ((uint64_t)W << kHllLog));
+            need_cls[W] = g->exact_sizing ? ~0ull : (uint64_t)(1.2 * e) + 256;   // ~9 sigma above the estimate
+        }
+    }
+    for (size_t j = 0; j < nj; ++j) {
         const Job& jb = jobs[j];
-        if (base + jb.first > g->bad_index) continue;       // cannot hold the first error any more
+        if (!live(jb)) continue;
         const bool cls = jb.bin > 32;
         Group& gr = g->groups[jb.bin];
         gr.L = cls ? 0u : jb.bin;
         gr.W1 = cls ? jb.bin - kClassBin0 + 1 : 1u;
-        if ((rc = group_room(g, gr, jb.m))) return rc;
+        const uint64_t need = std::min<uint64_t>(gr.rows + jb.m, cls ? need_cls[gr.W1 - 1] : ~0ull);
+        if ((rc = group_room(g, gr, jb.m, need))) return rc;
         if ((rc = gr.rowmap.ensure_keep(gr.rows + jb.m, gr.rows, s))) return rc;
         const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
         if (cls) {
-            // the class's rows packed straight from the chunk (no gather): W words + the length
-            if ((rc = g->cls_words.ensure(jb.m * gr.W1))) return rc;
-            rc = ss_encode_class_impl(d_buf, d_offs, d_lens, sel, dense_L, jb.m, gr.W1 - 1, g->cls_words.p,
-                                      g->first_bad.p + j, s);
-            if (!rc) rc = ss_counter_insert_words(gr.table, g->cls_words.p, jb.m, gr.rows, s);
+            rc = ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, s);
+            if (!rc) rc = ss_counter_overflow(gr.table, g->ovf.p + j, s);
         } else {
             const uint8_t* src = d_buf;
             uint64_t stride = dense_L;
@@ -626,24 +696,31 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         g->nreads += n;
         return SS_OK;
     }
-    rc = ss_check(hipMemcpyAsync(g->h_bad, g->first_bad.p, jobs.size() * 8, hipMemcpyDeviceToHost, s), "ingest bad copy");
+    // first-bad words and the class tables' overflow words back in one sync
+    uint64_t* hb = g->h_bad;
+    rc = ss_check(hipMemcpyAsync(hb, g->first_bad.p, (nj + 1) * 8, hipMemcpyDeviceToHost, s), "ingest bad copy");
+    if (!rc) rc = ss_check(hipMemcpyAsync(hb + nj + 1, g->ovf.p, nj * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest chunk");
     if (rc) return rc;
-    for (size_t j = 0; j < jobs.size(); ++j) {
-        const uint64_t fb = g->h_bad[j];
-        if (fb == kNoSlot || base + jobs[j].first > g->bad_index) continue;
-        // a length's insert reports its row (rows are in read order); a class reports the read
+    for (size_t j = 0; j < nj; ++j)
+        if (hb[nj + 1 + j])
+            return ss_fail(SS_EFULL, "ingest: a length class's table ran full (its distinct-key estimate was low); "
+                                     "count again with ss_ingest_set_exact");
+    for (size_t j = 0; j <= nj; ++j) {
+        const uint64_t fb = hb[j];
+        if (fb == kNoSlot || (j < nj && base + jobs[j].first > g->bad_index)) continue;
+        // a length's insert reports its row (rows are in read order); the class encodes report the read
+        const bool by_row = j < nj && !dense_L && jobs[j].bin <= 32;
         uint64_t idx = fb;
-        if (!dense_L && jobs[j].bin <= 32) {
+        if (by_row) {
             rc = ss_check(hipMemcpy(&idx, g->order.p + jobs[j].start + fb, 8, hipMemcpyDeviceToHost), "ingest bad row");
             if (rc) return rc;
         }
         if (base + idx < g->bad_index) {
             g->bad_index = base + idx;
             g->bad_kind = SS_EINVALID_BASE;
-            uint32_t L = dense_L ? dense_L : jobs[j].bin;
-            if (!dense_L && jobs[j].bin > 32 &&
-                (rc = ss_check(hipMemcpy(&L, d_lens + idx, 4, hipMemcpyDeviceToHost), "ingest bad len")))
+            uint32_t L = dense_L ? dense_L : (by_row ? jobs[j].bin : 0u);
+            if (!L && (rc = ss_check(hipMemcpy(&L, d_lens + idx, 4, hipMemcpyDeviceToHost), "ingest bad len")))
                 return rc;
             uint64_t off = dense_L ? idx * dense_L : 0;
             if (h_offs) {
@@ -708,7 +785,10 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
     g->device = device;
     rc = ss_check(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking), "ingest stream");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_split, 3 * kLenBins * 8, hipHostMallocDefault), "ingest pinned");
-    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_bad, (kLenBins + 2) * 8, hipHostMallocDefault), "ingest pinned");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_bad, (2 * kLenBins + 4) * 8, hipHostMallocDefault), "ingest pinned");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_hll, (33ull << kHllLog) * 4, hipHostMallocDefault), "ingest pinned");
+    if (!rc) rc = g->hll.ensure(33ull << kHllLog);
+    if (!rc) rc = ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
     if (rc) {
         ss_ingest_destroy(g);
         return rc;
@@ -737,6 +817,13 @@ int ss_ingest_reset(ss_ingest* g) {
     g->bad_bytes.clear();
     g->est_scale = 1.0;
     g->nkeys = g->nwords = 0;
+    if (!g->hll.p) return SS_OK;
+    return ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
+}
+
+int ss_ingest_set_exact(ss_ingest* g, int exact) {
+    if (!g) return ss_fail(SS_EARG, "null ingest");
+    g->exact_sizing = exact != 0;
     return SS_OK;
 }
 
@@ -758,6 +845,8 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->fq_ws.release(), g->fq_aux.release(), g->fq_counts.release();
     g->slot.release(), g->ordered.release(), g->woff.release(), g->scan.release(), g->out_len.release();
     g->out_cnt.release(), g->out_words.release(), g->gdesc.release();
+    g->cls_words.release(), g->posof.release(), g->hll.release(), g->ovf.release();
+    if (g->h_hll) (void)hipHostFree(g->h_hll);
     if (g->h_split) (void)hipHostFree(g->h_split);
     if (g->h_bad) (void)hipHostFree(g->h_bad);
     if (g->stream) (void)hipStreamDestroy(g->stream);
