@@ -481,15 +481,20 @@ class DeviceIngest:
                   "ss_ingest_error")
             raise_read_error(bytes(buf)[:ln.value], idx.value)
 
-    def results(self):
+    def results(self, copy: bool = True):
+        """(lens u32, counts u64, words u64) of the count so far, first-occurrence order.  copy=False
+        returns views of the engine's pinned result buffers, valid until the next count / reset /
+        close (no host-side copy of the rows)."""
         K, NW = C.c_uint64(), C.c_uint64()
         check(lib().ss_ingest_finish(self._h, C.byref(K), C.byref(NW)), "ss_ingest_finish")
         pl, pc, pw = C.c_void_p(), C.c_void_p(), C.c_void_p()
         check(lib().ss_ingest_results(self._h, C.byref(pl), C.byref(pc), C.byref(pw)), "ss_ingest_results")
         k, nw = K.value, NW.value
-        lens = np.ctypeslib.as_array((C.c_uint32 * max(1, k)).from_address(pl.value))[:k].copy() if k else np.zeros(0, np.uint32)
-        cnts = np.ctypeslib.as_array((C.c_uint64 * max(1, k)).from_address(pc.value))[:k].copy() if k else np.zeros(0, np.uint64)
-        wds = np.ctypeslib.as_array((C.c_uint64 * max(1, nw)).from_address(pw.value))[:nw].copy() if nw else np.zeros(0, np.uint64)
+        lens = np.ctypeslib.as_array((C.c_uint32 * max(1, k)).from_address(pl.value))[:k] if k else np.zeros(0, np.uint32)
+        cnts = np.ctypeslib.as_array((C.c_uint64 * max(1, k)).from_address(pc.value))[:k] if k else np.zeros(0, np.uint64)
+        wds = np.ctypeslib.as_array((C.c_uint64 * max(1, nw)).from_address(pw.value))[:nw] if nw else np.zeros(0, np.uint64)
+        if copy:
+            lens, cnts, wds = lens.copy(), cnts.copy(), wds.copy()
         return lens, cnts, wds
 
     def reset(self) -> None:
