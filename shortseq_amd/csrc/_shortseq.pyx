@@ -487,7 +487,8 @@ cdef class ShortSeqCounter(dict):
     """dict subclass {ShortSeq: count} in first-occurrence order (counter.pyx:10-54).
 
     ShortSeqCounter(list_of_bytes, device="auto"): lists of >= GPU_MIN_READS reads are encoded and
-    counted on the GPU (ss_ingest: split by length on the device, one counter table per length);
+    counted on the GPU (ss_ingest: split on the device into lengths 1-32 and length classes 33-1024,
+    one counter table per length / class, the key being (length, words));
     device="host" forces the per-object host path, device="cuda"/"cuda:N" forces the GPU.
     """
 
@@ -763,8 +764,9 @@ def _run_shards(jobs):
 def _count_batch_gpu(ShortSeqCounter self, list reads, devs):
     """Batch path (counter.pyx:22-39 over a whole list): the list is cut into len(devs) contiguous
     shards; each shard's bytes objects are copied back to back into its engine's pinned staging
-    buffer and counted on that engine's device (split by length on the device, one table per length:
-    the length is part of the key, short_seq_64.pyx:41-44), the shards concurrently.  The dict is
+    buffer and counted on that engine's device (split on the device into lengths 1-32 and length
+    classes, one table per length / class: the length is part of the key, short_seq_64.pyx:41-44),
+    the shards concurrently.  The dict is
     built from the shards' rows in shard order (each shard's rows in first-occurrence order), which
     is the first-occurrence order of the whole list.  The first rejected read in list order raises
     the reference's error."""
