@@ -278,28 +278,45 @@ __device__ __forceinline__ uint64_t encode_word_q(const uint8_t* p, uint32_t nb,
 // power-of-two padding and every wave stores 512 contiguous bytes.  Words at or past a read's length
 // are written as 0 (the row padding).  The blob's 16-B chunks are read whole (encode_word_q): the
 // blob must be readable to the end of its last 16-B chunk (any hipMalloc / torch allocation is).
+// Two words per lane (words base + lane and base + 64 + lane of its wave's 128-word span): both
+// words' offset / length loads, then both words' chunk loads, go out before either is packed
+// (tools/tune_encvar.hip on the F2 batch: 1 word 0.514, 2 words 0.561, 4 words 0.533 of 8 TB/s).
+constexpr int kVarK = 2;
 __global__ __launch_bounds__(kThreads) void k_encode_var_dense(const uint8_t* in, const uint64_t* __restrict__ offs,
                                                                const uint32_t* __restrict__ lens, uint64_t n,
                                                                uint64_t* __restrict__ out, uint32_t wpr,
                                                                double inv_wpr, unsigned long long* first_bad) {
     const uint64_t total = n * wpr;
-    for (uint64_t g = (uint64_t)blockIdx.x * kThreads + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kThreads) {
-        uint64_t r = (uint64_t)((double)g * inv_wpr);
-        if (r * wpr > g) --r;
-        else if ((r + 1) * wpr <= g) ++r;
-        const uint32_t w = (uint32_t)(g - r * wpr);
-        const uint32_t L = lens[r];
-        const uint64_t off = offs[r];
+    const uint64_t base = ((uint64_t)blockIdx.x * kThreads + (threadIdx.x & ~63u)) * kVarK + (threadIdx.x & 63u);
+    uint64_t r[kVarK], off[kVarK];
+    uint32_t w[kVarK], L[kVarK], nb[kVarK];
+#pragma unroll
+    for (int k = 0; k < kVarK; ++k) {
+        const uint64_t g = base + 64u * k;
+        uint64_t rr = (uint64_t)((double)g * inv_wpr);
+        if (rr * wpr > g) --rr;
+        else if ((rr + 1) * wpr <= g) ++rr;
+        r[k] = g < total ? rr : 0;
+        w[k] = (uint32_t)(g - rr * wpr);
+        L[k] = g < total ? lens[r[k]] : 0u;
+        off[k] = g < total ? offs[r[k]] : 0u;
+    }
+    Chunks3 c[kVarK];
+#pragma unroll
+    for (int k = 0; k < kVarK; ++k) {
+        nb[k] = (L[k] <= SS_MAX_NT && 32u * w[k] < L[k]) ? min(32u, L[k] - 32u * w[k]) : 0u;
+        if (nb[k]) c[k] = load_word_q(in + off[k] + 32u * w[k], nb[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kVarK; ++k) {
+        const uint64_t g = base + 64u * k;
+        if (g >= total) continue;
         uint32_t bad = 0;
         uint64_t word = 0;
-        if (L > SS_MAX_NT) {
-            bad = (w == 0);                     // short_seq.pyx:74 (too long), reported per read
-        } else if (32u * w < L) {
-            const uint32_t nb = min(32u, L - 32u * w);
-            word = encode_word_q(in + off + 32u * w, nb, (L <= 32u) || (nb < 32u), bad);
-        }
+        if (L[k] > SS_MAX_NT) bad = (w[k] == 0);          // short_seq.pyx:74 (too long), reported per read
+        else if (nb[k]) word = pack_word_q(c[k], nb[k], (L[k] <= 32u) || (nb[k] < 32u), bad);
         out[g] = word;
-        report_bad(bad != 0u, r, first_bad);
+        report_bad(bad != 0u, r[k], first_bad);
     }
 }
 
@@ -1056,9 +1073,10 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     hipStream_t s = (hipStream_t)stream;
     int rc = reset_first_bad(d_first_bad, s);
     if (rc || n == 0) return rc;
-    // one word per lane (no grid-stride round): every lane's two dependent loads (offset / length,
+    // kVarK words per lane, no grid-stride round: every lane's dependent loads (offset / length,
     // then the bytes) overlap across many resident waves
-    const unsigned grid = grid_for(n * wpr, kThreads, 0x7FFFFFFFu);
+    const unsigned grid = grid_for((n * wpr + kVarK - 1) / kVarK, kThreads, 0x7FFFFFFFu);
+    if ((uint64_t)grid * kThreads * kVarK < n * wpr) return ss_fail(SS_EARG, "ss_encode_var: batch too large");
     hipLaunchKernelGGL(k_encode_var_dense, dim3(grid), dim3(kThreads), 0, s, d_ascii, d_offsets, d_lens, n, d_words,
                        wpr, 1.0 / (double)wpr, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_var_dense");
