@@ -444,15 +444,16 @@ class DeviceIngest:
     words u64) numpy arrays in first-occurrence order (the ShortSeqCounter dict order: row k has
     ceil(lens[k] / 32) words, one for lengths 0..32).  A rejected read raises like ShortSeqCounter."""
 
-    def __init__(self, device=None, exact: bool = False):
+    def __init__(self, device=None, exact: bool = False, *, _sizing: Optional[int] = None):
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         h = C.c_void_p()
         check(lib().ss_ingest_create(dev.index or 0, C.byref(h)), "ss_ingest_create")
         self._h = h
         self._exact = exact
+        self._sizing = int(exact) if _sizing is None else _sizing   # 2: test hook, undersized class tables
         self._fresh = True
-        check(lib().ss_ingest_set_exact(h, int(exact)), "ss_ingest_set_exact")
+        check(lib().ss_ingest_set_exact(h, self._sizing), "ss_ingest_set_exact")
 
     def count(self, blob: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor) -> None:
         for t, name in ((blob, "blob"), (offsets, "offsets"), (lens, "lens")):
@@ -462,13 +463,15 @@ class DeviceIngest:
         torch.cuda.current_stream(self.device).synchronize()   # the engine runs on its own stream
         args = (self._h, blob.data_ptr(), blob.numel(), offsets.data_ptr(), lens.data_ptr(), lens.numel())
         rc = lib().ss_ingest_add_device(*args)
+        self.retried = False
         if rc == SS_EFULL and self._fresh and not self._exact:
             # a length class's table, sized by its distinct-key sketch, ran full: the first batch of the
             # count is counted again with tables sized by their rows (later batches cannot be redone)
             check(lib().ss_ingest_reset(self._h), "ss_ingest_reset")
             check(lib().ss_ingest_set_exact(self._h, 1), "ss_ingest_set_exact")
             rc = lib().ss_ingest_add_device(*args)
-            check(lib().ss_ingest_set_exact(self._h, 0), "ss_ingest_set_exact")
+            check(lib().ss_ingest_set_exact(self._h, self._sizing), "ss_ingest_set_exact")
+            self.retried = True
         check(rc, "ss_ingest_add_device")
         self._fresh = False
         idx, kind, ln = C.c_uint64(), C.c_int(), C.c_uint64()

@@ -1941,6 +1941,8 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
     uint32_t* lfst = lcnt + LS;                                           // [LS]
     const uint32_t region = blockIdx.x;
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
+    __shared__ int lds_full;   // an undersized table: the LDS hash ran full, the insert is void
+    if (threadIdx.x == 0) lds_full = 0;
     for (uint32_t i = threadIdx.x; i < LS; i += T) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
@@ -1954,6 +1956,7 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
         const uint64_t fp = w.bkey[e];
         const uint32_t idx = w.bidx[e];
         const uint64_t tag = (fp >> 32) << 32;
+        if (*(volatile int*)&lds_full) break;   // overflow raised: the rest of the region need not probe
         uint32_t ls = (uint32_t)((fp * 0x9E3779B97F4A7C15ull) >> lds_shift) & (LS - 1);
         bool placed = false;
         for (uint32_t probe = 0; probe < LS; ++probe) {   // bounded: a region with > 2S distinct keys
@@ -1974,6 +1977,7 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
         }
         if (!placed) {
             atomicOr(t.overflow, kOvfTable);
+            *(volatile int*)&lds_full = 1;
             continue;
         }
         atomicAdd(&lcnt[ls], 1u);

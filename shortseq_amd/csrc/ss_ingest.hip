@@ -432,7 +432,8 @@ struct ss_ingest {
     DBuf<uint32_t> hll;            // per class W: 2^kHllLog HyperLogLog registers over the call
     uint32_t* h_hll = nullptr;     // pinned copy
     DBuf<uint64_t> ovf;            // per job: its table's overflow word after the insert
-    bool exact_sizing = false;     // size class tables by their rows (ss_ingest_set_exact)
+    int sizing = 0;                // class tables: 0 by their sketch, 1 by their rows, 2 by 1/64 of the
+                                   // sketch (tests: forces the SS_EFULL path) -- ss_ingest_set_exact
     DBuf<uint64_t> first_bad;      // one u64 per length of the chunk
     uint64_t* h_bad = nullptr;     // pinned [2 kLenBins + 4]: first-bad and overflow words, a size query
     DBuf<uint64_t> fq_ws, fq_aux, fq_counts;
@@ -659,7 +660,9 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             if (jb.bin <= 32) continue;
             const uint32_t W = jb.bin - kClassBin0;
             const double e = hll_estimate(g->h_hll + ((uint64_t)W << kHllLog));
-            need_cls[W] = g->exact_sizing ? ~0ull : (uint64_t)(1.2 * e) + 256;   // ~9 sigma above the estimate
+            need_cls[W] = g->sizing == 1 ? ~0ull                                   // the rows bound
+                        : g->sizing == 2 ? (uint64_t)(e / 64.0) + 64                   // test: undersized
+                                         : (uint64_t)(1.2 * e) + 256;                  // ~9 sigma above the estimate
         }
     }
     for (size_t j = 0; j < nj; ++j) {
@@ -823,7 +826,8 @@ int ss_ingest_reset(ss_ingest* g) {
 
 int ss_ingest_set_exact(ss_ingest* g, int exact) {
     if (!g) return ss_fail(SS_EARG, "null ingest");
-    g->exact_sizing = exact != 0;
+    if (exact < 0 || exact > 2) return ss_fail(SS_EARG, "sizing mode 0, 1 or 2");
+    g->sizing = exact;
     return SS_OK;
 }
 

@@ -72,6 +72,29 @@ def test_device_ingest_ragged_small(gpu, oracle, case, exact):
     assert np.array_equal(gw, ew)
 
 
+def test_device_ingest_undersized_class_table_recounts(gpu, oracle):
+    """A class table sized below its distinct keys (the test hook: 1/64 of the sketch) runs full:
+    the add call returns SS_EFULL and the first batch is counted again with tables sized by rows;
+    the rows still equal the oracle's.  A later batch that overflows cannot be redone and raises."""
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import NativeError
+    seed, ps, U, n, lo, hi = 51, 52, 1 << 17, 400_000, 33, 150
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    eng = B.DeviceIngest(gpu, _sizing=2)
+    try:
+        eng.count(blob, offs, lens)
+        assert eng.retried
+        gl, gc, gw = eng.results()
+        eng.reset()
+        eng.count(blob, offs[:1000], lens[:1000])           # small: fits even undersized
+        with pytest.raises(NativeError, match="ran full"):
+            eng.count(blob, offs, lens)
+    finally:
+        eng.close()
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    assert gl.tolist() == el.tolist() and gc.tolist() == ec.tolist() and np.array_equal(gw, ew)
+
+
 def test_device_ingest_class_lengths_apart(gpu, oracle):
     """One length class (33..64 nt) holds reads that pack to the same words at different lengths
     (trailing 'A' = code 0): the class key's length word keeps them apart, as the reference's
