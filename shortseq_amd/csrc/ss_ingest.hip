@@ -432,6 +432,7 @@ struct ss_ingest {
     DBuf<uint32_t> hll;            // per class W: 2^kHllLog HyperLogLog registers over the call
     uint32_t* h_hll = nullptr;     // pinned copy
     DBuf<uint64_t> ovf;            // per job: its table's overflow word after the insert
+    bool failed = false;           // an add returned SS_EFULL: the counts are void until reset
     int sizing = 0;                // class tables: 0 by their sketch, 1 by their rows, 2 by 1/64 of the
                                    // sketch (tests: forces the SS_EFULL path) -- ss_ingest_set_exact
     DBuf<uint64_t> first_bad;      // one u64 per length of the chunk
@@ -565,6 +566,7 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
 // read's bytes are then taken from there, else copied back).
 int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t nbytes,
                   uint64_t n, uint32_t dense_L, const std::vector<uint64_t>* h_offs, const uint8_t* h_chunk) {
+    if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (n == 0) return SS_OK;
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "ingest: a chunk holds < 2^32 reads");
     // the row maps and first indices hold global read indices as u32
@@ -705,10 +707,12 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     if (!rc) rc = ss_check(hipMemcpyAsync(hb + nj + 1, g->ovf.p, nj * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest chunk");
     if (rc) return rc;
-    for (size_t j = 0; j < nj; ++j)
-        if (hb[nj + 1 + j])
-            return ss_fail(SS_EFULL, "ingest: a length class's table ran full (its distinct-key estimate was low); "
+    for (size_t j = 0; j < nj; ++j) {
+        if (!hb[nj + 1 + j]) continue;
+        g->failed = true;
+        return ss_fail(SS_EFULL, "ingest: a length class's table ran full (its distinct-key estimate was low); "
                                      "count again with ss_ingest_set_exact");
+    }
     for (size_t j = 0; j <= nj; ++j) {
         const uint64_t fb = hb[j];
         if (fb == kNoSlot || (j < nj && base + jobs[j].first > g->bad_index)) continue;
@@ -820,6 +824,7 @@ int ss_ingest_reset(ss_ingest* g) {
     g->bad_bytes.clear();
     g->est_scale = 1.0;
     g->nkeys = g->nwords = 0;
+    g->failed = false;
     if (!g->hll.p) return SS_OK;
     return ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
 }
@@ -1070,6 +1075,7 @@ int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_rea
 
 int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     if (!g || !h_nkeys || !h_nwords) return ss_fail(SS_EARG, "null argument");
+    if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     (void)hipSetDevice(g->device);
     hipStream_t s = g->stream;
     const uint64_t N = g->nreads;

@@ -89,6 +89,11 @@ def test_device_ingest_undersized_class_table_recounts(gpu, oracle):
         eng.count(blob, offs[:1000], lens[:1000])           # small: fits even undersized
         with pytest.raises(NativeError, match="ran full"):
             eng.count(blob, offs, lens)
+        with pytest.raises(NativeError, match="reset and count again"):   # the counts are void now
+            eng.results()
+        eng.reset()
+        eng.count(blob, offs[:1000], lens[:1000])
+        assert int(eng.results()[1].sum()) == 1000
     finally:
         eng.close()
     el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
