@@ -1502,8 +1502,29 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     __shared__ uint32_t sent[3];   // sentinel count, sentinel first, slice occupancy
     const uint32_t region = blockIdx.x;
     const uint64_t slice_base = (uint64_t)region << t.slice_log;
+    // The region's segment table first, one vector load per lane (lanes 0-7 the segment starts,
+    // 8-15 the ends; exact paths: lanes 0 / 1 the range), read back with readlane: ONE round trip,
+    // issued before the LDS fill.  As scalar loads the compiler waited for each (start, end) pair in
+    // turn, 8 dependent round trips per workgroup.
+    static_assert(kFinePerBin <= 32, "segment table: two lanes per segment");
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t meta;
+    if (w.seg_end) {
+        const uint32_t rpb = 1u << (w.rbits - kCoarseBits);
+        const uint32_t sg = lane % kFinePerBin;
+        const uint64_t at = (uint64_t)((region / rpb) * kFinePerBin + sg) * rpb + region % rpb;
+        meta = (lane < kFinePerBin ? w.hist : w.seg_end)[at];
+    } else {
+        meta = w.rstart[region + (lane & 1u)];
+    }
+    // fresh: the fill does not wait on any load (one loop with a per-slot select waited for the
+    // segment-table load in its first iteration)
+    if (fresh) {
+        for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = kEmpty;
+    } else {
+        for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = t.slots[slice_base + i].key;
+    }
     for (uint32_t i = threadIdx.x; i < S; i += T) {
-        skey[i] = fresh ? kEmpty : t.slots[slice_base + i].key;
         bcnt[i] = 0;
         bfst[i] = 0xFFFFFFFFu;
     }
@@ -1512,26 +1533,23 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         sent[1] = 0xFFFFFFFFu;
         sent[2] = 0;
     }
-    __syncthreads();
     constexpr int kP = kAggP;
     // the region's records: one range (exact paths) or its kFinePerBin fine-scatter segments,
     // walked as one flat index space (segment s covers flat [pre[s], pre[s + 1])) so every
     // iteration issues kP loads per thread whatever the segment lengths
-    static_assert(kFinePerBin <= 16, "segment table");
     uint32_t seg0[kFinePerBin], pre[kFinePerBin + 1];
     pre[0] = 0;
     if (w.seg_end) {
-        const uint32_t rpb = 1u << (w.rbits - kCoarseBits);
 #pragma unroll
         for (uint32_t sg = 0; sg < kFinePerBin; ++sg) {
-            const uint64_t at = (uint64_t)((region / rpb) * kFinePerBin + sg) * rpb + region % rpb;
-            seg0[sg] = w.hist[at];
-            pre[sg + 1] = pre[sg] + (w.seg_end[at] - seg0[sg]);
+            seg0[sg] = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)sg);
+            pre[sg + 1] = pre[sg] + ((uint32_t)__builtin_amdgcn_readlane((int)meta, (int)(kFinePerBin + sg)) - seg0[sg]);
         }
     } else {
-        seg0[0] = w.rstart[region];
+        seg0[0] = (uint32_t)__builtin_amdgcn_readlane((int)meta, 0);
+        const uint32_t end = (uint32_t)__builtin_amdgcn_readlane((int)meta, 1);
 #pragma unroll
-        for (uint32_t sg = 0; sg < kFinePerBin; ++sg) pre[sg + 1] = w.rstart[region + 1] - seg0[0];
+        for (uint32_t sg = 0; sg < kFinePerBin; ++sg) pre[sg + 1] = end - seg0[0];
     }
     const uint32_t total = pre[kFinePerBin];
     auto flat_at = [&](uint32_t f) -> uint32_t {   // element index of flat position f < total
@@ -1563,7 +1581,8 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
             }
         }
     };
-    if (total) load_step(0);
+    if (total) load_step(0);   // in flight across the barrier that publishes the LDS fill
+    __syncthreads();
     for (uint32_t e0 = 0; e0 < total; e0 += kP * T) {
         uint64_t key[kP];
         uint32_t idx[kP], el[kP];

@@ -229,6 +229,7 @@ __global__ void k_sig(Tbl t, unsigned long long* out) {
 int main(int argc, char** argv) {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 125000000ull;
     const int reps = argc > 2 ? atoi(argv[2]) : 10;
+    const int modes = argc > 3 ? atoi(argv[3]) : 15;   // bit m: run mode m
     const uint64_t U = 1ull << 24;
     uint8_t* ascii;
     uint64_t* fb;
@@ -274,6 +275,7 @@ int main(int argc, char** argv) {
     unsigned long long hp[2] = {0, 0};
     const char* names[4] = {"prod", "x4 T512", "x2 T512", "x4 T1024"};
     for (int mode = 0; mode < 4; ++mode) {
+        if (!((modes >> mode) & 1)) continue;
         double tc = 0, ta = 0;
         for (int r = -2; r < reps; ++r) {
             CK(hipDeviceSynchronize());
