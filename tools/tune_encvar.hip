@@ -1,7 +1,9 @@
 // tools/tune_encvar.hip — ss_encode_var on the F2 bench batch (50M reads of 50-150 nt from a 2^20
 // pool, wpr 5): the production kernel (one word per lane) against forms where a lane takes K words
 // of its wave's 64 K-word span and issues every offset / length load, then every chunk load, before
-// packing any (more bytes in flight per lane).  Output compared with the production launch.
+// packing any (more bytes in flight per lane), and block-of-reads forms that stage a dense span of
+// the blob in LDS with coalesced loads (profiles/r3/tune_encvar_span.log: 0.33-0.45 of 8 TB/s against
+// 0.59 for the production kernel, not kept).  Output compared with the production launch.
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include tools/tune_encvar.hip \
 //     shortseq_amd/csrc/ss_runtime.hip -o tools/tune_encvar
 #include "../shortseq_amd/csrc/ss_codec.hip"
@@ -54,6 +56,110 @@ __global__ __launch_bounds__(kThreads) void k_encvar_k(const uint8_t* in, const 
         report_bad(bad != 0u, r[k], first_bad);
     }
 }
+
+__device__ __forceinline__ uint64_t shx64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+// Block of R reads: when their bytes form one dense span (<= CAP bytes, <= 2x the reads' bytes),
+// the span is staged in LDS with coalesced 16-B loads and every word is packed from LDS chunks;
+// otherwise each word loads its chunks from global memory (k_encode_var_dense's path).
+template <uint32_t R, int T, int K, uint32_t CAP>
+__global__ __launch_bounds__(T) void k_encvar_span(const uint8_t* in, const uint64_t* __restrict__ offs,
+                                                   const uint32_t* __restrict__ lens, uint64_t n,
+                                                   uint64_t* __restrict__ out, uint32_t wpr, float inv_wpr,
+                                                   unsigned long long* first_bad) {
+    __shared__ uint4 sbuf[CAP / 16];
+    __shared__ uint64_t soff[R];
+    __shared__ uint32_t slen[R];
+    __shared__ uint64_t red[3][T / 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t r0 = (uint64_t)blockIdx.x * R;
+    const uint32_t nr = (uint32_t)min((uint64_t)R, n - r0);
+    uint64_t lo = ~0ull, hi = 0, sum = 0;
+    for (uint32_t i = threadIdx.x; i < R; i += T) {
+        const uint64_t o = offs[r0 + min(i, nr - 1)];
+        const uint32_t L = lens[r0 + min(i, nr - 1)];
+        soff[i] = o;
+        slen[i] = L;
+        if (i < nr && L && L <= SS_MAX_NT) {
+            lo = min(lo, o);
+            hi = max(hi, o + L);
+            sum += L;
+        }
+    }
+    for (int m = 32; m; m >>= 1) {
+        lo = min(lo, shx64(lo, m));
+        hi = max(hi, shx64(hi, m));
+        sum += shx64(sum, m);
+    }
+    if (lane == 0) {
+        red[0][wave] = lo;
+        red[1][wave] = hi;
+        red[2][wave] = sum;
+    }
+    __syncthreads();
+    lo = red[0][0];
+    hi = red[1][0];
+    sum = red[2][0];
+#pragma unroll
+    for (int v = 1; v < T / 64; ++v) {
+        lo = min(lo, red[0][v]);
+        hi = max(hi, red[1][v]);
+        sum += red[2][v];
+    }
+    const uint64_t base = lo & ~15ull;
+    const bool staged = hi > lo && hi - base <= CAP && hi - base <= 2 * sum + 256;
+    if (staged) {
+        const uint32_t nch = (uint32_t)((hi - base + 15) >> 4);
+        const uint4* src = (const uint4*)(in + base);
+        for (uint32_t c = threadIdx.x; c < nch; c += T) sbuf[c] = ld_stream(&src[c]);
+        __syncthreads();
+    }
+    const uint32_t words = nr * wpr;
+    for (uint32_t g0 = 0; g0 < words; g0 += T * K) {
+        uint32_t w[K], nb[K], L[K], rl[K];
+        uint64_t off[K];
+        Chunks3 c[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t g = min(g0 + (uint32_t)k * T + threadIdx.x, words - 1u);
+            uint32_t r = (uint32_t)((float)g * inv_wpr);
+            if (r * wpr > g) --r;
+            else if ((r + 1) * wpr <= g) ++r;
+            rl[k] = r;
+            w[k] = g - r * wpr;
+            L[k] = slen[r];
+            off[k] = soff[r];
+            nb[k] = (L[k] <= SS_MAX_NT && 32u * w[k] < L[k]) ? min(32u, L[k] - 32u * w[k]) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (!nb[k]) continue;
+            if (staged) {
+                const uint32_t p = (uint32_t)(off[k] + 32u * w[k] - base), q = p >> 4;
+                c[k].sh = p & 15u;
+                const uint32_t last = (c[k].sh + nb[k] - 1u) >> 4;
+                c[k].c0 = sbuf[q];
+                c[k].c1 = sbuf[q + min(1u, last)];
+                c[k].c2 = sbuf[q + min(2u, last)];
+            } else {
+                c[k] = load_word_q(in + off[k] + 32u * w[k], nb[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t g = g0 + (uint32_t)k * T + threadIdx.x;
+            if (g >= words) continue;
+            uint32_t bad = 0;
+            uint64_t word = 0;
+            if (L[k] > SS_MAX_NT) bad = (w[k] == 0);
+            else if (nb[k]) word = pack_word_q(c[k], nb[k], (L[k] <= 32u) || (nb[k] < 32u), bad);
+            out[r0 * wpr + g] = word;
+            report_bad(bad != 0u, r0 + rl[k], first_bad);
+        }
+    }
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -86,18 +192,19 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<uint64_t> h0(n * wpr), h1(n * wpr);
-    for (int mode = 0; mode < 4; ++mode) {
-        const int K = mode == 0 ? 1 : mode == 1 ? 2 : mode == 2 ? 4 : 8;
+    const char* names[6] = {"prod", "span R128 T256 K3", "span R64 T128 K3", "span R256 T256 K5", "span R128 T128 K5", "span R256 T512 K3"};
+    for (int mode = 0; mode < 6; ++mode) {
+        const int K = mode;
         auto launch = [&](uint64_t* out) {
-            if (mode == 0) {
-                CS(ss_encode_var(blob, offs, lens, n, out, wpr, fb, nullptr));
-                return;
+            const float inv = 1.0f / (float)wpr;
+            switch (mode) {
+            case 0: CS(ss_encode_var(blob, offs, lens, n, out, wpr, fb, nullptr)); return;
+            case 1: hipLaunchKernelGGL((k_encvar_span<128, 256, 3, 24576>), dim3((unsigned)((n + 127) / 128)), dim3(256), 0, 0, blob, offs, lens, n, out, wpr, inv, (unsigned long long*)fb); return;
+            case 2: hipLaunchKernelGGL((k_encvar_span<64, 128, 3, 12288>), dim3((unsigned)((n + 63) / 64)), dim3(128), 0, 0, blob, offs, lens, n, out, wpr, inv, (unsigned long long*)fb); return;
+            case 3: hipLaunchKernelGGL((k_encvar_span<256, 256, 5, 49152>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, blob, offs, lens, n, out, wpr, inv, (unsigned long long*)fb); return;
+            case 4: hipLaunchKernelGGL((k_encvar_span<128, 128, 5, 24576>), dim3((unsigned)((n + 127) / 128)), dim3(128), 0, 0, blob, offs, lens, n, out, wpr, inv, (unsigned long long*)fb); return;
+            case 5: hipLaunchKernelGGL((k_encvar_span<256, 512, 3, 49152>), dim3((unsigned)((n + 255) / 256)), dim3(512), 0, 0, blob, offs, lens, n, out, wpr, inv, (unsigned long long*)fb); return;
             }
-            const uint64_t lanes = (n * wpr + K - 1) / K;
-            const unsigned grid = (unsigned)((lanes + kThreads - 1) / kThreads);
-            if (K == 2) hipLaunchKernelGGL(k_encvar_k<2>, dim3(grid), dim3(kThreads), 0, 0, blob, offs, lens, n, out, wpr, 1.0 / wpr, (unsigned long long*)fb);
-            if (K == 4) hipLaunchKernelGGL(k_encvar_k<4>, dim3(grid), dim3(kThreads), 0, 0, blob, offs, lens, n, out, wpr, 1.0 / wpr, (unsigned long long*)fb);
-            if (K == 8) hipLaunchKernelGGL(k_encvar_k<8>, dim3(grid), dim3(kThreads), 0, 0, blob, offs, lens, n, out, wpr, 1.0 / wpr, (unsigned long long*)fb);
         };
         uint64_t* out = mode == 0 ? out0 : out1;
         launch(out);
@@ -116,7 +223,8 @@ int main(int argc, char** argv) {
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= reps;
-        printf("K=%d %s  %.4f ms  %.3f of 8 TB/s\n", K, ok ? "OK" : "MISMATCH", ms, bytes / ms / 1e6 / 8000.0);
+        (void)K;
+        printf("%-20s %s  %.4f ms  %.3f of 8 TB/s\n", names[mode], ok ? "OK" : "MISMATCH", ms, bytes / ms / 1e6 / 8000.0);
         fflush(stdout);
     }
     return 0;
