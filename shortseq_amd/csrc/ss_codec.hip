@@ -623,18 +623,22 @@ __device__ __forceinline__ void ham_store2(uint32_t* p, uint32_t lo, uint32_t hi
 // (lane 2k: dwords 0-2 = word 0 and the low half of word 1; lane 2k+1: dwords 3-5), so a
 // wave-instruction loads 768 contiguous bytes (32 reads, six whole lines) with no shuffle needed to
 // assemble a read.  The split at bit 32 of word 1 falls on a 2-bit boundary, so each lane's three
-// 32-bit XOR-collapse-popcounts plus one DPP pair swap give the read's distance, and the even lanes
-// store 32 consecutive distances (128 B).  A wave takes U groups of 32 reads.  Lanes past n load the
-// last read again (clamped, branch-free) and store nothing.  Same box (tools/tune_ham3.hip): 0.806
-// of the 8-TB/s peak against 0.776-0.786 for the former lane-triple form over 1-KiB chunks (three
-// shuffles and three partial 8-B stores per 128 reads), 0.791 with that form's distances gathered
-// into dwordx4 stores, 0.73 with the chunks DMA'd into LDS (global_load_lds) and read back per lane.
+// 32-bit XOR-collapse-popcounts plus one DPP pair swap give the read's distance.  A wave takes U
+// groups of 32 reads; their U x 32 distances go through LDS (one 4-B write per even lane and group)
+// and leave as ONE dwordx4 store from U x 8 lanes.  Lanes past n load the last read again (clamped,
+// branch-free); the wave holding the batch end (or an output that is not 16-B aligned) stores its
+// distances one by one.  Same box (tools/tune_ham3.hip, profiles/r3/ham3_x3s.log): 0.826-0.835 of the
+// 8-TB/s peak in 128-thread blocks at U = 2 (256 threads 0.819-0.829), against 0.793-0.796 for the same lanes storing
+// 4 B from every even lane (U = 4, one-wave blocks), 0.776-0.786 for the former lane-triple form
+// over 1-KiB chunks, 0.73 with the chunks DMA'd into LDS (global_load_lds) and read back per lane.
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 template <bool PAIR, int T, int U>
 __global__ __launch_bounds__(T) void k_ham_dense3x(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                                                    const uint64_t* __restrict__ ref, uint64_t n,
                                                    uint32_t* __restrict__ out) {
     constexpr uint32_t NWV = T / 64;
+    static_assert(U * 8 <= 64, "one dwordx4 store per wave");
+    __shared__ __attribute__((aligned(16))) uint32_t sd[NWV][U * 32];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, h = lane & 1u;
     const uint64_t g0 = ((uint64_t)blockIdx.x * NWV + wv) * U;     // the wave's first group of 32 reads
     u32x3 x[U], y[U];
@@ -657,8 +661,18 @@ __global__ __launch_bounds__(T) void k_ham_dense3x(const uint32_t* __restrict__ 
         if constexpr (PAIR) d = ham32(x[u].x ^ y[u].x) + ham32(x[u].y ^ y[u].y) + ham32(x[u].z ^ y[u].z);
         else d = ham32(x[u].x ^ c0) + ham32(x[u].y ^ c1) + ham32(x[u].z ^ c2);
         d += swap_pair(d);
-        const uint64_t r = (g0 + u) * 32 + (lane >> 1);
-        if (!h && r < n) ham_store(&out[r], d);
+        if (!h) sd[wv][u * 32 + (lane >> 1)] = d;
+    }
+    __syncthreads();
+    const uint64_t rb = g0 * 32;
+    if (rb + U * 32 <= n && (((uintptr_t)out) & 15u) == 0) {
+        if (lane < U * 8) {
+            const uint4 v = *(const uint4*)&sd[wv][4 * lane];
+            st_stream((uint4*)(out + rb + 4 * lane), v);
+        }
+    } else {
+        for (uint32_t k = lane; k < U * 32; k += 64)
+            if (rb + k < n) ham_store(&out[rb + k], sd[wv][k]);
     }
 }
 
@@ -1163,8 +1177,8 @@ static int launch_ham(const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t
     const bool aligned = (((uintptr_t)a | (uintptr_t)(pair ? b : a)) & 15u) == 0 && (((uintptr_t)out) & 7u) == 0;
     if (wpr == W && aligned && W <= 32) {   // dense rows: the streaming kernel (W <= 32 keeps wl < 4096 exact)
         hipStream_t s = (hipStream_t)stream;
-        if (W == 3) {   // 96 nt (C3'): lane pairs of dwordx3 halves, 4 x 32 reads per one-wave block
-            constexpr int T = 64, U = 4;
+        if (W == 3) {   // 96 nt (C3'): lane pairs of dwordx3 halves, 2 x 32 reads per wave, 2 waves per block
+            constexpr int T = 128, U = 2;
             const unsigned grid = grid_for(n, (uint64_t)32 * (T / 64) * U);
             const uint32_t *a32 = (const uint32_t*)a, *b32 = (const uint32_t*)b;
             if (pair) hipLaunchKernelGGL((k_ham_dense3x<true, T, U>), dim3(grid), dim3(T), 0, s, a32, b32, b, n, out);

@@ -194,6 +194,52 @@ static void launch_glds(const uint64_t* a, const uint64_t* ref, uint64_t n, uint
     hipLaunchKernelGGL((k_ham3_glds<T, G>), dim3((unsigned)(n / per)), dim3(T), 0, 0, (const uint4*)a, ref, n, out);
 }
 
+
+// x3 with the wave's U x 32 distances gathered through LDS into dwordx4 stores (U * 8 lanes, one
+// store instruction) instead of U stores of 4 B from 32 even lanes
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_ham3_x3s(const uint32_t* __restrict__ a, const uint64_t* __restrict__ ref,
+                                                uint64_t n, uint32_t* __restrict__ out) {
+    constexpr uint32_t NWV = T / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t sd[NWV][U * 32];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, h = lane & 1u;
+    const uint64_t g0 = ((uint64_t)blockIdx.x * NWV + wv) * U;
+    u32x3 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t rc = min((g0 + u) * 32 + (lane >> 1), n - 1);
+        x[u] = __builtin_nontemporal_load((const u32x3*)(a + rc * 6 + 3 * h));
+    }
+    const uint64_t r0 = ref[0], r1 = ref[1], r2 = ref[2];
+    const uint32_t c0 = h ? (uint32_t)(r1 >> 32) : (uint32_t)r0;
+    const uint32_t c1 = h ? (uint32_t)r2 : (uint32_t)(r0 >> 32);
+    const uint32_t c2 = h ? (uint32_t)(r2 >> 32) : (uint32_t)r1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint32_t d = ham32(x[u].x ^ c0) + ham32(x[u].y ^ c1) + ham32(x[u].z ^ c2);
+        d += swap_pair(d);
+        if (!h) sd[wv][u * 32 + (lane >> 1)] = d;
+    }
+    __syncthreads();
+    const uint64_t rb = g0 * 32;
+    if (rb + U * 32 <= n) {
+        if (lane < U * 8) {
+            const uint4 v = *(const uint4*)&sd[wv][4 * lane];
+            const u32x4 q = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(q, (u32x4*)(out + rb + 4 * lane));
+        }
+    } else {
+        for (uint32_t k = lane; k < U * 32; k += 64)
+            if (rb + k < n) out[rb + k] = sd[wv][k];
+    }
+}
+
+template <int T, int U>
+static void launch_x3s(const uint64_t* a, const uint64_t* ref, uint64_t n, uint32_t* out) {
+    const uint64_t per = (uint64_t)32 * (T / 64) * U;
+    hipLaunchKernelGGL((k_ham3_x3s<T, U>), dim3((unsigned)((n + per - 1) / per)), dim3(T), 0, 0, (const uint32_t*)a, ref, n, out);
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 30;
     const uint64_t n = argc > 2 ? strtoull(argv[2], 0, 10) : 100000000ull;
@@ -205,7 +251,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d1, n * 4));
     hipLaunchKernelGGL(k_fill_words, dim3(8192), dim3(256), 0, 0, w, n * 3);
     CK(hipMemcpy(ref, w + 3 * 12345, 24, hipMemcpyDeviceToDevice));
-    launch_w<64, 4>(w, ref, n, d0);
+    launch_w<128, 2>(w, ref, n, d0);
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> h0(n), h1(n);
     CK(hipMemcpy(h0.data(), d0, n * 4, hipMemcpyDeviceToHost));
@@ -229,15 +275,14 @@ int main(int argc, char** argv) {
         printf("%-28s %s  %.4f ms  %.3f of 8 TB/s\n", name, ok ? "OK " : "BAD", ms, n * 28.0 / (ms * 1e-3) / 8e12);
     };
     for (int pass = 0; pass < 3; ++pass) {
-        run("prod x3 T64 U4", launch_w<64, 4>);
-        run("prod x3 T128 U2", launch_w<128, 2>);
-        run("x4 T64 G1", launch_x4<64, 1>);
-        run("x3 T64 U4", launch_x3<64, 4>);
-        run("x3 T64 U8", launch_x3<64, 8>);
-        run("x3 T128 U4", launch_x3<128, 4>);
-        run("x3 T128 U2", launch_x3<128, 2>);
-        run("x3 T256 U2", launch_x3<256, 2>);
-        run("x3 T64 U2", launch_x3<64, 2>);
+        run("prod (x3 T128 U2, LDS-gathered stores)", launch_w<128, 2>);
+        run("x3s T256 U2", launch_x3s<256, 2>);
+        run("x3s T128 U2", launch_x3s<128, 2>);
+        run("x3s T512 U2", launch_x3s<512, 2>);
+        run("x3s T256 U1", launch_x3s<256, 1>);
+        run("x3s T512 U1", launch_x3s<512, 1>);
+        run("x3s T1024 U1", launch_x3s<1024, 1>);
+        run("x3s T256 U3", launch_x3s<256, 3>);
     }
     return 0;
 }
