@@ -2137,6 +2137,26 @@ __global__ __launch_bounds__(256) void k_mw_merge_claim(Tbl t, const uint64_t* _
     }
 }
 
+// Per-call resets in one dispatch: up to four 8-B words set and a run of u32 words zeroed.  The
+// streamed C5 step issued three stream write packets at ss_counter_reset, one for first_bad and a
+// two-part fill of the sub-bin counters, ~80 us per step with the command processor's gaps between
+// them (profiles/r3/r3e all-configs trace); as two of these launches they cost ~10 us.
+struct PrepWords {
+    unsigned long long* p[4];   // null: unused
+    unsigned long long v[4];
+    uint32_t* zero;             // [nzero] words set to 0 (or null)
+    uint32_t nzero;
+};
+__global__ __launch_bounds__(256) void k_prep(PrepWords w) {
+    if (threadIdx.x < 4 && w.p[threadIdx.x]) *w.p[threadIdx.x] = w.v[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < w.nzero; i += 256) w.zero[i] = 0u;
+}
+
+hipError_t launch_prep(const PrepWords& w, hipStream_t s) {
+    hipLaunchKernelGGL(k_prep, dim3(1), dim3(256), 0, s, w);
+    return hipGetLastError();
+}
+
 Tbl tbl_of(const ss_counter* c) {
     Tbl t;
     t.slots = c->slots;
@@ -2253,11 +2273,15 @@ int ss_counter_reset(ss_counter* c, void* stream) {
     c->L = -1;
     c->occ_src = 0;
     c->reset_pending = true;    // the slots [0, cap): flush_reset or a fresh aggregate
-    uint64_t* sent = (uint64_t*)(c->slots + c->cap);                        // the sentinel slot
-    hipError_t e = set_u64(sent, true, s);
-    if (e == hipSuccess) e = set_u64(sent + 1, true, s);
-    if (e == hipSuccess) e = set_u64((uint64_t*)c->work, false, s);
-    return ss_check(e, "ss_counter_reset");
+    unsigned long long* sent = (unsigned long long*)(c->slots + c->cap);     // the sentinel slot
+    PrepWords w{};
+    w.p[0] = sent;
+    w.v[0] = ~0ull;
+    w.p[1] = sent + 1;
+    w.v[1] = ~0ull;
+    w.p[2] = c->work;                                                        // overflow flags
+    w.v[2] = 0ull;
+    return ss_check(launch_prep(w, s), "ss_counter_reset");
 }
 
 uint64_t ss_counter_capacity(const ss_counter* c) { return c ? c->cap : 0; }
@@ -2376,11 +2400,16 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
                        uint64_t base_index, uint64_t* d_first_bad, void* stream, const uint64_t* words_in) {
     hipStream_t s = (hipStream_t)stream;
     int rc = SS_OK;
+    const uint32_t rb = c->log2cap - c->slice_log;
+    // the optimistic coarse partition below (the C5 path) resets first_bad with its sub-bin counters
+    const bool opt = !words_in && n > 0 && d_ascii && (L == 16 || L == 32) && stride % 16 == 0 &&
+                     (((uintptr_t)d_ascii) & 15) == 0 && n <= c->ws_reads && rb > kCoarseBits &&
+                     rb - kCoarseBits <= 8;
     if (!words_in) {
         if (!d_first_bad) return ss_fail(SS_EARG, "d_first_bad is required");
         if (stride < L) return ss_fail(SS_EARG, "stride < L");
         if ((rc = fix_length(c, L))) return rc;
-        rc = ss_check(set_u64(d_first_bad, true, s), "reset first_bad");
+        if (!opt) rc = ss_check(set_u64(d_first_bad, true, s), "reset first_bad");
         if (rc || n == 0) return rc;
         if (!d_ascii) return ss_fail(SS_EARG, "null buffer");
     } else if (n == 0) {
@@ -2484,7 +2513,12 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
             const uint64_t cap1 = c->ws_cap1;
             w.slab = (uint32_t)c->ws_slab;
             w.spill_ctr = c->ws_fill + fill_at(kSpillCtr);
-            rc = ss_check(hipMemsetAsync(c->ws_fill, 0, kFillWords * sizeof(uint32_t), s), "fill reset");
+            PrepWords pw{};
+            pw.p[0] = (unsigned long long*)d_first_bad;
+            pw.v[0] = ~0ull;
+            pw.zero = c->ws_fill;
+            pw.nzero = kFillWords;
+            rc = ss_check(launch_prep(pw, s), "first_bad / fill reset");
             if (rc) return rc;
             // grid-stride over tiles: exactly the resident blocks (no second, partial round)
             static const int pf_grid = [] {
