@@ -233,6 +233,15 @@ def test_hamming_out_alignment(gpu, oracle):
         pair = torch.zeros(n + 1, dtype=torch.int32, device=gpu)[1:]
         assert lib().ss_hamming_pair(wa.data_ptr(), wa.data_ptr(), n, L, wpr, pair.data_ptr(), s) == 0
         assert int(pair.abs().sum()) == 0, L
+        # 8-B aligned, off the 16-B grid: the streaming kernels, with the 96-nt kernel's per-distance
+        # stores in place of its dwordx4 runs
+        out8 = torch.zeros(n + 2, dtype=torch.int32, device=gpu)[2:]
+        assert out8.data_ptr() % 16 == 8
+        assert lib().ss_hamming_ref(wa.data_ptr(), n, L, wpr, ref.data_ptr(), out8.data_ptr(), s) == 0
+        assert np.array_equal(out8.cpu().numpy().astype(np.uint32), want), L
+        pair8 = torch.full((n + 2,), -1, dtype=torch.int32, device=gpu)[2:]
+        assert lib().ss_hamming_pair(wa.data_ptr(), wa.data_ptr(), n, L, wpr, pair8.data_ptr(), s) == 0
+        assert int(pair8.abs().sum()) == 0, L
 
 
 def test_synth_matches_oracle_generator(gpu, oracle):
