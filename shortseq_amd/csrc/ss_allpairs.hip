@@ -228,9 +228,6 @@ __device__ __forceinline__ void tri_pair(uint64_t k, uint64_t t, uint32_t& bi, u
     bj = (uint32_t)(i + (int64_t)(k - before(i)));
 }
 
-#ifndef SS_AP_PAIR_TILES
-#define SS_AP_PAIR_TILES 0   // 1 (two tiles interleaved) measured level at RB 8, slower at RB 4 (profiles/r2/r2f/tune_ap_pair.log)
-#endif
 // TAB: fragments from a 256-entry LDS table (4 codes of a byte -> the 4 one-hot VGPRs of a k-step
 // half, one ds_read_b128) instead of per-VGPR bit arithmetic.  Positions P .. 8 KS - 1 are then
 // code 0 on both sides and add the constant 8 KS - P to every result, folded into the threshold.
@@ -305,25 +302,10 @@ __global__ __launch_bounds__(256) void k_allpairs_mfma(AllPairsArgs a, uint32_t 
         // RB >= 4 (short reads): all RB tiles of the column block first, one ballot for all of
         // them: no branch between the tiles' MFMA chains, so they interleave; a hit (rare)
         // recomputes the tiles below.  (100k x 12 nt: 14.7 -> 15.6 T pairs/s; at RB <= 2 the
-        // per-tile form measured faster.)
+        // per-tile form measured faster.  Two tiles' chains explicitly interleaved with independent
+        // accumulators measured level at RB 8, slower at RB 4: profiles/r2/r2f/tune_ap_pair.log.)
         if constexpr (RB >= 4) {
             int any_all = 0;
-#if SS_AP_PAIR_TILES
-            // two tiles' chains interleaved (independent accumulators), so one tile's MFMAs cover the
-            // other's result latency instead of an s_nop before every OR-reduction
-#pragma unroll
-            for (int rb = 0; rb < RB; rb += 2) {
-                v16i32 D0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[rb][0], B[0], Cinit, 0, 0, 0);
-                v16i32 D1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[rb + 1][0], B[0], Cinit, 0, 0, 0);
-#pragma unroll
-                for (int s2 = 1; s2 < KS; ++s2) {
-                    D0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[rb][s2], B[s2], D0, 0, 0, 0);
-                    D1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[rb + 1][s2], B[s2], D1, 0, 0, 0);
-                }
-#pragma unroll
-                for (int q = 0; q < 16; ++q) any_all |= D0[q] | D1[q];
-            }
-#else
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
                 v16i32 D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[rb][0], B[0], Cinit, 0, 0, 0);
@@ -332,7 +314,6 @@ __global__ __launch_bounds__(256) void k_allpairs_mfma(AllPairsArgs a, uint32_t 
 #pragma unroll
                 for (int q = 0; q < 16; ++q) any_all |= D[q];
             }
-#endif
             if (!__ballot(any_all & 128)) continue;
         }
 #pragma unroll

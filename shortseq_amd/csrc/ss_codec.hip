@@ -605,18 +605,14 @@ __global__ __launch_bounds__(kThreads) void k_ham_group(const uint64_t* __restri
     if (r < n && k == 0) out[r] = part;
 }
 
-#ifndef SS_HAM_NT
-#define SS_HAM_NT 1   // same-box A/B, C3' 32 / 96 nt: 0.73 -> 0.78, 0.69 -> 0.72 of peak (512 nt unchanged)
-#endif
-// distance stores of the dense hamming kernels (streamed once: nontemporal)
+// distance stores of the dense hamming kernels (streamed once: nontemporal; same-box A/B against
+// plain stores, C3' 32 / 96 nt: 0.73 -> 0.78, 0.69 -> 0.72 of peak, 512 nt unchanged)
 __device__ __forceinline__ void ham_store(uint32_t* p, uint32_t v) {
-    if (SS_HAM_NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    __builtin_nontemporal_store(v, p);
 }
 __device__ __forceinline__ void ham_store2(uint32_t* p, uint32_t lo, uint32_t hi) {
     const uint64_t v = ((uint64_t)hi << 32) | lo;
-    if (SS_HAM_NT) __builtin_nontemporal_store(v, (uint64_t*)p);
-    else *(uint64_t*)p = v;
+    __builtin_nontemporal_store(v, (uint64_t*)p);
 }
 
 // Dense hamming for W = 3 (96 nt, C3'): a read's 24 B are two dwordx3 halves held by a lane pair

@@ -28,10 +28,8 @@ namespace {
 
 using namespace ssd;
 
-#ifndef SS_FQ_T
-#define SS_FQ_T 256   // 512 x 4 / 512 x 8 / 128 x 8 / 128 x 16 measured slower or level (profiles/r2/r2f/tune_f1_t.log)
-#endif
-constexpr int kFqT = SS_FQ_T;                               // threads per block
+// 512 x 4 / 512 x 8 / 128 x 8 / 128 x 16 measured slower or level (profiles/r2/r2f/tune_f1_t.log)
+constexpr int kFqT = 256;                                   // threads per block
 constexpr int kFqU = 4;                                     // 16-B chunks per thread
 constexpr uint64_t kFqTile = (uint64_t)kFqT * kFqU * 16;    // 16 KiB per block
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
@@ -328,10 +326,8 @@ __global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ bu
 //   k_fq_nulfix: sequence lines holding a NUL byte re-measured
 // HBM: the file once + 2 B per line written and read back (the newline's offset in its 32-KiB tile)
 // + 12 B per sequence line of output.
-#ifndef SS_FQ_U1
-#define SS_FQ_U1 8   // 16-KiB tiles (4) 0.525 ms, 64-KiB tiles (16) level with 32 KiB (tools/tune_f1.hip)
-#endif
-constexpr int kFqU1 = SS_FQ_U1;                                // 16-B chunks per thread
+// 16-KiB tiles (4) 0.525 ms, 64-KiB tiles (16) level with 32 KiB (tools/tune_f1.hip)
+constexpr int kFqU1 = 8;                                       // 16-B chunks per thread
 constexpr uint64_t kFqTile1 = (uint64_t)kFqT * kFqU1 * 16;     // 32 KiB per tile
 
 constexpr uint32_t kStageShards = 64, kShardStride = 32;       // counters 128 B apart
