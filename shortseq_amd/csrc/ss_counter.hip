@@ -1920,6 +1920,46 @@ __device__ __forceinline__ bool words_eq(const uint64_t* a, const uint64_t* b, u
     return eq;
 }
 
+// The same test for rows of a compile-time W1 words: each row read as the 16-B-aligned chunks
+// holding it, ceil((8 W1 + 8) / 16) dwordx4 gathers instead of W1 dwordx2 (the aggregate's row
+// gathers bound it on address processing, one cache line per lane per instruction).  An aligned
+// chunk never leaves the page of the row bytes it holds.  EVEN: W1 even and the rows' base 16-B
+// aligned, so every row starts a chunk.
+template <int W1, bool EVEN>
+__device__ __forceinline__ void row_chunks(const uint64_t* p, uint64_t (&v)[EVEN ? W1 : W1 + 2], bool& odd) {
+    constexpr int NC = EVEN ? W1 / 2 : (W1 + 2) / 2;
+    const uint4* c = (const uint4*)((uintptr_t)p & ~(uintptr_t)15);
+    odd = !EVEN && ((uintptr_t)p & 8u);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const uint4 x = c[k];
+        v[2 * k] = (uint64_t)x.y << 32 | x.x;
+        v[2 * k + 1] = (uint64_t)x.w << 32 | x.z;
+    }
+}
+
+template <int W1, bool EVEN>
+__device__ __forceinline__ bool rows_eq(const uint64_t* a, const uint64_t* b) {
+    uint64_t va[EVEN ? W1 : W1 + 2], vb[EVEN ? W1 : W1 + 2];
+    bool oa, ob;
+    row_chunks<W1, EVEN>(a, va, oa);
+    row_chunks<W1, EVEN>(b, vb, ob);
+    bool eq = true;
+    // the odd rows' words by masks, not a select of the element (which the compiler turned into a
+    // dynamically indexed array in scratch)
+    const uint64_t ma = 0ull - (uint64_t)oa, mb = 0ull - (uint64_t)ob;
+#pragma unroll
+    for (int j = 0; j < W1; ++j) {
+        if constexpr (EVEN) {
+            eq &= va[j] == vb[j];
+        } else {
+            const uint64_t a = (va[j + 1] & ma) | (va[j] & ~ma), b = (vb[j + 1] & mb) | (vb[j] & ~mb);
+            eq &= a == b;
+        }
+    }
+    return eq;
+}
+
 template <int T>
 __global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, const uint64_t* __restrict__ words,
                                              uint64_t n) {
@@ -1947,13 +1987,15 @@ __global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, con
 constexpr uint32_t kMwT = 1024;
 constexpr uint32_t kMwPerThread = (2u << kMwSliceLog) / kMwT;
 
-template <int T>
+// W1C: the rows' word count at compile time (row gathers as aligned dwordx4 chunks, rows_eq), 0 for
+// any other count (a dwordx2 per word)
+template <int T, int W1C, bool EVEN>
 __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint64_t* __restrict__ words,
                                                     uint64_t base_index) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t S = (uint32_t)t.slice_mask + 1;
     const uint32_t LS = 2 * S;
-    const uint32_t W = t.W;
+    const uint32_t W = W1C ? (uint32_t)W1C : t.W;
     unsigned long long* lkey = (unsigned long long*)smem;                 // [LS] (fp_hi << 32 | rep)
     unsigned long long* skey = lkey + LS;                                 // [S] slice fingerprints
     uint32_t* lcnt = (uint32_t*)(skey + S);                               // [LS]
@@ -1987,8 +2029,14 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
                     break;
                 }
             }
-            if ((cur & 0xFFFFFFFF00000000ull) == tag &&
-                words_eq(words + (cur & 0xFFFFFFFFull) * W, words + (uint64_t)idx * W, W)) {
+            bool same = (cur & 0xFFFFFFFF00000000ull) == tag;
+            if (same) {
+                const uint64_t* ra = words + (cur & 0xFFFFFFFFull) * W;
+                const uint64_t* rb = words + (uint64_t)idx * W;
+                if constexpr (W1C > 0) same = rows_eq<W1C, EVEN>(ra, rb);
+                else same = words_eq(ra, rb, W);
+            }
+            if (same) {
                 placed = true;
                 break;
             }
@@ -2067,6 +2115,29 @@ __global__ __launch_bounds__(T) void k_mw_aggregate(Tbl t, PartWs w, const uint6
             sl->ncount -= lcnt[ls];
             if ((uint32_t)f < sl->first) sl->first = (uint32_t)f;
         }
+    }
+}
+
+using MwAggFn = void (*)(Tbl, PartWs, const uint64_t*, uint64_t);
+constexpr int kMwAggFns = 10;
+// every k_mw_aggregate instance: rows of 2..7 words (keys of up to 192 nt, the ShortSeq192 class
+// widths plus the length word) with dwordx4 row gathers, then the any-width form
+constexpr MwAggFn kMwAgg[kMwAggFns] = {
+    k_mw_aggregate<kMwT, 0, false>, k_mw_aggregate<kMwT, 2, true>,  k_mw_aggregate<kMwT, 2, false>,
+    k_mw_aggregate<kMwT, 3, false>, k_mw_aggregate<kMwT, 4, true>,  k_mw_aggregate<kMwT, 4, false>,
+    k_mw_aggregate<kMwT, 5, false>, k_mw_aggregate<kMwT, 6, true>,  k_mw_aggregate<kMwT, 6, false>,
+    k_mw_aggregate<kMwT, 7, false>};
+
+inline MwAggFn mw_aggregate_fn(uint32_t W1, const uint64_t* rows) {
+    const bool a16 = ((uintptr_t)rows & 15u) == 0;
+    switch (W1) {
+    case 2: return kMwAgg[a16 ? 1 : 2];
+    case 3: return kMwAgg[3];
+    case 4: return kMwAgg[a16 ? 4 : 5];
+    case 5: return kMwAgg[6];
+    case 6: return kMwAgg[a16 ? 7 : 8];
+    case 7: return kMwAgg[9];
+    default: return kMwAgg[0];
     }
 }
 
@@ -2497,9 +2568,8 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
             if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_mw_fp<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          kMaxRegions * 4);
-            if (ea == hipSuccess)
-                ea = hipFuncSetAttribute((const void*)k_mw_aggregate<kMwT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         agg_max);
+            for (int f = 0; f < kMwAggFns && ea == hipSuccess; ++f)
+                ea = hipFuncSetAttribute((const void*)kMwAgg[f], hipFuncAttributeMaxDynamicSharedMemorySize, agg_max);
             return ea;
         }();
         if (attrs != hipSuccess) return ss_check(attrs, "hipFuncSetAttribute (dynamic LDS)");
@@ -2583,7 +2653,7 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
             w.bkey = w.akey;
         }
         if (multi)
-            hipLaunchKernelGGL((k_mw_aggregate<kMwT>), dim3(w.R), dim3(kMwT), mw_lds, s, t, w, mw, base_index);
+            hipLaunchKernelGGL(mw_aggregate_fn(t.W, mw), dim3(w.R), dim3(kMwT), mw_lds, s, t, w, mw, base_index);
         else
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);

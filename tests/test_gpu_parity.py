@@ -445,11 +445,16 @@ def test_counter_multiword_bad_read(gpu):
     c.close()
 
 
-@pytest.mark.parametrize("W,U,n", [(3, 5000, 200_000), (6, 100_000, 400_000), (33, 300, 20_000)])
-def test_counter_insert_words(gpu, W, U, n):
+@pytest.mark.parametrize("W,U,n,shift", [(3, 5000, 200_000, 0), (6, 100_000, 400_000, 0), (33, 300, 20_000, 0),
+                                         (2, 3000, 100_000, 1), (4, 50_000, 300_000, 0), (4, 50_000, 300_000, 1),
+                                         (5, 20_000, 150_000, 1), (6, 20_000, 150_000, 1), (7, 20_000, 150_000, 0),
+                                         (8, 20_000, 150_000, 0)])
+def test_counter_insert_words(gpu, W, U, n, shift):
     """Packed-word keys (ss_counter_set_words / ss_counter_insert_words, the drop-in engine's
     length-class tables): rows compared whole, counts and first index against numpy over two
-    inserts; rows one word apart (incl. only the last word, the class's length word) stay apart."""
+    inserts; rows one word apart (incl. only the last word, the class's length word) stay apart.
+    W 2-7 take the aggregate's chunked row gathers (shift 1: rows 8 B off a 16-B boundary, the
+    realigning form); W 8 and 33 the any-width one."""
     import torch
     import shortseq_amd.batch as B
     rng = np.random.default_rng(W)
@@ -463,8 +468,14 @@ def test_counter_insert_words(gpu, W, U, n):
     rows = pool[idx]
     c = B.GpuCounter(1 << max(12, int(2 * U).bit_length()), device=gpu)
     h = n // 2
-    c.insert_words(torch.from_numpy(rows[:h]).to(gpu))
-    c.insert_words(torch.from_numpy(rows[h:]).to(gpu), base_index=h)
+    def dev_rows(a):
+        buf = torch.zeros(a.size + 2, dtype=torch.int64, device=gpu)
+        v = buf[shift:shift + a.size].view(-1, W)
+        v.copy_(torch.from_numpy(a))
+        return v
+
+    c.insert_words(dev_rows(rows[:h]))
+    c.insert_words(dev_rows(rows[h:]), base_index=h)
     assert c.words == W and c.length == -2 and not c.overflowed()
     words, cnt, f = c.items_sorted_words()
     _u, first, counts = np.unique(idx, return_index=True, return_counts=True)
