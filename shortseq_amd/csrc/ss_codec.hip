@@ -361,11 +361,11 @@ __global__ __launch_bounds__(kThreads) void k_encode_class(const uint8_t* in, co
 //      class the tile's first row and count (LDS atomics); a scan of W + 1 over the reads
 //   b. lane per word slot in read order (k_encode_var_dense's access pattern: consecutive lanes,
 //      consecutive words of consecutive reads): word w < W packed (encode_word_q), w == W = the
-//      length, into the tile's LDS copy of its class spans; the read's 64-bit hash folded by an LDS
-//      xor (the row's words, mixed)
-//   c. the spans out with dense stores (a per-class run of whole rows), and each read's hash into
-//      class W's HyperLogLog registers (2^kHllLog per class, max of the rank), which the engine
-//      reads to size each class's table by its distinct keys rather than by its reads.
+//      length, into the tile's LDS copy of its class spans, its class beside it (a byte)
+//   c. the spans out with dense stores (a per-class run of whole rows), and each read's row hash
+//      (row_fold over its LDS row) into class W's HyperLogLog registers (2^kHllLog per class, max
+//      of the rank), which the engine reads to size each class's table by its distinct keys rather
+//      than by its reads.
 // (A lane-per-read-slot form with the rows stored straight from registers measured 3.6 ms against
 // 2.75 for the four per-class passes on the f2 batch: its row stores land 24-48 B at a time.)
 struct ClassOut {
@@ -373,6 +373,22 @@ struct ClassOut {
     uint32_t bin0;
 };
 constexpr uint32_t kClsTile = 256;
+
+// HyperLogLog hash of a packed row (k_encode_classes, k_hll_rows; only the class tables' sizing
+// reads it): the words rotated by position (23 w + 7 mod 64, distinct for w < 64) folded by xor,
+// then one splitmix64 finalizer -- two 64-bit multiplies per row.  (Mixing every word through
+// splitmix64 cost three quarter-rate 64-bit multiplies per word, plus an LDS atomic per word.)
+__device__ __forceinline__ uint64_t row_fold(uint64_t acc, uint64_t word, uint32_t w) {
+    const uint32_t r = (w * 23u + 7u) & 63u;
+    return acc ^ ((word << r) | (word >> ((64u - r) & 63u)));
+}
+
+__device__ __forceinline__ void hll_add(uint32_t* reg_base, uint64_t acc, uint32_t W1) {
+    const uint64_t h = splitmix64(acc ^ W1);
+    uint32_t* reg = reg_base + (uint32_t)(h >> (64 - kHllLog));
+    const uint32_t rho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
+    if (*reg < rho) atomicMax(reg, rho);    // registers settle early: most reads only load
+}
 
 template <int MAXW1>
 __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, const uint64_t* __restrict__ offs,
@@ -382,7 +398,7 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
                                                              uint64_t* __restrict__ out, uint32_t* hll,
                                                              unsigned long long* first_bad) {
     __shared__ uint64_t sw[kClsTile * MAXW1];             // the tile's class spans, class after class
-    __shared__ unsigned long long sfp[kClsTile];
+    __shared__ uint8_t scls[kClsTile * MAXW1];            // span slot -> its class
     __shared__ uint64_t soff[kClsTile];
     __shared__ uint32_t srow[kClsTile];                   // row within the tile's span of its class
     __shared__ uint16_t sqoff[kClsTile + 1], sL[kClsTile];
@@ -407,7 +423,6 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
         soff[t] = offs[r];
     }
     sL[t] = (uint16_t)(cls ? L : 0u);
-    sfp[t] = 0;
     uint32_t inc = w1;
     for (uint32_t d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(inc, d);
@@ -443,25 +458,22 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
             const uint32_t nb = min(32u, LL - 32u * w);
             word = encode_word_q(in + soff[tt] + 32u * w, nb, nb < 32u, bad);
         }
-        sw[cbase[WW] + srow[tt] * (WW + 1u) + w] = word;
-        atomicXor(&sfp[tt], (unsigned long long)splitmix64(word ^ (0x9E3779B97F4A7C15ull * (w + 1))));
+        const uint32_t at = cbase[WW] + srow[tt] * (WW + 1u) + w;
+        sw[at] = word;
+        scls[at] = (uint8_t)WW;
         report_bad(bad != 0u, r0 + tt, first_bad);
     }
     __syncthreads();
     // c. the class spans out (dense), the sketches
     for (uint32_t q = t; q < Q; q += kClsTile) {
-        uint32_t lo = 2, hi = 33;                          // the class whose span holds q: cbase[lo] <= q
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (cbase[mid] <= q) lo = mid; else hi = mid;
-        }
-        out[co.woff[lo] + (uint64_t)rmin[lo] * (lo + 1u) + (q - cbase[lo])] = sw[q];
+        const uint32_t c = scls[q];
+        out[co.woff[c] + (uint64_t)rmin[c] * (c + 1u) + (q - cbase[c])] = sw[q];
     }
     if (cls) {
-        const uint64_t h = sfp[t];
-        uint32_t* reg = hll + ((uint64_t)W << kHllLog) + (uint32_t)(h >> (64 - kHllLog));
-        const uint32_t rho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
-        if (*reg < rho) atomicMax(reg, rho);    // registers settle early: most reads only load
+        const uint64_t* row = sw + cbase[W] + srow[t] * w1;
+        uint64_t acc = 0;
+        for (uint32_t w = 0; w < w1; ++w) acc = row_fold(acc, row[w], w);
+        hll_add(hll + ((uint64_t)W << kHllLog), acc, w1);
     }
 }
 
@@ -469,11 +481,9 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
 __global__ __launch_bounds__(kThreads) void k_hll_rows(const uint64_t* __restrict__ rows, uint64_t m, uint32_t W1,
                                                        uint32_t* hll) {
     for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kThreads) {
-        uint64_t h = 0;
-        for (uint32_t w = 0; w < W1; ++w) h ^= splitmix64(rows[i * W1 + w] ^ (0x9E3779B97F4A7C15ull * (w + 1)));
-        uint32_t* reg = hll + (uint32_t)(h >> (64 - kHllLog));
-        const uint32_t rho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
-        if (*reg < rho) atomicMax(reg, rho);
+        uint64_t acc = 0;
+        for (uint32_t w = 0; w < W1; ++w) acc = row_fold(acc, rows[i * W1 + w], w);
+        hll_add(hll, acc, W1);
     }
 }
 
