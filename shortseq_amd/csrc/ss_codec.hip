@@ -251,17 +251,16 @@ __device__ __forceinline__ uint64_t pack_word_q(const Chunks3& c, uint32_t nb, b
 #pragma unroll
     for (int k = 0; k < 9; ++k) e[k] = a[k] ^ ((a[k] ^ a[min(k + 2, 10)]) & m2);
     uint32_t xw[8];
+    // bytes at or past nb read as 'A', branch-free: dword i keeps k = clamp(nb - 4i, 0, 4) bytes, the
+    // 'A' mask being ~0 << 8k as two shifts of 4k (a single shift by 32 would keep the word whole).
+    // (Per-dword branches on nb - 4i cost ~9 VALU plus exec-mask changes per dword, this 6.)
+    const int nb4 = 4 * (int)nb;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        uint32_t v = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
-        const int m = (int)nb - 4 * i;
-        if (m <= 0) {
-            v = 0x41414141u;
-        } else if (m < 4) {
-            const uint32_t keep = (1u << (8 * m)) - 1u;
-            v = (v & keep) | (0x41414141u & ~keep);
-        }
-        xw[i] = v;
+        const uint32_t v = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sb);
+        const uint32_t k4 = (uint32_t)min(max(nb4 - 16 * i, 0), 16);   // 4k (v_med3_i32)
+        const uint32_t pad = (~0u << k4) << k4;
+        xw[i] = (v & ~pad) | (0x41414141u & pad);
     }
     Enc32 lo = encode16(xw[0], xw[1], xw[2], xw[3], table);
     Enc32 hi = encode16(xw[4], xw[5], xw[6], xw[7], table);
