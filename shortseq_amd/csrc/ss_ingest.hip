@@ -457,13 +457,25 @@ struct ss_ingest {
 
 namespace {
 
-int table_get(ss_ingest* g, uint64_t cap, ss_counter** out) {
+// a pooled table of this capacity, preferring one whose key width W1 (its key-word array) and
+// partition workspace (rows) already fit: a mismatch reallocates them at the first insert (hipFree +
+// hipMalloc, 0.3-0.4 ms per class table on the f2 batch when two classes swapped tables of one size)
+int table_get(ss_ingest* g, uint64_t cap, uint32_t W1, uint64_t rows, ss_counter** out) {
+    size_t best = g->pool.size();
+    int best_score = -1;
     for (size_t i = g->pool.size(); i-- > 0;) {
-        if (g->pool[i].first == cap) {
-            *out = g->pool[i].second;
-            g->pool.erase(g->pool.begin() + (long)i);
-            return ss_counter_reset(*out, g->stream);
+        if (g->pool[i].first != cap) continue;
+        ss_counter* t = g->pool[i].second;
+        const int score = (ss_counter_words(t) == (int)W1 ? 2 : 0) + (ss_counter_reserved(t) >= rows ? 1 : 0);
+        if (score > best_score) {
+            best_score = score;
+            best = i;
         }
+    }
+    if (best < g->pool.size()) {
+        *out = g->pool[best].second;
+        g->pool.erase(g->pool.begin() + (long)best);
+        return ss_counter_reset(*out, g->stream);
     }
     return ss_counter_create(cap, out);
 }
@@ -524,7 +536,7 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
     if (!gr.table) {
         const double scale = gr.L || need < m ? 1.0 : g->est_scale;
         gr.cap = std::min<uint64_t>(1ull << 32, pow2_at_least((uint64_t)(2.0 * (double)need * scale) + 2));
-        int rc = table_get(g, gr.cap, &gr.table);
+        int rc = table_get(g, gr.cap, gr.W1, m, &gr.table);
         return rc ? rc : table_kind(gr, gr.table);
     }
     uint64_t size = 0;
@@ -534,7 +546,7 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
     if (need <= gr.cap / 2) return SS_OK;
     const uint64_t ncap = pow2_at_least(2 * need);
     ss_counter* nt = nullptr;
-    if ((rc = table_get(g, ncap, &nt)) != SS_OK) return rc;
+    if ((rc = table_get(g, ncap, gr.W1, m, &nt)) != SS_OK) return rc;
     if ((rc = table_kind(gr, nt)) != SS_OK) return rc;
     const uint64_t cap = gr.cap + 1;
     const uint32_t W = gr.W1;
