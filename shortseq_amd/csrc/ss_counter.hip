@@ -1960,7 +1960,26 @@ __device__ __forceinline__ bool rows_eq(const uint64_t* a, const uint64_t* b) {
     return eq;
 }
 
-template <int T>
+// words_fp of a row of W1C words read as its aligned dwordx4 chunks (row_chunks)
+template <int W1, bool EVEN>
+__device__ __forceinline__ uint64_t row_fp(const uint64_t* p) {
+    uint64_t v[EVEN ? W1 : W1 + 2];
+    bool odd;
+    row_chunks<W1, EVEN>(p, v, odd);
+    const uint64_t m = 0ull - (uint64_t)odd;
+    uint64_t h = 0x243F6A8885A308D3ull ^ (uint64_t)W1;
+#pragma unroll
+    for (int j = 0; j < W1; ++j) {
+        uint64_t x;
+        if constexpr (EVEN) x = v[j];
+        else x = (v[j + 1] & m) | (v[j] & ~m);
+        h = splitmix64(h ^ x);
+    }
+    return h == kEmpty ? ~1ull : h;
+}
+
+// W1C: rows of W1C words read as aligned chunks (row_fp), 0 for any width
+template <int T, int W1C, bool EVEN>
 __global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, const uint64_t* __restrict__ words,
                                              uint64_t n) {
     extern __shared__ uint32_t hist[];
@@ -1972,7 +1991,9 @@ __global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, con
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
     for (uint64_t r = lo + threadIdx.x; r < hi; r += T) {
-        const uint64_t fp = words_fp(words + r * t.W, t.W);
+        uint64_t fp;
+        if constexpr (W1C > 0) fp = row_fp<W1C, EVEN>(words + r * W1C);
+        else fp = words_fp(words + r * t.W, t.W);
         w.keys[r] = fp;
         atomicAdd(&my[bin_of<true>(t, w, fp)], 1u);
     }
@@ -2128,18 +2149,26 @@ constexpr MwAggFn kMwAgg[kMwAggFns] = {
     k_mw_aggregate<kMwT, 5, false>, k_mw_aggregate<kMwT, 6, true>,  k_mw_aggregate<kMwT, 6, false>,
     k_mw_aggregate<kMwT, 7, false>};
 
-inline MwAggFn mw_aggregate_fn(uint32_t W1, const uint64_t* rows) {
+// index into kMwAgg / kMwFp of the instance for rows of W1 words at `rows`
+inline int mw_variant(uint32_t W1, const uint64_t* rows) {
     const bool a16 = ((uintptr_t)rows & 15u) == 0;
     switch (W1) {
-    case 2: return kMwAgg[a16 ? 1 : 2];
-    case 3: return kMwAgg[3];
-    case 4: return kMwAgg[a16 ? 4 : 5];
-    case 5: return kMwAgg[6];
-    case 6: return kMwAgg[a16 ? 7 : 8];
-    case 7: return kMwAgg[9];
-    default: return kMwAgg[0];
+    case 2: return a16 ? 1 : 2;
+    case 3: return 3;
+    case 4: return a16 ? 4 : 5;
+    case 5: return 6;
+    case 6: return a16 ? 7 : 8;
+    case 7: return 9;
+    default: return 0;
     }
 }
+
+using MwFpFn = void (*)(Tbl, PartWs, uint32_t, const uint64_t*, uint64_t);
+constexpr int kMwFpT = 512;
+constexpr MwFpFn kMwFp[kMwAggFns] = {
+    k_mw_fp<kMwFpT, 0, false>, k_mw_fp<kMwFpT, 2, true>,  k_mw_fp<kMwFpT, 2, false>, k_mw_fp<kMwFpT, 3, false>,
+    k_mw_fp<kMwFpT, 4, true>,  k_mw_fp<kMwFpT, 4, false>, k_mw_fp<kMwFpT, 5, false>, k_mw_fp<kMwFpT, 6, true>,
+    k_mw_fp<kMwFpT, 6, false>, k_mw_fp<kMwFpT, 7, false>};
 
 // Merge of already-counted multi-word entries (distinct keys: e.g. the extraction of another
 // table when a per-length table grows): phase 1 finds each entry's key among the slots that existed
@@ -2565,8 +2594,8 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
             if (ea == hipSuccess)
                 ea = hipFuncSetAttribute((const void*)k_pc_hist<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          kMaxRegions * 4);
-            if (ea == hipSuccess)
-                ea = hipFuncSetAttribute((const void*)k_mw_fp<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            for (int f = 0; f < kMwAggFns && ea == hipSuccess; ++f)
+                ea = hipFuncSetAttribute((const void*)kMwFp[f], hipFuncAttributeMaxDynamicSharedMemorySize,
                                          kMaxRegions * 4);
             for (int f = 0; f < kMwAggFns && ea == hipSuccess; ++f)
                 ea = hipFuncSetAttribute((const void*)kMwAgg[f], hipFuncAttributeMaxDynamicSharedMemorySize, agg_max);
@@ -2628,7 +2657,8 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
         }
         if (multi) {
             const size_t fp_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
-            hipLaunchKernelGGL((k_mw_fp<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, mw, n);
+            static_assert(TF == kMwFpT, "k_mw_fp instances");
+            hipLaunchKernelGGL(kMwFp[mw_variant(t.W, mw)], dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, mw, n);
         } else if (packed_keys) {
             const size_t h_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             hipLaunchKernelGGL((k_pc_hist<TF>), dim3(kPartBlocks), dim3(TF), h_lds, s, t, w, bins1, n);
@@ -2653,7 +2683,7 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
             w.bkey = w.akey;
         }
         if (multi)
-            hipLaunchKernelGGL(mw_aggregate_fn(t.W, mw), dim3(w.R), dim3(kMwT), mw_lds, s, t, w, mw, base_index);
+            hipLaunchKernelGGL(kMwAgg[mw_variant(t.W, mw)], dim3(w.R), dim3(kMwT), mw_lds, s, t, w, mw, base_index);
         else
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, false>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
