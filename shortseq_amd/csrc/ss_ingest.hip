@@ -1130,34 +1130,37 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     unsigned long long* bits = (unsigned long long*)g->slot.p;
     std::vector<GDesc> desc;
     std::vector<Group*> placed;
-    uint32_t gi = 0;
+    // every table extracted, then their entry counts and overflow words back in one sync
+    if ((rc = g->scan.ensure(kScanBlocks + 2 + 2 * (uint64_t)kLenBins + 8))) return rc;
+    uint64_t* d_cnt = g->scan.p + kScanBlocks + 2;
     for (auto& kv : g->groups) {
         Group& gr = kv.second;
-        if (rc) break;
         if (!gr.table) continue;      // a length of an earlier call
         const uint32_t W = gr.W1;
         const uint64_t cap = gr.cap + 1;
+        const uint64_t q = placed.size();
         if ((rc = gr.fps.ensure(cap)) || (rc = gr.words.ensure(cap * W)) || (rc = gr.counts.ensure(cap)) ||
-            (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)) || (rc = g->scan.ensure(kScanBlocks + 8)))
-            break;
+            (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)))
+            return rc;
         rc = ss_counter_extract_words(gr.table, 1, gr.fps.p, gr.lens.p, gr.words.p, gr.counts.p, gr.first.p, cap,
-                                      g->scan.p + kScanBlocks + 2, s);
-        if (!rc) rc = ss_counter_overflow(gr.table, g->scan.p + kScanBlocks + 3, s);
-        if (!rc) rc = ss_check(hipMemcpyAsync(g->h_bad, g->scan.p + kScanBlocks + 2, 16, hipMemcpyDeviceToHost, s), "ingest");
+                                      d_cnt + 2 * q, s);
+        if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 2 * q + 1, s);
+        if (rc) return rc;
+        placed.push_back(&gr);
+    }
+    if (!placed.empty()) {
+        rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 2 * placed.size() * 8, hipMemcpyDeviceToHost, s), "ingest");
         if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest extract");
-        if (rc) break;
-        if (g->h_bad[1]) {
-            rc = ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
-            break;
-        }
-        gr.m = g->h_bad[0];
+        if (rc) return rc;
+    }
+    for (size_t q = 0; q < placed.size(); ++q) {
+        Group& gr = *placed[q];
+        if (g->h_bad[2 * q + 1]) return ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
+        gr.m = g->h_bad[2 * q];
         hipLaunchKernelGGL(k_mark, dim3(grid_of(gr.m + 1, 256)), dim3(256), 0, s, gr.first.p, gr.m, gr.rowmap.p,
                            kNoSlot, bits);
-        desc.push_back({gr.words.p, gr.counts.p, W, gr.L});
-        placed.push_back(&gr);
-        ++gi;
+        desc.push_back({gr.words.p, gr.counts.p, gr.W1, gr.L});
     }
-    if (rc) return rc;
     const uint64_t empty_at = g->empty_count ? g->empty_first : kNoSlot;
     if (g->empty_count)
         hipLaunchKernelGGL(k_mark, dim3(1), dim3(256), 0, s, (const uint64_t*)nullptr, (uint64_t)0,
