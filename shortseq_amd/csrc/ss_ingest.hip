@@ -447,6 +447,11 @@ struct Group {
 struct ss_ingest {
     int device = 0;
     hipStream_t stream = nullptr;
+    // the length classes' table inserts run on up to kSide + 1 streams (independent tables: one
+    // class's short partition kernels and aggregate tail overlap another's); forked / joined by events
+    static constexpr int kSide = 2;
+    hipStream_t side[kSide] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kSide] = {};
     HBuf stage;                    // list bytes / FASTQ chunks (pinned)
     HBuf out_host;                 // results: lens | counts | words (pinned)
     DBuf<uint8_t> dbuf;            // the chunk on the device
@@ -709,6 +714,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                                          : (uint64_t)(1.2 * e) + 256;                  // ~9 sigma above the estimate
         }
     }
+    std::vector<size_t> cls_jobs;
     for (size_t j = 0; j < nj; ++j) {
         const Job& jb = jobs[j];
         if (!live(jb)) continue;
@@ -721,8 +727,8 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if ((rc = gr.rowmap.ensure_keep(gr.rows + jb.m, gr.rows, s))) return rc;
         const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
         if (cls) {
-            rc = ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, s);
-            if (!rc) rc = ss_counter_overflow(gr.table, g->ovf.p + j, s);
+            cls_jobs.push_back(j);     // inserted below, on the class streams
+            continue;
         } else {
             const uint8_t* src = d_buf;
             uint64_t stride = dense_L;
@@ -738,6 +744,38 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (rc) return rc;
         hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, s, sel, jb.m, base, gr.rowmap.p + gr.rows);
         gr.rows += jb.m;
+    }
+    if (!cls_jobs.empty()) {
+        // every table of a class job is sized, reset and its row map grown on the main stream above
+        int used = 0;
+        if (cls_jobs.size() > 1) rc = ss_check(hipEventRecord(g->ev_fork, s), "ingest fork");
+        for (size_t q = 0; q < cls_jobs.size() && !rc; ++q) {
+            const size_t j = cls_jobs[q];
+            const Job& jb = jobs[j];
+            Group& gr = g->groups[jb.bin];
+            const int k = (int)(q % (ss_ingest::kSide + 1));
+            hipStream_t cs = s;
+            if (k > 0) {
+                cs = g->side[k - 1];
+                if (k > used) {
+                    rc = ss_check(hipStreamWaitEvent(cs, g->ev_fork, 0), "ingest fork wait");
+                    used = k;
+                }
+            }
+            if (!rc) rc = ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, cs);
+            if (!rc) rc = ss_counter_overflow(gr.table, g->ovf.p + j, cs);
+            if (rc) break;
+            const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
+            hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, cs, sel, jb.m, base,
+                               gr.rowmap.p + gr.rows);
+            gr.rows += jb.m;
+        }
+        for (int k = 0; k < used; ++k) {     // join (also after an error: nothing may run on past the call)
+            const int e = ss_check(hipEventRecord(g->ev_join[k], g->side[k]), "ingest join");
+            const int w = e ? e : ss_check(hipStreamWaitEvent(s, g->ev_join[k], 0), "ingest join wait");
+            if (!rc) rc = w;
+        }
+        if (rc) return rc;
     }
     if (jobs.empty()) {
         g->nreads += n;
@@ -833,6 +871,11 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
     ss_ingest* g = new ss_ingest();
     g->device = device;
     rc = ss_check(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking), "ingest stream");
+    for (int k = 0; k < ss_ingest::kSide && !rc; ++k) {
+        rc = ss_check(hipStreamCreateWithFlags(&g->side[k], hipStreamNonBlocking), "ingest side stream");
+        if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_join[k], hipEventDisableTiming), "ingest event");
+    }
+    if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming), "ingest event");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_split, 3 * kLenBins * 8, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_bad, (2 * kLenBins + 4) * 8, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_hll, (33ull << kHllLog) * 4, hipHostMallocDefault), "ingest pinned");
@@ -900,6 +943,11 @@ int ss_ingest_destroy(ss_ingest* g) {
     if (g->h_hll) (void)hipHostFree(g->h_hll);
     if (g->h_split) (void)hipHostFree(g->h_split);
     if (g->h_bad) (void)hipHostFree(g->h_bad);
+    for (int k = 0; k < ss_ingest::kSide; ++k) {
+        if (g->side[k]) (void)hipStreamDestroy(g->side[k]);
+        if (g->ev_join[k]) (void)hipEventDestroy(g->ev_join[k]);
+    }
+    if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
     return SS_OK;
