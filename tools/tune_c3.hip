@@ -113,6 +113,38 @@ __global__ __launch_bounds__(T) void k_encode_ham_dense8(G16Args a, uint32_t rpb
         st_stream(&a.counts[r0 + i], s);
     }
 }
+
+// Per-wave LDS form (no block barrier): a wave owns 64 whole reads = 384 consecutive chunks, 6
+// coalesced dwordx4 loads per lane; per-chunk distances go to the wave's own 512-B PAD8 LDS slice,
+// ordered by a wave barrier only, then lane i sums read i and stores its distance (256-B store).
+template <int T>
+__global__ __launch_bounds__(T) void k_encode_ham_wave(G16Args a) {
+    constexpr uint32_t NWV = T / 64;
+    __shared__ uint64_t part8[NWV * 64];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint8_t* part = (uint8_t*)(part8 + wv * 64);
+    const uint64_t r0 = ((uint64_t)blockIdx.x * NWV + wv) * 64;
+    const uint64_t nq = a.n * 6, qmax = nq - 1, c0 = r0 * 6;
+    uint4 x[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) x[j] = ld_stream(&a.in[min(c0 + j * 64 + lane, qmax)]);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t cl = j * 64 + lane, rl = cl / 6u, k = cl - 6u * rl;
+        uint32_t bad;
+        const uint32_t v = encode_chunk<kPathPext>(x[j], k, a, bad);
+        const bool live = c0 + cl < nq;
+        report_bad(live && bad != 0u, r0 + rl, a.first_bad);
+        if (live && a.out32) st_stream(&a.out32[c0 + cl], v);
+        part[8 * rl + k] = (uint8_t)((live && k < a.ham2) ? ham32(v ^ a.ref32[k]) : 0u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t p = part8[wv * 64 + lane] & 0xFFFFFFFFFFFFull;
+    const uint32_t s = __builtin_amdgcn_sad_u8((uint32_t)p, 0u, 0u) + __builtin_amdgcn_sad_u8((uint32_t)(p >> 32), 0u, 0u);
+    if (r0 + lane < a.n) st_stream(&a.counts[r0 + lane], s);
+}
 }  // namespace
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -161,6 +193,14 @@ static void prod(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t*
     if (ss_encode_hamming_ref(in, n, 96, 96, words, 3, ref, out, fb, 0)) { printf("prod failed\n"); exit(1); }
 }
 
+template <int T>
+static void vw(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
+    reset_first_bad(fb, 0);
+    const uint64_t per = (uint64_t)64 * (T / 64);
+    hipLaunchKernelGGL((k_encode_ham_wave<T>), dim3((unsigned)((n + per - 1) / per)), dim3(T), 0, 0,
+                       args(in, n, words, ref, out, fb));
+}
+
 typedef void (*Fn)(const uint8_t*, uint64_t, uint64_t*, const uint64_t*, uint32_t*, uint64_t*);
 
 int main(int argc, char** argv) {
@@ -186,6 +226,7 @@ int main(int argc, char** argv) {
         {"prod T128 U3", vp<128, 3>}, {"prod T96 U4", vp<96, 4>}, {"prod T192 U2", vp<192, 2>},
         {"prod T64 U6", vp<64, 6>}, {"prod T128 U6", vp<128, 6>}, {"prod T256 U3", vp<256, 3>},
         {"prod T64 U3", vp<64, 3>},
+        {"wave T64", vw<64>}, {"wave T128", vw<128>}, {"wave T256", vw<256>}, {"wave T512", vw<512>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // correctness: small batch with an invalid byte in read 777777 (chunk 4), then the full batch
