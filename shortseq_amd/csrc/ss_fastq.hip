@@ -156,6 +156,46 @@ __global__ __launch_bounds__(1024) void k_fq_scan_groups(uint64_t* __restrict__ 
     }
 }
 
+// One-pass path: k_fq_scan_local and k_fq_scan_groups in one launch.  The group blocks scan as
+// above; the last one to finish (a ticket among the per-call reset words) then turns the group
+// totals into group bases and writes the newline count (one launch and its gap fewer per chunk).
+__global__ __launch_bounds__(1024) void k_fq_scan_last(const uint32_t* __restrict__ tile_cnt, uint64_t ntiles,
+                                                       uint64_t* __restrict__ tile_base, uint64_t* group_tot,
+                                                       uint64_t ngroups, uint32_t* ticket, uint64_t* d_nl) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    __shared__ uint32_t last;
+    const uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+    const uint64_t v = i < ntiles ? tile_cnt[i] : 0;
+    uint64_t total;
+    const uint64_t ex = block_excl_scan_1024(v, wsum, total);
+    if (i < ntiles) tile_base[i] = ex;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&group_tot[blockIdx.x], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t k = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = k + 1 == gridDim.x;
+        carry = 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    for (uint64_t g0 = 0; g0 < ngroups; g0 += 1024) {
+        const uint64_t g = g0 + threadIdx.x;
+        const uint64_t gv = g < ngroups ? __hip_atomic_load(&group_tot[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        uint64_t gt;
+        const uint64_t gx = block_excl_scan_1024(gv, wsum, gt);
+        const uint64_t c = carry;
+        if (g < ngroups) group_tot[g] = c + gx;       // group base
+        __syncthreads();
+        if (threadIdx.x == 0) carry = c + gt;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        tile_base[ntiles] = carry;
+        *d_nl = carry;
+    }
+}
+
 // NUL bytes are rare in FASTQ text: a sequence line holding one is appended (once per lane) to a
 // short list in the workspace, and k_fq_nulfix re-measures those lines with a strlen scan.  A list
 // that overflows makes k_fq_nulfix re-measure every line (exact either way).  Neither the offsets
@@ -321,9 +361,10 @@ __global__ __launch_bounds__(kFqT) void k_fq_emit(const uint8_t* __restrict__ bu
 //                atomics per us, which capped a single shared counter at 0.75 ms per 60k tiles.
 //                A region that runs full raises the overflow word (the caller retries with a larger
 //                bound).  NUL bytes (rare) go to a position list.
-//   k_fq_scan_local / k_fq_scan_groups over the tile counts -> each tile's first line number
-//   k_fq_place : tile-wise, the staged positions with their line numbers -> offsets / lens
-//   k_fq_nulfix: sequence lines holding a NUL byte re-measured
+//   k_fq_scan_last over the tile counts -> each tile's first line number (group scans, then the
+//                last group block scans the group totals)
+//   k_fq_place : tile-wise, the staged positions with their line numbers -> offsets / lens; the
+//                sequence lines holding a NUL byte (when the chunk has any) re-measured in place
 // HBM: the file once + 2 B per line written and read back (the newline's offset in its 32-KiB tile)
 // + 12 B per sequence line of output.
 // 16-KiB tiles (4) 0.525 ms, 64-KiB tiles (16) level with 32 KiB (tools/tune_f1.hip)
@@ -498,6 +539,29 @@ __device__ __forceinline__ uint64_t start_before(const FqStage& st, uint64_t til
     return 0;
 }
 
+// A sequence line [start, stop) (stop: its '\n', or the chunk end for an unterminated last line)
+// with a NUL byte: strlen stops at the first NUL (the k_fq_nulfix rule, applied as the line is
+// placed).  Only when the chunk holds NULs: a short list is searched, a long or overflowed one
+// sends the line to a byte scan.
+constexpr uint32_t kNulListScan = 64;
+__device__ __forceinline__ uint32_t nul_len(const uint8_t* __restrict__ buf, const FqStage& st, uint32_t nulc,
+                                            uint64_t start, uint64_t stop, uint32_t len) {
+    uint64_t first = stop;
+    if (nulc <= kNulListScan) {
+        for (uint32_t k = 0; k < nulc; ++k) {
+            const uint64_t p = st.nul_pos[k];
+            if (p >= start && p < first) first = p;
+        }
+    } else {
+        for (uint64_t p = start; p < stop; ++p)
+            if (buf[p] == 0) {
+                first = p;
+                break;
+            }
+    }
+    return first < stop ? fq_len(first - start) : len;
+}
+
 __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ buf, FqOut o, uint64_t line0,
                                                   int at_eof, FqStage st, uint64_t ntiles,
                                                   const uint64_t* __restrict__ tile_base,
@@ -506,6 +570,7 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
                                                   uint64_t* d_nreads) {
     const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nulc = *st.nul_cnt;   // NUL bytes in the chunk (k_fq_nlpos): lines re-measured below
     if (tile < ntiles) {
         const uint32_t cnt = st.tile_cnt[tile];
         const uint32_t run = st.tile_run[tile];
@@ -540,7 +605,9 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
                             uint64_t start = q ? (uint64_t)pp[q - 1] + 1 : (lane ? (uint64_t)below + 1 : carry);
                             if (start == kNone64) start = start_before(st, tile);
                             o.offsets[i] = start;
-                            lens[i] = fq_len((uint64_t)pp[q] - start + 1);
+                            uint32_t len = fq_len((uint64_t)pp[q] - start + 1);
+                            if (nulc) len = nul_len(buf, st, nulc, start, pp[q], len);
+                            lens[i] = len;
                         }
                     }
                 }
@@ -557,7 +624,9 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
                     uint64_t start = lane ? (uint64_t)below + 1 : carry;
                     if (start == kNone64) start = start_before(st, tile);
                     o.offsets[i] = start;
-                    lens[i] = fq_len((uint64_t)p - start + 1);
+                    uint32_t len = fq_len((uint64_t)p - start + 1);
+                    if (nulc) len = nul_len(buf, st, nulc, start, p, len);
+                    lens[i] = len;
                 }
             }
             carry = (uint64_t)(uint32_t)__shfl((int)p, 63) + 1;
@@ -574,7 +643,8 @@ __global__ __launch_bounds__(256) void k_fq_place(const uint8_t* __restrict__ bu
             if (i < o.max_reads) {
                 const uint64_t start = nl ? start_before(st, ntiles) : 0;
                 o.offsets[i] = start;
-                lens[i] = fq_len(o.nbytes - start);
+                const uint32_t len = fq_len(o.nbytes - start);
+                lens[i] = nulc ? nul_len(buf, st, nulc, start, o.nbytes, len) : len;
             }
         }
     }
@@ -804,7 +874,7 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     st.used = (uint32_t*)(group_base + g + 1);
     st.ovf = st.used + kStageShards * kShardStride;
     st.nul_cnt = st.ovf + 1;
-    st.nul_pos = st.ovf + 4;      // two pad words: the reset below is one 16-B-sized fill, not two
+    st.nul_pos = st.ovf + 4;      // ovf + 2: k_fq_scan_last's ticket, ovf + 3 pad: one 16-B-sized reset fill
     st.tile_cnt = st.nul_pos + kNulCap;
     st.tile_run = st.tile_cnt + t;
     st.tile_last = st.tile_run + t;
@@ -818,17 +888,15 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     o.nul_list = st.nul_pos;
     if (t) {
         hipLaunchKernelGGL(k_fq_nlpos, dim3((unsigned)t), dim3(kFqT), 0, s, d_buf, nbytes, st);
-        hipLaunchKernelGGL(k_fq_scan_local, dim3((unsigned)g), dim3(1024), 0, s, (const uint32_t*)st.tile_cnt, t,
-                           tile_base, group_base);
-    }
-    hipLaunchKernelGGL(k_fq_scan_groups, dim3(1), dim3(1024), 0, s, group_base, g, t, tile_base, d_counts);
-    if (t) {
+        hipLaunchKernelGGL(k_fq_scan_last, dim3((unsigned)g), dim3(1024), 0, s, (const uint32_t*)st.tile_cnt, t,
+                           tile_base, group_base, g, st.ovf + 2, d_counts);
+        // NUL-holding sequence lines are re-measured inside k_fq_place (no k_fq_nulfix pass)
         hipLaunchKernelGGL(k_fq_place, dim3((unsigned)((t + 3) / 4)), dim3(256), 0, s, d_buf, o, line0, at_eof, st, t, tile_base,
                            group_base, (const uint64_t*)d_counts, d_lens, d_counts + 1);
-        hipLaunchKernelGGL(k_fq_nulfix<false>, dim3(256), dim3(256), 0, s, d_buf, o, line0, at_eof,
-                           (const uint64_t*)d_counts, d_lens);
+    } else {
+        hipLaunchKernelGGL(k_fq_scan_groups, dim3(1), dim3(1024), 0, s, group_base, g, t, tile_base, d_counts);
     }
-    rc = ss_check(hipGetLastError(), "k_fq_nlpos/k_fq_place/k_fq_nulfix");
+    rc = ss_check(hipGetLastError(), "k_fq_nlpos/k_fq_scan_last/k_fq_place");
     // k_fq_place's last block wrote the read count and the status word; an empty chunk has no tiles
     if (!rc && t == 0) rc = ss_check(hipMemsetAsync(d_counts + 1, 0, 16, s), "fastq read count / status");
     return rc;
