@@ -377,6 +377,26 @@ int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_rea
 int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords);
 int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words);
 
+/* Multi-device reduce of one call (ShortSeqCounter(list) / read_and_count_fastq sharded over several
+ * engines, counter.pyx:10-70; north_star: "an RCCL reduce over xGMI only for the final histogram
+ * merge").  Engines that counted contiguous shards of one input fold into the first shard's engine on
+ * the devices, so every distinct key crosses PCIe once and the host builds the dict from one
+ * first-occurrence-ordered row list (no per-shard dict merge).
+ *   ss_ingest_export: extract every table of the engine on its own device (entries, counts, and each
+ *                     entry's first read); *h_nkeys = its distinct keys.  Run it in the shard's own
+ *                     thread after its adds (the shards' exports run concurrently).
+ *   ss_ingest_merge:  fold an exported engine into dst: its entries cross to dst's device (peer copies
+ *                     over xGMI, hipMemcpyPeerAsync; a device copy when both share a device), become
+ *                     rows of dst's per-length / per-class tables appended as one block (first read =
+ *                     src_base + the entry's own), counts add, first index = min.  Sources follow
+ *                     dst's reads in input order (src_base = the reads before the source's shard,
+ *                     increasing from call to call).  Then ss_ingest_finish(dst) orders the union.
+ *                     The caller checks ss_ingest_error of every shard first (the first rejected read
+ *                     in input order raises).  Synchronous.  New in this ABI version; the reference
+ *                     has one process-wide dict (counter.pyx:41-54). */
+int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys);
+int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base);
+
 /* ------------------------------------------------------------------------------------------------
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):
  * read i word w: r = splitmix64(seed + i*W + w) masked to its nts, byte j = "ACTG"[(r >> 2j) & 3].

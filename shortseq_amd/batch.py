@@ -22,7 +22,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ._native import SS_EFULL, SsErr, check, lib
+from ._native import SS_EFULL, NativeError, SsErr, check, lib
 
 MAX_NT = 1024
 _NO_BAD = -1  # UINT64_MAX viewed as int64
@@ -472,6 +472,10 @@ class DeviceIngest:
             rc = lib().ss_ingest_add_device(*args)
             check(lib().ss_ingest_set_exact(self._h, self._sizing), "ss_ingest_set_exact")
             self.retried = True
+        if rc == SS_EFULL and not self._fresh:
+            raise NativeError("ss_ingest_add_device: a length class's table, sized by its distinct-key "
+                                  "sketch, ran full on a later batch; the counts so far are void -- reset() "
+                                  "and count every batch again with DeviceIngest(exact=True)")
         check(rc, "ss_ingest_add_device")
         self._fresh = False
         idx, kind, ln = C.c_uint64(), C.c_int(), C.c_uint64()
@@ -499,6 +503,17 @@ class DeviceIngest:
         if copy:
             lens, cnts, wds = lens.copy(), cnts.copy(), wds.copy()
         return lens, cnts, wds
+
+    def export(self) -> int:
+        """Extract this engine's tables for a device-side reduce (ss_ingest_export); its distinct keys."""
+        k = C.c_uint64()
+        check(lib().ss_ingest_export(self._h, C.byref(k)), "ss_ingest_export")
+        return k.value
+
+    def merge(self, src: "DeviceIngest", base: int) -> None:
+        """Fold an exported engine whose reads follow this one's (global read index `base` onward) into
+        this engine's tables on its device (ss_ingest_merge: peer copies, counts add, first = min)."""
+        check(lib().ss_ingest_merge(self._h, src._h, int(base)), "ss_ingest_merge")
 
     def reset(self) -> None:
         check(lib().ss_ingest_reset(self._h), "ss_ingest_reset")

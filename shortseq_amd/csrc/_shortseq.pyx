@@ -76,6 +76,8 @@ ctypedef int (*f_get_device)(int*) noexcept nogil
 ctypedef int (*f_fastq_split)(const char*, uint32_t, uint64_t*, uint64_t*) noexcept nogil
 ctypedef int (*f_add_fastq_range)(ss_ingest*, const char*, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t*) noexcept nogil
 ctypedef int (*f_set_exact)(ss_ingest*, int) noexcept nogil
+ctypedef int (*f_export)(ss_ingest*, uint64_t*) noexcept nogil
+ctypedef int (*f_merge)(ss_ingest*, ss_ingest*, uint64_t) noexcept nogil
 
 cdef struct _Abi:
     f_device_count device_count
@@ -92,6 +94,8 @@ cdef struct _Abi:
     f_fastq_split fastq_split
     f_add_fastq_range add_fastq_range
     f_set_exact set_exact
+    f_export export_keys
+    f_merge merge
 
 cdef _Abi _abi
 cdef bint _abi_ready = False
@@ -127,6 +131,8 @@ cdef int _bind_abi() except -1:
     _abi.fastq_split = <f_fastq_split>_sym(h, b"ss_fastq_split")
     _abi.add_fastq_range = <f_add_fastq_range>_sym(h, b"ss_ingest_add_fastq_range")
     _abi.set_exact = <f_set_exact>_sym(h, b"ss_ingest_set_exact")
+    _abi.export_keys = <f_export>_sym(h, b"ss_ingest_export")
+    _abi.merge = <f_merge>_sym(h, b"ss_ingest_merge")
     _abi_ready = True
     return 0
 
@@ -506,7 +512,7 @@ cdef class ShortSeqCounter(dict):
         cdef Py_ssize_t n = PyList_GET_SIZE(it)
         devs = []
         if device != "host" and n >= (GPU_MIN_READS if device == "auto" else 0):
-            devs = _resolve_devices(device, n)
+            devs = _resolve_devices(device)
         if devs:
             _count_batch_gpu(self, it, devs)
         else:
@@ -521,9 +527,6 @@ cdef class ShortSeqCounter(dict):
                 raise TypeError(f"expected bytes, {type(item).__name__} found")
             seq = _from_py_bytes(item)
             dict.__setitem__(self, seq, dict.get(self, seq, 0) + 1)
-
-
-GPU_MIN_READS_PER_DEVICE = 1 << 20   # "auto" adds a device per this many reads (list) / 256 MB (FASTQ)
 
 
 def _current_device():
@@ -543,19 +546,19 @@ def _current_device():
     return d
 
 
-def _resolve_devices(device, Py_ssize_t work=0, Py_ssize_t per_device=GPU_MIN_READS_PER_DEVICE):
+def _resolve_devices(device):
     """device argument -> the HIP devices a batch call shards over (contiguous read ranges, in
     order), or [] for the host path.
       "host"                 the reference's per-object loop
-      "auto"                 every visible device (one per `per_device` units of work, at least one);
-                             only the current device inside a multi-rank job (LOCAL_RANK set); the
-                             host path when no HIP runtime / device is usable
+      "auto"                 the caller's current device only (ADVICE r3: a worker of an mpirun /
+                             srun / multiprocessing job must not open engines on every GPU of the
+                             node); the host path when no HIP runtime / device is usable.  Fan-out
+                             over several devices is opt-in: "all" or a list
       "cuda"                 the current device
       "cuda:N" / torch.device("cuda", N) / N      device N
       "all"                  every visible device
       a list / tuple of the above                 those devices, in that order (one engine each; a
                                                   device may repeat)"""
-    import os
     cdef int count = 0
     if isinstance(device, str) and device == "host":
         return []
@@ -566,17 +569,14 @@ def _resolve_devices(device, Py_ssize_t work=0, Py_ssize_t per_device=GPU_MIN_RE
             return []
         if _abi.device_count(&count) != 0 or count <= 0:
             return []
-        if os.environ.get("LOCAL_RANK") is not None or int(os.environ.get("WORLD_SIZE", "1") or 1) > 1:
-            return [_current_device()]
-        want = max(1, min(count, work // max(1, per_device)))
-        return list(range(want))
+        return [_current_device()]
     _bind_abi()
     if _abi.device_count(&count) != 0 or count <= 0:
         raise RuntimeError(f"shortseq_amd: device {device!r} requested but no HIP device is visible")
     if isinstance(device, (list, tuple)):
         out = []
         for d in device:
-            out.extend(_resolve_devices(d, work, per_device))
+            out.extend(_resolve_devices(d))
         if not out:
             raise ValueError("empty device list")
         return out
@@ -649,33 +649,24 @@ cdef _raise_ingest_error(ss_ingest* g):
 
 
 cdef _fill_rows(ShortSeqCounter self, uint64_t K, const uint32_t* lens, const uint64_t* counts,
-                const uint64_t* words, bint add=False):
-    """Insert the engine's rows (first-occurrence order) into the dict: one key object per row,
-    inserted with its known hash (the objects' own __hash__ = packed word 0, -1 -> -2; counter.pyx
-    :44-50 inserts the same way), so the loop walks the arrays front to back with no per-key
-    __hash__ call, tuple or sort.  add: the rows of a later shard (every read of it comes after the
-    dict's reads): a key already present adds its count and keeps its place, a new key goes last --
-    the first-occurrence order of the whole list."""
+                const uint64_t* words):
+    """Insert the engine's rows (distinct keys in first-occurrence order) into the empty dict: one key
+    object per row, inserted with its known hash (the objects' own __hash__ = packed word 0, -1 ->
+    -2; counter.pyx:44-50 inserts the same way), so the loop walks the arrays front to back with no
+    per-key __hash__ call, lookup, tuple or sort.  A call sharded over several engines reaches here
+    once, with the shards already reduced on the devices (ss_ingest_merge)."""
     cdef uint64_t k, woff = 0
     cdef uint32_t L
     cdef Py_hash_t h
-    cdef PyObject* old
     for k in range(K):
         L = lens[k]
         if L == 0:
-            dict.__setitem__(self, empty, (dict.get(self, empty, 0) + counts[k]) if add else counts[k])
+            dict.__setitem__(self, empty, counts[k])
             continue
         h = <Py_hash_t>words[woff]
         if h == -1:
             h = -2
-        key = _from_words(words + woff, L)
-        if add:
-            old = _PyDict_GetItem_KnownHash(self, key, h)
-            if old != NULL:
-                _PyDict_SetItem_KnownHash(self, key, <object>old + counts[k], h)
-                woff += _nwords(L)
-                continue
-        _PyDict_SetItem_KnownHash(self, key, counts[k], h)
+        _PyDict_SetItem_KnownHash(self, _from_words(words + woff, L), counts[k], h)
         woff += _nwords(L)
 
 
@@ -688,14 +679,41 @@ def _fill_from_arrays(ShortSeqCounter counter, lens, counts, words):
     _fill_rows(counter, lv.shape[0], &lv[0] if lv.shape[0] else NULL, &cv[0] if cv.shape[0] else NULL, &wv[0])
 
 
-cdef _fill_from_engine(ShortSeqCounter self, ss_ingest* g, bint add=False):
-    """The rows of a finished shard (its first rejected read raises instead)."""
+cdef _fill_from_engine(ShortSeqCounter self, ss_ingest* g):
+    """The rows of a finished engine (its first rejected read raises instead)."""
     cdef const uint32_t* lens
     cdef const uint64_t* counts
     cdef const uint64_t* words
     _raise_ingest_error(g)
     _ingest_check(_abi.results(g, &lens, &counts, &words), "ingest results")
-    _fill_rows(self, _engine_keys(g), lens, counts, words, add)
+    _fill_rows(self, _engine_keys(g), lens, counts, words)
+
+
+cdef _reduce_fill(ShortSeqCounter self, list engines, list bases):
+    """The dict of a call counted on len(engines) shards (engine k: the reads from bases[k] on).  The
+    first rejected read in input order raises (shard order = input order).  Several shards reduce on
+    the devices: every later engine's exported entries fold into engine 0's tables (ss_ingest_merge:
+    peer copies over xGMI), engine 0 orders the union by first read (ss_ingest_finish), and the dict
+    is built once from those rows -- each distinct key crosses PCIe once and gets one dict insert."""
+    cdef Py_ssize_t k, D = len(engines)
+    cdef ss_ingest* g0 = <ss_ingest*><size_t>engines[0][1]
+    cdef ss_ingest* gk
+    cdef uint64_t b, K = 0, NW = 0
+    cdef int rc = 0
+    for k in range(D):
+        _raise_ingest_error(<ss_ingest*><size_t>engines[k][1])
+    if D > 1:
+        for k in range(1, D):
+            gk = <ss_ingest*><size_t>engines[k][1]
+            b = bases[k]
+            with nogil:
+                rc = _abi.merge(g0, gk, b)
+            _ingest_check(rc, "ingest merge")
+        with nogil:
+            rc = _abi.finish(g0, &K, &NW)
+        _ingest_check(rc, "ingest finish")
+        _engine_nkeys[<size_t>g0] = K
+    _fill_from_engine(self, g0)
 
 
 cdef dict _engine_nkeys = {}
@@ -706,9 +724,10 @@ cdef uint64_t _engine_keys(ss_ingest* g):
 
 
 def _shard_work(size_t gh, int kind, size_t blob, size_t lens, uint64_t n, bytes path, uint64_t begin,
-                uint64_t end, uint64_t line0, uint64_t chunk, size_t nseqs_p):
+                uint64_t end, uint64_t line0, uint64_t chunk, size_t nseqs_p, bint export):
     """One shard on its engine, GIL released: count (a staged list slice, or a FASTQ byte range),
-    then -- unless it holds a rejected read -- finish (its rows into the engine's pinned results)."""
+    then -- unless it holds a rejected read -- finish (its rows into the engine's pinned results), or
+    with `export` (one shard of several) extract its tables for the device-side reduce."""
     cdef ss_ingest* g = <ss_ingest*>gh
     cdef int rc, bad_kind = 0
     cdef uint64_t bad_idx = 0, K = 0, NW = 0
@@ -736,7 +755,10 @@ def _shard_work(size_t gh, int kind, size_t blob, size_t lens, uint64_t n, bytes
         if rc == 0:
             rc = _abi.error(g, &bad_idx, &bad_kind, NULL, 0, NULL)
         if rc == 0 and bad_idx == <uint64_t>-1:
-            rc = _abi.finish(g, &K, &NW)
+            if export:
+                rc = _abi.export_keys(g, &K)
+            else:
+                rc = _abi.finish(g, &K, &NW)
     _ingest_check(rc, "ingest")
     _engine_nkeys[gh] = K
 
@@ -766,9 +788,9 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, devs):
     shards; each shard's bytes objects are copied back to back into its engine's pinned staging
     buffer and counted on that engine's device (split on the device into lengths 1-32 and length
     classes, one table per length / class: the length is part of the key, short_seq_64.pyx:41-44),
-    the shards concurrently.  The dict is
-    built from the shards' rows in shard order (each shard's rows in first-occurrence order), which
-    is the first-occurrence order of the whole list.  The first rejected read in list order raises
+    the shards concurrently.  Several shards reduce on the devices into the first shard's engine
+    (_reduce_fill: ss_ingest_export + ss_ingest_merge), which orders the union by global first read
+    -- the first-occurrence order of the whole list.  The first rejected read in list order raises
     the reference's error."""
     cdef Py_ssize_t i, n = PyList_GET_SIZE(reads), ln
     cdef uint64_t total = 0, sub
@@ -809,8 +831,7 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, devs):
                 dst += ln
             jobs.append((<size_t>g, 0, <size_t>base, <size_t>(lens + lo), <uint64_t>(hi - lo), b"", 0, 0, 0, 0, None))
         _run_shard_jobs(jobs)
-        for k in range(D):
-            _fill_from_engine(self, <ss_ingest*><size_t>engines[k][1], k > 0)
+        _reduce_fill(self, engines, [n * k // D for k in range(D)])
     finally:
         free(lens)
         for d, h in engines:
@@ -819,7 +840,8 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, devs):
 
 
 def _run_shard_jobs(jobs):
-    """_run_shards with the nseqs out-pointer of every FASTQ job owned here."""
+    """_run_shards with the nseqs out-pointer of every FASTQ job owned here; several jobs export
+    their tables for the device-side reduce instead of finishing."""
     cdef uint64_t* ns = <uint64_t*>calloc(max(1, len(jobs)), sizeof(uint64_t))
     if ns == NULL:
         raise MemoryError()
@@ -828,7 +850,7 @@ def _run_shard_jobs(jobs):
     try:
         full = []
         for i in range(len(jobs)):
-            full.append((*jobs[i][:10], base + 8 * i))
+            full.append((*jobs[i][:10], base + 8 * i, len(jobs) > 1))
         _run_shards(full)
         return [ns[i] for i in range(len(jobs))]
     finally:
@@ -850,14 +872,13 @@ def _raise_first_error(list reads, Py_ssize_t upto):
 def read_and_count_fastq(filename, device="auto", *, _chunk_bytes=0):
     """counter.pyx:57-70 + fast_read.pyx:3-20: keep line 2 of every 4 lines; each kept line loses
     exactly its last character (strlen - 1, short_seq.pyx:50-52); prints the reference's timings.
-    device "auto" (the visible GPUs) / "cuda[:N]" / "all" / a list: the file is cut into one byte
+    device "auto" (the current GPU) / "cuda[:N]" / "all" / a list: the file is cut into one byte
     range per device at line boundaries (ss_fastq_split), each range streamed to its device in
     pinned chunks and indexed, split by length and counted there (ss_ingest_add_fastq_range), the
     ranges concurrently, and the dict built from the ranges' rows in file order; "host": the
     reference's per-line loop."""
     import os
-    work = os.path.getsize(filename) if os.path.isfile(filename) else 0
-    devs = _resolve_devices(device, work, 256 << 20)
+    devs = _resolve_devices(device)
     if devs:
         return _read_and_count_fastq_gpu(filename, devs, _chunk_bytes)
     cdef FILE* f
@@ -896,7 +917,8 @@ def read_and_count_fastq(filename, device="auto", *, _chunk_bytes=0):
 def _read_and_count_fastq_gpu(filename, devs, uint64_t chunk_bytes=0):
     """The file streamed through one engine per device: range k of ss_fastq_split on devs[k]
     (parallel preads into pinned staging, chunks ending after a newline, one-read FASTQ index, split
-    by length and counted on the device); rows merged in range order."""
+    by length and counted on the device); the ranges reduced on the devices in range order
+    (_reduce_fill)."""
     import os
     cdef int rc
     cdef Py_ssize_t D = len(devs), k
@@ -921,11 +943,11 @@ def _read_and_count_fastq_gpu(filename, devs, uint64_t chunk_bytes=0):
             g = <size_t>_engine(devs[k])
             engines.append((devs[k], g))
             jobs.append((g, 1, 0, 0, 0, fname, begin[k], begin[k + 1], line0[k], chunk_bytes, None))
-        nseqs = sum(_run_shard_jobs(jobs))
+        per = _run_shard_jobs(jobs)
+        nseqs = sum(per)
         t2 = time.time()
         counts = ShortSeqCounter()
-        for k in range(D):
-            _fill_from_engine(counts, <ss_ingest*><size_t>engines[k][1], k > 0)
+        _reduce_fill(counts, engines, [sum(per[:k]) for k in range(D)])
         t3 = time.time()
     finally:
         free(begin)

@@ -357,51 +357,82 @@ __global__ __launch_bounds__(kThreads) void k_encode_class(const uint8_t* in, co
 // block takes kClsTile consecutive reads.  Within the tile the reads of class W hold consecutive rows
 // of W's block (k_len_scatter is stable), so the tile's rows of a class are one contiguous span:
 //   a. per read: class W = ceil(L/32) (L 33..1024), its row (posof[r] - binstart[bin0 + W]); per
-//      class the tile's first row and count (LDS atomics); a scan of W + 1 over the reads
-//   b. lane per word slot in read order (k_encode_var_dense's access pattern: consecutive lanes,
-//      consecutive words of consecutive reads): word w < W packed (encode_word_q), w == W = the
-//      length, into the tile's LDS copy of its class spans, its class beside it (a byte)
-//   c. the spans out with dense stores (a per-class run of whole rows), and each read's row hash
-//      (row_fold over its LDS row) into class W's HyperLogLog registers (2^kHllLog per class, max
-//      of the rank), which the engine reads to size each class's table by its distinct keys rather
-//      than by its reads.
+//      class the tile's first row and count (LDS atomics); one scan gives each read its word slots
+//      (W + 1) and its 16-B chunk slots (the aligned chunks holding its bytes)
+//   b. lane per chunk slot: every chunk a read touches is loaded once (coalesced dwordx4) and
+//      encoded where it lies (encode16 without the alias carry) into 16 codes + a mask of its
+//      rejected bytes + a mask of its bit-6-clear bytes, kept in LDS.  A read starting at byte
+//      sh = off % 16 has word w at code sh of its chunk 2w, so
+//   c. lane per word slot: the word is a funnel shift of three LDS code words by 2 sh bits (tail
+//      codes past the read masked to 'A' = 0), its rejected bytes the same window of the masks; a
+//      partial tail word holding a bit-6-clear byte (the table path's alias carry) is
+//      re-encoded exactly from the blob (encode_word_q).  w == W is the length.  Into the tile's
+//      LDS class spans, the class beside it (a byte)
+//   d. the spans out with dense stores (a per-class run of whole rows); each read's row fingerprint
+//      (words_fp over its LDS row, the class table's slot key) to fps[fpoff[W] + row] when fps is
+//      given, and into class W's HyperLogLog registers (2^kHllLog per class, max of the rank), which
+//      the engine reads to size each class's table by its distinct keys rather than by its reads.
+// Per 32-nt word this is ~2 chunk encodes + a shift (the per-word realignment of encode_word_q from
+// three unaligned chunk loads cost ~210 VALU per word: the former form was VALU-bound at 2.1 ms on
+// the f2 batch).  Dynamic LDS: words kClsTile * w1max u64 + bytes, chunks kClsTile * (2 w1max - 1).
 // (A lane-per-read-slot form with the rows stored straight from registers measured 3.6 ms against
 // 2.75 for the four per-class passes on the f2 batch: its row stores land 24-48 B at a time.)
 struct ClassOut {
     uint64_t woff[33];
+    uint64_t fpoff[33];
     uint32_t bin0;
 };
 constexpr uint32_t kClsTile = 256;
 
-// HyperLogLog hash of a packed row (k_encode_classes, k_hll_rows; only the class tables' sizing
-// reads it): the words rotated by position (23 w + 7 mod 64, distinct for w < 64) folded by xor,
-// then one splitmix64 finalizer -- two 64-bit multiplies per row.  (Mixing every word through
-// splitmix64 cost three quarter-rate 64-bit multiplies per word, plus an LDS atomic per word.)
-__device__ __forceinline__ uint64_t row_fold(uint64_t acc, uint64_t word, uint32_t w) {
-    const uint32_t r = (w * 23u + 7u) & 63u;
-    return acc ^ ((word << r) | (word >> ((64u - r) & 63u)));
-}
-
-__device__ __forceinline__ void hll_add(uint32_t* reg_base, uint64_t acc, uint32_t W1) {
-    const uint64_t h = splitmix64(acc ^ W1);
+__device__ __forceinline__ void hll_add(uint32_t* reg_base, uint64_t fp, uint32_t W1) {
+    const uint64_t h = splitmix64(fp ^ W1);
     uint32_t* reg = reg_base + (uint32_t)(h >> (64 - kHllLog));
     const uint32_t rho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
     if (*reg < rho) atomicMax(reg, rho);    // registers settle early: most reads only load
 }
 
-template <int MAXW1>
+// bit b of the result: byte b of m is nonzero (b < 4)
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t m) {
+    const uint32_t t = ((m & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | m;
+    return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+}
+
+// 16 aligned bytes -> x: 16 codes (no alias carry), y: rejected-byte mask | bit-6-clear mask << 16
+__device__ __forceinline__ uint2 code_chunk(uint4 c) {
+    const uint32_t p0 = c.x & 0x06060606u, p1 = c.y & 0x06060606u, p2 = c.z & 0x06060606u, p3 = c.w & 0x06060606u;
+    const uint32_t m0 = (c.x & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p0);
+    const uint32_t m1 = (c.y & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p1);
+    const uint32_t m2 = (c.z & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p2);
+    const uint32_t m3 = (c.w & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p3);
+    uint2 r;
+    r.x = transpose2x4((p0 >> 1) | (p1 << 1) | (p2 << 3) | (p3 << 5));
+    r.y = 0;
+    if (m0 | m1 | m2 | m3) r.y = nz_bytes(m0) | nz_bytes(m1) << 4 | nz_bytes(m2) << 8 | nz_bytes(m3) << 12;
+    if ((c.x & c.y & c.z & c.w & 0x40404040u) != 0x40404040u)
+        r.y |= (nz_bytes(~c.x & 0x40404040u) | nz_bytes(~c.y & 0x40404040u) << 4 | nz_bytes(~c.z & 0x40404040u) << 8 |
+                nz_bytes(~c.w & 0x40404040u) << 12) << 16;
+    return r;
+}
+
+constexpr uint32_t kClsLoads = 4;     // chunk loads a lane issues before encoding any
+
 __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, const uint64_t* __restrict__ offs,
                                                              const uint32_t* __restrict__ lens, uint64_t n,
                                                              const uint32_t* __restrict__ posof,
                                                              const uint64_t* __restrict__ binstart, ClassOut co,
-                                                             uint64_t* __restrict__ out, uint32_t* hll,
+                                                             uint32_t w1max, uint64_t* __restrict__ out,
+                                                             uint64_t* __restrict__ fps, uint32_t* hll,
                                                              unsigned long long* first_bad) {
-    __shared__ uint64_t sw[kClsTile * MAXW1];             // the tile's class spans, class after class
-    __shared__ uint8_t scls[kClsTile * MAXW1];            // span slot -> its class
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    const uint32_t nslot = kClsTile * w1max, nck = kClsTile * (2u * w1max - 1u);
+    uint64_t* sw = (uint64_t*)dyn;                          // [nslot] the tile's class spans, class after class
+    uint2* ck = (uint2*)(sw + nslot);                       // [nck] chunk codes + masks
+    uint8_t* scls = (uint8_t*)(ck + nck);                   // [nslot] span slot -> its class
+    uint8_t* smap = scls + nslot;                           // [nslot] word slot -> read of the tile
+    uint8_t* cmap = smap + nslot;                           // [nck] chunk slot -> read of the tile
     __shared__ uint64_t soff[kClsTile];
-    __shared__ uint32_t srow[kClsTile];                   // row within the tile's span of its class
-    __shared__ uint16_t sqoff[kClsTile + 1], sL[kClsTile];
-    __shared__ uint8_t smap[kClsTile * MAXW1];            // word slot -> read of the tile
+    __shared__ uint32_t srow[kClsTile];                     // row within the tile's span of its class
+    __shared__ uint16_t sqoff[kClsTile + 1], scoff[kClsTile + 1], sL[kClsTile];
     __shared__ uint32_t rmin[33], rcnt[33], cbase[34], wsum[kClsTile / 64];
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     const uint64_t r0 = (uint64_t)blockIdx.x * kClsTile, r = r0 + t;
@@ -410,19 +441,23 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
         rcnt[t] = 0;
     }
     __syncthreads();
-    // a. classes, rows, spans
+    // a. classes, rows, word and chunk slots
     const uint32_t L = r < n ? lens[r] : 0u;
     const bool cls = L > 32u && L <= SS_MAX_NT;
     const uint32_t W = cls ? (L + 31u) / 32u : 0u, w1 = cls ? W + 1u : 0u;
-    uint32_t row = 0;
+    uint64_t off = 0;
+    uint32_t row = 0, nc = 0;
     if (cls) {
         row = posof[r] - (uint32_t)binstart[co.bin0 + W];
         atomicMin(&rmin[W], row);
         atomicAdd(&rcnt[W], 1u);
-        soff[t] = offs[r];
+        off = offs[r];
+        soff[t] = off;
+        nc = ((uint32_t)(off & 15u) + L + 15u) >> 4;
     }
     sL[t] = (uint16_t)(cls ? L : 0u);
-    uint32_t inc = w1;
+    const uint32_t v = w1 | nc << 16;       // word slots | chunk slots (each < 2^16 per tile)
+    uint32_t inc = v;
     for (uint32_t d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(inc, d);
         if (lane >= d) inc += y;
@@ -430,23 +465,45 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
     if (lane == 63) wsum[wave] = inc;
     __syncthreads();
     uint32_t before = 0;
-    for (uint32_t v = 0; v < wave; ++v) before += wsum[v];
-    const uint32_t q0 = before + inc - w1;
+    for (uint32_t u = 0; u < wave; ++u) before += wsum[u];
+    const uint32_t ex = before + inc - v, q0 = ex & 0xFFFFu, c0 = ex >> 16;
     sqoff[t] = (uint16_t)q0;
-    if (t == kClsTile - 1) sqoff[kClsTile] = (uint16_t)(q0 + w1);
+    scoff[t] = (uint16_t)c0;
+    if (t == kClsTile - 1) {
+        sqoff[kClsTile] = (uint16_t)(q0 + w1);
+        scoff[kClsTile] = (uint16_t)(c0 + nc);
+    }
     for (uint32_t k = 0; k < w1; ++k) smap[q0 + k] = (uint8_t)t;
+    for (uint32_t k = 0; k < nc; ++k) cmap[c0 + k] = (uint8_t)t;
     if (cls) srow[t] = row - rmin[W];
     if (t == 0) {
         uint32_t c = 0;
-        for (uint32_t v = 0; v < 33; ++v) {
-            cbase[v] = c;
-            c += v >= 2 ? rcnt[v] * (v + 1u) : 0u;
+        for (uint32_t u = 0; u < 33; ++u) {
+            cbase[u] = c;
+            c += u >= 2 ? rcnt[u] * (u + 1u) : 0u;
         }
         cbase[33] = c;
     }
     __syncthreads();
-    // b. lane per word slot, read order (a form issuing four slots' loads before packing any: 107
-    //    VGPRs, 3.0 vs 2.6 ms on the f2 batch)
+    // b. lane per chunk slot: kClsLoads chunk loads in flight per lane, then their codes
+    const uint32_t C = scoff[kClsTile];
+    const uint4* in16 = (const uint4*)in;
+    for (uint32_t qb = t; qb < C; qb += kClsLoads * kClsTile) {
+        uint4 x[kClsLoads];
+#pragma unroll
+        for (uint32_t k = 0; k < kClsLoads; ++k) {
+            const uint32_t q = min(qb + k * kClsTile, C - 1u);
+            const uint32_t tt = cmap[q];
+            x[k] = in16[(soff[tt] >> 4) + (q - scoff[tt])];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kClsLoads; ++k) {
+            const uint32_t q = qb + k * kClsTile;
+            if (q < C) ck[q] = code_chunk(x[k]);
+        }
+    }
+    __syncthreads();
+    // c. lane per word slot, read order
     const uint32_t Q = sqoff[kClsTile];
     for (uint32_t q = t; q < Q; q += kClsTile) {
         const uint32_t tt = smap[q];
@@ -455,7 +512,27 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
         uint64_t word = LL;
         if (w < WW) {
             const uint32_t nb = min(32u, LL - 32u * w);
-            word = encode_word_q(in + soff[tt] + 32u * w, nb, nb < 32u, bad);
+            const uint32_t sh = (uint32_t)(soff[tt] & 15u);
+            const uint32_t cb = scoff[tt] + 2u * w, ce = scoff[tt + 1];   // the read's chunks end at ce
+            const uint2 a = ck[cb];
+            const uint2 b = cb + 1u < ce ? ck[cb + 1u] : make_uint2(0u, 0u);
+            const uint2 c = cb + 2u < ce ? ck[cb + 2u] : make_uint2(0u, 0u);
+            const uint64_t lo = (uint64_t)b.x << 32 | a.x;
+            word = sh ? (lo >> (2u * sh)) | ((uint64_t)c.x << (64u - 2u * sh)) : lo;
+            const uint64_t keep = nb < 32u ? (1ull << (2u * nb)) - 1ull : ~0ull;
+            word &= keep;
+            const uint64_t bytes = ((uint64_t)1 << nb) - 1ull;                  // nb <= 32
+            const uint64_t rej = ((uint64_t)(a.y & 0xFFFFu) | (uint64_t)(b.y & 0xFFFFu) << 16 |
+                                  (uint64_t)(c.y & 0xFFFFu) << 32) >> sh;
+            bad = (rej & bytes) != 0ull;
+            if (nb < 32u) {
+                const uint64_t al = ((uint64_t)(a.y >> 16) | (uint64_t)(b.y >> 16) << 16 | (uint64_t)(c.y >> 16) << 32) >> sh;
+                if (al & bytes) {   // an aliased byte in a table-path word: its carry, exactly (rare)
+                    uint32_t b2 = 0;
+                    word = encode_word_q(in + soff[tt] + 32u * w, nb, true, b2);
+                    bad |= b2;
+                }
+            }
         }
         const uint32_t at = cbase[WW] + srow[tt] * (WW + 1u) + w;
         sw[at] = word;
@@ -463,27 +540,23 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
         report_bad(bad != 0u, r0 + tt, first_bad);
     }
     __syncthreads();
-    // c. the class spans out (dense), the sketches
+    // d. the class spans out (dense), fingerprints, sketches
     for (uint32_t q = t; q < Q; q += kClsTile) {
         const uint32_t c = scls[q];
         out[co.woff[c] + (uint64_t)rmin[c] * (c + 1u) + (q - cbase[c])] = sw[q];
     }
     if (cls) {
-        const uint64_t* row = sw + cbase[W] + srow[t] * w1;
-        uint64_t acc = 0;
-        for (uint32_t w = 0; w < w1; ++w) acc = row_fold(acc, row[w], w);
-        hll_add(hll + ((uint64_t)W << kHllLog), acc, w1);
+        const uint64_t fp = words_fp(sw + cbase[W] + srow[t] * w1, w1);
+        if (fps) fps[co.fpoff[W] + row] = fp;
+        hll_add(hll + ((uint64_t)W << kHllLog), fp, w1);
     }
 }
 
 // The same registers from rows already packed (k_encode_class's paths): lane per row, the same hash.
 __global__ __launch_bounds__(kThreads) void k_hll_rows(const uint64_t* __restrict__ rows, uint64_t m, uint32_t W1,
                                                        uint32_t* hll) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kThreads) {
-        uint64_t acc = 0;
-        for (uint32_t w = 0; w < W1; ++w) acc = row_fold(acc, rows[i * W1 + w], w);
-        hll_add(hll, acc, W1);
-    }
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kThreads)
+        hll_add(hll, words_fp(rows + i * W1, W1), W1);
 }
 
 // Lane slot g -> read r = g >> logG, word w = g & (G-1) (G = next_pow2(wpr)); lanes w >= wpr idle.
@@ -1102,22 +1175,26 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
 }
 
 int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
-                           const uint32_t* d_posof, const uint64_t* d_binstart, const uint64_t* h_woff, uint32_t bin0,
-                           uint32_t w1max, uint64_t* d_out, uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
+                           const uint32_t* d_posof, const uint64_t* d_binstart, const uint64_t* h_woff,
+                           const uint64_t* h_fpoff, uint32_t bin0, uint32_t w1max, uint64_t* d_out, uint64_t* d_fps,
+                           uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
     if (n == 0) return SS_OK;
-    if (w1max > 16) return ss_fail(SS_EARG, "k_encode_classes: classes of up to 15 words");
+    if (w1max < 3 || w1max > 16) return ss_fail(SS_EARG, "k_encode_classes: classes of 2 to 15 words");
     ClassOut co;
-    for (int W = 0; W < 33; ++W) co.woff[W] = h_woff[W];
+    for (int W = 0; W < 33; ++W) {
+        co.woff[W] = h_woff[W];
+        co.fpoff[W] = h_fpoff ? h_fpoff[W] : 0;
+    }
     co.bin0 = bin0;
     const uint64_t blocks = (n + kClsTile - 1) / kClsTile;
     if (blocks > 0x7FFFFFFFull) return ss_fail(SS_EARG, "chunk too large for k_encode_classes");
-    hipStream_t s = (hipStream_t)stream;
-    if (w1max <= 8)
-        hipLaunchKernelGGL((k_encode_classes<8>), dim3((unsigned)blocks), dim3(kClsTile), 0, s, d_buf, d_offs, d_lens, n,
-                           d_posof, d_binstart, co, d_out, d_hll, (unsigned long long*)d_first_bad);
-    else
-        hipLaunchKernelGGL((k_encode_classes<16>), dim3((unsigned)blocks), dim3(kClsTile), 0, s, d_buf, d_offs, d_lens, n,
-                           d_posof, d_binstart, co, d_out, d_hll, (unsigned long long*)d_first_bad);
+    const size_t lds = (size_t)kClsTile * w1max * 10 + (size_t)kClsTile * (2 * w1max - 1) * 9;
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_encode_classes,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)((size_t)kClsTile * 16 * 10 + (size_t)kClsTile * 31 * 9));
+    if (attr != hipSuccess) return ss_check(attr, "k_encode_classes LDS attribute");
+    hipLaunchKernelGGL(k_encode_classes, dim3((unsigned)blocks), dim3(kClsTile), lds, (hipStream_t)stream, d_buf, d_offs,
+                       d_lens, n, d_posof, d_binstart, co, w1max, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_classes");
 }
 

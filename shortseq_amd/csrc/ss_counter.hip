@@ -1908,12 +1908,6 @@ __global__ __launch_bounds__(kPackT) void k_region_pack(Tbl t, uint32_t R, uint3
 // read index), so a thread that meets a claimed slot can compare words immediately (no waiting on
 // another lane's second store); the global slice stores the full fingerprint plus the key words.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t words_fp(const uint64_t* w, uint32_t W) {
-    uint64_t h = 0x243F6A8885A308D3ull ^ W;
-    for (uint32_t j = 0; j < W; ++j) h = splitmix64(h ^ w[j]);
-    return h == kEmpty ? ~1ull : h;   // EMPTY marks free slots
-}
-
 __device__ __forceinline__ bool words_eq(const uint64_t* a, const uint64_t* b, uint32_t W) {
     bool eq = true;
     for (uint32_t j = 0; j < W; ++j) eq &= a[j] == b[j];
@@ -1994,6 +1988,32 @@ __global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, con
         uint64_t fp;
         if constexpr (W1C > 0) fp = row_fp<W1C, EVEN>(words + r * W1C);
         else fp = words_fp(words + r * t.W, t.W);
+        w.keys[r] = fp;
+        atomicAdd(&my[bin_of<true>(t, w, fp)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < bins; i += T) {
+        uint32_t sum = 0;
+        for (uint32_t c = 0; c < copies; ++c) sum += hist[c * bins + i];
+        w.hist[(uint64_t)blockIdx.x * bins + i] = sum;
+    }
+}
+
+// The same histogram from fingerprints computed upstream (ss_counter_insert_words_fp): 8 B per row
+// read instead of the row, no hashing.
+template <int T>
+__global__ __launch_bounds__(T) void k_mw_hist(Tbl t, PartWs w, uint32_t bins, const uint64_t* __restrict__ fps,
+                                               uint64_t n) {
+    extern __shared__ uint32_t hist[];
+    constexpr uint32_t kWaves = T / 64;
+    const uint32_t copies = bins * kWaves <= kMaxRegions ? kWaves : 1u;
+    uint32_t* my = hist + (copies > 1 ? (threadIdx.x >> 6) * bins : 0u);
+    for (uint32_t i = threadIdx.x; i < bins * copies; i += T) hist[i] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
+    for (uint64_t r = lo + threadIdx.x; r < hi; r += T) {
+        const uint64_t fp = fps[r];
         w.keys[r] = fp;
         atomicAdd(&my[bin_of<true>(t, w, fp)], 1u);
     }
@@ -2497,7 +2517,8 @@ int ss_counter_release(ss_counter* c) {
 // words_in: pre-packed multi-word rows (ss_counter_insert_words; d_ascii / L / stride / d_first_bad
 // unused), else ASCII reads of length L
 static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
-                       uint64_t base_index, uint64_t* d_first_bad, void* stream, const uint64_t* words_in) {
+                       uint64_t base_index, uint64_t* d_first_bad, void* stream, const uint64_t* words_in,
+                       const uint64_t* fps_in = nullptr) {
     hipStream_t s = (hipStream_t)stream;
     int rc = SS_OK;
     const uint32_t rb = c->log2cap - c->slice_log;
@@ -2599,6 +2620,9 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
                                          kMaxRegions * 4);
             for (int f = 0; f < kMwAggFns && ea == hipSuccess; ++f)
                 ea = hipFuncSetAttribute((const void*)kMwAgg[f], hipFuncAttributeMaxDynamicSharedMemorySize, agg_max);
+            if (ea == hipSuccess)
+                ea = hipFuncSetAttribute((const void*)k_mw_hist<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         kMaxRegions * 4);
             return ea;
         }();
         if (attrs != hipSuccess) return ss_check(attrs, "hipFuncSetAttribute (dynamic LDS)");
@@ -2658,7 +2682,10 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
         if (multi) {
             const size_t fp_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             static_assert(TF == kMwFpT, "k_mw_fp instances");
-            hipLaunchKernelGGL(kMwFp[mw_variant(t.W, mw)], dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, mw, n);
+            if (fps_in)
+                hipLaunchKernelGGL((k_mw_hist<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, fps_in, n);
+            else
+                hipLaunchKernelGGL(kMwFp[mw_variant(t.W, mw)], dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, mw, n);
         } else if (packed_keys) {
             const size_t h_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             hipLaunchKernelGGL((k_pc_hist<TF>), dim3(kPartBlocks), dim3(TF), h_lds, s, t, w, bins1, n);
@@ -2735,6 +2762,14 @@ int ss_counter_insert_words(ss_counter* c, const uint64_t* d_words, uint64_t n, 
     if (c->L != kWordKeys) return ss_fail(SS_EARG, "ss_counter_set_words first");
     if (n && !d_words) return ss_fail(SS_EARG, "null buffer");
     return insert_impl(c, nullptr, n, 0, 0, base_index, nullptr, stream, d_words);
+}
+
+int ss_counter_insert_words_fp(ss_counter* c, const uint64_t* d_words, const uint64_t* d_fps, uint64_t n,
+                               uint64_t base_index, void* stream) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (c->L != kWordKeys) return ss_fail(SS_EARG, "ss_counter_set_words first");
+    if (n && (!d_words || !d_fps)) return ss_fail(SS_EARG, "null buffer");
+    return insert_impl(c, nullptr, n, 0, 0, base_index, nullptr, stream, d_words, d_fps);
 }
 
 int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_lens,

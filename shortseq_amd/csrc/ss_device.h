@@ -109,6 +109,15 @@ __device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
 }
 
+// 64-bit fingerprint of a multi-word key (W words, compared whole): the slot key of the multi-word
+// counter tables (ss_counter.hip) and the drop-in engine's class rows (k_encode_classes emits it per
+// row, so the partition passes need not re-read the rows).  ~0 is reserved for free slots.
+__device__ __forceinline__ uint64_t words_fp(const uint64_t* w, uint32_t W) {
+    uint64_t h = 0x243F6A8885A308D3ull ^ W;
+    for (uint32_t j = 0; j < W; ++j) h = splitmix64(h ^ w[j]);
+    return h == ~0ull ? ~1ull : h;
+}
+
 // First-invalid-read report where the read index is only needed on the (rare) bad path:
 // read = slot / div, computed inside the ballot branch.
 __device__ __forceinline__ void report_bad_div(bool bad, uint64_t slot, uint64_t div, unsigned long long* first_bad) {

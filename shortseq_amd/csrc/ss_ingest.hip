@@ -233,6 +233,23 @@ __global__ __launch_bounds__(256) void k_rank(const uint64_t* __restrict__ first
     }
 }
 
+// export: entry e's first read (engine-local) = rowmap[first[e]]
+__global__ __launch_bounds__(256) void k_export_reads(const uint64_t* __restrict__ first, uint64_t m,
+                                                      const uint32_t* __restrict__ rowmap, uint32_t* __restrict__ out) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
+        out[e] = rowmap[first[e]];
+}
+
+// merge: a source group's m entries become rows `rows + e` of the destination group (first index of
+// the merged entry), their row map = the source's local first read + the source shard's base
+__global__ __launch_bounds__(256) void k_merge_rows(uint64_t m, uint64_t rows, uint64_t base,
+                                                    uint64_t* __restrict__ first, uint32_t* __restrict__ rowmap) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
+        first[e] = rows + e;
+        rowmap[rows + e] = (uint32_t)(base + rowmap[rows + e]);
+    }
+}
+
 // ---- stable compaction / exclusive scan over n items in 1024 contiguous block ranges -------------
 constexpr uint32_t kScanBlocks = 1024;
 
@@ -436,9 +453,10 @@ struct Group {
     uint64_t cap = 0;
     uint64_t rows = 0;            // rows inserted (= the table's first index space)
     DBuf<uint32_t> rowmap;        // row -> global read index
-    // finish(): the extracted entries
+    // finish() / ss_ingest_export(): the extracted entries
     DBuf<uint64_t> fps, words, counts, first;
     DBuf<uint32_t> lens;
+    DBuf<uint32_t> xread;         // export: each entry's first read (engine-local index)
     uint64_t m = 0;
 };
 
@@ -463,6 +481,7 @@ struct ss_ingest {
     uint64_t* h_split = nullptr;   // pinned [3 * kLenBins]
     DBuf<uint8_t> rows;            // gathered dense rows (lengths <= 32)
     DBuf<uint64_t> cls_words;      // the length classes' packed rows (k_encode_classes / k_encode_class)
+    DBuf<uint64_t> cls_fps;        // their fingerprints (k_encode_classes), class after class
     DBuf<uint32_t> posof;          // per read: its place in d_order (k_len_scatter)
     DBuf<uint32_t> hll;            // per class W: 2^kHllLog HyperLogLog registers over the call
     uint32_t* h_hll = nullptr;     // pinned copy
@@ -482,6 +501,10 @@ struct ss_ingest {
     int bad_kind = 0;
     std::string bad_bytes;
     double est_scale = 1.0;        // FASTQ: file bytes / bytes seen (multi-word table sizing)
+    bool exported = false;         // ss_ingest_export ran (the groups' m / buffers hold the entries)
+    // ss_ingest_merge scratch (this engine as the destination): a source group's entries on this device
+    DBuf<uint64_t> mg_words, mg_counts, mg_first;
+    DBuf<uint32_t> mg_lens;
     // finish() results
     uint64_t nkeys = 0, nwords = 0;
     DBuf<uint64_t> slot, ordered, woff, scan;
@@ -671,23 +694,27 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     if (nj && (rc = ss_check(hipMemsetAsync(g->ovf.p, 0, (nj + 1) * 8, s), "ingest overflow reset"))) return rc;
     auto live = [&](const Job& jb) { return base + jb.first <= g->bad_index; };   // may still hold the first error
     // ---- the length classes: rows packed (W words + the length) and their distinct keys sketched ----
-    uint64_t woff[33] = {0}, cls_words = 0;
+    uint64_t woff[33] = {0}, fpoff[33] = {0}, cls_words = 0, cls_rows = 0;
     uint32_t w1max = 0, wlo = 33, whi = 0;
     for (const Job& jb : jobs) {
         if (jb.bin <= 32) continue;
         const uint32_t W = jb.bin - kClassBin0;
         woff[W] = cls_words;
+        fpoff[W] = cls_rows;
         cls_words += jb.m * (W + 1);
+        cls_rows += jb.m;
         w1max = std::max(w1max, W + 1);
         wlo = std::min(wlo, W);
         whi = std::max(whi, W);
     }
     uint64_t need_cls[33] = {0};
+    const bool fused = !dense_L && w1max && w1max <= 16;   // fingerprints come with the rows
     if (w1max) {
         if ((rc = g->cls_words.ensure(cls_words))) return rc;
-        if (!dense_L && w1max <= 16) {      // one read-order pass, the registers updated in it
-            rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->posof.p, g->split_out.p + 2 * kLenBins, woff,
-                                        kClassBin0, w1max, g->cls_words.p, g->hll.p, g->first_bad.p + nj, s);
+        if (fused && (rc = g->cls_fps.ensure(cls_rows))) return rc;
+        if (fused) {                        // one read-order pass, the registers updated in it
+            rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->posof.p, g->split_out.p + 2 * kLenBins, woff, fpoff,
+                                        kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + nj, s);
         } else {                            // a class per pass (longer reads, or a dense chunk)
             for (size_t j = 0; j < nj && !rc; ++j) {
                 const Job& jb = jobs[j];
@@ -762,7 +789,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                     used = k;
                 }
             }
-            if (!rc) rc = ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, cs);
+            if (!rc)
+                rc = fused ? ss_counter_insert_words_fp(gr.table, g->cls_words.p + woff[gr.W1 - 1], g->cls_fps.p + fpoff[gr.W1 - 1],
+                                                        jb.m, gr.rows, cs)
+                           : ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, cs);
             if (!rc) rc = ss_counter_overflow(gr.table, g->ovf.p + j, cs);
             if (rc) break;
             const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
@@ -827,6 +857,41 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     }
     // a too-long read's bytes (the message does not quote them) are not needed
     g->nreads += n;
+    return SS_OK;
+}
+
+// Every table of the engine extracted (entries of group q into its fps / words / counts / first /
+// lens buffers, gr.m entries), then their entry counts and overflow words back in one sync.
+int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
+    hipStream_t s = g->stream;
+    int rc = g->scan.ensure(kScanBlocks + 2 + 2 * (uint64_t)kLenBins + 8);
+    if (rc) return rc;
+    uint64_t* d_cnt = g->scan.p + kScanBlocks + 2;
+    for (auto& kv : g->groups) {
+        Group& gr = kv.second;
+        gr.m = 0;
+        if (!gr.table) continue;      // a length of an earlier call
+        const uint32_t W = gr.W1;
+        const uint64_t cap = gr.cap + 1;
+        const uint64_t q = placed.size();
+        if ((rc = gr.fps.ensure(cap)) || (rc = gr.words.ensure(cap * W)) || (rc = gr.counts.ensure(cap)) ||
+            (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)))
+            return rc;
+        rc = ss_counter_extract_words(gr.table, 1, gr.fps.p, gr.lens.p, gr.words.p, gr.counts.p, gr.first.p, cap,
+                                      d_cnt + 2 * q, s);
+        if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 2 * q + 1, s);
+        if (rc) return rc;
+        placed.push_back(&gr);
+    }
+    if (!placed.empty()) {
+        rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 2 * placed.size() * 8, hipMemcpyDeviceToHost, s), "ingest");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest extract");
+        if (rc) return rc;
+    }
+    for (size_t q = 0; q < placed.size(); ++q) {
+        if (g->h_bad[2 * q + 1]) return ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
+        placed[q]->m = g->h_bad[2 * q];
+    }
     return SS_OK;
 }
 
@@ -910,6 +975,7 @@ int ss_ingest_reset(ss_ingest* g) {
     g->est_scale = 1.0;
     g->nkeys = g->nwords = 0;
     g->failed = false;
+    g->exported = false;
     if (!g->hll.p) return SS_OK;
     return ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
 }
@@ -927,7 +993,7 @@ int ss_ingest_destroy(ss_ingest* g) {
     for (auto& kv : g->groups) {
         kv.second.rowmap.release();
         kv.second.fps.release(), kv.second.words.release(), kv.second.counts.release(), kv.second.first.release();
-        kv.second.lens.release();
+        kv.second.lens.release(), kv.second.xread.release();
     }
     g->groups.clear();
     for (auto& p : g->pool) ss_counter_destroy(p.second);
@@ -939,7 +1005,8 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->fq_ws.release(), g->fq_aux.release(), g->fq_counts.release();
     g->slot.release(), g->ordered.release(), g->woff.release(), g->scan.release(), g->out_len.release();
     g->out_cnt.release(), g->out_words.release(), g->gdesc.release();
-    g->cls_words.release(), g->posof.release(), g->hll.release(), g->ovf.release();
+    g->cls_words.release(), g->cls_fps.release(), g->posof.release(), g->hll.release(), g->ovf.release();
+    g->mg_words.release(), g->mg_counts.release(), g->mg_first.release(), g->mg_lens.release();
     if (g->h_hll) (void)hipHostFree(g->h_hll);
     if (g->h_split) (void)hipHostFree(g->h_split);
     if (g->h_bad) (void)hipHostFree(g->h_bad);
@@ -1178,33 +1245,9 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     unsigned long long* bits = (unsigned long long*)g->slot.p;
     std::vector<GDesc> desc;
     std::vector<Group*> placed;
-    // every table extracted, then their entry counts and overflow words back in one sync
-    if ((rc = g->scan.ensure(kScanBlocks + 2 + 2 * (uint64_t)kLenBins + 8))) return rc;
-    uint64_t* d_cnt = g->scan.p + kScanBlocks + 2;
-    for (auto& kv : g->groups) {
-        Group& gr = kv.second;
-        if (!gr.table) continue;      // a length of an earlier call
-        const uint32_t W = gr.W1;
-        const uint64_t cap = gr.cap + 1;
-        const uint64_t q = placed.size();
-        if ((rc = gr.fps.ensure(cap)) || (rc = gr.words.ensure(cap * W)) || (rc = gr.counts.ensure(cap)) ||
-            (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)))
-            return rc;
-        rc = ss_counter_extract_words(gr.table, 1, gr.fps.p, gr.lens.p, gr.words.p, gr.counts.p, gr.first.p, cap,
-                                      d_cnt + 2 * q, s);
-        if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 2 * q + 1, s);
-        if (rc) return rc;
-        placed.push_back(&gr);
-    }
-    if (!placed.empty()) {
-        rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 2 * placed.size() * 8, hipMemcpyDeviceToHost, s), "ingest");
-        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest extract");
-        if (rc) return rc;
-    }
+    if ((rc = extract_groups(g, placed))) return rc;
     for (size_t q = 0; q < placed.size(); ++q) {
         Group& gr = *placed[q];
-        if (g->h_bad[2 * q + 1]) return ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
-        gr.m = g->h_bad[2 * q];
         hipLaunchKernelGGL(k_mark, dim3(grid_of(gr.m + 1, 256)), dim3(256), 0, s, gr.first.p, gr.m, gr.rowmap.p,
                            kNoSlot, bits);
         desc.push_back({gr.words.p, gr.counts.p, gr.W1, gr.L});
@@ -1264,6 +1307,91 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     *h_nkeys = K;
     *h_nwords = NW;
     return SS_OK;
+}
+
+int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys) {
+    if (!g) return ss_fail(SS_EARG, "null ingest");
+    if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
+    (void)hipSetDevice(g->device);
+    std::vector<Group*> placed;
+    int rc = extract_groups(g, placed);
+    if (rc) return rc;
+    uint64_t keys = 0;
+    for (Group* gr : placed) {
+        if (!gr->m) continue;
+        if ((rc = gr->xread.ensure(gr->m))) return rc;
+        hipLaunchKernelGGL(k_export_reads, dim3(grid_of(gr->m, 256)), dim3(256), 0, g->stream, gr->first.p, gr->m,
+                           gr->rowmap.p, gr->xread.p);
+        keys += gr->m;
+    }
+    rc = ss_check(hipStreamSynchronize(g->stream), "ingest export");
+    if (rc) return rc;
+    g->exported = true;
+    if (h_nkeys) *h_nkeys = keys + (g->empty_count ? 1 : 0);
+    return SS_OK;
+}
+
+int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
+    if (!dst || !src || dst == src) return ss_fail(SS_EARG, "ingest merge: two distinct engines");
+    if (!src->exported) return ss_fail(SS_EARG, "ingest merge: ss_ingest_export the source first");
+    if (dst->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
+    if (src_base < dst->nreads) return ss_fail(SS_EARG, "ingest merge: sources follow the destination's reads, in order");
+    if (src_base + src->nreads > 0xFFFFFFFEull)
+        return ss_fail(SS_EARG, "ingest: one call counts fewer than 2^32 - 1 reads");
+    int rc = ss_check(hipSetDevice(dst->device), "ingest merge device");
+    if (rc) return rc;
+    const bool peer = src->device != dst->device;
+    if (peer) {
+        int can = 0;
+        (void)hipDeviceCanAccessPeer(&can, dst->device, src->device);
+        if (can) {
+            const hipError_t e = hipDeviceEnablePeerAccess(src->device, 0);
+            if (e != hipSuccess) (void)hipGetLastError();     // already enabled, or unsupported: copies stage
+        }
+    }
+    hipStream_t s = dst->stream;
+    auto copy = [&](void* d, const void* p, uint64_t bytes) -> int {
+        if (!bytes) return SS_OK;
+        return ss_check(peer ? hipMemcpyPeerAsync(d, dst->device, p, src->device, bytes, s)
+                             : hipMemcpyAsync(d, p, bytes, hipMemcpyDeviceToDevice, s),
+                        "ingest merge copy");
+    };
+    const double scale = dst->est_scale;
+    dst->est_scale = 1.0;            // a new group is sized by the entries it receives
+    for (auto& kv : src->groups) {
+        const Group& sg = kv.second;
+        if (!sg.table || !sg.m) continue;
+        const uint64_t m = sg.m;
+        const uint32_t bin = kv.first;
+        Group& gr = dst->groups[bin];
+        gr.L = sg.L;
+        gr.W1 = sg.W1;
+        if ((rc = group_room(dst, gr, m, gr.rows + m))) break;
+        if ((rc = gr.rowmap.ensure_keep(gr.rows + m, gr.rows, s))) break;
+        if ((rc = dst->mg_words.ensure(m * gr.W1)) || (rc = dst->mg_counts.ensure(m)) || (rc = dst->mg_first.ensure(m)) ||
+            (rc = dst->mg_lens.ensure(m)))
+            break;
+        // the source's entries cross to this device (xGMI peer copies; a plain copy on one device)
+        if ((rc = copy(dst->mg_words.p, sg.words.p, m * gr.W1 * 8)) || (rc = copy(dst->mg_counts.p, sg.counts.p, m * 8)) ||
+            (rc = copy(dst->mg_lens.p, sg.lens.p, m * 4)) || (rc = copy(gr.rowmap.p + gr.rows, sg.xread.p, m * 4)))
+            break;
+        hipLaunchKernelGGL(k_merge_rows, dim3(grid_of(m, 256)), dim3(256), 0, s, m, gr.rows, src_base,
+                           dst->mg_first.p, gr.rowmap.p);
+        // appended as one block after every earlier row: a key already here keeps its (smaller) first
+        // row, a key also in a later source gets that source's larger rows -> min = first occurrence
+        rc = gr.W1 == 1 ? ss_counter_merge(gr.table, dst->mg_words.p, dst->mg_lens.p, dst->mg_counts.p, dst->mg_first.p, m, s)
+                        : ss_counter_merge_words(gr.table, dst->mg_words.p, dst->mg_counts.p, dst->mg_first.p, m, s);
+        if (rc) break;
+        gr.rows += m;
+    }
+    dst->est_scale = scale;
+    if (rc) return rc;
+    if (src->empty_count) {
+        dst->empty_count += src->empty_count;
+        dst->empty_first = std::min(dst->empty_first, src_base + src->empty_first);
+    }
+    dst->nreads = std::max(dst->nreads, src_base + src->nreads);
+    return ss_check(hipStreamSynchronize(s), "ingest merge");    // the source may be reset after return
 }
 
 int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words) {

@@ -13,13 +13,18 @@ extern "C" int ss_encode_fixed_impl(const uint8_t* d_ascii, uint64_t n, uint32_t
                                     const uint64_t* d_ref_words, uint32_t* d_out, void* stream);
 // All multi-word classes of a chunk in one read-order pass (k_encode_classes; every class present has
 // W + 1 <= w1max <= 16 words): class W's rows at d_out + h_woff[W] (W = 2..32; row = d_posof[r] -
-// d_binstart[bin0 + W]), and the classes' HyperLogLog registers d_hll[W << kHllLog ...] (u32,
-// max-updated; zeroed by the caller).
+// d_binstart[bin0 + W]), each row's fingerprint (words_fp over its W + 1 words) at
+// d_fps[h_fpoff[W] + row] when d_fps is given, and the classes' HyperLogLog registers
+// d_hll[W << kHllLog ...] (u32, max-updated; zeroed by the caller).
 constexpr uint32_t kHllLog = 11;
 extern "C" int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
                                       const uint32_t* d_posof, const uint64_t* d_binstart, const uint64_t* h_woff,
-                                      uint32_t bin0, uint32_t w1max, uint64_t* d_out, uint32_t* d_hll,
-                                      uint64_t* d_first_bad, void* stream);
+                                      const uint64_t* h_fpoff, uint32_t bin0, uint32_t w1max, uint64_t* d_out,
+                                      uint64_t* d_fps, uint32_t* d_hll, uint64_t* d_first_bad, void* stream);
+// ss_counter_insert_words with the rows' fingerprints already computed (d_fps[n], words_fp of each row,
+// e.g. by k_encode_classes): the partition passes read the 8-B fingerprints instead of hashing rows.
+extern "C" int ss_counter_insert_words_fp(struct ss_counter* c, const uint64_t* d_words, const uint64_t* d_fps,
+                                          uint64_t n, uint64_t base_index, void* stream);
 // HyperLogLog registers (2^kHllLog u32 at d_hll) of m packed rows of W1 words, k_encode_classes' hash.
 extern "C" int ss_hll_rows_impl(const uint64_t* d_rows, uint64_t m, uint32_t W1, uint32_t* d_hll, void* stream);
 // Drop-in engine (ss_ingest), one multi-word length class: rows of W words + the length (k_encode_class).

@@ -226,3 +226,63 @@ def test_engines_thread_safe(gpu):
     for t in ts:
         t.join()
     assert got == want
+
+
+def _rows_of(counter):
+    """A ShortSeqCounter's dict as the ss_ingest_results layout (lens, counts, words)."""
+    import numpy as np
+    lens, cnts, words = [], [], []
+    for k, v in counter.items():
+        lens.append(len(k))
+        cnts.append(v)
+        words.extend(int(w) for w in k.packed[:max(0, (len(k) + 31) // 32)])
+    return np.array(lens, np.uint32), np.array(cnts, np.uint64), np.array(words, np.uint64)
+
+
+@pytest.mark.parametrize("ndev", [2, 8])
+def test_multi_engine_ragged_device_reduce(gpu, oracle, ndev):
+    """a mixed 1-300-nt list through `ndev` engines reduces on the device
+    (ss_ingest_export + ss_ingest_merge into the first shard's engine: single-word length tables and
+    multi-word length classes alike) and the dict equals the generator-derived rows (pinned to
+    oracle.count): keys, counts and first-occurrence order across every shard boundary."""
+    import numpy as np
+    seed, ps, U, n, lo, hi = 43, 44, 1 << 12, 60_000, 1, 300
+    reads = oracle.ragged_pool_reads(seed, ps, U, 0, n, lo, hi)
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    gl, gc, gw = _rows_of(ShortSeqCounter(reads, device=[0] * ndev))
+    assert gl.tolist() == el.tolist()
+    assert gc.tolist() == ec.tolist()
+    assert np.array_equal(gw, ew)
+
+
+def test_device_ingest_export_merge(gpu, oracle):
+    """The reduce at the C ABI: three DeviceIngest engines count consecutive slices of one ragged
+    device batch (33-700 nt: class tables of several widths, plus 0-32 nt single-word tables in the
+    second case), export, and fold into the first (ss_ingest_merge with each slice's global base);
+    the first engine's rows equal the whole batch's generator-derived rows.  Merging out of order or
+    an engine that was not exported is refused."""
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import NativeError
+    for seed, ps, U, n, lo, hi in ((47, 48, 3000, 150_000, 33, 700), (45, 46, 5000, 120_000, 0, 90)):
+        blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+        cuts = [0, n // 5, n // 2, n]
+        engs = [B.DeviceIngest(gpu) for _ in range(3)]
+        try:
+            for k, e in enumerate(engs):
+                e.count(blob, offs[cuts[k]:cuts[k + 1]], lens[cuts[k]:cuts[k + 1]])
+            with pytest.raises(NativeError, match="export"):
+                engs[0].merge(engs[1], cuts[1])
+            for e in engs[1:]:
+                assert e.export() > 0
+            with pytest.raises(NativeError, match="in order"):
+                engs[0].merge(engs[2], 5)
+            engs[0].merge(engs[1], cuts[1])
+            engs[0].merge(engs[2], cuts[2])
+            gl, gc, gw = engs[0].results()
+        finally:
+            for e in engs:
+                e.close()
+        el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+        assert gl.tolist() == el.tolist()
+        assert gc.tolist() == ec.tolist()
+        assert (gw == ew).all()
