@@ -90,7 +90,7 @@ class Timer:
         return float(np.mean([s.elapsed_time(e) for s, e in self.pairs]))
 
 
-def timed_loop(step, steps, warmup, world):
+def timed_loop(step, steps, warmup, world, on_timed_start=None):
     """W untimed steps, then K steps between barrier + synchronize; returns max-over-ranks seconds
     and a Timer.  The Timer's `region` pair brackets all K steps on the launch stream, so
     region_ms / K is the per-step device time with the launch queue kept full (no host launch
@@ -117,6 +117,8 @@ def timed_loop(step, steps, warmup, world):
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    if on_timed_start is not None:
+        on_timed_start()      # e.g. drop the warmup steps' per-pass timings
     timer = Timer()
     r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -314,7 +316,11 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
     def step(timer):
         sc.count(ascii, L, base_index=i0, check_errors=False)
 
-    el, tr = timed_loop(step, steps, warmup, world)
+    # per-pass HIP events inside the insert (ss_counter_set_timing), folded over the timed steps only
+    sc.local.set_timing(True)
+    el, tr = timed_loop(step, steps, warmup, world, on_timed_start=lambda: sc.local.pass_times())
+    passes = sc.local.pass_times()
+    sc.local.set_timing(False)
     del ascii
     # parity after timing: the whole job's table gathered to rank 0 (all owners' regions), its
     # (key, count, first) rows sorted by key hashed and compared with the generator-derived digest of
@@ -335,7 +341,53 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
             if (uniq, table_digest(keys, counts, first)) != (want["unique"], want["digest"]):
                 raise SystemExit(f"PARITY FAILURE: counter table != {name}")
             check = f"digest {name}"
-    return el, tr.region_ms / steps, uniq, check
+    return el, tr.region_ms / steps, uniq, check, passes
+
+
+def bench_exchange(B, dev, n=125_000_000, U=1 << 24, owners=8, reps=5):
+    """The C5 exchange's device cost, rehearsed on one GPU: one rank's 125M-read
+    table (pool 2^24) packs the other 7 owners' regions into 16-B records (ss_counter_pack_ranges:
+    k_region_scan + k_region_pack), and folds 7 received runs into its own regions
+    (ss_counter_merge_packed: k_run_bounds + k_merge_runs) -- the runs are its own part-0 records
+    replicated 7 times, the size a peer's shard of the same pool sends.  The xGMI transfer between
+    them (RCCL all_to_all_single) is not on one GPU.  Roofline over each step's algorithmic bytes:
+    pack = the other owners' slots read (16 B each) + the records written; merge = the records read +
+    the owned slices read and written once."""
+    ascii = B.synth_pool_reads(n, 32, 5, 77, U, device=dev)
+    cap = 1 << int(np.ceil(np.log2(2 * U)))
+    gc = B.GpuCounter(cap, device=dev)
+    gc.reserve(n)
+    gc.insert(ascii, 32, check_errors=False)
+    del ascii
+    rec_all, parts_all = gc.pack_ranges(owners, skip=-1)
+    m0 = int(parts_all[0].item())
+    recv = rec_all[:m0].repeat(owners - 1, 1)
+    runs = [(k * m0, (k + 1) * m0, 0) for k in range(owners - 1)]
+    del rec_all
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    pk, mg = [], []
+    for r in range(reps + 1):
+        ev[0].record()
+        rec, parts = gc.pack_ranges(owners, skip=0)
+        ev[1].record()
+        gc.merge_packed(recv, runs, 0, owners, 32)
+        ev[2].record()
+        torch.cuda.synchronize()
+        if r:     # the first round warms up
+            pk.append(ev[0].elapsed_time(ev[1]))
+            mg.append(ev[1].elapsed_time(ev[2]))
+    sent = int(parts.sum().item())
+    gc.close()
+    pack_ms, merge_ms = float(np.median(pk)), float(np.median(mg))
+    pack_b = cap * (owners - 1) // owners * 16 + sent * 16
+    merge_b = recv.shape[0] * 16 + cap // owners * 16 * 2
+    return {"owners": owners, "reads_per_owner": n, "pool": U, "records_sent": sent, "records_received": recv.shape[0],
+            "pack_ms": pack_ms, "merge_ms": merge_ms,
+            "roofline": {"bound": "hbm", "kernel": "k_region_scan + k_region_pack | k_run_bounds + k_merge_runs",
+                         "pack_frac": pack_b / (pack_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "merge_frac": merge_b / (merge_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "pack_bytes": pack_b, "merge_bytes": merge_b, "peak": HBM_PEAK_GBS, "unit": "GB/s"},
+            "xgmi": "not measured (one GPU): RCCL all_to_all_single of records_sent x 16 B per rank"}
 
 
 def bench_fastq_index(B, lib, dev, n_rec=8 << 20, L=100, reps=10):
@@ -735,23 +787,24 @@ def main():
             n5, U5 = 125_000_000, 1 << 24
             log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
             s5 = max(3, args.steps // 4)
-            el5, d5, uniq, chk5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
-            # per-read bytes of the partitioned pipeline: coarse pass 32 in + 12 out (key,
-            # read index), fine scatter 12 + 12 (into per-sub-bin slabs: no count pass), aggregate 12 +
-            # the whole table written once (fresh slices: 16 B x 2^25 slots, amortised over the reads);
-            # the floor of the problem is the 32 B of ASCII per read
+            el5, d5, uniq, chk5, pass5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
+            # SURVEY §8(d) prices C5 at the 32 B of ASCII per read (the problem's floor): that is the
+            # headline frac.  Beside it, the partitioned pipeline's own pass bytes: coarse
+            # pass 32 in + 12 out (key, read index), fine scatter 12 + 12, aggregate 12 + the whole
+            # table written once (fresh slices: 16 B x 2^25 slots, amortised over the reads)
             table_b = 16 * (2 * U5) / n5
             pipe_b = 32 + 12 + 24 + 12 + table_b
             extra["C5_counter_32"] = {
                 "reads_per_s": n5 * world / (el5 / s5), "ms_per_step": el5 / s5 * 1e3, "device_ms_per_step": d5,
-                "reads_per_gpu": n5, "pool": U5, "unique": uniq, "parity": chk5,
+                "reads_per_gpu": n5, "pool": U5, "unique": uniq, "parity": chk5, "passes_ms": pass5,
                 "roofline": {"bound": "hbm", "kernel": "partitioned insert (k_pf_coarse, k_pf_scatter, "
                                                         "k_pc_aggregate_slice)",
-                             "achieved": n5 * pipe_b / (d5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": n5 * pipe_b / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_read": pipe_b,
-                             "floor_frac": n5 * 32 / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "achieved": n5 * 32 / (d5 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": n5 * 32 / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_read": 32,
+                             "frac_pipeline": n5 * pipe_b / (d5 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "pipeline_bytes_per_read": pipe_b,
                              "traffic": load_traffic("counter32_insert", n5),
-                             "note": "frac: the pipeline's own pass bytes; floor_frac: 32 B of ASCII per read"},
+                             "note": "frac: 32 B of ASCII per read (SURVEY 8d); frac_pipeline: the passes' own bytes"},
                 "merge": (f"all_to_all_single of 16-B (key, count, first) records by owner over {dist.get_backend()}"
                           f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
                          if world > 1 else "none (1 GPU)"}
@@ -759,19 +812,19 @@ def main():
             for name, U_, zs in (("C5_counter_32_U20", 1 << 20, None), ("C5_counter_32_zipf1.1_U24", 1 << 24, 1.1),
                                  ("C5_counter_32_zipf1.1_U20", 1 << 20, 1.1)):
                 log(f"C5 counter {n5} x 32 per GPU, pool {U_}, {'zipf ' + str(zs) if zs else 'uniform'}")
-                el_, d_, u_, chk_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
+                el_, d_, u_, chk_, pass_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
                 # the same pipeline bytes model with this pool's table (a skewed batch moves fewer records
                 # through the fine passes after deduplication: the model is then an upper bound)
                 pb_ = 32 + 12 + 24 + 12 + 16 * (2 * U_) / n5
                 extra[name] = {"reads_per_s": n5 * world / (el_ / s5), "ms_per_step": el_ / s5 * 1e3,
                                "device_ms_per_step": d_, "reads_per_gpu": n5, "pool": U_, "zipf_s": zs, "unique": u_,
-                               "parity": chk_,
+                               "parity": chk_, "passes_ms": pass_,
                                "vs_uniform_U24": d_ / d5,
                                "roofline": {"bound": "hbm", "kernel": "partitioned insert",
-                                            "achieved": n5 * pb_ / (d_ * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                                            "unit": "GB/s", "frac": n5 * pb_ / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                            "bytes_per_read": pb_,
-                                            "floor_frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                            "achieved": n5 * 32 / (d_ * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                            "unit": "GB/s", "frac": n5 * 32 / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                            "bytes_per_read": 32,
+                                            "frac_pipeline": n5 * pb_ / (d_ * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                             "traffic": load_traffic("counter32_insert_" + name[len("C5_counter_32_"):], n5)}}
 
         # C5 (and at world > 1 its RCCL exchange): an exception every rank raises alike (e.g. a backend
@@ -792,6 +845,9 @@ def main():
                     log(f"{name}: {type(e).__name__}: {e}")
                     extra[name] = {"error": f"{type(e).__name__}: {e}"}
 
+            if world == 1:
+                log("C5 exchange rehearsal (8 owners, one GPU)")
+                local_extra("C5_exchange_8owners", lambda: bench_exchange(B, dev))
             log("F1 FASTQ index / F4 all-pairs")
             local_extra("F1_fastq_index_100nt", lambda: bench_fastq_index(B, lib, dev))
             local_extra("F4_all_pairs_umi12", lambda: bench_all_pairs(B, lib, dev))

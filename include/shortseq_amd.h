@@ -216,6 +216,16 @@ int ss_counter_insert_words(ss_counter* c, const uint64_t* d_words, uint64_t n, 
  * bits, bit 3 = a read index did not fit 32 bits.  Nonzero means the result is invalid. */
 int ss_counter_overflow(ss_counter* c, uint64_t* d_flag, void* stream);
 
+/* Per-pass timing of the optimistic partitioned insert (tracing: bench.py's C5 lines attribute the
+ * insert's time to its passes).  With on != 0 every such insert records HIP events on its stream
+ * between its passes (a ring of 64 inserts, folded as it wraps); ss_counter_pass_times returns the
+ * mean ms per insert since the last call of: [0] coarse partition (k_prep + k_pf_coarse), [1] sub-bin
+ * order (k_pf_order), [2] fine scatter (k_pf_scatter), [3] aggregate (k_pc_aggregate_slice), [4]
+ * spill insert (k_spill_insert), and *h_inserts; then resets the sums.  Host calls.  New in this
+ * ABI version; replaces no reference interface. */
+int ss_counter_set_timing(ss_counter* c, int on);
+int ss_counter_pass_times(ss_counter* c, double* h_ms, uint64_t* h_inserts);
+
 /* Number of occupied slots -> *d_size (device u64). */
 int ss_counter_size(ss_counter* c, uint64_t* d_size, void* stream);
 
@@ -354,6 +364,11 @@ int ss_ingest_create(int device, ss_ingest** h_out);
 int ss_ingest_destroy(ss_ingest* g);
 int ss_ingest_reset(ss_ingest* g);
 int ss_ingest_set_exact(ss_ingest* g, int exact);
+/* Global read indices of one engine are u64 (a call counts any number of reads); a length's or class's
+ * table indexes its rows with a u32 first index, so a group about to pass 2^32 - 1 rows is re-keyed
+ * (its distinct keys become its first rows).  Test hook: lower that bound to `rows` (>= 1024) so the
+ * re-keying runs at small sizes.  New in this ABI version. */
+int ss_ingest_set_row_limit(ss_ingest* g, uint64_t rows);
 int ss_ingest_staging(ss_ingest* g, uint64_t nbytes, uint8_t** h_ptr);
 int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_lens, uint64_t n);
 int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, uint64_t* h_nseqs);

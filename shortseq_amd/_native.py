@@ -60,6 +60,8 @@ SIGNATURES = [
     ("ss_counter_insert_words", C.c_int, [_P, _P, _U64, _U64, _P]),
     ("ss_counter_overflow", C.c_int, [_P, _P, _P]),
     ("ss_counter_size", C.c_int, [_P, _P, _P]),
+    ("ss_counter_set_timing", C.c_int, [_P, C.c_int]),
+    ("ss_counter_pass_times", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     ("ss_counter_extract", C.c_int, [_P, _U32, _P, _P, _P, _P, _U64, _P, _P]),
     ("ss_counter_words", C.c_int, [_P]),
     ("ss_counter_extract_words", C.c_int, [_P, _U32, _P, _P, _P, _P, _P, _U64, _P, _P]),
@@ -86,6 +88,7 @@ SIGNATURES = [
     ("ss_ingest_destroy", C.c_int, [_P]),
     ("ss_ingest_reset", C.c_int, [_P]),
     ("ss_ingest_set_exact", C.c_int, [_P, C.c_int]),
+    ("ss_ingest_set_row_limit", C.c_int, [_P, _U64]),
     ("ss_ingest_staging", C.c_int, [_P, _U64, C.POINTER(C.c_void_p)]),
     ("ss_ingest_add_blob", C.c_int, [_P, _P, _P, _U64]),
     ("ss_ingest_add_fastq", C.c_int, [_P, C.c_char_p, _U64, C.POINTER(C.c_uint64)]),

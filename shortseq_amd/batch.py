@@ -504,6 +504,10 @@ class DeviceIngest:
             lens, cnts, wds = lens.copy(), cnts.copy(), wds.copy()
         return lens, cnts, wds
 
+    def set_row_limit(self, rows: int) -> None:
+        """Test hook: re-key a length's table once its rows pass `rows` (default 2^32 - 1)."""
+        check(lib().ss_ingest_set_row_limit(self._h, int(rows)), "ss_ingest_set_row_limit")
+
     def export(self) -> int:
         """Extract this engine's tables for a device-side reduce (ss_ingest_export); its distinct keys."""
         k = C.c_uint64()
@@ -695,6 +699,19 @@ class GpuCounter:
     def words(self) -> int:
         """Words per key (1 for L <= 32); fixed by the first insert."""
         return int(lib().ss_counter_words(self._h))
+
+    PASSES = ("coarse", "order", "scatter", "aggregate", "spill")
+
+    def set_timing(self, on: bool = True) -> None:
+        """Record HIP events between the partitioned insert's passes (ss_counter_set_timing)."""
+        check(lib().ss_counter_set_timing(self._h, int(bool(on))), "ss_counter_set_timing")
+
+    def pass_times(self) -> dict:
+        """Mean ms per insert of each pass since the last call ({} when none was timed)."""
+        ms = (C.c_double * 5)()
+        k = C.c_uint64()
+        check(lib().ss_counter_pass_times(self._h, ms, C.byref(k)), "ss_counter_pass_times")
+        return dict(zip(self.PASSES, list(ms))) if k.value else {}
 
     def reset(self) -> None:
         check(lib().ss_counter_reset(self._h, _stream(self.device)), "ss_counter_reset")

@@ -357,29 +357,31 @@ __global__ __launch_bounds__(kThreads) void k_encode_class(const uint8_t* in, co
 // block takes kClsTile consecutive reads.  Within the tile the reads of class W hold consecutive rows
 // of W's block (k_len_scatter is stable), so the tile's rows of a class are one contiguous span:
 //   a. per read: class W = ceil(L/32) (L 33..1024), its row (posof[r] - binstart[bin0 + W]); per
-//      class the tile's first row and count (LDS atomics); one scan gives each read its word slots
-//      (W + 1) and its 16-B chunk slots (the aligned chunks holding its bytes)
-//   b. lane per chunk slot: every chunk a read touches is loaded once (coalesced dwordx4) and
-//      encoded where it lies (encode16 without the alias carry) into 16 codes + a mask of its
-//      rejected bytes + a mask of its bit-6-clear bytes, kept in LDS.  A read starting at byte
-//      sh = off % 16 has word w at code sh of its chunk 2w, so
-//   c. lane per word slot: the word is a funnel shift of three LDS code words by 2 sh bits (tail
-//      codes past the read masked to 'A' = 0), its rejected bytes the same window of the masks; a
-//      partial tail word holding a bit-6-clear byte (the table path's alias carry) is
-//      re-encoded exactly from the blob (encode_word_q).  w == W is the length.  Into the tile's
-//      LDS class spans, the class beside it (a byte)
-//   d. the spans out with dense stores (a per-class run of whole rows); each read's row fingerprint
+//      class the tile's first row and count (LDS atomics); a scan of W + 1 over the reads
+//   b. lane per word slot in read order (k_encode_var_dense's access pattern: consecutive lanes,
+//      consecutive words of consecutive reads).  A read starting at byte sh = off % 16 has word w at
+//      byte sh of its 16-B-aligned chunk 2w, so each of the three aligned chunks holding the word is
+//      encoded where it lies (encode16 without the alias carry: 16 codes) and the word is a funnel
+//      shift of the three code words by 2 sh bits, tail codes past the read masked to 'A' = 0 --
+//      no byte realignment (encode_word_q's selects and v_alignbyte: ~210 VALU per word, which
+//      left the former form VALU-bound at 2.1 ms on the f2 batch).  Rejected bytes: a chunk with
+//      any gives its byte mask, windowed the same way (FASTQ neighbours are newlines and quality
+//      bytes: only a read's first and last chunks); a partial tail word holding a bit-6-clear byte
+//      (the table path's alias carry) is re-encoded exactly (encode_word_q).  w == W is
+//      the length.  Into the tile's LDS class spans, the class beside it (a byte)
+//   c. the spans out with dense stores (a per-class run of whole rows); each read's row fingerprint
 //      (words_fp over its LDS row, the class table's slot key) to fps[fpoff[W] + row] when fps is
 //      given, and into class W's HyperLogLog registers (2^kHllLog per class, max of the rank), which
 //      the engine reads to size each class's table by its distinct keys rather than by its reads.
-// Per 32-nt word this is ~2 chunk encodes + a shift (the per-word realignment of encode_word_q from
-// three unaligned chunk loads cost ~210 VALU per word: the former form was VALU-bound at 2.1 ms on
-// the f2 batch).  Dynamic LDS: words kClsTile * w1max u64 + bytes, chunks kClsTile * (2 w1max - 1).
 // (A lane-per-read-slot form with the rows stored straight from registers measured 3.6 ms against
-// 2.75 for the four per-class passes on the f2 batch: its row stores land 24-48 B at a time.)
+// 2.75 for the four per-class passes on the f2 batch: its row stores land 24-48 B at a time.  The
+// chunks staged once in LDS as codes + masks (each chunk encoded once) measured 3.08 ms: 46 KB of
+// LDS per 256 reads left 3 waves per SIMD for a kernel of three dependent load phases.)
 struct ClassOut {
     uint64_t woff[33];
     uint64_t fpoff[33];
+    uint64_t* rmap[33];     // class W's row map at its first row of this chunk (null: not written)
+    uint64_t base;          // global read index of the chunk's read 0
     uint32_t bin0;
 };
 constexpr uint32_t kClsTile = 256;
@@ -398,6 +400,7 @@ __device__ __forceinline__ uint32_t nz_bytes(uint32_t m) {
 }
 
 // 16 aligned bytes -> x: 16 codes (no alias carry), y: rejected-byte mask | bit-6-clear mask << 16
+// (both 0 on the common path: every byte a base with bit 6 set)
 __device__ __forceinline__ uint2 code_chunk(uint4 c) {
     const uint32_t p0 = c.x & 0x06060606u, p1 = c.y & 0x06060606u, p2 = c.z & 0x06060606u, p3 = c.w & 0x06060606u;
     const uint32_t m0 = (c.x & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p0);
@@ -414,141 +417,136 @@ __device__ __forceinline__ uint2 code_chunk(uint4 c) {
     return r;
 }
 
-constexpr uint32_t kClsLoads = 4;     // chunk loads a lane issues before encoding any
-
 __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, const uint64_t* __restrict__ offs,
                                                              const uint32_t* __restrict__ lens, uint64_t n,
-                                                             const uint32_t* __restrict__ posof,
-                                                             const uint64_t* __restrict__ binstart, ClassOut co,
-                                                             uint32_t w1max, uint64_t* __restrict__ out,
+                                                             const uint32_t* __restrict__ blkoff, uint32_t nblk,
+                                                             ClassOut co, uint32_t w1max, uint64_t* __restrict__ out,
                                                              uint64_t* __restrict__ fps, uint32_t* hll,
                                                              unsigned long long* first_bad) {
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-    const uint32_t nslot = kClsTile * w1max, nck = kClsTile * (2u * w1max - 1u);
+    constexpr uint32_t kWaves = kClsTile / 64;
+    const uint32_t nslot = kClsTile * w1max;
     uint64_t* sw = (uint64_t*)dyn;                          // [nslot] the tile's class spans, class after class
-    uint2* ck = (uint2*)(sw + nslot);                       // [nck] chunk codes + masks
-    uint8_t* scls = (uint8_t*)(ck + nck);                   // [nslot] span slot -> its class
+    uint8_t* scls = (uint8_t*)(sw + nslot);                 // [nslot] span slot -> its class
     uint8_t* smap = scls + nslot;                           // [nslot] word slot -> read of the tile
-    uint8_t* cmap = smap + nslot;                           // [nck] chunk slot -> read of the tile
     __shared__ uint64_t soff[kClsTile];
     __shared__ uint32_t srow[kClsTile];                     // row within the tile's span of its class
-    __shared__ uint16_t sqoff[kClsTile + 1], scoff[kClsTile + 1], sL[kClsTile];
-    __shared__ uint32_t rmin[33], rcnt[33], cbase[34], wsum[kClsTile / 64];
+    __shared__ uint16_t sqoff[kClsTile + 1], sL[kClsTile];
+    __shared__ uint32_t wcnt[kWaves][33], tcnt[33], cur[33], cbase[34], wsum[kWaves];
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-    const uint64_t r0 = (uint64_t)blockIdx.x * kClsTile, r = r0 + t;
-    if (t < 33) {
-        rmin[t] = 0xFFFFFFFFu;
-        rcnt[t] = 0;
-    }
-    __syncthreads();
-    // a. classes, rows, word and chunk slots
-    const uint32_t L = r < n ? lens[r] : 0u;
-    const bool cls = L > 32u && L <= SS_MAX_NT;
-    const uint32_t W = cls ? (L + 31u) / 32u : 0u, w1 = cls ? W + 1u : 0u;
-    uint64_t off = 0;
-    uint32_t row = 0, nc = 0;
-    if (cls) {
-        row = posof[r] - (uint32_t)binstart[co.bin0 + W];
-        atomicMin(&rmin[W], row);
-        atomicAdd(&rcnt[W], 1u);
-        off = offs[r];
-        soff[t] = off;
-        nc = ((uint32_t)(off & 15u) + L + 15u) >> 4;
-    }
-    sL[t] = (uint16_t)(cls ? L : 0u);
-    const uint32_t v = w1 | nc << 16;       // word slots | chunk slots (each < 2^16 per tile)
-    uint32_t inc = v;
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d);
-        if (lane >= d) inc += y;
-    }
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t u = 0; u < wave; ++u) before += wsum[u];
-    const uint32_t ex = before + inc - v, q0 = ex & 0xFFFFu, c0 = ex >> 16;
-    sqoff[t] = (uint16_t)q0;
-    scoff[t] = (uint16_t)c0;
-    if (t == kClsTile - 1) {
-        sqoff[kClsTile] = (uint16_t)(q0 + w1);
-        scoff[kClsTile] = (uint16_t)(c0 + nc);
-    }
-    for (uint32_t k = 0; k < w1; ++k) smap[q0 + k] = (uint8_t)t;
-    for (uint32_t k = 0; k < nc; ++k) cmap[c0 + k] = (uint8_t)t;
-    if (cls) srow[t] = row - rmin[W];
-    if (t == 0) {
-        uint32_t c = 0;
-        for (uint32_t u = 0; u < 33; ++u) {
-            cbase[u] = c;
-            c += u >= 2 ? rcnt[u] * (u + 1u) : 0u;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // this block's read range: k_len_count's (its class rows start at the binscan's offsets)
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
+    if (t < 33) cur[t] = t >= 2 ? blkoff[(uint64_t)(co.bin0 + t) * nblk + blockIdx.x] : 0u;
+    for (uint64_t r0 = lo; r0 < hi; r0 += kClsTile) {
+        const uint64_t r = r0 + t;
+        // a. classes, rows (stable: the wave's lanes ranked by ballot, the waves in order), word slots
+        const uint64_t rc = min(r, n - 1);
+        const uint32_t L0 = lens[rc];
+        const uint64_t off = offs[rc];
+        for (uint32_t i = t; i < kWaves * 33; i += kClsTile) (&wcnt[0][0])[i] = 0;
+        __syncthreads();
+        const uint32_t L = r < hi ? L0 : 0u;
+        const bool cls = L > 32u && L <= SS_MAX_NT;
+        const uint32_t W = cls ? (L + 31u) / 32u : 0u, w1 = cls ? W + 1u : 0u;
+        uint32_t rk = 0;
+        uint64_t pending = __ballot(cls);
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const uint32_t Wl = (uint32_t)__shfl((int)W, leader);
+            const uint64_t mine = __ballot(cls && W == Wl);
+            if (cls && W == Wl) rk = (uint32_t)__popcll(mine & lt);
+            if (lane == (uint32_t)leader) wcnt[wave][Wl] = (uint32_t)__popcll(mine);
+            pending &= ~mine;
         }
-        cbase[33] = c;
-    }
-    __syncthreads();
-    // b. lane per chunk slot: kClsLoads chunk loads in flight per lane, then their codes
-    const uint32_t C = scoff[kClsTile];
-    const uint4* in16 = (const uint4*)in;
-    for (uint32_t qb = t; qb < C; qb += kClsLoads * kClsTile) {
-        uint4 x[kClsLoads];
-#pragma unroll
-        for (uint32_t k = 0; k < kClsLoads; ++k) {
-            const uint32_t q = min(qb + k * kClsTile, C - 1u);
-            const uint32_t tt = cmap[q];
-            x[k] = in16[(soff[tt] >> 4) + (q - scoff[tt])];
+        if (cls) soff[t] = off;
+        sL[t] = (uint16_t)(cls ? L : 0u);
+        uint32_t inc = w1;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if (lane >= d) inc += y;
         }
-#pragma unroll
-        for (uint32_t k = 0; k < kClsLoads; ++k) {
-            const uint32_t q = qb + k * kClsTile;
-            if (q < C) ck[q] = code_chunk(x[k]);
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t before = 0;
+        for (uint32_t u = 0; u < wave; ++u) before += wsum[u];
+        const uint32_t q0 = before + inc - w1;
+        sqoff[t] = (uint16_t)q0;
+        if (t == kClsTile - 1) sqoff[kClsTile] = (uint16_t)(q0 + w1);
+        for (uint32_t k = 0; k < w1; ++k) smap[q0 + k] = (uint8_t)t;
+        if (cls) {
+            uint32_t pre = rk;
+            for (uint32_t u = 0; u < wave; ++u) pre += wcnt[u][W];
+            srow[t] = pre;
         }
-    }
-    __syncthreads();
-    // c. lane per word slot, read order
-    const uint32_t Q = sqoff[kClsTile];
-    for (uint32_t q = t; q < Q; q += kClsTile) {
-        const uint32_t tt = smap[q];
-        const uint32_t LL = sL[tt], WW = (LL + 31u) / 32u, w = q - sqoff[tt];
-        uint32_t bad = 0;
-        uint64_t word = LL;
-        if (w < WW) {
-            const uint32_t nb = min(32u, LL - 32u * w);
-            const uint32_t sh = (uint32_t)(soff[tt] & 15u);
-            const uint32_t cb = scoff[tt] + 2u * w, ce = scoff[tt + 1];   // the read's chunks end at ce
-            const uint2 a = ck[cb];
-            const uint2 b = cb + 1u < ce ? ck[cb + 1u] : make_uint2(0u, 0u);
-            const uint2 c = cb + 2u < ce ? ck[cb + 2u] : make_uint2(0u, 0u);
-            const uint64_t lo = (uint64_t)b.x << 32 | a.x;
-            word = sh ? (lo >> (2u * sh)) | ((uint64_t)c.x << (64u - 2u * sh)) : lo;
-            const uint64_t keep = nb < 32u ? (1ull << (2u * nb)) - 1ull : ~0ull;
-            word &= keep;
-            const uint64_t bytes = ((uint64_t)1 << nb) - 1ull;                  // nb <= 32
-            const uint64_t rej = ((uint64_t)(a.y & 0xFFFFu) | (uint64_t)(b.y & 0xFFFFu) << 16 |
-                                  (uint64_t)(c.y & 0xFFFFu) << 32) >> sh;
-            bad = (rej & bytes) != 0ull;
-            if (nb < 32u) {
-                const uint64_t al = ((uint64_t)(a.y >> 16) | (uint64_t)(b.y >> 16) << 16 | (uint64_t)(c.y >> 16) << 32) >> sh;
-                if (al & bytes) {   // an aliased byte in a table-path word: its carry, exactly (rare)
-                    uint32_t b2 = 0;
-                    word = encode_word_q(in + soff[tt] + 32u * w, nb, true, b2);
-                    bad |= b2;
+        if (t == 0) {
+            uint32_t c = 0;
+            for (uint32_t u = 0; u < 33; ++u) {
+                uint32_t m = 0;
+                for (uint32_t v = 0; v < kWaves; ++v) m += wcnt[v][u];
+                tcnt[u] = u >= 2 ? m : 0u;
+                cbase[u] = c;
+                c += tcnt[u] * (u + 1u);
+            }
+            cbase[33] = c;
+        }
+        __syncthreads();
+        // b. lane per word slot, read order: the word's three aligned chunks encoded where they lie
+        const uint32_t Q = sqoff[kClsTile];
+        const uint4* in16 = (const uint4*)in;
+        for (uint32_t q = t; q < Q; q += kClsTile) {
+            const uint32_t tt = smap[q];
+            const uint32_t LL = sL[tt], WW = (LL + 31u) / 32u, w = q - sqoff[tt];
+            uint32_t bad = 0;
+            uint64_t word = LL;
+            if (w < WW) {
+                const uint32_t nb = min(32u, LL - 32u * w);
+                const uint64_t ro = soff[tt];
+                const uint32_t sh = (uint32_t)(ro & 15u);
+                const uint32_t last = (sh + nb - 1u) >> 4;          // 0..2: the chunk holding the word's last byte
+                const uint64_t c0 = (ro >> 4) + 2u * w;
+                const uint2 a = code_chunk(in16[c0]);
+                const uint2 b = code_chunk(in16[c0 + min(1u, last)]);
+                const uint2 c = code_chunk(in16[c0 + min(2u, last)]);
+                const uint64_t lo64 = (uint64_t)b.x << 32 | a.x;
+                word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)c.x << (64u - 2u * sh)) : lo64;
+                if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
+                if ((a.y | b.y | c.y) != 0u) {      // rejected or bit-6-clear bytes somewhere in the chunks
+                    const uint64_t bytes = ((uint64_t)1 << nb) - 1ull;                  // nb <= 32
+                    const uint32_t by = last >= 1u ? b.y : 0u, cy = last >= 2u ? c.y : 0u;
+                    const uint64_t rej = ((uint64_t)(a.y & 0xFFFFu) | (uint64_t)(by & 0xFFFFu) << 16 |
+                                          (uint64_t)(cy & 0xFFFFu) << 32) >> sh;
+                    bad = (rej & bytes) != 0ull;
+                    const uint64_t al =
+                        ((uint64_t)(a.y >> 16) | (uint64_t)(by >> 16) << 16 | (uint64_t)(cy >> 16) << 32) >> sh;
+                    if (nb < 32u && (al & bytes)) {   // an aliased byte in a table-path word: its carry, exactly
+                        uint32_t b2 = 0;
+                        word = encode_word_q(in + ro + 32u * w, nb, true, b2);
+                        bad |= b2;
+                    }
                 }
             }
+            const uint32_t at = cbase[WW] + srow[tt] * (WW + 1u) + w;
+            sw[at] = word;
+            scls[at] = (uint8_t)WW;
+            report_bad(bad != 0u, r0 + tt, first_bad);
         }
-        const uint32_t at = cbase[WW] + srow[tt] * (WW + 1u) + w;
-        sw[at] = word;
-        scls[at] = (uint8_t)WW;
-        report_bad(bad != 0u, r0 + tt, first_bad);
-    }
-    __syncthreads();
-    // d. the class spans out (dense), fingerprints, sketches
-    for (uint32_t q = t; q < Q; q += kClsTile) {
-        const uint32_t c = scls[q];
-        out[co.woff[c] + (uint64_t)rmin[c] * (c + 1u) + (q - cbase[c])] = sw[q];
-    }
-    if (cls) {
-        const uint64_t fp = words_fp(sw + cbase[W] + srow[t] * w1, w1);
-        if (fps) fps[co.fpoff[W] + row] = fp;
-        hll_add(hll + ((uint64_t)W << kHllLog), fp, w1);
+        __syncthreads();
+        // c. the class spans out (dense), fingerprints, sketches, the rows' read indices
+        for (uint32_t q = t; q < Q; q += kClsTile) {
+            const uint32_t c = scls[q];
+            out[co.woff[c] + (uint64_t)cur[c] * (c + 1u) + (q - cbase[c])] = sw[q];
+        }
+        if (cls) {
+            const uint32_t row = cur[W] + srow[t];
+            const uint64_t fp = words_fp(sw + cbase[W] + srow[t] * w1, w1);
+            if (fps) fps[co.fpoff[W] + row] = fp;
+            if (co.rmap[W]) co.rmap[W][row] = co.base + r;
+            hll_add(hll + ((uint64_t)W << kHllLog), fp, w1);
+        }
+        __syncthreads();
+        if (t < 33) cur[t] += tcnt[t];
     }
 }
 
@@ -1175,26 +1173,22 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
 }
 
 int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
-                           const uint32_t* d_posof, const uint64_t* d_binstart, const uint64_t* h_woff,
-                           const uint64_t* h_fpoff, uint32_t bin0, uint32_t w1max, uint64_t* d_out, uint64_t* d_fps,
-                           uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
+                           const uint32_t* d_blkoff, uint32_t nblk, const uint64_t* h_woff, const uint64_t* h_fpoff,
+                           uint64_t* const* h_rmap, uint64_t base, uint32_t bin0, uint32_t w1max, uint64_t* d_out,
+                           uint64_t* d_fps, uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
     if (n == 0) return SS_OK;
     if (w1max < 3 || w1max > 16) return ss_fail(SS_EARG, "k_encode_classes: classes of 2 to 15 words");
     ClassOut co;
     for (int W = 0; W < 33; ++W) {
         co.woff[W] = h_woff[W];
         co.fpoff[W] = h_fpoff ? h_fpoff[W] : 0;
+        co.rmap[W] = h_rmap ? h_rmap[W] : nullptr;
     }
+    co.base = base;
     co.bin0 = bin0;
-    const uint64_t blocks = (n + kClsTile - 1) / kClsTile;
-    if (blocks > 0x7FFFFFFFull) return ss_fail(SS_EARG, "chunk too large for k_encode_classes");
-    const size_t lds = (size_t)kClsTile * w1max * 10 + (size_t)kClsTile * (2 * w1max - 1) * 9;
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_encode_classes,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)((size_t)kClsTile * 16 * 10 + (size_t)kClsTile * 31 * 9));
-    if (attr != hipSuccess) return ss_check(attr, "k_encode_classes LDS attribute");
-    hipLaunchKernelGGL(k_encode_classes, dim3((unsigned)blocks), dim3(kClsTile), lds, (hipStream_t)stream, d_buf, d_offs,
-                       d_lens, n, d_posof, d_binstart, co, w1max, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad);
+    const size_t lds = (size_t)kClsTile * w1max * 10;
+    hipLaunchKernelGGL(k_encode_classes, dim3(nblk), dim3(kClsTile), lds, (hipStream_t)stream, d_buf, d_offs, d_lens, n,
+                       d_blkoff, nblk, co, w1max, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_classes");
 }
 

@@ -88,6 +88,13 @@ struct ss_counter {
     // ss_counter_reset is lazy for the slot array: the next partitioned single-word insert's
     // aggregate writes whole slices instead (fresh mode); any other access memsets first
     bool reset_pending = false;
+    // per-pass timing of the optimistic partitioned insert (ss_counter_set_timing): a ring of event
+    // sets, one per insert, folded into the sums when read back (or when the ring wraps)
+    static constexpr uint32_t kTimerRing = 64, kPassEvents = 6;
+    hipEvent_t* tev = nullptr;             // [kTimerRing * kPassEvents] or null (timing off)
+    uint32_t thead = 0, tpend = 0;         // next set, sets recorded and not yet folded
+    double tsum[kPassEvents - 1] = {};
+    uint64_t tn = 0;
 };
 
 namespace {
@@ -919,7 +926,9 @@ __device__ __forceinline__ uint32_t dedup_home(uint64_t key, uint32_t log2n) {
     return (uint32_t)((key * 0xD6E8FEB86659FD93ull) >> (64 - log2n));
 }
 
-template <int T, int RPL>
+// KEYS: the keys come precomputed (in = n u64 keys, e.g. the drop-in engine's row fingerprints;
+// stride16 / cpr / first_bad unused) instead of being encoded from 16 / 32-nt ASCII rows.
+template <int T, int RPL, bool KEYS>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_coarse(
         Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16, uint64_t n, uint32_t cpr, uint64_t cap1,
         uint32_t* fill, unsigned long long* first_bad) {
@@ -938,6 +947,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t sub = blockIdx.x % kFinePerBin;   // this block's sub-bin of every bin
     uint4 nx[RPL][2];
+    uint64_t nk[RPL];
     // branch-free loads (read index clamped to the last read; lanes past n are never live): the
     // compiler then waits for each chunk just before its encode instead of for all 2 * RPL loads
     const uint32_t hi16 = cpr > 1 ? 1u : 0u;    // L = 16: one chunk (the high half reads 'A's below)
@@ -945,8 +955,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
             const uint64_t r = min(tile * TILE + j * T + threadIdx.x, n - 1);
-            nx[j][0] = ld_stream(&in[r * stride16]);
-            nx[j][1] = ld_stream(&in[r * stride16 + hi16]);
+            if constexpr (KEYS) {
+                nk[j] = ((const uint64_t*)in)[r];
+            } else {
+                nx[j][0] = ld_stream(&in[r * stride16]);
+                nx[j][1] = ld_stream(&in[r * stride16 + hi16]);
+            }
         }
     };
     // wave 0 lane, bins b0 = 2 lane and b0 + 1: reserve c0 / c1 slots of their sub-bins (b, sub) with
@@ -984,13 +998,17 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
             const uint64_t r = t0 + j * T + threadIdx.x;
-            // table path for both chunks (L <= 32); the low chunk's alias carry into the high half
-            const Enc32 a = encode16(nx[j][0].x, nx[j][0].y, nx[j][0].z, nx[j][0].w, true);
-            const uint4 h = hi16 ? nx[j][1] : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
-            const Enc32 b = encode16(h.x, h.y, h.z, h.w, true);
             const bool live = r < n;
-            report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
-            key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
+            if constexpr (KEYS) {
+                key[j] = nk[j];
+            } else {
+                // table path for both chunks (L <= 32); the low chunk's alias carry into the high half
+                const Enc32 a = encode16(nx[j][0].x, nx[j][0].y, nx[j][0].z, nx[j][0].w, true);
+                const uint4 h = hi16 ? nx[j][1] : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+                const Enc32 b = encode16(h.x, h.y, h.z, h.w, true);
+                report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
+                key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
+            }
             if (live) {
                 bin[j] = region_of(t, key[j]) >> shift;
                 rank[j] = atomicAdd(&lcount[bin[j]], 1u);
@@ -1999,32 +2017,6 @@ __global__ __launch_bounds__(T) void k_mw_fp(Tbl t, PartWs w, uint32_t bins, con
     }
 }
 
-// The same histogram from fingerprints computed upstream (ss_counter_insert_words_fp): 8 B per row
-// read instead of the row, no hashing.
-template <int T>
-__global__ __launch_bounds__(T) void k_mw_hist(Tbl t, PartWs w, uint32_t bins, const uint64_t* __restrict__ fps,
-                                               uint64_t n) {
-    extern __shared__ uint32_t hist[];
-    constexpr uint32_t kWaves = T / 64;
-    const uint32_t copies = bins * kWaves <= kMaxRegions ? kWaves : 1u;
-    uint32_t* my = hist + (copies > 1 ? (threadIdx.x >> 6) * bins : 0u);
-    for (uint32_t i = threadIdx.x; i < bins * copies; i += T) hist[i] = 0;
-    __syncthreads();
-    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n, lo + per);
-    for (uint64_t r = lo + threadIdx.x; r < hi; r += T) {
-        const uint64_t fp = fps[r];
-        w.keys[r] = fp;
-        atomicAdd(&my[bin_of<true>(t, w, fp)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < bins; i += T) {
-        uint32_t sum = 0;
-        for (uint32_t c = 0; c < copies; ++c) sum += hist[c * bins + i];
-        w.hist[(uint64_t)blockIdx.x * bins + i] = sum;
-    }
-}
-
 constexpr uint32_t kMwT = 1024;
 constexpr uint32_t kMwPerThread = (2u << kMwSliceLog) / kMwT;
 
@@ -2298,6 +2290,26 @@ int flush_reset(ss_counter* c, hipStream_t s) {
     return ss_check(hipMemsetAsync(c->slots, 0xFF, c->cap * sizeof(Slot), s), "ss_counter reset");
 }
 
+// fold the oldest recorded timing set into the sums (waits for its last event)
+void timer_fold_one(ss_counter* c) {
+    const uint32_t k = (c->thead + ss_counter::kTimerRing - c->tpend) % ss_counter::kTimerRing;
+    hipEvent_t* e = c->tev + (uint64_t)k * ss_counter::kPassEvents;
+    (void)hipEventSynchronize(e[ss_counter::kPassEvents - 1]);
+    for (uint32_t p = 0; p + 1 < ss_counter::kPassEvents; ++p) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e[p], e[p + 1]) == hipSuccess) c->tsum[p] += ms;
+    }
+    ++c->tn;
+    --c->tpend;
+}
+
+// event p of this insert's timing set (null when timing is off)
+hipEvent_t timer_event(ss_counter* c, uint32_t p) {
+    if (!c->tev) return nullptr;
+    if (p == 0 && c->tpend == ss_counter::kTimerRing) timer_fold_one(c);
+    return c->tev[(uint64_t)c->thead * ss_counter::kPassEvents + p];
+}
+
 unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap) {
     uint64_t b = (items + per_block - 1) / per_block;
     if (b == 0) b = 1;
@@ -2325,6 +2337,212 @@ int launch_merge(ss_counter* c, Recs recs, const uint64_t* d_run_offsets, uint32
 }  // namespace
 
 extern "C" {
+
+// ------------------------------------------------------------------------------------------------
+// The drop-in engine's length classes counted by fingerprint (ss_classes_* in ss_internal.h).  The
+// classes' rows (W1 = W + 1 words: the read's words and its length) are counted by their 64-bit
+// fingerprint alone in one single-word scratch table `fpt` (ss_counter_insert_keys: the optimistic
+// partitioned insert on 8-B keys, 12-B records, no row gathers), then
+//   k_cls_verify: every row is compared with the first row of its fingerprint (the scratch entry's
+//     first index is that row's place in the classes' combined row array): a difference means two
+//     keys share a fingerprint and raises *flag (the engine then counts those classes again on the
+//     exact multi-word path, whose aggregate decides equality on the words; the class tables are
+//     untouched until the fold)
+//   k_cls_fold_find / k_cls_fold_claim: unless *flag, every scratch entry -- a distinct key now --
+//     goes into its class's table with ss_counter_merge_words' two phases, its words taken from its
+//     first row.
+// The row gathers this replaces (the multi-word aggregate read its own row and its representative's
+// for every record: 1.9-3.3 ms of the f2 batch) become one compare per row against a row of ~1M
+// distinct representatives that stay in the Infinity Cache.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kMaxClassesDesc = 32;
+struct ClsDesc {
+    Tbl tbl[kMaxClassesDesc];
+    const uint64_t* rows[kMaxClassesDesc];
+    uint64_t row0[kMaxClassesDesc + 1];     // combined row index of each class's first row; [ncls] = total
+    uint64_t base[kMaxClassesDesc];         // the class table's first row index for this insert
+    uint32_t W1[kMaxClassesDesc];
+    uint32_t ncls;
+};
+
+__device__ __forceinline__ uint32_t cls_of(const ClsDesc& d, uint64_t g) {
+    uint32_t c = 0;
+    while (c + 1 < d.ncls && g >= d.row0[c + 1]) ++c;
+    return c;
+}
+
+// the scratch slot holding key fp (kEmpty when absent)
+__device__ __forceinline__ uint64_t find_slot(const Tbl& t, uint64_t fp) {
+    const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
+    uint64_t off = top & t.slice_mask;
+    for (uint64_t probe = 0; probe <= t.slice_mask; ++probe) {
+        const uint64_t k = t.slots[base + off].key;
+        if (k == fp) return base + off;
+        if (k == kEmpty) return kEmpty;
+        off = (off + 1) & t.slice_mask;
+    }
+    return kEmpty;
+}
+
+__global__ __launch_bounds__(256) void k_cls_verify(Tbl f, ClsDesc d, const uint64_t* __restrict__ fps,
+                                                    uint32_t* __restrict__ flag) {
+    const uint64_t n = d.row0[d.ncls];
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < n; g += (uint64_t)gridDim.x * 256) {
+        const uint32_t c = cls_of(d, g);
+        const uint64_t sl = find_slot(f, fps[g]);
+        bool bad = sl == kEmpty;
+        if (!bad) {
+            const uint64_t rep = f.slots[sl].first;
+            if (rep != g) {
+                bad = rep < d.row0[c] || rep >= d.row0[c + 1];
+                if (!bad) {
+                    const uint32_t W1 = d.W1[c];
+                    const uint64_t* a = d.rows[c] + (g - d.row0[c]) * W1;
+                    const uint64_t* b = d.rows[c] + (rep - d.row0[c]) * W1;
+                    for (uint32_t j = 0; j < W1; ++j) bad |= a[j] != b[j];
+                }
+            }
+        }
+        if (__ballot(bad) && bad) atomicOr(flag, 1u);
+    }
+}
+
+// The representatives beside the scratch slots (verify on rows of <= kRepW1 words): rep[s] = 64 B =
+// {slot s's key, its first row's W1 words, .., its class in word 7} (kEmpty key: a free slot), so the
+// check of a row is ONE 64-B read at its fingerprint's home slot (linear probing continues rarely)
+// instead of a slot probe plus a gather of the representative's row.  The table of 2^21 slots is
+// 128 MB: it stays in the Infinity Cache while the rows stream past.
+constexpr uint32_t kRepW1 = 6;
+__global__ __launch_bounds__(256) void k_cls_reps(Tbl f, ClsDesc d, uint64_t* __restrict__ rep) {
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+        const Slot sl = f.slots[s];
+        uint64_t v[8] = {sl.key, 0, 0, 0, 0, 0, 0, ~0ull};
+        if (sl.key != kEmpty) {
+            const uint64_t g = sl.first;
+            const uint32_t c = cls_of(d, g);
+            const uint64_t* kw = d.rows[c] + (g - d.row0[c]) * d.W1[c];
+            for (uint32_t j = 0; j < d.W1[c]; ++j) v[1 + j] = kw[j];
+            v[7] = c;
+        }
+        uint4* dst = (uint4*)(rep + s * 8);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k] = make_uint4((uint32_t)v[2 * k], (uint32_t)(v[2 * k] >> 32), (uint32_t)v[2 * k + 1],
+                                                       (uint32_t)(v[2 * k + 1] >> 32));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cls_verify_rep(Tbl f, ClsDesc d, const uint64_t* __restrict__ fps,
+                                                        const uint64_t* __restrict__ rep, uint32_t* __restrict__ flag) {
+    const uint64_t n = d.row0[d.ncls];
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < n; g += (uint64_t)gridDim.x * 256) {
+        const uint32_t c = cls_of(d, g);
+        const uint64_t fp = fps[g];
+        const uint64_t top = slot_top(f, fp), base = top & ~f.slice_mask;
+        uint64_t off = top & f.slice_mask;
+        bool bad = true;
+        for (uint64_t probe = 0; probe <= f.slice_mask; ++probe) {
+            const uint4* e = (const uint4*)(rep + (base + off) * 8);
+            const uint4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+            const uint64_t key = (uint64_t)e0.y << 32 | e0.x;
+            if (key == fp) {
+                const uint64_t rw[7] = {(uint64_t)e0.w << 32 | e0.z, (uint64_t)e1.y << 32 | e1.x,
+                                        (uint64_t)e1.w << 32 | e1.z, (uint64_t)e2.y << 32 | e2.x,
+                                        (uint64_t)e2.w << 32 | e2.z, (uint64_t)e3.y << 32 | e3.x,
+                                        (uint64_t)e3.w << 32 | e3.z};
+                bad = (uint32_t)rw[6] != c;
+                const uint32_t W1 = d.W1[c];
+                const uint64_t* a = d.rows[c] + (g - d.row0[c]) * W1;
+#pragma unroll
+                for (uint32_t j = 0; j < kRepW1; ++j)
+                    if (j < W1) bad |= a[j] != rw[j];
+                break;
+            }
+            if (key == kEmpty) break;
+            off = (off + 1) & f.slice_mask;
+        }
+        if (__ballot(bad) && bad) atomicOr(flag, 1u);
+    }
+}
+
+// scratch slot s (an entry: key fp, ~count, first row g) -> its class and first row's words
+__device__ __forceinline__ bool fold_entry(const Tbl& f, const ClsDesc& d, uint64_t s, uint64_t& fp, uint32_t& cnt,
+                                           uint32_t& c, const uint64_t*& kw, uint64_t& first) {
+    const Slot sl = f.slots[s];
+    if (s > f.mask || sl.key == kEmpty) return false;
+    fp = sl.key;
+    cnt = ~sl.ncount;
+    const uint64_t g = sl.first;
+    c = cls_of(d, g);
+    kw = d.rows[c] + (g - d.row0[c]) * d.W1[c];
+    first = d.base[c] + (g - d.row0[c]);
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_cls_fold_find(Tbl f, ClsDesc d, const uint32_t* __restrict__ flag,
+                                                       uint64_t* __restrict__ found) {
+    if (*flag) return;
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+        uint64_t fp, first;
+        uint32_t cnt, c;
+        const uint64_t* kw;
+        uint64_t at = kEmpty;
+        if (fold_entry(f, d, s, fp, cnt, c, kw, first)) {
+            const Tbl& t = d.tbl[c];
+            const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
+            uint64_t off = top & t.slice_mask;
+            for (uint64_t probe = 0; probe <= t.slice_mask; ++probe) {
+                const uint64_t k = t.slots[base + off].key;
+                if (k == kEmpty) break;
+                if (k == fp && words_eq(t.keywords + (base + off) * t.W, kw, t.W)) {
+                    at = base + off;
+                    break;
+                }
+                off = (off + 1) & t.slice_mask;
+            }
+        }
+        found[s] = at;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_cls_fold_claim(Tbl f, ClsDesc d, const uint32_t* __restrict__ flag,
+                                                        const uint64_t* __restrict__ found) {
+    if (*flag) return;
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+        uint64_t fp, first;
+        uint32_t cnt, c;
+        const uint64_t* kw;
+        if (!fold_entry(f, d, s, fp, cnt, c, kw, first)) continue;
+        const Tbl& t = d.tbl[c];
+        if (first > kMaxIndex) {
+            atomicOr(t.overflow, kOvfIndex);
+            first = kMaxIndex;
+        }
+        uint64_t at = found[s];
+        if (at == kEmpty) {
+            const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
+            uint64_t off = top & t.slice_mask;
+            for (uint64_t probe = 0; probe <= t.slice_mask; ++probe) {
+                if (t.slots[base + off].key == kEmpty &&
+                    atomicCAS(&t.slots[base + off].key, (unsigned long long)kEmpty, (unsigned long long)fp) == kEmpty) {
+                    at = base + off;
+                    break;
+                }
+                off = (off + 1) & t.slice_mask;
+            }
+            if (at == kEmpty) {
+                atomicOr(t.overflow, kOvfTable);
+                continue;
+            }
+            uint64_t* dst = t.keywords + at * t.W;
+            for (uint32_t q = 0; q < t.W; ++q) dst[q] = kw[q];
+            t.slots[at].ncount = ~cnt;
+            t.slots[at].first = (uint32_t)first;
+            continue;
+        }
+        atomicAdd(&t.slots[at].ncount, 0u - cnt);
+        if (t.slots[at].first > (uint32_t)first) atomicMin(&t.slots[at].first, (uint32_t)first);
+    }
+}
 
 int ss_counter_create(uint64_t capacity, ss_counter** out) {
     if (!out) return ss_fail(SS_EARG, "null out");
@@ -2361,8 +2579,37 @@ int ss_counter_create(uint64_t capacity, ss_counter** out) {
     return SS_OK;
 }
 
+int ss_counter_set_timing(ss_counter* c, int on) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (on && !c->tev) {
+        c->tev = new hipEvent_t[(uint64_t)ss_counter::kTimerRing * ss_counter::kPassEvents]();
+        for (uint32_t k = 0; k < ss_counter::kTimerRing * ss_counter::kPassEvents; ++k)
+            if (hipEventCreate(&c->tev[k]) != hipSuccess) return ss_check(hipGetLastError(), "timing events");
+    } else if (!on && c->tev) {
+        while (c->tpend) timer_fold_one(c);
+        for (uint32_t k = 0; k < ss_counter::kTimerRing * ss_counter::kPassEvents; ++k)
+            if (c->tev[k]) (void)hipEventDestroy(c->tev[k]);
+        delete[] c->tev;
+        c->tev = nullptr;
+    }
+    return SS_OK;
+}
+
+int ss_counter_pass_times(ss_counter* c, double* h_ms, uint64_t* h_inserts) {
+    if (!c || !h_ms || !h_inserts) return ss_fail(SS_EARG, "null argument");
+    while (c->tpend) timer_fold_one(c);
+    *h_inserts = c->tn;
+    for (uint32_t p = 0; p + 1 < ss_counter::kPassEvents; ++p) {
+        h_ms[p] = c->tn ? c->tsum[p] / (double)c->tn : 0.0;
+        c->tsum[p] = 0.0;
+    }
+    c->tn = 0;
+    return SS_OK;
+}
+
 int ss_counter_destroy(ss_counter* c) {
     if (!c) return SS_OK;
+    (void)ss_counter_set_timing(c, 0);
     if (c->slots) (void)hipFree(c->slots);
     if (c->work) (void)hipFree(c->work);
     if (c->keywords) (void)hipFree(c->keywords);
@@ -2518,15 +2765,21 @@ int ss_counter_release(ss_counter* c) {
 // unused), else ASCII reads of length L
 static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32_t L, uint64_t stride,
                        uint64_t base_index, uint64_t* d_first_bad, void* stream, const uint64_t* words_in,
-                       const uint64_t* fps_in = nullptr) {
+                       const uint64_t* keys_in = nullptr) {
     hipStream_t s = (hipStream_t)stream;
     int rc = SS_OK;
+    if (keys_in) {     // precomputed single-word keys: always partitioned
+        if (c->W != 1) return ss_fail(SS_EARG, "precomputed keys need a single-word handle");
+        if (n == 0) return SS_OK;
+        if (n > c->ws_reads && (rc = ss_counter_reserve(c, n)) != SS_OK) return rc;
+    }
     const uint32_t rb = c->log2cap - c->slice_log;
     // the optimistic coarse partition below (the C5 path) resets first_bad with its sub-bin counters
-    const bool opt = !words_in && n > 0 && d_ascii && (L == 16 || L == 32) && stride % 16 == 0 &&
-                     (((uintptr_t)d_ascii) & 15) == 0 && n <= c->ws_reads && rb > kCoarseBits &&
-                     rb - kCoarseBits <= 8;
-    if (!words_in) {
+    const bool opt = !words_in && n > 0 && n <= c->ws_reads && rb > kCoarseBits && rb - kCoarseBits <= 8 &&
+                     (keys_in || (d_ascii && (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0));
+    if (keys_in) {
+        // nothing to encode, no first_bad
+    } else if (!words_in) {
         if (!d_first_bad) return ss_fail(SS_EARG, "d_first_bad is required");
         if (stride < L) return ss_fail(SS_EARG, "stride < L");
         if ((rc = fix_length(c, L))) return rc;
@@ -2541,7 +2794,7 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
     c->occ_src = 0;   // set again below by the paths whose aggregate records the region occupancy
     Tbl t = tbl_of(c);
     const bool multi = c->W > 1;
-    const bool fast = !words_in && (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
+    const bool fast = !words_in && !keys_in && (L == 16 || L == 32) && stride % 16 == 0 && (((uintptr_t)d_ascii) & 15) == 0;
     const uint64_t* mw = words_in;          // the multi-word rows the partition passes read
     if (multi) {
         // multi-word keys: always partitioned; grow the workspace to this batch if needed
@@ -2566,7 +2819,10 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
     // single-word keys of any other length / layout: pack into the key workspace first, then the
     // same partitioned passes (k_pc_hist replaces the fused encode of k_pc_keys)
     const bool packed_keys = !multi && !fast && n <= c->ws_reads;
-    if (packed_keys) {
+    if (packed_keys && keys_in && !opt) {
+        rc = ss_check(hipMemcpyAsync(c->ws_keys, keys_in, n * 8, hipMemcpyDeviceToDevice, s), "counter key copy");
+        if (rc) return rc;
+    } else if (packed_keys && !keys_in) {
         rc = ss_encode_fixed_impl(d_ascii, n, L, stride, c->ws_keys, 1, d_first_bad, nullptr, nullptr, stream);
         if (rc) return rc;
     }
@@ -2620,9 +2876,7 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
                                          kMaxRegions * 4);
             for (int f = 0; f < kMwAggFns && ea == hipSuccess; ++f)
                 ea = hipFuncSetAttribute((const void*)kMwAgg[f], hipFuncAttributeMaxDynamicSharedMemorySize, agg_max);
-            if (ea == hipSuccess)
-                ea = hipFuncSetAttribute((const void*)k_mw_hist<TF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         kMaxRegions * 4);
+
             return ea;
         }();
         if (attrs != hipSuccess) return ss_check(attrs, "hipFuncSetAttribute (dynamic LDS)");
@@ -2631,11 +2885,17 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
             hipLaunchKernelGGL(k_pc_scan, dim3(1), dim3(1024), 0, s, w, bins, start);
             hipLaunchKernelGGL(k_pc_offsets, dim3(bins), dim3(1024), 0, s, w, bins, (const uint32_t*)start);
         };
-        if (!multi && !packed_keys && two_pass && w.rbits - kCoarseBits <= 8) {
+        if (!multi && (!packed_keys || (keys_in && opt)) && two_pass && w.rbits - kCoarseBits <= 8) {
             // optimistic coarse partition: encode + coarse scatter in one pass, fine pass by bin
             const uint64_t cap1 = c->ws_cap1;
             w.slab = (uint32_t)c->ws_slab;
             w.spill_ctr = c->ws_fill + fill_at(kSpillCtr);
+            hipEvent_t tev[ss_counter::kPassEvents] = {};
+            for (uint32_t p = 0; p < ss_counter::kPassEvents; ++p) tev[p] = timer_event(c, p);
+            auto mark = [&](uint32_t p) {
+                if (tev[p]) (void)hipEventRecord(tev[p], s);
+            };
+            mark(0);
             PrepWords pw{};
             pw.p[0] = (unsigned long long*)d_first_bad;
             pw.v[0] = ~0ull;
@@ -2648,12 +2908,17 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
                 int dev = 0, cus = 0, per = 0;
                 (void)hipGetDevice(&dev);
                 (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL>, kPfT, 0);
+                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL, false>, kPfT, 0);
                 return (cus > 0 && per > 0) ? cus * per : (int)kPartBlocks;
             }();
-            hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
-                               (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
-                               (unsigned long long*)d_first_bad);
+            if (keys_in)
+                hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, true>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
+                                   (const uint4*)keys_in, (uint64_t)0, n, 0u, cap1, c->ws_fill,
+                                   (unsigned long long*)nullptr);
+            else
+                hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, false>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
+                                   (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
+                                   (unsigned long long*)d_first_bad);
             const unsigned fine_blocks = kCB * kFinePerBin;
             if (!w.slab) {   // counted cursors: region histogram per sub-bin, then the scans
                 hipLaunchKernelGGL((k_pf_count<512>), dim3(fine_blocks), dim3(512), 0, s, t, w, cap1,
@@ -2665,27 +2930,33 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
             }
             w.seg_end = c->ws_segend;
             w.slabs = w.slab ? c->ws_order + kNFill : nullptr;
+            mark(1);
             hipLaunchKernelGGL(k_pf_order, dim3(1), dim3(512), 0, s, (const uint32_t*)c->ws_fill, cap1, c->ws_order,
                                1u << (w.rbits - kCoarseBits), w.slab ? c->ws_order + kNFill : nullptr);
+            mark(2);
             hipLaunchKernelGGL((k_pf_scatter<kFsT, kFsTile>), dim3(fine_blocks), dim3(kFsT), 0, s, t, w, cap1,
                                (const uint32_t*)c->ws_fill, (const uint32_t*)c->ws_order);
+            mark(3);
             w.bkey = w.keys;
             w.brec = (const Rec12*)w.keys;
             hipLaunchKernelGGL((k_pc_aggregate_slice<kAggSliceT, true>), dim3(w.R), dim3(kAggSliceT),
                                ((size_t)1 << c->slice_log) * 16, s, t, w, base_index, fresh);
+            mark(4);
             // records that found their sub-bin full (none unless many distinct keys pile into a bin)
             hipLaunchKernelGGL(k_spill_insert, dim3(1024), dim3(256), 0, s, t, w, (const uint32_t*)c->ws_fill,
                                base_index);
+            mark(5);
+            if (c->tev) {
+                c->thead = (c->thead + 1) % ss_counter::kTimerRing;
+                ++c->tpend;
+            }
             c->occ_src = 1;
             return ss_check(hipGetLastError(), "optimistic partitioned insert");
         }
         if (multi) {
             const size_t fp_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             static_assert(TF == kMwFpT, "k_mw_fp instances");
-            if (fps_in)
-                hipLaunchKernelGGL((k_mw_hist<TF>), dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, fps_in, n);
-            else
-                hipLaunchKernelGGL(kMwFp[mw_variant(t.W, mw)], dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, mw, n);
+            hipLaunchKernelGGL(kMwFp[mw_variant(t.W, mw)], dim3(kPartBlocks), dim3(TF), fp_lds, s, t, w, bins1, mw, n);
         } else if (packed_keys) {
             const size_t h_lds = (bins1 * (TF / 64) <= kMaxRegions ? bins1 * (TF / 64) : bins1) * 4;
             hipLaunchKernelGGL((k_pc_hist<TF>), dim3(kPartBlocks), dim3(TF), h_lds, s, t, w, bins1, n);
@@ -2764,12 +3035,14 @@ int ss_counter_insert_words(ss_counter* c, const uint64_t* d_words, uint64_t n, 
     return insert_impl(c, nullptr, n, 0, 0, base_index, nullptr, stream, d_words);
 }
 
-int ss_counter_insert_words_fp(ss_counter* c, const uint64_t* d_words, const uint64_t* d_fps, uint64_t n,
-                               uint64_t base_index, void* stream) {
+int ss_counter_insert_keys(ss_counter* c, const uint64_t* d_keys, uint64_t n, uint64_t base_index, void* stream) {
     if (!c) return ss_fail(SS_EARG, "null counter");
-    if (c->L != kWordKeys) return ss_fail(SS_EARG, "ss_counter_set_words first");
-    if (n && (!d_words || !d_fps)) return ss_fail(SS_EARG, "null buffer");
-    return insert_impl(c, nullptr, n, 0, 0, base_index, nullptr, stream, d_words, d_fps);
+    if (n && !d_keys) return ss_fail(SS_EARG, "null buffer");
+    if (c->L < 0) {
+        const int rc = fix_length(c, 32);
+        if (rc) return rc;
+    }
+    return insert_impl(c, nullptr, n, 0, 0, base_index, nullptr, stream, nullptr, d_keys);
 }
 
 int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_lens,
@@ -2947,3 +3220,55 @@ int ss_counter_extract_words(ss_counter* c, uint32_t n_parts, uint64_t* d_fps, u
 }
 
 }  // extern "C"
+
+int ss_classes_verify_fold(ss_counter* fpt, const uint64_t* d_fps, const ss_class_rows* cls, uint32_t ncls,
+                           uint32_t* d_flag, void* stream) {
+    if (!fpt || !cls || !d_flag) return ss_fail(SS_EARG, "null argument");
+    if (ncls == 0) return SS_OK;
+    if (ncls > kMaxClassesDesc) return ss_fail(SS_EARG, "at most 32 length classes per insert");
+    hipStream_t s = (hipStream_t)stream;
+    ClsDesc d{};
+    d.ncls = ncls;
+    uint64_t row = 0;
+    int rc = SS_OK;
+    for (uint32_t k = 0; k < ncls; ++k) {
+        ss_counter* t = cls[k].table;
+        if (!t || t->L != kWordKeys || t->W != cls[k].W1) return ss_fail(SS_EARG, "class table: set_words(W1) first");
+        if ((rc = flush_reset(t, s))) return rc;
+        t->occ_src = 0;
+        d.tbl[k] = tbl_of(t);
+        d.rows[k] = cls[k].rows;
+        d.row0[k] = row;
+        d.base[k] = cls[k].base;
+        d.W1[k] = cls[k].W1;
+        row += cls[k].m;
+    }
+    d.row0[ncls] = row;
+    if ((rc = flush_reset(fpt, s))) return rc;
+    const Tbl f = tbl_of(fpt);
+    uint32_t w1max = 0;
+    for (uint32_t k = 0; k < ncls; ++k) w1max = std::max(w1max, cls[k].W1);
+    if (w1max <= kRepW1) {
+        uint64_t* rep = nullptr;
+        rc = ss_check(hipMallocAsync((void**)&rep, (fpt->cap + 1) * 64, s), "class reps scratch");
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_cls_reps, dim3(grid_for(fpt->cap, 256, 256 * 16)), dim3(256), 0, s, f, d, rep);
+        hipLaunchKernelGGL(k_cls_verify_rep, dim3(grid_for(row, 256, 256 * 32)), dim3(256), 0, s, f, d, d_fps,
+                           (const uint64_t*)rep, d_flag);
+        rc = ss_check(hipFreeAsync(rep, s), "class reps scratch free");
+        if (rc) return rc;
+    } else {
+        hipLaunchKernelGGL(k_cls_verify, dim3(grid_for(row, 256, 256 * 32)), dim3(256), 0, s, f, d, d_fps, d_flag);
+    }
+    uint64_t* found = nullptr;
+    rc = ss_check(hipMallocAsync((void**)&found, (fpt->cap + 1) * sizeof(uint64_t), s), "class fold scratch");
+    if (rc) return rc;
+    const unsigned grid = grid_for(fpt->cap, 256, 256 * 16);
+    hipLaunchKernelGGL(k_cls_fold_find, dim3(grid), dim3(256), 0, s, f, d, (const uint32_t*)d_flag, found);
+    hipLaunchKernelGGL(k_cls_fold_claim, dim3(grid), dim3(256), 0, s, f, d, (const uint32_t*)d_flag,
+                       (const uint64_t*)found);
+    rc = ss_check(hipGetLastError(), "class verify / fold");
+    const int rf = ss_check(hipFreeAsync(found, s), "class fold scratch free");
+    return rc ? rc : rf;
+}
+

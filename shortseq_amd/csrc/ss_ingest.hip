@@ -169,7 +169,7 @@ __global__ __launch_bounds__(1024) void k_len_binstart(uint64_t* __restrict__ ou
 // advances that length's LDS cursor
 __global__ __launch_bounds__(64) void k_len_scatter(const uint32_t* __restrict__ lens, uint64_t n,
                                                     const uint32_t* __restrict__ blkoff, const uint64_t* __restrict__ split,
-                                                    uint64_t* __restrict__ order, uint32_t* __restrict__ posof) {
+                                                    uint64_t* __restrict__ order) {
     __shared__ uint32_t cur[kLenBins];
     for (uint32_t b = threadIdx.x; b < kLenBins; b += 64)
         cur[b] = (uint32_t)split[2 * kLenBins + b] + blkoff[(uint64_t)b * gridDim.x + blockIdx.x];
@@ -191,7 +191,6 @@ __global__ __launch_bounds__(64) void k_len_scatter(const uint32_t* __restrict__
             if (live && b == b0) {
                 const uint32_t pos = base + (uint32_t)__popcll(mine & lt);
                 order[pos] = i;
-                posof[i] = pos;                 // read -> its place in d_order (k_encode_classes)
             }
             __syncthreads();   // one wave: orders the cursor read before the update
             if (lane == (uint32_t)leader) cur[b0] = base + (uint32_t)__popcll(mine);
@@ -203,15 +202,15 @@ __global__ __launch_bounds__(64) void k_len_scatter(const uint32_t* __restrict__
 
 // row map of an insert: dst[r] = global index of row r (base + sel[r], or base + r when sel is null)
 __global__ __launch_bounds__(256) void k_rowmap(const uint64_t* __restrict__ sel, uint64_t m, uint64_t base,
-                                                uint32_t* __restrict__ dst) {
+                                                uint64_t* __restrict__ dst) {
     for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (uint64_t)gridDim.x * 256)
-        dst[r] = (uint32_t)(base + (sel ? sel[r] : r));
+        dst[r] = base + (sel ? sel[r] : r);
 }
 
 // table entry e -> the bit of its global first read (rowmap[first[e]]) in the read map; e == m: the
 // empty read's entry at global read `extra` (kNoSlot: none)
 __global__ __launch_bounds__(256) void k_mark(const uint64_t* __restrict__ first, uint64_t m,
-                                              const uint32_t* __restrict__ rowmap, uint64_t extra,
+                                              const uint64_t* __restrict__ rowmap, uint64_t extra,
                                               unsigned long long* __restrict__ bits) {
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e <= m; e += (uint64_t)gridDim.x * 256) {
         const uint64_t r = e < m ? rowmap[first[e]] : extra;
@@ -222,7 +221,7 @@ __global__ __launch_bounds__(256) void k_mark(const uint64_t* __restrict__ first
 // entry e of group g -> its place in read order: the marked reads before its first read
 // (wpre: exclusive prefix of the map words' popcounts)
 __global__ __launch_bounds__(256) void k_rank(const uint64_t* __restrict__ first, uint64_t m,
-                                              const uint32_t* __restrict__ rowmap, uint32_t g, uint64_t extra,
+                                              const uint64_t* __restrict__ rowmap, uint32_t g, uint64_t extra,
                                               const unsigned long long* __restrict__ bits,
                                               const uint64_t* __restrict__ wpre, uint64_t* __restrict__ ordered) {
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e <= m; e += (uint64_t)gridDim.x * 256) {
@@ -235,7 +234,7 @@ __global__ __launch_bounds__(256) void k_rank(const uint64_t* __restrict__ first
 
 // export: entry e's first read (engine-local) = rowmap[first[e]]
 __global__ __launch_bounds__(256) void k_export_reads(const uint64_t* __restrict__ first, uint64_t m,
-                                                      const uint32_t* __restrict__ rowmap, uint32_t* __restrict__ out) {
+                                                      const uint64_t* __restrict__ rowmap, uint64_t* __restrict__ out) {
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
         out[e] = rowmap[first[e]];
 }
@@ -243,10 +242,21 @@ __global__ __launch_bounds__(256) void k_export_reads(const uint64_t* __restrict
 // merge: a source group's m entries become rows `rows + e` of the destination group (first index of
 // the merged entry), their row map = the source's local first read + the source shard's base
 __global__ __launch_bounds__(256) void k_merge_rows(uint64_t m, uint64_t rows, uint64_t base,
-                                                    uint64_t* __restrict__ first, uint32_t* __restrict__ rowmap) {
+                                                    uint64_t* __restrict__ first, uint64_t* __restrict__ rowmap) {
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
         first[e] = rows + e;
-        rowmap[rows + e] = (uint32_t)(base + rowmap[rows + e]);
+        rowmap[rows + e] += base;
+    }
+}
+
+// re-key: entry e of a group's table becomes row e (its first index), the new row map = the entry's
+// first read
+__global__ __launch_bounds__(256) void k_rekey(const uint64_t* __restrict__ first, uint64_t m,
+                                               const uint64_t* __restrict__ rowmap, uint64_t* __restrict__ nmap,
+                                               uint64_t* __restrict__ nfirst) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
+        nmap[e] = rowmap[first[e]];
+        nfirst[e] = e;
     }
 }
 
@@ -452,11 +462,11 @@ struct Group {
     ss_counter* table = nullptr;
     uint64_t cap = 0;
     uint64_t rows = 0;            // rows inserted (= the table's first index space)
-    DBuf<uint32_t> rowmap;        // row -> global read index
+    DBuf<uint64_t> rowmap;        // row -> global read index (the table's first index is the row)
     // finish() / ss_ingest_export(): the extracted entries
     DBuf<uint64_t> fps, words, counts, first;
     DBuf<uint32_t> lens;
-    DBuf<uint32_t> xread;         // export: each entry's first read (engine-local index)
+    DBuf<uint64_t> xread;         // export: each entry's first read (engine-local index)
     uint64_t m = 0;
 };
 
@@ -482,7 +492,8 @@ struct ss_ingest {
     DBuf<uint8_t> rows;            // gathered dense rows (lengths <= 32)
     DBuf<uint64_t> cls_words;      // the length classes' packed rows (k_encode_classes / k_encode_class)
     DBuf<uint64_t> cls_fps;        // their fingerprints (k_encode_classes), class after class
-    DBuf<uint32_t> posof;          // per read: its place in d_order (k_len_scatter)
+    ss_counter* fpt = nullptr;     // the classes' rows counted by fingerprint (single-word scratch table)
+    DBuf<uint32_t> cls_flag;       // set by ss_classes_verify_fold: two keys share a fingerprint
     DBuf<uint32_t> hll;            // per class W: 2^kHllLog HyperLogLog registers over the call
     uint32_t* h_hll = nullptr;     // pinned copy
     DBuf<uint64_t> ovf;            // per job: its table's overflow word after the insert
@@ -502,6 +513,8 @@ struct ss_ingest {
     std::string bad_bytes;
     double est_scale = 1.0;        // FASTQ: file bytes / bytes seen (multi-word table sizing)
     bool exported = false;         // ss_ingest_export ran (the groups' m / buffers hold the entries)
+    uint64_t max_rows = 0xFFFFFFFFull;   // rows a group's table indexes (its first index is u32);
+                                         // ss_ingest_set_row_limit lowers it (test hook)
     // ss_ingest_merge scratch (this engine as the destination): a source group's entries on this device
     DBuf<uint64_t> mg_words, mg_counts, mg_first;
     DBuf<uint32_t> mg_lens;
@@ -587,9 +600,51 @@ int table_kind(const Group& gr, ss_counter* t) {
     return gr.L ? ss_counter_set_length(t, gr.L) : ss_counter_set_words(t, gr.W1);
 }
 
+// A group whose rows would pass the table's u32 first index (max_rows: 2^32 - 1 reads of one length
+// or class in one call) is re-keyed: its entries become its rows 0..K-1 (extract, then merge back
+// with first index = entry, the row map compacted to the entries' first reads), so one call counts
+// any number of reads (the row map holds u64 global read indices).
+int group_rekey(ss_ingest* g, Group& gr) {
+    hipStream_t s = g->stream;
+    const uint64_t cap = gr.cap + 1;
+    const uint32_t W = gr.W1;
+    int rc = g->scan.ensure(kScanBlocks + 2 + 2 * (uint64_t)kLenBins + 8);
+    if (rc || (rc = gr.fps.ensure(cap)) || (rc = gr.words.ensure(cap * W)) || (rc = gr.counts.ensure(cap)) ||
+        (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)))
+        return rc;
+    uint64_t* d_cnt = g->scan.p + kScanBlocks + 2;
+    rc = ss_counter_extract_words(gr.table, 1, gr.fps.p, gr.lens.p, gr.words.p, gr.counts.p, gr.first.p, cap, d_cnt, s);
+    if (!rc) rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 8, hipMemcpyDeviceToHost, s), "ingest rekey count");
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest rekey");
+    if (rc) return rc;
+    const uint64_t m = g->h_bad[0];
+    DBuf<uint64_t> nmap;
+    if ((rc = nmap.ensure(std::max<uint64_t>(m, gr.rows)))) return rc;
+    if (m)
+        hipLaunchKernelGGL(k_rekey, dim3(grid_of(m, 256)), dim3(256), 0, s, gr.first.p, m, gr.rowmap.p, nmap.p, gr.fps.p);
+    if ((rc = ss_counter_reset(gr.table, s)) || (rc = table_kind(gr, gr.table))) return rc;
+    rc = W == 1 ? ss_counter_merge(gr.table, gr.words.p, gr.lens.p, gr.counts.p, gr.fps.p, m, s)
+                : ss_counter_merge_words(gr.table, gr.words.p, gr.counts.p, gr.fps.p, m, s);
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest rekey merge");
+    if (rc) return rc;
+    gr.rowmap.release();
+    gr.rowmap = nmap;
+    nmap.p = nullptr;
+    nmap.cap = 0;
+    gr.rows = m;
+    return SS_OK;
+}
+
 // make room for m more rows in group gr (grow by extract + merge).  need: an upper bound of the
 // table's keys after them -- the rows so far (exact), or a class's distinct-key estimate
 int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
+    if (gr.table && gr.rows + m > g->max_rows) {
+        if (m > g->max_rows / 2) return ss_fail(SS_EARG, "ingest: a chunk's rows of one length exceed the row bound");
+        const int rc = group_rekey(g, gr);
+        if (rc) return rc;
+        need = std::min(need, gr.rows + m);
+        if (gr.rows + m > g->max_rows) return ss_fail(SS_EFULL, "ingest: a length's distinct keys exceed 2^32 - 1");
+    }
     if (gr.table && need <= gr.cap / 2) return SS_OK;
     if (!gr.table) {
         const double scale = gr.L || need < m ? 1.0 : g->est_scale;
@@ -639,9 +694,8 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (n == 0) return SS_OK;
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "ingest: a chunk holds < 2^32 reads");
-    // the row maps and first indices hold global read indices as u32
-    if (g->nreads + n > 0xFFFFFFFEull)
-        return ss_fail(SS_EARG, "ingest: one call counts fewer than 2^32 - 1 reads");
+    // global read indices are u64 (row maps); a table's first index is a row of its group, u32: a
+    // group about to pass kMaxRows rows is re-keyed first (group_room)
     hipStream_t s = g->stream;
     const uint64_t base = g->nreads;
     int rc = SS_OK;
@@ -654,15 +708,13 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (dense_L > SS_MAX_NT) return ss_fail(SS_EARG, "ingest: dense length > 1024");
         jobs.push_back({len_bin(dense_L), n, 0, 0});
     } else {
-        if ((rc = g->order.ensure(n)) || (rc = g->posof.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
+        if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins)))
             return rc;
         hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p, g->blkfirst.p);
         hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(256), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
                            g->split_out.p);
         hipLaunchKernelGGL(k_len_binstart, dim3(1), dim3(1024), 0, s, g->split_out.p);
-        hipLaunchKernelGGL(k_len_scatter, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p,
-                           (const uint64_t*)g->split_out.p, g->order.p, g->posof.p);
         rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, 3 * kLenBins * 8, hipMemcpyDeviceToHost, s),
                       "ingest split copy");
         if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest split");
@@ -708,12 +760,36 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         whi = std::max(whi, W);
     }
     uint64_t need_cls[33] = {0};
-    const bool fused = !dense_L && w1max && w1max <= 16;   // fingerprints come with the rows
+    const bool fused = !dense_L && w1max && w1max <= 16;   // fingerprints and row maps come with the rows
+    // the stable split into d_order: for the lengths 1..32 (row gathers) and the per-class passes; the
+    // fused class encode ranks its rows itself from k_len_binscan's per-block offsets
+    bool need_order = !dense_L && (!fused && w1max);
+    for (const Job& jb : jobs) need_order |= !dense_L && jb.bin <= 32;
+    if (need_order)
+        hipLaunchKernelGGL(k_len_scatter, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p,
+                           (const uint64_t*)g->split_out.p, g->order.p);
+    uint64_t* rmap[33] = {nullptr};
+    if (fused) {
+        // every class group's rows fit its table's u32 first index (re-keyed first otherwise) and its
+        // row map has room for the chunk's rows: the encode writes their read indices there
+        for (const Job& jb : jobs) {
+            if (jb.bin <= 32) continue;
+            Group& gr = g->groups[jb.bin];
+            gr.L = 0;
+            gr.W1 = jb.bin - kClassBin0 + 1;
+            if (gr.table && gr.rows + jb.m > g->max_rows) {
+                if (jb.m > g->max_rows / 2) return ss_fail(SS_EARG, "ingest: a chunk's rows of one length exceed the row bound");
+                if ((rc = group_rekey(g, gr))) return rc;
+            }
+            if ((rc = gr.rowmap.ensure_keep(gr.rows + jb.m, gr.rows, s))) return rc;
+            rmap[gr.W1 - 1] = gr.rowmap.p + gr.rows;
+        }
+    }
     if (w1max) {
         if ((rc = g->cls_words.ensure(cls_words))) return rc;
         if (fused && (rc = g->cls_fps.ensure(cls_rows))) return rc;
         if (fused) {                        // one read-order pass, the registers updated in it
-            rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->posof.p, g->split_out.p + 2 * kLenBins, woff, fpoff,
+            rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->blkhist.p, kSplitBlocks, woff, fpoff, rmap, base,
                                         kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + nj, s);
         } else {                            // a class per pass (longer reads, or a dense chunk)
             for (size_t j = 0; j < nj && !rc; ++j) {
@@ -744,8 +820,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     std::vector<size_t> cls_jobs;
     for (size_t j = 0; j < nj; ++j) {
         const Job& jb = jobs[j];
-        if (!live(jb)) continue;
         const bool cls = jb.bin > 32;
+        // (the fused classes are counted together: all of them, the call raises anyway when one lies
+        // past the first rejected read)
+        if (!live(jb) && !(cls && fused)) continue;
         Group& gr = g->groups[jb.bin];
         gr.L = cls ? 0u : jb.bin;
         gr.W1 = cls ? jb.bin - kClassBin0 + 1 : 1u;
@@ -772,7 +850,42 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, s, sel, jb.m, base, gr.rowmap.p + gr.rows);
         gr.rows += jb.m;
     }
-    if (!cls_jobs.empty()) {
+    std::vector<uint64_t> cls_base(nj, 0);     // each class job's first table row (the exact redo)
+    if (!cls_jobs.empty() && fused) {
+        // the classes' rows counted by fingerprint in one scratch table, checked against their
+        // fingerprints' first rows and folded into the class tables (ss_classes_verify_fold); a
+        // fingerprint shared by two keys sends the classes to the exact path below, after the sync
+        uint64_t need_all = 0;
+        std::vector<ss_class_rows> cr;
+        for (size_t j : cls_jobs) {
+            const Job& jb = jobs[j];
+            Group& gr = g->groups[jb.bin];
+            need_all += std::min<uint64_t>(jb.m, need_cls[gr.W1 - 1]);
+            cr.push_back({gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, gr.W1});
+        }
+        const uint64_t fcap = std::min<uint64_t>(1ull << 32, std::max<uint64_t>(1ull << 19, pow2_at_least(2 * need_all + 2)));
+        if (g->fpt && ss_counter_capacity(g->fpt) != fcap) {
+            (void)hipStreamSynchronize(s);
+            ss_counter_destroy(g->fpt);
+            g->fpt = nullptr;
+        }
+        if (!g->fpt && (rc = ss_counter_create(fcap, &g->fpt))) return rc;
+        if ((rc = ss_counter_reset(g->fpt, s))) return rc;
+        if ((rc = g->cls_flag.ensure(1))) return rc;
+        rc = ss_check(hipMemsetAsync(g->cls_flag.p, 0, 4, s), "ingest class flag reset");
+        if (!rc) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, cls_rows, 0, s);
+        if (!rc) rc = ss_classes_verify_fold(g->fpt, g->cls_fps.p, cr.data(), (uint32_t)cr.size(), g->cls_flag.p, s);
+        if (!rc) rc = ss_counter_overflow(g->fpt, g->ovf.p + nj, s);
+        for (size_t q = 0; q < cls_jobs.size() && !rc; ++q) {
+            const size_t j = cls_jobs[q];
+            const Job& jb = jobs[j];
+            Group& gr = g->groups[jb.bin];
+            cls_base[j] = gr.rows;
+            rc = ss_counter_overflow(gr.table, g->ovf.p + j, s);
+            gr.rows += jb.m;           // (their row map: written by the encode)
+        }
+        if (rc) return rc;
+    } else if (!cls_jobs.empty()) {
         // every table of a class job is sized, reset and its row map grown on the main stream above
         int used = 0;
         if (cls_jobs.size() > 1) rc = ss_check(hipEventRecord(g->ev_fork, s), "ingest fork");
@@ -789,10 +902,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                     used = k;
                 }
             }
-            if (!rc)
-                rc = fused ? ss_counter_insert_words_fp(gr.table, g->cls_words.p + woff[gr.W1 - 1], g->cls_fps.p + fpoff[gr.W1 - 1],
-                                                        jb.m, gr.rows, cs)
-                           : ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, cs);
+            if (!rc) rc = ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, cs);
             if (!rc) rc = ss_counter_overflow(gr.table, g->ovf.p + j, cs);
             if (rc) break;
             const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
@@ -811,17 +921,37 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         g->nreads += n;
         return SS_OK;
     }
-    // first-bad words and the class tables' overflow words back in one sync
+    // first-bad words, the class tables' overflow words (the scratch table's last) and the class
+    // fingerprint flag back in one sync
     uint64_t* hb = g->h_bad;
     rc = ss_check(hipMemcpyAsync(hb, g->first_bad.p, (nj + 1) * 8, hipMemcpyDeviceToHost, s), "ingest bad copy");
-    if (!rc) rc = ss_check(hipMemcpyAsync(hb + nj + 1, g->ovf.p, nj * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
+    if (!rc) rc = ss_check(hipMemcpyAsync(hb + nj + 1, g->ovf.p, (nj + 1) * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
+    if (!rc && fused && !cls_jobs.empty())
+        rc = ss_check(hipMemcpyAsync(hb + 2 * nj + 2, g->cls_flag.p, 4, hipMemcpyDeviceToHost, s), "ingest flag copy");
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest chunk");
     if (rc) return rc;
-    for (size_t j = 0; j < nj; ++j) {
-        if (!hb[nj + 1 + j]) continue;
+    for (size_t j = 0; j <= nj; ++j) {
+        if (!hb[nj + 1 + j] || (j == nj && !(fused && !cls_jobs.empty()))) continue;
         g->failed = true;
         return ss_fail(SS_EFULL, "ingest: a length class's table ran full (its distinct-key estimate was low); "
                                      "count again with ss_ingest_set_exact");
+    }
+    if (fused && !cls_jobs.empty() && (uint32_t)hb[2 * nj + 2]) {
+        // two keys share a fingerprint: the class tables were left untouched, count them exactly
+        for (size_t j : cls_jobs) {
+            Group& gr = g->groups[jobs[j].bin];
+            if ((rc = ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jobs[j].m, cls_base[j], s)) ||
+                (rc = ss_counter_overflow(gr.table, g->ovf.p + j, s)))
+                return rc;
+        }
+        rc = ss_check(hipMemcpyAsync(hb + nj + 1, g->ovf.p, nj * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest exact classes");
+        if (rc) return rc;
+        for (size_t j = 0; j < nj; ++j)
+            if (hb[nj + 1 + j]) {
+                g->failed = true;
+                return ss_fail(SS_EFULL, "ingest: a length class's table ran full; count again with ss_ingest_set_exact");
+            }
     }
     for (size_t j = 0; j <= nj; ++j) {
         const uint64_t fb = hb[j];
@@ -980,6 +1110,13 @@ int ss_ingest_reset(ss_ingest* g) {
     return ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
 }
 
+int ss_ingest_set_row_limit(ss_ingest* g, uint64_t rows) {
+    if (!g) return ss_fail(SS_EARG, "null ingest");
+    if (rows < 1024 || rows > 0xFFFFFFFFull) return ss_fail(SS_EARG, "row limit in 1024 .. 2^32 - 1");
+    g->max_rows = rows;
+    return SS_OK;
+}
+
 int ss_ingest_set_exact(ss_ingest* g, int exact) {
     if (!g) return ss_fail(SS_EARG, "null ingest");
     if (exact < 0 || exact > 2) return ss_fail(SS_EARG, "sizing mode 0, 1 or 2");
@@ -1005,7 +1142,10 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->fq_ws.release(), g->fq_aux.release(), g->fq_counts.release();
     g->slot.release(), g->ordered.release(), g->woff.release(), g->scan.release(), g->out_len.release();
     g->out_cnt.release(), g->out_words.release(), g->gdesc.release();
-    g->cls_words.release(), g->cls_fps.release(), g->posof.release(), g->hll.release(), g->ovf.release();
+    g->cls_words.release(), g->cls_fps.release(), g->hll.release(), g->ovf.release();
+    g->cls_flag.release();
+    if (g->fpt) ss_counter_destroy(g->fpt);
+    g->fpt = nullptr;
     g->mg_words.release(), g->mg_counts.release(), g->mg_first.release(), g->mg_lens.release();
     if (g->h_hll) (void)hipHostFree(g->h_hll);
     if (g->h_split) (void)hipHostFree(g->h_split);
@@ -1255,7 +1395,7 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     const uint64_t empty_at = g->empty_count ? g->empty_first : kNoSlot;
     if (g->empty_count)
         hipLaunchKernelGGL(k_mark, dim3(1), dim3(256), 0, s, (const uint64_t*)nullptr, (uint64_t)0,
-                           (const uint32_t*)nullptr, empty_at, bits);
+                           (const uint64_t*)nullptr, empty_at, bits);
     if ((rc = g->gdesc.ensure(desc.size() + 1))) return rc;
     if (!desc.empty())
         rc = ss_check(hipMemcpyAsync(g->gdesc.p, desc.data(), desc.size() * sizeof(GDesc), hipMemcpyHostToDevice, s),
@@ -1279,7 +1419,7 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
                            placed[q]->m, placed[q]->rowmap.p, (uint32_t)q, kNoSlot, bits, g->woff.p, g->ordered.p);
     if (g->empty_count)
         hipLaunchKernelGGL(k_rank, dim3(1), dim3(256), 0, s, (const uint64_t*)nullptr, (uint64_t)0,
-                           (const uint32_t*)nullptr, 0u, empty_at, bits, g->woff.p, g->ordered.p);
+                           (const uint64_t*)nullptr, 0u, empty_at, bits, g->woff.p, g->ordered.p);
     // word offsets of the ordered entries
     hipLaunchKernelGGL((k_scan_count<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->scan.p);
@@ -1336,8 +1476,6 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
     if (!src->exported) return ss_fail(SS_EARG, "ingest merge: ss_ingest_export the source first");
     if (dst->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (src_base < dst->nreads) return ss_fail(SS_EARG, "ingest merge: sources follow the destination's reads, in order");
-    if (src_base + src->nreads > 0xFFFFFFFEull)
-        return ss_fail(SS_EARG, "ingest: one call counts fewer than 2^32 - 1 reads");
     int rc = ss_check(hipSetDevice(dst->device), "ingest merge device");
     if (rc) return rc;
     const bool peer = src->device != dst->device;
@@ -1373,7 +1511,7 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
             break;
         // the source's entries cross to this device (xGMI peer copies; a plain copy on one device)
         if ((rc = copy(dst->mg_words.p, sg.words.p, m * gr.W1 * 8)) || (rc = copy(dst->mg_counts.p, sg.counts.p, m * 8)) ||
-            (rc = copy(dst->mg_lens.p, sg.lens.p, m * 4)) || (rc = copy(gr.rowmap.p + gr.rows, sg.xread.p, m * 4)))
+            (rc = copy(dst->mg_lens.p, sg.lens.p, m * 4)) || (rc = copy(gr.rowmap.p + gr.rows, sg.xread.p, m * 8)))
             break;
         hipLaunchKernelGGL(k_merge_rows, dim3(grid_of(m, 256)), dim3(256), 0, s, m, gr.rows, src_base,
                            dst->mg_first.p, gr.rowmap.p);

@@ -12,19 +12,38 @@ extern "C" int ss_encode_fixed_impl(const uint8_t* d_ascii, uint64_t n, uint32_t
                                     uint64_t* d_words, uint32_t wpr, uint64_t* d_first_bad,
                                     const uint64_t* d_ref_words, uint32_t* d_out, void* stream);
 // All multi-word classes of a chunk in one read-order pass (k_encode_classes; every class present has
-// W + 1 <= w1max <= 16 words): class W's rows at d_out + h_woff[W] (W = 2..32; row = d_posof[r] -
-// d_binstart[bin0 + W]), each row's fingerprint (words_fp over its W + 1 words) at
-// d_fps[h_fpoff[W] + row] when d_fps is given, and the classes' HyperLogLog registers
-// d_hll[W << kHllLog ...] (u32, max-updated; zeroed by the caller).
+// W + 1 <= w1max <= 16 words), over k_len_count's nblk block ranges: class W's rows at d_out + h_woff[W]
+// (W = 2..32; the block's first row of class W = d_blkoff[(bin0 + W) * nblk + block], k_len_binscan's
+// in-bin offsets; rows in read order), each row's fingerprint (words_fp over its W + 1 words) at
+// d_fps[h_fpoff[W] + row] when d_fps is given, its global read index (base + chunk read) at
+// h_rmap[W][row] when h_rmap[W] is given, and the classes' HyperLogLog registers d_hll[W << kHllLog
+// ...] (u32, max-updated; zeroed by the caller).
 constexpr uint32_t kHllLog = 11;
 extern "C" int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
-                                      const uint32_t* d_posof, const uint64_t* d_binstart, const uint64_t* h_woff,
-                                      const uint64_t* h_fpoff, uint32_t bin0, uint32_t w1max, uint64_t* d_out,
-                                      uint64_t* d_fps, uint32_t* d_hll, uint64_t* d_first_bad, void* stream);
-// ss_counter_insert_words with the rows' fingerprints already computed (d_fps[n], words_fp of each row,
-// e.g. by k_encode_classes): the partition passes read the 8-B fingerprints instead of hashing rows.
-extern "C" int ss_counter_insert_words_fp(struct ss_counter* c, const uint64_t* d_words, const uint64_t* d_fps,
-                                          uint64_t n, uint64_t base_index, void* stream);
+                                      const uint32_t* d_blkoff, uint32_t nblk, const uint64_t* h_woff,
+                                      const uint64_t* h_fpoff, uint64_t* const* h_rmap, uint64_t base, uint32_t bin0,
+                                      uint32_t w1max, uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll,
+                                      uint64_t* d_first_bad, void* stream);
+// Single-word keys already computed on the device (d_keys[n], any 64-bit values): counted with the
+// optimistic partitioned insert (12-B records, LDS aggregation) -- e.g. the class rows' fingerprints.
+extern "C" int ss_counter_insert_keys(ss_counter* c, const uint64_t* d_keys, uint64_t n, uint64_t base_index,
+                                      void* stream);
+// One length class of the drop-in engine's chunk for ss_classes_verify_fold: its table (set_words(W1)),
+// its m packed rows of W1 words, and the table's first row index for them.
+struct ss_class_rows {
+    ss_counter* table;
+    const uint64_t* rows;
+    uint64_t m;
+    uint64_t base;
+    uint32_t W1;
+};
+// After ss_counter_insert_keys(fpt, d_fps, sum of m, 0) over the classes' fingerprints (class after
+// class, in cls order): every row compared with its fingerprint's first row (a mismatch -- two keys
+// sharing a fingerprint -- sets *d_flag, zeroed by the caller) and, unless *d_flag, every fpt entry
+// folded into its class's table (count, first = base + row).  With *d_flag set the class tables are
+// untouched and the caller counts the classes on the exact multi-word path instead.
+extern "C" int ss_classes_verify_fold(ss_counter* fpt, const uint64_t* d_fps, const ss_class_rows* cls, uint32_t ncls,
+                                      uint32_t* d_flag, void* stream);
 // HyperLogLog registers (2^kHllLog u32 at d_hll) of m packed rows of W1 words, k_encode_classes' hash.
 extern "C" int ss_hll_rows_impl(const uint64_t* d_rows, uint64_t m, uint32_t W1, uint32_t* d_hll, void* stream);
 // Drop-in engine (ss_ingest), one multi-word length class: rows of W words + the length (k_encode_class).

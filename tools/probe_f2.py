@@ -3,7 +3,7 @@
 workload (50M reads of 50-150 nt): count (ss_ingest_add_device) vs results (ss_ingest_finish + copy
 back), per rep.  Run under `rocprofv3 --kernel-trace --stats` to set the kernel time beside it.
 
-    python tools/probe_f2.py [reps]
+    python tools/probe_f2.py [reps] [n] [Lmin] [Lmax]     (default 4 50000000 50 150)
 """
 import os
 import sys
@@ -18,8 +18,11 @@ import shortseq_amd.batch as B  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 50_000_000
+    lo = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+    hi = int(sys.argv[4]) if len(sys.argv) > 4 else 150
     dev = torch.device("cuda", 0)
-    blob, offs, lens = B.synth_ragged_pool_reads(50_000_000, 41, 42, 1 << 20, 50, 150, device=dev)
+    blob, offs, lens = B.synth_ragged_pool_reads(n, 41, 42, 1 << 20, lo, hi, device=dev)
     eng = B.DeviceIngest(dev)
     for r in range(reps):
         eng.reset()
