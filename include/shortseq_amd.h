@@ -356,8 +356,9 @@ int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_
  *                       256, at most half full); a table that still runs full makes the add call
  *                       return SS_EFULL, and the caller counts again with exact sizing (the drop-in
  *                       front does).  2 = size them by 1/64 of the sketch (a test hook that makes
- *                       the SS_EFULL path run).  New in this ABI version; the reference dict has no
- *                       sizing.
+ *                       the SS_EFULL path run).  3 = test hook: the classes' fingerprint count takes
+ *                       its exact fallback (as if two keys shared a 64-bit fingerprint).  New in this
+ *                       ABI version; the reference dict has no sizing.
  * ---------------------------------------------------------------------------------------------- */
 typedef struct ss_ingest ss_ingest;
 int ss_ingest_create(int device, ss_ingest** h_out);

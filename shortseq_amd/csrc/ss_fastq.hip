@@ -388,25 +388,30 @@ struct FqStage {
     uint32_t* tile_cnt;   // [t] newlines per tile
     uint32_t* tile_run;   // [t] start of the tile's run in pos
     uint32_t* tile_last;  // [t] position of the tile's last newline (kNone32: none staged)
+    uint32_t* tile_nul;   // [t] the tile's 1-KiB sub-blocks holding a NUL byte (bit b: bytes 1024 b ..)
     uint32_t* nul_cnt;    // NUL bytes seen (may exceed kNulCap)
     uint32_t* nul_pos;    // [kNulCap] their positions
 };
 
 __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ buf, uint64_t nbytes, FqStage st) {
     __shared__ uint64_t wtot[kFqT / 64][kFqU1 / 4];
-    __shared__ uint32_t s_run, s_cnt;
+    __shared__ uint32_t s_run, s_cnt, s_nul;
     __shared__ __attribute__((aligned(8))) uint16_t spos[kLdsPos];
     const uint64_t t0 = (uint64_t)blockIdx.x * kFqTile1;
+    if (threadIdx.x == 0) s_nul = 0;
     // the chunks live only until their newline masks are taken: 16 bits per chunk, two per VGPR
     uint32_t mk[kFqU1 / 2];
     bool nul = false;
+    uint32_t nsub = 0;     // the tile's 1-KiB sub-blocks with a NUL: chunk j of wave w lies in sub-block 4 j + w
     {
         uint4 x[kFqU1];
         load_chunks<kFqU1>(buf, nbytes, t0, x);
 #pragma unroll
         for (int j = 0; j < kFqU1; j += 2) {
             mk[j / 2] = nl_mask16(x[j]) | nl_mask16(x[j + 1]) << 16;
-            nul |= has_nul(x[j]) | has_nul(x[j + 1]);
+            const bool n0 = has_nul(x[j]), n1 = has_nul(x[j + 1]);
+            nul |= n0 | n1;
+            nsub |= (n0 ? 1u << (4 * j + (threadIdx.x >> 6)) : 0u) | (n1 ? 1u << (4 * (j + 1) + (threadIdx.x >> 6)) : 0u);
         }
     }
     // the wave's NUL verdict now: left to its use at the end, the compiler keeps the chunks live
@@ -425,6 +430,7 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
         cnt += (uint32_t)((total[k] & 0xFFFFu) + ((total[k] >> 16) & 0xFFFFu) + ((total[k] >> 32) & 0xFFFFu) +
                           (total[k] >> 48));
     const bool fixed = cnt <= kTileCap;    // block-uniform (the scan's totals)
+    if (any_nul && nsub) atomicOr(&s_nul, nsub);   // (s_nul zeroed before scan_packed's barrier)
     if (threadIdx.x == 0) {
         // the reservation's round trip overlaps the other waves' LDS staging below
         const uint32_t sh = blockIdx.x % kStageShards;
@@ -481,6 +487,7 @@ __global__ __launch_bounds__(kFqT) void k_fq_nlpos(const uint8_t* __restrict__ b
             put(s_run);
         }
     }
+    if (threadIdx.x == 0) st.tile_nul[blockIdx.x] = s_nul;   // written after the barrier above
     if (any_nul) {                         // rare: reload the lane's chunks (keeps them out of VGPRs)
 #pragma unroll 1
         for (int j = 0; j < kFqU1; ++j) {
@@ -541,8 +548,9 @@ __device__ __forceinline__ uint64_t start_before(const FqStage& st, uint64_t til
 
 // A sequence line [start, stop) (stop: its '\n', or the chunk end for an unterminated last line)
 // with a NUL byte: strlen stops at the first NUL (the k_fq_nulfix rule, applied as the line is
-// placed).  Only when the chunk holds NULs: a short list is searched, a long or overflowed one
-// sends the line to a byte scan.
+// placed).  Only when the chunk holds NULs: a short list is searched; with more, only the line's
+// 1-KiB sub-blocks that hold a NUL (k_fq_nlpos's per-tile masks) are byte-scanned, so a file with
+// a thousand stray NULs re-reads a few KiB around each, not every sequence line.
 constexpr uint32_t kNulListScan = 64;
 __device__ __forceinline__ uint32_t nul_len(const uint8_t* __restrict__ buf, const FqStage& st, uint32_t nulc,
                                             uint64_t start, uint64_t stop, uint32_t len) {
@@ -552,12 +560,16 @@ __device__ __forceinline__ uint32_t nul_len(const uint8_t* __restrict__ buf, con
             const uint64_t p = st.nul_pos[k];
             if (p >= start && p < first) first = p;
         }
-    } else {
-        for (uint64_t p = start; p < stop; ++p)
-            if (buf[p] == 0) {
-                first = p;
-                break;
-            }
+    } else if (stop > start) {
+        for (uint64_t sb = start >> 10; sb <= (stop - 1) >> 10 && first == stop; ++sb) {
+            if (!((st.tile_nul[sb >> 5] >> (sb & 31)) & 1u)) continue;
+            const uint64_t e = min(stop, (sb + 1) << 10);
+            for (uint64_t p = max(start, sb << 10); p < e; ++p)
+                if (buf[p] == 0) {
+                    first = p;
+                    break;
+                }
+        }
     }
     return first < stop ? fq_len(first - start) : len;
 }
@@ -842,6 +854,7 @@ int ss_fastq_index(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0, int at
 
 // one-pass workspace: tile_base u64 [t + 1] | group_base u64 [g + 1] | used u32 [64 x 32] | ovf u32,
 // nul_cnt u32, 2 pad u32 | nul_pos u32 [kNulCap] | tile_cnt u32 [t] | tile_run u32 [t] | tile_last u32 [t] |
+// tile_nul u32 [t] |
 // pos u16 [64 x region + t x kTileCap] (256-B aligned)
 inline uint64_t fq_tiles1(uint64_t nbytes) { return (nbytes + kFqTile1 - 1) / kFqTile1; }
 
@@ -854,7 +867,7 @@ inline uint64_t fq_region(uint64_t max_reads) {
 
 uint64_t ss_fastq_onepass_ws_bytes(uint64_t nbytes, uint64_t max_reads) {
     const uint64_t t = fq_tiles1(nbytes);
-    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 16 + 4ull * kNulCap + 12 * t +
+    return 8 * (t + 1) + 8 * (fq_groups(t) + 1) + 4ull * kStageShards * kShardStride + 16 + 4ull * kNulCap + 16 * t +
            2 * kStageShards * fq_region(max_reads) + 2ull * kTileCap * t + 256;
 }
 
@@ -878,8 +891,9 @@ int ss_fastq_index_onepass(const uint8_t* d_buf, uint64_t nbytes, uint64_t line0
     st.tile_cnt = st.nul_pos + kNulCap;
     st.tile_run = st.tile_cnt + t;
     st.tile_last = st.tile_run + t;
+    st.tile_nul = st.tile_last + t;
     // 256-B aligned: the fixed runs (4 KiB apart) are then 16-B aligned for k_fq_place's wide loads
-    st.pos = (uint16_t*)(((uintptr_t)(st.tile_last + t) + 255) & ~(uintptr_t)255);
+    st.pos = (uint16_t*)(((uintptr_t)(st.tile_nul + t) + 255) & ~(uintptr_t)255);
     st.region = fq_region(max_reads);
     static_assert((4 * (kStageShards * kShardStride + 4)) % 16 == 0, "one fill packet");
     rc = ss_check(hipMemsetAsync(st.used, 0, 4 * (kStageShards * kShardStride + 4), s), "fastq staging reset");

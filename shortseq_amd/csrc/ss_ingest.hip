@@ -249,6 +249,18 @@ __global__ __launch_bounds__(256) void k_merge_rows(uint64_t m, uint64_t rows, u
     }
 }
 
+// words the ordered output gives a class table's extracted entries: sum of ceil(L/32) over entries
+// e < *m (L = the entry's last key word) -> *total (zeroed by the caller)
+__global__ __launch_bounds__(256) void k_class_words(const uint64_t* __restrict__ words, uint32_t W1,
+                                                     const uint64_t* __restrict__ m, unsigned long long* total) {
+    uint64_t sum = 0;
+    const uint64_t n = *m;
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256)
+        sum += (words[e * W1 + W1 - 1] + 31) / 32;
+    for (int off = 32; off; off >>= 1) sum += (uint64_t)__shfl_xor((long long)sum, off);
+    if ((threadIdx.x & 63u) == 0 && sum) atomicAdd(total, (unsigned long long)sum);
+}
+
 // re-key: entry e of a group's table becomes row e (its first index), the new row map = the entry's
 // first read
 __global__ __launch_bounds__(256) void k_rekey(const uint64_t* __restrict__ first, uint64_t m,
@@ -467,7 +479,7 @@ struct Group {
     DBuf<uint64_t> fps, words, counts, first;
     DBuf<uint32_t> lens;
     DBuf<uint64_t> xread;         // export: each entry's first read (engine-local index)
-    uint64_t m = 0;
+    uint64_t m = 0, nw = 0;       // extracted entries, their output words
 };
 
 }  // namespace
@@ -872,7 +884,8 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (!g->fpt && (rc = ss_counter_create(fcap, &g->fpt))) return rc;
         if ((rc = ss_counter_reset(g->fpt, s))) return rc;
         if ((rc = g->cls_flag.ensure(1))) return rc;
-        rc = ss_check(hipMemsetAsync(g->cls_flag.p, 0, 4, s), "ingest class flag reset");
+        // (sizing mode 3, a test hook: the flag starts raised, as if two keys shared a fingerprint)
+        rc = ss_check(hipMemsetAsync(g->cls_flag.p, g->sizing == 3 ? 1 : 0, 4, s), "ingest class flag reset");
         if (!rc) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, cls_rows, 0, s);
         if (!rc) rc = ss_classes_verify_fold(g->fpt, g->cls_fps.p, cr.data(), (uint32_t)cr.size(), g->cls_flag.p, s);
         if (!rc) rc = ss_counter_overflow(g->fpt, g->ovf.p + nj, s);
@@ -991,12 +1004,16 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
 }
 
 // Every table of the engine extracted (entries of group q into its fps / words / counts / first /
-// lens buffers, gr.m entries), then their entry counts and overflow words back in one sync.
+// lens buffers, gr.m entries), then their entry counts, overflow words and output word totals
+// (gr.nw: ceil(L/32) summed over a class's entries; one per entry for a length 1..32) back in one
+// sync.
 int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
     hipStream_t s = g->stream;
-    int rc = g->scan.ensure(kScanBlocks + 2 + 2 * (uint64_t)kLenBins + 8);
+    int rc = g->scan.ensure(kScanBlocks + 2 + 3 * (uint64_t)kLenBins + 8);
     if (rc) return rc;
     uint64_t* d_cnt = g->scan.p + kScanBlocks + 2;
+    rc = ss_check(hipMemsetAsync(d_cnt, 0, 3 * (uint64_t)kLenBins * 8, s), "ingest word totals reset");
+    if (rc) return rc;
     for (auto& kv : g->groups) {
         Group& gr = kv.second;
         gr.m = 0;
@@ -1008,19 +1025,23 @@ int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
             (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)))
             return rc;
         rc = ss_counter_extract_words(gr.table, 1, gr.fps.p, gr.lens.p, gr.words.p, gr.counts.p, gr.first.p, cap,
-                                      d_cnt + 2 * q, s);
-        if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 2 * q + 1, s);
+                                      d_cnt + 3 * q, s);
+        if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 3 * q + 1, s);
         if (rc) return rc;
+        if (!gr.L)
+            hipLaunchKernelGGL(k_class_words, dim3(grid_of(gr.cap, 256, 1024)), dim3(256), 0, s, gr.words.p, gr.W1,
+                               (const uint64_t*)(d_cnt + 3 * q), (unsigned long long*)(d_cnt + 3 * q + 2));
         placed.push_back(&gr);
     }
     if (!placed.empty()) {
-        rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 2 * placed.size() * 8, hipMemcpyDeviceToHost, s), "ingest");
+        rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 3 * placed.size() * 8, hipMemcpyDeviceToHost, s), "ingest");
         if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest extract");
         if (rc) return rc;
     }
     for (size_t q = 0; q < placed.size(); ++q) {
-        if (g->h_bad[2 * q + 1]) return ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
-        placed[q]->m = g->h_bad[2 * q];
+        if (g->h_bad[3 * q + 1]) return ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
+        placed[q]->m = g->h_bad[3 * q];
+        placed[q]->nw = placed[q]->L ? placed[q]->m : g->h_bad[3 * q + 2];
     }
     return SS_OK;
 }
@@ -1072,7 +1093,7 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
     }
     if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming), "ingest event");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_split, 3 * kLenBins * 8, hipHostMallocDefault), "ingest pinned");
-    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_bad, (2 * kLenBins + 4) * 8, hipHostMallocDefault), "ingest pinned");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_bad, (3 * kLenBins + 8) * 8, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_hll, (33ull << kHllLog) * 4, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = g->hll.ensure(33ull << kHllLog);
     if (!rc) rc = ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
@@ -1119,7 +1140,7 @@ int ss_ingest_set_row_limit(ss_ingest* g, uint64_t rows) {
 
 int ss_ingest_set_exact(ss_ingest* g, int exact) {
     if (!g) return ss_fail(SS_EARG, "null ingest");
-    if (exact < 0 || exact > 2) return ss_fail(SS_EARG, "sizing mode 0, 1 or 2");
+    if (exact < 0 || exact > 3) return ss_fail(SS_EARG, "sizing mode 0 .. 3");
     g->sizing = exact;
     return SS_OK;
 }
@@ -1396,22 +1417,25 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     if (g->empty_count)
         hipLaunchKernelGGL(k_mark, dim3(1), dim3(256), 0, s, (const uint64_t*)nullptr, (uint64_t)0,
                            (const uint64_t*)nullptr, empty_at, bits);
-    if ((rc = g->gdesc.ensure(desc.size() + 1))) return rc;
+    // the entry and word totals came back with the extraction's sync: no sync until the results
+    uint64_t K = g->empty_count ? 1 : 0, NW = 0;
+    for (Group* gr : placed) {
+        K += gr->m;
+        NW += gr->nw;
+    }
+    if ((rc = g->gdesc.ensure(desc.size() + 1)) || (rc = g->ordered.ensure(K + 1)) ||
+        (rc = g->woff.ensure(std::max(K, NB) + 1)) || (rc = g->out_len.ensure(K + 1)) || (rc = g->out_cnt.ensure(K + 1)) ||
+        (rc = g->out_words.ensure(NW + 1)))
+        return rc;
     if (!desc.empty())
         rc = ss_check(hipMemcpyAsync(g->gdesc.p, desc.data(), desc.size() * sizeof(GDesc), hipMemcpyHostToDevice, s),
                       "ingest desc");
-    // marked reads before each read-map word (read order = dict order)
-    if (!rc) {
-        hipLaunchKernelGGL((k_scan_count<0>), dim3(kScanBlocks), dim3(256), 0, s, g->slot.p, NB, (const GDesc*)g->gdesc.p,
-                           g->scan.p);
-        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
-        rc = ss_check(hipMemcpyAsync(g->h_bad, g->scan.p + kScanBlocks, 8, hipMemcpyDeviceToHost, s), "ingest");
-        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest count");
-    }
     if (rc) return rc;
-    const uint64_t K = g->h_bad[0];
-    if ((rc = g->ordered.ensure(K + 1)) || (rc = g->woff.ensure(std::max(K, NB) + 1))) return rc;
-    // woff holds the read-map words' prefix first (it becomes the word offsets below)
+    // marked reads before each read-map word (read order = dict order); woff holds that prefix first
+    // (it becomes the word offsets below)
+    hipLaunchKernelGGL((k_scan_count<0>), dim3(kScanBlocks), dim3(256), 0, s, g->slot.p, NB, (const GDesc*)g->gdesc.p,
+                       g->scan.p);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<0>), dim3(kScanBlocks), dim3(256), 0, s, g->slot.p, NB, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p);
     for (size_t q = 0; q < placed.size(); ++q)
@@ -1426,12 +1450,6 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p);
-    rc = ss_check(hipMemcpyAsync(g->h_bad, g->scan.p + kScanBlocks, 8, hipMemcpyDeviceToHost, s), "ingest");
-    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest words");
-    if (rc) return rc;
-    const uint64_t NW = g->h_bad[0];
-    if ((rc = g->out_len.ensure(K + 1)) || (rc = g->out_cnt.ensure(K + 1)) || (rc = g->out_words.ensure(NW + 1)))
-        return rc;
     hipLaunchKernelGGL(k_gather_out, dim3(grid_of(K, 256)), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->woff.p, g->empty_count, g->out_len.p, g->out_cnt.p, g->out_words.p);
     // results -> pinned host: lens [K] u32 | pad | counts [K] u64 | words [NW] u64

@@ -202,6 +202,39 @@ def test_fastq_index_nul_list_overflow(gpu, oracle, onepass):
 
 
 @pytest.mark.gpu
+def test_fastq_index_onepass_scattered_nuls(gpu, oracle):
+    """~1,000 stray NULs over a 4-MB file (more than the short list, fewer than the NUL
+    list holds): only the lines overlapping a 1-KiB sub-block with a NUL are byte-scanned.  NULs in
+    sequence lines (first byte, inside, last byte), in headers and quality lines, and long lines that
+    cross sub-block and 32-KiB tile boundaries; the result equals the oracle's, whole and chunked."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(16)
+    parts = []
+    for i in range(20_000):
+        L = int(rng.integers(1, 400)) if i % 97 else 3000
+        seq = bytearray(rng.choice(np.frombuffer(b"ACGT", np.uint8), L).tobytes())
+        qual = bytearray(b"I" * L)
+        hdr = bytearray(b"@r%d" % i)
+        u = rng.random()
+        if u < 0.03:
+            seq[int(rng.choice([0, L // 2, L - 1]))] = 0
+        elif u < 0.04:
+            qual[int(rng.integers(0, L))] = 0
+        elif u < 0.05:
+            hdr[1] = 0
+        parts.append(bytes(hdr) + b"\n" + bytes(seq) + b"\n+\n" + bytes(qual) + b"\n")
+    data = b"".join(parts)
+    assert 100 < data.count(b"\x00") < 65_536
+    eo, el = oracle.fastq_index(data)
+    go, gl = _gpu_index(B, torch, gpu, data, onepass=True)
+    assert np.array_equal(go, eo) and np.array_equal(gl, el)
+    nls = [i + 1 for i in range(len(data)) if data[i] == 10 and i + 1 < len(data)]
+    go, gl = _gpu_index(B, torch, gpu, data, sorted(random.Random(17).sample(nls, 5)), onepass=True)
+    assert np.array_equal(go, eo) and np.array_equal(gl, el)
+
+
+@pytest.mark.gpu
 def test_gather_rows_gpu(gpu):
     import torch
     import shortseq_amd.batch as B

@@ -48,18 +48,19 @@ def test_encode_var_ragged_vs_oracle(gpu, oracle):
         assert not got[i, nw:].any()
 
 
-@pytest.mark.parametrize("exact", [False, True])
+@pytest.mark.parametrize("exact", [False, True, 3])
 @pytest.mark.parametrize("case", [(45, 46, 400, 50_000, 0, 6), (43, 44, 1 << 16, 200_000, 1, 300),
                                   (41, 42, 1 << 20, 300_000, 50, 150), (47, 48, 3000, 150_000, 33, 700)])
 def test_device_ingest_ragged_small(gpu, oracle, case, exact):
     """ss_ingest_add_device over a ragged device batch (two calls: global read indices continue)
     == the generator-derived rows (pinned to oracle.count); length-class tables sized by their
-    distinct-key sketch (default) or by their rows (exact); 33-700 nt takes the per-class encode."""
+    distinct-key sketch (default) or by their rows (exact); 33-700 nt takes the per-class encode;
+    3 (test hook): the classes' fingerprint count takes its exact multi-word fallback."""
     import shortseq_amd.batch as B
     seed, ps, U, n, lo, hi = case
     blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
     h = n // 3
-    eng = B.DeviceIngest(gpu, exact=exact)
+    eng = B.DeviceIngest(gpu, exact=exact) if exact != 3 else B.DeviceIngest(gpu, _sizing=3)
     try:
         eng.count(blob, offs[:h], lens[:h])
         eng.count(blob, offs[h:], lens[h:])
