@@ -399,22 +399,29 @@ __device__ __forceinline__ uint32_t nz_bytes(uint32_t m) {
     return ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
 }
 
-// 16 aligned bytes -> x: 16 codes (no alias carry), y: rejected-byte mask | bit-6-clear mask << 16
-// (both 0 on the common path: every byte a base with bit 6 set)
-__device__ __forceinline__ uint2 code_chunk(uint4 c) {
+// 16 aligned bytes -> their 16 codes (no alias carry); *odd != 0 when some byte is rejected or has
+// bit 6 clear (the rare path: chunk_masks then says which)
+__device__ __forceinline__ uint32_t code_chunk(const uint4& c, uint32_t& odd) {
     const uint32_t p0 = c.x & 0x06060606u, p1 = c.y & 0x06060606u, p2 = c.z & 0x06060606u, p3 = c.w & 0x06060606u;
-    const uint32_t m0 = (c.x & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p0);
-    const uint32_t m1 = (c.y & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p1);
-    const uint32_t m2 = (c.z & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p2);
-    const uint32_t m3 = (c.w & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p3);
-    uint2 r;
-    r.x = transpose2x4((p0 >> 1) | (p1 << 1) | (p2 << 3) | (p3 << 5));
-    r.y = 0;
-    if (m0 | m1 | m2 | m3) r.y = nz_bytes(m0) | nz_bytes(m1) << 4 | nz_bytes(m2) << 8 | nz_bytes(m3) << 12;
-    if ((c.x & c.y & c.z & c.w & 0x40404040u) != 0x40404040u)
-        r.y |= (nz_bytes(~c.x & 0x40404040u) | nz_bytes(~c.y & 0x40404040u) << 4 | nz_bytes(~c.z & 0x40404040u) << 8 |
-                nz_bytes(~c.w & 0x40404040u) << 12) << 16;
-    return r;
+    odd |= ((c.x & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p0)) |
+           ((c.y & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p1)) |
+           ((c.z & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p2)) |
+           ((c.w & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, p3)) |
+           (~(c.x & c.y & c.z & c.w) & 0x40404040u);
+    return transpose2x4((p0 >> 1) | (p1 << 1) | (p2 << 3) | (p3 << 5));
+}
+
+// rejected-byte mask | bit-6-clear byte mask << 16 of 16 aligned bytes
+__device__ __forceinline__ uint32_t chunk_masks(const uint4& c) {
+    const uint32_t x[4] = {c.x, c.y, c.z, c.w};
+    uint32_t bad = 0, al = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t m = (x[i] & 0x3F3F3F3Fu) ^ __builtin_amdgcn_perm(0x00070014u, 0x00030001u, x[i] & 0x06060606u);
+        bad |= nz_bytes(m) << (4 * i);
+        al |= nz_bytes(~x[i] & 0x40404040u) << (4 * i);
+    }
+    return bad | al << 16;
 }
 
 __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, const uint64_t* __restrict__ offs,
@@ -492,45 +499,66 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
             cbase[33] = c;
         }
         __syncthreads();
-        // b. lane per word slot, read order: the word's three aligned chunks encoded where they lie
+        // b. lane per word slot, read order: the word's three aligned chunks encoded where they lie;
+        //    two word slots per lane per round, their six chunk loads issued together (each code's
+        //    rare-path test was a branch between the loads: three serialized round trips per word,
+        //    3.37 ms on the f2 batch)
         const uint32_t Q = sqoff[kClsTile];
         const uint4* in16 = (const uint4*)in;
-        for (uint32_t q = t; q < Q; q += kClsTile) {
-            const uint32_t tt = smap[q];
-            const uint32_t LL = sL[tt], WW = (LL + 31u) / 32u, w = q - sqoff[tt];
-            uint32_t bad = 0;
-            uint64_t word = LL;
-            if (w < WW) {
-                const uint32_t nb = min(32u, LL - 32u * w);
-                const uint64_t ro = soff[tt];
-                const uint32_t sh = (uint32_t)(ro & 15u);
-                const uint32_t last = (sh + nb - 1u) >> 4;          // 0..2: the chunk holding the word's last byte
-                const uint64_t c0 = (ro >> 4) + 2u * w;
-                const uint2 a = code_chunk(in16[c0]);
-                const uint2 b = code_chunk(in16[c0 + min(1u, last)]);
-                const uint2 c = code_chunk(in16[c0 + min(2u, last)]);
-                const uint64_t lo64 = (uint64_t)b.x << 32 | a.x;
-                word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)c.x << (64u - 2u * sh)) : lo64;
-                if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
-                if ((a.y | b.y | c.y) != 0u) {      // rejected or bit-6-clear bytes somewhere in the chunks
-                    const uint64_t bytes = ((uint64_t)1 << nb) - 1ull;                  // nb <= 32
-                    const uint32_t by = last >= 1u ? b.y : 0u, cy = last >= 2u ? c.y : 0u;
-                    const uint64_t rej = ((uint64_t)(a.y & 0xFFFFu) | (uint64_t)(by & 0xFFFFu) << 16 |
-                                          (uint64_t)(cy & 0xFFFFu) << 32) >> sh;
-                    bad = (rej & bytes) != 0ull;
-                    const uint64_t al =
-                        ((uint64_t)(a.y >> 16) | (uint64_t)(by >> 16) << 16 | (uint64_t)(cy >> 16) << 32) >> sh;
-                    if (nb < 32u && (al & bytes)) {   // an aliased byte in a table-path word: its carry, exactly
-                        uint32_t b2 = 0;
-                        word = encode_word_q(in + ro + 32u * w, nb, true, b2);
-                        bad |= b2;
+        for (uint32_t q0 = t; q0 < Q; q0 += 2 * kClsTile) {
+            uint32_t tt[2], LL[2], WW[2], w[2], nb[2], sh[2], last[2];
+            uint64_t ro[2];
+            uint4 xa[2], xb[2], xc[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t q = min(q0 + k * kClsTile, Q - 1u);
+                tt[k] = smap[q];
+                LL[k] = sL[tt[k]];
+                WW[k] = (LL[k] + 31u) / 32u;
+                w[k] = q - sqoff[tt[k]];
+                const bool word = w[k] < WW[k];
+                nb[k] = word ? min(32u, LL[k] - 32u * w[k]) : 1u;
+                ro[k] = soff[tt[k]];
+                sh[k] = (uint32_t)(ro[k] & 15u);
+                last[k] = (sh[k] + nb[k] - 1u) >> 4;          // 0..2: the chunk holding the word's last byte
+                const uint64_t c0 = (ro[k] >> 4) + 2u * (word ? w[k] : 0u);
+                xa[k] = in16[c0];
+                xb[k] = in16[c0 + min(1u, last[k])];
+                xc[k] = in16[c0 + min(2u, last[k])];
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t q = q0 + k * kClsTile;
+                if (q >= Q) break;
+                uint32_t bad = 0;
+                uint64_t word = LL[k];
+                if (w[k] < WW[k]) {
+                    uint32_t odd = 0;
+                    const uint32_t ca = code_chunk(xa[k], odd), cb = code_chunk(xb[k], odd), cc = code_chunk(xc[k], odd);
+                    const uint64_t lo64 = (uint64_t)cb << 32 | ca;
+                    word = sh[k] ? (lo64 >> (2u * sh[k])) | ((uint64_t)cc << (64u - 2u * sh[k])) : lo64;
+                    if (nb[k] < 32u) word &= (1ull << (2u * nb[k])) - 1ull;
+                    if (odd) {      // rejected or bit-6-clear bytes somewhere in the chunks (FASTQ neighbours)
+                        const uint64_t bytes = ((uint64_t)1 << nb[k]) - 1ull;               // nb <= 32
+                        const uint32_t ay = chunk_masks(xa[k]), by = last[k] >= 1u ? chunk_masks(xb[k]) : 0u,
+                                       cy = last[k] >= 2u ? chunk_masks(xc[k]) : 0u;
+                        const uint64_t rej = ((uint64_t)(ay & 0xFFFFu) | (uint64_t)(by & 0xFFFFu) << 16 |
+                                              (uint64_t)(cy & 0xFFFFu) << 32) >> sh[k];
+                        bad = (rej & bytes) != 0ull;
+                        const uint64_t al =
+                            ((uint64_t)(ay >> 16) | (uint64_t)(by >> 16) << 16 | (uint64_t)(cy >> 16) << 32) >> sh[k];
+                        if (nb[k] < 32u && (al & bytes)) {   // an aliased byte in a table-path word: its carry, exactly
+                            uint32_t b2 = 0;
+                            word = encode_word_q(in + ro[k] + 32u * w[k], nb[k], true, b2);
+                            bad |= b2;
+                        }
                     }
                 }
+                const uint32_t at = cbase[WW[k]] + srow[tt[k]] * (WW[k] + 1u) + w[k];
+                sw[at] = word;
+                scls[at] = (uint8_t)WW[k];
+                report_bad(bad != 0u, r0 + tt[k], first_bad);
             }
-            const uint32_t at = cbase[WW] + srow[tt] * (WW + 1u) + w;
-            sw[at] = word;
-            scls[at] = (uint8_t)WW;
-            report_bad(bad != 0u, r0 + tt, first_bad);
         }
         __syncthreads();
         // c. the class spans out (dense), fingerprints, sketches, the rows' read indices

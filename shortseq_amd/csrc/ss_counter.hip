@@ -2436,6 +2436,13 @@ __global__ __launch_bounds__(256) void k_cls_verify_rep(Tbl f, ClsDesc d, const 
     const uint64_t n = d.row0[d.ncls];
     for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < n; g += (uint64_t)gridDim.x * 256) {
         const uint32_t c = cls_of(d, g);
+        const uint32_t W1 = d.W1[c];
+        // the row's words, its fingerprint and the home slot's representative all in flight together
+        // (clamped, unconditional loads: a branch between them serializes the round trips)
+        const uint64_t* a = d.rows[c] + (g - d.row0[c]) * W1;
+        uint64_t aw[kRepW1];
+#pragma unroll
+        for (uint32_t j = 0; j < kRepW1; ++j) aw[j] = a[min(j, W1 - 1)];
         const uint64_t fp = fps[g];
         const uint64_t top = slot_top(f, fp), base = top & ~f.slice_mask;
         uint64_t off = top & f.slice_mask;
@@ -2450,11 +2457,8 @@ __global__ __launch_bounds__(256) void k_cls_verify_rep(Tbl f, ClsDesc d, const 
                                         (uint64_t)e2.w << 32 | e2.z, (uint64_t)e3.y << 32 | e3.x,
                                         (uint64_t)e3.w << 32 | e3.z};
                 bad = (uint32_t)rw[6] != c;
-                const uint32_t W1 = d.W1[c];
-                const uint64_t* a = d.rows[c] + (g - d.row0[c]) * W1;
 #pragma unroll
-                for (uint32_t j = 0; j < kRepW1; ++j)
-                    if (j < W1) bad |= a[j] != rw[j];
+                for (uint32_t j = 0; j < kRepW1; ++j) bad |= j < W1 && aw[j] != rw[j];
                 break;
             }
             if (key == kEmpty) break;
