@@ -5,7 +5,8 @@
 #   scripts/gpu.sh pytest <secs> <pytest selection...>           -m gpu tests, log gpurun_out/pytest_<TAG>.log
 #   scripts/gpu.sh ab <rounds> "<args>" <tool_a> <tool_b> ...    interleaved same-box runs of tuner binaries
 #   scripts/gpu.sh abprof <rounds> "<args>" <regex> <tool>...    the same under rocprofv3 kernel stats (kernels ~ regex)
-#   scripts/gpu.sh libab <rounds> "<python cmd>"                 in-tree libshortseq_amd.so vs libshortseq_amd_old.so
+#   scripts/gpu.sh libab <rounds> "<python cmd>" [variants..]    in-tree libshortseq_amd.so ("new") vs
+#                                                                libshortseq_amd_<v>.so (default: old new)
 #   scripts/gpu.sh prof <name> <regex> -- <cmd...>               rocprofv3 kernel-trace summary of one command
 #   scripts/gpu.sh pmc <name> "<counters>" -- <cmd...>           one rocprofv3 --pmc pass (kernel rows grouped)
 #   scripts/gpu.sh full                                          whole GPU suite, then the default bench line
@@ -56,11 +57,12 @@ abprof)
     done
   done ;;
 libab)
-  rounds=$1; cmd=$2
+  rounds=$1; cmd=$2; shift 2
+  vs=${*:-old new}
   L=shortseq_amd/lib
   cp $L/libshortseq_amd.so $L/libshortseq_amd_new.so
   for r in $(seq 1 "$rounds"); do
-    for v in old new; do
+    for v in $vs; do
       cp $L/libshortseq_amd_$v.so $L/libshortseq_amd.so
       echo "== round $r $v: $(timeout -k 10 300 $cmd 2>&1 | tail -1)" | tee -a gpurun_out/libab_$TAG.log
     done

@@ -424,7 +424,9 @@ __device__ __forceinline__ uint32_t chunk_masks(const uint4& c) {
     return bad | al << 16;
 }
 
-__global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, const uint64_t* __restrict__ offs,
+// 6 waves per SIMD: left to itself the compiler spent 117-151 VGPRs (4 or 3 waves) on a kernel that
+// waits on memory two thirds of its cycles (SQ_WAIT_ANY / SQ_WAVE_CYCLES)
+__global__ __launch_bounds__(kClsTile) __attribute__((amdgpu_waves_per_eu(6))) void k_encode_classes(const uint8_t* in, const uint64_t* __restrict__ offs,
                                                              const uint32_t* __restrict__ lens, uint64_t n,
                                                              const uint32_t* __restrict__ blkoff, uint32_t nblk,
                                                              ClassOut co, uint32_t w1max, uint64_t* __restrict__ out,
@@ -436,23 +438,35 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
     uint64_t* sw = (uint64_t*)dyn;                          // [nslot] the tile's class spans, class after class
     uint8_t* scls = (uint8_t*)(sw + nslot);                 // [nslot] span slot -> its class
     uint8_t* smap = scls + nslot;                           // [nslot] word slot -> read of the tile
+    uint16_t* sodd = (uint16_t*)(smap + nslot);             // [nslot] word slots left to the exact re-encode
     __shared__ uint64_t soff[kClsTile];
     __shared__ uint32_t srow[kClsTile];                     // row within the tile's span of its class
     __shared__ uint16_t sqoff[kClsTile + 1], sL[kClsTile];
-    __shared__ uint32_t wcnt[kWaves][33], tcnt[33], cur[33], cbase[34], wsum[kWaves];
+    __shared__ uint32_t wcnt[kWaves][33], tcnt[33], cur[33], cbase[34], wsum[kWaves], nodd;
     const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
     // this block's read range: k_len_count's (its class rows start at the binscan's offsets)
     const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
     const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
     if (t < 33) cur[t] = t >= 2 ? blkoff[(uint64_t)(co.bin0 + t) * nblk + blockIdx.x] : 0u;
+    // loads carried across tiles, off the tile's chain of round trips: the next tile's length and
+    // offset (issued in phase c), and the previous tile's sketch register (checked one tile later)
+    uint32_t nL0 = 0;
+    uint64_t noff = 0;
+    if (lo < hi) {
+        const uint64_t rc = min(lo + t, n - 1);
+        nL0 = lens[rc];
+        noff = offs[rc];
+    }
+    uint32_t* hreg = nullptr;
+    uint32_t hrho = 0, hval = 0;
     for (uint64_t r0 = lo; r0 < hi; r0 += kClsTile) {
         const uint64_t r = r0 + t;
         // a. classes, rows (stable: the wave's lanes ranked by ballot, the waves in order), word slots
-        const uint64_t rc = min(r, n - 1);
-        const uint32_t L0 = lens[rc];
-        const uint64_t off = offs[rc];
+        const uint32_t L0 = nL0;
+        const uint64_t off = noff;
         for (uint32_t i = t; i < kWaves * 33; i += kClsTile) (&wcnt[0][0])[i] = 0;
+        if (t == 0) nodd = 0;
         __syncthreads();
         const uint32_t L = r < hi ? L0 : 0u;
         const bool cls = L > 32u && L <= SS_MAX_NT;
@@ -499,83 +513,73 @@ __global__ __launch_bounds__(kClsTile) void k_encode_classes(const uint8_t* in, 
             cbase[33] = c;
         }
         __syncthreads();
-        // b. lane per word slot, read order: the word's three aligned chunks encoded where they lie;
-        //    two word slots per lane per round, their six chunk loads issued together (each code's
-        //    rare-path test was a branch between the loads: three serialized round trips per word,
-        //    3.37 ms on the f2 batch)
+        // b. lane per word slot, read order: the word's three aligned chunks encoded where they lie,
+        //    the three loads issued together.  A word whose chunks hold a rejected or bit-6-clear byte
+        //    anywhere (an invalid base, an alias, or -- in a FASTQ chunk -- the newline and quality
+        //    bytes around a read) goes to a list and is re-encoded exactly after the pass
+        //    (encode_word_q: the byte-realigning form, table semantics for a partial tail word); kept
+        //    out of this loop, its registers would set the kernel's occupancy
         const uint32_t Q = sqoff[kClsTile];
         const uint4* in16 = (const uint4*)in;
-        for (uint32_t q0 = t; q0 < Q; q0 += 2 * kClsTile) {
-            uint32_t tt[2], LL[2], WW[2], w[2], nb[2], sh[2], last[2];
-            uint64_t ro[2];
-            uint4 xa[2], xb[2], xc[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t q = min(q0 + k * kClsTile, Q - 1u);
-                tt[k] = smap[q];
-                LL[k] = sL[tt[k]];
-                WW[k] = (LL[k] + 31u) / 32u;
-                w[k] = q - sqoff[tt[k]];
-                const bool word = w[k] < WW[k];
-                nb[k] = word ? min(32u, LL[k] - 32u * w[k]) : 1u;
-                ro[k] = soff[tt[k]];
-                sh[k] = (uint32_t)(ro[k] & 15u);
-                last[k] = (sh[k] + nb[k] - 1u) >> 4;          // 0..2: the chunk holding the word's last byte
-                const uint64_t c0 = (ro[k] >> 4) + 2u * (word ? w[k] : 0u);
-                xa[k] = in16[c0];
-                xb[k] = in16[c0 + min(1u, last[k])];
-                xc[k] = in16[c0 + min(2u, last[k])];
+        for (uint32_t q = t; q < Q; q += kClsTile) {
+            const uint32_t tt = smap[q];
+            const uint32_t LL = sL[tt], WW = (LL + 31u) / 32u, w = q - sqoff[tt];
+            const uint32_t at = cbase[WW] + srow[tt] * (WW + 1u) + w;
+            uint64_t word = LL;
+            if (w < WW) {
+                const uint64_t ro = soff[tt];
+                const uint32_t nb = min(32u, LL - 32u * w), sh = (uint32_t)(ro & 15u);
+                const uint32_t last = (sh + nb - 1u) >> 4;       // 0..2: the chunk holding the word's last byte
+                const uint64_t c0 = (ro >> 4) + 2u * w;
+                const uint4 xa = in16[c0], xb = in16[c0 + min(1u, last)], xc = in16[c0 + min(2u, last)];
+                uint32_t odd = 0;
+                const uint32_t ca = code_chunk(xa, odd), cb = code_chunk(xb, odd), cc = code_chunk(xc, odd);
+                const uint64_t lo64 = (uint64_t)cb << 32 | ca;
+                word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)cc << (64u - 2u * sh)) : lo64;
+                if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
+                if (odd) sodd[atomicAdd(&nodd, 1u)] = (uint16_t)q;
             }
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t q = q0 + k * kClsTile;
-                if (q >= Q) break;
-                uint32_t bad = 0;
-                uint64_t word = LL[k];
-                if (w[k] < WW[k]) {
-                    uint32_t odd = 0;
-                    const uint32_t ca = code_chunk(xa[k], odd), cb = code_chunk(xb[k], odd), cc = code_chunk(xc[k], odd);
-                    const uint64_t lo64 = (uint64_t)cb << 32 | ca;
-                    word = sh[k] ? (lo64 >> (2u * sh[k])) | ((uint64_t)cc << (64u - 2u * sh[k])) : lo64;
-                    if (nb[k] < 32u) word &= (1ull << (2u * nb[k])) - 1ull;
-                    if (odd) {      // rejected or bit-6-clear bytes somewhere in the chunks (FASTQ neighbours)
-                        const uint64_t bytes = ((uint64_t)1 << nb[k]) - 1ull;               // nb <= 32
-                        const uint32_t ay = chunk_masks(xa[k]), by = last[k] >= 1u ? chunk_masks(xb[k]) : 0u,
-                                       cy = last[k] >= 2u ? chunk_masks(xc[k]) : 0u;
-                        const uint64_t rej = ((uint64_t)(ay & 0xFFFFu) | (uint64_t)(by & 0xFFFFu) << 16 |
-                                              (uint64_t)(cy & 0xFFFFu) << 32) >> sh[k];
-                        bad = (rej & bytes) != 0ull;
-                        const uint64_t al =
-                            ((uint64_t)(ay >> 16) | (uint64_t)(by >> 16) << 16 | (uint64_t)(cy >> 16) << 32) >> sh[k];
-                        if (nb[k] < 32u && (al & bytes)) {   // an aliased byte in a table-path word: its carry, exactly
-                            uint32_t b2 = 0;
-                            word = encode_word_q(in + ro[k] + 32u * w[k], nb[k], true, b2);
-                            bad |= b2;
-                        }
-                    }
-                }
-                const uint32_t at = cbase[WW[k]] + srow[tt[k]] * (WW[k] + 1u) + w[k];
-                sw[at] = word;
-                scls[at] = (uint8_t)WW[k];
-                report_bad(bad != 0u, r0 + tt[k], first_bad);
-            }
+            sw[at] = word;
+            scls[at] = (uint8_t)WW;
         }
         __syncthreads();
+        if (nodd) {     // block-uniform
+            for (uint32_t k = t; k < nodd; k += kClsTile) {
+                const uint32_t q = sodd[k], tt = smap[q];
+                const uint32_t LL = sL[tt], WW = (LL + 31u) / 32u, w = q - sqoff[tt];
+                const uint32_t nb = min(32u, LL - 32u * w);
+                uint32_t bad = 0;
+                sw[cbase[WW] + srow[tt] * (WW + 1u) + w] = encode_word_q(in + soff[tt] + 32u * w, nb, nb < 32u, bad);
+                if (bad) atomicMin(first_bad, (unsigned long long)(r0 + tt));
+            }
+            __syncthreads();
+        }
         // c. the class spans out (dense), fingerprints, sketches, the rows' read indices
         for (uint32_t q = t; q < Q; q += kClsTile) {
             const uint32_t c = scls[q];
             out[co.woff[c] + (uint64_t)cur[c] * (c + 1u) + (q - cbase[c])] = sw[q];
         }
+        if (r0 + kClsTile < hi) {
+            const uint64_t rc = min(r + kClsTile, n - 1);
+            nL0 = lens[rc];
+            noff = offs[rc];
+        }
+        if (hreg && hval < hrho) atomicMax(hreg, hrho);     // registers settle early: most reads only load
+        hreg = nullptr;
         if (cls) {
             const uint32_t row = cur[W] + srow[t];
             const uint64_t fp = words_fp(sw + cbase[W] + srow[t] * w1, w1);
             if (fps) fps[co.fpoff[W] + row] = fp;
             if (co.rmap[W]) co.rmap[W][row] = co.base + r;
-            hll_add(hll + ((uint64_t)W << kHllLog), fp, w1);
+            const uint64_t h = splitmix64(fp ^ w1);       // hll_add's register and rank
+            hreg = hll + ((uint64_t)W << kHllLog) + (uint32_t)(h >> (64 - kHllLog));
+            hrho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
+            hval = *hreg;
         }
         __syncthreads();
         if (t < 33) cur[t] += tcnt[t];
     }
+    if (hreg && hval < hrho) atomicMax(hreg, hrho);
 }
 
 // The same registers from rows already packed (k_encode_class's paths): lane per row, the same hash.
@@ -1214,7 +1218,7 @@ int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const u
     }
     co.base = base;
     co.bin0 = bin0;
-    const size_t lds = (size_t)kClsTile * w1max * 10;
+    const size_t lds = (size_t)kClsTile * w1max * 12;
     hipLaunchKernelGGL(k_encode_classes, dim3(nblk), dim3(kClsTile), lds, (hipStream_t)stream, d_buf, d_offs, d_lens, n,
                        d_blkoff, nblk, co, w1max, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_classes");

@@ -2434,35 +2434,58 @@ __global__ __launch_bounds__(256) void k_cls_reps(Tbl f, ClsDesc d, uint64_t* __
 __global__ __launch_bounds__(256) void k_cls_verify_rep(Tbl f, ClsDesc d, const uint64_t* __restrict__ fps,
                                                         const uint64_t* __restrict__ rep, uint32_t* __restrict__ flag) {
     const uint64_t n = d.row0[d.ncls];
-    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < n; g += (uint64_t)gridDim.x * 256) {
-        const uint32_t c = cls_of(d, g);
-        const uint32_t W1 = d.W1[c];
-        // the row's words, its fingerprint and the home slot's representative all in flight together
-        // (clamped, unconditional loads: a branch between them serializes the round trips)
-        const uint64_t* a = d.rows[c] + (g - d.row0[c]) * W1;
-        uint64_t aw[kRepW1];
+    const uint64_t G = (uint64_t)gridDim.x * 256;
+    // two rows per lane per round: both rows' words and fingerprints, then both home slots'
+    // representatives, in flight together (clamped, unconditional loads: a branch between them
+    // serializes the round trips, and a lane's rounds are the kernel's critical path)
+    for (uint64_t g0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; g0 < n; g0 += 2 * G) {
+        uint32_t c[2], W1[2];
+        uint64_t aw[2][kRepW1], fp[2], base[2], off[2];
+        uint4 e[2][4];
 #pragma unroll
-        for (uint32_t j = 0; j < kRepW1; ++j) aw[j] = a[min(j, W1 - 1)];
-        const uint64_t fp = fps[g];
-        const uint64_t top = slot_top(f, fp), base = top & ~f.slice_mask;
-        uint64_t off = top & f.slice_mask;
-        bool bad = true;
-        for (uint64_t probe = 0; probe <= f.slice_mask; ++probe) {
-            const uint4* e = (const uint4*)(rep + (base + off) * 8);
-            const uint4 e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
-            const uint64_t key = (uint64_t)e0.y << 32 | e0.x;
-            if (key == fp) {
-                const uint64_t rw[7] = {(uint64_t)e0.w << 32 | e0.z, (uint64_t)e1.y << 32 | e1.x,
-                                        (uint64_t)e1.w << 32 | e1.z, (uint64_t)e2.y << 32 | e2.x,
-                                        (uint64_t)e2.w << 32 | e2.z, (uint64_t)e3.y << 32 | e3.x,
-                                        (uint64_t)e3.w << 32 | e3.z};
-                bad = (uint32_t)rw[6] != c;
+        for (int k = 0; k < 2; ++k) {
+            const uint64_t g = min(g0 + k * G, n - 1);
+            c[k] = cls_of(d, g);
+            W1[k] = d.W1[c[k]];
+            const uint64_t* a = d.rows[c[k]] + (g - d.row0[c[k]]) * W1[k];
 #pragma unroll
-                for (uint32_t j = 0; j < kRepW1; ++j) bad |= j < W1 && aw[j] != rw[j];
-                break;
+            for (uint32_t j = 0; j < kRepW1; ++j) aw[k][j] = a[min(j, W1[k] - 1)];
+            fp[k] = fps[g];
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint64_t top = slot_top(f, fp[k]);
+            base[k] = top & ~f.slice_mask;
+            off[k] = top & f.slice_mask;
+            const uint4* p = (const uint4*)(rep + (base[k] + off[k]) * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[k][j] = p[j];
+        }
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            bool b = true;
+            for (uint64_t probe = 0; probe <= f.slice_mask; ++probe) {
+                if (probe) {        // the home slot held another key: linear probing continues (rare)
+                    off[k] = (off[k] + 1) & f.slice_mask;
+                    const uint4* p = (const uint4*)(rep + (base[k] + off[k]) * 8);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) e[k][j] = p[j];
+                }
+                const uint64_t key = (uint64_t)e[k][0].y << 32 | e[k][0].x;
+                if (key == fp[k]) {
+                    const uint64_t rw[7] = {(uint64_t)e[k][0].w << 32 | e[k][0].z, (uint64_t)e[k][1].y << 32 | e[k][1].x,
+                                            (uint64_t)e[k][1].w << 32 | e[k][1].z, (uint64_t)e[k][2].y << 32 | e[k][2].x,
+                                            (uint64_t)e[k][2].w << 32 | e[k][2].z, (uint64_t)e[k][3].y << 32 | e[k][3].x,
+                                            (uint64_t)e[k][3].w << 32 | e[k][3].z};
+                    b = (uint32_t)rw[6] != c[k];
+#pragma unroll
+                    for (uint32_t j = 0; j < kRepW1; ++j) b |= j < W1[k] && aw[k][j] != rw[j];
+                    break;
+                }
+                if (key == kEmpty) break;
             }
-            if (key == kEmpty) break;
-            off = (off + 1) & f.slice_mask;
+            bad |= b && g0 + k * G < n;
         }
         if (__ballot(bad) && bad) atomicOr(flag, 1u);
     }

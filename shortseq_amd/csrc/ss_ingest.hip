@@ -249,18 +249,6 @@ __global__ __launch_bounds__(256) void k_merge_rows(uint64_t m, uint64_t rows, u
     }
 }
 
-// words the ordered output gives a class table's extracted entries: sum of ceil(L/32) over entries
-// e < *m (L = the entry's last key word) -> *total (zeroed by the caller)
-__global__ __launch_bounds__(256) void k_class_words(const uint64_t* __restrict__ words, uint32_t W1,
-                                                     const uint64_t* __restrict__ m, unsigned long long* total) {
-    uint64_t sum = 0;
-    const uint64_t n = *m;
-    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256)
-        sum += (words[e * W1 + W1 - 1] + 31) / 32;
-    for (int off = 32; off; off >>= 1) sum += (uint64_t)__shfl_xor((long long)sum, off);
-    if ((threadIdx.x & 63u) == 0 && sum) atomicAdd(total, (unsigned long long)sum);
-}
-
 // re-key: entry e of a group's table becomes row e (its first index), the new row map = the entry's
 // first read
 __global__ __launch_bounds__(256) void k_rekey(const uint64_t* __restrict__ first, uint64_t m,
@@ -1004,9 +992,9 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
 }
 
 // Every table of the engine extracted (entries of group q into its fps / words / counts / first /
-// lens buffers, gr.m entries), then their entry counts, overflow words and output word totals
-// (gr.nw: ceil(L/32) summed over a class's entries; one per entry for a length 1..32) back in one
-// sync.
+// lens buffers, gr.m entries), then their entry counts and overflow words back in one sync; the
+// output word total gr.nw follows from the count (one word per entry for a length 1..32, W1 - 1 for
+// a class table).
 int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
     hipStream_t s = g->stream;
     int rc = g->scan.ensure(kScanBlocks + 2 + 3 * (uint64_t)kLenBins + 8);
@@ -1028,9 +1016,6 @@ int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
                                       d_cnt + 3 * q, s);
         if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 3 * q + 1, s);
         if (rc) return rc;
-        if (!gr.L)
-            hipLaunchKernelGGL(k_class_words, dim3(grid_of(gr.cap, 256, 1024)), dim3(256), 0, s, gr.words.p, gr.W1,
-                               (const uint64_t*)(d_cnt + 3 * q), (unsigned long long*)(d_cnt + 3 * q + 2));
         placed.push_back(&gr);
     }
     if (!placed.empty()) {
@@ -1041,7 +1026,8 @@ int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
     for (size_t q = 0; q < placed.size(); ++q) {
         if (g->h_bad[3 * q + 1]) return ss_fail(SS_EFULL, "ingest: a length's counter table overflowed");
         placed[q]->m = g->h_bad[3 * q];
-        placed[q]->nw = placed[q]->L ? placed[q]->m : g->h_bad[3 * q + 2];
+        // a class table keys W = W1 - 1 words for every entry (its lengths are 32(W-1)+1 .. 32W)
+        placed[q]->nw = placed[q]->L ? placed[q]->m : placed[q]->m * (placed[q]->W1 - 1);
     }
     return SS_OK;
 }
