@@ -582,6 +582,93 @@ __global__ __launch_bounds__(kClsTile) __attribute__((amdgpu_waves_per_eu(6))) v
     if (hreg && hval < hrho) atomicMax(hreg, hrho);
 }
 
+// Drop-in engine, a chunk whose reads are all class reads of at most S - 1 words (S <= 6): every
+// read's row in READ order at a fixed stride of S words -- its W words, its length, zeros -- so no
+// class ranks, no LDS staging, no barriers and no row map (the row of read r is r).  A wave holds
+// R = 64 / S reads per group, S lanes each (lane w: word w, the length at w == W, 0 past it), and
+// kRowsK groups: the groups' length / offset loads, then their chunk loads, go out together (one
+// group per wave measured 3.35 ms on the f2 batch: three dependent round trips for 1 KB of input).
+// The words are k_encode_classes' phase b (16-B chunk loads, funnel shift, the rare odd word
+// re-encoded exactly).  The row fingerprint (words_fp over the W + 1 words) is folded across the
+// read's lanes with shuffles; lane 0 of the read stores it and updates its class's sketch.  Reads
+// that are not class reads (empty: the length split counts those) get a zero row and the
+// fingerprint of one zero word, an entry the fold skips.
+constexpr int kRowsK = 4;
+__global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const uint64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ lens, uint64_t n, uint32_t S,
+                                                     uint64_t* __restrict__ out, uint64_t* __restrict__ fps,
+                                                     uint32_t* hll, unsigned long long* first_bad) {
+    const uint32_t lane = threadIdx.x & 63u, R = 64u / S;
+    const uint32_t i = lane / S, w = lane - i * S;
+    const uint64_t r0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * R * kRowsK + i;
+    const uint4* in16 = (const uint4*)in;
+    uint32_t L[kRowsK];
+    uint64_t off[kRowsK];
+#pragma unroll
+    for (int k = 0; k < kRowsK; ++k) {
+        const uint64_t r = r0 + (uint64_t)k * R;
+        const uint64_t rc = (i < R && r < n) ? r : 0;
+        L[k] = (i < R && r < n) ? lens[rc] : 0u;
+        off[k] = offs[rc];
+    }
+    uint4 xa[kRowsK], xb[kRowsK], xc[kRowsK];
+#pragma unroll
+    for (int k = 0; k < kRowsK; ++k) {
+        // clamped, unconditional loads: a lane with no word of its read reloads the read's first
+        // chunk, one of an empty read (its offset may be the blob's end) the blob's first
+        const uint32_t W = (L[k] + 31u) / 32u;
+        const uint32_t ww = w < W ? w : 0u;
+        const uint32_t nb = L[k] ? min(32u, L[k] - 32u * ww) : 1u, sh = (uint32_t)(off[k] & 15u);
+        const uint32_t last = L[k] ? (sh + nb - 1u) >> 4 : 0u;
+        const uint64_t c0 = L[k] ? (off[k] >> 4) + 2u * ww : 0u;
+        xa[k] = in16[c0];
+        xb[k] = in16[c0 + min(1u, last)];
+        xc[k] = in16[c0 + min(2u, last)];
+    }
+    __shared__ uint64_t srow[4][kRowsK * 64];     // the wave's rows (group k: lanes k * 64 ..)
+    __shared__ uint16_t slen[4][kRowsK * 24];     // the wave's reads' lengths (read j = k * R + i; R <= 21)
+    const uint32_t wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kRowsK; ++k) {
+        const uint64_t r = r0 + (uint64_t)k * R;
+        const bool live = i < R && r < n;
+        const uint32_t W = (L[k] + 31u) / 32u;
+        const bool cls = L[k] > 32u && W < S;
+        uint64_t word = 0;
+        uint32_t bad = 0;
+        if (cls && w < W) {
+            const uint32_t nb = min(32u, L[k] - 32u * w), sh = (uint32_t)(off[k] & 15u);
+            uint32_t odd = 0;
+            const uint32_t ca = code_chunk(xa[k], odd), cb = code_chunk(xb[k], odd), cc = code_chunk(xc[k], odd);
+            const uint64_t lo64 = (uint64_t)cb << 32 | ca;
+            word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)cc << (64u - 2u * sh)) : lo64;
+            if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
+            if (odd) word = encode_word_q(in + off[k] + 32u * w, nb, nb < 32u, bad);   // rare: exact semantics
+        } else if (cls && w == W) {
+            word = L[k];
+        }
+        if (live) out[r * S + w] = word;
+        report_bad(bad != 0u, r, first_bad);
+        srow[wave][k * 64 + lane] = word;
+        if (w == 0 && i < R) slen[wave][k * R + i] = (uint16_t)(cls ? L[k] : 0u);
+    }
+    __syncthreads();
+    // lane per read: its row's fingerprint (words_fp over W + 1 words; one zero word for a read that
+    // is no class read) and its class's sketch -- one chain per read, not one per word lane
+    const uint64_t rb = ((uint64_t)blockIdx.x * 4 + wave) * R * kRowsK;
+    for (uint32_t j = lane; j < R * kRowsK && rb + j < n; j += 64) {
+        const uint32_t k = j / R, ii = j - k * R;
+        const uint32_t LL = slen[wave][j];
+        const uint32_t W1 = LL ? (LL + 31u) / 32u + 1u : 1u;
+        const uint64_t* row = &srow[wave][k * 64 + ii * S];
+        uint64_t h = 0x243F6A8885A308D3ull ^ W1;
+        for (uint32_t q = 0; q < W1; ++q) h = splitmix64(h ^ row[q]);
+        if (h == ~0ull) h = ~1ull;
+        fps[rb + j] = h;
+        if (LL) hll_add(hll + ((uint64_t)(W1 - 1) << kHllLog), h, W1);
+    }
+}
+
 // The same registers from rows already packed (k_encode_class's paths): lane per row, the same hash.
 __global__ __launch_bounds__(kThreads) void k_hll_rows(const uint64_t* __restrict__ rows, uint64_t m, uint32_t W1,
                                                        uint32_t* hll) {
@@ -1202,6 +1289,17 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     hipLaunchKernelGGL(k_encode_var_dense, dim3(grid), dim3(kThreads), 0, s, d_ascii, d_offsets, d_lens, n, d_words,
                        wpr, 1.0 / (double)wpr, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_var_dense");
+}
+
+int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n, uint32_t S,
+                        uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
+    if (S < 3 || S > 6) return ss_fail(SS_EARG, "k_encode_rows: rows of 3 to 6 words");
+    if (n == 0) return SS_OK;
+    const uint64_t per = (uint64_t)(64 / S) * kRowsK, waves = (n + per - 1) / per, blocks = (waves + 3) / 4;
+    if (blocks > 0x7FFFFFFFull) return ss_fail(SS_EARG, "k_encode_rows: chunk too large");
+    hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, d_buf, d_offs, d_lens,
+                       n, S, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_encode_rows");
 }
 
 int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,

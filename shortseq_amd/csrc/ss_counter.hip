@@ -2571,6 +2571,234 @@ __global__ __launch_bounds__(256) void k_cls_fold_claim(Tbl f, ClsDesc d, const 
     }
 }
 
+// ---- the same on read-order rows (k_encode_rows: read r's row at rows + r * S, S <= kRepW1 words:
+// its W words, its length, zeros).  The scratch entry's first index is a read; the representative
+// carries the row's S words and its class W (the index of its last nonzero word: the length; 0 for
+// the zero row of a read that is no class read, an entry the fold skips).  A whole-row compare
+// decides equality (the zero tail is part of every row), so verify needs no class lookups; the fold
+// gives each new key its class table's next row (a wave-aggregated counter per class) and writes
+// that row's read index into the class's row map.
+struct FlatDesc {
+    Tbl tbl[kRepW1];                // class W's table (W = 2 .. kRepW1 - 1; W1 = W + 1 <= S)
+    uint64_t row0[kRepW1];          // its first row of this chunk (the row counter adds to it)
+    uint64_t* rmap[kRepW1];         // its row map at row0
+    uint64_t base;                  // global read index of the chunk's read 0
+    uint32_t S;
+};
+
+__global__ __launch_bounds__(256) void k_flat_reps(Tbl f, const uint64_t* __restrict__ rows, uint32_t S,
+                                                   uint64_t* __restrict__ rep) {
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+        const Slot sl = f.slots[s];
+        uint64_t v[8] = {sl.key, 0, 0, 0, 0, 0, 0, 0};
+        if (sl.key != kEmpty) {
+            const uint64_t* row = rows + (uint64_t)sl.first * S;
+#pragma unroll
+            for (uint32_t j = 0; j < kRepW1; ++j) {
+                v[1 + j] = j < S ? row[j] : 0ull;
+                if (v[1 + j]) v[7] = j;
+            }
+        }
+        uint4* dst = (uint4*)(rep + s * 8);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k] = make_uint4((uint32_t)v[2 * k], (uint32_t)(v[2 * k] >> 32), (uint32_t)v[2 * k + 1],
+                                                       (uint32_t)(v[2 * k + 1] >> 32));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_flat_verify(Tbl f, const uint64_t* __restrict__ rows, uint32_t S, uint64_t n,
+                                                     const uint64_t* __restrict__ fps, const uint64_t* __restrict__ rep,
+                                                     uint32_t* __restrict__ flag) {
+    const uint64_t G = (uint64_t)gridDim.x * 256;
+    // two rows per lane per round, every load of both in flight before either is probed
+    for (uint64_t g0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; g0 < n; g0 += 2 * G) {
+        uint64_t aw[2][kRepW1], fp[2], base[2], off[2];
+        uint4 e[2][4];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint64_t g = min(g0 + k * G, n - 1);
+            const uint64_t* a = rows + g * S;
+#pragma unroll
+            for (uint32_t j = 0; j < kRepW1; ++j) aw[k][j] = a[min(j, S - 1)];
+            fp[k] = fps[g];
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+#pragma unroll
+            for (uint32_t j = 0; j < kRepW1; ++j)
+                if (j >= S) aw[k][j] = 0;
+            const uint64_t top = slot_top(f, fp[k]);
+            base[k] = top & ~f.slice_mask;
+            off[k] = top & f.slice_mask;
+            const uint4* p = (const uint4*)(rep + (base[k] + off[k]) * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[k][j] = p[j];
+        }
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            bool b = true;
+            for (uint64_t probe = 0; probe <= f.slice_mask; ++probe) {
+                if (probe) {
+                    off[k] = (off[k] + 1) & f.slice_mask;
+                    const uint4* p = (const uint4*)(rep + (base[k] + off[k]) * 8);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) e[k][j] = p[j];
+                }
+                const uint64_t key = (uint64_t)e[k][0].y << 32 | e[k][0].x;
+                if (key == fp[k]) {
+                    const uint64_t rw[6] = {(uint64_t)e[k][0].w << 32 | e[k][0].z, (uint64_t)e[k][1].y << 32 | e[k][1].x,
+                                            (uint64_t)e[k][1].w << 32 | e[k][1].z, (uint64_t)e[k][2].y << 32 | e[k][2].x,
+                                            (uint64_t)e[k][2].w << 32 | e[k][2].z, (uint64_t)e[k][3].y << 32 | e[k][3].x};
+                    b = false;
+#pragma unroll
+                    for (uint32_t j = 0; j < kRepW1; ++j) b |= aw[k][j] != rw[j];
+                    break;
+                }
+                if (key == kEmpty) break;
+            }
+            bad |= b && g0 + k * G < n;
+        }
+        if (__ballot(bad) && bad) atomicOr(flag, 1u);
+    }
+}
+
+// scratch slot s -> (fp, count, first read, class W, the rep's words); false for a free slot, the
+// zero row's entry, or a class without a table
+__device__ __forceinline__ bool flat_entry(const Tbl& f, const FlatDesc& d, const uint64_t* rep, uint64_t s,
+                                           uint64_t& fp, uint32_t& cnt, uint32_t& W, const uint64_t*& kw,
+                                           uint64_t& first) {
+    if (s > f.mask) return false;
+    const Slot sl = f.slots[s];
+    if (sl.key == kEmpty) return false;
+    W = (uint32_t)rep[s * 8 + 7];
+    if (W < 2 || W + 1 > d.S || !d.tbl[W].slots) return false;
+    fp = sl.key;
+    cnt = ~sl.ncount;
+    first = sl.first;
+    kw = rep + s * 8 + 1;
+    return true;
+}
+
+// find: the class table slot of each entry's key (kEmpty: a new key), and per block the new keys of
+// each class (blkcnt[block * kRepW1 + W]); k_flat_fold_scan turns those into each block's first
+// row per class; claim (the same grid, the same slots per block) gives each new key its block's
+// next row (LDS counters) -- no contended global counters (one per class, wave-aggregated, took
+// 3.1 ms on the f2 batch)
+__global__ __launch_bounds__(256) void k_flat_fold_find(Tbl f, FlatDesc d, const uint64_t* __restrict__ rep,
+                                                        const uint32_t* __restrict__ flag, uint64_t* __restrict__ found,
+                                                        uint32_t* __restrict__ blkcnt) {
+    __shared__ uint32_t lc[kRepW1];
+    if (threadIdx.x < kRepW1) lc[threadIdx.x] = 0;
+    __syncthreads();
+    if (!*flag) {
+        for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+            uint64_t fp, first, at = kEmpty;
+            uint32_t cnt, W;
+            const uint64_t* kw;
+            if (flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) {
+                const Tbl& t = d.tbl[W];
+                const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
+                uint64_t off = top & t.slice_mask;
+                for (uint64_t probe = 0; probe <= t.slice_mask; ++probe) {
+                    const uint64_t k = t.slots[base + off].key;
+                    if (k == kEmpty) break;
+                    if (k == fp && words_eq(t.keywords + (base + off) * t.W, kw, t.W)) {
+                        at = base + off;
+                        break;
+                    }
+                    off = (off + 1) & t.slice_mask;
+                }
+                if (at == kEmpty) atomicAdd(&lc[W], 1u);
+            }
+            found[s] = at;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kRepW1) blkcnt[(uint64_t)blockIdx.x * kRepW1 + threadIdx.x] = lc[threadIdx.x];
+}
+
+// one block: blkcnt -> each block's first row per class (exclusive scan over the blocks, in place)
+__global__ __launch_bounds__(1024) void k_flat_fold_scan(uint32_t* __restrict__ blkcnt, uint32_t nblk) {
+    __shared__ uint32_t carry[kRepW1];
+    __shared__ uint32_t wsum[16][kRepW1];
+    if (threadIdx.x < kRepW1) carry[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
+        const uint32_t b = b0 + threadIdx.x;
+        uint32_t v[kRepW1], inc[kRepW1];
+#pragma unroll
+        for (uint32_t W = 0; W < kRepW1; ++W) {
+            v[W] = b < nblk ? blkcnt[(uint64_t)b * kRepW1 + W] : 0u;
+            inc[W] = v[W];
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc[W], o);
+                if (lane >= o) inc[W] += y;
+            }
+            if (lane == 63) wsum[wave][W] = inc[W];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t W = 0; W < kRepW1; ++W) {
+            uint32_t before = carry[W];
+            for (uint32_t u = 0; u < wave; ++u) before += wsum[u][W];
+            if (b < nblk) blkcnt[(uint64_t)b * kRepW1 + W] = before + inc[W] - v[W];
+        }
+        __syncthreads();
+        if (threadIdx.x < kRepW1)
+            for (uint32_t u = 0; u < 16; ++u) carry[threadIdx.x] += wsum[u][threadIdx.x];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_flat_fold_claim(Tbl f, FlatDesc d, const uint64_t* __restrict__ rep,
+                                                         const uint32_t* __restrict__ flag,
+                                                         const uint64_t* __restrict__ found,
+                                                         const uint32_t* __restrict__ blkoff) {
+    __shared__ uint32_t lc[kRepW1];
+    if (threadIdx.x < kRepW1) lc[threadIdx.x] = blkoff[(uint64_t)blockIdx.x * kRepW1 + threadIdx.x];
+    __syncthreads();
+    if (*flag) return;
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+        uint64_t fp, first;
+        uint32_t cnt, W;
+        const uint64_t* kw;
+        if (!flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) continue;
+        const Tbl& t = d.tbl[W];
+        const uint64_t at0 = found[s];
+        if (at0 != kEmpty) {
+            atomicAdd(&t.slots[at0].ncount, 0u - cnt);
+            continue;
+        }
+        const uint32_t row = atomicAdd(&lc[W], 1u);     // LDS: this block's next row of class W
+        d.rmap[W][row] = d.base + first;
+        uint64_t trow = d.row0[W] + row;
+        if (trow > kMaxIndex) {
+            atomicOr(t.overflow, kOvfIndex);
+            trow = kMaxIndex;
+        }
+        const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
+        uint64_t off = top & t.slice_mask, at = kEmpty;
+        for (uint64_t probe = 0; probe <= t.slice_mask; ++probe) {
+            if (t.slots[base + off].key == kEmpty &&
+                atomicCAS(&t.slots[base + off].key, (unsigned long long)kEmpty, (unsigned long long)fp) == kEmpty) {
+                at = base + off;
+                break;
+            }
+            off = (off + 1) & t.slice_mask;
+        }
+        if (at == kEmpty) {
+            atomicOr(t.overflow, kOvfTable);
+            continue;
+        }
+        uint64_t* dst = t.keywords + at * t.W;
+        for (uint32_t q = 0; q < t.W; ++q) dst[q] = kw[q];
+        t.slots[at].ncount = ~cnt;
+        t.slots[at].first = (uint32_t)trow;
+    }
+}
+
 int ss_counter_create(uint64_t capacity, ss_counter** out) {
     if (!out) return ss_fail(SS_EARG, "null out");
     if (capacity < 64) capacity = 64;
@@ -3247,6 +3475,53 @@ int ss_counter_extract_words(ss_counter* c, uint32_t n_parts, uint64_t* d_fps, u
 }
 
 }  // extern "C"
+
+int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n, const uint64_t* d_fps,
+                                const ss_flat_class* cls, uint64_t base, uint32_t* d_flag,
+                                void* stream) {
+    if (!fpt || !cls || !d_flag || !d_rows || !d_fps) return ss_fail(SS_EARG, "null argument");
+    if (S < 3 || S > kRepW1) return ss_fail(SS_EARG, "read-order rows of 3 to 6 words");
+    if (n == 0) return SS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    FlatDesc d{};
+    d.S = S;
+    d.base = base;
+    int rc = SS_OK;
+    for (uint32_t W = 2; W + 1 <= S; ++W) {
+        ss_counter* t = cls[W].table;
+        if (!t) continue;
+        if (t->L != kWordKeys || t->W != W + 1) return ss_fail(SS_EARG, "class table: set_words(W + 1) first");
+        if ((rc = flush_reset(t, s))) return rc;
+        t->occ_src = 0;
+        d.tbl[W] = tbl_of(t);
+        d.row0[W] = cls[W].base;
+        d.rmap[W] = cls[W].rmap;
+    }
+    if ((rc = flush_reset(fpt, s))) return rc;
+    const Tbl f = tbl_of(fpt);
+    uint64_t* rep = nullptr;
+    uint64_t* found = nullptr;
+    const unsigned grid = grid_for(fpt->cap, 256, 256 * 16);
+    // found[cap + 1] then the per-block class counts / first rows
+    const uint64_t fwords = fpt->cap + 1 + ((uint64_t)grid * kRepW1 + 1) / 2;
+    rc = ss_check(hipMallocAsync((void**)&rep, (fpt->cap + 1) * 64, s), "class reps scratch");
+    if (!rc) rc = ss_check(hipMallocAsync((void**)&found, fwords * sizeof(uint64_t), s), "class fold scratch");
+    if (!rc) {
+        uint32_t* blk = (uint32_t*)(found + fpt->cap + 1);
+        hipLaunchKernelGGL(k_flat_reps, dim3(grid), dim3(256), 0, s, f, d_rows, S, rep);
+        hipLaunchKernelGGL(k_flat_verify, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, s, f, d_rows, S, n, d_fps,
+                           (const uint64_t*)rep, d_flag);
+        hipLaunchKernelGGL(k_flat_fold_find, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep,
+                           (const uint32_t*)d_flag, found, blk);
+        hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(1024), 0, s, blk, grid);
+        hipLaunchKernelGGL(k_flat_fold_claim, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep,
+                           (const uint32_t*)d_flag, (const uint64_t*)found, (const uint32_t*)blk);
+        rc = ss_check(hipGetLastError(), "class verify / fold (read-order rows)");
+    }
+    const int r1 = rep ? ss_check(hipFreeAsync(rep, s), "class reps scratch free") : SS_OK;
+    const int r2 = found ? ss_check(hipFreeAsync(found, s), "class fold scratch free") : SS_OK;
+    return rc ? rc : r1 ? r1 : r2;
+}
 
 int ss_classes_verify_fold(ss_counter* fpt, const uint64_t* d_fps, const ss_class_rows* cls, uint32_t ncls,
                            uint32_t* d_flag, void* stream) {

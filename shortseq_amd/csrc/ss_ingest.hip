@@ -761,6 +761,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     }
     uint64_t need_cls[33] = {0};
     const bool fused = !dense_L && w1max && w1max <= 16;   // fingerprints and row maps come with the rows
+    // every read a class read of <= 5 words (or empty / too long): rows in read order at a stride of
+    // w1max words (k_encode_rows), no class ranks and no row maps in the encode
+    bool flat = fused && w1max <= 6;
+    for (const Job& jb : jobs) flat &= jb.bin > 32;
     // the stable split into d_order: for the lengths 1..32 (row gathers) and the per-class passes; the
     // fused class encode ranks its rows itself from k_len_binscan's per-block offsets
     bool need_order = !dense_L && (!fused && w1max);
@@ -787,8 +791,12 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     }
     if (w1max) {
         if ((rc = g->cls_words.ensure(cls_words))) return rc;
-        if (fused && (rc = g->cls_fps.ensure(cls_rows))) return rc;
-        if (fused) {                        // one read-order pass, the registers updated in it
+        if (fused && (rc = g->cls_fps.ensure(flat ? n : cls_rows))) return rc;
+        if (flat) {
+            if ((rc = g->cls_words.ensure(n * w1max))) return rc;
+            rc = ss_encode_rows_impl(d_buf, d_offs, d_lens, n, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p,
+                                     g->first_bad.p + nj, s);
+        } else if (fused) {                 // one read-order pass, the registers updated in it
             rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->blkhist.p, kSplitBlocks, woff, fpoff, rmap, base,
                                         kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + nj, s);
         } else {                            // a class per pass (longer reads, or a dense chunk)
@@ -855,13 +863,15 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         // the classes' rows counted by fingerprint in one scratch table, checked against their
         // fingerprints' first rows and folded into the class tables (ss_classes_verify_fold); a
         // fingerprint shared by two keys sends the classes to the exact path below, after the sync
-        uint64_t need_all = 0;
+        uint64_t need_all = flat ? 1 : 0;     // (the zero rows' entry)
         std::vector<ss_class_rows> cr;
+        ss_flat_class fc[6] = {};
         for (size_t j : cls_jobs) {
             const Job& jb = jobs[j];
             Group& gr = g->groups[jb.bin];
             need_all += std::min<uint64_t>(jb.m, need_cls[gr.W1 - 1]);
             cr.push_back({gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, gr.W1});
+            if (flat) fc[gr.W1 - 1] = {gr.table, gr.rows, gr.rowmap.p + gr.rows};
         }
         const uint64_t fcap = std::min<uint64_t>(1ull << 32, std::max<uint64_t>(1ull << 19, pow2_at_least(2 * need_all + 2)));
         if (g->fpt && ss_counter_capacity(g->fpt) != fcap) {
@@ -874,8 +884,11 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if ((rc = g->cls_flag.ensure(1))) return rc;
         // (sizing mode 3, a test hook: the flag starts raised, as if two keys shared a fingerprint)
         rc = ss_check(hipMemsetAsync(g->cls_flag.p, g->sizing == 3 ? 1 : 0, 4, s), "ingest class flag reset");
-        if (!rc) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, cls_rows, 0, s);
-        if (!rc) rc = ss_classes_verify_fold(g->fpt, g->cls_fps.p, cr.data(), (uint32_t)cr.size(), g->cls_flag.p, s);
+        if (!rc && !flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, cls_rows, 0, s);
+        if (!rc && !flat) rc = ss_classes_verify_fold(g->fpt, g->cls_fps.p, cr.data(), (uint32_t)cr.size(), g->cls_flag.p, s);
+        if (!rc && flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, n, 0, s);
+        if (!rc && flat)
+            rc = ss_classes_flat_verify_fold(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, fc, base, g->cls_flag.p, s);
         if (!rc) rc = ss_counter_overflow(g->fpt, g->ovf.p + nj, s);
         for (size_t q = 0; q < cls_jobs.size() && !rc; ++q) {
             const size_t j = cls_jobs[q];
@@ -883,7 +896,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             Group& gr = g->groups[jb.bin];
             cls_base[j] = gr.rows;
             rc = ss_counter_overflow(gr.table, g->ovf.p + j, s);
-            gr.rows += jb.m;           // (their row map: written by the encode)
+            gr.rows += jb.m;           // (their row map: written by the encode, or by the fold for new keys)
         }
         if (rc) return rc;
     } else if (!cls_jobs.empty()) {
@@ -939,6 +952,16 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     }
     if (fused && !cls_jobs.empty() && (uint32_t)hb[2 * nj + 2]) {
         // two keys share a fingerprint: the class tables were left untouched, count them exactly
+        if (flat) {     // class-ordered rows and their row maps first (the one-pass class encode)
+            uint64_t* cmap[33] = {nullptr};
+            for (size_t j : cls_jobs) {
+                Group& gr = g->groups[jobs[j].bin];
+                cmap[gr.W1 - 1] = gr.rowmap.p + cls_base[j];
+            }
+            rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->blkhist.p, kSplitBlocks, woff, fpoff, cmap, base,
+                                        kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + nj, s);
+            if (rc) return rc;
+        }
         for (size_t j : cls_jobs) {
             Group& gr = g->groups[jobs[j].bin];
             if ((rc = ss_counter_insert_words(gr.table, g->cls_words.p + woff[gr.W1 - 1], jobs[j].m, cls_base[j], s)) ||

@@ -24,6 +24,13 @@ extern "C" int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_of
                                       const uint64_t* h_fpoff, uint64_t* const* h_rmap, uint64_t base, uint32_t bin0,
                                       uint32_t w1max, uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll,
                                       uint64_t* d_first_bad, void* stream);
+// A chunk of class reads of at most S - 1 words (3 <= S <= 6; k_encode_rows): read r's row at
+// d_out + r * S (its W words, its length, zeros), its fingerprint (words_fp over W + 1 words) at
+// d_fps[r], its class's HyperLogLog registers updated; a read that is not a class read (empty) gets a
+// zero row and words_fp of one zero word.  *d_first_bad (not reset) = min read with a rejected byte.
+extern "C" int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
+                                   uint32_t S, uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll,
+                                   uint64_t* d_first_bad, void* stream);
 // Single-word keys already computed on the device (d_keys[n], any 64-bit values): counted with the
 // optimistic partitioned insert (12-B records, LDS aggregation) -- e.g. the class rows' fingerprints.
 extern "C" int ss_counter_insert_keys(ss_counter* c, const uint64_t* d_keys, uint64_t n, uint64_t base_index,
@@ -44,6 +51,19 @@ struct ss_class_rows {
 // untouched and the caller counts the classes on the exact multi-word path instead.
 extern "C" int ss_classes_verify_fold(ss_counter* fpt, const uint64_t* d_fps, const ss_class_rows* cls, uint32_t ncls,
                                       uint32_t* d_flag, void* stream);
+// The same for read-order rows (ss_encode_rows_impl, stride S <= 6, fingerprints d_fps[n], after
+// ss_counter_insert_keys(fpt, d_fps, n, 0)): cls[W] (W = 2 .. S - 1; null table: no reads of class W)
+// holds class W's table, its first free row (base) and its row map at that row (rmap).  Each new key
+// of class W takes the next row (base + the new keys before it: at most the class's reads) and
+// rmap[row] = base + its first read; the zero rows of reads that are no class reads are skipped.
+struct ss_flat_class {
+    ss_counter* table;
+    uint64_t base;
+    uint64_t* rmap;
+};
+extern "C" int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n,
+                                           const uint64_t* d_fps, const ss_flat_class* cls, uint64_t base,
+                                           uint32_t* d_flag, void* stream);
 // HyperLogLog registers (2^kHllLog u32 at d_hll) of m packed rows of W1 words, k_encode_classes' hash.
 extern "C" int ss_hll_rows_impl(const uint64_t* d_rows, uint64_t m, uint32_t W1, uint32_t* d_hll, void* stream);
 // Drop-in engine (ss_ingest), one multi-word length class: rows of W words + the length (k_encode_class).

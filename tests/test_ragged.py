@@ -130,6 +130,67 @@ def test_device_ingest_class_lengths_apart(gpu, oracle):
     assert gw.tolist() == [int(x) for (w, _L, _c, _f) in exp for x in w]
 
 
+@pytest.mark.parametrize("exact", [False, 3])
+def test_device_ingest_read_order_rows(gpu, oracle, exact):
+    """Chunks whose reads are all 33-160 nt (or empty) take the read-order rows (k_encode_rows, the
+    flat verify / fold); empties stay out of the class tables, a second call continues the global
+    read indices and the first occurrences, exact=3 (test hook) takes the exact fallback through the
+    one-pass class encode.  == oracle.count over the same reads."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(11)
+    pool = ["".join(rng.choice(list("ACGT"), int(L))) for L in rng.integers(33, 161, 700)]
+    pool += ["A" * 33, "A" * 64, "A" * 65, "T" * 96, "T" * 128, "G" * 160, pool[0] + "A", ""]
+    reads = [pool[i] for i in rng.integers(0, len(pool), 60_000)]
+
+    def device(rs):
+        enc = [r.encode() for r in rs]
+        lens = torch.tensor([len(r) for r in enc], dtype=torch.int32)
+        offs = torch.zeros(len(enc), dtype=torch.int64)
+        offs[1:] = torch.cumsum(lens.to(torch.int64), 0)[:-1]
+        blob = torch.frombuffer(bytearray(b"".join(enc) + b"\0" * 16), dtype=torch.uint8)
+        return blob.to(gpu), offs.to(gpu), lens.to(gpu)
+
+    eng = B.DeviceIngest(gpu) if exact != 3 else B.DeviceIngest(gpu, _sizing=3)
+    try:
+        eng.count(*device(reads[:25_000]))
+        eng.count(*device(reads[25_000:]))
+        gl, gc, gw = eng.results()
+    finally:
+        eng.close()
+    exp = oracle.count([r.encode() for r in reads])
+    assert gl.tolist() == [L for (_w, L, _c, _f) in exp]
+    assert gc.tolist() == [c for (_w, _L, c, _f) in exp]
+    # (ss_ingest_results: ceil(L / 32) words a key, none for the empty read)
+    assert gw.tolist() == [int(x) for (w, L, _c, _f) in exp for x in w[:(L + 31) // 32]]
+
+
+def test_device_ingest_read_order_rows_error(gpu):
+    """A rejected byte inside a read of a read-order chunk raises the reference's message for the
+    first such read."""
+    import torch
+    import shortseq_amd as sq
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(12)
+    reads = ["".join(rng.choice(list("ACGT"), int(L))) for L in rng.integers(33, 150, 20_000)]
+    reads[7000] = reads[7000][:40] + "N" + reads[7000][41:]
+    reads[9000] = reads[9000][:3] + "x" + reads[9000][4:]
+    with pytest.raises(Exception) as want:
+        sq.pack(reads[7000].encode())
+    enc = [r.encode() for r in reads]
+    lens = torch.tensor([len(r) for r in enc], dtype=torch.int32)
+    offs = torch.zeros(len(enc), dtype=torch.int64)
+    offs[1:] = torch.cumsum(lens.to(torch.int64), 0)[:-1]
+    blob = torch.frombuffer(bytearray(b"".join(enc) + b"\0" * 16), dtype=torch.uint8)
+    eng = B.DeviceIngest(gpu)
+    try:
+        with pytest.raises(Exception) as ei:
+            eng.count(blob.to(gpu), offs.to(gpu), lens.to(gpu))
+        assert str(ei.value) == str(want.value)
+    finally:
+        eng.close()
+
+
 def test_device_ingest_ragged_errors(gpu):
     """A rejected read in a device batch raises the reference's message (the first in read order)."""
     import shortseq_amd as sq
