@@ -82,6 +82,9 @@ struct ss_counter {
     // kept by the spill insert); lets ss_counter_pack_ranges skip its counting pass.
     // occ_src: 0 = stale, 1 = valid
     uint32_t* occ = nullptr;               // [R]
+    void* aux = nullptr;                   // scratch of the fold / merge passes, kept between calls
+    size_t aux_bytes = 0;                  // (stream-ordered allocations were released to the OS at
+                                           // every sync: ~0.4 ms of unmap / remap per f2 chunk)
     unsigned long long* roff = nullptr;    // [R + 2] pack scratch: region offsets, sentinel position
     uint64_t occ_R = 0;
     int occ_src = 0;
@@ -2870,6 +2873,7 @@ int ss_counter_destroy(ss_counter* c) {
     if (c->keywords) (void)hipFree(c->keywords);
     if (c->occ) (void)hipFree(c->occ);
     if (c->roff) (void)hipFree(c->roff);
+    if (c->aux) (void)hipFree(c->aux);
     ss_counter_release(c);
     if (c->ws_hist) (void)hipFree(c->ws_hist);
     if (c->ws_rstart) (void)hipFree(c->ws_rstart);
@@ -2878,6 +2882,24 @@ int ss_counter_destroy(ss_counter* c) {
     if (c->ws_tot) (void)hipFree(c->ws_tot);
     if (c->ws_fill) (void)hipFree(c->ws_fill);
     delete c;
+    return SS_OK;
+}
+
+// the handle's scratch of at least `bytes` (grown by hipFree + hipMalloc: the free waits for the
+// device, so earlier users on any stream are done with it; same-stream users are ordered anyway)
+static int aux_scratch(ss_counter* c, size_t bytes, void** out) {
+    if (c->aux_bytes < bytes) {
+        if (c->aux) (void)hipFree(c->aux);
+        c->aux = nullptr;
+        c->aux_bytes = 0;
+        const size_t want = std::max(bytes, (size_t)1 << 20);
+        if (hipMalloc(&c->aux, want) != hipSuccess) {
+            ss_check(hipGetLastError(), "counter scratch hipMalloc");
+            return ss_fail(SS_ENOMEM, "counter scratch: out of device memory");
+        }
+        c->aux_bytes = want;
+    }
+    *out = c->aux;
     return SS_OK;
 }
 
@@ -3326,16 +3348,13 @@ int ss_counter_merge_words(ss_counter* c, const uint64_t* d_words, const uint64_
     int rc = flush_reset(c, s);
     if (rc) return rc;
     uint64_t* found = nullptr;
-    rc = ss_check(hipMallocAsync((void**)&found, m * sizeof(uint64_t), s), "merge_words scratch");
-    if (rc) return rc;
+    if ((rc = aux_scratch(c, m * sizeof(uint64_t), (void**)&found))) return rc;
     const unsigned grid = grid_for(m, 256, 256 * 16);
     const Tbl t = tbl_of(c);
     hipLaunchKernelGGL(k_mw_merge_find, dim3(grid), dim3(256), 0, s, t, d_words, m, found);
     hipLaunchKernelGGL(k_mw_merge_claim, dim3(grid), dim3(256), 0, s, t, d_words, d_counts, d_first, m,
                        (const uint64_t*)found);
-    rc = ss_check(hipGetLastError(), "ss_counter_merge_words");
-    const int rf = ss_check(hipFreeAsync(found, s), "merge_words scratch free");
-    return rc ? rc : rf;
+    return ss_check(hipGetLastError(), "ss_counter_merge_words");
 }
 
 int ss_counter_set_length(ss_counter* c, uint32_t L) {
@@ -3500,12 +3519,11 @@ int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_
     if ((rc = flush_reset(fpt, s))) return rc;
     const Tbl f = tbl_of(fpt);
     uint64_t* rep = nullptr;
-    uint64_t* found = nullptr;
     const unsigned grid = grid_for(fpt->cap, 256, 256 * 16);
-    // found[cap + 1] then the per-block class counts / first rows
+    // the scratch: rep[(cap + 1) * 8], found[cap + 1], then the per-block class counts / first rows
     const uint64_t fwords = fpt->cap + 1 + ((uint64_t)grid * kRepW1 + 1) / 2;
-    rc = ss_check(hipMallocAsync((void**)&rep, (fpt->cap + 1) * 64, s), "class reps scratch");
-    if (!rc) rc = ss_check(hipMallocAsync((void**)&found, fwords * sizeof(uint64_t), s), "class fold scratch");
+    rc = aux_scratch(fpt, ((fpt->cap + 1) * 8 + fwords) * sizeof(uint64_t), (void**)&rep);
+    uint64_t* found = rep + (fpt->cap + 1) * 8;
     if (!rc) {
         uint32_t* blk = (uint32_t*)(found + fpt->cap + 1);
         hipLaunchKernelGGL(k_flat_reps, dim3(grid), dim3(256), 0, s, f, d_rows, S, rep);
@@ -3518,9 +3536,7 @@ int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_
                            (const uint32_t*)d_flag, (const uint64_t*)found, (const uint32_t*)blk);
         rc = ss_check(hipGetLastError(), "class verify / fold (read-order rows)");
     }
-    const int r1 = rep ? ss_check(hipFreeAsync(rep, s), "class reps scratch free") : SS_OK;
-    const int r2 = found ? ss_check(hipFreeAsync(found, s), "class fold scratch free") : SS_OK;
-    return rc ? rc : r1 ? r1 : r2;
+    return rc;
 }
 
 int ss_classes_verify_fold(ss_counter* fpt, const uint64_t* d_fps, const ss_class_rows* cls, uint32_t ncls,
@@ -3550,27 +3566,21 @@ int ss_classes_verify_fold(ss_counter* fpt, const uint64_t* d_fps, const ss_clas
     const Tbl f = tbl_of(fpt);
     uint32_t w1max = 0;
     for (uint32_t k = 0; k < ncls; ++k) w1max = std::max(w1max, cls[k].W1);
+    // the scratch: rep[(cap + 1) * 8] (rows of <= kRepW1 words), then found[cap + 1]
+    uint64_t* rep = nullptr;
+    if ((rc = aux_scratch(fpt, (fpt->cap + 1) * 9 * sizeof(uint64_t), (void**)&rep))) return rc;
+    uint64_t* found = rep + (fpt->cap + 1) * 8;
     if (w1max <= kRepW1) {
-        uint64_t* rep = nullptr;
-        rc = ss_check(hipMallocAsync((void**)&rep, (fpt->cap + 1) * 64, s), "class reps scratch");
-        if (rc) return rc;
         hipLaunchKernelGGL(k_cls_reps, dim3(grid_for(fpt->cap, 256, 256 * 16)), dim3(256), 0, s, f, d, rep);
         hipLaunchKernelGGL(k_cls_verify_rep, dim3(grid_for(row, 256, 256 * 32)), dim3(256), 0, s, f, d, d_fps,
                            (const uint64_t*)rep, d_flag);
-        rc = ss_check(hipFreeAsync(rep, s), "class reps scratch free");
-        if (rc) return rc;
     } else {
         hipLaunchKernelGGL(k_cls_verify, dim3(grid_for(row, 256, 256 * 32)), dim3(256), 0, s, f, d, d_fps, d_flag);
     }
-    uint64_t* found = nullptr;
-    rc = ss_check(hipMallocAsync((void**)&found, (fpt->cap + 1) * sizeof(uint64_t), s), "class fold scratch");
-    if (rc) return rc;
     const unsigned grid = grid_for(fpt->cap, 256, 256 * 16);
     hipLaunchKernelGGL(k_cls_fold_find, dim3(grid), dim3(256), 0, s, f, d, (const uint32_t*)d_flag, found);
     hipLaunchKernelGGL(k_cls_fold_claim, dim3(grid), dim3(256), 0, s, f, d, (const uint32_t*)d_flag,
                        (const uint64_t*)found);
-    rc = ss_check(hipGetLastError(), "class verify / fold");
-    const int rf = ss_check(hipFreeAsync(found, s), "class fold scratch free");
-    return rc ? rc : rf;
+    return ss_check(hipGetLastError(), "class verify / fold");
 }
 
