@@ -661,8 +661,13 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
         const uint32_t LL = slen[wave][j];
         const uint32_t W1 = LL ? (LL + 31u) / 32u + 1u : 1u;
         const uint64_t* row = &srow[wave][k * 64 + ii * S];
+        uint64_t rw[6];                     // all LDS reads issued before the chain (S <= 6)
+#pragma unroll
+        for (uint32_t q = 0; q < 6; ++q) rw[q] = row[min(q, S - 1)];
         uint64_t h = 0x243F6A8885A308D3ull ^ W1;
-        for (uint32_t q = 0; q < W1; ++q) h = splitmix64(h ^ row[q]);
+#pragma unroll
+        for (uint32_t q = 0; q < 6; ++q)
+            if (q < W1) h = splitmix64(h ^ rw[q]);
         if (h == ~0ull) h = ~1ull;
         fps[rb + j] = h;
         if (LL) hll_add(hll + ((uint64_t)(W1 - 1) << kHllLog), h, W1);

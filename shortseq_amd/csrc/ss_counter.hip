@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(512) void k_pf_order(const uint32_t* __restrict__ f
 // (sub-bin, region) segments then end before their reserved size; the end of each is written to
 // w.seg_end and the aggregate reads only the written part.
 constexpr uint32_t kHeavyFine = 2;    // x the mean records per region per tile
-constexpr uint32_t kFsT = 512, kFsTile = 4096;   // k_pf_scatter block and tile
+constexpr uint32_t kFsT = 1024, kFsTile = 8192;  // k_pf_scatter block and tile (512 x 4096: +4 % C5, same box)
 template <int T, uint32_t kTile>
 __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1, const uint32_t* fill,
                                                   const uint32_t* __restrict__ order) {
@@ -1712,6 +1712,15 @@ struct PackedRecs {
     }
 };
 
+// record j's region relative to reg_lo (clamped to [0, nreg]); the sentinel sorts last
+template <typename Recs>
+__device__ __forceinline__ uint32_t run_rel(const Tbl& t, const Recs& recs, uint64_t j, uint32_t reg_lo, uint32_t nreg) {
+    const uint64_t k = recs.key(j);
+    if (k == kEmpty) return nreg;
+    const uint32_t r = region_of(t, k);
+    return r < reg_lo ? 0u : min(r - reg_lo, nreg);
+}
+
 template <typename Recs>
 __global__ __launch_bounds__(256) void k_run_bounds(Tbl t, Recs recs,
                                                    const uint64_t* __restrict__ run_off, uint32_t n_runs,
@@ -1722,12 +1731,7 @@ __global__ __launch_bounds__(256) void k_run_bounds(Tbl t, Recs recs,
     while (run < n_runs && !(run_off[2 * run] <= i && i < run_off[2 * run + 1])) ++run;
     if (run == n_runs) return;
     const uint64_t beg = run_off[2 * run], end = run_off[2 * run + 1];
-    auto rel = [&](uint64_t j) -> uint32_t {    // region relative to reg_lo; the sentinel sorts last
-        const uint64_t k = recs.key(j);
-        if (k == kEmpty) return nreg;
-        const uint32_t r = region_of(t, k);
-        return r < reg_lo ? 0u : min(r - reg_lo, nreg);
-    };
+    auto rel = [&](uint64_t j) { return run_rel(t, recs, j, reg_lo, nreg); };
     const uint32_t r = rel(i);
     const uint32_t prev = i == beg ? 0u : rel(i - 1) + 1u;   // regions [prev, r] start at i
     uint32_t* b = bounds + (uint64_t)run * (nreg + 1);
@@ -1737,6 +1741,7 @@ __global__ __launch_bounds__(256) void k_run_bounds(Tbl t, Recs recs,
 }
 
 constexpr uint32_t kMergeT = 512;
+constexpr uint32_t kMergeSearchRuns = 64;   // up to this many runs, each block finds its own bounds
 
 template <typename Recs>
 __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
@@ -1757,12 +1762,34 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
         scnt[q] = ~v.z;
         sfst[q] = v.w;
     }
+    // bounds == null: this region's segment of every run by a 64-ary search per (run, edge), one wave
+    // each (4 dependent steps for a 2M-record run) -- no separate pass over every record
+    __shared__ uint32_t s_lo[kMergeSearchRuns], s_hi[kMergeSearchRuns];
+    if (!bounds) {
+        const uint32_t lane = threadIdx.x & 63u;
+        for (uint32_t q = threadIdx.x >> 6; q < 2 * n_runs; q += kMergeT / 64) {
+            const uint32_t run = q >> 1, target = j + (q & 1u);
+            const uint64_t beg = run_off[2 * run], end = run_off[2 * run + 1];
+            uint64_t L = beg, H = end;     // the first record of region >= target lies in [L, H]
+            while (H > L) {
+                const uint64_t len = H - L;
+                const uint64_t p = L + len * lane / 64;
+                const bool below = run_rel(t, recs, p, reg_lo, nreg) < target;
+                const uint32_t c = (uint32_t)__popcll(__ballot(below));
+                if (c == 0) break;
+                const uint64_t nx = c < 64 ? L + len * c / 64 : H;
+                L = L + len * (c - 1) / 64 + 1;
+                H = nx;
+            }
+            if (lane == 0) ((q & 1u) ? s_hi : s_lo)[run] = (uint32_t)(L - beg);
+        }
+    }
     __syncthreads();
     for (uint32_t run = 0; run < n_runs; ++run) {
         const uint64_t r0 = run_off[2 * run];
         if (run_off[2 * run + 1] == r0) continue;              // empty run: no bounds were written
         const uint32_t* b = bounds + (uint64_t)run * (nreg + 1);
-        const uint32_t lo = b[j], hi = b[j + 1];
+        const uint32_t lo = bounds ? b[j] : s_lo[run], hi = bounds ? b[j + 1] : s_hi[run];
         for (uint32_t e = lo + threadIdx.x; e < hi; e += kMergeT) {
             uint64_t key;
             unsigned long long c, f;
@@ -2326,12 +2353,16 @@ int launch_merge(ss_counter* c, Recs recs, const uint64_t* d_run_offsets, uint32
     int rc = flush_reset(c, s);
     if (rc) return rc;
     Tbl t = tbl_of(c);
-    hipLaunchKernelGGL((k_run_bounds<Recs>), dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, t, recs,
-                       d_run_offsets, n_runs, reg_lo, nreg, d_bounds);
+    // few runs (the exchange's owners - 1): each region's block searches its segments itself;
+    // otherwise one pass over every record writes the bounds (d_bounds)
+    const bool search = n_runs <= kMergeSearchRuns;
+    if (!search)
+        hipLaunchKernelGGL((k_run_bounds<Recs>), dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, t, recs,
+                           d_run_offsets, n_runs, reg_lo, nreg, d_bounds);
     if (nreg) {
         const size_t lds = ((size_t)1 << c->slice_log) * 16;
         hipLaunchKernelGGL((k_merge_runs<Recs>), dim3(nreg), dim3(kMergeT), lds, s, t, recs, d_run_offsets, n_runs,
-                           reg_lo, nreg, (const uint32_t*)d_bounds);
+                           reg_lo, nreg, search ? (const uint32_t*)nullptr : (const uint32_t*)d_bounds);
     }
     hipLaunchKernelGGL((k_merge_sentinel<Recs>), dim3(1), dim3(64), 0, s, t, recs, d_run_offsets, n_runs);
     return ss_check(hipGetLastError(), what);
