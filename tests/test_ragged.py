@@ -165,6 +165,34 @@ def test_device_ingest_read_order_rows(gpu, oracle, exact):
     assert gw.tolist() == [int(x) for (w, L, _c, _f) in exp for x in w[:(L + 31) // 32]]
 
 
+@pytest.mark.parametrize("lo,hi", [(33, 64), (33, 96), (65, 128), (129, 160), (150, 170)])
+def test_device_ingest_row_widths(gpu, oracle, lo, hi):
+    """Read-order rows of every stride (S = 3..6 words: lengths up to 64 / 96 / 128 / 160) and, past 160
+    nt, the one-pass class encode; lengths at the class edges (32k, 32k + 1) included; == oracle.count."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(lo * 1000 + hi)
+    edges = [L for L in (lo, hi, 64, 65, 96, 97, 128, 129, 160, 161) if lo <= L <= hi]
+    lens_pool = list(rng.integers(lo, hi + 1, 300)) + edges
+    pool = ["".join(rng.choice(list("ACGT"), int(L))) for L in lens_pool]
+    reads = [pool[i] for i in rng.integers(0, len(pool), 30_000)]
+    enc = [r.encode() for r in reads]
+    lens = torch.tensor([len(r) for r in enc], dtype=torch.int32)
+    offs = torch.zeros(len(enc), dtype=torch.int64)
+    offs[1:] = torch.cumsum(lens.to(torch.int64), 0)[:-1]
+    blob = torch.frombuffer(bytearray(b"".join(enc) + b"\0" * 16), dtype=torch.uint8)
+    eng = B.DeviceIngest(gpu)
+    try:
+        eng.count(blob.to(gpu), offs.to(gpu), lens.to(gpu))
+        gl, gc, gw = eng.results()
+    finally:
+        eng.close()
+    exp = oracle.count(enc)
+    assert gl.tolist() == [L for (_w, L, _c, _f) in exp]
+    assert gc.tolist() == [c for (_w, _L, c, _f) in exp]
+    assert gw.tolist() == [int(x) for (w, L, _c, _f) in exp for x in w[:(L + 31) // 32]]
+
+
 def test_device_ingest_read_order_rows_error(gpu):
     """A rejected byte inside a read of a read-order chunk raises the reference's message for the
     first such read."""
