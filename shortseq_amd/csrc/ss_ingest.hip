@@ -27,8 +27,8 @@
 // Finish: every table entry marks its global first read in a one-bit-per-read map (k_mark); an
 // exclusive scan of the map words' popcounts gives each entry its place in read order (k_rank:
 // the words before its bit + the bits below it in its word), and the ordered entries are gathered
-// into (length u32, count u64, words u64[ceil(L/32)]) rows (k_gather_out, word offsets by a second
-// scan), copied into engine-owned pinned buffers.  (A per-read 8-B slot array compacted in read
+// into (length u32, count u64, words u64[ceil(L/32)]) rows (k_gather_host, word offsets by a second
+// scan), written straight into engine-owned pinned buffers.  (A per-read 8-B slot array compacted in read
 // order cost a 400-MB fill and two passes over it for 50M reads: 0.41 ms against 0.05.)
 //
 // Tables: one ss_counter per length (1..32) or length class, pooled across calls (reset is lazy).
@@ -353,26 +353,54 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint64_t* __restrict__
     }
 }
 
-// ordered entry k -> (length, count, words at woff[k])
-__global__ __launch_bounds__(256) void k_gather_out(const uint64_t* __restrict__ ordered, uint64_t K,
-                                                    const GDesc* __restrict__ gd, const uint64_t* __restrict__ woff,
-                                                    uint64_t empty_count, uint32_t* __restrict__ out_len,
-                                                    uint64_t* __restrict__ out_cnt, uint64_t* __restrict__ out_words) {
-    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < K; k += (uint64_t)gridDim.x * 256) {
+// ordered entry k -> (length, count, words at woff[k]) straight into the pinned host result arrays
+// (no device copy, no D2H copies after it):
+// one block per 256 ordered entries; lengths and counts lane per entry, the block's words (one
+// contiguous run of the output) staged in LDS and stored lane per word, so every store to host
+// memory is a coalesced run (the device-to-host stores run at the PCIe rate, ~55 GB/s, as the blit
+// copies did, with the gather itself hidden under them).
+constexpr uint32_t kOutBuf = 4096;
+__global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict__ ordered, uint64_t K,
+                                                     const GDesc* __restrict__ gd, const uint64_t* __restrict__ woff,
+                                                     uint64_t empty_count, uint32_t* h_len, uint64_t* h_cnt,
+                                                     uint64_t* h_words) {
+    __shared__ uint64_t buf[kOutBuf];
+    __shared__ uint64_t s_lo, s_hi;
+    const uint64_t k0 = (uint64_t)blockIdx.x * 256, k = k0 + threadIdx.x;
+    uint32_t L = 0, nw = 0;
+    uint64_t cnt = 0, wo = 0;
+    const uint64_t* src = nullptr;
+    if (k < K) {
         const uint64_t v = ordered[k];
         const uint32_t g = (uint32_t)(v >> 32);
         if (g == kEmptyGroup) {
-            out_len[k] = 0;
-            out_cnt[k] = empty_count;
-            continue;
+            cnt = empty_count;
+        } else {
+            const uint64_t e = (uint32_t)v;
+            const GDesc d = gd[g];
+            L = entry_len(d, e);
+            nw = d.L ? d.W : (L + 31) / 32;
+            cnt = d.counts[e];
+            src = d.words + e * d.W;
         }
-        const uint64_t e = (uint32_t)v;
-        const GDesc d = gd[g];
-        const uint32_t L = entry_len(d, e);
-        const uint32_t nw = d.L ? d.W : (L + 31) / 32;
-        out_len[k] = L;
-        out_cnt[k] = d.counts[e];
-        for (uint32_t q = 0; q < nw; ++q) out_words[woff[k] + q] = d.words[e * d.W + q];
+        wo = woff[k];
+        h_len[k] = L;
+        h_cnt[k] = cnt;
+    }
+    const uint64_t klast = min(k0 + 255, K - 1);
+    if (k == k0) s_lo = wo;
+    if (k == klast) s_hi = wo + nw;
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi;
+    for (uint64_t c0 = lo; c0 < hi; c0 += kOutBuf) {      // one round unless the block's rows are long
+        const uint64_t c1 = min(hi, c0 + kOutBuf);
+        for (uint32_t q = 0; q < nw; ++q) {
+            const uint64_t o = wo + q;
+            if (o >= c0 && o < c1) buf[o - c0] = src[q];
+        }
+        __syncthreads();
+        for (uint64_t o = c0 + threadIdx.x; o < c1; o += 256) h_words[o] = buf[o - c0];
+        __syncthreads();
     }
 }
 
@@ -521,8 +549,6 @@ struct ss_ingest {
     // finish() results
     uint64_t nkeys = 0, nwords = 0;
     DBuf<uint64_t> slot, ordered, woff, scan;
-    DBuf<uint32_t> out_len;
-    DBuf<uint64_t> out_cnt, out_words;
     DBuf<GDesc> gdesc;
 };
 
@@ -1170,8 +1196,7 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->dbuf.release(), g->offs.release(), g->dlens.release(), g->order.release(), g->blkhist.release();
     g->blkfirst.release(), g->split_out.release(), g->rows.release(), g->first_bad.release();
     g->fq_ws.release(), g->fq_aux.release(), g->fq_counts.release();
-    g->slot.release(), g->ordered.release(), g->woff.release(), g->scan.release(), g->out_len.release();
-    g->out_cnt.release(), g->out_words.release(), g->gdesc.release();
+    g->slot.release(), g->ordered.release(), g->woff.release(), g->scan.release(), g->gdesc.release();
     g->cls_words.release(), g->cls_fps.release(), g->hll.release(), g->ovf.release();
     g->cls_flag.release();
     if (g->fpt) ss_counter_destroy(g->fpt);
@@ -1432,9 +1457,10 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
         K += gr->m;
         NW += gr->nw;
     }
+    // results -> pinned host: lens [K] u32 | pad | counts [K] u64 | words [NW] u64, written by the gather
+    const uint64_t lb = (K * 4 + 15) & ~15ull, cb = K * 8, wb = NW * 8;
     if ((rc = g->gdesc.ensure(desc.size() + 1)) || (rc = g->ordered.ensure(K + 1)) ||
-        (rc = g->woff.ensure(std::max(K, NB) + 1)) || (rc = g->out_len.ensure(K + 1)) || (rc = g->out_cnt.ensure(K + 1)) ||
-        (rc = g->out_words.ensure(NW + 1)))
+        (rc = g->woff.ensure(std::max(K, NB) + 1)) || (rc = g->out_host.ensure(lb + cb + wb + 16)))
         return rc;
     if (!desc.empty())
         rc = ss_check(hipMemcpyAsync(g->gdesc.p, desc.data(), desc.size() * sizeof(GDesc), hipMemcpyHostToDevice, s),
@@ -1459,14 +1485,11 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p);
-    hipLaunchKernelGGL(k_gather_out, dim3(grid_of(K, 256)), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
-                       g->woff.p, g->empty_count, g->out_len.p, g->out_cnt.p, g->out_words.p);
-    // results -> pinned host: lens [K] u32 | pad | counts [K] u64 | words [NW] u64
-    const uint64_t lb = (K * 4 + 15) & ~15ull, cb = K * 8, wb = NW * 8;
-    if ((rc = g->out_host.ensure(lb + cb + wb + 16))) return rc;
-    rc = ss_check(hipMemcpyAsync(g->out_host.p, g->out_len.p, K * 4, hipMemcpyDeviceToHost, s), "ingest out");
-    if (!rc) rc = ss_check(hipMemcpyAsync(g->out_host.p + lb, g->out_cnt.p, cb, hipMemcpyDeviceToHost, s), "ingest out");
-    if (!rc && wb) rc = ss_check(hipMemcpyAsync(g->out_host.p + lb + cb, g->out_words.p, wb, hipMemcpyDeviceToHost, s), "ingest out");
+    if (K >= (1ull << 31) * 256) return ss_fail(SS_EARG, "ingest: too many distinct keys for one gather");
+    hipLaunchKernelGGL(k_gather_host, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, g->ordered.p, K,
+                       (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, (uint32_t*)g->out_host.p,
+                       (uint64_t*)(g->out_host.p + lb), (uint64_t*)(g->out_host.p + lb + cb));
+    rc = ss_check(hipGetLastError(), "k_gather_host");
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest out");
     if (rc) return rc;
     g->nkeys = K;
