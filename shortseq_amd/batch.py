@@ -863,6 +863,19 @@ class GpuCounter:
               "ss_counter_extract_words")
         return fps, lens, words, counts, first, parts
 
+    def merge_words(self, words: torch.Tensor, counts: torch.Tensor, first: torch.Tensor) -> None:
+        """Fold rows of packed multi-word keys (int64 [m, W], W = the handle's words) with their counts
+        and global first indices into the table (ss_counter_merge_words: keys already present add
+        their counts and keep the smaller first index)."""
+        m = words.shape[0]
+        if m == 0:
+            return
+        if words.dim() != 2 or words.shape[1] != self.words:
+            raise ValueError("merge_words: rows of the handle's word count")
+        w, c, f = (x.contiguous() for x in (words, counts.to(torch.int64), first.to(torch.int64)))
+        check(lib().ss_counter_merge_words(self._h, w.data_ptr(), c.data_ptr(), f.data_ptr(), m,
+                                           _stream(self.device)), "ss_counter_merge_words")
+
     def items_words(self):
         """Host copy of (words u64 [m, W], counts, first) in table order (unsorted)."""
         _, _, words, counts, first, parts = self.extract_words(1)

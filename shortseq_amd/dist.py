@@ -15,6 +15,13 @@ insert aggregates) are split into `world` contiguous ranges, rank p owning
 The result is the union of the ranks' owned regions; gather_items() brings it to one rank in
 first-occurrence order (the reference dict's insertion order, counter.pyx:41-54).
 
+Keys longer than 32 nt (ShortSeq192 / ShortSeqVar keys, W = ceil(L / 32) packed words, counted under
+a 64-bit fingerprint with equality on the words): the owner is owner_of(fingerprint); each rank
+extracts its entries grouped by owner (GpuCounter.extract_words), sends the other owners' rows
+(W words, count, first) in one all_to_all_single of int64 rows, and folds what it receives into its
+own table (GpuCounter.merge_words: find / claim on the words).  owned_items() / gather_items() then
+return the words rows.
+
 Encode / decode / hamming need no collective at all: their shards are independent.
 """
 from __future__ import annotations
@@ -78,6 +85,26 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, part
     return out + (rc_l,) if with_sizes else out
 
 
+def exchange_rows(rows: torch.Tensor, part_counts, group=None):
+    """All-to-all of owner-grouped int64 rows ([m, k], part_counts[r] rows for rank r in rank order):
+    one small all-to-all of the sizes, one host sync, one all-to-all of the rows.  Returns (the rows
+    this rank receives in source-rank order, per-source sizes)."""
+    world = dist.get_world_size(group)
+    dev = rows.device
+    if dev.type != "cpu" and dist.get_backend(group) == "gloo":
+        out, sizes = exchange_rows(rows.cpu(), torch.as_tensor(part_counts).cpu(), group)
+        return out.to(dev), sizes
+    sc = torch.as_tensor(part_counts, dtype=torch.int64).to(dev)
+    rc = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rc, sc, group=group)
+    host = torch.cat([sc, rc]).cpu().tolist()                            # the one host sync
+    sc_l, rc_l = [int(x) for x in host[:world]], [int(x) for x in host[world:]]
+    m = sum(sc_l)
+    recv = torch.empty((sum(rc_l), rows.shape[1]), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(recv, rows[:m].contiguous(), output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
+    return recv, rc_l
+
+
 def exchange_packed(rec: torch.Tensor, part_counts: torch.Tensor, first_base: int, group=None,
                     extra: torch.Tensor = None):
     """All-to-all of owner-grouped packed records (int64 [m, 2] = 16 B each, ss_counter_pack_ranges).
@@ -139,6 +166,9 @@ class ShardedCounter:
         self.local.insert(ascii_local, L, base_index=base_index, check_errors=check_errors)
         if self.world == 1:
             return self.local
+        if L > 32:
+            self._exchange_words()
+            return self.local
         # the other owners' regions as 16-B records (the rank's own part stays in its table)
         rec, parts = self.local.pack_ranges(self.world, skip=self.rank, first_base=base_index)
         # the table's overflow word rides along the exchange's one host sync
@@ -154,11 +184,35 @@ class ShardedCounter:
         self.local.merge_packed(recv, runs, self.rank, self.world, L)
         return self.local
 
+    def _exchange_words(self) -> None:
+        """Multi-word keys: the other owners' rows (W words, count, first) out in one all-to-all, the
+        received rows folded into this rank's table (merge_words)."""
+        _fps, _lens, words, counts, first, parts = self.local.extract_words(self.world)
+        pc = [int(x) for x in parts.cpu().tolist()]
+        starts = np.cumsum([0] + pc).tolist()
+        a, b = starts[self.rank], starts[self.rank + 1]
+        W = words.shape[1]
+        rows = torch.cat([words[:starts[-1]], counts[:starts[-1], None], first[:starts[-1], None]], 1)
+        send = torch.cat([rows[:a], rows[b:]], 0)                          # this rank's own part stays
+        sizes = list(pc)
+        sizes[self.rank] = 0
+        recv, _rs = exchange_rows(send, sizes, group=self.group)
+        if recv.shape[0]:
+            self.local.merge_words(recv[:, :W].contiguous(), recv[:, W].contiguous(), recv[:, W + 1].contiguous())
+        if self.local.overflowed():
+            raise RuntimeError("counter table overflow (a count or first index past 32 bits, or the table)")
+
     def owned(self):
         return self.local
 
     def owned_items(self):
-        """(keys, counts, first) of the regions this rank owns, on its device."""
+        """(keys, counts, first) of the regions this rank owns, on its device (keys: words [m, W] for
+        keys longer than 32 nt)."""
+        if self.L is not None and self.L > 32:
+            _fps, _lens, words, counts, first, parts = self.local.extract_words(self.world)
+            starts = [0] + np.cumsum(parts.cpu().numpy()).tolist()
+            a, b = int(starts[self.rank]), int(starts[self.rank + 1])
+            return words[a:b], counts[a:b], first[a:b]
         if self.world == 1:
             keys, _l, counts, first, parts = self.local.extract(n_parts=1)
             m = int(parts.sum().item())
@@ -172,6 +226,20 @@ class ShardedCounter:
         """All owners' entries on rank `dst`, sorted by first occurrence: (keys u64, counts, first)
         as numpy arrays on dst, None elsewhere."""
         k, c, f = self.owned_items()
+        if k.dim() == 2:                     # multi-word keys: rows of (W words, count, first)
+            if self.world > 1:
+                sizes = [0] * self.world
+                sizes[dst] = k.shape[0]
+                W = k.shape[1]
+                rows, _ = exchange_rows(torch.cat([k, c[:, None], f[:, None]], 1), sizes, group=self.group)
+                k, c, f = rows[:, :W], rows[:, W], rows[:, W + 1]
+            if self.rank != dst:
+                return None
+            kk = k.cpu().numpy().view(np.uint64)
+            cc = c.cpu().numpy()
+            ff = f.cpu().numpy()
+            o = np.argsort(ff, kind="stable")
+            return kk[o], cc[o], ff[o]
         if self.world > 1:
             sizes = torch.zeros(self.world, dtype=torch.int64, device=self.device)
             sizes[dst] = k.numel()

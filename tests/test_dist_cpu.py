@@ -41,10 +41,48 @@ class HostTable:
         n = a.size // L
         words, rc, _ = oracle.encode_batch(a, n, L)
         assert rc == 0
-        for i, w in enumerate(words[:, 0]):
-            k = int(w)
+        self.W = words.shape[1] if L > 32 else 1
+        for i in range(n):
+            k = tuple(int(x) for x in words[i, :self.W]) if L > 32 else int(words[i, 0])
             c, f = self.d.get(k, (0, 1 << 62))
             self.d[k] = (c + 1, min(f, base_index + i))
+
+    # multi-word keys (L > 32): rows of W words; the owner is owner_of(fingerprint) as on the device
+    @staticmethod
+    def _fp(words):
+        m = (1 << 64) - 1
+
+        def mix(z):
+            z = (z + 0x9E3779B97F4A7C15) & m
+            z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+            z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+            return z ^ (z >> 31)
+        h = 0x243F6A8885A308D3 ^ len(words)
+        for w in words:
+            h = mix(h ^ (w & m))
+        return h
+
+    def extract_words(self, n_parts=1, cap=None):
+        from shortseq_amd.dist import owner_of_np
+        ks = sorted(self.d)
+        fps = np.array([self._fp(k) for k in ks], dtype=np.uint64)
+        own = owner_of_np(fps, n_parts) if len(ks) else np.zeros(0, np.int64)
+        o = np.argsort(own, kind="stable")
+        ks = [ks[i] for i in o]
+        words = np.array(ks, dtype=np.uint64).reshape(len(ks), self.W)
+        cs = np.array([self.d[k][0] for k in ks], np.int64)
+        fs = np.array([self.d[k][1] for k in ks], np.int64)
+        parts = np.bincount(own, minlength=n_parts).astype(np.int64)
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x))  # noqa: E731
+        return (t(fps[o].view(np.int64)), t(np.zeros(len(ks), np.int32)), t(words.view(np.int64)), t(cs), t(fs),
+                t(parts))
+
+    def merge_words(self, words, counts, first):
+        ws = words.numpy().view(np.uint64)
+        for row, c, f in zip(ws.tolist(), counts.tolist(), first.tolist()):
+            k = tuple(int(x) for x in row)
+            c0, f0 = self.d.get(k, (0, 1 << 62))
+            self.d[k] = (c0 + c, min(f0, f))
 
     def _region(self, ks):
         with np.errstate(over="ignore"):
@@ -111,6 +149,24 @@ class HostTable:
                 self.d[k] = (c0 + c, min(f0, f))
 
 
+def _worker_words(rank, world, port, n, L, U, q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from shortseq_amd.dist import ShardedCounter
+        per = n // world
+        a = oracle.gen_pool_reads(7, 8, U, rank * per, per, L)
+        sc = ShardedCounter(1 << 14, device="cpu", table_factory=HostTable)
+        sc.count(torch.from_numpy(a).view(per, L), L, base_index=rank * per)
+        res = sc.gather_items(dst=0)
+        if rank == 0:
+            q.put([np.asarray(x).tolist() for x in res])
+    finally:
+        dist.destroy_process_group()
+
+
 def _worker(rank, world, port, n, L, U, q):
     sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -160,6 +216,31 @@ def test_sharded_counter_gloo(oracle, world):
     a = oracle.gen_pool_reads(5, 6, U, 0, per * world, L)
     exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(per * world)])
     assert [int(k) for k in keys] == [w[0] for (w, _L, _c, _f) in exp]
+    assert counts == [c for (_w, _L, c, _f) in exp]
+    assert first == [f for (_w, _L, _c, f) in exp]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_counter_gloo_multiword(oracle, world):
+    """Keys longer than 32 nt (L = 100: four-word keys) through the sharded counter's row exchange
+    (extract_words by owner, one all-to-all of rows, merge_words) over gloo: the gathered rows, in
+    first-occurrence order, equal oracle.count over the whole stream."""
+    n, L, U = 1800, 100, 150
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_words, args=(r, world, port, n, L, U, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    words, counts, first = res
+    per = n // world
+    a = oracle.gen_pool_reads(7, 8, U, 0, per * world, L)
+    exp = oracle.count([a[i * L:(i + 1) * L].tobytes() for i in range(per * world)])
+    assert [[int(x) for x in w] for w in words] == [[int(x) for x in w] for (w, _L, _c, _f) in exp]
     assert counts == [c for (_w, _L, c, _f) in exp]
     assert first == [f for (_w, _L, _c, f) in exp]
 
