@@ -370,6 +370,11 @@ int ss_ingest_set_exact(ss_ingest* g, int exact);
  * (its distinct keys become its first rows).  Test hook: lower that bound to `rows` (>= 1024) so the
  * re-keying runs at small sizes.  New in this ABI version. */
 int ss_ingest_set_row_limit(ss_ingest* g, uint64_t rows);
+/* A slot's count is u32: before the reads counted since the last spill pass 2^32 - 2, every table's
+ * counts move into its group's u64 row counts (added back at finish / export), so a key's count is
+ * exact past 2^32.  Test hook: spill once `reads` (1 .. 2^32 - 2) reads have been counted since the
+ * last spill.  New in this ABI version. */
+int ss_ingest_set_count_limit(ss_ingest* g, uint64_t reads);
 int ss_ingest_staging(ss_ingest* g, uint64_t nbytes, uint8_t** h_ptr);
 int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_lens, uint64_t n);
 int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, uint64_t* h_nseqs);

@@ -89,6 +89,7 @@ SIGNATURES = [
     ("ss_ingest_reset", C.c_int, [_P]),
     ("ss_ingest_set_exact", C.c_int, [_P, C.c_int]),
     ("ss_ingest_set_row_limit", C.c_int, [_P, _U64]),
+    ("ss_ingest_set_count_limit", C.c_int, [_P, _U64]),
     ("ss_ingest_staging", C.c_int, [_P, _U64, C.POINTER(C.c_void_p)]),
     ("ss_ingest_add_blob", C.c_int, [_P, _P, _P, _U64]),
     ("ss_ingest_add_fastq", C.c_int, [_P, C.c_char_p, _U64, C.POINTER(C.c_uint64)]),

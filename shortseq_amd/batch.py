@@ -508,6 +508,10 @@ class DeviceIngest:
         """Test hook: re-key a length's table once its rows pass `rows` (default 2^32 - 1)."""
         check(lib().ss_ingest_set_row_limit(self._h, int(rows)), "ss_ingest_set_row_limit")
 
+    def set_count_limit(self, reads: int) -> None:
+        """Test hook: spill the tables' u32 counts into u64 row counts every `reads` reads (default 2^32 - 2)."""
+        check(lib().ss_ingest_set_count_limit(self._h, int(reads)), "ss_ingest_set_count_limit")
+
     def export(self) -> int:
         """Extract this engine's tables for a device-side reduce (ss_ingest_export); its distinct keys."""
         k = C.c_uint64()

@@ -3526,6 +3526,30 @@ int ss_counter_extract_words(ss_counter* c, uint32_t n_parts, uint64_t* d_fps, u
 
 }  // extern "C"
 
+// Counts moved out of the slots (the drop-in engine's spill, before a slot's u32 count could wrap):
+// acc[first] += count for every entry (first = the entry's row), the slot's count set to 0 -- the
+// sentinel slot (key ~0, present iff its count is nonzero) keeps 1 and spills count - 1.
+__global__ __launch_bounds__(256) void k_spill_counts(Tbl t, uint64_t* __restrict__ acc) {
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= t.mask + 1; s += (uint64_t)gridDim.x * 256) {
+        const Slot sl = t.slots[s];
+        const bool sent = s > t.mask;
+        if (sent ? sl.ncount == 0xFFFFFFFFu : sl.key == kEmpty) continue;
+        const uint32_t cnt = ~sl.ncount, keep = sent ? 1u : 0u;
+        if (cnt <= keep || sl.first == kMaxIndex) continue;
+        acc[sl.first] += cnt - keep;
+        t.slots[s].ncount = ~keep;
+    }
+}
+
+int ss_counter_spill_counts(ss_counter* c, uint64_t* d_acc, void* stream) {
+    if (!c || !d_acc) return ss_fail(SS_EARG, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    int rc = flush_reset(c, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_spill_counts, dim3(grid_for(c->cap + 1, 256, 256 * 16)), dim3(256), 0, s, tbl_of(c), d_acc);
+    return ss_check(hipGetLastError(), "k_spill_counts");
+}
+
 int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n, const uint64_t* d_fps,
                                 const ss_flat_class* cls, uint64_t base, uint32_t* d_flag,
                                 void* stream) {

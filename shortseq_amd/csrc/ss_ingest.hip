@@ -249,6 +249,23 @@ __global__ __launch_bounds__(256) void k_merge_rows(uint64_t m, uint64_t rows, u
     }
 }
 
+// spilled counts back onto extracted entries: counts[e] += acc[first[e]] for e < *m (rows < acc_rows)
+__global__ __launch_bounds__(256) void k_add_acc(uint64_t* __restrict__ counts, const uint64_t* __restrict__ first,
+                                                 const uint64_t* __restrict__ m, const uint64_t* __restrict__ acc,
+                                                 uint64_t acc_rows) {
+    const uint64_t n = *m;
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (uint64_t)gridDim.x * 256)
+        if (first[e] < acc_rows) counts[e] += acc[first[e]];
+}
+
+// re-key with spilled counts: entry e's spilled count moves to its new row e
+__global__ __launch_bounds__(256) void k_rekey_acc(const uint64_t* __restrict__ first, uint64_t m,
+                                                   const uint64_t* __restrict__ acc, uint64_t acc_rows,
+                                                   uint64_t* __restrict__ nacc) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
+        nacc[e] = first[e] < acc_rows ? acc[first[e]] : 0ull;
+}
+
 // re-key: entry e of a group's table becomes row e (its first index), the new row map = the entry's
 // first read
 __global__ __launch_bounds__(256) void k_rekey(const uint64_t* __restrict__ first, uint64_t m,
@@ -496,6 +513,8 @@ struct Group {
     DBuf<uint32_t> lens;
     DBuf<uint64_t> xread;         // export: each entry's first read (engine-local index)
     uint64_t m = 0, nw = 0;       // extracted entries, their output words
+    DBuf<uint64_t> acc;           // row -> counts spilled out of the table (u64; rows < acc_rows)
+    uint64_t acc_rows = 0;
 };
 
 }  // namespace
@@ -541,6 +560,9 @@ struct ss_ingest {
     std::string bad_bytes;
     double est_scale = 1.0;        // FASTQ: file bytes / bytes seen (multi-word table sizing)
     bool exported = false;         // ss_ingest_export ran (the groups' m / buffers hold the entries)
+    // reads counted since the tables' counts were last spilled into the groups' u64 row counts: a
+    // slot's u32 count cannot pass it, so the spill before it reaches 2^32 - 1 keeps every count exact
+    uint64_t since_spill = 0, spill_limit = 0xFFFFFFFEull;
     uint64_t max_rows = 0xFFFFFFFFull;   // rows a group's table indexes (its first index is u32);
                                          // ss_ingest_set_row_limit lowers it (test hook)
     // ss_ingest_merge scratch (this engine as the destination): a source group's entries on this device
@@ -644,8 +666,14 @@ int group_rekey(ss_ingest* g, Group& gr) {
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest rekey");
     if (rc) return rc;
     const uint64_t m = g->h_bad[0];
-    DBuf<uint64_t> nmap;
+    DBuf<uint64_t> nmap, nacc;
     if ((rc = nmap.ensure(std::max<uint64_t>(m, gr.rows)))) return rc;
+    if (gr.acc_rows) {      // spilled counts follow their entries to the new rows
+        if ((rc = nacc.ensure(std::max<uint64_t>(m, 1)))) return rc;
+        if (m)
+            hipLaunchKernelGGL(k_rekey_acc, dim3(grid_of(m, 256)), dim3(256), 0, s, gr.first.p, m, gr.acc.p,
+                               gr.acc_rows, nacc.p);
+    }
     if (m)
         hipLaunchKernelGGL(k_rekey, dim3(grid_of(m, 256)), dim3(256), 0, s, gr.first.p, m, gr.rowmap.p, nmap.p, gr.fps.p);
     if ((rc = ss_counter_reset(gr.table, s)) || (rc = table_kind(gr, gr.table))) return rc;
@@ -657,7 +685,32 @@ int group_rekey(ss_ingest* g, Group& gr) {
     gr.rowmap = nmap;
     nmap.p = nullptr;
     nmap.cap = 0;
+    if (gr.acc_rows) {
+        gr.acc.release();
+        gr.acc = nacc;
+        nacc.p = nullptr;
+        nacc.cap = 0;
+        gr.acc_rows = m;
+    }
     gr.rows = m;
+    return SS_OK;
+}
+
+// every table's counts into its group's u64 row counts (ss_counter_spill_counts), so the next
+// 2^32 - 1 reads cannot wrap a slot's u32 count
+int spill_counts(ss_ingest* g) {
+    hipStream_t s = g->stream;
+    for (auto& kv : g->groups) {
+        Group& gr = kv.second;
+        if (!gr.table || !gr.rows) continue;
+        int rc = gr.acc.ensure_keep(gr.rows, gr.acc_rows, s);
+        if (!rc && gr.rows > gr.acc_rows)
+            rc = ss_check(hipMemsetAsync(gr.acc.p + gr.acc_rows, 0, (gr.rows - gr.acc_rows) * 8, s), "ingest spill rows");
+        if (!rc) rc = ss_counter_spill_counts(gr.table, gr.acc.p, s);
+        if (rc) return rc;
+        gr.acc_rows = gr.rows;
+    }
+    g->since_spill = 0;
     return SS_OK;
 }
 
@@ -720,6 +773,11 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (n == 0) return SS_OK;
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "ingest: a chunk holds < 2^32 reads");
+    if (g->since_spill + n > g->spill_limit) {
+        const int src = spill_counts(g);
+        if (src) return src;
+    }
+    g->since_spill += n;
     // global read indices are u64 (row maps); a table's first index is a row of its group, u32: a
     // group about to pass kMaxRows rows is re-keyed first (group_room)
     hipStream_t s = g->stream;
@@ -1065,6 +1123,9 @@ int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
                                       d_cnt + 3 * q, s);
         if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 3 * q + 1, s);
         if (rc) return rc;
+        if (gr.acc_rows)    // the counts spilled out of the table (u64) back onto its entries
+            hipLaunchKernelGGL(k_add_acc, dim3(grid_of(cap, 256)), dim3(256), 0, s, gr.counts.p, gr.first.p,
+                               (const uint64_t*)(d_cnt + 3 * q), gr.acc.p, gr.acc_rows);
         placed.push_back(&gr);
     }
     if (!placed.empty()) {
@@ -1151,8 +1212,10 @@ int ss_ingest_reset(ss_ingest* g) {
         kv.second.cap = 0;
         kv.second.rows = 0;
         kv.second.m = 0;
+        kv.second.acc_rows = 0;
     }
     g->nreads = 0;
+    g->since_spill = 0;
     g->empty_count = 0;
     g->empty_first = kNoSlot;
     g->bad_index = kNoSlot;
@@ -1164,6 +1227,13 @@ int ss_ingest_reset(ss_ingest* g) {
     g->exported = false;
     if (!g->hll.p) return SS_OK;
     return ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
+}
+
+int ss_ingest_set_count_limit(ss_ingest* g, uint64_t reads) {
+    if (!g) return ss_fail(SS_EARG, "null ingest");
+    if (reads < 1 || reads > 0xFFFFFFFEull) return ss_fail(SS_EARG, "count limit in 1 .. 2^32 - 2");
+    g->spill_limit = reads;
+    return SS_OK;
 }
 
 int ss_ingest_set_row_limit(ss_ingest* g, uint64_t rows) {
@@ -1544,6 +1614,10 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
                              : hipMemcpyAsync(d, p, bytes, hipMemcpyDeviceToDevice, s),
                         "ingest merge copy");
     };
+    // the source's reads count toward the destination's spill: its slots stay below 2^32 after the merge
+    // (one source's key past 2^32 - 1 copies still raises SS_EFULL)
+    if (dst->since_spill + src->nreads > dst->spill_limit && (rc = spill_counts(dst))) return rc;
+    dst->since_spill += std::min<uint64_t>(src->nreads, dst->spill_limit);
     const double scale = dst->est_scale;
     dst->est_scale = 1.0;            // a new group is sized by the entries it receives
     for (auto& kv : src->groups) {

@@ -64,6 +64,10 @@ struct ss_flat_class {
 extern "C" int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n,
                                            const uint64_t* d_fps, const ss_flat_class* cls, uint64_t base,
                                            uint32_t* d_flag, void* stream);
+// Every entry's count moved into d_acc[first] (u64, indexed by the entry's first index: the drop-in
+// engine's rows) and the slot's count zeroed (the single-word sentinel keeps 1), so later inserts
+// cannot wrap a slot's u32 count (k_spill_counts).
+extern "C" int ss_counter_spill_counts(ss_counter* c, uint64_t* d_acc, void* stream);
 // HyperLogLog registers (2^kHllLog u32 at d_hll) of m packed rows of W1 words, k_encode_classes' hash.
 extern "C" int ss_hll_rows_impl(const uint64_t* d_rows, uint64_t m, uint32_t W1, uint32_t* d_hll, void* stream);
 // Drop-in engine (ss_ingest), one multi-word length class: rows of W words + the length (k_encode_class).
