@@ -588,90 +588,139 @@ __global__ __launch_bounds__(kClsTile) __attribute__((amdgpu_waves_per_eu(6))) v
 // R = 64 / S reads per group, S lanes each (lane w: word w, the length at w == W, 0 past it), and
 // kRowsK groups: the groups' length / offset loads, then their chunk loads, go out together (one
 // group per wave measured 3.35 ms on the f2 batch: three dependent round trips for 1 KB of input).
-// The words are k_encode_classes' phase b (16-B chunk loads, funnel shift, the rare odd word
-// re-encoded exactly).  The row fingerprint (words_fp over the W + 1 words) is folded across the
+// The words are k_encode_classes' phase b (16-B chunks, funnel shift, the rare odd word re-encoded
+// exactly), each chunk of a read loaded by one lane only.  The row fingerprint (words_fp over the W + 1 words) is folded across the
 // read's lanes with shuffles; lane 0 of the read stores it and updates its class's sketch.  Reads
 // that are not class reads (empty: the length split counts those) get a zero row and the
 // fingerprint of one zero word, an entry the fold skips.
 constexpr int kRowsK = 4;
-__global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const uint64_t* __restrict__ offs,
-                                                     const uint32_t* __restrict__ lens, uint64_t n, uint32_t S,
-                                                     uint64_t* __restrict__ out, uint64_t* __restrict__ fps,
-                                                     uint32_t* hll, unsigned long long* first_bad) {
-    const uint32_t lane = threadIdx.x & 63u, R = 64u / S;
-    const uint32_t i = lane / S, w = lane - i * S;
-    const uint64_t r0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * R * kRowsK + i;
-    const uint4* in16 = (const uint4*)in;
-    uint32_t L[kRowsK];
-    uint64_t off[kRowsK];
-#pragma unroll
-    for (int k = 0; k < kRowsK; ++k) {
-        const uint64_t r = r0 + (uint64_t)k * R;
-        const uint64_t rc = (i < R && r < n) ? r : 0;
-        L[k] = (i < R && r < n) ? lens[rc] : 0u;
-        off[k] = offs[rc];
-    }
-    uint4 xa[kRowsK], xb[kRowsK], xc[kRowsK];
-#pragma unroll
-    for (int k = 0; k < kRowsK; ++k) {
-        // clamped, unconditional loads: a lane with no word of its read reloads the read's first
-        // chunk, one of an empty read (its offset may be the blob's end) the blob's first
-        const uint32_t W = (L[k] + 31u) / 32u;
-        const uint32_t ww = w < W ? w : 0u;
-        const uint32_t nb = L[k] ? min(32u, L[k] - 32u * ww) : 1u, sh = (uint32_t)(off[k] & 15u);
-        const uint32_t last = L[k] ? (sh + nb - 1u) >> 4 : 0u;
-        const uint64_t c0 = L[k] ? (off[k] >> 4) + 2u * ww : 0u;
-        xa[k] = in16[c0];
-        xb[k] = in16[c0 + min(1u, last)];
-        xc[k] = in16[c0 + min(2u, last)];
-    }
-    __shared__ uint64_t srow[4][kRowsK * 64];     // the wave's rows (group k: lanes k * 64 ..)
-    __shared__ uint16_t slen[4][kRowsK * 24];     // the wave's reads' lengths (read j = k * R + i; R <= 21)
-    const uint32_t wave = threadIdx.x >> 6;
+__device__ __forceinline__ void rows_meta(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
+                                          uint64_t n, uint64_t r0, uint32_t R, uint32_t i, uint32_t* L,
+                                          uint64_t* off) {
 #pragma unroll
     for (int k = 0; k < kRowsK; ++k) {
         const uint64_t r = r0 + (uint64_t)k * R;
         const bool live = i < R && r < n;
-        const uint32_t W = (L[k] + 31u) / 32u;
-        const bool cls = L[k] > 32u && W < S;
-        uint64_t word = 0;
-        uint32_t bad = 0;
-        if (cls && w < W) {
-            const uint32_t nb = min(32u, L[k] - 32u * w), sh = (uint32_t)(off[k] & 15u);
-            uint32_t odd = 0;
-            const uint32_t ca = code_chunk(xa[k], odd), cb = code_chunk(xb[k], odd), cc = code_chunk(xc[k], odd);
-            const uint64_t lo64 = (uint64_t)cb << 32 | ca;
-            word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)cc << (64u - 2u * sh)) : lo64;
-            if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
-            if (odd) word = encode_word_q(in + off[k] + 32u * w, nb, nb < 32u, bad);   // rare: exact semantics
-        } else if (cls && w == W) {
-            word = L[k];
+        L[k] = live ? lens[r] : 0u;
+        off[k] = live ? offs[r] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const uint64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ lens, uint64_t n, uint32_t S,
+                                                     uint64_t* __restrict__ out, uint64_t* __restrict__ fps,
+                                                     uint32_t* hll, unsigned long long* first_bad) {
+    const uint32_t lane = threadIdx.x & 63u, R = 64u / S, wave = threadIdx.x >> 6;
+    const uint32_t i = lane / S, w = lane - i * S;
+    const uint64_t per = (uint64_t)R * kRowsK, tiles = (n + per - 1) / per, stride = (uint64_t)gridDim.x * 4;
+    const uint4* in16 = (const uint4*)in;
+    __shared__ uint64_t srow[4][kRowsK * 64];     // the wave's rows (group k: lanes k * 64 ..)
+    __shared__ uint16_t slen[4][kRowsK * 24];     // the wave's reads' lengths (read j = k * R + i; R <= 21)
+    uint32_t L[kRowsK];
+    uint64_t off[kRowsK];
+    uint64_t tile = (uint64_t)blockIdx.x * 4 + wave;
+    rows_meta(offs, lens, n, tile * per + i, R, i, L, off);
+    uint32_t* hreg[2] = {nullptr, nullptr};       // the previous tile's sketch updates (<= 2 reads a lane)
+    uint32_t hval[2] = {0, 0}, hrho[2] = {0, 0};
+    for (; tile < tiles; tile += stride) {
+        const uint64_t r0 = tile * per + i;
+        // the read's 16-B chunks once each: lane w loads chunks 2w and 2w + 1 of its read (relative to
+        // the read's first chunk, clamped to its last), the length lane W only chunk 2W when the read
+        // reaches it; word w's third chunk 2w + 2 is lane w + 1's first (a shuffle).  Lanes past W load
+        // nothing.
+        uint4 xa[kRowsK], xb[kRowsK];
+#pragma unroll
+        for (int k = 0; k < kRowsK; ++k) {
+            const uint32_t W = (L[k] + 31u) / 32u;
+            const uint64_t cb = off[k] >> 4;
+            const uint32_t lastc = L[k] ? (uint32_t)(((off[k] + L[k] - 1u) >> 4) - cb) : 0u;
+            xa[k] = make_uint4(0u, 0u, 0u, 0u);
+            xb[k] = xa[k];
+            if (L[k] && w <= W && 2u * w <= lastc) xa[k] = in16[cb + 2u * w];
+            if (L[k] && w < W) xb[k] = in16[cb + min(2u * w + 1u, lastc)];
         }
-        if (live) out[r * S + w] = word;
-        report_bad(bad != 0u, r, first_bad);
-        srow[wave][k * 64 + lane] = word;
-        if (w == 0 && i < R) slen[wave][k * R + i] = (uint16_t)(cls ? L[k] : 0u);
-    }
-    __syncthreads();
-    // lane per read: its row's fingerprint (words_fp over W + 1 words; one zero word for a read that
-    // is no class read) and its class's sketch -- one chain per read, not one per word lane
-    const uint64_t rb = ((uint64_t)blockIdx.x * 4 + wave) * R * kRowsK;
-    for (uint32_t j = lane; j < R * kRowsK && rb + j < n; j += 64) {
-        const uint32_t k = j / R, ii = j - k * R;
-        const uint32_t LL = slen[wave][j];
-        const uint32_t W1 = LL ? (LL + 31u) / 32u + 1u : 1u;
-        const uint64_t* row = &srow[wave][k * 64 + ii * S];
-        uint64_t rw[6];                     // all LDS reads issued before the chain (S <= 6)
+        // the next tile's lengths / offsets go out behind the chunks
+        uint32_t nL[kRowsK];
+        uint64_t noff[kRowsK];
+        rows_meta(offs, lens, n, (tile + stride) * per + i, R, i, nL, noff);
 #pragma unroll
-        for (uint32_t q = 0; q < 6; ++q) rw[q] = row[min(q, S - 1)];
-        uint64_t h = 0x243F6A8885A308D3ull ^ W1;
+        for (int k = 0; k < kRowsK; ++k) {
+            const uint64_t r = r0 + (uint64_t)k * R;
+            const bool live = i < R && r < n;
+            const uint32_t W = (L[k] + 31u) / 32u;
+            const bool cls = L[k] > 32u && W < S;
+            uint4 xn;                           // lane w + 1's first chunk (every lane shuffles)
+            xn.x = __shfl_down(xa[k].x, 1);
+            xn.y = __shfl_down(xa[k].y, 1);
+            xn.z = __shfl_down(xa[k].z, 1);
+            xn.w = __shfl_down(xa[k].w, 1);
+            uint64_t word = 0;
+            uint32_t bad = 0;
+            if (cls && w < W) {
+                const uint32_t nb = min(32u, L[k] - 32u * w), sh = (uint32_t)(off[k] & 15u);
+                const uint32_t last = (sh + nb - 1u) >> 4;
+                uint32_t odd = 0;
+                const uint32_t ca = code_chunk(xa[k], odd), cb = code_chunk(xb[k], odd);
+                const uint32_t cc = last == 2u ? code_chunk(xn, odd) : cb;
+                const uint64_t lo64 = (uint64_t)cb << 32 | ca;
+                word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)cc << (64u - 2u * sh)) : lo64;
+                if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
+                if (odd) word = encode_word_q(in + off[k] + 32u * w, nb, nb < 32u, bad);   // rare: exact semantics
+            } else if (cls && w == W) {
+                word = L[k];
+            }
+            if (live) out[r * S + w] = word;
+            report_bad(bad != 0u, r, first_bad);
+            srow[wave][k * 64 + lane] = word;
+            if (w == 0 && i < R) slen[wave][k * R + i] = (uint16_t)(cls ? L[k] : 0u);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");     // srow / slen are the wave's own
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the previous tile's sketch registers (loaded a tile ago) settle now
 #pragma unroll
-        for (uint32_t q = 0; q < 6; ++q)
-            if (q < W1) h = splitmix64(h ^ rw[q]);
-        if (h == ~0ull) h = ~1ull;
-        fps[rb + j] = h;
-        if (LL) hll_add(hll + ((uint64_t)(W1 - 1) << kHllLog), h, W1);
+        for (int p = 0; p < 2; ++p)
+            if (hreg[p] && hval[p] < hrho[p]) atomicMax(hreg[p], hrho[p]);
+        // lane per read: its row's fingerprint (words_fp over W + 1 words; one zero word for a read
+        // that is no class read) and its class's sketch register -- one chain per read
+        const uint64_t rb = tile * per;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const uint32_t j = lane + 64u * p;
+            hreg[p] = nullptr;
+            if (j >= per || rb + j >= n) continue;
+            const uint32_t k = j / R, ii = j - k * R;
+            const uint32_t LL = slen[wave][j];
+            const uint32_t W1 = LL ? (LL + 31u) / 32u + 1u : 1u;
+            const uint64_t* row = &srow[wave][k * 64 + ii * S];
+            uint64_t rw[6];                     // all LDS reads issued before the chain (S <= 6)
+#pragma unroll
+            for (uint32_t q = 0; q < 6; ++q) rw[q] = row[min(q, S - 1)];
+            uint64_t h = 0x243F6A8885A308D3ull ^ W1;
+#pragma unroll
+            for (uint32_t q = 0; q < 6; ++q)
+                if (q < W1) h = splitmix64(h ^ rw[q]);
+            if (h == ~0ull) h = ~1ull;
+            fps[rb + j] = h;
+            if (LL) {       // hll_add, its register's load left in flight until the next tile
+                const uint64_t hh = splitmix64(h ^ W1);
+                hreg[p] = hll + ((uint64_t)(W1 - 1) << kHllLog) + (uint32_t)(hh >> (64 - kHllLog));
+                hrho[p] = (uint32_t)__clzll((hh << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
+                hval[p] = *hreg[p];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");     // this tile's LDS reads before the next's writes
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int k = 0; k < kRowsK; ++k) {
+            L[k] = nL[k];
+            off[k] = noff[k];
+        }
     }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+        if (hreg[p] && hval[p] < hrho[p]) atomicMax(hreg[p], hrho[p]);
 }
 
 // The same registers from rows already packed (k_encode_class's paths): lane per row, the same hash.
@@ -1300,8 +1349,18 @@ int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint
                         uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
     if (S < 3 || S > 6) return ss_fail(SS_EARG, "k_encode_rows: rows of 3 to 6 words");
     if (n == 0) return SS_OK;
-    const uint64_t per = (uint64_t)(64 / S) * kRowsK, waves = (n + per - 1) / per, blocks = (waves + 3) / 4;
-    if (blocks > 0x7FFFFFFFull) return ss_fail(SS_EARG, "k_encode_rows: chunk too large");
+    // persistent waves (the occupancy's worth of blocks), each over tiles of R * kRowsK reads with the
+    // next tile's lengths / offsets and the last tile's sketch registers in flight
+    static int resident = 0;
+    if (!resident) {
+        int dev = 0, cus = 0, occ = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_encode_rows, 256, 0);
+        resident = std::max(1, cus) * std::max(1, occ);
+    }
+    const uint64_t per = (uint64_t)(64 / S) * kRowsK, tiles = (n + per - 1) / per;
+    const uint64_t blocks = std::min<uint64_t>((tiles + 3) / 4, (uint64_t)resident);
     hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, d_buf, d_offs, d_lens,
                        n, S, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_rows");
