@@ -61,7 +61,8 @@ constexpr uint32_t kClassBin0 = 31;                 // bin of class W = kClassBi
 constexpr uint32_t kTooLongBin = kClassBin0 + SS_MAX_NT / 32 + 1;
 constexpr uint32_t kLenBins = kTooLongBin + 1;
 // k_len_count / k_len_scatter: one wave per block, 8 per SIMD (2048 blocks, 2 per SIMD, left both
-// passes latency-bound: 0.21 + 0.49 ms for 50M reads)
+// passes latency-bound: 0.21 + 0.49 ms for 50M reads), 8 steps' lengths loaded at once (one a step:
+// the f2 count 50 us slower, profiles/r4/f2/libab_lenstep.log)
 constexpr uint32_t kSplitBlocks = 8192;
 constexpr uint32_t kEmptyGroup = 0xFFFFFFFFu;       // slot marker of the empty read's entry
 constexpr uint64_t kNoSlot = ~0ull;
@@ -82,20 +83,32 @@ __global__ __launch_bounds__(64) void k_len_count(const uint32_t* __restrict__ l
     const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
     // wave-aggregated: one LDS update per distinct bin of a step (the lanes of a bin counted by a
     // ballot, its first read = the step's lowest lane of that bin), not an LDS atomic pair per read
-    for (uint64_t i0 = lo; i0 < hi; i0 += 64) {
-        const uint64_t i = i0 + threadIdx.x;
-        const bool live = i < hi;
-        const uint32_t b = live ? len_bin(lens[i]) : 0u;
-        uint64_t pending = __ballot(live);
-        while (pending) {
-            const int leader = __ffsll((long long)pending) - 1;
-            const uint32_t b0 = (uint32_t)__shfl((int)b, leader);
-            const uint64_t mine = __ballot(live && b == b0);
-            if (threadIdx.x == (uint32_t)leader) {
-                h[b0] += (uint32_t)__popcll(mine);
-                if (f[b0] == 0xFFFFFFFFu) f[b0] = (uint32_t)(i0 + (uint64_t)leader);   // steps go in read order
+    // kLenStep steps' lengths loaded before any is binned (one load per step left the pass
+    // latency-bound: 130 us for 50M reads)
+    constexpr int kLenStep = 8;
+    for (uint64_t s0 = lo; s0 < hi; s0 += 64 * kLenStep) {
+        uint32_t bs[kLenStep];
+#pragma unroll
+        for (int k = 0; k < kLenStep; ++k) {
+            const uint64_t i = s0 + 64u * k + threadIdx.x;
+            bs[k] = i < hi ? len_bin(lens[i]) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kLenStep; ++k) {
+            const uint64_t i0 = s0 + 64u * k;
+            const bool live = i0 + threadIdx.x < hi;
+            const uint32_t b = bs[k];
+            uint64_t pending = __ballot(live);
+            while (pending) {
+                const int leader = __ffsll((long long)pending) - 1;
+                const uint32_t b0 = (uint32_t)__shfl((int)b, leader);
+                const uint64_t mine = __ballot(live && b == b0);
+                if (threadIdx.x == (uint32_t)leader) {
+                    h[b0] += (uint32_t)__popcll(mine);
+                    if (f[b0] == 0xFFFFFFFFu) f[b0] = (uint32_t)(i0 + (uint64_t)leader);   // steps go in read order
+                }
+                pending &= ~mine;
             }
-            pending &= ~mine;
         }
     }
     __syncthreads();
@@ -107,9 +120,9 @@ __global__ __launch_bounds__(64) void k_len_count(const uint32_t* __restrict__ l
 
 // one block per length bin: exclusive scan of the bin's per-block counts (bin-major rows of blkhist,
 // in place) -> offsets inside the bin; out[b] = bin total, out[kLenBins + b] = first read of the bin
-__global__ __launch_bounds__(256) void k_len_binscan(uint32_t nblk, uint32_t* __restrict__ blkhist,
-                                                     const uint32_t* __restrict__ blkfirst, uint64_t* __restrict__ out) {
-    __shared__ uint32_t wsum[4];
+__global__ __launch_bounds__(1024) void k_len_binscan(uint32_t nblk, uint32_t* __restrict__ blkhist,
+                                                      const uint32_t* __restrict__ blkfirst, uint64_t* __restrict__ out) {
+    __shared__ uint32_t wsum[16];
     __shared__ uint32_t run, fmin;
     const uint32_t b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* row = blkhist + (uint64_t)b * nblk;
@@ -120,7 +133,7 @@ __global__ __launch_bounds__(256) void k_len_binscan(uint32_t nblk, uint32_t* __
     }
     __syncthreads();
     uint32_t f = 0xFFFFFFFFu;
-    for (uint32_t k0 = 0; k0 < nblk; k0 += 256) {
+    for (uint32_t k0 = 0; k0 < nblk; k0 += 1024) {
         const uint32_t k = k0 + threadIdx.x;
         const uint32_t v = k < nblk ? row[k] : 0u;
         if (k < nblk) f = min(f, frow[k]);
@@ -135,7 +148,8 @@ __global__ __launch_bounds__(256) void k_len_binscan(uint32_t nblk, uint32_t* __
         for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
         if (k < nblk) row[k] = before + incl - v;
         __syncthreads();
-        if (threadIdx.x == 0) run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (threadIdx.x == 0)
+            for (uint32_t w = 0; w < 16; ++w) run += wsum[w];
         __syncthreads();
     }
     if (f != 0xFFFFFFFFu) atomicMin(&fmin, f);
@@ -178,24 +192,34 @@ __global__ __launch_bounds__(64) void k_len_scatter(const uint32_t* __restrict__
     const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
     const uint32_t lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1ull;
-    for (uint64_t i0 = lo; i0 < hi; i0 += 64) {
-        const uint64_t i = i0 + lane;
-        const bool live = i < hi;
-        const uint32_t b = live ? len_bin(lens[i]) : 0u;
-        uint64_t pending = __ballot(live);
-        while (pending) {
-            const int leader = __ffsll((long long)pending) - 1;
-            const uint32_t b0 = (uint32_t)__shfl((int)b, leader);
-            const uint64_t mine = __ballot(live && b == b0);
-            const uint32_t base = cur[b0];
-            if (live && b == b0) {
-                const uint32_t pos = base + (uint32_t)__popcll(mine & lt);
-                order[pos] = i;
+    constexpr int kLenStep = 8;         // as k_len_count: the steps' lengths loaded together
+    for (uint64_t s0 = lo; s0 < hi; s0 += 64 * kLenStep) {
+        uint32_t bs[kLenStep];
+#pragma unroll
+        for (int k = 0; k < kLenStep; ++k) {
+            const uint64_t i = s0 + 64u * k + lane;
+            bs[k] = i < hi ? len_bin(lens[i]) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kLenStep; ++k) {
+            const uint64_t i = s0 + 64u * k + lane;
+            const bool live = i < hi;
+            const uint32_t b = bs[k];
+            uint64_t pending = __ballot(live);
+            while (pending) {
+                const int leader = __ffsll((long long)pending) - 1;
+                const uint32_t b0 = (uint32_t)__shfl((int)b, leader);
+                const uint64_t mine = __ballot(live && b == b0);
+                const uint32_t base = cur[b0];
+                if (live && b == b0) {
+                    const uint32_t pos = base + (uint32_t)__popcll(mine & lt);
+                    order[pos] = i;
+                }
+                __syncthreads();   // one wave: orders the cursor read before the update
+                if (lane == (uint32_t)leader) cur[b0] = base + (uint32_t)__popcll(mine);
+                __syncthreads();
+                pending &= ~mine;
             }
-            __syncthreads();   // one wave: orders the cursor read before the update
-            if (lane == (uint32_t)leader) cur[b0] = base + (uint32_t)__popcll(mine);
-            __syncthreads();
-            pending &= ~mine;
         }
     }
 }
@@ -796,7 +820,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins)))
             return rc;
         hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p, g->blkfirst.p);
-        hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(256), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
+        hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(1024), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
                            g->split_out.p);
         hipLaunchKernelGGL(k_len_binstart, dim3(1), dim3(1024), 0, s, g->split_out.p);
         rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, 3 * kLenBins * 8, hipMemcpyDeviceToHost, s),
