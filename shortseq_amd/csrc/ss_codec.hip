@@ -386,8 +386,11 @@ struct ClassOut {
 };
 constexpr uint32_t kClsTile = 256;
 
+// the class's sketch register from the fingerprint's own bits (words_fp ends in a full mix; the
+// class width is in its seed)
 __device__ __forceinline__ void hll_add(uint32_t* reg_base, uint64_t fp, uint32_t W1) {
-    const uint64_t h = splitmix64(fp ^ W1);
+    (void)W1;
+    const uint64_t h = fp;
     uint32_t* reg = reg_base + (uint32_t)(h >> (64 - kHllLog));
     const uint32_t rho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
     if (*reg < rho) atomicMax(reg, rho);    // registers settle early: most reads only load
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(kClsTile) __attribute__((amdgpu_waves_per_eu(6))) v
             const uint64_t fp = words_fp(sw + cbase[W] + srow[t] * w1, w1);
             if (fps) fps[co.fpoff[W] + row] = fp;
             if (co.rmap[W]) co.rmap[W][row] = co.base + r;
-            const uint64_t h = splitmix64(fp ^ w1);       // hll_add's register and rank
+            const uint64_t h = fp;                         // hll_add's register and rank
             hreg = hll + ((uint64_t)W << kHllLog) + (uint32_t)(h >> (64 - kHllLog));
             hrho = (uint32_t)__clzll((h << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
             hval = *hreg;
@@ -696,14 +699,14 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
             uint64_t rw[6];                     // all LDS reads issued before the chain (S <= 6)
 #pragma unroll
             for (uint32_t q = 0; q < 6; ++q) rw[q] = row[min(q, S - 1)];
-            uint64_t h = 0x243F6A8885A308D3ull ^ W1;
+            uint64_t h = fp_seed(W1);
 #pragma unroll
             for (uint32_t q = 0; q < 6; ++q)
-                if (q < W1) h = splitmix64(h ^ rw[q]);
-            if (h == ~0ull) h = ~1ull;
+                if (q < W1) h = fp_step(h, rw[q]);
+            h = fp_final(h);
             fps[rb + j] = h;
             if (LL) {       // hll_add, its register's load left in flight until the next tile
-                const uint64_t hh = splitmix64(h ^ W1);
+                const uint64_t hh = h;
                 hreg[p] = hll + ((uint64_t)(W1 - 1) << kHllLog) + (uint32_t)(hh >> (64 - kHllLog));
                 hrho[p] = (uint32_t)__clzll((hh << kHllLog) | (1ull << (kHllLog - 1))) + 1u;
                 hval[p] = *hreg[p];

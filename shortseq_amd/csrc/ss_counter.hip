@@ -2009,15 +2009,15 @@ __device__ __forceinline__ uint64_t row_fp(const uint64_t* p) {
     bool odd;
     row_chunks<W1, EVEN>(p, v, odd);
     const uint64_t m = 0ull - (uint64_t)odd;
-    uint64_t h = 0x243F6A8885A308D3ull ^ (uint64_t)W1;
+    uint64_t h = fp_seed(W1);
 #pragma unroll
     for (int j = 0; j < W1; ++j) {
         uint64_t x;
         if constexpr (EVEN) x = v[j];
         else x = (v[j + 1] & m) | (v[j] & ~m);
-        h = splitmix64(h ^ x);
+        h = fp_step(h, x);
     }
-    return h == kEmpty ? ~1ull : h;
+    return fp_final(h);
 }
 
 // W1C: rows of W1C words read as aligned chunks (row_fp), 0 for any width

@@ -111,11 +111,28 @@ __device__ __forceinline__ uint32_t swap_pair(uint32_t v) {
 
 // 64-bit fingerprint of a multi-word key (W words, compared whole): the slot key of the multi-word
 // counter tables (ss_counter.hip) and the drop-in engine's class rows (k_encode_classes emits it per
-// row, so the partition passes need not re-read the rows).  ~0 is reserved for free slots.
-__device__ __forceinline__ uint64_t words_fp(const uint64_t* w, uint32_t W) {
-    uint64_t h = 0x243F6A8885A308D3ull ^ W;
-    for (uint32_t j = 0; j < W; ++j) h = splitmix64(h ^ w[j]);
+// row, so the partition passes need not re-read the rows).  ~0 is reserved for free slots.  One
+// xorshift-multiply round per word (the xorshift first, so a difference in a word's top bits reaches
+// the multiply's low bits and cannot cancel against the next word's), then a final xorshift-multiply
+// so the top bits (slot position, sketch register) depend on every word: one 64-bit multiply per
+// word where splitmix64 per word took two.  Equal keys are decided on the words (a collision only
+// sends a chunk down the exact path), so the function is a speed choice, not a correctness one.
+__device__ __forceinline__ uint64_t fp_seed(uint32_t W) { return 0x243F6A8885A308D3ull ^ W; }
+__device__ __forceinline__ uint64_t fp_step(uint64_t h, uint64_t x) {
+    h ^= x;
+    h ^= h >> 29;
+    return h * 0xBF58476D1CE4E5B9ull;
+}
+__device__ __forceinline__ uint64_t fp_final(uint64_t h) {
+    h ^= h >> 32;
+    h *= 0x94D049BB133111EBull;
+    h ^= h >> 29;
     return h == ~0ull ? ~1ull : h;
+}
+__device__ __forceinline__ uint64_t words_fp(const uint64_t* w, uint32_t W) {
+    uint64_t h = fp_seed(W);
+    for (uint32_t j = 0; j < W; ++j) h = fp_step(h, w[j]);
+    return fp_final(h);
 }
 
 // First-invalid-read report where the read index is only needed on the (rare) bad path:

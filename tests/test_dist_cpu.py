@@ -52,15 +52,15 @@ class HostTable:
     def _fp(words):
         m = (1 << 64) - 1
 
-        def mix(z):
-            z = (z + 0x9E3779B97F4A7C15) & m
-            z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
-            z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
-            return z ^ (z >> 31)
-        h = 0x243F6A8885A308D3 ^ len(words)
+        h = 0x243F6A8885A308D3 ^ len(words)          # ss_device.h words_fp: fp_step per word, fp_final
         for w in words:
-            h = mix(h ^ (w & m))
-        return h
+            h ^= w & m
+            h ^= h >> 29
+            h = (h * 0xBF58476D1CE4E5B9) & m
+        h ^= h >> 32
+        h = (h * 0x94D049BB133111EB) & m
+        h ^= h >> 29
+        return h if h != m else m - 1
 
     def extract_words(self, n_parts=1, cap=None):
         from shortseq_amd.dist import owner_of_np
