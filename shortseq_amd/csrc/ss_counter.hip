@@ -2640,16 +2640,17 @@ __global__ __launch_bounds__(256) void k_flat_reps(Tbl f, const uint64_t* __rest
     }
 }
 
+constexpr int kFlatVK = 2;
 __global__ __launch_bounds__(256) void k_flat_verify(Tbl f, const uint64_t* __restrict__ rows, uint32_t S, uint64_t n,
                                                      const uint64_t* __restrict__ fps, const uint64_t* __restrict__ rep,
                                                      uint32_t* __restrict__ flag) {
     const uint64_t G = (uint64_t)gridDim.x * 256;
     // two rows per lane per round, every load of both in flight before either is probed
-    for (uint64_t g0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; g0 < n; g0 += 2 * G) {
-        uint64_t aw[2][kRepW1], fp[2], base[2], off[2];
-        uint4 e[2][4];
+    for (uint64_t g0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; g0 < n; g0 += kFlatVK * G) {
+        uint64_t aw[kFlatVK][kRepW1], fp[kFlatVK], base[kFlatVK], off[kFlatVK];
+        uint4 e[kFlatVK][4];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kFlatVK; ++k) {
             const uint64_t g = min(g0 + k * G, n - 1);
             const uint64_t* a = rows + g * S;
 #pragma unroll
@@ -2657,7 +2658,7 @@ __global__ __launch_bounds__(256) void k_flat_verify(Tbl f, const uint64_t* __re
             fp[k] = fps[g];
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kFlatVK; ++k) {
 #pragma unroll
             for (uint32_t j = 0; j < kRepW1; ++j)
                 if (j >= S) aw[k][j] = 0;
@@ -2670,7 +2671,7 @@ __global__ __launch_bounds__(256) void k_flat_verify(Tbl f, const uint64_t* __re
         }
         bool bad = false;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kFlatVK; ++k) {
             bool b = true;
             for (uint64_t probe = 0; probe <= f.slice_mask; ++probe) {
                 if (probe) {
