@@ -1,5 +1,6 @@
 // tools/tune_c3.hip — C3 fused encode + hamming (96 nt, dense): the production kernel k_encode_ham_dense
-// (production) against a no-LDS lane-row form k_encode_ham6w in block shapes (measured slower:
+// (production) in block shapes (T192 U4 stays best of 17; profiles/r4/tune_c3_shapes_r4.log) and a
+// no-LDS lane-row form k_encode_ham6w (measured slower:
 // 0.772 vs 0.784 of 8 TB/s for the best shape, T256 G1, same box, gpurun_out/tune_c3_6w.log).  Every
 // variant's packed words, distances and first-bad read are checked against the production launch
 // (ss_encode_hamming_ref) on a tail-heavy small batch with an invalid byte and on the timed batch.
@@ -226,7 +227,9 @@ int main(int argc, char** argv) {
         {"prod T128 U3", vp<128, 3>}, {"prod T96 U4", vp<96, 4>}, {"prod T192 U2", vp<192, 2>},
         {"prod T64 U6", vp<64, 6>}, {"prod T128 U6", vp<128, 6>}, {"prod T256 U3", vp<256, 3>},
         {"prod T64 U3", vp<64, 3>},
-        {"wave T64", vw<64>}, {"wave T128", vw<128>}, {"wave T256", vw<256>}, {"wave T512", vw<512>},
+        {"prod T256 U6", vp<256, 6>}, {"prod T384 U2", vp<384, 2>}, {"prod T384 U4", vp<384, 4>},
+        {"prod T512 U3", vp<512, 3>}, {"prod T768 U2", vp<768, 2>}, {"prod T1024 U3", vp<1024, 3>},
+        {"prod T192 U8", vp<192, 8>}, {"prod T96 U8", vp<96, 8>},
     };
     const int nv = sizeof(vs) / sizeof(vs[0]);
     // correctness: small batch with an invalid byte in read 777777 (chunk 4), then the full batch
