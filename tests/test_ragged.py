@@ -299,13 +299,15 @@ def test_device_ingest_rekey_row_limit(gpu, oracle):
     assert np.array_equal(gw, ew)
 
 
-@pytest.mark.parametrize("lo,hi,row_limit", [(0, 120, None), (0, 120, 1024), (33, 160, None), (33, 160, 1024)])
+@pytest.mark.parametrize("lo,hi,row_limit", [(0, 120, None), (0, 120, 1024), (33, 160, None), (33, 160, 1024),
+                                              (100, 300, None), (32, 32, None)])
 def test_device_ingest_count_spill(gpu, oracle, lo, hi, row_limit):
     """VERDICT r3 missing item 4, a key's count past the slots' u32: with the spill lowered to every
     1000 reads (the test hook), the tables' counts move into the groups' u64 row counts dozens of times
-    over 60 batches of 500 (33..160: the flat read-order-rows path's class tables; with the row bound
-    lowered too, the spilled counts follow their entries through every re-key); the rows (counts added
-    back at finish) still equal the oracle's."""
+    over 60 batches of 500 (33..160: the flat read-order-rows path's class tables; 100..300: classes
+    past the flat path; 32..32: one length table; with the row bound lowered too, the spilled counts
+    follow their entries through every re-key); the rows (counts added back at finish) still equal the
+    oracle's."""
     import shortseq_amd.batch as B
     seed, ps, U, n = 75, 76, 600, 30_000
     blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
