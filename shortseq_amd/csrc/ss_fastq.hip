@@ -372,12 +372,14 @@ constexpr int kFqU1 = 8;                                       // 16-B chunks pe
 constexpr uint64_t kFqTile1 = (uint64_t)kFqT * kFqU1 * 16;     // 32 KiB per tile
 
 constexpr uint32_t kStageShards = 64, kShardStride = 32;       // counters 128 B apart
-constexpr uint32_t kLdsPos = 4096;                             // newline positions gathered in LDS
+constexpr uint32_t kLdsPos = (uint32_t)(kFqTile1 / 8);       // newline positions gathered in LDS (4096)
+constexpr uint32_t kSubPerTile = (uint32_t)(kFqTile1 / 1024);  // 1-KiB NUL sub-blocks per tile (32)
+static_assert(kSubPerTile <= 32, "a tile's NUL sub-blocks are one u32 mask");
 // Every tile owns a fixed run of kTileCap staging words (after the shards' regions, 8 KiB per 32-KiB
 // tile): a tile with at most that many newlines (lines of 16 B or more on average) writes its
 // positions there straight from registers -- no reservation atomic, no LDS staging, no second
 // barrier; a denser tile reserves a run of its shard as before.
-constexpr uint32_t kTileCap = 2048;
+constexpr uint32_t kTileCap = (uint32_t)(kFqTile1 / 16);      // 2048
 
 struct FqStage {
     uint16_t* pos;        // [kStageShards * region + tiles * kTileCap] staged newline positions, as
@@ -562,7 +564,7 @@ __device__ __forceinline__ uint32_t nul_len(const uint8_t* __restrict__ buf, con
         }
     } else if (stop > start) {
         for (uint64_t sb = start >> 10; sb <= (stop - 1) >> 10 && first == stop; ++sb) {
-            if (!((st.tile_nul[sb >> 5] >> (sb & 31)) & 1u)) continue;
+            if (!((st.tile_nul[sb / kSubPerTile] >> (sb % kSubPerTile)) & 1u)) continue;
             const uint64_t e = min(stop, (sb + 1) << 10);
             for (uint64_t p = max(start, sb << 10); p < e; ++p)
                 if (buf[p] == 0) {
