@@ -1354,14 +1354,13 @@ int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint
     if (n == 0) return SS_OK;
     // persistent waves (the occupancy's worth of blocks), each over tiles of R * kRowsK reads with the
     // next tile's lengths / offsets and the last tile's sketch registers in flight
-    static int resident = 0;
-    if (!resident) {
+    static const int resident = [] {         // thread-safe one-time init (every device is a gfx950)
         int dev = 0, cus = 0, occ = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)k_encode_rows, 256, 0);
-        resident = std::max(1, cus) * std::max(1, occ);
-    }
+        return std::max(1, cus) * std::max(1, occ);
+    }();
     const uint64_t per = (uint64_t)(64 / S) * kRowsK, tiles = (n + per - 1) / per;
     const uint64_t blocks = std::min<uint64_t>((tiles + 3) / 4, (uint64_t)resident);
     hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, d_buf, d_offs, d_lens,

@@ -105,7 +105,7 @@ int main(int argc, char** argv) {
         printf("== decode 100M x 32 nt\n");
         for (int round = 0; round < 2; ++round) {
             DEC(256, 2, false, false, "32 (production)");
-            DEC(128, 2, false, false, "32");
+            DEC(256, 2, false, true, "32 nt-store");
         }
     }
     {   // ---- C4: 50M x 512 nt
@@ -124,8 +124,11 @@ int main(int argc, char** argv) {
         printf("== C4 decode 50M x 512 nt\n");
         for (int round = 0; round < 3; ++round) {
             DEC(256, 2, false, false, "512 (production)");
-            DEC(128, 2, false, false, "512");
-            DEC(192, 2, false, false, "512");
+            DEC(256, 2, false, true, "512 nt-store");
+            DEC(256, 2, true, true, "512 nt-load nt-store");
+            DEC(256, 4, false, true, "512 nt-store");
+            DEC(512, 2, false, true, "512 nt-store");
+            DEC(256, 1, false, true, "512 nt-store");
         }
     }
     return 0;
