@@ -652,19 +652,20 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
             const bool live = i < R && r < n;
             const uint32_t W = (L[k] + 31u) / 32u;
             const bool cls = L[k] > 32u && W < S;
-            uint4 xn;                           // lane w + 1's first chunk (every lane shuffles)
-            xn.x = __shfl_down(xa[k].x, 1);
-            xn.y = __shfl_down(xa[k].y, 1);
-            xn.z = __shfl_down(xa[k].z, 1);
-            xn.w = __shfl_down(xa[k].w, 1);
+            // every lane codes its first chunk; lane w + 1's code (and its odd flag) is word w's
+            // third chunk, one shuffle each instead of coding the shuffled chunk again
+            uint32_t oa = 0;
+            const uint32_t ca = code_chunk(xa[k], oa);
+            const uint32_t cn = (uint32_t)__shfl_down((int)ca, 1), on = (uint32_t)__shfl_down((int)oa, 1);
             uint64_t word = 0;
             uint32_t bad = 0;
             if (cls && w < W) {
                 const uint32_t nb = min(32u, L[k] - 32u * w), sh = (uint32_t)(off[k] & 15u);
                 const uint32_t last = (sh + nb - 1u) >> 4;
-                uint32_t odd = 0;
-                const uint32_t ca = code_chunk(xa[k], odd), cb = code_chunk(xb[k], odd);
-                const uint32_t cc = last == 2u ? code_chunk(xn, odd) : cb;
+                uint32_t odd = oa;
+                const uint32_t cb = code_chunk(xb[k], odd);
+                const uint32_t cc = last == 2u ? cn : cb;
+                odd |= last == 2u ? on : 0u;
                 const uint64_t lo64 = (uint64_t)cb << 32 | ca;
                 word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)cc << (64u - 2u * sh)) : lo64;
                 if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
