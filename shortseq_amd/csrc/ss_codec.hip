@@ -642,6 +642,7 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
             if (L[k] && w <= W && 2u * w <= lastc) xa[k] = in16[cb + 2u * w];
             if (L[k] && w < W) xb[k] = in16[cb + min(2u * w + 1u, lastc)];
         }
+        uint64_t badr = ~0ull;              // the tile's first rejected read of this lane (one report)
         // the next tile's lengths / offsets go out behind the chunks
         uint32_t nL[kRowsK];
         uint64_t noff[kRowsK];
@@ -666,18 +667,22 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
                 const uint32_t cb = code_chunk(xb[k], odd);
                 const uint32_t cc = last == 2u ? cn : cb;
                 odd |= last == 2u ? on : 0u;
-                const uint64_t lo64 = (uint64_t)cb << 32 | ca;
-                word = sh ? (lo64 >> (2u * sh)) | ((uint64_t)cc << (64u - 2u * sh)) : lo64;
-                if (nb < 32u) word &= (1ull << (2u * nb)) - 1ull;
+                // bits 2 sh .. 2 sh + 63 of cc:cb:ca by two 32-bit funnel shifts, then the 2 nb bits kept
+                const uint32_t s2 = 2u * sh, b2 = 2u * nb;
+                const uint32_t lo = __builtin_amdgcn_alignbit(cb, ca, s2), hi = __builtin_amdgcn_alignbit(cc, cb, s2);
+                const uint32_t mlo = b2 >= 32u ? ~0u : (1u << b2) - 1u;
+                const uint32_t mhi = b2 >= 64u ? ~0u : b2 <= 32u ? 0u : (1u << (b2 - 32u)) - 1u;
+                word = (uint64_t)(hi & mhi) << 32 | (lo & mlo);
                 if (odd) word = encode_word_q(in + off[k] + 32u * w, nb, nb < 32u, bad);   // rare: exact semantics
             } else if (cls && w == W) {
                 word = L[k];
             }
             if (live) out[r * S + w] = word;
-            report_bad(bad != 0u, r, first_bad);
+            if (bad) badr = min(badr, r);
             srow[wave][k * 64 + lane] = word;
             if (w == 0 && i < R) slen[wave][k * R + i] = (uint16_t)(cls ? L[k] : 0u);
         }
+        report_bad(badr != ~0ull, badr, first_bad);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");     // srow / slen are the wave's own
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
