@@ -589,14 +589,18 @@ __global__ __launch_bounds__(kClsTile) __attribute__((amdgpu_waves_per_eu(6))) v
 // read's row in READ order at a fixed stride of S words -- its W words, its length, zeros -- so no
 // class ranks, no LDS staging, no barriers and no row map (the row of read r is r).  A wave holds
 // R = 64 / S reads per group, S lanes each (lane w: word w, the length at w == W, 0 past it), and
-// kRowsK groups: the groups' length / offset loads, then their chunk loads, go out together (one
-// group per wave measured 3.35 ms on the f2 batch: three dependent round trips for 1 KB of input).
-// The words are k_encode_classes' phase b (16-B chunks, funnel shift, the rare odd word re-encoded
-// exactly), each chunk of a read loaded by one lane only.  The row fingerprint (words_fp over the W + 1 words) is folded across the
-// read's lanes with shuffles; lane 0 of the read stores it and updates its class's sketch.  Reads
+// kRowsK groups per tile: the groups' length / offset loads, then their chunk loads, go out together
+// (one group per wave measured 3.35 ms on the f2 batch: three dependent round trips for 1 KB of
+// input; 1 / 2 / 4 / 5 / 6 groups as persistent waves 2.35 / 2.04 / 1.91 / 1.93 / 1.89 ms,
+// profiles/r4/f2/libab_encrows_occupancy.log, libab_encrows_k56.log).  The words are
+// k_encode_classes' phase b (16-B chunks, funnel shift, the rare odd word re-encoded exactly), each
+// chunk of a read loaded by one lane only.  The row goes through the wave's LDS to one lane per read,
+// which runs its fingerprint (words_fp over the W + 1 words) and its class's sketch update.  Reads
 // that are not class reads (empty: the length split counts those) get a zero row and the
-// fingerprint of one zero word, an entry the fold skips.
-constexpr int kRowsK = 4;
+// fingerprint of one zero word, an entry the fold skips.  A tile holds R kRowsK <= 128 reads (the
+// fingerprint lanes take two each at most: S = 3, R = 21).
+constexpr int kRowsK = 6;
+static_assert(21 * kRowsK <= 128, "a tile's reads: two per fingerprint lane at most");
 __device__ __forceinline__ void rows_meta(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
                                           uint64_t n, uint64_t r0, uint32_t R, uint32_t i, uint32_t* L,
                                           uint64_t* off) {
