@@ -257,6 +257,26 @@ __global__ __launch_bounds__(256) void k_rank(const uint64_t* __restrict__ first
 }
 
 // export: entry e's first read (engine-local) = rowmap[first[e]]
+// the largest of m counts (atomicMax into *mx): an export's largest count sizes the merge passes
+__global__ __launch_bounds__(256) void k_count_max(const uint64_t* __restrict__ counts, uint64_t m,
+                                                   unsigned long long* mx) {
+    uint64_t v = 0;
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
+        v = max(v, counts[e]);
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint64_t)__shfl_xor((unsigned long long)v, o));
+    if ((threadIdx.x & 63u) == 0 && v) atomicMax(mx, (unsigned long long)v);
+}
+
+// one merge pass: take = min(left, room) of every entry's remaining count
+__global__ __launch_bounds__(256) void k_count_take(uint64_t* __restrict__ left, uint64_t* __restrict__ take, uint64_t m,
+                                                    uint64_t room) {
+    for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
+        const uint64_t t = min(left[e], room);
+        take[e] = t;
+        left[e] -= t;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_export_reads(const uint64_t* __restrict__ first, uint64_t m,
                                                       const uint64_t* __restrict__ rowmap, uint64_t* __restrict__ out) {
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
@@ -584,13 +604,14 @@ struct ss_ingest {
     std::string bad_bytes;
     double est_scale = 1.0;        // FASTQ: file bytes / bytes seen (multi-word table sizing)
     bool exported = false;         // ss_ingest_export ran (the groups' m / buffers hold the entries)
+    uint64_t xmax = 0;             // the export's largest count (the merge passes it needs)
     // reads counted since the tables' counts were last spilled into the groups' u64 row counts: a
     // slot's u32 count cannot pass it, so the spill before it reaches 2^32 - 1 keeps every count exact
     uint64_t since_spill = 0, spill_limit = 0xFFFFFFFEull;
     uint64_t max_rows = 0xFFFFFFFFull;   // rows a group's table indexes (its first index is u32);
                                          // ss_ingest_set_row_limit lowers it (test hook)
     // ss_ingest_merge scratch (this engine as the destination): a source group's entries on this device
-    DBuf<uint64_t> mg_words, mg_counts, mg_first;
+    DBuf<uint64_t> mg_words, mg_counts, mg_first, mg_take;
     DBuf<uint32_t> mg_lens;
     // finish() results
     uint64_t nkeys = 0, nwords = 0;
@@ -1295,7 +1316,7 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->cls_flag.release();
     if (g->fpt) ss_counter_destroy(g->fpt);
     g->fpt = nullptr;
-    g->mg_words.release(), g->mg_counts.release(), g->mg_first.release(), g->mg_lens.release();
+    g->mg_words.release(), g->mg_counts.release(), g->mg_first.release(), g->mg_lens.release(), g->mg_take.release();
     if (g->h_hll) (void)hipHostFree(g->h_hll);
     if (g->h_split) (void)hipHostFree(g->h_split);
     if (g->h_bad) (void)hipHostFree(g->h_bad);
@@ -1608,8 +1629,19 @@ int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys) {
                            gr->rowmap.p, gr->xread.p);
         keys += gr->m;
     }
-    rc = ss_check(hipStreamSynchronize(g->stream), "ingest export");
+    // the largest exported count: a merge takes it in passes of what a u32 slot can hold
+    if ((rc = g->mg_take.ensure(1)) ||
+        (rc = ss_check(hipMemsetAsync(g->mg_take.p, 0, 8, g->stream), "ingest export max")))
+        return rc;
+    for (Group* gr : placed)
+        if (gr->m)
+            hipLaunchKernelGGL(k_count_max, dim3(grid_of(gr->m, 256)), dim3(256), 0, g->stream, gr->counts.p, gr->m,
+                               (unsigned long long*)g->mg_take.p);
+    rc = ss_check(hipMemcpyAsync(g->h_bad + 3 * kLenBins + 4, g->mg_take.p, 8, hipMemcpyDeviceToHost, g->stream),
+                  "ingest export max");
+    if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest export");
     if (rc) return rc;
+    g->xmax = g->h_bad[3 * kLenBins + 4];
     g->exported = true;
     if (h_nkeys) *h_nkeys = keys + (g->empty_count ? 1 : 0);
     return SS_OK;
@@ -1641,7 +1673,9 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
     // the source's reads count toward the destination's spill: its slots stay below 2^32 after the merge
     // (one source's key past 2^32 - 1 copies still raises SS_EFULL)
     if (dst->since_spill + src->nreads > dst->spill_limit && (rc = spill_counts(dst))) return rc;
-    dst->since_spill += std::min<uint64_t>(src->nreads, dst->spill_limit);
+    // what a slot can still take before the next spill (no fewer than the source's reads unless the
+    // source itself spilled: then its counts go in passes)
+    const uint64_t room0 = std::max<uint64_t>(1, std::min<uint64_t>(dst->spill_limit, 0xFFFFFFFEull) - dst->since_spill);
     const double scale = dst->est_scale;
     dst->est_scale = 1.0;            // a new group is sized by the entries it receives
     for (auto& kv : src->groups) {
@@ -1664,13 +1698,33 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
         hipLaunchKernelGGL(k_merge_rows, dim3(grid_of(m, 256)), dim3(256), 0, s, m, gr.rows, src_base,
                            dst->mg_first.p, gr.rowmap.p);
         // appended as one block after every earlier row: a key already here keeps its (smaller) first
-        // row, a key also in a later source gets that source's larger rows -> min = first occurrence
-        rc = gr.W1 == 1 ? ss_counter_merge(gr.table, dst->mg_words.p, dst->mg_lens.p, dst->mg_counts.p, dst->mg_first.p, m, s)
-                        : ss_counter_merge_words(gr.table, dst->mg_words.p, dst->mg_counts.p, dst->mg_first.p, m, s);
+        // row, a key also in a later source gets that source's larger rows -> min = first occurrence.
+        // Counts a u32 slot cannot take at once go in passes of `room`, the destination's counts
+        // spilled to its u64 row counts between passes.
+        const uint64_t* cnt = dst->mg_counts.p;
+        uint64_t left = src->xmax, room = room0;
+        const bool passes = left > room;
+        if (passes && (rc = dst->mg_take.ensure(m))) break;
+        gr.rows += m;               // the appended rows (the spill between passes sizes the row counts by them)
+        do {
+            if (passes) {           // every pass takes min(remaining, room), the last one the rest
+                hipLaunchKernelGGL(k_count_take, dim3(grid_of(m, 256)), dim3(256), 0, s, dst->mg_counts.p, dst->mg_take.p,
+                                   m, room);
+                cnt = dst->mg_take.p;
+            }
+            rc = gr.W1 == 1 ? ss_counter_merge(gr.table, dst->mg_words.p, dst->mg_lens.p, cnt, dst->mg_first.p, m, s)
+                            : ss_counter_merge_words(gr.table, dst->mg_words.p, cnt, dst->mg_first.p, m, s);
+            if (rc) break;
+            left = left > room ? left - room : 0;
+            if (left) {
+                if ((rc = spill_counts(dst))) break;
+                room = std::min<uint64_t>(dst->spill_limit, 0xFFFFFFFEull);
+            }
+        } while (left);
         if (rc) break;
-        gr.rows += m;
     }
     dst->est_scale = scale;
+    dst->since_spill = std::min<uint64_t>(dst->spill_limit, dst->since_spill + src->nreads);
     if (rc) return rc;
     if (src->empty_count) {
         dst->empty_count += src->empty_count;

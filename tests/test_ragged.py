@@ -361,6 +361,36 @@ def test_device_ingest_count_spill_merge(gpu, oracle, lo, hi):
     assert np.array_equal(gw, ew)
 
 
+@pytest.mark.parametrize("lo,hi", [(0, 40), (33, 100), (100, 300)])
+def test_device_ingest_merge_counts_past_slot(gpu, oracle, lo, hi):
+    """Counts a slot cannot take in one merge: with the spill lowered to every 500 reads, a 6-key pool
+    gives every key ~1700 copies per engine, so the source's exported counts (its spilled counts
+    added back) exceed what a destination slot may take before its next spill; ss_ingest_merge takes
+    them in passes, spilling the destination between passes, and the rows equal the oracle's."""
+    import shortseq_amd.batch as B
+    seed, ps, U, n = 79, 80, 6, 20_000
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    h = n // 2
+    a, b = B.DeviceIngest(gpu), B.DeviceIngest(gpu)
+    try:
+        for e in (a, b):
+            e.set_count_limit(500)
+        for x in range(0, h, 1000):
+            a.count(blob, offs[x:x + 1000], lens[x:x + 1000])
+            b.count(blob, offs[h + x:h + x + 1000], lens[h + x:h + x + 1000])
+        b.export()
+        a.merge(b, h)
+        gl, gc, gw = a.results()
+    finally:
+        a.close()
+        b.close()
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    assert int(ec.max()) > 1000
+    assert gl.tolist() == el.tolist()
+    assert gc.tolist() == ec.tolist()
+    assert np.array_equal(gw, ew)
+
+
 def test_device_ingest_read_index_past_2_32(gpu, oracle):
     """VERDICT r3 item 7, global read indices past 2^32 - 1: an engine's reads folded into another at
     base 2^32 + 7 (ss_ingest_merge) -- the row maps and the first-occurrence order run on u64 read
