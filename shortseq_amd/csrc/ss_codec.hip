@@ -601,15 +601,45 @@ __global__ __launch_bounds__(kClsTile) __attribute__((amdgpu_waves_per_eu(6))) v
 // fingerprint lanes take two each at most: S = 3, R = 21).
 constexpr int kRowsK = 6;
 static_assert(21 * kRowsK <= 128, "a tile's reads: two per fingerprint lane at most");
-__device__ __forceinline__ void rows_meta(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
-                                          uint64_t n, uint64_t r0, uint32_t R, uint32_t i, uint32_t* L,
-                                          uint64_t* off) {
+// the tile's lengths / offsets (reads rb .. rb + R kRowsK - 1): loaded coalesced, a lane per read (two
+// rounds past 64 reads; rows_meta_load, issued a tile ahead), then handed to the S lanes of each read
+// by shuffles (rows_meta_split, when the tile starts) -- not loaded by every lane of the read
+struct RowsMeta {
+    uint32_t la, lb;
+    uint64_t oa, ob;
+};
+__device__ __forceinline__ RowsMeta rows_meta_load(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
+                                                   uint64_t n, uint64_t rb, uint32_t per, uint32_t lane) {
+    RowsMeta m;
+    const uint64_t ra = rb + lane, rbb = rb + 64u + lane;
+    m.la = (lane < per && ra < n) ? lens[ra] : 0u;
+    m.oa = (lane < per && ra < n) ? offs[ra] : 0ull;
+    m.lb = 0;
+    m.ob = 0;
+    if (per > 64u) {            // wave-uniform (S <= 5)
+        m.lb = (64u + lane < per && rbb < n) ? lens[rbb] : 0u;
+        m.ob = (64u + lane < per && rbb < n) ? offs[rbb] : 0ull;
+    }
+    return m;
+}
+
+__device__ __forceinline__ void rows_meta_split(const RowsMeta& m, uint32_t R, uint32_t i, uint32_t* L, uint64_t* off) {
+    const bool two = R * kRowsK > 64u;
 #pragma unroll
     for (int k = 0; k < kRowsK; ++k) {
-        const uint64_t r = r0 + (uint64_t)k * R;
-        const bool live = i < R && r < n;
-        L[k] = live ? lens[r] : 0u;
-        off[k] = live ? offs[r] : 0u;
+        const uint32_t jj = (uint32_t)k * R + i;            // this lane's read in the tile
+        const int src = (int)(jj & 63u);
+        const uint32_t l0 = (uint32_t)__shfl((int)m.la, src), o0l = (uint32_t)__shfl((int)(uint32_t)m.oa, src),
+                       o0h = (uint32_t)__shfl((int)(uint32_t)(m.oa >> 32), src);
+        uint32_t l1 = 0, o1l = 0, o1h = 0;
+        if (two) {
+            l1 = (uint32_t)__shfl((int)m.lb, src);
+            o1l = (uint32_t)__shfl((int)(uint32_t)m.ob, src);
+            o1h = (uint32_t)__shfl((int)(uint32_t)(m.ob >> 32), src);
+        }
+        const bool hi = jj >= 64u, live = i < R;
+        L[k] = live ? (hi ? l1 : l0) : 0u;
+        off[k] = live ? ((uint64_t)(hi ? o1h : o0h) << 32 | (hi ? o1l : o0l)) : 0ull;
     }
 }
 
@@ -623,14 +653,15 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
     const uint4* in16 = (const uint4*)in;
     __shared__ uint64_t srow[4][kRowsK * 64];     // the wave's rows (group k: lanes k * 64 ..)
     __shared__ uint16_t slen[4][kRowsK * 24];     // the wave's reads' lengths (read j = k * R + i; R <= 21)
-    uint32_t L[kRowsK];
-    uint64_t off[kRowsK];
     uint64_t tile = (uint64_t)blockIdx.x * 4 + wave;
-    rows_meta(offs, lens, n, tile * per + i, R, i, L, off);
+    RowsMeta meta = rows_meta_load(offs, lens, n, tile * per, (uint32_t)per, lane);
     uint32_t* hreg[2] = {nullptr, nullptr};       // the previous tile's sketch updates (<= 2 reads a lane)
     uint32_t hval[2] = {0, 0}, hrho[2] = {0, 0};
     for (; tile < tiles; tile += stride) {
         const uint64_t r0 = tile * per + i;
+        uint32_t L[kRowsK];
+        uint64_t off[kRowsK];
+        rows_meta_split(meta, R, i, L, off);
         // the read's 16-B chunks once each: lane w loads chunks 2w and 2w + 1 of its read (relative to
         // the read's first chunk, clamped to its last), the length lane W only chunk 2W when the read
         // reaches it; word w's third chunk 2w + 2 is lane w + 1's first (a shuffle).  Lanes past W load
@@ -648,9 +679,7 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
         }
         uint64_t badr = ~0ull;              // the tile's first rejected read of this lane (one report)
         // the next tile's lengths / offsets go out behind the chunks
-        uint32_t nL[kRowsK];
-        uint64_t noff[kRowsK];
-        rows_meta(offs, lens, n, (tile + stride) * per + i, R, i, nL, noff);
+        meta = rows_meta_load(offs, lens, n, (tile + stride) * per, (uint32_t)per, lane);
 #pragma unroll
         for (int k = 0; k < kRowsK; ++k) {
             const uint64_t r = r0 + (uint64_t)k * R;
@@ -725,11 +754,6 @@ __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const ui
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");     // this tile's LDS reads before the next's writes
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int k = 0; k < kRowsK; ++k) {
-            L[k] = nL[k];
-            off[k] = noff[k];
-        }
     }
 #pragma unroll
     for (int p = 0; p < 2; ++p)
