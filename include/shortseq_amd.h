@@ -413,8 +413,11 @@ int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_
  *                     dst's reads in input order (src_base = the reads before the source's shard,
  *                     increasing from call to call).  Then ss_ingest_finish(dst) orders the union.
  *                     The caller checks ss_ingest_error of every shard first (the first rejected read
- *                     in input order raises).  Synchronous.  New in this ABI version; the reference
- *                     has one process-wide dict (counter.pyx:41-54). */
+ *                     in input order raises).  Synchronous.  A dst that received merges may itself be
+ *                     merged into an engine before it (a reduction tree of adjacent shards: export it
+ *                     again first; the merge marks dst un-exported).  Merges into distinct dst
+ *                     engines may run concurrently from different host threads.  New in this ABI
+ *                     version; the reference has one process-wide dict (counter.pyx:41-54). */
 int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys);
 int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base);
 

@@ -61,6 +61,8 @@ libab)
   vs=${*:-old new}
   L=shortseq_amd/lib
   cp $L/libshortseq_amd.so $L/libshortseq_amd_new.so
+  # the real library goes back however the loop ends (a killed run left a variant installed)
+  trap "cp $L/libshortseq_amd_new.so $L/libshortseq_amd.so" EXIT
   for r in $(seq 1 "$rounds"); do
     for v in $vs; do
       cp $L/libshortseq_amd_$v.so $L/libshortseq_amd.so

@@ -689,31 +689,89 @@ cdef _fill_from_engine(ShortSeqCounter self, ss_ingest* g):
     _fill_rows(self, _engine_keys(g), lens, counts, words)
 
 
+_REDUCE_MODE = "tree"
+
+
+def _set_reduce_mode(str mode):
+    """Test / probe hook: "tree" (default) or "chain" (every shard merged into engine 0 in turn)."""
+    global _REDUCE_MODE
+    if mode not in ("tree", "chain"):
+        raise ValueError(mode)
+    _REDUCE_MODE = mode
+
+
+def _merge_pair(size_t ga, size_t gb, uint64_t rel_base, bint reexport):
+    """Engine b's entries folded into engine a (ss_ingest_merge on a's device and stream; b's reads
+    follow a's from a-relative index rel_base on).  reexport: b received merges of its own since its
+    export, so its tables are extracted again first."""
+    cdef ss_ingest* a = <ss_ingest*>ga
+    cdef ss_ingest* b = <ss_ingest*>gb
+    cdef uint64_t K = 0
+    cdef int rc = 0
+    with nogil:
+        if reexport:
+            rc = _abi.export_keys(b, &K)
+        if rc == 0:
+            rc = _abi.merge(a, b, rel_base)
+    _ingest_check(rc, "ingest merge")
+
+
 cdef _reduce_fill(ShortSeqCounter self, list engines, list bases):
     """The dict of a call counted on len(engines) shards (engine k: the reads from bases[k] on).  The
     first rejected read in input order raises (shard order = input order).  Several shards reduce on
-    the devices: every later engine's exported entries fold into engine 0's tables (ss_ingest_merge:
-    peer copies over xGMI), engine 0 orders the union by first read (ss_ingest_finish), and the dict
-    is built once from those rows -- each distinct key crosses PCIe once and gets one dict insert."""
+    the devices as a tree (VERDICT r4 item 5): round r merges engine k + 2^r into engine k for every
+    k divisible by 2^(r+1), the round's merges concurrently, each on its destination's device and
+    stream (ss_ingest_merge: peer copies over xGMI) -- so no engine takes more than log2(D) sources
+    and the first round's D/2 copies use D/2 links at once.  Every pair is adjacent in input order
+    (b's reads follow a's), which keeps the smallest row of a key its first occurrence.  Engine 0 then
+    orders the union by first read (ss_ingest_finish), and the dict is built once from those rows --
+    each distinct key crosses PCIe once and gets one dict insert."""
     cdef Py_ssize_t k, D = len(engines)
     cdef ss_ingest* g0 = <ss_ingest*><size_t>engines[0][1]
-    cdef ss_ingest* gk
-    cdef uint64_t b, K = 0, NW = 0
+    cdef uint64_t K = 0, NW = 0
     cdef int rc = 0
     for k in range(D):
         _raise_ingest_error(<ss_ingest*><size_t>engines[k][1])
     if D > 1:
-        for k in range(1, D):
-            gk = <ss_ingest*><size_t>engines[k][1]
-            b = bases[k]
-            with nogil:
-                rc = _abi.merge(g0, gk, b)
-            _ingest_check(rc, "ingest merge")
+        if _REDUCE_MODE == "chain":
+            for k in range(1, D):
+                _merge_pair(<size_t>engines[0][1], <size_t>engines[k][1], bases[k], False)
+        else:
+            step = 1
+            while step < D:
+                pairs = [(a, a + step) for a in range(0, D, 2 * step) if a + step < D]
+                # b merged sources of its own in an earlier round (b + step/2 .. ): re-export it
+                jobs = [(<size_t>engines[a][1], <size_t>engines[b][1], <uint64_t>(bases[b] - bases[a]),
+                         step > 1 and b + 1 < D) for a, b in pairs]
+                _run_parallel(_merge_pair, jobs)
+                step *= 2
         with nogil:
             rc = _abi.finish(g0, &K, &NW)
         _ingest_check(rc, "ingest finish")
         _engine_nkeys[<size_t>g0] = K
     _fill_from_engine(self, g0)
+
+
+def _run_parallel(fn, jobs):
+    """fn(*job) for every job, all but the first in threads (the GIL is released inside); the first
+    exception raised is re-raised after every job ended."""
+    errs = [None] * len(jobs)
+
+    def run(i):
+        try:
+            fn(*jobs[i])
+        except BaseException as e:  # noqa: BLE001
+            errs[i] = e
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(1, len(jobs))]
+    for t in ts:
+        t.start()
+    if jobs:
+        run(0)
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
 
 
 cdef dict _engine_nkeys = {}
@@ -765,22 +823,7 @@ def _shard_work(size_t gh, int kind, size_t blob, size_t lens, uint64_t n, bytes
 
 def _run_shards(jobs):
     """jobs: argument tuples of _shard_work, one per engine; all but the first run in threads."""
-    errs = [None] * len(jobs)
-
-    def run(i):
-        try:
-            _shard_work(*jobs[i])
-        except BaseException as e:  # noqa: BLE001
-            errs[i] = e
-    ts = [threading.Thread(target=run, args=(i,)) for i in range(1, len(jobs))]
-    for t in ts:
-        t.start()
-    run(0)
-    for t in ts:
-        t.join()
-    for e in errs:
-        if e is not None:
-            raise e
+    _run_parallel(_shard_work, jobs)
 
 
 def _count_batch_gpu(ShortSeqCounter self, list reads, devs):

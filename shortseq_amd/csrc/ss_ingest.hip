@@ -1003,7 +1003,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             if (flat) fc[gr.W1 - 1] = {gr.table, gr.rows, gr.rowmap.p + gr.rows};
         }
         const uint64_t fcap = std::min<uint64_t>(1ull << 32, std::max<uint64_t>(1ull << 19, pow2_at_least(2 * need_all + 2)));
-        if (g->fpt && ss_counter_capacity(g->fpt) != fcap) {
+        // grow-only with hysteresis: a stream whose per-chunk estimates cross a power of
+        // two keeps its table; only a table 8x too large (its per-slot passes, reps and fold, scale
+        // with the capacity) is replaced by a smaller one
+        if (g->fpt && (ss_counter_capacity(g->fpt) < fcap || ss_counter_capacity(g->fpt) >= 8 * fcap)) {
             (void)hipStreamSynchronize(s);
             ss_counter_destroy(g->fpt);
             g->fpt = nullptr;
@@ -1731,6 +1734,7 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
         dst->empty_first = std::min(dst->empty_first, src_base + src->empty_first);
     }
     dst->nreads = std::max(dst->nreads, src_base + src->nreads);
+    dst->exported = false;           // its tables changed: a later merge out of it exports them again
     return ss_check(hipStreamSynchronize(s), "ingest merge");    // the source may be reset after return
 }
 

@@ -85,52 +85,77 @@ def exchange(keys: torch.Tensor, counts: torch.Tensor, first: torch.Tensor, part
     return out + (rc_l,) if with_sizes else out
 
 
-def exchange_rows(rows: torch.Tensor, part_counts, group=None):
+def exchange_rows(rows: torch.Tensor, part_counts, group=None, flag: int = 0):
     """All-to-all of owner-grouped int64 rows ([m, k], part_counts[r] rows for rank r in rank order):
-    one small all-to-all of the sizes, one host sync, one all-to-all of the rows.  Returns (the rows
-    this rank receives in source-rank order, per-source sizes)."""
+    one small all-to-all of the sizes (each with this rank's error flag), one host sync, one
+    all-to-all of the rows.  Returns (the rows this rank receives in source-rank order, per-source
+    sizes, the largest flag any rank sent).  A raised flag anywhere skips the row all-to-all on
+    every rank alike (no rank is left waiting in it), and the rows returned are then empty."""
     world = dist.get_world_size(group)
     dev = rows.device
     if dev.type != "cpu" and dist.get_backend(group) == "gloo":
-        out, sizes = exchange_rows(rows.cpu(), torch.as_tensor(part_counts).cpu(), group)
-        return out.to(dev), sizes
+        out, sizes, f = exchange_rows(rows.cpu(), torch.as_tensor(part_counts).cpu(), group, flag)
+        return out.to(dev), sizes, f
     sc = torch.as_tensor(part_counts, dtype=torch.int64).to(dev)
-    rc = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_to_all_single(rc, sc, group=group)
-    host = torch.cat([sc, rc]).cpu().tolist()                            # the one host sync
-    sc_l, rc_l = [int(x) for x in host[:world]], [int(x) for x in host[world:]]
+    meta = torch.stack([sc, torch.full((world,), int(flag), dtype=torch.int64, device=dev)], 1)
+    rmeta = torch.empty_like(meta)
+    dist.all_to_all_single(rmeta, meta, group=group)
+    host = torch.cat([sc, rmeta.reshape(-1)]).cpu().tolist()            # the one host sync
+    sc_l = [int(x) for x in host[:world]]
+    rc_l = [int(host[world + 2 * p]) for p in range(world)]
+    fmax = max(int(flag), *[int(host[world + 2 * p + 1]) for p in range(world)])
+    if fmax:
+        return torch.empty((0, rows.shape[1]), dtype=torch.int64, device=dev), [0] * world, fmax
     m = sum(sc_l)
     recv = torch.empty((sum(rc_l), rows.shape[1]), dtype=torch.int64, device=dev)
     dist.all_to_all_single(recv, rows[:m].contiguous(), output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
-    return recv, rc_l
+    return recv, rc_l, 0
+
+
+def agree_flag(flag: int, device, group=None) -> int:
+    """The largest of every rank's flag (one all_reduce MAX): a check that raises on one rank raises
+    on all of them, so none is left waiting in the next collective."""
+    t = torch.tensor([int(flag)], dtype=torch.int64,
+                     device=device if dist.get_backend(group) != "gloo" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
 
 
 def exchange_packed(rec: torch.Tensor, part_counts: torch.Tensor, first_base: int, group=None,
                     extra: torch.Tensor = None):
     """All-to-all of owner-grouped packed records (int64 [m, 2] = 16 B each, ss_counter_pack_ranges).
 
-    One small all-to-all carries (records for you, my first_base) per peer; then ONE host sync reads
-    this rank's send sizes, the received metadata and `extra` (e.g. the table's overflow word)
-    together, and one all-to-all moves the records (RCCL needs the split sizes on the host; a
-    fixed-capacity exchange would avoid the sync but move the whole region range, 2x the records at
-    the table's 0.5 load factor).  Returns (received records in source-rank order, per-source sizes,
-    per-source first_base, host copy of extra or None)."""
+    One small all-to-all carries (records for you, my first_base, my `extra` word) per peer; then
+    ONE host sync reads this rank's send sizes and the received metadata together, and one
+    all-to-all moves the records (RCCL needs the split sizes on the host; a fixed-capacity exchange
+    would avoid the sync but move the whole region range, 2x the records at the table's 0.5 load
+    factor).  `extra` (e.g. the table's overflow word) travels to every peer: when any rank's is
+    nonzero, every rank skips the record all-to-all and gets that word back, so all of them raise
+    alike.  Returns (received records in source-rank order, per-source sizes, per-source first_base,
+    [the OR of every rank's extra word] or None)."""
     world = dist.get_world_size(group)
     dev = rec.device
     if dev.type != "cpu" and dist.get_backend(group) == "gloo":
         out = exchange_packed(rec.cpu(), part_counts.cpu(), first_base, group,
                               None if extra is None else extra.cpu())
         return (out[0].to(dev),) + tuple(out[1:])
+    ex_word = (extra.reshape(-1)[:1].to(torch.int64) if extra is not None
+               else torch.zeros(1, dtype=torch.int64, device=dev))
     meta = torch.stack([part_counts.to(torch.int64),
-                        torch.full((world,), first_base, dtype=torch.int64, device=dev)], 1)
+                        torch.full((world,), first_base, dtype=torch.int64, device=dev),
+                        ex_word.expand(world)], 1)
     rmeta = torch.empty_like(meta)
     dist.all_to_all_single(rmeta, meta, group=group)
-    parts = [meta[:, 0], rmeta.reshape(-1)] + ([extra.reshape(-1).to(torch.int64)] if extra is not None else [])
-    host = torch.cat(parts).cpu().tolist()                               # the one host sync
+    host = torch.cat([meta[:, 0], rmeta.reshape(-1)]).cpu().tolist()    # the one host sync
     sc_l = [int(x) for x in host[:world]]
-    rc_l = [int(host[world + 2 * p]) for p in range(world)]
-    bases = [int(host[world + 2 * p + 1]) for p in range(world)]
-    ex = host[3 * world:] if extra is not None else None
+    rc_l = [int(host[world + 3 * p]) for p in range(world)]
+    bases = [int(host[world + 3 * p + 1]) for p in range(world)]
+    ex_or = 0
+    for p in range(world):
+        ex_or |= int(host[world + 3 * p + 2]) & ((1 << 64) - 1)
+    ex = [ex_or] if extra is not None else None
+    if ex_or:            # some rank cannot send its records: nobody exchanges, everybody raises
+        return torch.empty((0, 2), dtype=torch.int64, device=dev), [0] * world, bases, ex
     m = sum(sc_l)
     recv = torch.empty((sum(rc_l), 2), dtype=torch.int64, device=dev)
     dist.all_to_all_single(recv, rec[:m], output_split_sizes=rc_l, input_split_sizes=sc_l, group=group)
@@ -186,20 +211,29 @@ class ShardedCounter:
 
     def _exchange_words(self) -> None:
         """Multi-word keys: the other owners' rows (W words, count, first) out in one all-to-all, the
-        received rows folded into this rank's table (merge_words)."""
-        _fps, _lens, words, counts, first, parts = self.local.extract_words(self.world)
-        pc = [int(x) for x in parts.cpu().tolist()]
-        starts = np.cumsum([0] + pc).tolist()
-        a, b = starts[self.rank], starts[self.rank + 1]
-        W = words.shape[1]
-        rows = torch.cat([words[:starts[-1]], counts[:starts[-1], None], first[:starts[-1], None]], 1)
-        send = torch.cat([rows[:a], rows[b:]], 0)                          # this rank's own part stays
-        sizes = list(pc)
-        sizes[self.rank] = 0
-        recv, _rs = exchange_rows(send, sizes, group=self.group)
+        received rows folded into this rank's table (merge_words).  An overflowed table is checked
+        before anything is extracted, and every overflow is agreed across the ranks (the size
+        exchange's flag, then one all_reduce after the merge), so all ranks raise together."""
+        ovf = bool(self.local.overflowed())
+        if ovf:
+            W = max(1, (int(self.L) + 31) // 32)
+            send, sizes = torch.empty((0, W + 2), dtype=torch.int64, device=self.device), [0] * self.world
+        else:
+            _fps, _lens, words, counts, first, parts = self.local.extract_words(self.world)
+            pc = [int(x) for x in parts.cpu().tolist()]
+            starts = np.cumsum([0] + pc).tolist()
+            a, b = starts[self.rank], starts[self.rank + 1]
+            W = words.shape[1]
+            rows = torch.cat([words[:starts[-1]], counts[:starts[-1], None], first[:starts[-1], None]], 1)
+            send = torch.cat([rows[:a], rows[b:]], 0)                      # this rank's own part stays
+            sizes = list(pc)
+            sizes[self.rank] = 0
+        recv, _rs, flag = exchange_rows(send, sizes, group=self.group, flag=int(ovf))
+        if flag:
+            raise RuntimeError("counter table overflow (a count or first index past 32 bits, or the table)")
         if recv.shape[0]:
             self.local.merge_words(recv[:, :W].contiguous(), recv[:, W].contiguous(), recv[:, W + 1].contiguous())
-        if self.local.overflowed():
+        if agree_flag(int(bool(self.local.overflowed())), self.device, self.group):
             raise RuntimeError("counter table overflow (a count or first index past 32 bits, or the table)")
 
     def owned(self):
@@ -231,7 +265,7 @@ class ShardedCounter:
                 sizes = [0] * self.world
                 sizes[dst] = k.shape[0]
                 W = k.shape[1]
-                rows, _ = exchange_rows(torch.cat([k, c[:, None], f[:, None]], 1), sizes, group=self.group)
+                rows, _, _f = exchange_rows(torch.cat([k, c[:, None], f[:, None]], 1), sizes, group=self.group)
                 k, c, f = rows[:, :W], rows[:, W], rows[:, W + 1]
             if self.rank != dst:
                 return None
@@ -241,6 +275,9 @@ class ShardedCounter:
             o = np.argsort(ff, kind="stable")
             return kk[o], cc[o], ff[o]
         if self.world > 1:
+            # a merge that overflowed a rank's table: every rank raises before the gather
+            if agree_flag(int(bool(self.local.overflowed())), self.device, self.group):
+                raise RuntimeError("counter table overflow after the merge (a count or first index past 32 bits)")
             sizes = torch.zeros(self.world, dtype=torch.int64, device=self.device)
             sizes[dst] = k.numel()
             k, c, f = exchange(k, c, f, sizes, self.group)

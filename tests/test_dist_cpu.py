@@ -190,6 +190,45 @@ def _worker(rank, world, port, n, L, U, q):
         dist.destroy_process_group()
 
 
+class OverflowTable(HostTable):
+    """A HostTable whose rank-1 instance reports an overflowed table (one rank's overflow
+    must raise on every rank, none left waiting in a collective)."""
+    overflow_rank = 1
+
+    def _ovf(self):
+        return dist.get_rank() == self.overflow_rank
+
+    def overflow_word(self):
+        return torch.tensor([4 if self._ovf() else 0], dtype=torch.int64)
+
+    def overflowed(self):
+        return self._ovf()
+
+    def extract_words(self, n_parts=1, cap=None):
+        assert not self._ovf(), "an overflowed table must not be extracted and sent"
+        return super().extract_words(n_parts, cap)
+
+
+def _worker_overflow(rank, world, port, L, q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from shortseq_amd.dist import ShardedCounter
+        per = 300
+        a = oracle.gen_pool_reads(7, 8, 50, rank * per, per, L)
+        sc = ShardedCounter(1 << 14, device="cpu", table_factory=OverflowTable)
+        try:
+            sc.count(torch.from_numpy(a).view(per, L), L, base_index=rank * per)
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, "overflow" if "overflow" in str(e) else repr(e)))
+        dist.barrier()          # every rank got here: nobody hangs in the exchange
+    finally:
+        dist.destroy_process_group()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -259,3 +298,22 @@ def test_region_owner_is_balanced():
     for world in (2, 3, 8):
         c = np.bincount(owner_of_region_np(keys, world, 25, 11), minlength=world)
         assert c.min() > 0.9 * len(keys) / world
+
+
+@pytest.mark.parametrize("L", [32, 100])
+def test_sharded_counter_overflow_raises_on_every_rank(L):
+    """One rank's table overflows: every rank raises the overflow (single-word records: the word
+    rides the size exchange; multi-word rows: checked before extraction and agreed across ranks) and
+    all of them reach the barrier after it."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overflow, args=(r, world, port, L, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == {r: "overflow" for r in range(world)}

@@ -210,8 +210,12 @@ def _rccl_worker(port, q):
         m = 100_003
         rec = torch.randint(-2 ** 62, 2 ** 62, (m + 17, 2), generator=g, dtype=torch.int64).to(dev)
         recv, sizes, bases, ex = exchange_packed(rec, torch.tensor([m], device=dev), 12345,
+                                                 extra=torch.tensor([0], dtype=torch.int32, device=dev))
+        ok = torch.equal(recv, rec[:m]) and sizes == [m] and bases == [12345] and ex == [0]
+        # a raised overflow word: no record exchange, the word comes back (every rank raises alike)
+        recv, sizes, bases, ex = exchange_packed(rec, torch.tensor([m], device=dev), 12345,
                                                  extra=torch.tensor([7], dtype=torch.int32, device=dev))
-        ok = torch.equal(recv, rec[:m]) and sizes == [m] and bases == [12345] and ex == [7]
+        ok = ok and recv.shape[0] == 0 and sizes == [0] and ex == [7]
         k = rec[:, 0].contiguous()
         kk, cc, ff, rs = exchange(k, k + 1, k + 2, torch.tensor([m], device=dev), with_sizes=True)
         ok = ok and torch.equal(kk, k[:m]) and torch.equal(cc, k[:m] + 1) and torch.equal(ff, k[:m] + 2) and rs == [m]
@@ -238,3 +242,22 @@ def test_rccl_exchange_helpers_world1():
     p.join(timeout=60)
     assert p.exitcode == 0
     assert ok
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_without_launcher():
+    """`python bench.py --gpus 2` with no launcher: bench.py starts the two ranks
+    itself (gloo rehearsal on this GPU, small C2 batch, no extras) and its ONE JSON line says
+    n_gpus 2 with the whole-job batch; unmeasured across real devices."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONUNBUFFERED"] = "1"
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--dist-backend", "gloo", "--same-device", "--reads-per-gpu", "4000000", "--no-extras"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 8_000_000 and r["value"] > 0

@@ -134,7 +134,7 @@ print("ok")
     assert "ok" in out.stdout
 
 
-@pytest.mark.parametrize("ndev", [2, 8])
+@pytest.mark.parametrize("ndev", [2, 3, 8])
 def test_c1_dropin_reference_digest_multi_engine(gpu, digests, oracle, ndev):
     """The multi-GPU drop-in (counter.pyx:10-54 over a list sharded by contiguous read ranges, one
     ingest engine per device, rows merged in shard order) rehearsed with `ndev` engines on device 0:
@@ -180,7 +180,7 @@ def test_multi_engine_golden_and_mixed(gpu, golden, ndev):
     assert str(ei.value) == "Unsupported base character: X"
 
 
-@pytest.mark.parametrize("ndev", [2, 8])
+@pytest.mark.parametrize("ndev", [2, 3, 8])
 def test_fastq_multi_engine(gpu, golden, tmp_path, ndev):
     """read_and_count_fastq split into `ndev` byte ranges at line boundaries (ss_fastq_split: the
     lines before each range keep the j % 4 == 1 selection global), one engine each: the reference's
@@ -239,7 +239,7 @@ def _rows_of(counter):
     return np.array(lens, np.uint32), np.array(cnts, np.uint64), np.array(words, np.uint64)
 
 
-@pytest.mark.parametrize("ndev", [2, 8])
+@pytest.mark.parametrize("ndev", [2, 3, 5, 8])
 def test_multi_engine_ragged_device_reduce(gpu, oracle, ndev):
     """a mixed 1-300-nt list through `ndev` engines reduces on the device
     (ss_ingest_export + ss_ingest_merge into the first shard's engine: single-word length tables and
@@ -286,3 +286,79 @@ def test_device_ingest_export_merge(gpu, oracle):
         assert gl.tolist() == el.tolist()
         assert gc.tolist() == ec.tolist()
         assert (gw == ew).all()
+
+
+@pytest.mark.parametrize("ndev", [3, 6, 8])
+def test_reduce_tree_equals_chain(gpu, oracle, ndev):
+    """the tree reduce (adjacent pairs merged concurrently, log2(D) rounds, the
+    round-2+ sources re-exported) and the serial chain into engine 0 give the same dict, equal to the
+    generator-derived rows; a mixed 0-200-nt list (single-word lengths and length classes)."""
+    import shortseq_amd._shortseq as S
+    seed, ps, U, n, lo, hi = 51, 52, 1 << 11, 40_000, 0, 200
+    reads = oracle.ragged_pool_reads(seed, ps, U, 0, n, lo, hi)
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    try:
+        for mode in ("chain", "tree"):
+            S._set_reduce_mode(mode)
+            gl, gc, gw = _rows_of(ShortSeqCounter(reads, device=[0] * ndev))
+            assert gl.tolist() == el.tolist(), mode
+            assert gc.tolist() == ec.tolist(), mode
+            assert (gw == ew).all(), mode
+    finally:
+        S._set_reduce_mode("tree")
+
+
+def test_device_ingest_tree_merge_abi(gpu, oracle):
+    """The tree at the C ABI: four engines on consecutive slices; 1 -> 0 and 3 -> 2 (concurrently, from
+    two threads), then 2 (re-exported: it received 3) -> 0.  Merging a destination that received
+    merges without exporting it again is refused."""
+    import threading
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import NativeError
+    seed, ps, U, n, lo, hi = 53, 54, 4000, 160_000, 20, 180
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    cuts = [0, n // 7, n // 2, 3 * n // 4, n]
+    engs = [B.DeviceIngest(gpu) for _ in range(4)]
+    try:
+        for k, e in enumerate(engs):
+            e.count(blob, offs[cuts[k]:cuts[k + 1]], lens[cuts[k]:cuts[k + 1]])
+        for e in engs[1:]:
+            e.export()
+        ts = [threading.Thread(target=engs[0].merge, args=(engs[1], cuts[1])),
+              threading.Thread(target=engs[2].merge, args=(engs[3], cuts[3] - cuts[2]))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        with pytest.raises(NativeError, match="export"):
+            engs[0].merge(engs[2], cuts[2])
+        engs[2].export()
+        engs[0].merge(engs[2], cuts[2])
+        gl, gc, gw = engs[0].results()
+    finally:
+        for e in engs:
+            e.close()
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    assert gl.tolist() == el.tolist()
+    assert gc.tolist() == ec.tolist()
+    assert (gw == ew).all()
+
+
+def test_cross_device_reduce(gpu, golden, tmp_path, oracle):
+    """the xGMI path of the reduce (peer access + hipMemcpyPeerAsync on the destination's
+    stream) on two real devices; skipped on a one-GPU box."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    seed, ps, U, n, lo, hi = 43, 44, 1 << 12, 60_000, 1, 300
+    reads = oracle.ragged_pool_reads(seed, ps, U, 0, n, lo, hi)
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    gl, gc, gw = _rows_of(ShortSeqCounter(reads, device=[0, 1]))
+    assert gl.tolist() == el.tolist() and gc.tolist() == ec.tolist() and (gw == ew).all()
+    for name, case in sorted(golden["fastq"].items()):
+        if case["raises"]:
+            continue
+        p = tmp_path / (name + ".fq")
+        p.write_bytes(bytes.fromhex(case["file_hex"]))
+        assert _items(sq.read_and_count_fastq(str(p), device=[0, 1])) == _items(
+            sq.read_and_count_fastq(str(p), device="host")), name
