@@ -491,7 +491,7 @@ def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):
                                  "whole k-steps); frac_algorithmic: L compares per pair x2; dense i8 peak = 2x bf16"}}
 
 
-def bench_ragged(B, lib, dev, reps=5):
+def bench_ragged(B, lib, dev, reps=5, name="ragged_50M_L50-150_U20", encode=True):
     """50M ragged reads of 50-150 nt drawn from a 2^20-item pool, device-resident
     (ss_synth_ragged_*: blob + offsets + lengths).  (a) ss_encode_var over the batch (wpr 5); (b) the
     drop-in counter engine fed from device memory, ss_ingest_add_device + ss_ingest_finish: the
@@ -500,7 +500,7 @@ def bench_ragged(B, lib, dev, reps=5):
     from shortseq_amd._native import check
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     with open(os.path.join(REPO, "tests", "golden", "ragged_digests.json")) as f:
-        d = json.load(f)["ragged_50M_L50-150_U20"]
+        d = json.load(f)[name]
     n = d["n"]
     blob, offs, lens = B.synth_ragged_pool_reads(n, d["seed"], d["pool_seed"], d["U"], d["Lmin"], d["Lmax"], device=dev)
     nt = int(lens.sum().item())
@@ -512,11 +512,12 @@ def bench_ragged(B, lib, dev, reps=5):
     def enc(_t):
         check(lib.ss_encode_var(blob.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, words.data_ptr(), wpr,
                                 fb.data_ptr(), s), "encode_var")
-    _el, tr = timed_loop(enc, reps, 2, 1)
-    if int(fb.item()) != -1:
-        raise SystemExit("PARITY FAILURE: ragged encode flagged a read")
-    enc_ms = tr.region_ms / reps
     enc_bytes = nt + n * (8 + 4) + n * wpr * 8        # ASCII + offset + length in, wpr words out
+    if encode:
+        _el, tr = timed_loop(enc, reps, 2, 1)
+        if int(fb.item()) != -1:
+            raise SystemExit("PARITY FAILURE: ragged encode flagged a read")
+        enc_ms = tr.region_ms / reps
     del words
     eng = B.DeviceIngest(dev)
     ts = []
@@ -534,20 +535,22 @@ def bench_ragged(B, lib, dev, reps=5):
         eng.close()
     import oracle as _o   # the digest helper only (numpy), after timing
     if len(gl) != d["unique"] or _o.rows_digest(gl, gc, gw) != d["digest"]:
-        raise SystemExit("PARITY FAILURE: ragged counter rows != ragged_50M_L50-150_U20")
+        raise SystemExit(f"PARITY FAILURE: ragged counter rows != {name}")
     t = float(np.median(ts))
     floor = nt + n * 12
-    return {"reads": n, "nt": nt, "len_range": [d["Lmin"], d["Lmax"]], "pool": d["U"], "unique": len(gl),
-            "encode_var": {"ms_per_step": enc_ms, "nt_per_s": nt / enc_ms * 1e3,
-                           "roofline": {"bound": "hbm", "kernel": "k_encode_var_dense", "achieved": enc_bytes / enc_ms / 1e6,
-                                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                        "frac": enc_bytes / enc_ms / 1e6 / HBM_PEAK_GBS,
-                                        "traffic": load_traffic("encode_var_ragged", n)}},
+    out = {"reads": n, "nt": nt, "len_range": [d["Lmin"], d["Lmax"]], "pool": d["U"], "unique": len(gl)}
+    if encode:
+        out["encode_var"] = {"ms_per_step": enc_ms, "nt_per_s": nt / enc_ms * 1e3,
+                             "roofline": {"bound": "hbm", "kernel": "k_encode_var_dense",
+                                          "achieved": enc_bytes / enc_ms / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                          "frac": enc_bytes / enc_ms / 1e6 / HBM_PEAK_GBS,
+                                          "traffic": load_traffic("encode_var_ragged", n)}}
+    return dict(out, **{
             "count": {"s_per_call": t, "reads_per_s": n / t, "nt_per_s": nt / t,
-                      "floor_frac": floor / t / 1e9 / HBM_PEAK_GBS, "parity": "digest ragged_50M_L50-150_U20",
+                      "floor_frac": floor / t / 1e9 / HBM_PEAK_GBS, "parity": f"digest {name}",
                       "note": "ss_ingest_add_device + ss_ingest_finish wall time (host-synchronous engine: length "
                               "split, class encode + sketch, per-class tables, rows copied back to pinned host "
-                              "memory); floor_frac = one read of the blob + offsets + lengths at 8 TB/s"}}
+                              "memory); floor_frac = one read of the blob + offsets + lengths at 8 TB/s"}})
 
 
 def bench_host_staged(B, dev, n=32_000_000, L=32, reps=5):
@@ -923,6 +926,9 @@ def main():
             local_extra("F4_all_pairs_umi12", lambda: bench_all_pairs(B, lib, dev))
             log("F2 ragged 50-150 nt")
             local_extra("F2_ragged_50_150", lambda: bench_ragged(B, lib, dev))
+            # the same reads over a 2^24-item pool: ~16M distinct keys, tables past the Infinity Cache
+            local_extra("F2_ragged_50_150_U24", lambda: bench_ragged(B, lib, dev, reps=3, name="ragged_50M_L50-150_U24",
+                                                                     encode=False))
             log("C2 host-staged (PCIe-inclusive)")
             local_extra("C2_host_staged_32", lambda: bench_host_staged(B, dev))
             log("C1 drop-in API")

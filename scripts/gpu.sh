@@ -70,6 +70,19 @@ libab)
     done
   done
   cp $L/libshortseq_amd_new.so $L/libshortseq_amd.so ;;
+libprof)      # libprof <name> <regex> "<variants>" -- <cmd...>: rocprof kernel stats of cmd per library variant
+  name=$1; pat=$2; vs=$3; shift 3; [ "$1" = "--" ] && shift
+  L=shortseq_amd/lib
+  cp $L/libshortseq_amd.so $L/libshortseq_amd_new.so
+  trap "cp $L/libshortseq_amd_new.so $L/libshortseq_amd.so" EXIT
+  for v in $vs; do
+    cp $L/libshortseq_amd_$v.so $L/libshortseq_amd.so
+    d=gpurun_out/prof_${name}_$v
+    mkdir -p $d
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- "$@" > $d.log 2>&1 || { echo "libprof $v rc=$?"; tail -20 $d.log; exit 1; }
+    echo "== $v: $(grep -v '^[WE]2' $d.log | tail -1)"
+    stats $d "$pat"
+  done ;;
 prof)
   name=$1; pat=$2; shift 2; [ "$1" = "--" ] && shift
   d=gpurun_out/prof_$name

@@ -1742,6 +1742,7 @@ __global__ __launch_bounds__(256) void k_run_bounds(Tbl t, Recs recs,
 
 constexpr uint32_t kMergeT = 512;
 constexpr uint32_t kMergeSearchRuns = 64;   // up to this many runs, each block finds its own bounds
+constexpr int kMergeK = 4;                  // k_merge_runs: records in flight per thread
 
 template <typename Recs>
 __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
@@ -1785,25 +1786,66 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
         }
     }
     __syncthreads();
-    for (uint32_t run = 0; run < n_runs; ++run) {
-        const uint64_t r0 = run_off[2 * run];
-        if (run_off[2 * run + 1] == r0) continue;              // empty run: no bounds were written
-        const uint32_t* b = bounds + (uint64_t)run * (nreg + 1);
-        const uint32_t lo = bounds ? b[j] : s_lo[run], hi = bounds ? b[j + 1] : s_hi[run];
-        for (uint32_t e = lo + threadIdx.x; e < hi; e += kMergeT) {
-            uint64_t key;
-            unsigned long long c, f;
-            recs.load(r0 + e, run, key, c, f);
-            const uint32_t off = lds_probe<kAggProbe>(skey, (uint32_t)t.slice_mask,
-                                                          (uint32_t)(slot_top(t, key) & t.slice_mask), key);
-            if (off == S) {
-                atomicOr(t.overflow, kOvfTable);
-                continue;
+    // the region's segments of up to kMergeSearchRuns runs folded as ONE flat index space (prefix of
+    // their lengths in LDS): every thread keeps kMergeK records in flight, where run after run each
+    // segment of ~1k records was one or two dependent load round trips of the whole block
+    __shared__ uint32_t s_pre[kMergeSearchRuns + 1];
+    __shared__ uint64_t s_at[kMergeSearchRuns];
+    for (uint32_t g0 = 0; g0 < n_runs; g0 += kMergeSearchRuns) {
+        const uint32_t nr = min(n_runs - g0, kMergeSearchRuns);
+        if (threadIdx.x < 64) {           // wave 0: the group's segment starts and length prefix
+            const uint32_t lane = threadIdx.x, run = g0 + lane;
+            uint32_t len = 0;
+            if (lane < nr) {
+                const uint64_t r0 = run_off[2 * run];
+                uint32_t lo = 0, hi = 0;
+                if (run_off[2 * run + 1] != r0) {               // empty run: no bounds were written
+                    const uint32_t* b = bounds + (uint64_t)run * (nreg + 1);
+                    lo = bounds ? b[j] : s_lo[run];
+                    hi = bounds ? b[j + 1] : s_hi[run];
+                }
+                len = hi - lo;
+                s_at[lane] = r0 + lo;
             }
-            if ((c >> 32) || f > kMaxIndex) atomicOr(t.overflow, f > kMaxIndex ? kOvfIndex : kOvfField);
-            atomicAdd(&scnt[off], (uint32_t)c);
-            atomicMin(&sfst[off], (uint32_t)min((unsigned long long)kMaxIndex, f));
+            uint32_t incl = len;
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (lane < nr) s_pre[lane + 1] = incl;
+            if (lane == 0) s_pre[0] = 0;
         }
+        __syncthreads();
+        const uint32_t tot = s_pre[nr];
+        for (uint32_t e0 = 0; e0 < tot; e0 += kMergeT * kMergeK) {
+            uint64_t key[kMergeK];
+            unsigned long long c[kMergeK], f[kMergeK];
+#pragma unroll
+            for (int k = 0; k < kMergeK; ++k) {
+                const uint32_t e = min(e0 + (uint32_t)k * kMergeT + threadIdx.x, tot - 1u);
+                uint32_t lo = 0, hi = nr - 1;         // the run holding flat record e: s_pre[run] <= e
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) >> 1;
+                    if (s_pre[mid] <= e) lo = mid;
+                    else hi = mid - 1;
+                }
+                recs.load(s_at[lo] + (e - s_pre[lo]), g0 + lo, key[k], c[k], f[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < kMergeK; ++k) {
+                if (e0 + (uint32_t)k * kMergeT + threadIdx.x >= tot) break;
+                const uint32_t off = lds_probe<kAggProbe>(skey, (uint32_t)t.slice_mask,
+                                                              (uint32_t)(slot_top(t, key[k]) & t.slice_mask), key[k]);
+                if (off == S) {
+                    atomicOr(t.overflow, kOvfTable);
+                    continue;
+                }
+                if ((c[k] >> 32) || f[k] > kMaxIndex) atomicOr(t.overflow, f[k] > kMaxIndex ? kOvfIndex : kOvfField);
+                atomicAdd(&scnt[off], (uint32_t)c[k]);
+                atomicMin(&sfst[off], (uint32_t)min((unsigned long long)kMaxIndex, f[k]));
+            }
+        }
+        __syncthreads();                  // s_pre / s_at of the next group
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < S; q += kMergeT) {
@@ -2620,17 +2662,20 @@ struct FlatDesc {
     uint32_t S;
 };
 
+// rep layout, 8 u64 per scratch slot: the row's words w0 .. w5 (zeros past S), the key, the class W --
+// so the 16-B pieces of a representative line up with the row's own pieces (w0 w1 | w2 w3 | w4 w5) and
+// with (key, W) last, one piece per lane of k_flat_verify's quads
 __global__ __launch_bounds__(256) void k_flat_reps(Tbl f, const uint64_t* __restrict__ rows, uint32_t S,
                                                    uint64_t* __restrict__ rep) {
     for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
         const Slot sl = f.slots[s];
-        uint64_t v[8] = {sl.key, 0, 0, 0, 0, 0, 0, 0};
+        uint64_t v[8] = {0, 0, 0, 0, 0, 0, sl.key, 0};
         if (sl.key != kEmpty) {
             const uint64_t* row = rows + (uint64_t)sl.first * S;
 #pragma unroll
             for (uint32_t j = 0; j < kRepW1; ++j) {
-                v[1 + j] = j < S ? row[j] : 0ull;
-                if (v[1 + j]) v[7] = j;
+                v[j] = j < S ? row[j] : 0ull;
+                if (v[j]) v[7] = j;
             }
         }
         uint4* dst = (uint4*)(rep + s * 8);
@@ -2640,62 +2685,75 @@ __global__ __launch_bounds__(256) void k_flat_reps(Tbl f, const uint64_t* __rest
     }
 }
 
-constexpr int kFlatVK = 2;
+// Every row against the representative of its fingerprint's slot, a quad of lanes per row: lane q
+// (0..2) loads the row's 16-B piece q (words 2q, 2q + 1) and the representative's piece q, lane 3
+// the representative's (key, W); the quad's four compares are AND-ed by two DPP quad permutes.  A
+// wave-instruction thus loads 16 whole rows (768 contiguous bytes) and 16 whole 64-B
+// representatives -- one cache line each -- where a lane per row issued six 8-B row loads and four
+// 16-B representative loads, each of the latter touching 64 different lines.  kFlatQK rows per quad
+// are in flight before any compare.  Every lane loads the row's fingerprint (the quad's four lanes
+// read one address).  A key other than the fingerprint at the slot sends the quad on to the next
+// slot (linear probing inside the slice); an empty slot or a word difference raises the flag.
+constexpr int kFlatQK = 4;
+__device__ __forceinline__ uint32_t quad_and(uint32_t v) {
+    v &= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);    // quad_perm [1, 0, 3, 2]
+    v &= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);    // quad_perm [2, 3, 0, 1]
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_flat_verify(Tbl f, const uint64_t* __restrict__ rows, uint32_t S, uint64_t n,
                                                      const uint64_t* __restrict__ fps, const uint64_t* __restrict__ rep,
                                                      uint32_t* __restrict__ flag) {
-    const uint64_t G = (uint64_t)gridDim.x * 256;
-    // two rows per lane per round, every load of both in flight before either is probed
-    for (uint64_t g0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; g0 < n; g0 += kFlatVK * G) {
-        uint64_t aw[kFlatVK][kRepW1], fp[kFlatVK], base[kFlatVK], off[kFlatVK];
-        uint4 e[kFlatVK][4];
+    const uint32_t q = threadIdx.x & 3u;
+    const uint64_t nq = (uint64_t)gridDim.x * 64u;
+    const uint64_t quad = (uint64_t)blockIdx.x * 64u + (threadIdx.x >> 2);
+    // this lane's words of a row: 2q, 2q + 1 (masked past S)
+    const bool w0in = 2u * q < S, w1in = 2u * q + 1u < S;
+    bool bad = false;
+    for (uint64_t r0 = quad; r0 < n; r0 += kFlatQK * nq) {
+        uint4 a[kFlatQK], e[kFlatQK];
+        uint64_t fp[kFlatQK], at[kFlatQK];
 #pragma unroll
-        for (int k = 0; k < kFlatVK; ++k) {
-            const uint64_t g = min(g0 + k * G, n - 1);
-            const uint64_t* a = rows + g * S;
-#pragma unroll
-            for (uint32_t j = 0; j < kRepW1; ++j) aw[k][j] = a[min(j, S - 1)];
-            fp[k] = fps[g];
+        for (int k = 0; k < kFlatQK; ++k) {
+            const uint64_t r = min(r0 + (uint64_t)k * nq, n - 1);
+            a[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (w0in) a[k] = *(const uint4*)(rows + r * S + 2u * q);
+            fp[k] = fps[r];
         }
 #pragma unroll
-        for (int k = 0; k < kFlatVK; ++k) {
-#pragma unroll
-            for (uint32_t j = 0; j < kRepW1; ++j)
-                if (j >= S) aw[k][j] = 0;
-            const uint64_t top = slot_top(f, fp[k]);
-            base[k] = top & ~f.slice_mask;
-            off[k] = top & f.slice_mask;
-            const uint4* p = (const uint4*)(rep + (base[k] + off[k]) * 8);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) e[k][j] = p[j];
+        for (int k = 0; k < kFlatQK; ++k) {
+            if (!w1in) a[k].z = a[k].w = 0u;
+            if (!w0in) a[k].x = a[k].y = 0u;
+            at[k] = slot_top(f, fp[k]);
+            e[k] = *(const uint4*)(rep + at[k] * 8 + 2u * q);
         }
-        bool bad = false;
 #pragma unroll
-        for (int k = 0; k < kFlatVK; ++k) {
-            bool b = true;
+        for (int k = 0; k < kFlatQK; ++k) {
+            const bool live = r0 + (uint64_t)k * nq < n;
+            const uint64_t base = at[k] & ~f.slice_mask;
+            uint64_t off = at[k] & f.slice_mask;
             for (uint64_t probe = 0; probe <= f.slice_mask; ++probe) {
                 if (probe) {
-                    off[k] = (off[k] + 1) & f.slice_mask;
-                    const uint4* p = (const uint4*)(rep + (base[k] + off[k]) * 8);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) e[k][j] = p[j];
+                    off = (off + 1) & f.slice_mask;
+                    e[k] = *(const uint4*)(rep + (base + off) * 8 + 2u * q);
                 }
-                const uint64_t key = (uint64_t)e[k][0].y << 32 | e[k][0].x;
-                if (key == fp[k]) {
-                    const uint64_t rw[6] = {(uint64_t)e[k][0].w << 32 | e[k][0].z, (uint64_t)e[k][1].y << 32 | e[k][1].x,
-                                            (uint64_t)e[k][1].w << 32 | e[k][1].z, (uint64_t)e[k][2].y << 32 | e[k][2].x,
-                                            (uint64_t)e[k][2].w << 32 | e[k][2].z, (uint64_t)e[k][3].y << 32 | e[k][3].x};
-                    b = false;
-#pragma unroll
-                    for (uint32_t j = 0; j < kRepW1; ++j) b |= aw[k][j] != rw[j];
+                const uint64_t key = (uint64_t)e[k].y << 32 | e[k].x;     // lane 3's piece: (key, W)
+                const bool same = a[k].x == e[k].x && a[k].y == e[k].y && a[k].z == e[k].z && a[k].w == e[k].w;
+                const uint32_t bits = (q < 3u ? (same ? 1u : 0u) | 6u
+                                              : 1u | (key == fp[k] ? 2u : 0u) | (key != kEmpty ? 4u : 0u));
+                const uint32_t all = quad_and(bits);
+                if (all & 2u) {              // the fingerprint's slot: its words decide
+                    bad |= live && !(all & 1u);
                     break;
                 }
-                if (key == kEmpty) break;
+                if (!(all & 4u)) {           // an empty slot: the fingerprint was never inserted
+                    bad |= live;
+                    break;
+                }
             }
-            bad |= b && g0 + k * G < n;
         }
-        if (__ballot(bad) && bad) atomicOr(flag, 1u);
     }
+    if (__ballot(bad) && bad) atomicOr(flag, 1u);
 }
 
 // scratch slot s -> (fp, count, first read, class W, the rep's words); false for a free slot, the
@@ -2711,7 +2769,7 @@ __device__ __forceinline__ bool flat_entry(const Tbl& f, const FlatDesc& d, cons
     fp = sl.key;
     cnt = ~sl.ncount;
     first = sl.first;
-    kw = rep + s * 8 + 1;
+    kw = rep + s * 8;
     return true;
 }
 
@@ -2720,6 +2778,10 @@ __device__ __forceinline__ bool flat_entry(const Tbl& f, const FlatDesc& d, cons
 // row per class; claim (the same grid, the same slots per block) gives each new key its block's
 // next row (LDS counters) -- no contended global counters (one per class, wave-aggregated, took
 // 3.1 ms on the f2 batch)
+// EXTRACT (the class tables are known to be empty, ss_classes_flat_extract): every entry is new, no
+// probe; found is not written
+extern "C++" {      // (a template inside this file's extern "C" section)
+template <bool EXTRACT>
 __global__ __launch_bounds__(256) void k_flat_fold_find(Tbl f, FlatDesc d, const uint64_t* __restrict__ rep,
                                                         const uint32_t* __restrict__ flag, uint64_t* __restrict__ found,
                                                         uint32_t* __restrict__ blkcnt) {
@@ -2731,6 +2793,10 @@ __global__ __launch_bounds__(256) void k_flat_fold_find(Tbl f, FlatDesc d, const
             uint64_t fp, first, at = kEmpty;
             uint32_t cnt, W;
             const uint64_t* kw;
+            if (EXTRACT) {
+                if (flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) atomicAdd(&lc[W], 1u);
+                continue;
+            }
             if (flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) {
                 const Tbl& t = d.tbl[W];
                 const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
@@ -2752,9 +2818,14 @@ __global__ __launch_bounds__(256) void k_flat_fold_find(Tbl f, FlatDesc d, const
     __syncthreads();
     if (threadIdx.x < kRepW1) blkcnt[(uint64_t)blockIdx.x * kRepW1 + threadIdx.x] = lc[threadIdx.x];
 }
+}  // extern "C++"
 
 // one block: blkcnt -> each block's first row per class (exclusive scan over the blocks, in place)
-__global__ __launch_bounds__(1024) void k_flat_fold_scan(uint32_t* __restrict__ blkcnt, uint32_t nblk) {
+struct FlatTotals {
+    uint64_t* p[kRepW1];            // class W's total (entries of the scratch of class W), null: not wanted
+};
+
+__global__ __launch_bounds__(1024) void k_flat_fold_scan(uint32_t* __restrict__ blkcnt, uint32_t nblk, FlatTotals tot) {
     __shared__ uint32_t carry[kRepW1];
     __shared__ uint32_t wsum[16][kRepW1];
     if (threadIdx.x < kRepW1) carry[threadIdx.x] = 0;
@@ -2785,6 +2856,7 @@ __global__ __launch_bounds__(1024) void k_flat_fold_scan(uint32_t* __restrict__ 
             for (uint32_t u = 0; u < 16; ++u) carry[threadIdx.x] += wsum[u][threadIdx.x];
         __syncthreads();
     }
+    if (threadIdx.x < kRepW1 && tot.p[threadIdx.x]) *tot.p[threadIdx.x] = carry[threadIdx.x];
 }
 
 __global__ __launch_bounds__(256) void k_flat_fold_claim(Tbl f, FlatDesc d, const uint64_t* __restrict__ rep,
@@ -2831,6 +2903,42 @@ __global__ __launch_bounds__(256) void k_flat_fold_claim(Tbl f, FlatDesc d, cons
         for (uint32_t q = 0; q < t.W; ++q) dst[q] = kw[q];
         t.slots[at].ncount = ~cnt;
         t.slots[at].first = (uint32_t)trow;
+    }
+}
+
+// the scratch's entries of every class as dense per-class arrays in the fold's row order (the rows
+// k_flat_fold_claim would give them in empty class tables): class W's entry at row gets its W + 1
+// key words (the W words and the length: the class table's key layout), its count, first = row, and
+// rmap[row] = base + its first read -- the layout ss_counter_extract_words gives the finish
+struct FlatOut {
+    uint64_t* words[kRepW1];
+    uint64_t* counts[kRepW1];
+    uint64_t* first[kRepW1];
+    uint64_t* rmap[kRepW1];
+    unsigned long long* ovf[kRepW1];
+    uint64_t cap[kRepW1];
+};
+
+__global__ __launch_bounds__(256) void k_flat_extract_claim(Tbl f, FlatDesc d, FlatOut o, const uint64_t* __restrict__ rep,
+                                                            const uint32_t* __restrict__ blkoff) {
+    __shared__ uint32_t lc[kRepW1];
+    if (threadIdx.x < kRepW1) lc[threadIdx.x] = blkoff[(uint64_t)blockIdx.x * kRepW1 + threadIdx.x];
+    __syncthreads();
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+        uint64_t fp, first;
+        uint32_t cnt, W;
+        const uint64_t* kw;
+        if (!flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) continue;
+        const uint32_t row = atomicAdd(&lc[W], 1u);     // LDS: this block's next row of class W
+        if (row >= o.cap[W]) {
+            atomicOr(o.ovf[W], (unsigned long long)kOvfTable);
+            continue;
+        }
+        o.rmap[W][row] = d.base + first;
+        o.counts[W][row] = cnt;
+        o.first[W][row] = row;
+        uint64_t* dst = o.words[W] + (uint64_t)row * (W + 1);
+        for (uint32_t q = 0; q <= W; ++q) dst[q] = kw[q];
     }
 }
 
@@ -3551,47 +3659,113 @@ int ss_counter_spill_counts(ss_counter* c, uint64_t* d_acc, void* stream) {
     return ss_check(hipGetLastError(), "k_spill_counts");
 }
 
-int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n, const uint64_t* d_fps,
-                                const ss_flat_class* cls, uint64_t base, uint32_t* d_flag,
-                                void* stream) {
-    if (!fpt || !cls || !d_flag || !d_rows || !d_fps) return ss_fail(SS_EARG, "null argument");
-    if (S < 3 || S > kRepW1) return ss_fail(SS_EARG, "read-order rows of 3 to 6 words");
-    if (n == 0) return SS_OK;
-    hipStream_t s = (hipStream_t)stream;
-    FlatDesc d{};
+// the scratch of the read-order path: rep[(cap + 1) * 8], found[cap + 1], then the per-block class
+// counts / first rows (fpt's aux buffer: it outlives the call, a deferred fold or extract reads it)
+static int flat_scratch(ss_counter* fpt, unsigned grid, uint64_t** rep, uint64_t** found, uint32_t** blk) {
+    const uint64_t fwords = fpt->cap + 1 + ((uint64_t)grid * kRepW1 + 1) / 2;
+    int rc = aux_scratch(fpt, ((fpt->cap + 1) * 8 + fwords) * sizeof(uint64_t), (void**)rep);
+    if (rc) return rc;
+    *found = *rep + (fpt->cap + 1) * 8;
+    *blk = (uint32_t*)(*found + fpt->cap + 1);
+    return SS_OK;
+}
+
+static int flat_desc(const ss_flat_class* cls, uint32_t S, uint64_t base, hipStream_t s, FlatDesc& d) {
+    d = FlatDesc{};
     d.S = S;
     d.base = base;
-    int rc = SS_OK;
     for (uint32_t W = 2; W + 1 <= S; ++W) {
         ss_counter* t = cls[W].table;
         if (!t) continue;
         if (t->L != kWordKeys || t->W != W + 1) return ss_fail(SS_EARG, "class table: set_words(W + 1) first");
-        if ((rc = flush_reset(t, s))) return rc;
+        int rc = flush_reset(t, s);
+        if (rc) return rc;
         t->occ_src = 0;
         d.tbl[W] = tbl_of(t);
         d.row0[W] = cls[W].base;
         d.rmap[W] = cls[W].rmap;
     }
-    if ((rc = flush_reset(fpt, s))) return rc;
+    return SS_OK;
+}
+
+int ss_classes_flat_verify(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n, const uint64_t* d_fps,
+                           uint32_t* d_flag, void* stream) {
+    if (!fpt || !d_flag || !d_rows || !d_fps) return ss_fail(SS_EARG, "null argument");
+    if (S < 3 || S > kRepW1) return ss_fail(SS_EARG, "read-order rows of 3 to 6 words");
+    if (n == 0) return SS_OK;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = flush_reset(fpt, s);
+    if (rc) return rc;
     const Tbl f = tbl_of(fpt);
-    uint64_t* rep = nullptr;
     const unsigned grid = grid_for(fpt->cap, 256, 256 * 16);
-    // the scratch: rep[(cap + 1) * 8], found[cap + 1], then the per-block class counts / first rows
-    const uint64_t fwords = fpt->cap + 1 + ((uint64_t)grid * kRepW1 + 1) / 2;
-    rc = aux_scratch(fpt, ((fpt->cap + 1) * 8 + fwords) * sizeof(uint64_t), (void**)&rep);
-    uint64_t* found = rep + (fpt->cap + 1) * 8;
-    if (!rc) {
-        uint32_t* blk = (uint32_t*)(found + fpt->cap + 1);
-        hipLaunchKernelGGL(k_flat_reps, dim3(grid), dim3(256), 0, s, f, d_rows, S, rep);
-        hipLaunchKernelGGL(k_flat_verify, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, s, f, d_rows, S, n, d_fps,
-                           (const uint64_t*)rep, d_flag);
-        hipLaunchKernelGGL(k_flat_fold_find, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep,
-                           (const uint32_t*)d_flag, found, blk);
-        hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(1024), 0, s, blk, grid);
-        hipLaunchKernelGGL(k_flat_fold_claim, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep,
-                           (const uint32_t*)d_flag, (const uint64_t*)found, (const uint32_t*)blk);
-        rc = ss_check(hipGetLastError(), "class verify / fold (read-order rows)");
+    uint64_t *rep = nullptr, *found = nullptr;
+    uint32_t* blk = nullptr;
+    if ((rc = flat_scratch(fpt, grid, &rep, &found, &blk))) return rc;
+    hipLaunchKernelGGL(k_flat_reps, dim3(grid), dim3(256), 0, s, f, d_rows, S, rep);
+    hipLaunchKernelGGL(k_flat_verify, dim3(grid_for(n, 64 * kFlatQK, 8192)), dim3(256), 0, s, f, d_rows, S, n, d_fps,
+                       (const uint64_t*)rep, d_flag);
+    return ss_check(hipGetLastError(), "class verify (read-order rows)");
+}
+
+int ss_classes_flat_fold(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, uint64_t base, const uint32_t* d_flag,
+                         void* stream) {
+    if (!fpt || !cls || !d_flag) return ss_fail(SS_EARG, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    FlatDesc d;
+    int rc = flat_desc(cls, S, base, s, d);
+    if (rc) return rc;
+    const Tbl f = tbl_of(fpt);
+    const unsigned grid = grid_for(fpt->cap, 256, 256 * 16);
+    uint64_t *rep = nullptr, *found = nullptr;
+    uint32_t* blk = nullptr;
+    if ((rc = flat_scratch(fpt, grid, &rep, &found, &blk))) return rc;
+    hipLaunchKernelGGL(k_flat_fold_find<false>, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep, d_flag, found, blk);
+    hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(1024), 0, s, blk, grid, FlatTotals{});
+    hipLaunchKernelGGL(k_flat_fold_claim, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep, d_flag,
+                       (const uint64_t*)found, (const uint32_t*)blk);
+    return ss_check(hipGetLastError(), "class fold (read-order rows)");
+}
+
+int ss_classes_flat_extract(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, uint64_t base,
+                            const ss_flat_out* out, const uint32_t* d_zero, void* stream) {
+    if (!fpt || !cls || !out || !d_zero) return ss_fail(SS_EARG, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    FlatDesc d;
+    int rc = flat_desc(cls, S, base, s, d);
+    if (rc) return rc;
+    FlatOut o{};
+    FlatTotals tot{};
+    for (uint32_t W = 2; W + 1 <= S; ++W) {
+        if (!cls[W].table) continue;
+        if (!out[W].words || !out[W].counts || !out[W].first || !out[W].total || !out[W].ovf)
+            return ss_fail(SS_EARG, "flat extract: outputs of every class");
+        if (cls[W].base) return ss_fail(SS_EARG, "flat extract: the class tables must hold no earlier rows");
+        o.words[W] = out[W].words;
+        o.counts[W] = out[W].counts;
+        o.first[W] = out[W].first;
+        o.rmap[W] = cls[W].rmap;
+        o.ovf[W] = (unsigned long long*)out[W].ovf;
+        o.cap[W] = out[W].cap;
+        tot.p[W] = out[W].total;
     }
+    const Tbl f = tbl_of(fpt);
+    const unsigned grid = grid_for(fpt->cap, 256, 256 * 16);
+    uint64_t *rep = nullptr, *found = nullptr;
+    uint32_t* blk = nullptr;
+    if ((rc = flat_scratch(fpt, grid, &rep, &found, &blk))) return rc;
+    hipLaunchKernelGGL(k_flat_fold_find<true>, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep, d_zero, found, blk);
+    hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(1024), 0, s, blk, grid, tot);
+    hipLaunchKernelGGL(k_flat_extract_claim, dim3(grid), dim3(256), 0, s, f, d, o, (const uint64_t*)rep,
+                       (const uint32_t*)blk);
+    return ss_check(hipGetLastError(), "class extract (read-order rows)");
+}
+
+int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n, const uint64_t* d_fps,
+                                const ss_flat_class* cls, uint64_t base, uint32_t* d_flag,
+                                void* stream) {
+    if (!cls) return ss_fail(SS_EARG, "null argument");
+    int rc = ss_classes_flat_verify(fpt, d_rows, S, n, d_fps, d_flag, stream);
+    if (!rc && n) rc = ss_classes_flat_fold(fpt, S, cls, base, d_flag, stream);
     return rc;
 }
 

@@ -610,6 +610,15 @@ struct ss_ingest {
     uint64_t since_spill = 0, spill_limit = 0xFFFFFFFEull;
     uint64_t max_rows = 0xFFFFFFFFull;   // rows a group's table indexes (its first index is u32);
                                          // ss_ingest_set_row_limit lowers it (test hook)
+    // A read-order chunk whose class tables held no rows before it (a single-chunk count, the usual
+    // case) leaves its verified scratch (fpt and its representatives) unfolded: the next add / export /
+    // merge folds it into the class tables first (flush_pending), a finish takes the entries straight
+    // from the scratch (ss_classes_flat_extract: no class-table inserts, no table extraction)
+    bool pend = false;
+    uint32_t pend_S = 0;
+    uint64_t pend_base = 0;
+    ss_flat_class pend_fc[6] = {};
+    DBuf<uint32_t> zero32;         // a device u32 that stays 0
     // ss_ingest_merge scratch (this engine as the destination): a source group's entries on this device
     DBuf<uint64_t> mg_words, mg_counts, mg_first, mg_take;
     DBuf<uint32_t> mg_lens;
@@ -808,6 +817,29 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
     return SS_OK;
 }
 
+// the deferred fold of a read-order chunk's scratch into its class tables (see ss_ingest::pend); one
+// sync for the tables' overflow words (sized from the sketch as for an immediate fold)
+int flush_pending(ss_ingest* g) {
+    if (!g->pend) return SS_OK;
+    g->pend = false;
+    hipStream_t s = g->stream;
+    int rc = g->ovf.ensure(6);
+    if (!rc) rc = ss_check(hipMemsetAsync(g->ovf.p, 0, 6 * 8, s), "ingest overflow reset");
+    if (!rc) rc = ss_classes_flat_fold(g->fpt, g->pend_S, g->pend_fc, g->pend_base, g->zero32.p, s);
+    for (uint32_t W = 2; W < 6 && !rc; ++W)
+        if (g->pend_fc[W].table) rc = ss_counter_overflow(g->pend_fc[W].table, g->ovf.p + W, s);
+    if (!rc) rc = ss_check(hipMemcpyAsync(g->h_bad, g->ovf.p, 6 * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
+    if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest deferred fold");
+    if (rc) return rc;
+    for (uint32_t W = 2; W < 6; ++W)
+        if (g->h_bad[W]) {
+            g->failed = true;
+            return ss_fail(SS_EFULL, "ingest: a length class's table ran full (its distinct-key estimate was low); "
+                                     "count again with ss_ingest_set_exact");
+        }
+    return SS_OK;
+}
+
 // The chunk's reads: d_buf[offs[i], + lens[i]) for i < n (global index base + i).  dense: reads are
 // back to back (offs = exclusive prefix of lens) and all have length dense_L (no split, no gather).
 // d_buf / d_offs / d_lens: the chunk on the device (the engine's own buffers, or the caller's for
@@ -818,6 +850,8 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (n == 0) return SS_OK;
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "ingest: a chunk holds < 2^32 reads");
+    int frc = flush_pending(g);      // the previous chunk's deferred fold (its scratch is reused below)
+    if (frc) return frc;
     if (g->since_spill + n > g->spill_limit) {
         const int src = spill_counts(g);
         if (src) return src;
@@ -922,7 +956,8 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if ((rc = g->cls_words.ensure(cls_words))) return rc;
         if (fused && (rc = g->cls_fps.ensure(flat ? n : cls_rows))) return rc;
         if (flat) {
-            if ((rc = g->cls_words.ensure(n * w1max))) return rc;
+            // (+2: k_flat_verify's quads load a row's last piece as 16 B, one word past an odd stride)
+            if ((rc = g->cls_words.ensure(n * w1max + 2))) return rc;
             rc = ss_encode_rows_impl(d_buf, d_offs, d_lens, n, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p,
                                      g->first_bad.p + nj, s);
         } else if (fused) {                 // one read-order pass, the registers updated in it
@@ -988,6 +1023,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         gr.rows += jb.m;
     }
     std::vector<uint64_t> cls_base(nj, 0);     // each class job's first table row (the exact redo)
+    bool pend_now = false;                     // this chunk's fold deferred (set below)
     if (!cls_jobs.empty() && fused) {
         // the classes' rows counted by fingerprint in one scratch table, checked against their
         // fingerprints' first rows and folded into the class tables (ss_classes_verify_fold); a
@@ -1018,9 +1054,21 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         rc = ss_check(hipMemsetAsync(g->cls_flag.p, g->sizing == 3 ? 1 : 0, 4, s), "ingest class flag reset");
         if (!rc && !flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, cls_rows, 0, s);
         if (!rc && !flat) rc = ss_classes_verify_fold(g->fpt, g->cls_fps.p, cr.data(), (uint32_t)cr.size(), g->cls_flag.p, s);
+        // the fold is deferred when every class of the chunk starts from an empty table (see pend)
+        bool defer = flat && g->sizing == 0;
+        for (uint32_t W = 2; W < 6; ++W) defer &= !fc[W].table || fc[W].base == 0;
         if (!rc && flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, n, 0, s);
-        if (!rc && flat)
+        if (!rc && flat && defer) {
+            rc = ss_classes_flat_verify(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, g->cls_flag.p, s);
+            if (!rc) {      // pending once the flag comes back clear (checked after the sync below)
+                g->pend_S = w1max;
+                g->pend_base = base;
+                for (uint32_t W = 0; W < 6; ++W) g->pend_fc[W] = fc[W];
+            }
+        } else if (!rc && flat) {
             rc = ss_classes_flat_verify_fold(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, fc, base, g->cls_flag.p, s);
+        }
+        pend_now = !rc && flat && defer;
         if (!rc) rc = ss_counter_overflow(g->fpt, g->ovf.p + nj, s);
         for (size_t q = 0; q < cls_jobs.size() && !rc; ++q) {
             const size_t j = cls_jobs[q];
@@ -1082,6 +1130,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         return ss_fail(SS_EFULL, "ingest: a length class's table ran full (its distinct-key estimate was low); "
                                      "count again with ss_ingest_set_exact");
     }
+    g->pend = pend_now && !(uint32_t)hb[2 * nj + 2];
     if (fused && !cls_jobs.empty() && (uint32_t)hb[2 * nj + 2]) {
         // two keys share a fingerprint: the class tables were left untouched, count them exactly
         if (flat) {     // class-ordered rows and their row maps first (the one-pass class encode)
@@ -1150,13 +1199,17 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
 // lens buffers, gr.m entries), then their entry counts and overflow words back in one sync; the
 // output word total gr.nw follows from the count (one word per entry for a length 1..32, W1 - 1 for
 // a class table).
-int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
+// flat: the pending scratch's classes are taken from the scratch (ss_classes_flat_extract) instead of
+// their (empty) tables -- the finish; export and merge flush the scratch into the tables first.
+int extract_groups(ss_ingest* g, std::vector<Group*>& placed, bool flat = false) {
     hipStream_t s = g->stream;
     int rc = g->scan.ensure(kScanBlocks + 2 + 3 * (uint64_t)kLenBins + 8);
     if (rc) return rc;
     uint64_t* d_cnt = g->scan.p + kScanBlocks + 2;
     rc = ss_check(hipMemsetAsync(d_cnt, 0, 3 * (uint64_t)kLenBins * 8, s), "ingest word totals reset");
     if (rc) return rc;
+    ss_flat_out fo[6] = {};
+    bool any_flat = false;
     for (auto& kv : g->groups) {
         Group& gr = kv.second;
         gr.m = 0;
@@ -1167,6 +1220,13 @@ int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
         if ((rc = gr.fps.ensure(cap)) || (rc = gr.words.ensure(cap * W)) || (rc = gr.counts.ensure(cap)) ||
             (rc = gr.first.ensure(cap)) || (rc = gr.lens.ensure(cap)))
             return rc;
+        if (flat && !gr.L && W - 1 < 6 && g->pend_fc[W - 1].table == gr.table) {
+            // at most cap entries (the extract raises the overflow word past it, as the fold would)
+            fo[W - 1] = {gr.words.p, gr.counts.p, gr.first.p, d_cnt + 3 * q, d_cnt + 3 * q + 1, cap};
+            any_flat = true;
+            placed.push_back(&gr);
+            continue;
+        }
         rc = ss_counter_extract_words(gr.table, 1, gr.fps.p, gr.lens.p, gr.words.p, gr.counts.p, gr.first.p, cap,
                                       d_cnt + 3 * q, s);
         if (!rc) rc = ss_counter_overflow(gr.table, d_cnt + 3 * q + 1, s);
@@ -1176,6 +1236,8 @@ int extract_groups(ss_ingest* g, std::vector<Group*>& placed) {
                                (const uint64_t*)(d_cnt + 3 * q), gr.acc.p, gr.acc_rows);
         placed.push_back(&gr);
     }
+    if (any_flat && (rc = ss_classes_flat_extract(g->fpt, g->pend_S, g->pend_fc, g->pend_base, fo, g->zero32.p, s)))
+        return rc;
     if (!placed.empty()) {
         rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 3 * placed.size() * 8, hipMemcpyDeviceToHost, s), "ingest");
         if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest extract");
@@ -1241,6 +1303,8 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_hll, (33ull << kHllLog) * 4, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = g->hll.ensure(33ull << kHllLog);
     if (!rc) rc = ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
+    if (!rc) rc = g->zero32.ensure(1);
+    if (!rc) rc = ss_check(hipMemsetAsync(g->zero32.p, 0, 4, g->stream), "ingest zero word");
     if (rc) {
         ss_ingest_destroy(g);
         return rc;
@@ -1273,6 +1337,7 @@ int ss_ingest_reset(ss_ingest* g) {
     g->nkeys = g->nwords = 0;
     g->failed = false;
     g->exported = false;
+    g->pend = false;
     if (!g->hll.p) return SS_OK;
     return ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
 }
@@ -1316,7 +1381,7 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->fq_ws.release(), g->fq_aux.release(), g->fq_counts.release();
     g->slot.release(), g->ordered.release(), g->woff.release(), g->scan.release(), g->gdesc.release();
     g->cls_words.release(), g->cls_fps.release(), g->hll.release(), g->ovf.release();
-    g->cls_flag.release();
+    g->cls_flag.release(), g->zero32.release();
     if (g->fpt) ss_counter_destroy(g->fpt);
     g->fpt = nullptr;
     g->mg_words.release(), g->mg_counts.release(), g->mg_first.release(), g->mg_lens.release(), g->mg_take.release();
@@ -1558,7 +1623,8 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     unsigned long long* bits = (unsigned long long*)g->slot.p;
     std::vector<GDesc> desc;
     std::vector<Group*> placed;
-    if ((rc = extract_groups(g, placed))) return rc;
+    // a deferred fold's classes come straight from the scratch (they stay pending: a later add folds them)
+    if ((rc = extract_groups(g, placed, g->pend))) return rc;
     for (size_t q = 0; q < placed.size(); ++q) {
         Group& gr = *placed[q];
         hipLaunchKernelGGL(k_mark, dim3(grid_of(gr.m + 1, 256)), dim3(256), 0, s, gr.first.p, gr.m, gr.rowmap.p,
@@ -1622,7 +1688,8 @@ int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys) {
     if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     (void)hipSetDevice(g->device);
     std::vector<Group*> placed;
-    int rc = extract_groups(g, placed);
+    int rc = flush_pending(g);
+    if (!rc) rc = extract_groups(g, placed);
     if (rc) return rc;
     uint64_t keys = 0;
     for (Group* gr : placed) {
@@ -1656,6 +1723,7 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
     if (dst->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (src_base < dst->nreads) return ss_fail(SS_EARG, "ingest merge: sources follow the destination's reads, in order");
     int rc = ss_check(hipSetDevice(dst->device), "ingest merge device");
+    if (!rc) rc = flush_pending(dst);
     if (rc) return rc;
     const bool peer = src->device != dst->device;
     if (peer) {

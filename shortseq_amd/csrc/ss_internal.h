@@ -64,6 +64,28 @@ struct ss_flat_class {
 extern "C" int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n,
                                            const uint64_t* d_fps, const ss_flat_class* cls, uint64_t base,
                                            uint32_t* d_flag, void* stream);
+// The same in two steps, so the fold can be deferred: ss_classes_flat_verify (representatives +
+// verify: sets *d_flag on a difference) then ss_classes_flat_fold (into the class tables; a no-op when
+// *d_flag).  The scratch (fpt and its representatives) must be left untouched in between.
+extern "C" int ss_classes_flat_verify(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n,
+                                      const uint64_t* d_fps, uint32_t* d_flag, void* stream);
+extern "C" int ss_classes_flat_fold(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, uint64_t base,
+                                    const uint32_t* d_flag, void* stream);
+// Instead of a fold into class tables that hold no earlier rows (cls[W].base == 0): the scratch's
+// entries as dense per-class arrays in the rows the fold would give them -- words [m][W + 1] (the
+// class table's key words), counts, first = row -- with cls[W].rmap[row] written as the fold writes
+// it, and the entry count into *total (u64).  The finish then orders them like extracted entries; a
+// later ss_classes_flat_fold of the same scratch gives the same rows.  d_zero: a device u32 holding 0.
+struct ss_flat_out {
+    uint64_t* words;
+    uint64_t* counts;
+    uint64_t* first;
+    uint64_t* total;
+    uint64_t* ovf;        // set nonzero when the class has more than cap entries (those are dropped)
+    uint64_t cap;
+};
+extern "C" int ss_classes_flat_extract(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, uint64_t base,
+                                       const ss_flat_out* out, const uint32_t* d_zero, void* stream);
 // Every entry's count moved into d_acc[first] (u64, indexed by the entry's first index: the drop-in
 // engine's rows) and the slot's count zeroed (the single-word sentinel keeps 1), so later inserts
 // cannot wrap a slot's u32 count (k_spill_counts).

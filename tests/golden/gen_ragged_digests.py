@@ -19,20 +19,27 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 import oracle  # noqa: E402
 
-# bench.py F2 line / tests/test_ragged.py
+# bench.py F2 lines / tests/test_ragged.py (U24: the high-diversity line, ~16M distinct keys)
 CASES = {"ragged_50M_L50-150_U20": dict(seed=41, pool_seed=42, U=1 << 20, n=50_000_000, Lmin=50, Lmax=150),
-         "ragged_1M_L1-300_U16": dict(seed=43, pool_seed=44, U=1 << 16, n=1_000_000, Lmin=1, Lmax=300)}
+         "ragged_1M_L1-300_U16": dict(seed=43, pool_seed=44, U=1 << 16, n=1_000_000, Lmin=1, Lmax=300),
+         "ragged_50M_L50-150_U24": dict(seed=41, pool_seed=42, U=1 << 24, n=50_000_000, Lmin=50, Lmax=150)}
 
 
 def main():
-    out = {}
+    """python3 gen_ragged_digests.py [names...]: (re)computes the named cases (default: all) and keeps
+    the others already in ragged_digests.json."""
+    path = os.path.join(HERE, "ragged_digests.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    only = set(sys.argv[1:]) or set(CASES)
     for name, c in CASES.items():
+        if name not in only:
+            continue
         t = time.time()
         lens, counts, words = oracle.ragged_pool_rows(c["seed"], c["pool_seed"], c["U"], c["n"], c["Lmin"], c["Lmax"])
         out[name] = dict(c, unique=int(len(lens)), nt=int((lens.astype("u8") * counts).sum()),
                          digest=oracle.rows_digest(lens, counts, words))
         print(name, out[name], f"{time.time() - t:.1f}s", flush=True)
-    with open(os.path.join(HERE, "ragged_digests.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -239,7 +239,28 @@ def test_device_ingest_ragged_errors(gpu):
         eng.close()
 
 
-@pytest.mark.parametrize("name", ["ragged_1M_L1-300_U16", "ragged_50M_L50-150_U20"])
+def test_device_ingest_high_diversity_slice(gpu, oracle):
+    """the F2 reads at high diversity (pool 2^24), a 5M-read slice (~4.3M distinct
+    keys: the scratch table, its representatives and the class tables far past one per 48 reads)
+    against the generator-derived rows (oracle.ragged_pool_rows, pinned to oracle.count)."""
+    import shortseq_amd.batch as B
+    d = _digests()["ragged_50M_L50-150_U24"]
+    n = 5_000_000
+    blob, offs, lens = B.synth_ragged_pool_reads(n, d["seed"], d["pool_seed"], d["U"], d["Lmin"], d["Lmax"],
+                                                 device=gpu)
+    eng = B.DeviceIngest(gpu)
+    try:
+        eng.count(blob, offs, lens)
+        gl, gc, gw = eng.results()
+    finally:
+        eng.close()
+    del blob, offs, lens
+    el, ec, ew = oracle.ragged_pool_rows(d["seed"], d["pool_seed"], d["U"], n, d["Lmin"], d["Lmax"])
+    assert len(gl) == len(el) and len(el) > 4_000_000
+    assert np.array_equal(gl, el) and np.array_equal(gc, ec) and np.array_equal(gw, ew)
+
+
+@pytest.mark.parametrize("name", ["ragged_1M_L1-300_U16", "ragged_50M_L50-150_U20", "ragged_50M_L50-150_U24"])
 def test_device_ingest_ragged_digest(gpu, oracle, name):
     """Full size (bench.py F2): the engine's rows (dict order, lengths, counts, words) hash to the
     generator-derived digest (tests/golden/ragged_digests.json)."""

@@ -71,7 +71,8 @@ def main():
         t2 = time.perf_counter()
         lens_, cnts, _w = engs[0].results(copy=False)
         t3 = time.perf_counter()
-        assert len(lens_) == n and int(cnts.sum()) == n, (len(lens_), int(cnts.sum()))
+        # (a 2^40 pool repeats ~n^2 / 2^41 items: distinct keys slightly below n)
+        assert len(lens_) > 0.999 * n and int(cnts.sum()) == n, (len(lens_), int(cnts.sum()))
         return (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3
 
     for r in range(a.rounds + 1):
