@@ -397,6 +397,14 @@ int ss_ingest_add_device(ss_ingest* g, const uint8_t* d_blob, uint64_t nbytes, c
 int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_read, uint64_t cap, uint64_t* h_len);
 int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords);
 int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words);
+/* Compact results (new in this ABI version; replaces nothing -- the reference's dict holds Python
+ * ints): with ss_ingest_set_results_format(g, 1) the finish writes lengths as u16 and counts as u32
+ * (*h_count_bytes = 4) unless a count needs u64 (8); the words are as above.  About 15 % fewer bytes
+ * over PCIe for ragged keys.  ss_ingest_results refuses the compact format and
+ * ss_ingest_results_compact the plain one.  Format 2: compact with u64 counts always (a test hook). */
+int ss_ingest_set_results_format(ss_ingest* g, int compact);
+int ss_ingest_results_compact(ss_ingest* g, const uint16_t** h_lens, const void** h_counts, uint32_t* h_count_bytes,
+                              const uint64_t** h_words);
 
 /* Multi-device reduce of one call (ShortSeqCounter(list) / read_and_count_fastq sharded over several
  * engines, counter.pyx:10-70; north_star: "an RCCL reduce over xGMI only for the final histogram

@@ -99,6 +99,9 @@ SIGNATURES = [
     ("ss_ingest_error", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int), _P, _U64, C.POINTER(C.c_uint64)]),
     ("ss_ingest_finish", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("ss_ingest_results", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    ("ss_ingest_set_results_format", C.c_int, [_P, C.c_int]),
+    ("ss_ingest_results_compact", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                            C.POINTER(C.c_uint32), C.POINTER(C.c_void_p)]),
     ("ss_ingest_export", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("ss_ingest_merge", C.c_int, [_P, _P, _U64]),
     ("ss_stager_create", C.c_int, [C.c_int, _U64, _U32, _U32, C.POINTER(C.c_void_p)]),

@@ -444,12 +444,16 @@ class DeviceIngest:
     words u64) numpy arrays in first-occurrence order (the ShortSeqCounter dict order: row k has
     ceil(lens[k] / 32) words, one for lengths 0..32).  A rejected read raises like ShortSeqCounter."""
 
-    def __init__(self, device=None, exact: bool = False, *, _sizing: Optional[int] = None):
+    def __init__(self, device=None, exact: bool = False, *, compact=True, _sizing: Optional[int] = None):
+        """compact: the rows cross PCIe with u16 lengths and u32 counts (u64 when a count needs it):
+        results() then returns those dtypes (ss_ingest_set_results_format)."""
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         h = C.c_void_p()
         check(lib().ss_ingest_create(dev.index or 0, C.byref(h)), "ss_ingest_create")
         self._h = h
+        self.compact = int(compact)      # (2: compact with u64 counts, a test hook)
+        check(lib().ss_ingest_set_results_format(h, self.compact), "ss_ingest_set_results_format")
         self._exact = exact
         self._sizing = int(exact) if _sizing is None else _sizing   # 2: test hook, undersized class tables
         self._fresh = True
@@ -489,16 +493,24 @@ class DeviceIngest:
             raise_read_error(bytes(buf)[:ln.value], idx.value)
 
     def results(self, copy: bool = True):
-        """(lens u32, counts u64, words u64) of the count so far, first-occurrence order.  copy=False
+        """(lens, counts, words u64) of the count so far, first-occurrence order: lens u32 and counts
+        u64, or with compact=True lens u16 and counts u32 (u64 when a count needs it).  copy=False
         returns views of the engine's pinned result buffers, valid until the next count / reset /
         close (no host-side copy of the rows)."""
         K, NW = C.c_uint64(), C.c_uint64()
         check(lib().ss_ingest_finish(self._h, C.byref(K), C.byref(NW)), "ss_ingest_finish")
         pl, pc, pw = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        check(lib().ss_ingest_results(self._h, C.byref(pl), C.byref(pc), C.byref(pw)), "ss_ingest_results")
         k, nw = K.value, NW.value
-        lens = np.ctypeslib.as_array((C.c_uint32 * max(1, k)).from_address(pl.value))[:k] if k else np.zeros(0, np.uint32)
-        cnts = np.ctypeslib.as_array((C.c_uint64 * max(1, k)).from_address(pc.value))[:k] if k else np.zeros(0, np.uint64)
+        if self.compact:
+            cb = C.c_uint32()
+            check(lib().ss_ingest_results_compact(self._h, C.byref(pl), C.byref(pc), C.byref(cb), C.byref(pw)),
+                  "ss_ingest_results_compact")
+            lt, ct = C.c_uint16, (C.c_uint32 if cb.value == 4 else C.c_uint64)
+        else:
+            check(lib().ss_ingest_results(self._h, C.byref(pl), C.byref(pc), C.byref(pw)), "ss_ingest_results")
+            lt, ct = C.c_uint32, C.c_uint64
+        lens = np.ctypeslib.as_array((lt * max(1, k)).from_address(pl.value))[:k] if k else np.zeros(0, lt)
+        cnts = np.ctypeslib.as_array((ct * max(1, k)).from_address(pc.value))[:k] if k else np.zeros(0, ct)
         wds = np.ctypeslib.as_array((C.c_uint64 * max(1, nw)).from_address(pw.value))[:nw] if nw else np.zeros(0, np.uint64)
         if copy:
             lens, cnts, wds = lens.copy(), cnts.copy(), wds.copy()

@@ -3689,7 +3689,7 @@ static int flat_desc(const ss_flat_class* cls, uint32_t S, uint64_t base, hipStr
 }
 
 int ss_classes_flat_verify(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n, const uint64_t* d_fps,
-                           uint32_t* d_flag, void* stream) {
+                           uint32_t* d_flag, void* stream, void* ev_reps) {
     if (!fpt || !d_flag || !d_rows || !d_fps) return ss_fail(SS_EARG, "null argument");
     if (S < 3 || S > kRepW1) return ss_fail(SS_EARG, "read-order rows of 3 to 6 words");
     if (n == 0) return SS_OK;
@@ -3702,6 +3702,7 @@ int ss_classes_flat_verify(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, 
     uint32_t* blk = nullptr;
     if ((rc = flat_scratch(fpt, grid, &rep, &found, &blk))) return rc;
     hipLaunchKernelGGL(k_flat_reps, dim3(grid), dim3(256), 0, s, f, d_rows, S, rep);
+    if (ev_reps && (rc = ss_check(hipEventRecord((hipEvent_t)ev_reps, s), "class reps event"))) return rc;
     hipLaunchKernelGGL(k_flat_verify, dim3(grid_for(n, 64 * kFlatQK, 8192)), dim3(256), 0, s, f, d_rows, S, n, d_fps,
                        (const uint64_t*)rep, d_flag);
     return ss_check(hipGetLastError(), "class verify (read-order rows)");
@@ -3764,7 +3765,7 @@ int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_rows, uint32_
                                 const ss_flat_class* cls, uint64_t base, uint32_t* d_flag,
                                 void* stream) {
     if (!cls) return ss_fail(SS_EARG, "null argument");
-    int rc = ss_classes_flat_verify(fpt, d_rows, S, n, d_fps, d_flag, stream);
+    int rc = ss_classes_flat_verify(fpt, d_rows, S, n, d_fps, d_flag, stream, nullptr);
     if (!rc && n) rc = ss_classes_flat_fold(fpt, S, cls, base, d_flag, stream);
     return rc;
 }

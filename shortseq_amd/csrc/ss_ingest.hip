@@ -233,9 +233,11 @@ __global__ __launch_bounds__(256) void k_rowmap(const uint64_t* __restrict__ sel
 
 // table entry e -> the bit of its global first read (rowmap[first[e]]) in the read map; e == m: the
 // empty read's entry at global read `extra` (kNoSlot: none)
+// (dm: the entry count on the device instead -- the speculative finish, which runs without a sync)
 __global__ __launch_bounds__(256) void k_mark(const uint64_t* __restrict__ first, uint64_t m,
                                               const uint64_t* __restrict__ rowmap, uint64_t extra,
-                                              unsigned long long* __restrict__ bits) {
+                                              unsigned long long* __restrict__ bits, const uint64_t* dm = nullptr) {
+    if (dm) m = min(m, *dm);          // (m: the buffers' capacity then)
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e <= m; e += (uint64_t)gridDim.x * 256) {
         const uint64_t r = e < m ? rowmap[first[e]] : extra;
         if (r != kNoSlot) atomicOr(&bits[r >> 6], 1ull << (r & 63));
@@ -247,19 +249,22 @@ __global__ __launch_bounds__(256) void k_mark(const uint64_t* __restrict__ first
 __global__ __launch_bounds__(256) void k_rank(const uint64_t* __restrict__ first, uint64_t m,
                                               const uint64_t* __restrict__ rowmap, uint32_t g, uint64_t extra,
                                               const unsigned long long* __restrict__ bits,
-                                              const uint64_t* __restrict__ wpre, uint64_t* __restrict__ ordered) {
+                                              const uint64_t* __restrict__ wpre, uint64_t* __restrict__ ordered,
+                                              const uint64_t* dm = nullptr, uint64_t ocap = ~0ull) {
+    if (dm) m = min(m, *dm);          // (m: the buffers' capacity then; ocap: ordered's)
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e <= m; e += (uint64_t)gridDim.x * 256) {
         const uint64_t r = e < m ? rowmap[first[e]] : extra;
         if (r == kNoSlot) continue;
         const uint64_t pos = wpre[r >> 6] + (uint64_t)__popcll(bits[r >> 6] & ((1ull << (r & 63)) - 1ull));
-        ordered[pos] = e < m ? ((uint64_t)g << 32) | e : (uint64_t)kEmptyGroup << 32;
+        if (pos < ocap) ordered[pos] = e < m ? ((uint64_t)g << 32) | e : (uint64_t)kEmptyGroup << 32;
     }
 }
 
 // export: entry e's first read (engine-local) = rowmap[first[e]]
 // the largest of m counts (atomicMax into *mx): an export's largest count sizes the merge passes
 __global__ __launch_bounds__(256) void k_count_max(const uint64_t* __restrict__ counts, uint64_t m,
-                                                   unsigned long long* mx) {
+                                                   unsigned long long* mx, const uint64_t* dm = nullptr) {
+    if (dm) m = min(m, *dm);
     uint64_t v = 0;
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
         v = max(v, counts[e]);
@@ -349,8 +354,9 @@ __device__ __forceinline__ uint32_t item_val(const uint64_t* src, uint64_t i, co
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_scan_count(const uint64_t* __restrict__ src, uint64_t n, const GDesc* gd,
-                                                    uint64_t* __restrict__ blksum) {
+                                                    uint64_t* __restrict__ blksum, const uint64_t* dn = nullptr) {
     __shared__ uint64_t s[256];
+    if (dn) n = min(n, *dn);
     const uint64_t per = (n + kScanBlocks - 1) / kScanBlocks;
     const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
     uint64_t c = 0;
@@ -385,9 +391,11 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint64_t* __restrict__ blksum
 // offset)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_scan_apply(const uint64_t* __restrict__ src, uint64_t n, const GDesc* gd,
-                                                    const uint64_t* __restrict__ blksum, uint64_t* __restrict__ dst) {
+                                                    const uint64_t* __restrict__ blksum, uint64_t* __restrict__ dst,
+                                                    const uint64_t* dn = nullptr) {
     __shared__ uint64_t wsum[4];
     __shared__ uint64_t run;
+    if (dn) n = min(n, *dn);
     const uint64_t per = (n + kScanBlocks - 1) / kScanBlocks;
     const uint64_t lo = min(n, (uint64_t)blockIdx.x * per), hi = min(n, lo + per);
     if (threadIdx.x == 0) run = blksum[blockIdx.x];
@@ -420,14 +428,52 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint64_t* __restrict__
 // contiguous run of the output) staged in LDS and stored lane per word, so every store to host
 // memory is a coalesced run (the device-to-host stores run at the PCIe rate, ~55 GB/s, as the blit
 // copies did, with the gather itself hidden under them).
+// Where the rows go: the pinned buffer hbase (hcap bytes) laid out as results_layout() says.  dK /
+// dNW: the entry and word totals on the device (the speculative finish; K is then the ordered
+// buffer's bound) -- a layout past hcap, or more entries than the bound, raises *bad and writes
+// nothing.  compact: lengths u16, and counts u32 unless *dmax (the largest count) needs u64.
+struct OutLayout {
+    uint8_t* hbase;
+    uint64_t hcap;
+    const uint64_t* dK;
+    const uint64_t* dNW;
+    uint64_t NW;
+    const unsigned long long* dmax;
+    unsigned long long* bad;
+    int compact;
+};
+
+// byte offsets of the counts and words arrays of K rows (lengths at 0): the plain layout has u32
+// lengths and u64 counts; compact, u16 lengths and counts of cw bytes (4 or 8)
+__host__ __device__ __forceinline__ void results_layout(uint64_t K, int compact, uint32_t cw, uint64_t& cnt_off,
+                                                        uint64_t& word_off) {
+    cnt_off = ((compact ? K * 2 : K * 4) + 15) & ~15ull;
+    word_off = cnt_off + (((compact ? K * cw : K * 8) + 15) & ~15ull);
+}
+
 constexpr uint32_t kOutBuf = 4096;
 __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict__ ordered, uint64_t K,
                                                      const GDesc* __restrict__ gd, const uint64_t* __restrict__ woff,
-                                                     uint64_t empty_count, uint32_t* h_len, uint64_t* h_cnt,
-                                                     uint64_t* h_words) {
+                                                     uint64_t empty_count, OutLayout o) {
     __shared__ uint64_t buf[kOutBuf];
     __shared__ uint64_t s_lo, s_hi;
+    const uint32_t cw = (o.compact == 2 || (o.compact && ((o.dmax && (*o.dmax >> 32)) || (empty_count >> 32)))) ? 8u : 4u;
+    uint64_t co, wo0;
+    if (o.dK) {                     // (K: the ordered buffer's bound then)
+        const uint64_t Kd = *o.dK;
+        results_layout(Kd, o.compact, cw, co, wo0);
+        if (Kd > K || wo0 + *o.dNW * 8 > o.hcap) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(o.bad, 1ull);
+            return;
+        }
+        K = Kd;
+    } else {
+        results_layout(K, o.compact, cw, co, wo0);
+    }
+    uint8_t* h_cnt = o.hbase + co;
+    uint64_t* h_words = (uint64_t*)(o.hbase + wo0);
     const uint64_t k0 = (uint64_t)blockIdx.x * 256, k = k0 + threadIdx.x;
+    if (k0 >= K) return;
     uint32_t L = 0, nw = 0;
     uint64_t cnt = 0, wo = 0;
     const uint64_t* src = nullptr;
@@ -445,8 +491,14 @@ __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict_
             src = d.words + e * d.W;
         }
         wo = woff[k];
-        h_len[k] = L;
-        h_cnt[k] = cnt;
+        if (o.compact) {
+            ((uint16_t*)o.hbase)[k] = (uint16_t)L;
+            if (cw == 4) ((uint32_t*)h_cnt)[k] = (uint32_t)cnt;
+            else ((uint64_t*)h_cnt)[k] = cnt;
+        } else {
+            ((uint32_t*)o.hbase)[k] = L;
+            ((uint64_t*)h_cnt)[k] = cnt;
+        }
     }
     const uint64_t klast = min(k0 + 255, K - 1);
     if (k == k0) s_lo = wo;
@@ -462,6 +514,22 @@ __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict_
         __syncthreads();
         for (uint64_t o = c0 + threadIdx.x; o < c1; o += 256) h_words[o] = buf[o - c0];
         __syncthreads();
+    }
+}
+
+// the speculative finish's entry total: the classes' extracted counts (tot[2 .. 5]) + the empty read's
+// entry; out[1] = the words total (the word scan's), out[2] = its bad flag folded with the extract's
+// capacity overflow -- then one D2H copy of out[0 .. 2]
+__global__ void k_spec_total(uint64_t* sd, uint64_t empty, const uint64_t* nw_total, uint64_t empty_count = 0) {
+    if (threadIdx.x != 0) return;
+    uint64_t K = empty;
+    for (int W = 2; W < 6; ++W) K += sd[W];
+    sd[6] = K;
+    if (nw_total) {
+        sd[9] = sd[6];
+        sd[10] = *nw_total;
+        sd[11] = sd[7] | sd[8];
+        sd[12] = max(sd[12], empty_count);   // (the largest count, the empty read's entry too)
     }
 }
 
@@ -619,6 +687,22 @@ struct ss_ingest {
     uint64_t pend_base = 0;
     ss_flat_class pend_fc[6] = {};
     DBuf<uint32_t> zero32;         // a device u32 that stays 0
+    // The speculative finish: the FIRST chunk of a count (nothing before it), taken by the read-order
+    // path with its fold deferred, queues the finish's whole work -- the scratch's entries extracted,
+    // read-order ranks, the rows gathered into the pinned result buffer -- on spec_stream right after
+    // the scratch's representatives, beside the verify, with every size kept on the device (no sync).
+    // ss_ingest_finish then only waits for it; any other call waits for it first (spec_wait) and
+    // drops it.  A verify that flags a shared fingerprint, a rejected read, or a result larger than
+    // the bound it was given invalidates it (the finish then runs the ordinary way).
+    hipStream_t spec_stream = nullptr;
+    hipEvent_t ev_reps = nullptr, ev_spec = nullptr;
+    bool spec_inflight = false;
+    bool spec_valid = false;
+    DBuf<uint64_t> spec_dev;       // [12]: class totals [2..5], K [6], gather bad [7], extract overflow [8], K NW bad [9..11]
+    uint64_t* h_spec = nullptr;    // pinned [4]: K, NW, bad, the largest count
+    int compact = 0;               // ss_ingest_set_results_format: u16 lengths, u32 counts when they fit
+    bool wide = false;             // compact results whose counts need u64
+    GDesc* h_gdesc = nullptr;      // pinned [8]
     // ss_ingest_merge scratch (this engine as the destination): a source group's entries on this device
     DBuf<uint64_t> mg_words, mg_counts, mg_first, mg_take;
     DBuf<uint32_t> mg_lens;
@@ -840,13 +924,112 @@ int flush_pending(ss_ingest* g) {
     return SS_OK;
 }
 
+// wait for a queued speculative finish (its buffers are about to be reused) and drop it
+void spec_wait(ss_ingest* g) {
+    if (g->spec_inflight) (void)hipEventSynchronize(g->ev_spec);
+    g->spec_inflight = false;
+    g->spec_valid = false;
+}
+
+// the speculative finish of a first read-order chunk (see ss_ingest::spec_stream); need[W]: the class's
+// distinct-key estimate (bounds the result buffer; a larger result invalidates the speculation)
+int spec_launch(ss_ingest* g, const uint64_t* need, uint64_t N) {
+    hipStream_t ss = g->spec_stream;
+    int rc = ss_check(hipStreamWaitEvent(ss, g->ev_reps, 0), "spec wait");
+    if (rc) return rc;
+    std::vector<Group*> cls;
+    ss_flat_out fo[6] = {};
+    uint64_t k_ub = 1, nw_ub = 0;
+    if ((rc = g->spec_dev.ensure(13))) return rc;
+    for (auto& kv : g->groups) {
+        Group& gr = kv.second;
+        if (!gr.table || gr.L || gr.W1 - 1 >= 6 || g->pend_fc[gr.W1 - 1].table != gr.table) continue;
+        const uint32_t W = gr.W1 - 1;
+        const uint64_t cap = gr.cap + 1;
+        if ((rc = gr.words.ensure(cap * gr.W1)) || (rc = gr.counts.ensure(cap)) || (rc = gr.first.ensure(cap)))
+            return rc;
+        fo[W] = {gr.words.p, gr.counts.p, gr.first.p, g->spec_dev.p + W, g->spec_dev.p + 8, cap};
+        const uint64_t kb = std::min<uint64_t>(cap, need[W] + 1024);
+        k_ub += kb;
+        nw_ub += kb * W;
+        cls.push_back(&gr);
+    }
+    if (cls.empty() || cls.size() > 8) return SS_OK;
+    const uint64_t NB = (N + 63) / 64;
+    const uint64_t lb = (k_ub * 4 + 15) & ~15ull, out_bytes = lb + k_ub * 8 + nw_ub * 8 + 16;
+    if ((rc = g->slot.ensure(NB)) || (rc = g->ordered.ensure(k_ub + 1)) || (rc = g->woff.ensure(std::max(k_ub, NB) + 1)) ||
+        (rc = g->gdesc.ensure(8)) || (rc = g->scan.ensure(kScanBlocks + 2 + 3 * (uint64_t)kLenBins + 8)) ||
+        (rc = g->out_host.ensure(out_bytes)))
+        return rc;
+    uint64_t* sd = g->spec_dev.p;
+    unsigned long long* bits = (unsigned long long*)g->slot.p;
+    if ((rc = ss_check(hipMemsetAsync(sd, 0, 13 * 8, ss), "spec reset")) ||
+        (rc = ss_check(hipMemsetAsync(g->slot.p, 0, NB * 8, ss), "spec read map reset")))
+        return rc;
+    if ((rc = ss_classes_flat_extract(g->fpt, g->pend_S, g->pend_fc, g->pend_base, fo, g->zero32.p, ss))) return rc;
+    for (size_t q = 0; q < cls.size(); ++q) {
+        Group& gr = *cls[q];
+        const uint64_t cap = gr.cap + 1;
+        hipLaunchKernelGGL(k_mark, dim3(grid_of(cap, 256)), dim3(256), 0, ss, gr.first.p, cap, gr.rowmap.p, kNoSlot, bits,
+                           (const uint64_t*)(sd + gr.W1 - 1));
+        g->h_gdesc[q] = {gr.words.p, gr.counts.p, gr.W1, gr.L};
+    }
+    const uint64_t empty_at = g->empty_count ? g->empty_first : kNoSlot;
+    if (g->empty_count)
+        hipLaunchKernelGGL(k_mark, dim3(1), dim3(256), 0, ss, (const uint64_t*)nullptr, (uint64_t)0,
+                           (const uint64_t*)nullptr, empty_at, bits, (const uint64_t*)nullptr);
+    hipLaunchKernelGGL(k_spec_total, dim3(1), dim3(64), 0, ss, sd, g->empty_count ? 1ull : 0ull, (const uint64_t*)nullptr);
+    if ((rc = ss_check(hipMemcpyAsync(g->gdesc.p, g->h_gdesc, cls.size() * sizeof(GDesc), hipMemcpyHostToDevice, ss),
+                       "spec desc")))
+        return rc;
+    hipLaunchKernelGGL((k_scan_count<0>), dim3(kScanBlocks), dim3(256), 0, ss, g->slot.p, NB, (const GDesc*)g->gdesc.p,
+                       g->scan.p, (const uint64_t*)nullptr);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ss, g->scan.p);
+    hipLaunchKernelGGL((k_scan_apply<0>), dim3(kScanBlocks), dim3(256), 0, ss, g->slot.p, NB, (const GDesc*)g->gdesc.p,
+                       g->scan.p, g->woff.p, (const uint64_t*)nullptr);
+    for (size_t q = 0; q < cls.size(); ++q) {
+        Group& gr = *cls[q];
+        const uint64_t cap = gr.cap + 1;
+        hipLaunchKernelGGL(k_rank, dim3(grid_of(cap, 256)), dim3(256), 0, ss, gr.first.p, cap, gr.rowmap.p, (uint32_t)q,
+                           kNoSlot, bits, g->woff.p, g->ordered.p, (const uint64_t*)(sd + gr.W1 - 1), k_ub);
+    }
+    if (g->empty_count)
+        hipLaunchKernelGGL(k_rank, dim3(1), dim3(256), 0, ss, (const uint64_t*)nullptr, (uint64_t)0,
+                           (const uint64_t*)nullptr, 0u, empty_at, bits, g->woff.p, g->ordered.p, (const uint64_t*)nullptr,
+                           k_ub);
+    // word offsets of the ordered entries (K on the device; past the bound the gather refuses)
+    hipLaunchKernelGGL((k_scan_count<1>), dim3(kScanBlocks), dim3(256), 0, ss, g->ordered.p, k_ub, (const GDesc*)g->gdesc.p,
+                       g->scan.p, (const uint64_t*)(sd + 6));
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ss, g->scan.p);
+    hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, ss, g->ordered.p, k_ub, (const GDesc*)g->gdesc.p,
+                       g->scan.p, g->woff.p, (const uint64_t*)(sd + 6));
+    // the largest count (the compact layout's count width) into sd[12]
+    unsigned long long* dmax = (unsigned long long*)(sd + 12);
+    for (size_t q = 0; q < cls.size() && g->compact; ++q)
+        hipLaunchKernelGGL(k_count_max, dim3(grid_of(cls[q]->cap + 1, 256)), dim3(256), 0, ss, cls[q]->counts.p,
+                           cls[q]->cap + 1, dmax, (const uint64_t*)(sd + cls[q]->W1 - 1));
+    OutLayout ol{g->out_host.p, g->out_host.cap, sd + 6, g->scan.p + kScanBlocks, 0, dmax,
+                 (unsigned long long*)(sd + 7), g->compact};
+    hipLaunchKernelGGL(k_gather_host, dim3((unsigned)((k_ub + 255) / 256)), dim3(256), 0, ss, g->ordered.p, k_ub,
+                       (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, ol);
+    hipLaunchKernelGGL(k_spec_total, dim3(1), dim3(64), 0, ss, sd, g->empty_count ? 1ull : 0ull,
+                       (const uint64_t*)(g->scan.p + kScanBlocks), g->empty_count);
+    rc = ss_check(hipMemcpyAsync(g->h_spec, sd + 9, 4 * 8, hipMemcpyDeviceToHost, ss), "spec sizes");
+    if (!rc) rc = ss_check(hipEventRecord(g->ev_spec, ss), "spec event");
+    if (!rc) rc = ss_check(hipGetLastError(), "spec finish");
+    if (!rc) g->spec_inflight = true;
+    return rc;
+}
+
 // The chunk's reads: d_buf[offs[i], + lens[i]) for i < n (global index base + i).  dense: reads are
 // back to back (offs = exclusive prefix of lens) and all have length dense_L (no split, no gather).
 // d_buf / d_offs / d_lens: the chunk on the device (the engine's own buffers, or the caller's for
 // ss_ingest_add_device); h_chunk / h_offs: the same bytes on the host when there (the first rejected
 // read's bytes are then taken from there, else copied back).
 int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t nbytes,
-                  uint64_t n, uint32_t dense_L, const std::vector<uint64_t>* h_offs, const uint8_t* h_chunk) {
+                  uint64_t n, uint32_t dense_L, const std::vector<uint64_t>* h_offs, const uint8_t* h_chunk,
+                  bool spec_ok = false) {
+    spec_wait(g);                    // (its buffers are reused below; the results change)
     if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (n == 0) return SS_OK;
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "ingest: a chunk holds < 2^32 reads");
@@ -1059,12 +1242,16 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         for (uint32_t W = 2; W < 6; ++W) defer &= !fc[W].table || fc[W].base == 0;
         if (!rc && flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, n, 0, s);
         if (!rc && flat && defer) {
-            rc = ss_classes_flat_verify(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, g->cls_flag.p, s);
+            // a first chunk of an add_device / add_blob also queues the speculative finish beside the verify
+            const bool spec = spec_ok && base == 0 && g->bad_index == kNoSlot;
+            rc = ss_classes_flat_verify(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, g->cls_flag.p, s,
+                                        spec ? (void*)g->ev_reps : nullptr);
             if (!rc) {      // pending once the flag comes back clear (checked after the sync below)
                 g->pend_S = w1max;
                 g->pend_base = base;
                 for (uint32_t W = 0; W < 6; ++W) g->pend_fc[W] = fc[W];
             }
+            if (!rc && spec) rc = spec_launch(g, need_cls, base + n);
         } else if (!rc && flat) {
             rc = ss_classes_flat_verify_fold(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, fc, base, g->cls_flag.p, s);
         }
@@ -1132,6 +1319,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     }
     g->pend = pend_now && !(uint32_t)hb[2 * nj + 2];
     if (fused && !cls_jobs.empty() && (uint32_t)hb[2 * nj + 2]) {
+        spec_wait(g);                  // (it reads the class tables the exact path now fills)
         // two keys share a fingerprint: the class tables were left untouched, count them exactly
         if (flat) {     // class-ordered rows and their row maps first (the one-pass class encode)
             uint64_t* cmap[33] = {nullptr};
@@ -1192,6 +1380,8 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     }
     // a too-long read's bytes (the message does not quote them) are not needed
     g->nreads += n;
+    // the queued finish stands for this count unless a read was rejected (the finish is then not asked for)
+    g->spec_valid = g->spec_inflight && g->pend && g->bad_index == kNoSlot;
     return SS_OK;
 }
 
@@ -1303,6 +1493,11 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_hll, (33ull << kHllLog) * 4, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = g->hll.ensure(33ull << kHllLog);
     if (!rc) rc = ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
+    if (!rc) rc = ss_check(hipStreamCreateWithFlags(&g->spec_stream, hipStreamNonBlocking), "ingest spec stream");
+    if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_reps, hipEventDisableTiming), "ingest event");
+    if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_spec, hipEventDisableTiming), "ingest event");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_spec, 4 * 8, hipHostMallocDefault), "ingest pinned");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_gdesc, 8 * sizeof(GDesc), hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = g->zero32.ensure(1);
     if (!rc) rc = ss_check(hipMemsetAsync(g->zero32.p, 0, 4, g->stream), "ingest zero word");
     if (rc) {
@@ -1316,6 +1511,7 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
 int ss_ingest_reset(ss_ingest* g) {
     if (!g) return ss_fail(SS_EARG, "null ingest");
     (void)hipSetDevice(g->device);
+    spec_wait(g);
     // tables go back to the pool; a length's row map and extraction buffers stay (grow-only) for the
     // next call (a fresh hipMalloc per call and length costs more than the counting)
     for (auto& kv : g->groups) {
@@ -1388,6 +1584,12 @@ int ss_ingest_destroy(ss_ingest* g) {
     if (g->h_hll) (void)hipHostFree(g->h_hll);
     if (g->h_split) (void)hipHostFree(g->h_split);
     if (g->h_bad) (void)hipHostFree(g->h_bad);
+    if (g->h_spec) (void)hipHostFree(g->h_spec);
+    if (g->h_gdesc) (void)hipHostFree(g->h_gdesc);
+    g->spec_dev.release();
+    if (g->ev_reps) (void)hipEventDestroy(g->ev_reps);
+    if (g->ev_spec) (void)hipEventDestroy(g->ev_spec);
+    if (g->spec_stream) (void)hipStreamDestroy(g->spec_stream);
     for (int k = 0; k < ss_ingest::kSide; ++k) {
         if (g->side[k]) (void)hipStreamDestroy(g->side[k]);
         if (g->ev_join[k]) (void)hipEventDestroy(g->ev_join[k]);
@@ -1426,7 +1628,7 @@ int ss_ingest_add_blob(ss_ingest* g, const uint8_t* h_blob, const uint32_t* h_le
         rc = ss_check(hipMemcpyAsync(g->offs.p, offs.data(), n * 8, hipMemcpyHostToDevice, s), "ingest H2D");
         if (!rc) rc = ss_check(hipMemcpyAsync(g->dlens.p, h_lens, n * 4, hipMemcpyHostToDevice, s), "ingest H2D");
     }
-    if (!rc) rc = process_chunk(g, g->dbuf.p, g->offs.p, g->dlens.p, total, n, dense, &offs, h_blob);
+    if (!rc) rc = process_chunk(g, g->dbuf.p, g->offs.p, g->dlens.p, total, n, dense, &offs, h_blob, true);
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest blob");   // staging reusable after return
     return rc;
 }
@@ -1436,7 +1638,7 @@ int ss_ingest_add_device(ss_ingest* g, const uint8_t* d_blob, uint64_t nbytes, c
     if (!g || (n && (!d_blob || !d_offsets || !d_lens))) return ss_fail(SS_EARG, "null argument");
     if (n == 0 || g->bad_index != kNoSlot) return SS_OK;
     (void)hipSetDevice(g->device);
-    int rc = process_chunk(g, d_blob, d_offsets, d_lens, nbytes, n, 0, nullptr, nullptr);
+    int rc = process_chunk(g, d_blob, d_offsets, d_lens, nbytes, n, 0, nullptr, nullptr, true);
     if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest device blob");
     return rc;
 }
@@ -1616,6 +1818,20 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     const uint64_t N = g->nreads;
     int rc = SS_OK;
     *h_nkeys = *h_nwords = 0;
+    if (g->spec_valid) {            // the speculative finish queued by the add: wait for it
+        const int e = ss_check(hipEventSynchronize(g->ev_spec), "ingest spec finish");
+        g->spec_inflight = false;
+        if (e) return e;
+        if (!g->h_spec[2]) {        // (stays valid: a second finish returns the same rows)
+            g->nkeys = g->h_spec[0];
+            g->nwords = g->h_spec[1];
+            g->wide = g->compact == 2 || (g->compact && ((g->h_spec[3] >> 32) || (g->empty_count >> 32)));
+            *h_nkeys = g->nkeys;
+            *h_nwords = g->nwords;
+            return SS_OK;
+        }
+    }
+    spec_wait(g);
     if (N == 0) return SS_OK;
     const uint64_t NB = (N + 63) / 64;      // read-map words
     if ((rc = g->slot.ensure(NB))) return rc;
@@ -1641,11 +1857,22 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
         K += gr->m;
         NW += gr->nw;
     }
-    // results -> pinned host: lens [K] u32 | pad | counts [K] u64 | words [NW] u64, written by the gather
-    const uint64_t lb = (K * 4 + 15) & ~15ull, cb = K * 8, wb = NW * 8;
+    // results -> pinned host (results_layout: lens | counts | words), written by the gather
+    uint64_t co = 0, wo0 = 0;
+    results_layout(K, 0, 8, co, wo0);      // (the plain layout bounds the compact one)
     if ((rc = g->gdesc.ensure(desc.size() + 1)) || (rc = g->ordered.ensure(K + 1)) ||
-        (rc = g->woff.ensure(std::max(K, NB) + 1)) || (rc = g->out_host.ensure(lb + cb + wb + 16)))
+        (rc = g->woff.ensure(std::max(K, NB) + 1)) || (rc = g->out_host.ensure(wo0 + NW * 8 + 16)) ||
+        (rc = g->spec_dev.ensure(13)))
         return rc;
+    // compact results: the largest count decides the count width (on the device: no sync)
+    unsigned long long* dmax = (unsigned long long*)(g->spec_dev.p + 12);
+    if (g->compact) {
+        if ((rc = ss_check(hipMemsetAsync(dmax, 0, 8, s), "ingest count max"))) return rc;
+        for (Group* gr : placed)
+            if (gr->m)
+                hipLaunchKernelGGL(k_count_max, dim3(grid_of(gr->m, 256)), dim3(256), 0, s, gr->counts.p, gr->m, dmax,
+                                   (const uint64_t*)nullptr);
+    }
     if (!desc.empty())
         rc = ss_check(hipMemcpyAsync(g->gdesc.p, desc.data(), desc.size() * sizeof(GDesc), hipMemcpyHostToDevice, s),
                       "ingest desc");
@@ -1670,14 +1897,17 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p);
     if (K >= (1ull << 31) * 256) return ss_fail(SS_EARG, "ingest: too many distinct keys for one gather");
+    OutLayout ol{g->out_host.p, g->out_host.cap, nullptr, nullptr, NW, dmax, nullptr, g->compact};
     hipLaunchKernelGGL(k_gather_host, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, g->ordered.p, K,
-                       (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, (uint32_t*)g->out_host.p,
-                       (uint64_t*)(g->out_host.p + lb), (uint64_t*)(g->out_host.p + lb + cb));
+                       (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, ol);
     rc = ss_check(hipGetLastError(), "k_gather_host");
+    if (!rc && g->compact)
+        rc = ss_check(hipMemcpyAsync(g->h_spec + 3, dmax, 8, hipMemcpyDeviceToHost, s), "ingest count max");
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest out");
     if (rc) return rc;
     g->nkeys = K;
     g->nwords = NW;
+    g->wide = g->compact == 2 || (g->compact && ((g->h_spec[3] >> 32) || (g->empty_count >> 32)));
     *h_nkeys = K;
     *h_nwords = NW;
     return SS_OK;
@@ -1688,6 +1918,7 @@ int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys) {
     if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     (void)hipSetDevice(g->device);
     std::vector<Group*> placed;
+    spec_wait(g);
     int rc = flush_pending(g);
     if (!rc) rc = extract_groups(g, placed);
     if (rc) return rc;
@@ -1722,6 +1953,8 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
     if (!src->exported) return ss_fail(SS_EARG, "ingest merge: ss_ingest_export the source first");
     if (dst->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     if (src_base < dst->nreads) return ss_fail(SS_EARG, "ingest merge: sources follow the destination's reads, in order");
+    spec_wait(dst);
+    spec_wait(src);
     int rc = ss_check(hipSetDevice(dst->device), "ingest merge device");
     if (!rc) rc = flush_pending(dst);
     if (rc) return rc;
@@ -1808,10 +2041,35 @@ int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
 
 int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words) {
     if (!g || !h_lens || !h_counts || !h_words) return ss_fail(SS_EARG, "null argument");
-    const uint64_t lb = (g->nkeys * 4 + 15) & ~15ull;
+    if (g->compact) return ss_fail(SS_EARG, "ingest results: compact format set (ss_ingest_results_compact)");
+    uint64_t co = 0, wo = 0;
+    results_layout(g->nkeys, 0, 8, co, wo);
     *h_lens = (const uint32_t*)g->out_host.p;
-    *h_counts = (const uint64_t*)(g->out_host.p + lb);
-    *h_words = (const uint64_t*)(g->out_host.p + lb + g->nkeys * 8);
+    *h_counts = (const uint64_t*)(g->out_host.p + co);
+    *h_words = (const uint64_t*)(g->out_host.p + wo);
+    return SS_OK;
+}
+
+int ss_ingest_set_results_format(ss_ingest* g, int compact) {
+    if (!g) return ss_fail(SS_EARG, "null ingest");
+    // (2: compact with u64 counts whatever they hold -- a test hook for the wide branch)
+    if (compact < 0 || compact > 2) return ss_fail(SS_EARG, "results format 0 (plain), 1 (compact) or 2");
+    spec_wait(g);                  // (a queued finish wrote the other layout)
+    g->compact = compact;
+    return SS_OK;
+}
+
+int ss_ingest_results_compact(ss_ingest* g, const uint16_t** h_lens, const void** h_counts, uint32_t* h_count_bytes,
+                              const uint64_t** h_words) {
+    if (!g || !h_lens || !h_counts || !h_count_bytes || !h_words) return ss_fail(SS_EARG, "null argument");
+    if (!g->compact) return ss_fail(SS_EARG, "ingest results: plain format (ss_ingest_results)");
+    const uint32_t cw = g->wide ? 8u : 4u;
+    uint64_t co = 0, wo = 0;
+    results_layout(g->nkeys, 1, cw, co, wo);
+    *h_lens = (const uint16_t*)g->out_host.p;
+    *h_counts = (const void*)(g->out_host.p + co);
+    *h_count_bytes = cw;
+    *h_words = (const uint64_t*)(g->out_host.p + wo);
     return SS_OK;
 }
 

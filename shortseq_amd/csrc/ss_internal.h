@@ -65,10 +65,10 @@ extern "C" int ss_classes_flat_verify_fold(ss_counter* fpt, const uint64_t* d_ro
                                            const uint64_t* d_fps, const ss_flat_class* cls, uint64_t base,
                                            uint32_t* d_flag, void* stream);
 // The same in two steps, so the fold can be deferred: ss_classes_flat_verify (representatives +
-// verify: sets *d_flag on a difference) then ss_classes_flat_fold (into the class tables; a no-op when
+// verify: sets *d_flag on a difference; ev_reps, when given, is recorded between the two) then ss_classes_flat_fold (into the class tables; a no-op when
 // *d_flag).  The scratch (fpt and its representatives) must be left untouched in between.
 extern "C" int ss_classes_flat_verify(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, uint64_t n,
-                                      const uint64_t* d_fps, uint32_t* d_flag, void* stream);
+                                      const uint64_t* d_fps, uint32_t* d_flag, void* stream, void* ev_reps);
 extern "C" int ss_classes_flat_fold(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, uint64_t base,
                                     const uint32_t* d_flag, void* stream);
 // Instead of a fold into class tables that hold no earlier rows (cls[W].base == 0): the scratch's

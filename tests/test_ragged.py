@@ -435,3 +435,117 @@ def test_device_ingest_read_index_past_2_32(gpu, oracle):
     assert gl.tolist() == el.tolist()
     assert gc.tolist() == ec.tolist()
     assert np.array_equal(gw, ew)
+
+
+def test_device_ingest_flat_pending_paths(gpu, oracle):
+    """The read-order path's deferred fold and speculative finish (50-150 nt: every read a class read
+    of at most 5 words).  A first chunk leaves its scratch unfolded and queues the finish beside the
+    verify; results() twice, a second chunk after results() (the pending scratch folded first), and a
+    second chunk with no results() in between all give the generator-derived rows of the reads so far."""
+    import shortseq_amd.batch as B
+    seed, ps, U, n, lo, hi = 61, 62, 30_000, 400_000, 50, 150
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    cut = 150_000
+
+    def rows(m):
+        return oracle.ragged_pool_rows(seed, ps, U, m, lo, hi)
+
+    def same(got, want):
+        assert got[0].tolist() == want[0].tolist()
+        assert got[1].tolist() == want[1].tolist()
+        assert np.array_equal(got[2], want[2])
+
+    eng = B.DeviceIngest(gpu)
+    try:
+        eng.count(blob, offs[:cut], lens[:cut])
+        first = eng.results()
+        same(first, rows(cut))
+        same(eng.results(), rows(cut))                 # a second finish: the same rows
+        eng.count(blob, offs[cut:], lens[cut:])        # folds the pending scratch, then counts
+        same(eng.results(), rows(n))
+        eng.reset()
+        eng.count(blob, offs[:cut], lens[:cut])
+        eng.count(blob, offs[cut:], lens[cut:])        # no finish between the two chunks
+        same(eng.results(), rows(n))
+        eng.reset()
+        eng.count(blob, offs, lens)                    # one chunk after a reset: speculation again
+        same(eng.results(), rows(n))
+    finally:
+        eng.close()
+
+
+def test_device_ingest_flat_pending_export_merge(gpu, oracle):
+    """Engines whose only chunk took the read-order path (fold pending, finish queued) exported and
+    merged: the export folds the scratch first, the destination's queued finish is dropped by the merge."""
+    import shortseq_amd.batch as B
+    seed, ps, U, n, lo, hi = 63, 64, 20_000, 300_000, 60, 140
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    cuts = [0, 100_000, 170_000, n]
+    engs = [B.DeviceIngest(gpu) for _ in range(3)]
+    try:
+        for k, e in enumerate(engs):
+            e.count(blob, offs[cuts[k]:cuts[k + 1]], lens[cuts[k]:cuts[k + 1]])
+        for e in engs[1:]:
+            e.export()
+        engs[0].merge(engs[1], cuts[1])
+        engs[0].merge(engs[2], cuts[2])
+        gl, gc, gw = engs[0].results()
+    finally:
+        for e in engs:
+            e.close()
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    assert gl.tolist() == el.tolist() and gc.tolist() == ec.tolist() and np.array_equal(gw, ew)
+
+
+def test_device_ingest_flat_rejected_read_then_reset(gpu):
+    """A rejected read in a read-order first chunk: the queued finish is dropped, count() raises the
+    reference's message, and after reset() the engine counts a clean batch exactly."""
+    import shortseq_amd.batch as B
+    from shortseq_amd import ShortSeqCounter
+    blob, offs, lens = B.synth_ragged_pool_reads(200_000, 65, 66, 5000, 50, 150, device=gpu)
+    import shortseq_amd as sq
+    bad = blob.clone()
+    o, ln = int(offs[123_456].item()), int(lens[123_456].item())
+    bad[o + 7] = ord("N")
+    with pytest.raises(Exception) as want:          # the reference's message for that read
+        sq.pack(bytes(bad[o:o + ln].cpu().numpy()))
+    eng = B.DeviceIngest(gpu)
+    try:
+        with pytest.raises(Exception) as ei:
+            eng.count(bad, offs, lens)
+        assert str(ei.value) == str(want.value)
+        eng.reset()
+        eng.count(blob, offs, lens)
+        gl, gc, _gw = eng.results()
+        assert int(gc.sum()) == 200_000
+        host = blob.cpu().numpy().tobytes()
+        oo, ll = offs.cpu().numpy(), lens.cpu().numpy()
+        want = ShortSeqCounter([host[oo[i]:oo[i] + ll[i]] for i in range(200_000)], device="host")
+        assert len(gl) == len(want) and sorted(gc.tolist()) == sorted(want.values())
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("fmt", [0, 1, 2])
+def test_device_ingest_results_formats(gpu, oracle, fmt):
+    """The three result layouts (plain u32 / u64; compact u16 / u32; compact with u64 counts) carry
+    the same rows, through the speculative finish (first read-order chunk) and the ordinary one
+    (mixed lengths, a second chunk)."""
+    import shortseq_amd.batch as B
+    for seed, ps, U, n, lo, hi in ((71, 72, 9000, 200_000, 50, 150), (73, 74, 9000, 200_000, 0, 300)):
+        blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+        eng = B.DeviceIngest(gpu, compact=fmt)
+        try:
+            eng.count(blob, offs[:n // 2], lens[:n // 2])
+            eng.count(blob, offs[n // 2:], lens[n // 2:])
+            gl, gc, gw = eng.results()
+            eng.reset()
+            eng.count(blob, offs, lens)
+            gl1, gc1, gw1 = eng.results()
+        finally:
+            eng.close()
+        assert gl.dtype == (np.uint32 if fmt == 0 else np.uint16)
+        assert gc.dtype == (np.uint32 if fmt == 1 else np.uint64)
+        el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+        for a, b, c in ((gl, gc, gw), (gl1, gc1, gw1)):
+            assert a.tolist() == el.tolist() and b.tolist() == ec.tolist() and np.array_equal(c, ew)
