@@ -70,6 +70,14 @@ libab)
     done
   done
   cp $L/libshortseq_amd_new.so $L/libshortseq_amd.so ;;
+libtest)      # libtest <variant> <secs> <pytest selection...>: the -m gpu tests against libshortseq_amd_<variant>.so
+  v=$1; secs=$2; shift 2
+  L=shortseq_amd/lib
+  cp $L/libshortseq_amd.so $L/libshortseq_amd_new.so
+  trap "cp $L/libshortseq_amd_new.so $L/libshortseq_amd.so" EXIT
+  cp $L/libshortseq_amd_$v.so $L/libshortseq_amd.so
+  timeout -k 10 "$secs" python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu "$@" > gpurun_out/pytest_${TAG}_$v.log 2>&1
+  rc=$?; tail -5 gpurun_out/pytest_${TAG}_$v.log; exit $rc ;;
 libprof)      # libprof <name> <regex> "<variants>" -- <cmd...>: rocprof kernel stats of cmd per library variant
   name=$1; pat=$2; vs=$3; shift 3; [ "$1" = "--" ] && shift
   L=shortseq_amd/lib

@@ -1767,22 +1767,25 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
     // each (4 dependent steps for a 2M-record run) -- no separate pass over every record
     __shared__ uint32_t s_lo[kMergeSearchRuns], s_hi[kMergeSearchRuns];
     if (!bounds) {
-        const uint32_t lane = threadIdx.x & 63u;
-        for (uint32_t q = threadIdx.x >> 6; q < 2 * n_runs; q += kMergeT / 64) {
+        // a 32-ary search per (run, edge), one half-wave each: the block's 16 half-waves take up to 16
+        // searches at once (8 owners: all 14 in one round of ~5 dependent steps, where a wave per
+        // search took two rounds of 4)
+        const uint32_t hl = threadIdx.x & 31u, hsh = threadIdx.x & 32u;
+        for (uint32_t q = threadIdx.x >> 5; q < 2 * n_runs; q += kMergeT / 32) {
             const uint32_t run = q >> 1, target = j + (q & 1u);
             const uint64_t beg = run_off[2 * run], end = run_off[2 * run + 1];
             uint64_t L = beg, H = end;     // the first record of region >= target lies in [L, H]
             while (H > L) {
                 const uint64_t len = H - L;
-                const uint64_t p = L + len * lane / 64;
+                const uint64_t p = L + len * hl / 32;
                 const bool below = run_rel(t, recs, p, reg_lo, nreg) < target;
-                const uint32_t c = (uint32_t)__popcll(__ballot(below));
+                const uint32_t c = (uint32_t)__popcll((__ballot(below) >> hsh) & 0xFFFFFFFFull);
                 if (c == 0) break;
-                const uint64_t nx = c < 64 ? L + len * c / 64 : H;
-                L = L + len * (c - 1) / 64 + 1;
+                const uint64_t nx = c < 32 ? L + len * c / 32 : H;
+                L = L + len * (c - 1) / 32 + 1;
                 H = nx;
             }
-            if (lane == 0) ((q & 1u) ? s_hi : s_lo)[run] = (uint32_t)(L - beg);
+            if (hl == 0) ((q & 1u) ? s_hi : s_lo)[run] = (uint32_t)(L - beg);
         }
     }
     __syncthreads();
@@ -3670,7 +3673,7 @@ static int flat_scratch(ss_counter* fpt, unsigned grid, uint64_t** rep, uint64_t
     return SS_OK;
 }
 
-static int flat_desc(const ss_flat_class* cls, uint32_t S, uint64_t base, hipStream_t s, FlatDesc& d) {
+static int flat_desc(const ss_flat_class* cls, uint32_t S, uint64_t base, hipStream_t s, FlatDesc& d, bool flush = true) {
     d = FlatDesc{};
     d.S = S;
     d.base = base;
@@ -3678,6 +3681,12 @@ static int flat_desc(const ss_flat_class* cls, uint32_t S, uint64_t base, hipStr
         ss_counter* t = cls[W].table;
         if (!t) continue;
         if (t->L != kWordKeys || t->W != W + 1) return ss_fail(SS_EARG, "class table: set_words(W + 1) first");
+        if (!flush) {
+            d.tbl[W] = tbl_of(t);
+            d.row0[W] = cls[W].base;
+            d.rmap[W] = cls[W].rmap;
+            continue;
+        }
         int rc = flush_reset(t, s);
         if (rc) return rc;
         t->occ_src = 0;
@@ -3703,7 +3712,9 @@ int ss_classes_flat_verify(ss_counter* fpt, const uint64_t* d_rows, uint32_t S, 
     if ((rc = flat_scratch(fpt, grid, &rep, &found, &blk))) return rc;
     hipLaunchKernelGGL(k_flat_reps, dim3(grid), dim3(256), 0, s, f, d_rows, S, rep);
     if (ev_reps && (rc = ss_check(hipEventRecord((hipEvent_t)ev_reps, s), "class reps event"))) return rc;
-    hipLaunchKernelGGL(k_flat_verify, dim3(grid_for(n, 64 * kFlatQK, 8192)), dim3(256), 0, s, f, d_rows, S, n, d_fps,
+    // one short block per 64 kFlatQK rows (no persistent grid): a kernel queued on another stream
+    // beside the verify (the speculative finish) gets CU slots as the verify's blocks retire
+    hipLaunchKernelGGL(k_flat_verify, dim3(grid_for(n, 64 * kFlatQK, 0)), dim3(256), 0, s, f, d_rows, S, n, d_fps,
                        (const uint64_t*)rep, d_flag);
     return ss_check(hipGetLastError(), "class verify (read-order rows)");
 }
@@ -3732,7 +3743,7 @@ int ss_classes_flat_extract(ss_counter* fpt, uint32_t S, const ss_flat_class* cl
     if (!fpt || !cls || !out || !d_zero) return ss_fail(SS_EARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
     FlatDesc d;
-    int rc = flat_desc(cls, S, base, s, d);
+    int rc = flat_desc(cls, S, base, s, d, false);
     if (rc) return rc;
     FlatOut o{};
     FlatTotals tot{};

@@ -86,6 +86,11 @@ __global__ __launch_bounds__(64) void k_len_count(const uint32_t* __restrict__ l
     // kLenStep steps' lengths loaded before any is binned (one load per step left the pass
     // latency-bound: 130 us for 50M reads)
     constexpr int kLenStep = 8;
+    // fast set (a 33-160-nt batch, empty reads too): a step whose reads all fall in the empty bin or
+    // the classes W = 2 .. 5 is counted in lane registers -- count and first read per bin, reduced
+    // across the wave once at the end -- with no peels and no LDS updates
+    constexpr uint32_t kFast = 5;            // bins 0, kClassBin0 + 2 .. kClassBin0 + 5
+    uint32_t rc[kFast] = {0, 0, 0, 0, 0}, rf[kFast] = {~0u, ~0u, ~0u, ~0u, ~0u};
     for (uint64_t s0 = lo; s0 < hi; s0 += 64 * kLenStep) {
         uint32_t bs[kLenStep];
 #pragma unroll
@@ -98,6 +103,16 @@ __global__ __launch_bounds__(64) void k_len_count(const uint32_t* __restrict__ l
             const uint64_t i0 = s0 + 64u * k;
             const bool live = i0 + threadIdx.x < hi;
             const uint32_t b = bs[k];
+            const uint32_t fi = b == 0u ? 0u : (b >= kClassBin0 + 2u && b <= kClassBin0 + 5u) ? b - kClassBin0 - 1u : kFast;
+            if (__ballot(live && fi == kFast) == 0ull) {
+#pragma unroll
+                for (uint32_t t = 0; t < kFast; ++t)
+                    if (live && fi == t) {
+                        ++rc[t];
+                        rf[t] = min(rf[t], (uint32_t)(i0 + threadIdx.x));
+                    }
+                continue;
+            }
             uint64_t pending = __ballot(live);
             while (pending) {
                 const int leader = __ffsll((long long)pending) - 1;
@@ -109,6 +124,19 @@ __global__ __launch_bounds__(64) void k_len_count(const uint32_t* __restrict__ l
                 }
                 pending &= ~mine;
             }
+        }
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < kFast; ++t) {
+        uint32_t c = rc[t], m = rf[t];
+        for (int o = 32; o > 0; o >>= 1) {
+            c += (uint32_t)__shfl_xor((int)c, o);
+            m = min(m, (uint32_t)__shfl_xor((int)m, o));
+        }
+        if (threadIdx.x == 0 && c) {
+            const uint32_t b = t == 0 ? 0u : kClassBin0 + 1u + t;
+            h[b] += c;
+            f[b] = min(f[b], m);
         }
     }
     __syncthreads();
@@ -349,7 +377,7 @@ __device__ __forceinline__ uint32_t item_val(const uint64_t* src, uint64_t i, co
     const uint32_t g = (uint32_t)(v >> 32);
     if (g == kEmptyGroup) return 0u;
     const GDesc d = gd[g];
-    return d.L ? d.W : (entry_len(d, (uint32_t)v) + 31) / 32;
+    return d.L ? d.W : d.W - 1;      // a class table's entries (W + 1 key words) all have W words
 }
 
 template <int MODE>
@@ -431,16 +459,17 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint64_t* __restrict__
 // Where the rows go: the pinned buffer hbase (hcap bytes) laid out as results_layout() says.  dK /
 // dNW: the entry and word totals on the device (the speculative finish; K is then the ordered
 // buffer's bound) -- a layout past hcap, or more entries than the bound, raises *bad and writes
-// nothing.  compact: lengths u16, and counts u32 unless *dmax (the largest count) needs u64.
+// nothing.  compact: lengths u16, and counts u32 unless wide (the host's rule: a count can reach
+// 2^32 only when the engine has counted that many reads).
 struct OutLayout {
     uint8_t* hbase;
     uint64_t hcap;
     const uint64_t* dK;
     const uint64_t* dNW;
     uint64_t NW;
-    const unsigned long long* dmax;
     unsigned long long* bad;
     int compact;
+    int wide;               // compact counts as u64 (a count can reach 2^32: the engine's reads can)
 };
 
 // byte offsets of the counts and words arrays of K rows (lengths at 0): the plain layout has u32
@@ -457,7 +486,7 @@ __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict_
                                                      uint64_t empty_count, OutLayout o) {
     __shared__ uint64_t buf[kOutBuf];
     __shared__ uint64_t s_lo, s_hi;
-    const uint32_t cw = (o.compact == 2 || (o.compact && ((o.dmax && (*o.dmax >> 32)) || (empty_count >> 32)))) ? 8u : 4u;
+    const uint32_t cw = o.wide ? 8u : 4u;
     uint64_t co, wo0;
     if (o.dK) {                     // (K: the ordered buffer's bound then)
         const uint64_t Kd = *o.dK;
@@ -924,6 +953,12 @@ int flush_pending(ss_ingest* g) {
     return SS_OK;
 }
 
+// compact results carry u64 counts only when a count can reach 2^32: no count exceeds the reads
+// counted (format 2 forces u64: a test hook)
+bool results_wide(const ss_ingest* g) {
+    return g->compact == 2 || (g->compact && g->nreads > 0xFFFFFFFFull);
+}
+
 // wait for a queued speculative finish (its buffers are about to be reused) and drop it
 void spec_wait(ss_ingest* g) {
     if (g->spec_inflight) (void)hipEventSynchronize(g->ev_spec);
@@ -1003,13 +1038,9 @@ int spec_launch(ss_ingest* g, const uint64_t* need, uint64_t N) {
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ss, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, ss, g->ordered.p, k_ub, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p, (const uint64_t*)(sd + 6));
-    // the largest count (the compact layout's count width) into sd[12]
-    unsigned long long* dmax = (unsigned long long*)(sd + 12);
-    for (size_t q = 0; q < cls.size() && g->compact; ++q)
-        hipLaunchKernelGGL(k_count_max, dim3(grid_of(cls[q]->cap + 1, 256)), dim3(256), 0, ss, cls[q]->counts.p,
-                           cls[q]->cap + 1, dmax, (const uint64_t*)(sd + cls[q]->W1 - 1));
-    OutLayout ol{g->out_host.p, g->out_host.cap, sd + 6, g->scan.p + kScanBlocks, 0, dmax,
-                 (unsigned long long*)(sd + 7), g->compact};
+    g->wide = results_wide(g);
+    OutLayout ol{g->out_host.p, g->out_host.cap, sd + 6, g->scan.p + kScanBlocks, 0, (unsigned long long*)(sd + 7),
+                 g->compact, g->wide ? 1 : 0};
     hipLaunchKernelGGL(k_gather_host, dim3((unsigned)((k_ub + 255) / 256)), dim3(256), 0, ss, g->ordered.p, k_ub,
                        (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, ol);
     hipLaunchKernelGGL(k_spec_total, dim3(1), dim3(64), 0, ss, sd, g->empty_count ? 1ull : 0ull,
@@ -1493,7 +1524,11 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_hll, (33ull << kHllLog) * 4, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = g->hll.ensure(33ull << kHllLog);
     if (!rc) rc = ss_check(hipMemsetAsync(g->hll.p, 0, (33ull << kHllLog) * 4, g->stream), "ingest sketch reset");
-    if (!rc) rc = ss_check(hipStreamCreateWithFlags(&g->spec_stream, hipStreamNonBlocking), "ingest spec stream");
+    if (!rc) {       // the speculative finish runs beside the verify: it gets the CU slots first
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        rc = ss_check(hipStreamCreateWithPriority(&g->spec_stream, hipStreamNonBlocking, hi), "ingest spec stream");
+    }
     if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_reps, hipEventDisableTiming), "ingest event");
     if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_spec, hipEventDisableTiming), "ingest event");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_spec, 4 * 8, hipHostMallocDefault), "ingest pinned");
@@ -1825,7 +1860,6 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
         if (!g->h_spec[2]) {        // (stays valid: a second finish returns the same rows)
             g->nkeys = g->h_spec[0];
             g->nwords = g->h_spec[1];
-            g->wide = g->compact == 2 || (g->compact && ((g->h_spec[3] >> 32) || (g->empty_count >> 32)));
             *h_nkeys = g->nkeys;
             *h_nwords = g->nwords;
             return SS_OK;
@@ -1864,15 +1898,7 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
         (rc = g->woff.ensure(std::max(K, NB) + 1)) || (rc = g->out_host.ensure(wo0 + NW * 8 + 16)) ||
         (rc = g->spec_dev.ensure(13)))
         return rc;
-    // compact results: the largest count decides the count width (on the device: no sync)
-    unsigned long long* dmax = (unsigned long long*)(g->spec_dev.p + 12);
-    if (g->compact) {
-        if ((rc = ss_check(hipMemsetAsync(dmax, 0, 8, s), "ingest count max"))) return rc;
-        for (Group* gr : placed)
-            if (gr->m)
-                hipLaunchKernelGGL(k_count_max, dim3(grid_of(gr->m, 256)), dim3(256), 0, s, gr->counts.p, gr->m, dmax,
-                                   (const uint64_t*)nullptr);
-    }
+
     if (!desc.empty())
         rc = ss_check(hipMemcpyAsync(g->gdesc.p, desc.data(), desc.size() * sizeof(GDesc), hipMemcpyHostToDevice, s),
                       "ingest desc");
@@ -1897,17 +1923,15 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p);
     if (K >= (1ull << 31) * 256) return ss_fail(SS_EARG, "ingest: too many distinct keys for one gather");
-    OutLayout ol{g->out_host.p, g->out_host.cap, nullptr, nullptr, NW, dmax, nullptr, g->compact};
+    g->wide = results_wide(g);
+    OutLayout ol{g->out_host.p, g->out_host.cap, nullptr, nullptr, NW, nullptr, g->compact, g->wide ? 1 : 0};
     hipLaunchKernelGGL(k_gather_host, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, g->ordered.p, K,
                        (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, ol);
     rc = ss_check(hipGetLastError(), "k_gather_host");
-    if (!rc && g->compact)
-        rc = ss_check(hipMemcpyAsync(g->h_spec + 3, dmax, 8, hipMemcpyDeviceToHost, s), "ingest count max");
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest out");
     if (rc) return rc;
     g->nkeys = K;
     g->nwords = NW;
-    g->wide = g->compact == 2 || (g->compact && ((g->h_spec[3] >> 32) || (g->empty_count >> 32)));
     *h_nkeys = K;
     *h_nwords = NW;
     return SS_OK;

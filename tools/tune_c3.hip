@@ -199,6 +199,46 @@ __global__ __launch_bounds__(T) void k_encode_ham_pipe(G16Args a, uint32_t rpb, 
         __syncthreads();
     }
 }
+
+// Production kernel with XCD-contiguous block order (block b -> XCD b % 8 gets one contiguous eighth
+// of the stream) and/or plain (temporal) loads
+template <int T, int U, bool XCDO, bool NTLD>
+__global__ __launch_bounds__(T) void k_encode_ham_x(G16Args a, uint32_t rpb, float inv_cpr) {
+    __shared__ uint64_t part8[T * U / 2];
+    uint8_t* part = (uint8_t*)part8;
+    const uint64_t bo = XCDO ? (uint64_t)(blockIdx.x % 8u) * ((gridDim.x + 7u) / 8u) + blockIdx.x / 8u : blockIdx.x;
+    const uint64_t r0 = bo * rpb;
+    if (r0 >= a.n) return;
+    const uint32_t nr = (uint32_t)min((uint64_t)rpb, a.n - r0);
+    const uint32_t nloc = nr * a.cpr;
+    const uint64_t c0 = r0 * a.cpr;
+    uint4 x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t cl = j * T + threadIdx.x;
+        x[j] = cl < nloc ? (NTLD ? ld_stream(&a.in[c0 + cl]) : a.in[c0 + cl])
+                         : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint32_t cl = j * T + threadIdx.x;
+        const uint32_t rl = (uint32_t)__fmul_rn(__fadd_rn((float)cl, 0.5f), inv_cpr);
+        const uint32_t k = cl - rl * a.cpr;
+        uint32_t bad;
+        const uint32_t v = encode_chunk<kPathPext>(x[j], k, a, bad);
+        const bool live = cl < nloc;
+        report_bad(live && bad != 0u, r0 + rl, a.first_bad);
+        if (live && a.out32) st_stream(&a.out32[c0 + cl], v);
+        const uint8_t d = (uint8_t)((live && k < a.ham2) ? ham32(v ^ a.ref32[k]) : 0u);
+        if (live) part[8 * rl + k] = d;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nr; i += T) {
+        const uint64_t p = part8[i] & (~0ull >> (64 - 8 * a.cpr));
+        const uint32_t sum = __builtin_amdgcn_sad_u8((uint32_t)p, 0u, 0u) + __builtin_amdgcn_sad_u8((uint32_t)(p >> 32), 0u, 0u);
+        st_stream(&a.counts[r0 + i], sum);
+    }
+}
 }  // namespace
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -264,6 +304,16 @@ static void vpipe(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t
                        1.0f / 6.0f, ntiles);
 }
 
+template <int T, int U, bool XCDO, bool NTLD>
+static void vx(const uint8_t* in, uint64_t n, uint64_t* words, const uint64_t* ref, uint32_t* out, uint64_t* fb) {
+    reset_first_bad(fb, 0);
+    const uint32_t rpb = (U * T) / 6;
+    unsigned grid = (unsigned)((n + rpb - 1) / rpb);
+    if (XCDO) grid = (grid + 7u) / 8u * 8u;
+    hipLaunchKernelGGL((k_encode_ham_x<T, U, XCDO, NTLD>), dim3(grid), dim3(T), 0, 0, args(in, n, words, ref, out, fb), rpb,
+                       1.0f / 6.0f);
+}
+
 typedef void (*Fn)(const uint8_t*, uint64_t, uint64_t*, const uint64_t*, uint32_t*, uint64_t*);
 
 int main(int argc, char** argv) {
@@ -286,9 +336,9 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(ref, w0 + 3 * 12345, 24, hipMemcpyDeviceToDevice));
     const struct { const char* name; Fn f; } vs[] = {
         {"prod k_encode_ham_dense<192,4>", prod},
-        {"pipe T192 U4 x8", vpipe<192, 4, 8>}, {"pipe T192 U4 x12", vpipe<192, 4, 12>},
-        {"pipe T256 U3 x8", vpipe<256, 3, 8>}, {"pipe T384 U2 x6", vpipe<384, 2, 6>},
-        {"pipe T192 U4 x16", vpipe<192, 4, 16>}, {"pipe T512 U3 x4", vpipe<512, 3, 4>},
+        {"x T192 U4 xcd", vx<192, 4, true, true>}, {"x T192 U4 temporal-ld", vx<192, 4, false, false>},
+        {"x T192 U4 xcd temporal-ld", vx<192, 4, true, false>}, {"x T192 U4 (same as prod)", vx<192, 4, false, true>},
+        {"x T256 U3 xcd", vx<256, 3, true, true>},
         {"prod T128 U3", vp<128, 3>}, {"prod T96 U4", vp<96, 4>}, {"prod T192 U2", vp<192, 2>},
         {"prod T64 U6", vp<64, 6>}, {"prod T128 U6", vp<128, 6>}, {"prod T256 U3", vp<256, 3>},
         {"prod T64 U3", vp<64, 3>},
