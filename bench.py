@@ -461,34 +461,41 @@ def bench_fastq_index(B, lib, dev, n_rec=8 << 20, L=100, reps=10):
                     "ss_fastq_index; device-resident synthetic FASTQ, every offset / length checked"}
 
 
-def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10):
-    """all unordered pairs of n UMIs (L nt) within hamming k."""
+def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10, method="tiles"):
+    """all unordered pairs of n UMIs (L nt) within hamming k.  method "tiles" checks
+    every pair on the MFMA tiles (priced against the i8 peak); "pigeonhole" / "auto" check only the
+    pairs sharing one of k + 1 segments (bucketed on the device) -- same counts and total, reported
+    as covered pairs per second (n (n - 1) / 2 per step), with no MFMA roofline."""
     from shortseq_amd._native import check
+    code = B.ALL_PAIRS_METHODS[method]
     w = B.encode(B.synth_reads(n, L, seed=7, device=dev), L)
     cnt = torch.empty(n, dtype=torch.int32, device=dev)
     tot = torch.empty(1, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
 
     def step(_t):
-        check(lib.ss_hamming_all_pairs(w.data_ptr(), n, L, w.shape[1], k, cnt.data_ptr(), None, 0,
-                                       tot.data_ptr(), s), "all_pairs")
+        check(lib.ss_hamming_all_pairs_ex(w.data_ptr(), n, L, w.shape[1], k, cnt.data_ptr(), None, 0,
+                                          tot.data_ptr(), code, s), "all_pairs")
     el, tr = timed_loop(step, reps, 2, 1)
     if int(cnt.sum().item()) != 2 * int(tot.item()):
         raise SystemExit("PARITY FAILURE: all-pairs counts")
     ms = tr.region_ms / reps
     pairs = n * (n - 1) // 2
+    out = {"n": n, "read_len": L, "max_dist": k, "method": method, "pairs": pairs, "ms_per_step": ms,
+           "pairs_per_s": pairs / ms * 1e3, "hits": int(tot.item())}
+    if method != "tiles":
+        return out
     # issued i8 MACs: one-hot codes, 8 positions (32 MACs) per k-step, ceil(min(L + 1, 32) / 8) steps
     ks = (min(L + 1, 32) + 7) // 8
     tops = pairs * 2 * 32 * ks / (ms * 1e-3) / 1e12
     # algorithmic work: L position compares per pair (one MAC each, x2 ops) against the same peak
     algo_tops = pairs * 2 * L / (ms * 1e-3) / 1e12
-    return {"n": n, "read_len": L, "max_dist": k, "pairs": pairs, "ms_per_step": ms,
-            "pairs_per_s": pairs / ms * 1e3, "hits": int(tot.item()),
-            "roofline": {"bound": "mfma", "kernel": "k_allpairs_mfma (v_mfma_i32_32x32x32_i8)", "achieved": tops,
-                         "peak": I8_PEAK_TOPS, "unit": "TOP/s", "frac": tops / I8_PEAK_TOPS,
-                         "frac_algorithmic": algo_tops / I8_PEAK_TOPS,
-                         "note": "frac: issued i8 MAC ops x2 (one-hot codes, 4 MACs per position, K padded to "
-                                 "whole k-steps); frac_algorithmic: L compares per pair x2; dense i8 peak = 2x bf16"}}
+    out["roofline"] = {"bound": "mfma", "kernel": "k_allpairs_mfma (v_mfma_i32_32x32x32_i8)", "achieved": tops,
+                       "peak": I8_PEAK_TOPS, "unit": "TOP/s", "frac": tops / I8_PEAK_TOPS,
+                       "frac_algorithmic": algo_tops / I8_PEAK_TOPS,
+                       "note": "frac: issued i8 MAC ops x2 (one-hot codes, 4 MACs per position, K padded to "
+                               "whole k-steps); frac_algorithmic: L compares per pair x2; dense i8 peak = 2x bf16"}
+    return out
 
 
 def bench_ragged(B, lib, dev, reps=5, name="ragged_50M_L50-150_U20", encode=True):
@@ -924,6 +931,8 @@ def main():
             log("F1 FASTQ index / F4 all-pairs")
             local_extra("F1_fastq_index_100nt", lambda: bench_fastq_index(B, lib, dev))
             local_extra("F4_all_pairs_umi12", lambda: bench_all_pairs(B, lib, dev))
+            # the default entry point (auto: pigeonhole buckets for this batch), same results
+            local_extra("F4_all_pairs_umi12_auto", lambda: bench_all_pairs(B, lib, dev, method="auto"))
             log("F2 ragged 50-150 nt")
             local_extra("F2_ragged_50_150", lambda: bench_ragged(B, lib, dev))
             # the same reads over a 2^24-item pool: ~16M distinct keys, tables past the Infinity Cache

@@ -140,10 +140,25 @@ int ss_slice_var(const uint64_t* d_words, uint64_t n, uint32_t wpr, const uint32
  * <= max_dist, d_counts[i] and d_counts[j] += 1 (neighbours per read; if d_counts != NULL) and the
  * pair (i, j) is appended as two u32 to d_pairs (if != NULL) while fewer than max_pairs were written.
  * *d_npairs = all such pairs (may exceed max_pairs).  The entry point zeroes d_counts / *d_npairs.
- * Pair order is unspecified.  n <= 65535 * 1024 per call (L <= 32). */
+ * Pair order is unspecified (each pair is written as i < j).  n <= 65535 * 1024 per call (L <= 32).
+ * Same as ss_hamming_all_pairs_ex(..., SS_ALLPAIRS_AUTO, stream). */
 int ss_hamming_all_pairs(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr, uint32_t max_dist,
                          uint32_t* d_counts, uint32_t* d_pairs, uint64_t max_pairs, uint64_t* d_npairs,
                          void* stream);
+
+/* Method of ss_hamming_all_pairs_ex; every method gives the same counts, total and pair set.
+ * TILES: every pair checked (MFMA one-hot tiles for L <= 128, bit-plane tiles above).
+ * PIGEONHOLE (L <= 32, max_dist < 16): the min(L + 1, 32) positions split into max_dist + 1
+ *   segments; only pairs with an equal segment are checked (bucketed per segment on the device).
+ *   Blocks the calling thread once on the stream (the candidate totals are read back).
+ * AUTO: PIGEONHOLE when L <= 32, segments >= 3 nt, n >= 32768 and the bucket histogram shows fewer
+ *   than 1/64 of all pairs as candidates; TILES otherwise. */
+#define SS_ALLPAIRS_AUTO 0u
+#define SS_ALLPAIRS_TILES 1u
+#define SS_ALLPAIRS_PIGEONHOLE 2u
+int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr, uint32_t max_dist,
+                            uint32_t* d_counts, uint32_t* d_pairs, uint64_t max_pairs, uint64_t* d_npairs,
+                            uint32_t method, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Dedup counter — replaces ShortSeqCounter._count_sequence (counter.pyx:41-54): key = (length,

@@ -59,6 +59,7 @@ abprof)
 libab)
   rounds=$1; cmd=$2; shift 2
   vs=${*:-old new}
+  export SHORTSEQ_AMD_LENIENT_ABI=1
   L=shortseq_amd/lib
   cp $L/libshortseq_amd.so $L/libshortseq_amd_new.so
   # the real library goes back however the loop ends (a killed run left a variant installed)

@@ -584,19 +584,25 @@ def slice_var(words: torch.Tensor, starts: torch.Tensor, lens: torch.Tensor, *,
     return out
 
 
+ALL_PAIRS_METHODS = {"auto": 0, "tiles": 1, "pigeonhole": 2}
+
+
 def hamming_all_pairs(words: torch.Tensor, L: int, max_dist: int, *, counts: bool = True,
-                      max_pairs: int = 0):
+                      max_pairs: int = 0, method: str = "auto"):
     """Unordered pairs (i < j) of a packed batch within `max_dist` (the reference __xor__ distance)
     -> (neighbour counts int32 [n] or None, pairs int32 [m, 2] or None, total pairs).  Pairs are
-    returned sorted; at most max_pairs are kept (0: count only)."""
+    returned sorted; at most max_pairs are kept (0: count only).  method: "tiles" checks every pair,
+    "pigeonhole" (L <= 32) only pairs sharing one of max_dist + 1 segments, "auto" picks
+    (ss_hamming_all_pairs_ex); the results are the same."""
     _require_cuda(words, "words")
     n, wpr = words.shape
     dev = words.device
     cnt = torch.empty(n, dtype=torch.int32, device=dev) if counts else None
     pairs = torch.empty((max(1, max_pairs), 2), dtype=torch.int32, device=dev) if max_pairs else None
     tot = torch.empty(1, dtype=torch.int64, device=dev)
-    check(lib().ss_hamming_all_pairs(words.data_ptr(), n, L, wpr, max_dist, _ptr(cnt), _ptr(pairs), max_pairs,
-                                     tot.data_ptr(), _stream(dev)), "ss_hamming_all_pairs")
+    check(lib().ss_hamming_all_pairs_ex(words.data_ptr(), n, L, wpr, max_dist, _ptr(cnt), _ptr(pairs), max_pairs,
+                                        tot.data_ptr(), ALL_PAIRS_METHODS[method], _stream(dev)),
+          "ss_hamming_all_pairs_ex")
     total = int(tot.item())
     if pairs is not None:
         m = min(total, max_pairs)

@@ -689,13 +689,13 @@ cdef _fill_from_engine(ShortSeqCounter self, ss_ingest* g):
     _fill_rows(self, _engine_keys(g), lens, counts, words)
 
 
-_REDUCE_MODE = "tree"
+_REDUCE_MODE = "auto"
 
 
 def _set_reduce_mode(str mode):
     """Test / probe hook: "tree" (default) or "chain" (every shard merged into engine 0 in turn)."""
     global _REDUCE_MODE
-    if mode not in ("tree", "chain"):
+    if mode not in ("auto", "tree", "chain"):
         raise ValueError(mode)
     _REDUCE_MODE = mode
 
@@ -718,11 +718,14 @@ def _merge_pair(size_t ga, size_t gb, uint64_t rel_base, bint reexport):
 
 cdef _reduce_fill(ShortSeqCounter self, list engines, list bases):
     """The dict of a call counted on len(engines) shards (engine k: the reads from bases[k] on).  The
-    first rejected read in input order raises (shard order = input order).  Several shards reduce on
-    the devices as a tree (VERDICT r4 item 5): round r merges engine k + 2^r into engine k for every
-    k divisible by 2^(r+1), the round's merges concurrently, each on its destination's device and
-    stream (ss_ingest_merge: peer copies over xGMI) -- so no engine takes more than log2(D) sources
-    and the first round's D/2 copies use D/2 links at once.  Every pair is adjacent in input order
+    first rejected read in input order raises (shard order = input order).  Shards on distinct
+    devices reduce on the devices as a tree (VERDICT r4 item 5): round r merges engine k + 2^r into
+    engine k for every k divisible by 2^(r+1), the round's merges concurrently, each on its
+    destination's device and stream (ss_ingest_merge: peer copies over xGMI) -- so no engine takes
+    more than log2(D) sources and the first round's D/2 copies use D/2 links at once.  Shards that all
+    share one device reduce as a chain into engine 0: there the tree's concurrent merges share one
+    GPU and its re-exports are extra work (tools/probe_reduce.py, profiles/r5: 8 x 2^24 keys, chain
+    30 ms vs tree 49 ms).  Every pair is adjacent in input order
     (b's reads follow a's), which keeps the smallest row of a key its first occurrence.  Engine 0 then
     orders the union by first read (ss_ingest_finish), and the dict is built once from those rows --
     each distinct key crosses PCIe once and gets one dict insert."""
@@ -733,7 +736,10 @@ cdef _reduce_fill(ShortSeqCounter self, list engines, list bases):
     for k in range(D):
         _raise_ingest_error(<ss_ingest*><size_t>engines[k][1])
     if D > 1:
-        if _REDUCE_MODE == "chain":
+        mode = _REDUCE_MODE
+        if mode == "auto":
+            mode = "chain" if len(set(e[0] for e in engines)) == 1 else "tree"
+        if mode == "chain":
             for k in range(1, D):
                 _merge_pair(<size_t>engines[0][1], <size_t>engines[k][1], bases[k], False)
         else:

@@ -15,6 +15,8 @@
 // diagonal tile masks j <= i).  Hits are rare for UMI thresholds, so they leave the inner loop
 // through a wave ballot: row counts stay in registers, column counts go to LDS counters, pairs
 // are appended with one global atomic per wave.
+#include <mutex>
+
 #include "ss_device.h"
 #include "ss_internal.h"
 
@@ -71,6 +73,8 @@ __global__ __launch_bounds__(256) void k_allpairs(AllPairsArgs a) {
     if (bj < bi) return;                                    // unordered pairs: upper triangle only
     __shared__ uint2 pl[C * WT];                             // {lo, hi} planes per column word
     __shared__ uint32_t colcnt[C];
+    __shared__ unsigned long long blkhits;   // count-only calls: the block's hits, one global atomic
+    if (threadIdx.x == 0) blkhits = 0;
     const bool diag = bi == bj;
     // rows of this lane: i = bi*S + r*256 + tid
     uint32_t alo[R][WT], ahi[R][WT];
@@ -129,8 +133,10 @@ __global__ __launch_bounds__(256) void k_allpairs(AllPairsArgs a) {
                             a.pairs[2 * slot] = (uint32_t)i;
                             a.pairs[2 * slot + 1] = (uint32_t)j;
                         }
-                    } else if (hit) {
-                        atomicAdd(a.npairs, 1ull);
+                    } else {
+                        const uint64_t mask = __ballot(hit);   // all lanes, before the leader's branch
+                        if ((threadIdx.x & 63u) == (uint32_t)__ffsll((unsigned long long)mask) - 1u)
+                            atomicAdd(&blkhits, (unsigned long long)__popcll(mask));
                     }
                 }
             }
@@ -141,6 +147,8 @@ __global__ __launch_bounds__(256) void k_allpairs(AllPairsArgs a) {
                 if (colcnt[c]) atomicAdd(&a.counts[j0 + c], colcnt[c]);
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0 && blkhits) atomicAdd(a.npairs, blkhits);
     if (a.counts) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -187,7 +195,8 @@ __device__ __forceinline__ void onehot_frag(uint64_t word, bool valid, uint32_t 
 // Hit path of one 32 x 32 result tile (st = its 16 result registers per lane, [reg][lane], hit =
 // bit 7): index checks, LDS row / column counts, wave-aggregated pair append.
 __device__ __noinline__ void ap_hits(const AllPairsArgs& a, const int* st, uint32_t rl0, uint32_t cl, uint64_t row0,
-                                     uint64_t col0, bool diag, uint32_t* rowcnt, uint32_t* colcnt) {
+                                     uint64_t col0, bool diag, uint32_t* rowcnt, uint32_t* colcnt,
+                                     unsigned long long* blkhits) {
     const uint32_t lane = threadIdx.x & 63u, h = lane >> 5;
 #pragma unroll 1
     for (int q = 0; q < 16; ++q) {
@@ -202,10 +211,14 @@ __device__ __noinline__ void ap_hits(const AllPairsArgs& a, const int* st, uint3
             atomicAdd(&colcnt[cl], 1u);
         }
         const int leader = __ffsll((unsigned long long)mask) - 1;
+        if (!a.pairs) {         // count only: the block's LDS total, one global atomic per block
+            if ((int)lane == leader) atomicAdd(blkhits, (unsigned long long)__popcll(mask));
+            continue;
+        }
         unsigned long long base = 0;
         if ((int)lane == leader) base = atomicAdd(a.npairs, (unsigned long long)__popcll(mask));
         base = __shfl(base, leader);
-        if (hit && a.pairs) {
+        if (hit) {
             const uint64_t slot = base + __popcll(mask & ((1ull << lane) - 1ull));
             if (slot < a.max_pairs) {
                 a.pairs[2 * slot] = (uint32_t)i;
@@ -246,7 +259,9 @@ __global__ __launch_bounds__(256) void k_allpairs_mfma(AllPairsArgs a, uint32_t 
     __shared__ uint32_t rowcnt[S], colcnt[S];
     __shared__ int stash[4 * 1024];                        // hit path: [wave][result reg][lane]
     __shared__ v4i32 ohtab[TAB ? 256 : 1];
+    __shared__ unsigned long long blkhits;
     const bool diag = bi == bj;
+    if (threadIdx.x == 0) blkhits = 0;
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, h = lane >> 5, r = lane & 31u;
     const uint64_t row0 = (uint64_t)bi * S, col0 = (uint64_t)bj * S;
     if (TAB) {
@@ -330,10 +345,11 @@ __global__ __launch_bounds__(256) void k_allpairs_mfma(AllPairsArgs a, uint32_t 
             int* st = stash + wave * 1024;
 #pragma unroll
             for (int q = 0; q < 16; ++q) st[q * 64 + lane] = D[q];
-            ap_hits(a, st, (wave * RB + rb) * 32, cl, row0, col0, diag, rowcnt, colcnt);
+            ap_hits(a, st, (wave * RB + rb) * 32, cl, row0, col0, diag, rowcnt, colcnt, &blkhits);
         }
     }
     __syncthreads();
+    if (threadIdx.x == 0 && blkhits) atomicAdd(a.npairs, blkhits);
     if (a.counts) {
         for (int c = threadIdx.x; c < S; c += 256) {
             if (rowcnt[c]) atomicAdd(&a.counts[row0 + c], rowcnt[c]);
@@ -368,6 +384,390 @@ int launch_allpairs(AllPairsArgs a, hipStream_t s) {
     return ss_check(hipGetLastError(), "k_allpairs");
 }
 
+// ------------------------------------------------------------------------------------------------
+// Pigeonhole form (one-word reads, small max_dist k): split the P compared positions into G = k + 1
+// contiguous segments.  Two reads within distance k differ in at most k positions, so at least one
+// segment is equal in both.  Per segment g the reads are bucketed by that segment's value (counting
+// sort: histogram -> tile sums -> scan -> scatter of {word, index}); only pairs sharing a bucket are
+// candidates, and a candidate (i, j) is reported by segment g only when segment g is equal and
+// every segment g' < g differs (the pair's first equal segment), so each pair is reported once.
+// Work is sum over buckets of c (c - 1) / 2 per segment instead of n (n - 1) / 2: for n random UMIs
+// of 12 nt and k = 1, 2 segments of 6-7 nt, ~n^2 / 2 / 4096 candidates.  Skewed batches (one UMI
+// repeated many times, low-complexity segments) make buckets large; the host reads the candidate
+// totals after the histogram and hands such batches to the tiled MFMA form (ss_hamming_all_pairs).
+// Buckets: the segment value itself when it has <= nbmax bits, else a 64-bit multiplicative hash of
+// it (colliding values only add candidates: the equality test is on the segment value).
+// ------------------------------------------------------------------------------------------------
+constexpr int kPigMaxG = 16;
+constexpr uint32_t kPigTile = 4096;      // buckets per scan tile: 256 threads x 16
+constexpr uint32_t kPigMaxBits = 22;     // <= 1024 tiles per segment (one k_pig_top block)
+constexpr uint64_t kPigRatio = 16;       // auto: pigeonhole when candidates < all pairs / kPigRatio
+
+struct PigArgs {
+    const uint64_t* words;
+    uint64_t n;
+    uint32_t wpr, k, G, nbmax, maxtiles, exact;   // exact: bit g = segment g buckets by value
+    uint32_t shift[kPigMaxG], nb[kPigMaxG];
+    uint64_t mask[kPigMaxG];
+    uint32_t* hist;       // G << nbmax: counts, then bucket starts (k_pig_apply)
+    uint32_t* tile_cnt;   // G * maxtiles: bucket sums, then tile bases
+    uint64_t* tile_cand;  // G * maxtiles
+    uint64_t* cand;       // G: candidate pairs per segment
+    uint64_t* sw;         // G * n words in bucket order
+    uint32_t* sid;        // G * n read indices in bucket order
+    uint32_t* rank;       // G * n: read i's rank in its bucket of segment g (k_pig_hist's atomics)
+    uint32_t* counts;
+    uint32_t* pairs;
+    uint64_t max_pairs;
+    unsigned long long* npairs;
+};
+
+__device__ __forceinline__ uint64_t shfl64x(uint64_t v, int o) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ uint64_t pig_key(const PigArgs& a, uint32_t g, uint64_t w) {
+    return (w >> a.shift[g]) & a.mask[g];
+}
+__device__ __forceinline__ uint32_t pig_bucket(const PigArgs& a, uint32_t g, uint64_t w) {
+    const uint64_t key = pig_key(a, g, w);
+    return (a.exact >> g) & 1u ? (uint32_t)key : (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - a.nb[g]));
+}
+
+__global__ __launch_bounds__(256) void k_pig_hist(PigArgs a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t w = a.words[i * a.wpr];
+        for (uint32_t g = 0; g < a.G; ++g)
+            a.rank[g * a.n + i] = atomicAdd(&a.hist[((uint64_t)g << a.nbmax) + pig_bucket(a, g, w)], 1u);
+    }
+}
+
+// block sums of a 256-thread block: returns the total to every thread
+template <typename T>
+__device__ __forceinline__ T block_sum256(T v, T* red) {
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63u) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const T t = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return t;
+}
+
+// per tile of 4096 buckets: number of reads and candidate pairs
+__global__ __launch_bounds__(256) void k_pig_tile(PigArgs a) {
+    const uint32_t g = blockIdx.y, t0 = blockIdx.x * kPigTile, nbk = 1u << a.nb[g];
+    if (t0 >= nbk) return;
+    const uint32_t* h = a.hist + ((uint64_t)g << a.nbmax) + t0;
+    uint32_t c = 0;
+    uint64_t cand = 0;
+    for (uint32_t j = threadIdx.x; j < kPigTile && t0 + j < nbk; j += 256) {
+        const uint64_t v = h[j];
+        c += (uint32_t)v;
+        cand += v * (v - (v ? 1 : 0)) / 2;
+    }
+    __shared__ uint32_t r32[4];
+    __shared__ uint64_t r64[4];
+    c = block_sum256(c, r32);
+    cand = block_sum256(cand, r64);
+    if (threadIdx.x == 0) {
+        a.tile_cnt[g * a.maxtiles + blockIdx.x] = c;
+        a.tile_cand[g * a.maxtiles + blockIdx.x] = cand;
+    }
+}
+
+// per segment: exclusive scan of the tile sums (<= 1024 tiles), candidate total
+__global__ __launch_bounds__(1024) void k_pig_top(PigArgs a) {
+    const uint32_t g = blockIdx.x, nt = ((1u << a.nb[g]) + kPigTile - 1) / kPigTile, t = threadIdx.x;
+    const uint32_t lane = t & 63u, wv = t >> 6;
+    uint32_t v = t < nt ? a.tile_cnt[g * a.maxtiles + t] : 0u;
+    uint64_t cand = t < nt ? a.tile_cand[g * a.maxtiles + t] : 0ull;
+    uint32_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    for (int o = 32; o; o >>= 1) cand += __shfl_xor(cand, o);
+    __shared__ uint32_t ws[16];
+    __shared__ uint64_t cs[16];
+    if (lane == 63) ws[wv] = inc;
+    if (lane == 0) cs[wv] = cand;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t i = 0; i < wv; ++i) before += ws[i];
+    if (t < nt) a.tile_cnt[g * a.maxtiles + t] = before + inc - v;
+    if (t == 0) {
+        uint64_t tot = 0;
+        for (int i = 0; i < 16; ++i) tot += cs[i];
+        a.cand[g] = tot;
+    }
+}
+
+// bucket starts: each thread owns 16 consecutive buckets of the tile
+__global__ __launch_bounds__(256) void k_pig_apply(PigArgs a) {
+    const uint32_t g = blockIdx.y, t0 = blockIdx.x * kPigTile, nbk = 1u << a.nb[g];
+    if (t0 >= nbk) return;
+    uint32_t* h = a.hist + ((uint64_t)g << a.nbmax) + t0;
+    const uint32_t b0 = threadIdx.x * 16u;
+    const uint32_t m = b0 < nbk - t0 ? min(16u, nbk - t0 - b0) : 0u;
+    uint32_t v[16];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        v[j] = j < m ? h[b0 + j] : 0u;
+        s += v[j];
+    }
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    __shared__ uint32_t ws[4];
+    if (lane == 63) ws[wv] = inc;
+    __syncthreads();
+    uint32_t run = a.tile_cnt[g * a.maxtiles + blockIdx.x] + inc - s;
+    for (uint32_t i = 0; i < wv; ++i) run += ws[i];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        if (j < m) h[b0 + j] = run;
+        run += v[j];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pig_scatter(PigArgs a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t w = a.words[i * a.wpr];
+        for (uint32_t g = 0; g < a.G; ++g) {
+            const uint32_t pos = a.hist[((uint64_t)g << a.nbmax) + pig_bucket(a, g, w)] + a.rank[g * a.n + i];
+            a.sw[g * a.n + pos] = w;
+            a.sid[g * a.n + pos] = (uint32_t)i;
+        }
+    }
+}
+
+// Hit output of a wave without one global atomic per hit ballot: pairs gather in a per-wave LDS
+// buffer and leave in runs (one pair-counter atomic per run of up to kPairBuf); count-only calls keep
+// the wave's hit count in a register and add it once.
+constexpr uint32_t kPairBuf = 512;
+struct WaveHits {
+    uint2* buf;          // this wave's kPairBuf LDS entries
+    uint32_t fill = 0;   // wave-uniform
+    uint64_t nh = 0;     // wave-uniform (count-only)
+};
+__device__ __forceinline__ void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void hits_flush(const PigArgs& a, WaveHits& wh) {
+    if (!wh.fill) return;
+    lds_wave_sync();
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(a.npairs, (unsigned long long)wh.fill);
+    base = __shfl(base, 0);
+    for (uint32_t e = lane; e < wh.fill; e += 64) {
+        const uint64_t slot = base + e;
+        if (slot < a.max_pairs) {
+            const uint2 pr = wh.buf[e];
+            a.pairs[2 * slot] = pr.x;
+            a.pairs[2 * slot + 1] = pr.y;
+        }
+    }
+    lds_wave_sync();
+    wh.fill = 0;
+}
+__device__ __forceinline__ void hits_add(const PigArgs& a, WaveHits& wh, bool hit, uint64_t mask, uint32_t i, uint32_t j) {
+    const uint32_t c = (uint32_t)__popcll(mask);
+    if (!a.pairs) {
+        wh.nh += c;
+        return;
+    }
+    if (wh.fill + c > kPairBuf) hits_flush(a, wh);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (hit) wh.buf[wh.fill + __popcll(mask & ((1ull << lane) - 1ull))] = make_uint2(min(i, j), max(i, j));
+    wh.fill += c;
+}
+__device__ __forceinline__ void hits_done(const PigArgs& a, WaveHits& wh) {
+    if (a.pairs) hits_flush(a, wh);
+    else if ((threadIdx.x & 63u) == 0 && wh.nh) atomicAdd(a.npairs, (unsigned long long)wh.nh);
+}
+
+// one lane per read in bucket order of segment g = blockIdx.y, compared with the reads after it in its
+// bucket.  A wave's 64 reads are consecutive, so the reads they need are one run, [p0 + 1, the wave's
+// largest bucket end): it goes through in tiles of 64 -- one coalesced load per tile, then each
+// entry broadcast to the wave from its lane (v_readlane: a scalar operand), so the 64 compares of a
+// tile wait on no memory.  Hits leave through wave ballots into the wave's hit buffer.
+template <int GM>   // G <= GM segments: the first-equal-segment test unrolled over GM - 1 masks
+__global__ __launch_bounds__(256) void k_pig_pairs(PigArgs a) {
+    __shared__ uint2 pbuf[4][kPairBuf];
+    const uint32_t g = blockIdx.y, lane = threadIdx.x & 63u;
+    // the wave's first position, made scalar (threadIdx.x & ~63 is wave-uniform)
+    const uint64_t p0 = (uint64_t)blockIdx.x * 256 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+    const uint64_t p = p0 + lane;
+    if (p0 >= a.n) return;                                   // whole wave past the batch
+    const bool valid = p < a.n;
+    const uint64_t* sw = a.sw + g * a.n;
+    const uint32_t* sid = a.sid + g * a.n;
+    const uint32_t* start = a.hist + ((uint64_t)g << a.nbmax);
+    const uint32_t nbk = 1u << a.nb[g];
+    const uint64_t w = valid ? sw[p] : 0ull;
+    const uint32_t id = valid ? sid[p] : 0u;
+    const uint32_t b = pig_bucket(a, g, w);
+    const uint64_t end = valid ? (b + 1 < nbk ? start[b + 1] : a.n) : 0ull;
+    // segment h's positions as one bit per position (the low bit of its 2-bit code): with
+    // d = the positions where two words differ, the pair is segment g's iff d misses segment g and
+    // meets every segment before it (g is the pair's first equal segment) and popcount(d) <= k
+    constexpr uint64_t kLo = 0x5555555555555555ull;
+    uint64_t segm[GM];
+#pragma unroll
+    for (int h = 0; h < GM; ++h) segm[h] = (uint32_t)h < g ? (a.mask[h] << a.shift[h]) & kLo : 0ull;
+    const uint64_t mg = (a.mask[g] << a.shift[g]) & kLo;
+    const uint32_t kmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.k);
+    uint64_t wend = end;                                     // the wave's largest bucket end
+    for (int o = 32; o; o >>= 1) {
+        const uint64_t y = shfl64x(wend, o);
+        wend = y > wend ? y : wend;
+    }
+    wend = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wend >> 32)) << 32 |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wend);   // uniform: scalar loop bounds
+    WaveHits wh;
+    wh.buf = pbuf[threadIdx.x >> 6];
+    uint32_t row = 0;
+    for (uint64_t t0 = p0 + 1; t0 < wend; t0 += 64) {
+        const uint64_t qt = t0 + lane;
+        const uint64_t tw = qt < a.n ? sw[qt] : 0ull;
+        const uint32_t tid = qt < a.n ? sid[qt] : 0u;
+        const uint32_t twl = (uint32_t)tw, twh = (uint32_t)(tw >> 32);
+        const uint32_t ne = (uint32_t)((wend - t0) < 64 ? (wend - t0) : 64);
+        for (uint32_t e = 0; e < ne; ++e) {
+            const uint64_t q = t0 + e;
+            const uint64_t w2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)twh, (int)e) << 32 |
+                                (uint32_t)__builtin_amdgcn_readlane((int)twl, (int)e);
+            const uint64_t x = w ^ w2, d = (x | (x >> 1)) & kLo;
+            bool hit = (q > p) & (q < end) & ((uint32_t)__popcll(d) <= kmax) & !(d & mg);
+#pragma unroll
+            for (int h = 0; h < GM - 1; ++h) hit = hit && ((uint32_t)h >= g || (d & segm[h]) != 0ull);
+            const uint64_t mask = __ballot(hit);
+            if (!mask) continue;
+            const uint32_t jd = (uint32_t)__builtin_amdgcn_readlane((int)tid, (int)e);
+            row += hit ? 1u : 0u;
+            if (a.counts && lane == (uint32_t)__ffsll((unsigned long long)mask) - 1u)
+                atomicAdd(&a.counts[jd], (uint32_t)__popcll(mask));
+            hits_add(a, wh, hit, mask, id, jd);
+        }
+    }
+    hits_done(a, wh);
+    if (a.counts && row) atomicAdd(&a.counts[id], row);
+}
+
+// Per-device scratch of the pigeonhole form, grow-only and stream-ordered: a call holds the device's
+// lock, waits (on its stream) for the previous call's kernels before reusing the buffer, and records
+// its own end.
+struct PigScratch {
+    std::mutex mu;
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipEvent_t done = nullptr;
+    uint64_t* h_cand = nullptr;   // pinned: the candidate totals read back
+};
+PigScratch g_pig[64];
+
+// returns 0 with *done = false when the auto choice hands the batch to the tiled form
+int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hipStream_t s, bool* done) {
+    *done = false;
+    PigArgs a{};
+    a.words = b.words;
+    a.n = b.n;
+    a.wpr = b.wpr;
+    a.k = b.k;
+    a.G = b.k + 1;
+    a.counts = b.counts;
+    a.pairs = b.pairs;
+    a.max_pairs = b.max_pairs;
+    a.npairs = b.npairs;
+    uint32_t lg = 0;
+    while ((1ull << lg) < a.n) ++lg;
+    a.nbmax = lg < 10 ? 10 : (lg > kPigMaxBits ? kPigMaxBits : lg);
+    a.maxtiles = ((1u << a.nbmax) + kPigTile - 1) / kPigTile;
+    // the L read positions split evenly (the first L % G segments one longer); the alias position L
+    // (P = L + 1: nearly always code 0, so no bucketing entropy) joins the last segment
+    const uint32_t Lr = P < L ? P : L;
+    for (uint32_t g = 0, pos = 0; g < a.G; ++g) {
+        uint32_t len = Lr / a.G + (g < Lr % a.G ? 1u : 0u);
+        if (g + 1 == a.G) len = P - pos;
+        a.shift[g] = 2 * pos;
+        a.mask[g] = len >= 32 ? ~0ull : ((1ull << (2 * len)) - 1ull);
+        a.nb[g] = 2 * len < a.nbmax ? 2 * len : a.nbmax;
+        if (2 * len <= a.nbmax) a.exact |= 1u << g;
+        pos += len;
+    }
+    int dev = 0;
+    int rc = ss_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    if (dev < 0 || dev >= 64) return ss_fail(SS_EARG, "all-pairs: device index past 63");
+    PigScratch& ps = g_pig[dev];
+    std::lock_guard<std::mutex> lock(ps.mu);
+    const size_t hist_n = (size_t)a.G << a.nbmax, tiles_n = (size_t)a.G * a.maxtiles;
+    const size_t need = tiles_n * 8 + a.G * 8 + hist_n * 4 + tiles_n * 4 + 64 + (size_t)a.G * a.n * 16;
+    if (!ps.done) rc = ss_check(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming), "pig event");
+    if (!rc && !ps.h_cand) rc = ss_check(hipHostMalloc((void**)&ps.h_cand, kPigMaxG * 8, hipHostMallocDefault), "pinned totals");
+    if (!rc && ps.bytes < need) {
+        if (ps.p) {
+            rc = ss_check(hipEventSynchronize(ps.done), "pig scratch idle");
+            if (!rc) rc = ss_check(hipFree(ps.p), "pig scratch free");
+            ps.p = nullptr;
+            ps.bytes = 0;
+        }
+        const size_t want = need + need / 4;
+        if (!rc) rc = ss_check(hipMalloc(&ps.p, want), "pig scratch");
+        if (!rc) ps.bytes = want;
+    } else if (!rc) {
+        rc = ss_check(hipStreamWaitEvent(s, ps.done, 0), "pig scratch wait");
+    }
+    if (rc) return rc;
+    char* q = (char*)ps.p;
+    a.tile_cand = (uint64_t*)q;
+    a.cand = a.tile_cand + tiles_n;
+    a.sw = a.cand + a.G;
+    a.hist = (uint32_t*)(a.sw + (size_t)a.G * a.n);
+    a.tile_cnt = a.hist + hist_n;
+    a.sid = a.tile_cnt + tiles_n;
+    a.rank = a.sid + (size_t)a.G * a.n;
+    const unsigned rgrid = (unsigned)std::min<uint64_t>((a.n + 255) / 256, 2048);
+    const dim3 tgrid(a.maxtiles, a.G);
+    rc = ss_check(hipMemsetAsync(a.hist, 0, hist_n * 4, s), "pig hist reset");
+    if (!rc) {
+        hipLaunchKernelGGL(k_pig_hist, dim3(rgrid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_pig_tile, tgrid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_pig_top, dim3(a.G), dim3(1024), 0, s, a);
+        rc = ss_check(hipGetLastError(), "k_pig_hist/tile/top");
+    }
+    bool use = forced;
+    if (!rc && !forced) {
+        rc = ss_check(hipMemcpyAsync(ps.h_cand, a.cand, a.G * 8, hipMemcpyDeviceToHost, s), "pig totals");
+        if (!rc) rc = ss_check(hipStreamSynchronize(s), "pig totals sync");
+        uint64_t cand = 0;
+        for (uint32_t g = 0; !rc && g < a.G; ++g) cand += ps.h_cand[g];
+        // measured (tools/probe_f4.py, profiles/r5/probe_f4_*.log): see kPigRatio
+        use = cand < a.n * (a.n - 1) / 2 / kPigRatio;
+    }
+    if (!rc && use) {
+        hipLaunchKernelGGL(k_pig_apply, tgrid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_pig_scatter, dim3(rgrid), dim3(256), 0, s, a);
+        const uint64_t pb = (a.n + 255) / 256;
+        if (pb > 0x7FFFFFFFull) rc = ss_fail(SS_EARG, "all-pairs: n too large");
+        else if (a.G <= 2) hipLaunchKernelGGL(k_pig_pairs<2>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
+        else if (a.G <= 4) hipLaunchKernelGGL(k_pig_pairs<4>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
+        else if (a.G <= 8) hipLaunchKernelGGL(k_pig_pairs<8>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_pig_pairs<kPigMaxG>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
+        if (!rc) rc = ss_check(hipGetLastError(), "k_pig_apply/scatter/pairs");
+        if (!rc) *done = true;
+    }
+    const int r2 = ss_check(hipEventRecord(ps.done, s), "pig scratch event");
+    return rc ? rc : r2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -375,6 +775,14 @@ extern "C" {
 int ss_hamming_all_pairs(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr, uint32_t max_dist,
                          uint32_t* d_counts, uint32_t* d_pairs, uint64_t max_pairs, uint64_t* d_npairs,
                          void* stream) {
+    return ss_hamming_all_pairs_ex(d_words, n, L, wpr, max_dist, d_counts, d_pairs, max_pairs, d_npairs,
+                                   SS_ALLPAIRS_AUTO, stream);
+}
+
+int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uint32_t wpr, uint32_t max_dist,
+                            uint32_t* d_counts, uint32_t* d_pairs, uint64_t max_pairs, uint64_t* d_npairs,
+                            uint32_t method, void* stream) {
+    if (method > SS_ALLPAIRS_PIGEONHOLE) return ss_fail(SS_EARG, "unknown all-pairs method");
     if (L > SS_MAX_NT) return ss_fail(SS_EARG, "L must be <= 1024");
     const uint32_t W = L <= 32u ? 1u : (L + 31u) / 32u;
     if (wpr < W || wpr > 32) return ss_fail(SS_EARG, "bad wpr");
@@ -396,6 +804,18 @@ int ss_hamming_all_pairs(const uint64_t* d_words, uint64_t n, uint32_t L, uint32
     a.pairs = d_pairs;
     a.max_pairs = d_pairs ? max_pairs : 0;
     a.npairs = (unsigned long long*)d_npairs;
+    if (method == SS_ALLPAIRS_PIGEONHOLE && (W != 1 || max_dist + 1 > (uint32_t)kPigMaxG))
+        return ss_fail(SS_EARG, "pigeonhole all-pairs needs L <= 32 and max_dist < 16");
+    if (W == 1 && method != SS_ALLPAIRS_TILES) {
+        const uint32_t P = L + 1 < 32u ? L + 1 : 32u, G = max_dist + 1;
+        // auto: segments of >= 3 nt and a batch large enough to pay the host read of the totals
+        const bool eligible = G <= (uint32_t)kPigMaxG && P / G >= 3 && n >= (1u << 15);
+        if (method == SS_ALLPAIRS_PIGEONHOLE || eligible) {
+            bool done = false;
+            rc = pig_all_pairs(a, L, P, method == SS_ALLPAIRS_PIGEONHOLE, s, &done);
+            if (rc || done) return rc;
+        }
+    }
     if (W <= 4) {
         // MFMA form: P = min(L + 1, 32 W) positions (the alias bit of the tail block can sit at
         // position L), 8 per k-step; k-steps rounded up to an instantiated count (the padding

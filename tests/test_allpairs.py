@@ -60,3 +60,80 @@ def test_all_pairs_gpu(gpu, oracle, L, n, k):
     if total > 4:
         _, p3, total3 = B.hamming_all_pairs(d, L, k, counts=False, max_pairs=3)
         assert total3 == total and p3.shape[0] == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,n,k", [(12, 3000, 1), (10, 2500, 2), (32, 1500, 3), (31, 1200, 5), (1, 2000, 0),
+                                   (8, 1000, 15), (20, 1500, 0), (16, 800, 4)])
+def test_all_pairs_pigeonhole_gpu(gpu, oracle, L, n, k):
+    """The bucketed pigeonhole form against the oracle's brute force (same pairs, counts, total)."""
+    import torch
+    import shortseq_amd.batch as B
+    ascii = _umis(oracle, n, L, max(2, n // 20), 3 * L + n)
+    words, _, _ = oracle.encode_batch(ascii, n, L)
+    cnt_e, pairs_e = _brute(oracle, words, n, L, k)
+    d = torch.from_numpy(words.view(np.int64)).to(gpu)
+    cnt, pairs, total = B.hamming_all_pairs(d, L, k, max_pairs=len(pairs_e) + 10, method="pigeonhole")
+    assert total == len(pairs_e)
+    assert np.array_equal(cnt.cpu().numpy().astype(np.int64), cnt_e)
+    assert [tuple(int(x) for x in p) for p in pairs.cpu().numpy()] == pairs_e
+    cnt2, _, total2 = B.hamming_all_pairs(d, L, k, method="pigeonhole")
+    assert total2 == total and torch.equal(cnt2, cnt)
+
+
+def _pair_set(pairs):
+    p = pairs.cpu().numpy().astype(np.int64)
+    return p[:, 0] * (1 << 32) + p[:, 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["random12", "umi_pool12", "dups10", "random16k2", "one_read"])
+def test_all_pairs_methods_agree_large(gpu, oracle, case):
+    """At bench-like sizes (n >= 2^15, where auto may pick either form): tiles, pigeonhole and auto
+    give the same counts, totals and pair sets, for uniform UMIs, a UMI pool with 1-nt variants,
+    10-fold duplicates and a batch of one repeated read (every pair a hit)."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(11)
+    L, k, n = 12, 1, 100_000
+    if case == "random12":
+        ascii = oracle.gen_reads(5, 0, n, L)
+    elif case == "umi_pool12":
+        ascii = _umis(oracle, n, L, 20_000, 5)
+    elif case == "dups10":
+        base = oracle.gen_reads(6, 0, n // 10, L).reshape(-1, L)
+        ascii = base[rng.integers(0, n // 10, size=n)].reshape(-1)
+    elif case == "random16k2":
+        L, k = 16, 2
+        ascii = oracle.gen_reads(7, 0, n, L)
+    else:
+        n = 40_000
+        ascii = np.tile(oracle.gen_reads(8, 0, 1, L), n)
+    words, _, _ = oracle.encode_batch(ascii, n, L)
+    d = torch.from_numpy(words.view(np.int64)).to(gpu)
+    cnt_t, _, tot_t = B.hamming_all_pairs(d, L, k, method="tiles")
+    # one repeated read: auto must hand it to the tiles (forced pigeonhole runs on a slice below)
+    for m in (("auto",) if case == "one_read" else ("pigeonhole", "auto")):
+        cnt, _, tot = B.hamming_all_pairs(d, L, k, method=m)
+        assert tot == tot_t and torch.equal(cnt, cnt_t), m
+    if tot_t <= 2_000_000:
+        _, p_t, _ = B.hamming_all_pairs(d, L, k, max_pairs=tot_t, counts=False, method="tiles")
+        _, p_g, _ = B.hamming_all_pairs(d, L, k, max_pairs=tot_t, counts=False, method="pigeonhole")
+        assert np.array_equal(_pair_set(p_t), _pair_set(p_g))
+    assert int(cnt_t.sum().item()) == 2 * tot_t
+    if case == "one_read":
+        m = 3000
+        cnt, _, tot = B.hamming_all_pairs(d[:m], L, k, method="pigeonhole")
+        assert tot == m * (m - 1) // 2 and bool((cnt == m - 1).all())
+
+
+@pytest.mark.gpu
+def test_all_pairs_pigeonhole_refuses_long_reads(gpu):
+    import torch
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import NativeError
+    d = torch.zeros((10, 2), dtype=torch.int64, device=gpu)
+    with pytest.raises(NativeError):
+        B.hamming_all_pairs(d, 40, 1, method="pigeonhole")
+    with pytest.raises(NativeError):
+        B.hamming_all_pairs(d[:, :1].contiguous(), 20, 16, method="pigeonhole")

@@ -298,14 +298,14 @@ def test_reduce_tree_equals_chain(gpu, oracle, ndev):
     reads = oracle.ragged_pool_reads(seed, ps, U, 0, n, lo, hi)
     el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
     try:
-        for mode in ("chain", "tree"):
+        for mode in ("chain", "tree", "auto"):
             S._set_reduce_mode(mode)
             gl, gc, gw = _rows_of(ShortSeqCounter(reads, device=[0] * ndev))
             assert gl.tolist() == el.tolist(), mode
             assert gc.tolist() == ec.tolist(), mode
             assert (gw == ew).all(), mode
     finally:
-        S._set_reduce_mode("tree")
+        S._set_reduce_mode("auto")
 
 
 def test_device_ingest_tree_merge_abi(gpu, oracle):

@@ -12,8 +12,18 @@ import shortseq_amd.batch as B  # noqa: E402
 from shortseq_amd._native import lib  # noqa: E402
 
 dev = torch.device("cuda", 0)
+if len(sys.argv) > 1 and sys.argv[1] == "quick":     # one case per method (rocprof kernel tables)
+    for m in ("tiles", "pigeonhole"):
+        r = bench.bench_all_pairs(B, lib(), dev, method=m, reps=20)
+        print(m, f"{r['ms_per_step']:.4f} ms", flush=True)
+    sys.exit(0)
 for _ in range(2):
     print(bench.bench_all_pairs(B, lib(), dev), flush=True)
-for n, L, k in ((200_000, 12, 1), (50_000, 32, 2), (20_000, 96, 4)):
-    r = bench.bench_all_pairs(B, lib(), dev, n=n, L=L, k=k)
-    print(n, L, k, f"{r['pairs_per_s'] / 1e12:.2f} T pairs/s", r["ms_per_step"], flush=True)
+for n, L, k in ((100_000, 12, 1), (200_000, 12, 1), (1_000_000, 12, 1), (100_000, 16, 2), (50_000, 32, 2),
+                (200_000, 32, 3), (100_000, 8, 1), (20_000, 96, 4)):
+    for m in (("tiles", "pigeonhole", "auto") if L <= 32 else ("tiles",)):
+        if m == "tiles" and n > 200_000:
+            continue
+        r = bench.bench_all_pairs(B, lib(), dev, n=n, L=L, k=k, method=m, reps=5)
+        print(n, L, k, m, f"{r['pairs_per_s'] / 1e12:.2f} T pairs/s", f"{r['ms_per_step']:.4f} ms",
+              "hits", r["hits"], flush=True)
