@@ -624,36 +624,36 @@ __global__ __launch_bounds__(256) void k_pig_pairs(PigArgs a) {
     for (int h = 0; h < GM; ++h) segm[h] = (uint32_t)h < g ? (a.mask[h] << a.shift[h]) & kLo : 0ull;
     const uint64_t mg = (a.mask[g] << a.shift[g]) & kLo;
     const uint32_t kmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.k);
-    uint64_t wend = end;                                     // the wave's largest bucket end
-    for (int o = 32; o; o >>= 1) {
-        const uint64_t y = shfl64x(wend, o);
-        wend = y > wend ? y : wend;
-    }
-    wend = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wend >> 32)) << 32 |
-           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wend);   // uniform: scalar loop bounds
     WaveHits wh;
     wh.buf = pbuf[threadIdx.x >> 6];
     uint32_t row = 0;
-    for (uint64_t t0 = p0 + 1; t0 < wend; t0 += 64) {
-        const uint64_t qt = t0 + lane;
-        const uint64_t tw = qt < a.n ? sw[qt] : 0ull;
-        const uint32_t tid = qt < a.n ? sid[qt] : 0u;
-        const uint32_t twl = (uint32_t)tw, twh = (uint32_t)(tw >> 32);
-        const uint32_t ne = (uint32_t)((wend - t0) < 64 ? (wend - t0) : 64);
-        for (uint32_t e = 0; e < ne; ++e) {
-            const uint64_t q = t0 + e;
-            const uint64_t w2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)twh, (int)e) << 32 |
-                                (uint32_t)__builtin_amdgcn_readlane((int)twl, (int)e);
-            const uint64_t x = w ^ w2, d = (x | (x >> 1)) & kLo;
-            bool hit = (q > p) & (q < end) & ((uint32_t)__popcll(d) <= kmax) & !(d & mg);
+    // each lane walks its own bucket run (p, end): consecutive lanes read consecutive entries, so a
+    // step's 64 loads are one coalesced run; kPigStep entries per step, the next step's in flight
+    constexpr int kPigStep = 4;
+    uint64_t nx[kPigStep];
+#pragma unroll
+    for (int u = 0; u < kPigStep; ++u) nx[u] = p + 1 + u < end ? sw[p + 1 + u] : 0ull;
+    for (uint64_t q0 = p + 1;; q0 += kPigStep) {
+        if (!__ballot(q0 < end)) break;
+        uint64_t cur[kPigStep];
+#pragma unroll
+        for (int u = 0; u < kPigStep; ++u) {
+            cur[u] = nx[u];
+            const uint64_t qn = q0 + kPigStep + u;
+            nx[u] = qn < end ? sw[qn] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kPigStep; ++u) {
+            const uint64_t q = q0 + u;
+            const uint64_t x = w ^ cur[u], d = (x | (x >> 1)) & kLo;
+            bool hit = (q < end) & ((uint32_t)__popcll(d) <= kmax) & !(d & mg);
 #pragma unroll
             for (int h = 0; h < GM - 1; ++h) hit = hit && ((uint32_t)h >= g || (d & segm[h]) != 0ull);
             const uint64_t mask = __ballot(hit);
             if (!mask) continue;
-            const uint32_t jd = (uint32_t)__builtin_amdgcn_readlane((int)tid, (int)e);
+            const uint32_t jd = hit ? sid[q] : 0u;
             row += hit ? 1u : 0u;
-            if (a.counts && lane == (uint32_t)__ffsll((unsigned long long)mask) - 1u)
-                atomicAdd(&a.counts[jd], (uint32_t)__popcll(mask));
+            if (hit && a.counts) atomicAdd(&a.counts[jd], 1u);
             hits_add(a, wh, hit, mask, id, jd);
         }
     }

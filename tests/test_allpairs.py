@@ -79,6 +79,10 @@ def test_all_pairs_pigeonhole_gpu(gpu, oracle, L, n, k):
     assert [tuple(int(x) for x in p) for p in pairs.cpu().numpy()] == pairs_e
     cnt2, _, total2 = B.hamming_all_pairs(d, L, k, method="pigeonhole")
     assert total2 == total and torch.equal(cnt2, cnt)
+    if total > 4:    # truncated pair output: the total still counts every pair, the kept ones are real
+        _, p3, total3 = B.hamming_all_pairs(d, L, k, counts=False, max_pairs=3, method="pigeonhole")
+        assert total3 == total and p3.shape[0] == 3
+        assert {tuple(int(x) for x in q) for q in p3.cpu().numpy()} <= set(pairs_e)
 
 
 def _pair_set(pairs):
