@@ -91,7 +91,7 @@ def _pair_set(pairs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["random12", "umi_pool12", "dups10", "random16k2", "one_read"])
+@pytest.mark.parametrize("case", ["random12", "umi_pool12", "dups10", "random16k2", "random32_hashed", "one_read"])
 def test_all_pairs_methods_agree_large(gpu, oracle, case):
     """At bench-like sizes (n >= 2^15, where auto may pick either form): tiles, pigeonhole and auto
     give the same counts, totals and pair sets, for uniform UMIs, a UMI pool with 1-nt variants,
@@ -110,6 +110,9 @@ def test_all_pairs_methods_agree_large(gpu, oracle, case):
     elif case == "random16k2":
         L, k = 16, 2
         ascii = oracle.gen_reads(7, 0, n, L)
+    elif case == "random32_hashed":      # 16-nt segments: buckets by a hash of 32 bits to 17
+        L, k = 32, 1
+        ascii = _umis(oracle, n, L, 30_000, 9)
     else:
         n = 40_000
         ascii = np.tile(oracle.gen_reads(8, 0, 1, L), n)
@@ -141,3 +144,19 @@ def test_all_pairs_pigeonhole_refuses_long_reads(gpu):
         B.hamming_all_pairs(d, 40, 1, method="pigeonhole")
     with pytest.raises(NativeError):
         B.hamming_all_pairs(d[:, :1].contiguous(), 20, 16, method="pigeonhole")
+
+
+@pytest.mark.gpu
+def test_all_pairs_pigeonhole_past_2_22(gpu, oracle):
+    """n > 2^22 reads (the bucket tables at their 2^22 cap: 1024 scan tiles per segment, hashed
+    segment values): the pigeonhole form's counts and total equal the tiled form's."""
+    import torch
+    import shortseq_amd.batch as B
+    n, L, k = (1 << 22) + 12345, 20, 1
+    ascii = _umis(oracle, n, L, 1 << 21, 13)
+    words, _, _ = oracle.encode_batch(ascii, n, L)
+    d = torch.from_numpy(words.view(np.int64)).to(gpu)
+    cnt_t, _, tot_t = B.hamming_all_pairs(d, L, k, method="tiles")
+    cnt_p, _, tot_p = B.hamming_all_pairs(d, L, k, method="pigeonhole")
+    assert tot_p == tot_t and torch.equal(cnt_p, cnt_t)
+    assert int(cnt_t.sum().item()) == 2 * tot_t and tot_t > 0
