@@ -400,7 +400,7 @@ int launch_allpairs(AllPairsArgs a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 constexpr int kPigMaxG = 16;
 constexpr uint32_t kPigTile = 4096;      // buckets per scan tile: 256 threads x 16
-constexpr uint32_t kPigMaxBits = 22;     // <= 1024 tiles per segment (one k_pig_top block)
+constexpr uint32_t kPigMaxBits = 22;     // <= 1024 tiles per segment (4 per thread of the scanning block)
 constexpr uint64_t kPigRatio = 16;       // auto: pigeonhole when candidates < all pairs / kPigRatio
 
 struct PigArgs {
@@ -413,6 +413,8 @@ struct PigArgs {
     uint32_t* tile_cnt;   // G * maxtiles: bucket sums, then tile bases
     uint64_t* tile_cand;  // G * maxtiles
     uint64_t* cand;       // G: candidate pairs per segment
+    uint32_t* done;       // k_pig_tile's finished-block count (zeroed with hist)
+    uint32_t zero_out;    // k_pig_hist zeroes counts and *npairs (the entry point left them)
     uint64_t* sw;         // G * n words in bucket order
     uint32_t* sid;        // G * n read indices in bucket order
     uint32_t* rank;       // G * n: read i's rank in its bucket of segment g (k_pig_hist's atomics)
@@ -435,7 +437,9 @@ __device__ __forceinline__ uint32_t pig_bucket(const PigArgs& a, uint32_t g, uin
 }
 
 __global__ __launch_bounds__(256) void k_pig_hist(PigArgs a) {
+    if (a.zero_out && blockIdx.x == 0 && threadIdx.x == 0) *a.npairs = 0ull;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256) {
+        if (a.zero_out && a.counts) a.counts[i] = 0u;
         const uint64_t w = a.words[i * a.wpr];
         for (uint32_t g = 0; g < a.G; ++g)
             a.rank[g * a.n + i] = atomicAdd(&a.hist[((uint64_t)g << a.nbmax) + pig_bucket(a, g, w)], 1u);
@@ -453,52 +457,69 @@ __device__ __forceinline__ T block_sum256(T v, T* red) {
     return t;
 }
 
-// per tile of 4096 buckets: number of reads and candidate pairs
+// per tile of 4096 buckets: number of reads and candidate pairs; the grid's last block to finish
+// then scans every segment's tile sums (<= 1024 tiles: 4 per thread) into tile bases and the
+// segment's candidate total -- no separate scan launch
 __global__ __launch_bounds__(256) void k_pig_tile(PigArgs a) {
     const uint32_t g = blockIdx.y, t0 = blockIdx.x * kPigTile, nbk = 1u << a.nb[g];
-    if (t0 >= nbk) return;
-    const uint32_t* h = a.hist + ((uint64_t)g << a.nbmax) + t0;
-    uint32_t c = 0;
-    uint64_t cand = 0;
-    for (uint32_t j = threadIdx.x; j < kPigTile && t0 + j < nbk; j += 256) {
-        const uint64_t v = h[j];
-        c += (uint32_t)v;
-        cand += v * (v - (v ? 1 : 0)) / 2;
-    }
     __shared__ uint32_t r32[4];
     __shared__ uint64_t r64[4];
-    c = block_sum256(c, r32);
-    cand = block_sum256(cand, r64);
+    __shared__ uint32_t s_last;
+    if (t0 < nbk) {
+        const uint32_t* h = a.hist + ((uint64_t)g << a.nbmax) + t0;
+        uint32_t c = 0;
+        uint64_t cand = 0;
+        for (uint32_t j = threadIdx.x; j < kPigTile && t0 + j < nbk; j += 256) {
+            const uint64_t v = h[j];
+            c += (uint32_t)v;
+            cand += v * (v - (v ? 1 : 0)) / 2;
+        }
+        c = block_sum256(c, r32);
+        cand = block_sum256(cand, r64);
+        if (threadIdx.x == 0) {
+            a.tile_cnt[g * a.maxtiles + blockIdx.x] = c;
+            a.tile_cand[g * a.maxtiles + blockIdx.x] = cand;
+        }
+    }
     if (threadIdx.x == 0) {
-        a.tile_cnt[g * a.maxtiles + blockIdx.x] = c;
-        a.tile_cand[g * a.maxtiles + blockIdx.x] = cand;
+        __threadfence();                                          // this block's sums before its count
+        s_last = atomicAdd(a.done, 1u) + 1u == gridDim.x * gridDim.y;
     }
-}
-
-// per segment: exclusive scan of the tile sums (<= 1024 tiles), candidate total
-__global__ __launch_bounds__(1024) void k_pig_top(PigArgs a) {
-    const uint32_t g = blockIdx.x, nt = ((1u << a.nb[g]) + kPigTile - 1) / kPigTile, t = threadIdx.x;
-    const uint32_t lane = t & 63u, wv = t >> 6;
-    uint32_t v = t < nt ? a.tile_cnt[g * a.maxtiles + t] : 0u;
-    uint64_t cand = t < nt ? a.tile_cand[g * a.maxtiles + t] : 0ull;
-    uint32_t inc = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o);
-        if (lane >= (uint32_t)o) inc += y;
-    }
-    for (int o = 32; o; o >>= 1) cand += __shfl_xor(cand, o);
-    __shared__ uint32_t ws[16];
-    __shared__ uint64_t cs[16];
-    if (lane == 63) ws[wv] = inc;
-    if (lane == 0) cs[wv] = cand;
     __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t i = 0; i < wv; ++i) before += ws[i];
-    if (t < nt) a.tile_cnt[g * a.maxtiles + t] = before + inc - v;
-    if (t == 0) {
-        uint64_t tot = 0;
-        for (int i = 0; i < 16; ++i) tot += cs[i];
-        a.cand[g] = tot;
+    if (!s_last) return;
+    __threadfence();                                              // every block's sums visible
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint32_t gg = 0; gg < a.G; ++gg) {
+        const uint32_t nt = ((1u << a.nb[gg]) + kPigTile - 1) / kPigTile;
+        uint32_t* tc = a.tile_cnt + gg * a.maxtiles;
+        uint64_t* td = a.tile_cand + gg * a.maxtiles;
+        uint32_t v[4], sum = 0;
+        uint64_t cand = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t t = 4 * threadIdx.x + k;
+            // device-scope loads (other blocks wrote them): past this CU's cache
+            v[k] = t < nt ? __hip_atomic_load(&tc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            cand += t < nt ? __hip_atomic_load(&td[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+            sum += v[k];
+        }
+        uint32_t inc = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o);
+            if (lane >= (uint32_t)o) inc += y;
+        }
+        if (lane == 63) r32[wv] = inc;
+        const uint64_t ctot = block_sum256(cand, r64);              // (its barriers order r32 too)
+        uint32_t run = inc - sum;
+        for (uint32_t i = 0; i < wv; ++i) run += r32[i];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t t = 4 * threadIdx.x + k;
+            if (t < nt) tc[t] = run;
+            run += v[k];
+        }
+        if (threadIdx.x == 0) a.cand[gg] = ctot;
+        __syncthreads();                                          // r32 of the next segment
     }
 }
 
@@ -686,6 +707,7 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     a.pairs = b.pairs;
     a.max_pairs = b.max_pairs;
     a.npairs = b.npairs;
+    a.zero_out = 1;
     uint32_t lg = 0;
     while ((1ull << lg) < a.n) ++lg;
     a.nbmax = lg < 10 ? 10 : (lg > kPigMaxBits ? kPigMaxBits : lg);
@@ -709,7 +731,7 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     PigScratch& ps = g_pig[dev];
     std::lock_guard<std::mutex> lock(ps.mu);
     const size_t hist_n = (size_t)a.G << a.nbmax, tiles_n = (size_t)a.G * a.maxtiles;
-    const size_t need = tiles_n * 8 + a.G * 8 + hist_n * 4 + tiles_n * 4 + 64 + (size_t)a.G * a.n * 16;
+    const size_t need = tiles_n * 8 + a.G * 8 + (hist_n + 2) * 4 + tiles_n * 4 + 64 + (size_t)a.G * a.n * 16;
     if (!ps.done) rc = ss_check(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming), "pig event");
     if (!rc && !ps.h_cand) rc = ss_check(hipHostMalloc((void**)&ps.h_cand, kPigMaxG * 8, hipHostMallocDefault), "pinned totals");
     if (!rc && ps.bytes < need) {
@@ -731,17 +753,17 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     a.cand = a.tile_cand + tiles_n;
     a.sw = a.cand + a.G;
     a.hist = (uint32_t*)(a.sw + (size_t)a.G * a.n);
-    a.tile_cnt = a.hist + hist_n;
+    a.done = a.hist + hist_n;                 // zeroed with hist
+    a.tile_cnt = a.done + 2;
     a.sid = a.tile_cnt + tiles_n;
     a.rank = a.sid + (size_t)a.G * a.n;
     const unsigned rgrid = (unsigned)std::min<uint64_t>((a.n + 255) / 256, 2048);
     const dim3 tgrid(a.maxtiles, a.G);
-    rc = ss_check(hipMemsetAsync(a.hist, 0, hist_n * 4, s), "pig hist reset");
+    rc = ss_check(hipMemsetAsync(a.hist, 0, (hist_n + 2) * 4, s), "pig hist reset");
     if (!rc) {
         hipLaunchKernelGGL(k_pig_hist, dim3(rgrid), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_pig_tile, tgrid, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(k_pig_top, dim3(a.G), dim3(1024), 0, s, a);
-        rc = ss_check(hipGetLastError(), "k_pig_hist/tile/top");
+        rc = ss_check(hipGetLastError(), "k_pig_hist/tile");
     }
     bool use = forced;
     if (!rc && !forced) {
@@ -789,8 +811,16 @@ int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uin
     if (!d_npairs) return ss_fail(SS_EARG, "d_npairs is required");
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "n must be < 2^32");
     hipStream_t s = (hipStream_t)stream;
-    int rc = ss_check(hipMemsetAsync(d_npairs, 0, sizeof(uint64_t), s), "npairs reset");
-    if (!rc && d_counts && n) rc = ss_check(hipMemsetAsync(d_counts, 0, n * sizeof(uint32_t), s), "counts reset");
+    // the pigeonhole form (tried first when it may apply) zeroes the outputs in its first kernel
+    const uint32_t Pw = L + 1 < 32u ? L + 1 : 32u, Gw = max_dist + 1;
+    const bool pig_try = n >= 2 && W == 1 && method != SS_ALLPAIRS_TILES && wpr >= W && d_words &&
+                         (method == SS_ALLPAIRS_PIGEONHOLE ? Gw <= (uint32_t)kPigMaxG
+                                                           : Gw <= (uint32_t)kPigMaxG && Pw / Gw >= 3 && n >= (1u << 15));
+    int rc = SS_OK;
+    if (!pig_try) {
+        rc = ss_check(hipMemsetAsync(d_npairs, 0, sizeof(uint64_t), s), "npairs reset");
+        if (!rc && d_counts && n) rc = ss_check(hipMemsetAsync(d_counts, 0, n * sizeof(uint32_t), s), "counts reset");
+    }
     if (rc || n < 2) return rc;
     if (!d_words || (d_pairs && max_pairs == 0)) return ss_fail(SS_EARG, "null buffer");
     AllPairsArgs a;
@@ -806,15 +836,11 @@ int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uin
     a.npairs = (unsigned long long*)d_npairs;
     if (method == SS_ALLPAIRS_PIGEONHOLE && (W != 1 || max_dist + 1 > (uint32_t)kPigMaxG))
         return ss_fail(SS_EARG, "pigeonhole all-pairs needs L <= 32 and max_dist < 16");
-    if (W == 1 && method != SS_ALLPAIRS_TILES) {
-        const uint32_t P = L + 1 < 32u ? L + 1 : 32u, G = max_dist + 1;
-        // auto: segments of >= 3 nt and a batch large enough to pay the host read of the totals
-        const bool eligible = G <= (uint32_t)kPigMaxG && P / G >= 3 && n >= (1u << 15);
-        if (method == SS_ALLPAIRS_PIGEONHOLE || eligible) {
-            bool done = false;
-            rc = pig_all_pairs(a, L, P, method == SS_ALLPAIRS_PIGEONHOLE, s, &done);
-            if (rc || done) return rc;
-        }
+    // auto: segments of >= 3 nt and a batch large enough to pay the host read of the totals
+    if (pig_try) {
+        bool done = false;
+        rc = pig_all_pairs(a, L, Pw, method == SS_ALLPAIRS_PIGEONHOLE, s, &done);
+        if (rc || done) return rc;
     }
     if (W <= 4) {
         // MFMA form: P = min(L + 1, 32 W) positions (the alias bit of the tail block can sit at
