@@ -38,7 +38,7 @@ enum ss_status {
     SS_ETOO_LONG = 2,       /* "Sequences longer than 1024 bases are not supported." (short_seq.pyx:74) */
     SS_EARG = -1,           /* bad argument (NULL pointer, L out of range, wpr too small, misalignment) */
     SS_EHIP = -2,           /* HIP runtime error; see ss_last_error_string() */
-    SS_ENOMEM = -3,         /* allocation failed (counter handles only) */
+    SS_ENOMEM = -3,         /* device allocation failed (counter handles, forced pigeonhole all-pairs) */
     SS_EFULL = -4           /* counter table full */
 };
 

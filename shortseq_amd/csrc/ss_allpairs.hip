@@ -742,7 +742,15 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
             ps.bytes = 0;
         }
         const size_t want = need + need / 4;
-        if (!rc) rc = ss_check(hipMalloc(&ps.p, want), "pig scratch");
+        if (!rc && hipMalloc(&ps.p, want) != hipSuccess) {
+            (void)hipGetLastError();
+            ps.p = nullptr;
+            if (forced) return ss_fail(SS_ENOMEM, "pigeonhole all-pairs scratch: out of device memory");
+            // auto: the tiled form needs no scratch; it gets the outputs zeroed as the entry skipped that
+            rc = ss_check(hipMemsetAsync(a.npairs, 0, sizeof(uint64_t), s), "npairs reset");
+            if (!rc && a.counts) rc = ss_check(hipMemsetAsync(a.counts, 0, a.n * sizeof(uint32_t), s), "counts reset");
+            return rc;
+        }
         if (!rc) ps.bytes = want;
     } else if (!rc) {
         rc = ss_check(hipStreamWaitEvent(s, ps.done, 0), "pig scratch wait");
