@@ -10,6 +10,10 @@
  *     `h_*` arguments are host pointers.  `stream` is a hipStream_t passed as void* (NULL = default).
  *   - Device entry points are asynchronous on `stream`, never allocate, never synchronise, and are
  *     safe to capture in a hipGraph.  They return SS_OK or a launch/argument error immediately.
+ *     Exceptions, each documented at its declaration: the counter and ingest handles (their own
+ *     workspaces; the ingest calls are synchronous), and ss_hamming_all_pairs / _ex when they take
+ *     the pigeonhole form (a per-device scratch buffer cached across calls; AUTO reads its candidate
+ *     totals back with one stream sync).  SS_ALLPAIRS_TILES keeps the plain contract.
  *   - Validation mirrors util.pxd:98-99 (bloom filter 0xFFFFFFFFFFEFFF75, util.pyx:75).  A kernel
  *     that meets an invalid byte writes the index of the FIRST invalid read (input order) into
  *     *d_first_bad (atomicMin; the entry point resets it to UINT64_MAX first).  The caller re-scans
