@@ -570,6 +570,7 @@ __global__ __launch_bounds__(256) void k_pig_scatter(PigArgs a) {
 // buffer and leave in runs (one pair-counter atomic per run of up to kPairBuf); count-only calls keep
 // the wave's hit count in a register and add it once.
 constexpr uint32_t kPairBuf = 512;
+constexpr uint64_t kPigTileWalk = 256;     // a wave's entry run past this: walked as broadcast tiles
 struct WaveHits {
     uint2* buf;          // this wave's kPairBuf LDS entries
     uint32_t fill = 0;   // wave-uniform
@@ -609,25 +610,22 @@ __device__ __forceinline__ void hits_add(const PigArgs& a, WaveHits& wh, bool hi
     if (hit) wh.buf[wh.fill + __popcll(mask & ((1ull << lane) - 1ull))] = make_uint2(min(i, j), max(i, j));
     wh.fill += c;
 }
-__device__ __forceinline__ void hits_done(const PigArgs& a, WaveHits& wh) {
-    if (a.pairs) hits_flush(a, wh);
-    else if ((threadIdx.x & 63u) == 0 && wh.nh) atomicAdd(a.npairs, (unsigned long long)wh.nh);
-}
 
 // one lane per read in bucket order of segment g = blockIdx.y, compared with the reads after it in its
-// bucket.  A wave's 64 reads are consecutive, so the reads they need are one run, [p0 + 1, the wave's
-// largest bucket end): it goes through in tiles of 64 -- one coalesced load per tile, then each
-// entry broadcast to the wave from its lane (v_readlane: a scalar operand), so the 64 compares of a
-// tile wait on no memory.  Hits leave through wave ballots into the wave's hit buffer.
+// bucket (see the walk below).  Hits leave through wave ballots into the wave's hit buffer; a
+// count-only call sums the block's hits in LDS and adds them with one atomic per block (one per
+// wave on the single pair counter measured a third of the kernel).
 template <int GM>   // G <= GM segments: the first-equal-segment test unrolled over GM - 1 masks
 __global__ __launch_bounds__(256) void k_pig_pairs(PigArgs a) {
     __shared__ uint2 pbuf[4][kPairBuf];
+    __shared__ unsigned long long s_hits;
+    if (threadIdx.x == 0) s_hits = 0;
+    __syncthreads();
     const uint32_t g = blockIdx.y, lane = threadIdx.x & 63u;
     // the wave's first position, made scalar (threadIdx.x & ~63 is wave-uniform)
     const uint64_t p0 = (uint64_t)blockIdx.x * 256 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
     const uint64_t p = p0 + lane;
-    if (p0 >= a.n) return;                                   // whole wave past the batch
-    const bool valid = p < a.n;
+    const bool valid = p < a.n;                              // (a wave past the batch walks nothing)
     const uint64_t* sw = a.sw + g * a.n;
     const uint32_t* sid = a.sid + g * a.n;
     const uint32_t* start = a.hist + ((uint64_t)g << a.nbmax);
@@ -635,7 +633,7 @@ __global__ __launch_bounds__(256) void k_pig_pairs(PigArgs a) {
     const uint64_t w = valid ? sw[p] : 0ull;
     const uint32_t id = valid ? sid[p] : 0u;
     const uint32_t b = pig_bucket(a, g, w);
-    const uint64_t end = valid ? (b + 1 < nbk ? start[b + 1] : a.n) : 0ull;
+    uint64_t end = valid ? (b + 1 < nbk ? start[b + 1] : a.n) : 0ull;
     // segment h's positions as one bit per position (the low bit of its 2-bit code): with
     // d = the positions where two words differ, the pair is segment g's iff d misses segment g and
     // meets every segment before it (g is the pair's first equal segment) and popcount(d) <= k
@@ -648,6 +646,43 @@ __global__ __launch_bounds__(256) void k_pig_pairs(PigArgs a) {
     WaveHits wh;
     wh.buf = pbuf[threadIdx.x >> 6];
     uint32_t row = 0;
+    // the wave's run of entries, [p0 + 1, its largest bucket end): long (large buckets: heavy
+    // duplicates, short segments) -> the wave walks it in 64-entry tiles, one coalesced load per tile
+    // and each entry broadcast to the wave by v_readlane (the 64 compares of a tile wait on no
+    // memory); short (the UMI case) -> each lane walks its own run (below)
+    uint64_t wend = end;
+    for (int o = 32; o; o >>= 1) {
+        const uint64_t y = shfl64x(wend, o);
+        wend = y > wend ? y : wend;
+    }
+    wend = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wend >> 32)) << 32 |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wend);   // uniform: scalar loop bounds
+    if (wend > p0 + kPigTileWalk) {
+        for (uint64_t t0 = p0 + 1; t0 < wend; t0 += 64) {
+            const uint64_t qt = t0 + lane;
+            const uint64_t tw = qt < a.n ? sw[qt] : 0ull;
+            const uint32_t tid = qt < a.n ? sid[qt] : 0u;
+            const uint32_t twl = (uint32_t)tw, twh = (uint32_t)(tw >> 32);
+            const uint32_t ne = (uint32_t)((wend - t0) < 64 ? (wend - t0) : 64);
+            for (uint32_t e = 0; e < ne; ++e) {
+                const uint64_t q = t0 + e;
+                const uint64_t w2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)twh, (int)e) << 32 |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)twl, (int)e);
+                const uint64_t x = w ^ w2, d = (x | (x >> 1)) & kLo;
+                bool hit = (q > p) & (q < end) & ((uint32_t)__popcll(d) <= kmax) & !(d & mg);
+#pragma unroll
+                for (int h = 0; h < GM - 1; ++h) hit = hit && ((uint32_t)h >= g || (d & segm[h]) != 0ull);
+                const uint64_t mask = __ballot(hit);
+                if (!mask) continue;
+                const uint32_t jd = (uint32_t)__builtin_amdgcn_readlane((int)tid, (int)e);
+                row += hit ? 1u : 0u;
+                if (a.counts && lane == (uint32_t)__ffsll((unsigned long long)mask) - 1u)
+                    atomicAdd(&a.counts[jd], (uint32_t)__popcll(mask));
+                hits_add(a, wh, hit, mask, id, jd);
+            }
+        }
+        end = 0;                                           // (the lane walk below has nothing left)
+    }
     // each lane walks its own bucket run (p, end): consecutive lanes read consecutive entries, so a
     // step's 64 loads are one coalesced run; kPigStep entries per step, the next step's in flight
     constexpr int kPigStep = 4;
@@ -678,8 +713,11 @@ __global__ __launch_bounds__(256) void k_pig_pairs(PigArgs a) {
             hits_add(a, wh, hit, mask, id, jd);
         }
     }
-    hits_done(a, wh);
+    if (a.pairs) hits_flush(a, wh);
+    else if (lane == 0 && wh.nh) atomicAdd(&s_hits, (unsigned long long)wh.nh);
     if (a.counts && row) atomicAdd(&a.counts[id], row);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_hits) atomicAdd(a.npairs, s_hits);
 }
 
 // Per-device scratch of the pigeonhole form, grow-only and stream-ordered: a call holds the device's
