@@ -13,11 +13,14 @@ from shortseq_amd._native import lib  # noqa: E402
 
 dev = torch.device("cuda", 0)
 if len(sys.argv) > 1 and sys.argv[1] == "quick":     # one case per method (rocprof kernel tables)
-    # python tools/probe_f4.py quick [n L k]: the pigeonhole time last (scripts/gpu.sh libab)
+    # python tools/probe_f4.py quick [n L k]: pigeonhole and auto times on the last line (scripts/gpu.sh libab)
     n, L, k = (int(x) for x in sys.argv[2:5]) if len(sys.argv) > 4 else (100_000, 12, 1)
-    for m in ("tiles", "pigeonhole"):
+    res = []
+    for m in ("tiles", "pigeonhole", "auto"):
         r = bench.bench_all_pairs(B, lib(), dev, n=n, L=L, k=k, method=m, reps=20)
-        print(m, f"{r['ms_per_step']:.4f} ms", flush=True)
+        res.append(f"{m} {r['ms_per_step']:.4f} ms")
+        print(res[-1], flush=True)
+    print(" | ".join(res[1:]), flush=True)
     sys.exit(0)
 for _ in range(2):
     print(bench.bench_all_pairs(B, lib(), dev), flush=True)
