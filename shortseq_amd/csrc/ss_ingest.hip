@@ -289,7 +289,10 @@ __global__ __launch_bounds__(256) void k_rank(const uint64_t* __restrict__ first
 }
 
 // export: entry e's first read (engine-local) = rowmap[first[e]]
-// the largest of m counts (atomicMax into *mx): an export's largest count sizes the merge passes
+// the largest of m counts (atomicMax into *mx): an export's largest count sizes the merge passes.
+// Grid-stride with a capped grid and one atomic per block: the single counter takes kMaxBlocks
+// atomics, not one per wave of the entries (262k at 2^24 entries, serialised on one address)
+constexpr unsigned kCountMaxBlocks = 1024;
 __global__ __launch_bounds__(256) void k_count_max(const uint64_t* __restrict__ counts, uint64_t m,
                                                    unsigned long long* mx, const uint64_t* dm = nullptr) {
     if (dm) m = min(m, *dm);
@@ -297,7 +300,13 @@ __global__ __launch_bounds__(256) void k_count_max(const uint64_t* __restrict__ 
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256)
         v = max(v, counts[e]);
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint64_t)__shfl_xor((unsigned long long)v, o));
-    if ((threadIdx.x & 63u) == 0 && v) atomicMax(mx, (unsigned long long)v);
+    __shared__ uint64_t wmax[4];
+    if ((threadIdx.x & 63u) == 0) wmax[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (b) atomicMax(mx, (unsigned long long)b);
+    }
 }
 
 // one merge pass: take = min(left, room) of every entry's remaining count
@@ -1960,7 +1969,8 @@ int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys) {
         return rc;
     for (Group* gr : placed)
         if (gr->m)
-            hipLaunchKernelGGL(k_count_max, dim3(grid_of(gr->m, 256)), dim3(256), 0, g->stream, gr->counts.p, gr->m,
+            hipLaunchKernelGGL(k_count_max, dim3(std::min<unsigned>(grid_of(gr->m, 256), kCountMaxBlocks)), dim3(256), 0,
+                               g->stream, gr->counts.p, gr->m,
                                (unsigned long long*)g->mg_take.p);
     rc = ss_check(hipMemcpyAsync(g->h_bad + 3 * kLenBins + 4, g->mg_take.p, 8, hipMemcpyDeviceToHost, g->stream),
                   "ingest export max");
