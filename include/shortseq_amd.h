@@ -447,6 +447,10 @@ int ss_ingest_results_compact(ss_ingest* g, const uint16_t** h_lens, const void*
  *                     version; the reference has one process-wide dict (counter.pyx:41-54). */
 int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys);
 int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base);
+/* Optional, before a destination's merges: size dst's tables and row maps once for the union of
+ * the nsrc (exported) sources' entries, so the merges that follow do not grow a table -- re-inserting
+ * every entry it holds -- one merge at a time.  Synchronous.  New in this ABI version. */
+int ss_ingest_reserve_merge(ss_ingest* dst, ss_ingest* const* srcs, uint32_t nsrc);
 
 /* ------------------------------------------------------------------------------------------------
  * Synthetic reads on the device (SURVEY §8(d) generator; identical to oracle/ss_oracle.c):

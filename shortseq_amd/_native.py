@@ -105,6 +105,7 @@ SIGNATURES = [
                                             C.POINTER(C.c_uint32), C.POINTER(C.c_void_p)]),
     ("ss_ingest_export", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("ss_ingest_merge", C.c_int, [_P, _P, _U64]),
+    ("ss_ingest_reserve_merge", C.c_int, [_P, _P, _U32]),
     ("ss_stager_create", C.c_int, [C.c_int, _U64, _U32, _U32, C.POINTER(C.c_void_p)]),
     ("ss_stager_destroy", C.c_int, [_P]),
     ("ss_encode_host", C.c_int, [_P, _P, _U64, _U32, _U64, _P, _U32, C.POINTER(C.c_uint64)]),

@@ -535,6 +535,12 @@ class DeviceIngest:
         this engine's tables on its device (ss_ingest_merge: peer copies, counts add, first = min)."""
         check(lib().ss_ingest_merge(self._h, src._h, int(base)), "ss_ingest_merge")
 
+    def reserve_merge(self, srcs) -> None:
+        """Size this engine's tables once for the union of the exported engines `srcs` it will merge
+        (ss_ingest_reserve_merge): no table growth per merge."""
+        arr = (C.c_void_p * max(1, len(srcs)))(*[e._h.value for e in srcs])
+        check(lib().ss_ingest_reserve_merge(self._h, arr, len(srcs)), "ss_ingest_reserve_merge")
+
     def reset(self) -> None:
         check(lib().ss_ingest_reset(self._h), "ss_ingest_reset")
         self._fresh = True

@@ -78,6 +78,7 @@ ctypedef int (*f_add_fastq_range)(ss_ingest*, const char*, uint64_t, uint64_t, u
 ctypedef int (*f_set_exact)(ss_ingest*, int) noexcept nogil
 ctypedef int (*f_export)(ss_ingest*, uint64_t*) noexcept nogil
 ctypedef int (*f_merge)(ss_ingest*, ss_ingest*, uint64_t) noexcept nogil
+ctypedef int (*f_reserve_merge)(ss_ingest*, ss_ingest**, uint32_t) noexcept nogil
 
 cdef struct _Abi:
     f_device_count device_count
@@ -96,6 +97,7 @@ cdef struct _Abi:
     f_set_exact set_exact
     f_export export_keys
     f_merge merge
+    f_reserve_merge reserve_merge
 
 cdef _Abi _abi
 cdef bint _abi_ready = False
@@ -133,6 +135,7 @@ cdef int _bind_abi() except -1:
     _abi.set_exact = <f_set_exact>_sym(h, b"ss_ingest_set_exact")
     _abi.export_keys = <f_export>_sym(h, b"ss_ingest_export")
     _abi.merge = <f_merge>_sym(h, b"ss_ingest_merge")
+    _abi.reserve_merge = <f_reserve_merge>_sym(h, b"ss_ingest_reserve_merge")
     _abi_ready = True
     return 0
 
@@ -740,9 +743,19 @@ cdef _reduce_fill(ShortSeqCounter self, list engines, list bases):
         if mode == "auto":
             mode = "chain" if len(set(e[0] for e in engines)) == 1 else "tree"
         if mode == "chain":
+            _reserve_merge(<size_t>engines[0][1], [<size_t>engines[k][1] for k in range(1, D)])
             for k in range(1, D):
                 _merge_pair(<size_t>engines[0][1], <size_t>engines[k][1], bases[k], False)
         else:
+            # every destination sized once for the union of the engines it will absorb (a absorbs
+            # a + 1 .. a + lowbit(a) - 1; engine 0 all others), each on its own device
+            res = []
+            for a in range(0, D, 2):
+                span = (a & -a) if a else D
+                srcs = [<size_t>engines[b][1] for b in range(a + 1, min(D, a + span))]
+                if srcs:
+                    res.append((<size_t>engines[a][1], srcs))
+            _run_parallel(_reserve_merge, res)
             step = 1
             while step < D:
                 pairs = [(a, a + step) for a in range(0, D, 2 * step) if a + step < D]
@@ -756,6 +769,25 @@ cdef _reduce_fill(ShortSeqCounter self, list engines, list bases):
         _ingest_check(rc, "ingest finish")
         _engine_nkeys[<size_t>g0] = K
     _fill_from_engine(self, g0)
+
+
+def _reserve_merge(size_t gd, list srcs):
+    """Destination gd's tables and row maps sized once for the union of the (exported) sources'
+    entries (ss_ingest_reserve_merge), so its merges do not grow the tables one merge at a time."""
+    cdef ss_ingest* d = <ss_ingest*>gd
+    cdef uint32_t k, n = len(srcs)
+    cdef ss_ingest** arr = <ss_ingest**>malloc(max(1, n) * sizeof(ss_ingest*))
+    cdef int rc = 0
+    if arr == NULL:
+        raise MemoryError()
+    try:
+        for k in range(n):
+            arr[k] = <ss_ingest*><size_t>srcs[k]
+        with nogil:
+            rc = _abi.reserve_merge(d, arr, n)
+    finally:
+        free(arr)
+    _ingest_check(rc, "ingest reserve merge")
 
 
 def _run_parallel(fn, jobs):

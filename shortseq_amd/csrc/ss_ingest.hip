@@ -1982,6 +1982,42 @@ int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys) {
     return SS_OK;
 }
 
+int ss_ingest_reserve_merge(ss_ingest* dst, ss_ingest* const* srcs, uint32_t nsrc) {
+    if (!dst || (nsrc && !srcs)) return ss_fail(SS_EARG, "ingest reserve merge: null argument");
+    if (dst->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
+    std::map<uint32_t, std::pair<uint64_t, const Group*>> total;      // bin -> (entries, a source group)
+    for (uint32_t k = 0; k < nsrc; ++k) {
+        ss_ingest* src = srcs[k];
+        if (!src || src == dst) return ss_fail(SS_EARG, "ingest reserve merge: sources distinct from the destination");
+        if (!src->exported) return ss_fail(SS_EARG, "ingest reserve merge: ss_ingest_export the sources first");
+        for (auto& kv : src->groups)
+            if (kv.second.table && kv.second.m) {
+                auto& t = total[kv.first];
+                t.first += kv.second.m;
+                t.second = &kv.second;
+            }
+    }
+    if (total.empty()) return SS_OK;
+    spec_wait(dst);
+    int rc = ss_check(hipSetDevice(dst->device), "ingest reserve merge device");
+    if (!rc) rc = flush_pending(dst);
+    if (rc) return rc;
+    hipStream_t s = dst->stream;
+    const double scale = dst->est_scale;
+    dst->est_scale = 1.0;
+    for (auto& kv : total) {
+        const uint64_t m = kv.second.first;
+        Group& gr = dst->groups[kv.first];
+        gr.L = kv.second.second->L;
+        gr.W1 = kv.second.second->W1;
+        // one table growth (at most) for the union of every source's entries, and the row map's
+        // room, instead of a growth -- every existing entry re-inserted -- at each merge
+        if ((rc = group_room(dst, gr, m, gr.rows + m)) || (rc = gr.rowmap.ensure_keep(gr.rows + m, gr.rows, s))) break;
+    }
+    dst->est_scale = scale;
+    return rc;
+}
+
 int ss_ingest_merge(ss_ingest* dst, ss_ingest* src, uint64_t src_base) {
     if (!dst || !src || dst == src) return ss_fail(SS_EARG, "ingest merge: two distinct engines");
     if (!src->exported) return ss_fail(SS_EARG, "ingest merge: ss_ingest_export the source first");

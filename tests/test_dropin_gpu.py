@@ -344,6 +344,40 @@ def test_device_ingest_tree_merge_abi(gpu, oracle):
     assert (gw == ew).all()
 
 
+@pytest.mark.parametrize("reserve", [False, True])
+def test_device_ingest_chain_reserve_abi(gpu, oracle, reserve):
+    """A chain of five exported engines into engine 0, with and without ss_ingest_reserve_merge
+    (engine 0's tables sized once for the union): the same rows as the generator; reserving with an
+    unexported source or with the destination among the sources is refused."""
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import NativeError
+    seed, ps, U, n, lo, hi = 57, 58, 1 << 15, 300_000, 1, 200
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    cuts = [0, n // 9, n // 3, n // 2, 4 * n // 5, n]
+    engs = [B.DeviceIngest(gpu) for _ in range(5)]
+    try:
+        for k, e in enumerate(engs):
+            e.count(blob, offs[cuts[k]:cuts[k + 1]], lens[cuts[k]:cuts[k + 1]])
+        with pytest.raises(NativeError, match="export"):
+            engs[0].reserve_merge(engs[1:])
+        for e in engs[1:]:
+            e.export()
+        with pytest.raises(NativeError, match="distinct"):
+            engs[1].reserve_merge([engs[1], engs[2]])
+        if reserve:
+            engs[0].reserve_merge(engs[1:])
+        for k in range(1, 5):
+            engs[0].merge(engs[k], cuts[k])
+        gl, gc, gw = engs[0].results()
+    finally:
+        for e in engs:
+            e.close()
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    assert gl.tolist() == el.tolist()
+    assert gc.tolist() == ec.tolist()
+    assert (gw == ew).all()
+
+
 def test_cross_device_reduce(gpu, golden, tmp_path, oracle):
     """the xGMI path of the reduce (peer access + hipMemcpyPeerAsync on the destination's
     stream) on two real devices; skipped on a one-GPU box."""

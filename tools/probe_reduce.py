@@ -54,10 +54,16 @@ def main():
         t0 = time.perf_counter()
         par([(e.export, ()) for e in engs[1:]])       # the shards' exports run in their own threads
         t1 = time.perf_counter()
+        from shortseq_amd._native import lib as _lib
+        reserve = hasattr(_lib(), "ss_ingest_reserve_merge")     # (an A/B against a build without it)
         if mode == "chain":
+            if reserve:
+                engs[0].reserve_merge(engs[1:])
             for k in range(1, D):
                 engs[0].merge(engs[k], cuts[k])
         else:
+            if reserve:
+                par([(engs[p].reserve_merge, (engs[p + 1:min(D, p + ((p & -p) or D))],)) for p in range(0, D, 2)])
             step = 1
             while step < D:
                 pairs = [(p, p + step) for p in range(0, D, 2 * step) if p + step < D]
@@ -75,14 +81,17 @@ def main():
         assert len(lens_) > 0.999 * n and int(cnts.sum()) == n, (len(lens_), int(cnts.sum()))
         return (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3
 
+    last = {}
     for r in range(a.rounds + 1):
         for mode in ("chain", "tree"):
             count_all()
             torch.cuda.synchronize()
             ex, mg, fin = reduce(mode)
+            last[mode] = mg
             if r:
                 print(f"round {r} {mode:5s}: D={D} shard=2^{a.shard_log} L={a.lo}-{a.hi}: export {ex:7.2f} ms, "
                       f"reduce {mg:7.2f} ms, finish {fin:7.2f} ms", flush=True)
+    print(f"last round reduce: chain {last['chain']:.2f} ms, tree {last['tree']:.2f} ms", flush=True)
     for e in engs:
         e.close()
 
