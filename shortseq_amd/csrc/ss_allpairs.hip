@@ -392,9 +392,11 @@ int launch_allpairs(AllPairsArgs a, hipStream_t s) {
 // candidates, and a candidate (i, j) is reported by segment g only when segment g is equal and
 // every segment g' < g differs (the pair's first equal segment), so each pair is reported once.
 // Work is sum over buckets of c (c - 1) / 2 per segment instead of n (n - 1) / 2: for n random UMIs
-// of 12 nt and k = 1, 2 segments of 6-7 nt, ~n^2 / 2 / 4096 candidates.  Skewed batches (one UMI
-// repeated many times, low-complexity segments) make buckets large; the host reads the candidate
-// totals after the histogram and hands such batches to the tiled MFMA form (ss_hamming_all_pairs).
+// of 12 nt and k = 1, 2 segments of 6 nt (the alias position L joins the last), ~n^2 / 4096
+// candidates.  Skewed batches (one UMI repeated many times, low-complexity segments) make buckets
+// large; AUTO reads the candidate totals back after the histogram and hands such batches to the
+// tiled MFMA form.  Kernels: k_pig_hist (bucket counts, each read's rank), k_pig_tile (tile sums;
+// its last block scans them), k_pig_apply (bucket starts), k_pig_scatter, k_pig_pairs.
 // Buckets: the segment value itself when it has <= nbmax bits, else a 64-bit multiplicative hash of
 // it (colliding values only add candidates: the equality test is on the segment value).
 // ------------------------------------------------------------------------------------------------
