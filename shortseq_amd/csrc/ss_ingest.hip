@@ -1261,7 +1261,12 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             cr.push_back({gr.table, g->cls_words.p + woff[gr.W1 - 1], jb.m, gr.rows, gr.W1});
             if (flat) fc[gr.W1 - 1] = {gr.table, gr.rows, gr.rowmap.p + gr.rows};
         }
-        const uint64_t fcap = std::min<uint64_t>(1ull << 32, std::max<uint64_t>(1ull << 19, pow2_at_least(2 * need_all + 2)));
+        // twice the estimate; past 2^24 slots 1.5 times: the per-slot passes (a 64-B representative per
+        // slot, the extract) then cost more than a fuller table's longer probes (2^24-pool batch
+        // 20.8 -> 19.4 ms; at 2^20 the fuller 2^21 table was 0.4 ms slower, libab_f2_lf15_u2{0,4}.log)
+        uint64_t fwant = pow2_at_least(2 * need_all + 2);
+        if (fwant > (1ull << 24)) fwant = pow2_at_least(need_all + need_all / 2 + 2);
+        const uint64_t fcap = std::min<uint64_t>(1ull << 32, std::max<uint64_t>(1ull << 19, fwant));
         // grow-only with hysteresis: a stream whose per-chunk estimates cross a power of
         // two keeps its table; only a table 8x too large (its per-slot passes, reps and fold, scale
         // with the capacity) is replaced by a smaller one
