@@ -646,7 +646,9 @@ __device__ __forceinline__ void rows_meta_split(const RowsMeta& m, uint32_t R, u
 __global__ __launch_bounds__(256) void k_encode_rows(const uint8_t* in, const uint64_t* __restrict__ offs,
                                                      const uint32_t* __restrict__ lens, uint64_t n, uint32_t S,
                                                      uint64_t* __restrict__ out, uint64_t* __restrict__ fps,
-                                                     uint32_t* hll, unsigned long long* first_bad) {
+                                                     uint32_t* hll, unsigned long long* first_bad,
+                                                     const uint64_t* __restrict__ gate) {
+    if (gate && *gate != S) return;       // queued before the split came back: the split chose another path
     const uint32_t lane = threadIdx.x & 63u, R = 64u / S, wave = threadIdx.x >> 6;
     const uint32_t i = lane / S, w = lane - i * S;
     const uint64_t per = (uint64_t)R * kRowsK, tiles = (n + per - 1) / per, stride = (uint64_t)gridDim.x * 4;
@@ -1383,7 +1385,8 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
 }
 
 int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n, uint32_t S,
-                        uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll, uint64_t* d_first_bad, void* stream) {
+                        uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll, uint64_t* d_first_bad, void* stream,
+                        const uint64_t* d_gate) {
     if (S < 3 || S > 6) return ss_fail(SS_EARG, "k_encode_rows: rows of 3 to 6 words");
     if (n == 0) return SS_OK;
     // persistent waves (the occupancy's worth of blocks), each over tiles of R * kRowsK reads with the
@@ -1398,7 +1401,7 @@ int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint
     const uint64_t per = (uint64_t)(64 / S) * kRowsK, tiles = (n + per - 1) / per;
     const uint64_t blocks = std::min<uint64_t>((tiles + 3) / 4, (uint64_t)resident);
     hipLaunchKernelGGL(k_encode_rows, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, d_buf, d_offs, d_lens,
-                       n, S, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad);
+                       n, S, d_out, d_fps, d_hll, (unsigned long long*)d_first_bad, d_gate);
     return ss_check(hipGetLastError(), "k_encode_rows");
 }
 

@@ -2828,13 +2828,15 @@ struct FlatTotals {
     uint64_t* p[kRepW1];            // class W's total (entries of the scratch of class W), null: not wanted
 };
 
-__global__ __launch_bounds__(1024) void k_flat_fold_scan(uint32_t* __restrict__ blkcnt, uint32_t nblk, FlatTotals tot) {
+// (256 threads: the extract runs on the speculative finish's stream beside the verify, where a
+// 1024-thread workgroup waited up to ~0.5 ms for one CU to free 16 wave slots)
+__global__ __launch_bounds__(256) void k_flat_fold_scan(uint32_t* __restrict__ blkcnt, uint32_t nblk, FlatTotals tot) {
     __shared__ uint32_t carry[kRepW1];
-    __shared__ uint32_t wsum[16][kRepW1];
+    __shared__ uint32_t wsum[4][kRepW1];
     if (threadIdx.x < kRepW1) carry[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
+    for (uint32_t b0 = 0; b0 < nblk; b0 += 256) {
         const uint32_t b = b0 + threadIdx.x;
         uint32_t v[kRepW1], inc[kRepW1];
 #pragma unroll
@@ -2856,7 +2858,7 @@ __global__ __launch_bounds__(1024) void k_flat_fold_scan(uint32_t* __restrict__ 
         }
         __syncthreads();
         if (threadIdx.x < kRepW1)
-            for (uint32_t u = 0; u < 16; ++u) carry[threadIdx.x] += wsum[u][threadIdx.x];
+            for (uint32_t u = 0; u < 4; ++u) carry[threadIdx.x] += wsum[u][threadIdx.x];
         __syncthreads();
     }
     if (threadIdx.x < kRepW1 && tot.p[threadIdx.x]) *tot.p[threadIdx.x] = carry[threadIdx.x];
@@ -3732,7 +3734,7 @@ int ss_classes_flat_fold(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, 
     uint32_t* blk = nullptr;
     if ((rc = flat_scratch(fpt, grid, &rep, &found, &blk))) return rc;
     hipLaunchKernelGGL(k_flat_fold_find<false>, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep, d_flag, found, blk);
-    hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(1024), 0, s, blk, grid, FlatTotals{});
+    hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(256), 0, s, blk, grid, FlatTotals{});
     hipLaunchKernelGGL(k_flat_fold_claim, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep, d_flag,
                        (const uint64_t*)found, (const uint32_t*)blk);
     return ss_check(hipGetLastError(), "class fold (read-order rows)");
@@ -3766,7 +3768,7 @@ int ss_classes_flat_extract(ss_counter* fpt, uint32_t S, const ss_flat_class* cl
     uint32_t* blk = nullptr;
     if ((rc = flat_scratch(fpt, grid, &rep, &found, &blk))) return rc;
     hipLaunchKernelGGL(k_flat_fold_find<true>, dim3(grid), dim3(256), 0, s, f, d, (const uint64_t*)rep, d_zero, found, blk);
-    hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(1024), 0, s, blk, grid, tot);
+    hipLaunchKernelGGL(k_flat_fold_scan, dim3(1), dim3(256), 0, s, blk, grid, tot);
     hipLaunchKernelGGL(k_flat_extract_claim, dim3(grid), dim3(256), 0, s, f, d, o, (const uint64_t*)rep,
                        (const uint32_t*)blk);
     return ss_check(hipGetLastError(), "class extract (read-order rows)");

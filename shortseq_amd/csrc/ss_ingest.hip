@@ -204,6 +204,18 @@ __global__ __launch_bounds__(1024) void k_len_binstart(uint64_t* __restrict__ ou
         __syncthreads();
     }
     for (uint32_t b = threadIdx.x; b < kLenBins; b += 1024) out[2 * kLenBins + b] = s[b] - out[b];
+    // the read-order stride the host will choose (process_chunk's `flat`): every counted read a class
+    // read of 2 .. 5 words -> W + 1 of the longest; else 0
+    if (threadIdx.x == 0) {
+        uint32_t w1 = 0;
+        bool ok = true;
+        for (uint32_t b = 1; b < kTooLongBin; ++b) {
+            if (!out[b]) continue;
+            if (b <= 32) ok = false;
+            else w1 = max(w1, b - kClassBin0 + 1u);
+        }
+        out[3 * kLenBins] = ok && w1 >= 3u && w1 <= 6u ? w1 : 0u;
+    }
 }
 
 // stable scatter: block k walks its range in input order, 64 reads per step; the wave peels the
@@ -408,19 +420,34 @@ __global__ __launch_bounds__(256) void k_scan_count(const uint64_t* __restrict__
 }
 
 // exclusive scan of kScanBlocks block sums (one block); blksum[kScanBlocks] = total
-__global__ __launch_bounds__(1024) void k_scan_top(uint64_t* __restrict__ blksum) {
-    __shared__ uint64_t s[1024];
-    const uint64_t v = blksum[threadIdx.x];
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint64_t y = threadIdx.x >= off ? s[threadIdx.x - off] : 0ull;
-        __syncthreads();
-        s[threadIdx.x] += y;
-        __syncthreads();
+// 256 threads x 4 sums (not 1024 x 1): on the speculative finish's stream a 16-wave workgroup waits
+// for one CU to free 16 wave slots of the verify beside it; four waves find room as soon as one of the
+// verify's blocks retires
+__global__ __launch_bounds__(256) void k_scan_top(uint64_t* __restrict__ blksum) {
+    static_assert(kScanBlocks == 1024, "4 block sums per thread");
+    __shared__ uint64_t wsum[4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    uint64_t v[4], tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = blksum[4 * t + k];
+        tot += v[k];
     }
-    blksum[threadIdx.x] = s[threadIdx.x] - v;
-    if (threadIdx.x == 1023) blksum[1024] = s[1023];
+    uint64_t incl = tot;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t ylo = (uint32_t)__shfl_up((int)(uint32_t)incl, off), yhi = (uint32_t)__shfl_up((int)(uint32_t)(incl >> 32), off);
+        if (lane >= off) incl += (uint64_t)yhi << 32 | ylo;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t run = incl - tot;
+    for (uint32_t w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        blksum[4 * t + k] = run;
+        run += v[k];
+    }
+    if (t == 255) blksum[1024] = run;
 }
 
 // block-local ordered walk (256 items per step, wave scans + a 4-wave prefix): each item's exclusive
@@ -684,8 +711,12 @@ struct ss_ingest {
     DBuf<uint32_t> dlens;          // per read: length (0xFFFFFFFF = strlen underflow)
     DBuf<uint64_t> order;          // split output
     DBuf<uint32_t> blkhist, blkfirst;
-    DBuf<uint64_t> split_out;      // [3 * kLenBins]
-    uint64_t* h_split = nullptr;   // pinned [3 * kLenBins]
+    DBuf<uint64_t> split_out;      // [3 * kLenBins + 1]: totals, first reads, starts, the read-order stride
+    uint64_t* h_split = nullptr;   // pinned copy
+    // the previous chunk's read-order stride (0: it took another path): the next chunk's row encode is
+    // queued at that stride before its split comes back, gated on the device by the split's own stride
+    uint32_t flat_hint = 0;
+    hipEvent_t ev_split = nullptr;
     DBuf<uint8_t> rows;            // gathered dense rows (lengths <= 32)
     DBuf<uint64_t> cls_words;      // the length classes' packed rows (k_encode_classes / k_encode_class)
     DBuf<uint64_t> cls_fps;        // their fingerprints (k_encode_classes), class after class
@@ -697,8 +728,8 @@ struct ss_ingest {
     bool failed = false;           // an add returned SS_EFULL: the counts are void until reset
     int sizing = 0;                // class tables: 0 by their sketch, 1 by their rows, 2 by 1/64 of the
                                    // sketch (tests: forces the SS_EFULL path) -- ss_ingest_set_exact
-    DBuf<uint64_t> first_bad;      // one u64 per length of the chunk
-    uint64_t* h_bad = nullptr;     // pinned [2 kLenBins + 4]: first-bad and overflow words, a size query
+    DBuf<uint64_t> first_bad;      // [kLenBins + 1]: one u64 per length bin, the class encode's last
+    uint64_t* h_bad = nullptr;     // pinned [3 kLenBins + 8]: first-bad and overflow words, a size query
     DBuf<uint64_t> fq_ws, fq_aux, fq_counts;
     std::map<uint32_t, Group> groups;
     std::vector<std::pair<uint64_t, ss_counter*>> pool;    // idle tables (capacity, handle)
@@ -1028,7 +1059,7 @@ int spec_launch(ss_ingest* g, const uint64_t* need, uint64_t N) {
         return rc;
     hipLaunchKernelGGL((k_scan_count<0>), dim3(kScanBlocks), dim3(256), 0, ss, g->slot.p, NB, (const GDesc*)g->gdesc.p,
                        g->scan.p, (const uint64_t*)nullptr);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ss, g->scan.p);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, ss, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<0>), dim3(kScanBlocks), dim3(256), 0, ss, g->slot.p, NB, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p, (const uint64_t*)nullptr);
     for (size_t q = 0; q < cls.size(); ++q) {
@@ -1044,7 +1075,7 @@ int spec_launch(ss_ingest* g, const uint64_t* need, uint64_t N) {
     // word offsets of the ordered entries (K on the device; past the bound the gather refuses)
     hipLaunchKernelGGL((k_scan_count<1>), dim3(kScanBlocks), dim3(256), 0, ss, g->ordered.p, k_ub, (const GDesc*)g->gdesc.p,
                        g->scan.p, (const uint64_t*)(sd + 6));
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, ss, g->scan.p);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, ss, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, ss, g->ordered.p, k_ub, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p, (const uint64_t*)(sd + 6));
     g->wide = results_wide(g);
@@ -1090,22 +1121,40 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         uint64_t m, start, first;
     };
     std::vector<Job> jobs;
+    // first-bad words: one per length bin (a length's insert, a class's pass), the class encode's at
+    // kLenBins -- all reset here, before anything that may report
+    if ((rc = g->first_bad.ensure(kLenBins + 1))) return rc;
+    if ((rc = ss_check(hipMemsetAsync(g->first_bad.p, 0xFF, (kLenBins + 1) * 8, s), "ingest first_bad reset"))) return rc;
+    uint32_t spec_S = 0;         // the row encode queued behind the split at this stride (gated on the device)
     if (dense_L) {
         if (dense_L > SS_MAX_NT) return ss_fail(SS_EARG, "ingest: dense length > 1024");
         jobs.push_back({len_bin(dense_L), n, 0, 0});
     } else {
         if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
-            (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins)))
+            (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins + 1)))
             return rc;
         hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p, g->blkfirst.p);
         hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(1024), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
                            g->split_out.p);
         hipLaunchKernelGGL(k_len_binstart, dim3(1), dim3(1024), 0, s, g->split_out.p);
-        rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, 3 * kLenBins * 8, hipMemcpyDeviceToHost, s),
+        rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, (3 * kLenBins + 1) * 8, hipMemcpyDeviceToHost, s),
                       "ingest split copy");
-        if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest split");
+        if (!rc) rc = ss_check(hipEventRecord(g->ev_split, s), "ingest split event");
+        // the previous chunk took the read-order path: its stride's row encode goes out now, so the
+        // GPU encodes while the host waits for the split (the kernel returns at once when the split's
+        // stride differs; the host then takes the path the split names)
+        if (!rc && g->flat_hint) {
+            const uint32_t S = g->flat_hint;
+            if (!(rc = g->cls_words.ensure(n * S + 2)) && !(rc = g->cls_fps.ensure(n))) {
+                rc = ss_encode_rows_impl(d_buf, d_offs, d_lens, n, S, g->cls_words.p, g->cls_fps.p, g->hll.p,
+                                         g->first_bad.p + kLenBins, s, g->split_out.p + 3 * kLenBins);
+                if (!rc) spec_S = S;
+            }
+        }
+        if (!rc) rc = ss_check(hipEventSynchronize(g->ev_split), "ingest split");
         if (rc) return rc;
         const uint64_t* hh = g->h_split;
+        if (spec_S && hh[3 * kLenBins] != spec_S) spec_S = 0;    // the queued encode did nothing
         for (uint32_t b = 0; b < kLenBins; ++b) {
             const uint64_t m = hh[b];
             if (!m) continue;
@@ -1125,10 +1174,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         }
     }
     const size_t nj = jobs.size();
-    // first-bad slots: one per job, plus nj for the one-pass class encode (a read index)
-    if ((rc = g->first_bad.ensure(nj + 1)) || (rc = g->ovf.ensure(nj + 1))) return rc;
-    if (nj && (rc = ss_check(hipMemsetAsync(g->first_bad.p, 0xFF, (nj + 1) * 8, s), "ingest first_bad reset")))
-        return rc;
+    if ((rc = g->ovf.ensure(nj + 1))) return rc;
     if (nj && (rc = ss_check(hipMemsetAsync(g->ovf.p, 0, (nj + 1) * 8, s), "ingest overflow reset"))) return rc;
     auto live = [&](const Job& jb) { return base + jb.first <= g->bad_index; };   // may still hold the first error
     // ---- the length classes: rows packed (W words + the length) and their distinct keys sketched ----
@@ -1151,6 +1197,9 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     // w1max words (k_encode_rows), no class ranks and no row maps in the encode
     bool flat = fused && w1max <= 6;
     for (const Job& jb : jobs) flat &= jb.bin > 32;
+    if (spec_S && !(flat && w1max == spec_S))
+        return ss_fail(SS_EARG, "ingest: the device's read-order stride disagrees with the host's split");
+    if (!dense_L) g->flat_hint = flat ? w1max : 0u;
     // the stable split into d_order: for the lengths 1..32 (row gathers) and the per-class passes; the
     // fused class encode ranks its rows itself from k_len_binscan's per-block offsets
     bool need_order = !dense_L && (!fused && w1max);
@@ -1181,11 +1230,12 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (flat) {
             // (+2: k_flat_verify's quads load a row's last piece as 16 B, one word past an odd stride)
             if ((rc = g->cls_words.ensure(n * w1max + 2))) return rc;
-            rc = ss_encode_rows_impl(d_buf, d_offs, d_lens, n, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p,
-                                     g->first_bad.p + nj, s);
+            if (!spec_S)      // (else queued behind the split)
+                rc = ss_encode_rows_impl(d_buf, d_offs, d_lens, n, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p,
+                                         g->first_bad.p + kLenBins, s);
         } else if (fused) {                 // one read-order pass, the registers updated in it
             rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->blkhist.p, kSplitBlocks, woff, fpoff, rmap, base,
-                                        kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + nj, s);
+                                        kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + kLenBins, s);
         } else {                            // a class per pass (longer reads, or a dense chunk)
             for (size_t j = 0; j < nj && !rc; ++j) {
                 const Job& jb = jobs[j];
@@ -1193,7 +1243,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 const uint32_t W = jb.bin - kClassBin0;
                 const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
                 rc = ss_encode_class_impl(d_buf, d_offs, d_lens, sel, dense_L, jb.m, W, g->cls_words.p + woff[W],
-                                          g->first_bad.p + j, s);
+                                          g->first_bad.p + jb.bin, s);
                 if (!rc) rc = ss_hll_rows_impl(g->cls_words.p + woff[W], jb.m, W + 1, g->hll.p + ((uint64_t)W << kHllLog), s);
             }
         }
@@ -1239,7 +1289,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 src = g->rows.p;
             }
             if (jb.m >= (1u << 16) && jb.m < (1ull << 31)) (void)ss_counter_reserve(gr.table, jb.m);
-            rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, stride, gr.rows, g->first_bad.p + j, s);
+            rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, stride, gr.rows, g->first_bad.p + jb.bin, s);
         }
         if (rc) return rc;
         hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, s, sel, jb.m, base, gr.rowmap.p + gr.rows);
@@ -1349,21 +1399,23 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     }
     // first-bad words, the class tables' overflow words (the scratch table's last) and the class
     // fingerprint flag back in one sync
+    // (hb: the kLenBins + 1 first-bad words, then ho: the nj + 1 overflow words and the flag)
     uint64_t* hb = g->h_bad;
-    rc = ss_check(hipMemcpyAsync(hb, g->first_bad.p, (nj + 1) * 8, hipMemcpyDeviceToHost, s), "ingest bad copy");
-    if (!rc) rc = ss_check(hipMemcpyAsync(hb + nj + 1, g->ovf.p, (nj + 1) * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
+    uint64_t* ho = hb + kLenBins + 1;
+    rc = ss_check(hipMemcpyAsync(hb, g->first_bad.p, (kLenBins + 1) * 8, hipMemcpyDeviceToHost, s), "ingest bad copy");
+    if (!rc) rc = ss_check(hipMemcpyAsync(ho, g->ovf.p, (nj + 1) * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
     if (!rc && fused && !cls_jobs.empty())
-        rc = ss_check(hipMemcpyAsync(hb + 2 * nj + 2, g->cls_flag.p, 4, hipMemcpyDeviceToHost, s), "ingest flag copy");
+        rc = ss_check(hipMemcpyAsync(ho + nj + 1, g->cls_flag.p, 4, hipMemcpyDeviceToHost, s), "ingest flag copy");
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest chunk");
     if (rc) return rc;
     for (size_t j = 0; j <= nj; ++j) {
-        if (!hb[nj + 1 + j] || (j == nj && !(fused && !cls_jobs.empty()))) continue;
+        if (!ho[j] || (j == nj && !(fused && !cls_jobs.empty()))) continue;
         g->failed = true;
         return ss_fail(SS_EFULL, "ingest: a length class's table ran full (its distinct-key estimate was low); "
                                      "count again with ss_ingest_set_exact");
     }
-    g->pend = pend_now && !(uint32_t)hb[2 * nj + 2];
-    if (fused && !cls_jobs.empty() && (uint32_t)hb[2 * nj + 2]) {
+    g->pend = pend_now && !(uint32_t)ho[nj + 1];
+    if (fused && !cls_jobs.empty() && (uint32_t)ho[nj + 1]) {
         spec_wait(g);                  // (it reads the class tables the exact path now fills)
         // two keys share a fingerprint: the class tables were left untouched, count them exactly
         if (flat) {     // class-ordered rows and their row maps first (the one-pass class encode)
@@ -1373,7 +1425,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 cmap[gr.W1 - 1] = gr.rowmap.p + cls_base[j];
             }
             rc = ss_encode_classes_impl(d_buf, d_offs, d_lens, n, g->blkhist.p, kSplitBlocks, woff, fpoff, cmap, base,
-                                        kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + nj, s);
+                                        kClassBin0, w1max, g->cls_words.p, g->cls_fps.p, g->hll.p, g->first_bad.p + kLenBins, s);
             if (rc) return rc;
         }
         for (size_t j : cls_jobs) {
@@ -1382,17 +1434,17 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 (rc = ss_counter_overflow(gr.table, g->ovf.p + j, s)))
                 return rc;
         }
-        rc = ss_check(hipMemcpyAsync(hb + nj + 1, g->ovf.p, nj * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
+        rc = ss_check(hipMemcpyAsync(ho, g->ovf.p, nj * 8, hipMemcpyDeviceToHost, s), "ingest overflow copy");
         if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest exact classes");
         if (rc) return rc;
         for (size_t j = 0; j < nj; ++j)
-            if (hb[nj + 1 + j]) {
+            if (ho[j]) {
                 g->failed = true;
                 return ss_fail(SS_EFULL, "ingest: a length class's table ran full; count again with ss_ingest_set_exact");
             }
     }
     for (size_t j = 0; j <= nj; ++j) {
-        const uint64_t fb = hb[j];
+        const uint64_t fb = hb[j < nj ? jobs[j].bin : kLenBins];
         if (fb == kNoSlot || (j < nj && base + jobs[j].first > g->bad_index)) continue;
         // a length's insert reports its row (rows are in read order); the class encodes report the read
         const bool by_row = j < nj && !dense_L && jobs[j].bin <= 32;
@@ -1533,7 +1585,7 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
         if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_join[k], hipEventDisableTiming), "ingest event");
     }
     if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming), "ingest event");
-    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_split, 3 * kLenBins * 8, hipHostMallocDefault), "ingest pinned");
+    if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_split, (3 * kLenBins + 1) * 8, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_bad, (3 * kLenBins + 8) * 8, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_hll, (33ull << kHllLog) * 4, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = g->hll.ensure(33ull << kHllLog);
@@ -1544,6 +1596,7 @@ int ss_ingest_create(int device, ss_ingest** h_out) {
         rc = ss_check(hipStreamCreateWithPriority(&g->spec_stream, hipStreamNonBlocking, hi), "ingest spec stream");
     }
     if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_reps, hipEventDisableTiming), "ingest event");
+    if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_split, hipEventDisableTiming), "ingest event");
     if (!rc) rc = ss_check(hipEventCreateWithFlags(&g->ev_spec, hipEventDisableTiming), "ingest event");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_spec, 4 * 8, hipHostMallocDefault), "ingest pinned");
     if (!rc) rc = ss_check(hipHostMalloc((void**)&g->h_gdesc, 8 * sizeof(GDesc), hipHostMallocDefault), "ingest pinned");
@@ -1637,6 +1690,7 @@ int ss_ingest_destroy(ss_ingest* g) {
     if (g->h_gdesc) (void)hipHostFree(g->h_gdesc);
     g->spec_dev.release();
     if (g->ev_reps) (void)hipEventDestroy(g->ev_reps);
+    if (g->ev_split) (void)hipEventDestroy(g->ev_split);
     if (g->ev_spec) (void)hipEventDestroy(g->ev_spec);
     if (g->spec_stream) (void)hipStreamDestroy(g->spec_stream);
     for (int k = 0; k < ss_ingest::kSide; ++k) {
@@ -1921,7 +1975,7 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     // (it becomes the word offsets below)
     hipLaunchKernelGGL((k_scan_count<0>), dim3(kScanBlocks), dim3(256), 0, s, g->slot.p, NB, (const GDesc*)g->gdesc.p,
                        g->scan.p);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<0>), dim3(kScanBlocks), dim3(256), 0, s, g->slot.p, NB, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p);
     for (size_t q = 0; q < placed.size(); ++q)
@@ -1933,7 +1987,7 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     // word offsets of the ordered entries
     hipLaunchKernelGGL((k_scan_count<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->scan.p);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, g->scan.p);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g->scan.p);
     hipLaunchKernelGGL((k_scan_apply<1>), dim3(kScanBlocks), dim3(256), 0, s, g->ordered.p, K, (const GDesc*)g->gdesc.p,
                        g->scan.p, g->woff.p);
     if (K >= (1ull << 31) * 256) return ss_fail(SS_EARG, "ingest: too many distinct keys for one gather");

@@ -28,9 +28,11 @@ extern "C" int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_of
 // d_out + r * S (its W words, its length, zeros), its fingerprint (words_fp over W + 1 words) at
 // d_fps[r], its class's HyperLogLog registers updated; a read that is not a class read (empty) gets a
 // zero row and words_fp of one zero word.  *d_first_bad (not reset) = min read with a rejected byte.
+// d_gate (or null): the kernel does nothing unless *d_gate == S when it runs (an encode queued before
+// the host has seen the length split).
 extern "C" int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
                                    uint32_t S, uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll,
-                                   uint64_t* d_first_bad, void* stream);
+                                   uint64_t* d_first_bad, void* stream, const uint64_t* d_gate = nullptr);
 // Single-word keys already computed on the device (d_keys[n], any 64-bit values): counted with the
 // optimistic partitioned insert (12-B records, LDS aggregation) -- e.g. the class rows' fingerprints.
 extern "C" int ss_counter_insert_keys(ss_counter* c, const uint64_t* d_keys, uint64_t n, uint64_t base_index,
