@@ -582,6 +582,92 @@ __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict_
     }
 }
 
+// The speculative finish's gather, run beside the verify: kGatherWaves waves in all (a short grid),
+// each over chunks of 64 ordered entries on its own (no block barriers; its words staged in its own
+// LDS window), the next chunk's entries loaded before the current one's stores.  The rows reach the
+// pinned buffer at the PCIe rate from few waves, and the verify keeps the chip: a 50-MB store into
+// pinned memory beside a verify-shaped kernel held it 0.94 -> 1.64 ms from 4096 blocks, 1.03 ms from
+// 64 at the same ~52 GB/s (tools/probe_overlap.hip).
+constexpr uint32_t kGatherBlocks = 64, kGatherWin = 1024;
+constexpr uint64_t kGatherWavesMax = 4ull << 20;     // entries (bound) up to which the speculative finish uses it
+__global__ __launch_bounds__(256) void k_gather_host_waves(const uint64_t* __restrict__ ordered, uint64_t K,
+                                                           const GDesc* __restrict__ gd, const uint64_t* __restrict__ woff,
+                                                           uint64_t empty_count, OutLayout o) {
+    __shared__ uint64_t buf[4][kGatherWin];
+    const uint32_t cw = o.wide ? 8u : 4u, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint64_t co, wo0;
+    const uint64_t Kd = *o.dK;              // (K: the ordered buffer's bound)
+    results_layout(Kd, o.compact, cw, co, wo0);
+    if (Kd > K || wo0 + *o.dNW * 8 > o.hcap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(o.bad, 1ull);
+        return;
+    }
+    K = Kd;
+    uint8_t* h_cnt = o.hbase + co;
+    uint64_t* h_words = (uint64_t*)(o.hbase + wo0);
+    uint64_t* wb = buf[wave];
+    const uint64_t nchunk = (K + 63) / 64, cstride = (uint64_t)gridDim.x * 4;
+    uint64_t c = (uint64_t)blockIdx.x * 4 + wave;
+    uint64_t v = 0, wo = 0;
+    if (c < nchunk) {
+        const uint64_t k = min(c * 64 + lane, K - 1);
+        v = ordered[k];
+        wo = woff[k];
+    }
+    for (; c < nchunk; c += cstride) {
+        const uint64_t k0 = c * 64, k = k0 + lane;
+        const bool live = k < K;
+        const uint64_t cv = v, cwo = wo;
+        if (c + cstride < nchunk) {         // the next chunk's entries in flight behind this one
+            const uint64_t kn = min((c + cstride) * 64 + lane, K - 1);
+            v = ordered[kn];
+            wo = woff[kn];
+        }
+        uint32_t L = 0, nw = 0;
+        uint64_t cnt = 0;
+        const uint64_t* src = nullptr;
+        if (live) {
+            const uint32_t g = (uint32_t)(cv >> 32);
+            if (g == kEmptyGroup) {
+                cnt = empty_count;
+            } else {
+                const uint64_t e = (uint32_t)cv;
+                const GDesc d = gd[g];
+                L = entry_len(d, e);
+                nw = d.L ? d.W : (L + 31) / 32;
+                cnt = d.counts[e];
+                src = d.words + e * d.W;
+            }
+            if (o.compact) {
+                ((uint16_t*)o.hbase)[k] = (uint16_t)L;
+                if (cw == 4) ((uint32_t*)h_cnt)[k] = (uint32_t)cnt;
+                else ((uint64_t*)h_cnt)[k] = cnt;
+            } else {
+                ((uint32_t*)o.hbase)[k] = L;
+                ((uint64_t*)h_cnt)[k] = cnt;
+            }
+        }
+        // the chunk's words are one run of the output: [lane 0's offset, the last live lane's end)
+        const uint32_t last = (uint32_t)min((uint64_t)63, K - 1 - k0);
+        const uint64_t lo = (uint64_t)__shfl((long long)cwo, 0);
+        const uint64_t hi = (uint64_t)__shfl((long long)(cwo + nw), (int)last);
+        for (uint64_t c0 = lo; c0 < hi; c0 += kGatherWin) {     // one window unless the chunk's rows are long
+            const uint64_t c1 = min(hi, c0 + kGatherWin);
+            for (uint32_t q = 0; q < nw; ++q) {
+                const uint64_t oo = cwo + q;
+                if (oo >= c0 && oo < c1) wb[oo - c0] = src[q];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint64_t oo = c0 + lane; oo < c1; oo += 64) h_words[oo] = wb[oo - c0];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+}
+
 // the speculative finish's entry total: the classes' extracted counts (tot[2 .. 5]) + the empty read's
 // entry; out[1] = the words total (the word scan's), out[2] = its bad flag folded with the extract's
 // capacity overflow -- then one D2H copy of out[0 .. 2]
@@ -1081,8 +1167,14 @@ int spec_launch(ss_ingest* g, const uint64_t* need, uint64_t N) {
     g->wide = results_wide(g);
     OutLayout ol{g->out_host.p, g->out_host.cap, sd + 6, g->scan.p + kScanBlocks, 0, (unsigned long long*)(sd + 7),
                  g->compact, g->wide ? 1 : 0};
-    hipLaunchKernelGGL(k_gather_host, dim3((unsigned)((k_ub + 255) / 256)), dim3(256), 0, ss, g->ordered.p, k_ub,
-                       (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, ol);
+    // up to a few million entries the rows take about as long as the verify beside them: few waves,
+    // and the verify keeps the chip; past that the gather is the call's bound and takes the full grid
+    if (k_ub <= kGatherWavesMax)
+        hipLaunchKernelGGL(k_gather_host_waves, dim3(kGatherBlocks), dim3(256), 0, ss, g->ordered.p, k_ub,
+                           (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, ol);
+    else
+        hipLaunchKernelGGL(k_gather_host, dim3((unsigned)((k_ub + 255) / 256)), dim3(256), 0, ss, g->ordered.p, k_ub,
+                           (const GDesc*)g->gdesc.p, g->woff.p, g->empty_count, ol);
     hipLaunchKernelGGL(k_spec_total, dim3(1), dim3(64), 0, ss, sd, g->empty_count ? 1ull : 0ull,
                        (const uint64_t*)(g->scan.p + kScanBlocks), g->empty_count);
     rc = ss_check(hipMemcpyAsync(g->h_spec, sd + 9, 4 * 8, hipMemcpyDeviceToHost, ss), "spec sizes");
