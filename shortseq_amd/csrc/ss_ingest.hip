@@ -44,6 +44,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <atomic>
 #include <map>
@@ -924,12 +925,20 @@ int table_size(ss_ingest* g, ss_counter* t, uint64_t* out) {
 // HyperLogLog estimate of the distinct keys behind 2^kHllLog registers (Flajolet et al. 2007, with
 // linear counting below 2.5 m)
 double hll_estimate(const uint32_t* reg) {
+    // 2^-k from a table: the estimate sits between the encode and the inserts it sizes, and 2048
+    // ldexp calls per class were ~40 us of host time there (a register is <= 64 - kHllLog + 1)
+    static const auto pw = [] {
+        std::array<double, 66> t{};
+        for (int k = 0; k < 66; ++k) t[k] = std::ldexp(1.0, -k);
+        return t;
+    }();
     const double m = (double)(1u << kHllLog);
     double sum = 0;
     uint32_t zeros = 0;
     for (uint32_t j = 0; j < (1u << kHllLog); ++j) {
-        sum += std::ldexp(1.0, -(int)reg[j]);
-        zeros += reg[j] == 0;
+        const uint32_t r = std::min<uint32_t>(reg[j], 65u);
+        sum += pw[r];
+        zeros += r == 0;
     }
     double e = 0.7213 / (1.0 + 1.079 / m) * m * m / sum;
     if (e <= 2.5 * m && zeros) e = m * std::log(m / (double)zeros);
@@ -1225,26 +1234,41 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins + 1)))
             return rc;
+        // (the side stream's speculative encode below starts behind everything queued so far, not behind the split)
+        const bool spec_enc = g->flat_hint != 0;
+        if (spec_enc) rc = ss_check(hipEventRecord(g->ev_fork, s), "ingest fork");
         hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p, g->blkfirst.p);
         hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(1024), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
                            g->split_out.p);
         hipLaunchKernelGGL(k_len_binstart, dim3(1), dim3(1024), 0, s, g->split_out.p);
-        rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, (3 * kLenBins + 1) * 8, hipMemcpyDeviceToHost, s),
-                      "ingest split copy");
+        if (!rc) rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, (3 * kLenBins + 1) * 8, hipMemcpyDeviceToHost, s),
+                               "ingest split copy");
         if (!rc) rc = ss_check(hipEventRecord(g->ev_split, s), "ingest split event");
-        // the previous chunk took the read-order path: its stride's row encode goes out now, so the
-        // GPU encodes while the host waits for the split (the kernel returns at once when the split's
-        // stride differs; the host then takes the path the split names)
-        if (!rc && g->flat_hint) {
+        // the previous chunk took the read-order path: its stride's row encode goes out now on a side
+        // stream, beside the split, so the GPU encodes while the split runs and the host waits for it.
+        // When the split names another path the rows and fingerprints are rewritten by that path; the
+        // sketch registers and the class first-bad word it touched are harmless: it sketches only class
+        // reads of < S words, by the fingerprint every class path sketches them by (a max register:
+        // a subset of the same updates), and reports only rejected class reads, which every path reports
+        bool joined = false;
+        if (!rc && spec_enc) {
             const uint32_t S = g->flat_hint;
-            if (!(rc = g->cls_words.ensure(n * S + 2)) && !(rc = g->cls_fps.ensure(n))) {
+            if (!(rc = g->cls_words.ensure(n * S + 2)) && !(rc = g->cls_fps.ensure(n)) &&
+                !(rc = ss_check(hipStreamWaitEvent(g->side[0], g->ev_fork, 0), "ingest fork wait"))) {
                 rc = ss_encode_rows_impl(d_buf, d_offs, d_lens, n, S, g->cls_words.p, g->cls_fps.p, g->hll.p,
-                                         g->first_bad.p + kLenBins, s, g->split_out.p + 3 * kLenBins);
+                                         g->first_bad.p + kLenBins, g->side[0], nullptr);
+                if (!rc) rc = ss_check(hipEventRecord(g->ev_join[0], g->side[0]), "ingest spec encode join");
+                // everything queued on the stream from here on runs behind the encode
+                if (!rc) rc = ss_check(hipStreamWaitEvent(s, g->ev_join[0], 0), "ingest spec encode wait");
+                joined = !rc;
                 if (!rc) spec_S = S;
             }
         }
         if (!rc) rc = ss_check(hipEventSynchronize(g->ev_split), "ingest split");
-        if (rc) return rc;
+        if (rc) {
+            if (spec_enc && !joined) (void)hipStreamSynchronize(g->side[0]);   // nothing left writing the buffers
+            return rc;
+        }
         const uint64_t* hh = g->h_split;
         if (spec_S && hh[3 * kLenBins] != spec_S) spec_S = 0;    // the queued encode did nothing
         for (uint32_t b = 0; b < kLenBins; ++b) {
