@@ -3056,21 +3056,51 @@ static hipError_t set_u64(uint64_t* p, bool ones, hipStream_t s) {
     return hipMemsetAsync(p, ones ? 0xFF : 0, sizeof(uint64_t), s);
 }
 
-int ss_counter_reset(ss_counter* c, void* stream) {
+// the host half of a reset; the three device words it needs set go to p / v
+int ss_counter_reset_host(ss_counter* c, unsigned long long** p, unsigned long long* v) {
     if (!c) return ss_fail(SS_EARG, "null counter");
-    hipStream_t s = (hipStream_t)stream;
     c->L = -1;
     c->occ_src = 0;
     c->reset_pending = true;    // the slots [0, cap): flush_reset or a fresh aggregate
     unsigned long long* sent = (unsigned long long*)(c->slots + c->cap);     // the sentinel slot
+    p[0] = sent;
+    v[0] = ~0ull;
+    p[1] = sent + 1;
+    v[1] = ~0ull;
+    p[2] = c->work;                                                          // overflow flags
+    v[2] = 0ull;
+    return SS_OK;
+}
+
+int ss_counter_reset(ss_counter* c, void* stream) {
     PrepWords w{};
-    w.p[0] = sent;
-    w.v[0] = ~0ull;
-    w.p[1] = sent + 1;
-    w.v[1] = ~0ull;
-    w.p[2] = c->work;                                                        // overflow flags
-    w.v[2] = 0ull;
-    return ss_check(launch_prep(w, s), "ss_counter_reset");
+    const int rc = ss_counter_reset_host(c, w.p, w.v);
+    if (rc) return rc;
+    return ss_check(launch_prep(w, (hipStream_t)stream), "ss_counter_reset");
+}
+
+// Several tables' reset words in one dispatch (the drop-in engine resets up to six tables between
+// two kernels of a chunk; one launch each left ~5 us of command-processor gap between them)
+struct PrepMany {
+    unsigned long long* p[kPrepMany];
+    unsigned long long v[kPrepMany];
+    uint32_t n;
+};
+__global__ __launch_bounds__(64) void k_prep_many(PrepMany w) {
+    if (threadIdx.x < w.n) *w.p[threadIdx.x] = w.v[threadIdx.x];
+}
+
+int ss_prep_words(unsigned long long* const* p, const unsigned long long* v, uint32_t n, void* stream) {
+    if (n > kPrepMany) return ss_fail(SS_EARG, "ss_prep_words: too many words");
+    if (!n) return SS_OK;
+    PrepMany w{};
+    for (uint32_t i = 0; i < n; ++i) {
+        w.p[i] = p[i];
+        w.v[i] = v[i];
+    }
+    w.n = n;
+    hipLaunchKernelGGL(k_prep_many, dim3(1), dim3(64), 0, (hipStream_t)stream, w);
+    return ss_check(hipGetLastError(), "ss_prep_words");
 }
 
 uint64_t ss_counter_capacity(const ss_counter* c) { return c ? c->cap : 0; }

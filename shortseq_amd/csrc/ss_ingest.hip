@@ -801,8 +801,13 @@ struct ss_ingest {
     DBuf<uint64_t> split_out;      // [3 * kLenBins + 1]: totals, first reads, starts, the read-order stride
     uint64_t* h_split = nullptr;   // pinned copy
     // the previous chunk's read-order stride (0: it took another path): the next chunk's row encode is
-    // queued at that stride before its split comes back, gated on the device by the split's own stride
+    // queued at that stride beside its split, on a side stream (process_chunk)
     uint32_t flat_hint = 0;
+    // process_chunk: pooled tables taken for new groups have their reset words queued here and set in
+    // one dispatch (flush_prep) before any of them is used, not one launch per table
+    bool defer_prep = false;
+    std::vector<unsigned long long*> prep_p;
+    std::vector<unsigned long long> prep_v;
     hipEvent_t ev_split = nullptr;
     DBuf<uint8_t> rows;            // gathered dense rows (lengths <= 32)
     DBuf<uint64_t> cls_words;      // the length classes' packed rows (k_encode_classes / k_encode_class)
@@ -888,9 +893,27 @@ int table_get(ss_ingest* g, uint64_t cap, uint32_t W1, uint64_t rows, ss_counter
     if (best < g->pool.size()) {
         *out = g->pool[best].second;
         g->pool.erase(g->pool.begin() + (long)best);
-        return ss_counter_reset(*out, g->stream);
+        if (!g->defer_prep) return ss_counter_reset(*out, g->stream);
+        unsigned long long* p[3];
+        unsigned long long v[3];
+        const int rc = ss_counter_reset_host(*out, p, v);
+        g->prep_p.insert(g->prep_p.end(), p, p + 3);
+        g->prep_v.insert(g->prep_v.end(), v, v + 3);
+        return rc;
     }
     return ss_counter_create(cap, out);
+}
+
+// the queued reset words in one dispatch on the engine's stream (or several, past kPrepMany words)
+int flush_prep(ss_ingest* g) {
+    int rc = SS_OK;
+    for (size_t i = 0; i < g->prep_p.size() && !rc; i += kPrepMany) {
+        const uint32_t k = (uint32_t)std::min<size_t>(kPrepMany, g->prep_p.size() - i);
+        rc = ss_prep_words(g->prep_p.data() + i, g->prep_v.data() + i, k, g->stream);
+    }
+    g->prep_p.clear();
+    g->prep_v.clear();
+    return rc;
 }
 
 // device bytes a pooled table holds: its slots and its partition workspace (~100 B per reserved read)
@@ -1040,7 +1063,11 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
     if (need <= gr.cap / 2) return SS_OK;
     const uint64_t ncap = pow2_at_least(2 * need);
     ss_counter* nt = nullptr;
-    if ((rc = table_get(g, ncap, gr.W1, m, &nt)) != SS_OK) return rc;
+    const bool defer = g->defer_prep;     // (merged into at once: its reset goes out now)
+    g->defer_prep = false;
+    rc = table_get(g, ncap, gr.W1, m, &nt);
+    g->defer_prep = defer;
+    if (rc != SS_OK) return rc;
     if ((rc = table_kind(gr, nt)) != SS_OK) return rc;
     const uint64_t cap = gr.cap + 1;
     const uint32_t W = gr.W1;
@@ -1379,6 +1406,16 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         }
     }
     std::vector<size_t> cls_jobs;
+    // new groups' pooled tables: their resets queued (table_get) and set in one dispatch below, before
+    // the first insert; whatever is still queued goes out when this function returns
+    g->defer_prep = true;
+    struct PrepScope {
+        ss_ingest* g;
+        ~PrepScope() {
+            g->defer_prep = false;
+            if (!g->prep_p.empty()) (void)flush_prep(g);
+        }
+    } prep_scope{g};
     for (size_t j = 0; j < nj; ++j) {
         const Job& jb = jobs[j];
         const bool cls = jb.bin > 32;
@@ -1404,6 +1441,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 if ((rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.bin, g->rows.p, stride, s))) return rc;
                 src = g->rows.p;
             }
+            if ((rc = flush_prep(g))) return rc;
             if (jb.m >= (1u << 16) && jb.m < (1ull << 31)) (void)ss_counter_reserve(gr.table, jb.m);
             rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, stride, gr.rows, g->first_bad.p + jb.bin, s);
         }
@@ -1411,8 +1449,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, s, sel, jb.m, base, gr.rowmap.p + gr.rows);
         gr.rows += jb.m;
     }
+    g->defer_prep = false;
     std::vector<uint64_t> cls_base(nj, 0);     // each class job's first table row (the exact redo)
     bool pend_now = false;                     // this chunk's fold deferred (set below)
+    if (!(!cls_jobs.empty() && fused) && (rc = flush_prep(g))) return rc;
     if (!cls_jobs.empty() && fused) {
         // the classes' rows counted by fingerprint in one scratch table, checked against their
         // fingerprints' first rows and folded into the class tables (ss_classes_verify_fold); a
@@ -1442,7 +1482,14 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             g->fpt = nullptr;
         }
         if (!g->fpt && (rc = ss_counter_create(fcap, &g->fpt))) return rc;
-        if ((rc = ss_counter_reset(g->fpt, s))) return rc;
+        {   // the scratch table's reset with the class tables' queued ones, one dispatch
+            unsigned long long* p[3];
+            unsigned long long v[3];
+            if ((rc = ss_counter_reset_host(g->fpt, p, v))) return rc;
+            g->prep_p.insert(g->prep_p.end(), p, p + 3);
+            g->prep_v.insert(g->prep_v.end(), v, v + 3);
+            if ((rc = flush_prep(g))) return rc;
+        }
         if ((rc = g->cls_flag.ensure(1))) return rc;
         // (sizing mode 3, a test hook: the flag starts raised, as if two keys shared a fingerprint)
         rc = ss_check(hipMemsetAsync(g->cls_flag.p, g->sizing == 3 ? 1 : 0, 4, s), "ingest class flag reset");

@@ -19,6 +19,12 @@ extern "C" int ss_encode_fixed_impl(const uint8_t* d_ascii, uint64_t n, uint32_t
 // h_rmap[W][row] when h_rmap[W] is given, and the classes' HyperLogLog registers d_hll[W << kHllLog
 // ...] (u32, max-updated; zeroed by the caller).
 constexpr uint32_t kHllLog = 11;
+// ss_counter_reset in two halves: the host state now, its three device words (p[0..2] = v[0..2])
+// queued later, several tables' words in one ss_prep_words dispatch (n <= kPrepMany), before any use
+// of the tables on that stream
+constexpr uint32_t kPrepMany = 32;
+extern "C" int ss_counter_reset_host(ss_counter* c, unsigned long long** p, unsigned long long* v);
+extern "C" int ss_prep_words(unsigned long long* const* p, const unsigned long long* v, uint32_t n, void* stream);
 extern "C" int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
                                       const uint32_t* d_blkoff, uint32_t nblk, const uint64_t* h_woff,
                                       const uint64_t* h_fpoff, uint64_t* const* h_rmap, uint64_t base, uint32_t bin0,
