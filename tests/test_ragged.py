@@ -193,6 +193,41 @@ def test_device_ingest_row_widths(gpu, oracle, lo, hi):
     assert gw.tolist() == [int(x) for (w, L, _c, _f) in exp for x in w[:(L + 31) // 32]]
 
 
+def test_device_ingest_stride_guess_changes(gpu, oracle):
+    """One engine over chunks whose read-order stride changes from chunk to chunk: each chunk's row
+    encode is queued at the previous chunk's stride beside its length split, so every kind of wrong
+    guess is taken -- a narrower and a wider stride, a chunk past 160 nt and one mixed with <= 32-nt
+    reads (both off the read-order path), and the first read-order chunk after those.  The results
+    after every chunk == oracle.count of all reads so far."""
+    import torch
+    import shortseq_amd.batch as B
+    rng = np.random.default_rng(2024)
+    ranges = [(33, 64), (65, 160), (33, 96), (100, 300), (40, 90), (40, 90), (10, 150), (129, 160), (33, 64)]
+    chunks = []
+    for lo, hi in ranges:
+        pool = ["".join(rng.choice(list("ACGT"), int(L))) for L in rng.integers(lo, hi + 1, 400)]
+        chunks.append([pool[i].encode() for i in rng.integers(0, len(pool), 6_000)])
+    enc = [r for c in chunks for r in c]
+    lens = torch.tensor([len(r) for r in enc], dtype=torch.int32)
+    offs = torch.zeros(len(enc), dtype=torch.int64)
+    offs[1:] = torch.cumsum(lens.to(torch.int64), 0)[:-1]
+    blob = torch.frombuffer(bytearray(b"".join(enc) + b"\0" * 16), dtype=torch.uint8).to(gpu)
+    offs, lens = offs.to(gpu), lens.to(gpu)
+    eng = B.DeviceIngest(gpu)
+    try:
+        at = 0
+        for c in chunks:
+            eng.count(blob, offs[at:at + len(c)], lens[at:at + len(c)])
+            at += len(c)
+            gl, gc, gw = eng.results()
+            exp = oracle.count(enc[:at])
+            assert gl.tolist() == [L for (_w, L, _c, _f) in exp], at
+            assert gc.tolist() == [c for (_w, _L, c, _f) in exp], at
+            assert gw.tolist() == [int(x) for (w, L, _c, _f) in exp for x in w[:(L + 31) // 32]], at
+    finally:
+        eng.close()
+
+
 def test_device_ingest_read_order_rows_error(gpu):
     """A rejected byte inside a read of a read-order chunk raises the reference's message for the
     first such read."""
