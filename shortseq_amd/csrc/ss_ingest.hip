@@ -801,8 +801,9 @@ struct ss_ingest {
     DBuf<uint64_t> split_out;      // [3 * kLenBins + 1]: totals, first reads, starts, the read-order stride
     uint64_t* h_split = nullptr;   // pinned copy
     // the previous chunk's read-order stride (0: it took another path): the next chunk's row encode is
-    // queued at that stride beside its split, on a side stream (process_chunk)
-    uint32_t flat_hint = 0;
+    // queued at that stride before its split comes back (process_chunk); flat_streak = how many chunks
+    // in a row took the read-order path at that stride
+    uint32_t flat_hint = 0, flat_streak = 0;
     // process_chunk: pooled tables taken for new groups have their reset words queued here and set in
     // one dispatch (flush_prep) before any of them is used, not one launch per table
     bool defer_prep = false;
@@ -1262,7 +1263,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins + 1)))
             return rc;
         // (the side stream's speculative encode below starts behind everything queued so far, not behind the split)
-        const bool spec_enc = g->flat_hint != 0;
+        const bool spec_enc = g->flat_hint != 0 && g->flat_streak >= 2;
         if (spec_enc) rc = ss_check(hipEventRecord(g->ev_fork, s), "ingest fork");
         hipLaunchKernelGGL(k_len_count, dim3(kSplitBlocks), dim3(64), 0, s, d_lens, n, g->blkhist.p, g->blkfirst.p);
         hipLaunchKernelGGL(k_len_binscan, dim3(kLenBins), dim3(1024), 0, s, kSplitBlocks, g->blkhist.p, g->blkfirst.p,
@@ -1271,12 +1272,23 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (!rc) rc = ss_check(hipMemcpyAsync(g->h_split, g->split_out.p, (3 * kLenBins + 1) * 8, hipMemcpyDeviceToHost, s),
                                "ingest split copy");
         if (!rc) rc = ss_check(hipEventRecord(g->ev_split, s), "ingest split event");
-        // the previous chunk took the read-order path: its stride's row encode goes out now on a side
-        // stream, beside the split, so the GPU encodes while the split runs and the host waits for it.
-        // When the split names another path the rows and fingerprints are rewritten by that path; the
-        // sketch registers and the class first-bad word it touched are harmless: it sketches only class
-        // reads of < S words, by the fingerprint every class path sketches them by (a max register:
-        // a subset of the same updates), and reports only rejected class reads, which every path reports
+        // The previous chunks took the read-order path: its stride's row encode goes out now.  After two
+        // or more chunks at one stride it runs on a side stream beside the split, so the GPU encodes
+        // while the split runs and the host waits for it.  When the split then names another path the
+        // rows and fingerprints are rewritten by that path (the wasted encode is the price of a wrong
+        // guess, hence the streak); the sketch registers and the class first-bad word it touched are
+        // harmless: it sketches only class reads of < S words, by the fingerprint every class path
+        // sketches them by (a max register: a subset of the same updates), and reports only rejected
+        // class reads, which every path reports.  After one chunk it is queued behind the split on the
+        // stream, gated on the device by the split's own stride (a wrong guess returns at once).
+        if (!rc && g->flat_hint && !spec_enc) {
+            const uint32_t S = g->flat_hint;
+            if (!(rc = g->cls_words.ensure(n * S + 2)) && !(rc = g->cls_fps.ensure(n))) {
+                rc = ss_encode_rows_impl(d_buf, d_offs, d_lens, n, S, g->cls_words.p, g->cls_fps.p, g->hll.p,
+                                         g->first_bad.p + kLenBins, s, g->split_out.p + 3 * kLenBins);
+                if (!rc) spec_S = S;
+            }
+        }
         bool joined = false;
         if (!rc && spec_enc) {
             const uint32_t S = g->flat_hint;
@@ -1297,7 +1309,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             return rc;
         }
         const uint64_t* hh = g->h_split;
-        if (spec_S && hh[3 * kLenBins] != spec_S) spec_S = 0;    // the queued encode did nothing
+        if (spec_S && hh[3 * kLenBins] != spec_S) spec_S = 0;    // the queued encode did nothing (or is rewritten)
         for (uint32_t b = 0; b < kLenBins; ++b) {
             const uint64_t m = hh[b];
             if (!m) continue;
@@ -1342,7 +1354,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     for (const Job& jb : jobs) flat &= jb.bin > 32;
     if (spec_S && !(flat && w1max == spec_S))
         return ss_fail(SS_EARG, "ingest: the device's read-order stride disagrees with the host's split");
-    if (!dense_L) g->flat_hint = flat ? w1max : 0u;
+    if (!dense_L) {
+        g->flat_streak = flat ? (w1max == g->flat_hint ? g->flat_streak + 1 : 1u) : 0u;
+        g->flat_hint = flat ? w1max : 0u;
+    }
     // the stable split into d_order: for the lengths 1..32 (row gathers) and the per-class passes; the
     // fused class encode ranks its rows itself from k_len_binscan's per-block offsets
     bool need_order = !dense_L && (!fused && w1max);

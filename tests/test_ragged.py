@@ -197,16 +197,20 @@ def test_device_ingest_stride_guess_changes(gpu, oracle):
     """One engine over chunks whose read-order stride changes from chunk to chunk: each chunk's row
     encode is queued at the previous chunk's stride beside its length split, so every kind of wrong
     guess is taken -- a narrower and a wider stride, a chunk past 160 nt and one mixed with <= 32-nt
-    reads (both off the read-order path), and the first read-order chunk after those.  The results
-    after every chunk == oracle.count of all reads so far."""
+    reads (both off the read-order path), and the first read-order chunk after those -- both as the
+    side-stream encode and as the gated one.  The results after every chunk == oracle.count of all
+    reads so far."""
     import torch
     import shortseq_amd.batch as B
     rng = np.random.default_rng(2024)
-    ranges = [(33, 64), (65, 160), (33, 96), (100, 300), (40, 90), (40, 90), (10, 150), (129, 160), (33, 64)]
+    # (after two chunks at one stride the guess runs on a side stream, after one it is gated on the
+    # device: both kinds are taken wrong below)
+    ranges = [(33, 64), (65, 160), (33, 96), (100, 300), (40, 90), (40, 90), (40, 90), (10, 150), (129, 160),
+              (129, 160), (129, 160), (33, 64), (33, 64), (33, 64), (65, 160), (65, 160), (100, 300), (33, 64)]
     chunks = []
     for lo, hi in ranges:
         pool = ["".join(rng.choice(list("ACGT"), int(L))) for L in rng.integers(lo, hi + 1, 400)]
-        chunks.append([pool[i].encode() for i in rng.integers(0, len(pool), 6_000)])
+        chunks.append([pool[i].encode() for i in rng.integers(0, len(pool), 4_000)])
     enc = [r for c in chunks for r in c]
     lens = torch.tensor([len(r) for r in enc], dtype=torch.int32)
     offs = torch.zeros(len(enc), dtype=torch.int64)
