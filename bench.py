@@ -368,6 +368,7 @@ def bench_exchange(B, dev, n=125_000_000, U=1 << 24, owners=8, reps=5):
     for r in range(reps + 1):
         # as in the job, the pack follows an insert, whose aggregate leaves the regions' occupancy
         # fresh (after a merge it is stale and the pack would first recount it: k_region_occ, ~0.1 ms)
+        gc.reset()            # (as ShardedCounter.count: a fresh table per count)
         gc.insert(ascii, 32, check_errors=False)
         ev[0].record()
         rec, parts = gc.pack_ranges(owners, skip=0)

@@ -154,9 +154,11 @@ int ss_hamming_all_pairs(const uint64_t* d_words, uint64_t n, uint32_t L, uint32
  * TILES: every pair checked (MFMA one-hot tiles for L <= 128, bit-plane tiles above).
  * PIGEONHOLE (L <= 32, max_dist < 16): the min(L + 1, 32) positions split into max_dist + 1
  *   segments; only pairs with an equal segment are checked (bucketed per segment on the device).
- *   Blocks the calling thread once on the stream (the candidate totals are read back).
+ *   Blocks the calling thread once on the stream (the candidate totals are read back) only in AUTO;
+ *   forced, it queues everything.  Its scratch lives on the device that holds d_words.
  * AUTO: PIGEONHOLE when L <= 32, segments >= 3 nt, n >= 32768 and the bucket histogram shows fewer
- *   than 1/64 of all pairs as candidates; TILES otherwise. */
+ *   than 1/16 of all pairs as candidates; TILES otherwise.  A stream under hipGraph capture always
+ *   gets TILES in AUTO (no allocation, no host read-back: the call stays capturable). */
 #define SS_ALLPAIRS_AUTO 0u
 #define SS_ALLPAIRS_TILES 1u
 #define SS_ALLPAIRS_PIGEONHOLE 2u
@@ -172,7 +174,13 @@ int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uin
  * L <= 32: the slot key is the packed word.  L > 32: W = ceil(L/32) words per key, kept beside the
  * slots; the slot holds a 64-bit fingerprint of the words and equality is decided on the words.
  * A slot is 16 B (key u64, count u32, first index u32): global read indices of one handle stay below
- * 2^32 - 1 (inserts past that return SS_EARG) and a key counts at most 2^32 - 1 copies.
+ * 2^32 - 1 (inserts past that return SS_EARG).  Counts are u64 (ShortSeqCounter's are Python ints,
+ * counter.pyx:53): before the reads inserted since the last spill could wrap a slot's u32, every
+ * count moves into a per-slot u64 array (allocated then, 8 B per slot) and ss_counter_merge /
+ * _merge_words carry past 32 bits into it; extracts return the sum.  The packed exchange records
+ * (ss_counter_pack_ranges) carry u32 counts and flag bit 2 for a count past that.  Packed-word
+ * handles (ss_counter_set_words) keep u32 slot counts: the drop-in engine that keys them spills
+ * their counts per row itself (its per-row u64 counts).
  * ---------------------------------------------------------------------------------------------- */
 typedef struct ss_counter ss_counter;
 
@@ -212,6 +220,10 @@ int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_le
  * replaces no reference interface (the reference's dict grows by itself, counter.pyx:41-54). */
 int ss_counter_merge_words(ss_counter* c, const uint64_t* d_words, const uint64_t* d_counts,
                            const uint64_t* d_first, uint64_t m, void* stream);
+
+/* Test hook: spill the u32 slot counts into the u64 array once more than `reads` (1 .. 2^32 - 1,
+ * default 2^32 - 1) reads were inserted since the last spill.  New in this ABI version. */
+int ss_counter_set_spill_limit(ss_counter* c, uint64_t reads);
 
 /* Fix the key length of an empty handle (also done by the first insert); -1 from ss_counter_length
  * means not fixed yet, -2 a packed-word handle (ss_counter_set_words). */
@@ -376,8 +388,11 @@ int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_
  *                       return SS_EFULL, and the caller counts again with exact sizing (the drop-in
  *                       front does).  2 = size them by 1/64 of the sketch (a test hook that makes
  *                       the SS_EFULL path run).  3 = test hook: the classes' fingerprint count takes
- *                       its exact fallback (as if two keys shared a 64-bit fingerprint).  New in this
- *                       ABI version; the reference dict has no sizing.
+ *                       its exact fallback (as if two keys shared a 64-bit fingerprint).  4 = as 3,
+ *                       but found only after the deferred fold and the speculative finish were queued.
+ *                       5 = test hook: the speculative finish's result bound as if the sketch said 0,
+ *                       so it is dropped and the finish runs the ordinary way.  New in this ABI
+ *                       version; the reference dict has no sizing.
  * ---------------------------------------------------------------------------------------------- */
 typedef struct ss_ingest ss_ingest;
 int ss_ingest_create(int device, ss_ingest** h_out);

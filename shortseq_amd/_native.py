@@ -54,6 +54,7 @@ SIGNATURES = [
     ("ss_counter_insert_fixed", C.c_int, [_P, _P, _U64, _U32, _U64, _U64, _P, _P]),
     ("ss_counter_merge", C.c_int, [_P, _P, _P, _P, _P, _U64, _P]),
     ("ss_counter_merge_words", C.c_int, [_P, _P, _P, _P, _U64, _P]),
+    ("ss_counter_set_spill_limit", C.c_int, [_P, _U64]),
     ("ss_counter_set_length", C.c_int, [_P, _U32]),
     ("ss_counter_length", C.c_int, [_P]),
     ("ss_counter_set_words", C.c_int, [_P, _U32]),

@@ -780,6 +780,11 @@ class GpuCounter:
         check(lib().ss_counter_merge(self._h, keys.data_ptr(), None, counts.data_ptr(), first.data_ptr(), m,
                                      _stream(self.device)), "ss_counter_merge")
 
+    def set_spill_limit(self, reads: int) -> None:
+        """Test hook (ss_counter_set_spill_limit): move the u32 slot counts into the u64 array once more
+        than `reads` reads were inserted since the last spill (default 2^32 - 1)."""
+        check(lib().ss_counter_set_spill_limit(self._h, int(reads)), "ss_counter_set_spill_limit")
+
     def size(self) -> int:
         check(lib().ss_counter_size(self._h, self._scratch.data_ptr(), _stream(self.device)), "ss_counter_size")
         return int(self._scratch[0].item())

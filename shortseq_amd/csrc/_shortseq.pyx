@@ -748,14 +748,14 @@ cdef _reduce_fill(ShortSeqCounter self, list engines, list bases):
                 _merge_pair(<size_t>engines[0][1], <size_t>engines[k][1], bases[k], False)
         else:
             # every destination sized once for the union of the engines it will absorb (a absorbs
-            # a + 1 .. a + lowbit(a) - 1; engine 0 all others), each on its own device
-            res = []
+            # a + 1 .. a + lowbit(a) - 1; engine 0 all others).  One after another: a reserve reads
+            # its sources' bin maps while another destination's reserve may add bins to them
+            # (ADVICE r5: concurrent reserves raced on a std::map); they are cheap next to the merges
             for a in range(0, D, 2):
                 span = (a & -a) if a else D
                 srcs = [<size_t>engines[b][1] for b in range(a + 1, min(D, a + span))]
                 if srcs:
-                    res.append((<size_t>engines[a][1], srcs))
-            _run_parallel(_reserve_merge, res)
+                    _reserve_merge(<size_t>engines[a][1], srcs)
             step = 1
             while step < D:
                 pairs = [(a, a + step) for a in range(0, D, 2 * step) if a + step < D]

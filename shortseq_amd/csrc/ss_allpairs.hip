@@ -764,10 +764,26 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
         if (2 * len <= a.nbmax) a.exact |= 1u << g;
         pos += len;
     }
-    int dev = 0;
-    int rc = ss_check(hipGetDevice(&dev), "hipGetDevice");
+    // the scratch, its event and the pinned totals belong to the device that holds the words (the
+    // kernels run there, on the caller's stream), not to whichever device is current
+    int cur = 0, dev = 0;
+    int rc = ss_check(hipGetDevice(&cur), "hipGetDevice");
     if (rc) return rc;
+    hipPointerAttribute_t pa{};
+    rc = ss_check(hipPointerGetAttributes(&pa, b.words), "all-pairs: words pointer attributes");
+    if (rc) return rc;
+    dev = pa.device;
     if (dev < 0 || dev >= 64) return ss_fail(SS_EARG, "all-pairs: device index past 63");
+    struct DevGuard {
+        int prev, now;
+        ~DevGuard() {
+            if (prev != now) (void)hipSetDevice(prev);
+        }
+    } guard{cur, dev};
+    if (dev != cur) {
+        rc = ss_check(hipSetDevice(dev), "all-pairs: hipSetDevice");
+        if (rc) return rc;
+    }
     PigScratch& ps = g_pig[dev];
     std::lock_guard<std::mutex> lock(ps.mu);
     const size_t hist_n = (size_t)a.G << a.nbmax, tiles_n = (size_t)a.G * a.maxtiles;
@@ -861,7 +877,17 @@ int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uin
     hipStream_t s = (hipStream_t)stream;
     // the pigeonhole form (tried first when it may apply) zeroes the outputs in its first kernel
     const uint32_t Pw = L + 1 < 32u ? L + 1 : 32u, Gw = max_dist + 1;
-    const bool pig_try = n >= 2 && W == 1 && method != SS_ALLPAIRS_TILES && wpr >= W && d_words &&
+    // AUTO on a stream being captured into a hipGraph stays on the tiles: the pigeonhole decision
+    // allocates and reads the candidate totals back (a host sync), neither of which a capture allows
+    // (the entry point was capturable before AUTO existed)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (method == SS_ALLPAIRS_AUTO && hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        cap = hipStreamCaptureStatusNone;
+    }
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    const bool pig_try = n >= 2 && W == 1 && method != SS_ALLPAIRS_TILES && !(capturing && method == SS_ALLPAIRS_AUTO) &&
+                         wpr >= W && d_words &&
                          (method == SS_ALLPAIRS_PIGEONHOLE ? Gw <= (uint32_t)kPigMaxG
                                                            : Gw <= (uint32_t)kPigMaxG && Pw / Gw >= 3 && n >= (1u << 15));
     int rc = SS_OK;

@@ -98,12 +98,22 @@ struct ss_counter {
     uint32_t thead = 0, tpend = 0;         // next set, sets recorded and not yet folded
     double tsum[kPassEvents - 1] = {};
     uint64_t tn = 0;
+    // u64 counts: a slot's u32 count is its low part; wide[s] (allocated on first need,
+    // zeroed when it goes live) holds the rest.  Inserts add at most one per read, so before the reads
+    // inserted since the last spill could pass spill_at, every slot's count moves into wide
+    // (k_spill_wide) and the slot restarts at 0 (the sentinel keeps 1); merges carry into wide as they
+    // add.  Nothing reads wide while it is not live (tbl_of passes null), so the C5 insert is unchanged.
+    uint64_t* wide = nullptr;              // [cap + 1]
+    bool wide_live = false;
+    uint64_t since = 0;                    // reads inserted since the last reset / spill (kSinceUnknown after a merge)
+    uint64_t spill_at = 0xFFFFFFFFull;     // ss_counter_set_spill_limit (a test hook lowers it)
 };
 
 namespace {
 
 struct Tbl {
     Slot* slots;
+    uint64_t* wide;       // [cap + 1] high parts of the counts, or null (ss_counter::wide)
     uint64_t* keywords;   // multi-word keys only
     uint32_t* occ;        // [R] used slots per region (written by the single-word aggregate) or null
     uint32_t W;
@@ -133,7 +143,9 @@ __device__ __forceinline__ uint64_t slot_top(const Tbl& t, uint64_t key) {
 
 // Insert / count `cnt` copies of `key` first seen at global read index `idx`.  Returns true when this
 // call claimed a new slot (the spill pass keeps the region occupancy current with it).
-__device__ __forceinline__ bool tbl_add(const Tbl& t, uint64_t key, uint32_t cnt, unsigned long long idx) {
+__device__ __forceinline__ void count_add_wide(const Tbl& t, uint64_t s, uint32_t old_count, uint32_t lo, uint64_t hi);
+__device__ __forceinline__ bool tbl_add(const Tbl& t, uint64_t key, uint64_t cnt64, unsigned long long idx) {
+    const uint32_t cnt = (uint32_t)cnt64;
     bool claimed = false;
     uint64_t s;
     if (key == kEmpty) {
@@ -171,9 +183,21 @@ __device__ __forceinline__ bool tbl_add(const Tbl& t, uint64_t key, uint32_t cnt
         idx = kMaxIndex;
     }
     Slot* sl = &t.slots[s];
-    atomicAdd(&sl->ncount, 0u - cnt);
+    const uint32_t old = atomicAdd(&sl->ncount, 0u - cnt);
+    count_add_wide(t, s, ~old, cnt, cnt64 & ~0xFFFFFFFFull);
     if (sl->first > (uint32_t)idx) atomicMin(&sl->first, (uint32_t)idx);
     return claimed;
+}
+
+// The part of a count add the slot's u32 cannot hold (hi: the added count's high part; the carry out
+// of old_count + lo) goes to wide[s]; without a live wide array such an add flags kOvfField.
+__device__ __forceinline__ void count_add_wide(const Tbl& t, uint64_t s, uint32_t old_count, uint32_t lo, uint64_t hi) {
+    const uint64_t extra = hi + ((((uint64_t)old_count + lo) >> 32) << 32);
+    if (!extra) return;
+    if (t.wide)
+        atomicAdd((unsigned long long*)&t.wide[s], (unsigned long long)extra);
+    else
+        atomicOr(t.overflow, kOvfField);
 }
 
 // Fast path, L in {16, 32}, 16-B aligned rows: two lanes per read (lane pair = one packed word,
@@ -262,8 +286,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(Tbl t, const uint64_t* keys,
                                                     const uint64_t* first, uint64_t m) {
     for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < m; i += (uint64_t)gridDim.x * kThreads)
     {
-        if (counts[i] >> 32) atomicOr(t.overflow, kOvfField);   // a slot counts up to 2^32 - 1
-        tbl_add(t, keys[i], (uint32_t)counts[i], first[i]);
+        tbl_add(t, keys[i], counts[i], first[i]);   // (a count past 2^32 carries into wide)
     }
 }
 
@@ -411,7 +434,7 @@ __global__ __launch_bounds__(kExtractT) void k_part_scatter(Tbl t, uint32_t npar
         }
         okeys[pos] = key;
         olens[pos] = (uint32_t)L;
-        ocounts[pos] = (uint32_t)~sl.ncount;
+        ocounts[pos] = (uint64_t)(uint32_t)~sl.ncount + (t.wide ? t.wide[s] : 0ull);
         ofirst[pos] = sl.first;
     }
 }
@@ -1843,8 +1866,10 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
                     atomicOr(t.overflow, kOvfTable);
                     continue;
                 }
-                if ((c[k] >> 32) || f[k] > kMaxIndex) atomicOr(t.overflow, f[k] > kMaxIndex ? kOvfIndex : kOvfField);
-                atomicAdd(&scnt[off], (uint32_t)c[k]);
+                if (f[k] > kMaxIndex) atomicOr(t.overflow, kOvfIndex);
+                const uint32_t old = atomicAdd(&scnt[off], (uint32_t)c[k]);
+                if ((c[k] >> 32) || old + (uint32_t)c[k] < old)     // a carry past 32 bits: rare
+                    count_add_wide(t, base + off, old, (uint32_t)c[k], c[k] & ~0xFFFFFFFFull);
                 atomicMin(&sfst[off], (uint32_t)min((unsigned long long)kMaxIndex, f[k]));
             }
         }
@@ -1868,8 +1893,9 @@ __global__ void k_merge_sentinel(Tbl t, Recs recs, const uint64_t* run_off, uint
             unsigned long long c, f;
             recs.load(end - 1, run, k, c, f);
             Slot* sl = &t.slots[t.mask + 1];
-            if ((c >> 32) || f > kMaxIndex) atomicOr(t.overflow, f > kMaxIndex ? kOvfIndex : kOvfField);
-            atomicAdd(&sl->ncount, 0u - (uint32_t)c);
+            if (f > kMaxIndex) atomicOr(t.overflow, kOvfIndex);
+            const uint32_t old = atomicAdd(&sl->ncount, 0u - (uint32_t)c);
+            count_add_wide(t, t.mask + 1, ~old, (uint32_t)c, c & ~0xFFFFFFFFull);
             atomicMin(&sl->first, (uint32_t)min((unsigned long long)kMaxIndex, f));
         }
     }
@@ -1956,8 +1982,8 @@ __global__ __launch_bounds__(kPackT) void k_region_pack(Tbl t, uint32_t R, uint3
     __shared__ unsigned long long cursor;
     if (r == 0 && threadIdx.x == 0 && roff[R] != ~0ull) {   // the sentinel record
         const Slot& sl = t.slots[t.mask + 1];
-        const unsigned long long c = (uint32_t)~sl.ncount, f = sl.first - first_base;
-        if (f >> 32 || sl.first < first_base) atomicOr(flags, kOvfField);
+        const unsigned long long c = (uint32_t)~sl.ncount + (t.wide ? t.wide[t.mask + 1] : 0ull), f = sl.first - first_base;
+        if (f >> 32 || sl.first < first_base || (c >> 32)) atomicOr(flags, kOvfField);   // (u32 record counts)
         if (roff[R] < cap)
             rec[roff[R]] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, (uint32_t)c, (uint32_t)f);
         else
@@ -1983,7 +2009,8 @@ __global__ __launch_bounds__(kPackT) void k_region_pack(Tbl t, uint32_t R, uint3
             const unsigned long long pos = wave_reserve(used, 0u, &cursor);
             if (!used) continue;
             const uint32_t c = ~a[u].z;
-            if (a[u].w < first_base) atomicOr(flags, kOvfField);
+            // the 16-B record carries a u32 count: a count with a high part (wide) cannot cross
+            if (a[u].w < first_base || (t.wide && t.wide[base + i0 + u * kPackT + threadIdx.x])) atomicOr(flags, kOvfField);
             if (pos < cap)
                 rec[pos] = make_uint4(a[u].x, a[u].y, c, (uint32_t)(a[u].w - first_base));
             else
@@ -2289,8 +2316,8 @@ __global__ __launch_bounds__(256) void k_mw_merge_claim(Tbl t, const uint64_t* _
                                                         const uint64_t* __restrict__ found) {
     for (uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x; e < m; e += (uint64_t)gridDim.x * 256) {
         const uint64_t* kw = words + e * t.W;
-        if (counts[e] >> 32) atomicOr(t.overflow, kOvfField);
         const uint32_t c = (uint32_t)counts[e];
+        const uint64_t chi = counts[e] & ~0xFFFFFFFFull;
         uint64_t f = first[e];
         if (f > kMaxIndex) {
             atomicOr(t.overflow, kOvfIndex);
@@ -2317,9 +2344,11 @@ __global__ __launch_bounds__(256) void k_mw_merge_claim(Tbl t, const uint64_t* _
             for (uint32_t q = 0; q < t.W; ++q) dst[q] = kw[q];
             t.slots[at].ncount = ~c;
             t.slots[at].first = (uint32_t)f;
+            count_add_wide(t, at, 0u, c, chi);
             continue;
         }
-        atomicAdd(&t.slots[at].ncount, 0u - c);
+        const uint32_t old = atomicAdd(&t.slots[at].ncount, 0u - c);
+        count_add_wide(t, at, ~old, c, chi);
         if (t.slots[at].first > (uint32_t)f) atomicMin(&t.slots[at].first, (uint32_t)f);
     }
 }
@@ -2347,6 +2376,7 @@ hipError_t launch_prep(const PrepWords& w, hipStream_t s) {
 Tbl tbl_of(const ss_counter* c) {
     Tbl t;
     t.slots = c->slots;
+    t.wide = c->wide_live ? c->wide : nullptr;
     t.keywords = c->keywords;
     t.occ = c->occ;
     t.W = c->W;
@@ -2363,6 +2393,44 @@ int flush_reset(ss_counter* c, hipStream_t s) {
     if (!c->reset_pending) return SS_OK;
     c->reset_pending = false;
     return ss_check(hipMemsetAsync(c->slots, 0xFF, c->cap * sizeof(Slot), s), "ss_counter reset");
+}
+
+constexpr uint64_t kSinceUnknown = 1ull << 62;
+unsigned grid_for(uint64_t items, uint64_t per_block, unsigned cap);   // ss_counter::since after a merge: spill before the next insert
+
+// the wide count array allocated and, when it goes live, zeroed on `s`
+int wide_on(ss_counter* c, hipStream_t s) {
+    if (!c->wide && hipMalloc((void**)&c->wide, (c->cap + 1) * sizeof(uint64_t)) != hipSuccess) {
+        ss_check(hipGetLastError(), "counter wide counts hipMalloc");
+        c->wide = nullptr;
+        return ss_fail(SS_ENOMEM, "counter wide counts: out of device memory");
+    }
+    if (c->wide_live) return SS_OK;
+    c->wide_live = true;
+    return ss_check(hipMemsetAsync(c->wide, 0, (c->cap + 1) * sizeof(uint64_t), s), "counter wide counts reset");
+}
+
+// Every slot's count into wide (the sentinel slot, present iff its count is nonzero, keeps 1): the
+// slots restart below 2 and take another spill_at reads before the next spill.
+__global__ __launch_bounds__(256) void k_spill_wide(Tbl t) {
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= t.mask + 1; s += (uint64_t)gridDim.x * 256) {
+        const Slot sl = t.slots[s];
+        const bool sent = s > t.mask;
+        if (sent ? sl.ncount == 0xFFFFFFFFu : sl.key == kEmpty) continue;
+        const uint32_t cnt = ~sl.ncount, keep = sent ? 1u : 0u;
+        if (cnt <= keep) continue;
+        t.wide[s] += cnt - keep;
+        t.slots[s].ncount = ~keep;
+    }
+}
+
+int spill_wide(ss_counter* c, hipStream_t s) {
+    int rc = flush_reset(c, s);
+    if (!rc) rc = wide_on(c, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_spill_wide, dim3(grid_for(c->cap + 1, 256, 256 * 16)), dim3(256), 0, s, tbl_of(c));
+    c->since = 1;
+    return ss_check(hipGetLastError(), "k_spill_wide");
 }
 
 // fold the oldest recorded timing set into the sums (waits for its last event)
@@ -2397,6 +2465,7 @@ int launch_merge(ss_counter* c, Recs recs, const uint64_t* d_run_offsets, uint32
                         uint32_t reg_lo, uint32_t nreg, uint32_t* d_bounds, hipStream_t s, const char* what) {
     int rc = flush_reset(c, s);
     if (rc) return rc;
+    c->since = kSinceUnknown;   // (a carry past 32 bits goes to wide when live, else it is flagged)
     Tbl t = tbl_of(c);
     // few runs (the exchange's owners - 1): each region's block searches its segments itself;
     // otherwise one pass over every record writes the bounds (d_bounds)
@@ -3016,6 +3085,7 @@ int ss_counter_destroy(ss_counter* c) {
     if (c->slots) (void)hipFree(c->slots);
     if (c->work) (void)hipFree(c->work);
     if (c->keywords) (void)hipFree(c->keywords);
+    if (c->wide) (void)hipFree(c->wide);
     if (c->occ) (void)hipFree(c->occ);
     if (c->roff) (void)hipFree(c->roff);
     if (c->aux) (void)hipFree(c->aux);
@@ -3061,6 +3131,8 @@ int ss_counter_reset_host(ss_counter* c, unsigned long long** p, unsigned long l
     if (!c) return ss_fail(SS_EARG, "null counter");
     c->L = -1;
     c->occ_src = 0;
+    c->wide_live = false;       // (zeroed when it next goes live)
+    c->since = 0;
     c->reset_pending = true;    // the slots [0, cap): flush_reset or a fresh aggregate
     unsigned long long* sent = (unsigned long long*)(c->slots + c->cap);     // the sentinel slot
     p[0] = sent;
@@ -3243,6 +3315,11 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
     }
     if (base_index > kMaxIndex || n - 1 > kMaxIndex - base_index)
         return ss_fail(SS_EARG, "global read indices of a counter handle must stay below 2^32 - 1");
+    // u64 counts: a slot's u32 could wrap within this insert -> every count into wide first
+    // (not the drop-in engine's packed-word class tables: it spills their counts per row itself,
+    // ss_counter_spill_counts, and its class kernels read the slot counts directly)
+    if (c->L != kWordKeys && c->since + n > c->spill_at && (rc = spill_wide(c, s))) return rc;
+    c->since += n;
     c->occ_src = 0;   // set again below by the paths whose aggregate records the region occupancy
     Tbl t = tbl_of(c);
     const bool multi = c->W > 1;
@@ -3507,7 +3584,9 @@ int ss_counter_merge(ss_counter* c, const uint64_t* d_keys, const uint32_t* d_le
     const unsigned grid = grid_for(m, kThreads, 256 * 16);
     c->occ_src = 0;
     int rc = flush_reset(c, (hipStream_t)stream);
+    if (!rc) rc = wide_on(c, (hipStream_t)stream);    // u64 counts come in: carries go to wide
     if (rc) return rc;
+    c->since = kSinceUnknown;
     hipLaunchKernelGGL(k_merge, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, tbl_of(c), d_keys, d_counts,
                        d_first, m);
     return ss_check(hipGetLastError(), "k_merge");
@@ -3521,7 +3600,9 @@ int ss_counter_merge_words(ss_counter* c, const uint64_t* d_words, const uint64_
     if (c->W < 2) return ss_fail(SS_EARG, "ss_counter_merge_words takes multi-word keys (L > 32): use ss_counter_merge");
     hipStream_t s = (hipStream_t)stream;
     int rc = flush_reset(c, s);
+    if (!rc && c->L != kWordKeys) rc = wide_on(c, s);   // (the engine's class tables: see insert_impl)
     if (rc) return rc;
+    c->since = kSinceUnknown;
     uint64_t* found = nullptr;
     if ((rc = aux_scratch(c, m * sizeof(uint64_t), (void**)&found))) return rc;
     const unsigned grid = grid_for(m, 256, 256 * 16);
@@ -3691,7 +3772,15 @@ int ss_counter_spill_counts(ss_counter* c, uint64_t* d_acc, void* stream) {
     int rc = flush_reset(c, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_spill_counts, dim3(grid_for(c->cap + 1, 256, 256 * 16)), dim3(256), 0, s, tbl_of(c), d_acc);
+    c->since = 1;
     return ss_check(hipGetLastError(), "k_spill_counts");
+}
+
+int ss_counter_set_spill_limit(ss_counter* c, uint64_t reads) {
+    if (!c) return ss_fail(SS_EARG, "null counter");
+    if (reads < 1 || reads > 0xFFFFFFFFull) return ss_fail(SS_EARG, "spill limit in 1 .. 2^32 - 1");
+    c->spill_at = reads;
+    return SS_OK;
 }
 
 // the scratch of the read-order path: rep[(cap + 1) * 8], found[cap + 1], then the per-block class

@@ -1147,7 +1147,9 @@ int spec_launch(ss_ingest* g, const uint64_t* need, uint64_t N) {
         if ((rc = gr.words.ensure(cap * gr.W1)) || (rc = gr.counts.ensure(cap)) || (rc = gr.first.ensure(cap)))
             return rc;
         fo[W] = {gr.words.p, gr.counts.p, gr.first.p, g->spec_dev.p + W, g->spec_dev.p + 8, cap};
-        const uint64_t kb = std::min<uint64_t>(cap, need[W] + 1024);
+        // (sizing mode 5, a test hook: the result bound taken as if the estimate were 0, so a chunk of
+        // more than ~1024 distinct keys per class passes it and the finish runs the ordinary way)
+        const uint64_t kb = std::min<uint64_t>(cap, (g->sizing == 5 ? 0 : need[W]) + 1024);
         k_ub += kb;
         nw_ub += kb * W;
         cls.push_back(&gr);
@@ -1506,12 +1508,14 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             if ((rc = flush_prep(g))) return rc;
         }
         if ((rc = g->cls_flag.ensure(1))) return rc;
-        // (sizing mode 3, a test hook: the flag starts raised, as if two keys shared a fingerprint)
-        rc = ss_check(hipMemsetAsync(g->cls_flag.p, g->sizing == 3 ? 1 : 0, 4, s), "ingest class flag reset");
+        // (sizing modes 3 / 4, test hooks: the flag starts raised, as if two keys shared a fingerprint;
+        // 4 keeps the deferred fold and the speculative finish, so the flag is found after they were queued)
+        rc = ss_check(hipMemsetAsync(g->cls_flag.p, g->sizing == 3 || g->sizing == 4 ? 1 : 0, 4, s),
+                      "ingest class flag reset");
         if (!rc && !flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, cls_rows, 0, s);
         if (!rc && !flat) rc = ss_classes_verify_fold(g->fpt, g->cls_fps.p, cr.data(), (uint32_t)cr.size(), g->cls_flag.p, s);
         // the fold is deferred when every class of the chunk starts from an empty table (see pend)
-        bool defer = flat && g->sizing == 0;
+        bool defer = flat && (g->sizing == 0 || g->sizing >= 4);
         for (uint32_t W = 2; W < 6; ++W) defer &= !fc[W].table || fc[W].base == 0;
         if (!rc && flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, n, 0, s);
         if (!rc && flat && defer) {
@@ -1834,7 +1838,7 @@ int ss_ingest_set_row_limit(ss_ingest* g, uint64_t rows) {
 
 int ss_ingest_set_exact(ss_ingest* g, int exact) {
     if (!g) return ss_fail(SS_EARG, "null ingest");
-    if (exact < 0 || exact > 3) return ss_fail(SS_EARG, "sizing mode 0 .. 3");
+    if (exact < 0 || exact > 5) return ss_fail(SS_EARG, "sizing mode 0 .. 5");
     g->sizing = exact;
     return SS_OK;
 }

@@ -160,3 +160,30 @@ def test_all_pairs_pigeonhole_past_2_22(gpu, oracle):
     cnt_p, _, tot_p = B.hamming_all_pairs(d, L, k, method="pigeonhole")
     assert tot_p == tot_t and torch.equal(cnt_p, cnt_t)
     assert int(cnt_t.sum().item()) == 2 * tot_t and tot_t > 0
+
+
+@pytest.mark.gpu
+def test_all_pairs_auto_is_capturable(gpu, oracle):
+    """AUTO on a stream under hipGraph capture stays on the tiles (no allocation, no host read-back:
+    ADVICE r5), so a batch auto would hand to the pigeonhole form captures and replays with the same
+    counts and total as the eager call."""
+    import torch
+    import shortseq_amd.batch as B
+    from shortseq_amd._native import lib, check
+    n, L, k = 1 << 15, 12, 1
+    ascii = _umis(oracle, n, L, 8000, 21)
+    words, _, _ = oracle.encode_batch(ascii, n, L)
+    d = torch.from_numpy(words.view(np.int64)).to(gpu)
+    cnt_e, _, tot_e = B.hamming_all_pairs(d, L, k, method="auto")
+    cnt = torch.empty(n, dtype=torch.int32, device=gpu)
+    tot = torch.empty(1, dtype=torch.int64, device=gpu)
+    torch.cuda.synchronize(gpu)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream(gpu).cuda_stream
+        check(lib().ss_hamming_all_pairs_ex(d.data_ptr(), n, L, 1, k, cnt.data_ptr(), 0, 0, tot.data_ptr(),
+                                            B.ALL_PAIRS_METHODS["auto"], s), "captured all pairs")
+    cnt.fill_(-1)
+    g.replay()
+    torch.cuda.synchronize(gpu)
+    assert int(tot.item()) == tot_e and torch.equal(cnt, cnt_e)

@@ -73,6 +73,32 @@ def test_device_ingest_ragged_small(gpu, oracle, case, exact):
     assert np.array_equal(gw, ew)
 
 
+@pytest.mark.parametrize("hook", [4, 5])
+@pytest.mark.parametrize("U", [1 << 12, 1 << 18])
+def test_device_ingest_speculative_finish_dropped(gpu, oracle, hook, U):
+    """One read-order chunk (50-150 nt), so the class fold is deferred and the finish is queued
+    speculatively beside the verify; then (test hooks) 4: the fingerprint flag comes back
+    raised only after both were queued -- the speculation is dropped, the classes are re-encoded and
+    counted exactly over the rows the speculative extract had written; 5: the result bound is taken
+    as if the sketch said 0, so the speculative gather refuses (its bad flag) and the finish runs the
+    ordinary way.  Both == the generator-derived rows, twice (a second results() call)."""
+    import shortseq_amd.batch as B
+    seed, ps, n, lo, hi = 61, 62, 250_000, 50, 150
+    blob, offs, lens = B.synth_ragged_pool_reads(n, seed, ps, U, lo, hi, device=gpu)
+    eng = B.DeviceIngest(gpu, _sizing=hook)
+    try:
+        eng.count(blob, offs, lens)
+        gl, gc, gw = (a.copy() for a in eng.results())
+        gl2, gc2, gw2 = eng.results()
+    finally:
+        eng.close()
+    el, ec, ew = oracle.ragged_pool_rows(seed, ps, U, n, lo, hi)
+    for l_, c_, w_ in ((gl, gc, gw), (gl2, gc2, gw2)):
+        assert l_.tolist() == el.tolist()
+        assert c_.tolist() == ec.tolist()
+        assert np.array_equal(w_, ew)
+
+
 def test_device_ingest_undersized_class_table_recounts(gpu, oracle):
     """A class table sized below its distinct keys (the test hook: 1/64 of the sketch) runs full:
     the add call returns SS_EFULL and the first batch is counted again with tables sized by rows;
