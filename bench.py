@@ -38,15 +38,17 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def compact(x, sig: int = 4):
+def compact(x, sig: int = 4, _depth: int = 0):
     """The JSON line the driver keeps is the tail of stdout (~8.8 KB): floats to `sig` significant
-    digits, explanatory strings (note / how / where) dropped -- DESIGN.md section 5 holds them."""
+    digits, explanatory strings (note / how / where / xgmi, and the kernel names of the extras'
+    rooflines) dropped -- DESIGN.md section 5 and section 4 hold them; the headline keeps its kernel."""
     if isinstance(x, float):
         return float(f"{x:.{sig}g}") if x == x else None
     if isinstance(x, dict):
-        return {k: compact(v, sig) for k, v in x.items() if k not in ("note", "how", "where")}
+        drop = ("note", "how", "where", "xgmi") + (("kernel",) if _depth > 1 else ())
+        return {k: compact(v, sig, _depth + 1) for k, v in x.items() if k not in drop}
     if isinstance(x, (list, tuple)):
-        return [compact(v, sig) for v in x]
+        return [compact(v, sig, _depth + 1) for v in x]
     return x
 
 
@@ -321,6 +323,18 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
     _el_p, _tr_p = timed_loop(step, max(2, steps // 2), 1, world, on_timed_start=lambda: sc.local.pass_times())
     passes = sc.local.pass_times()
     sc.local.set_timing(False)
+    exch = None
+    if world > 1:
+        # one diagnostic count with the device synchronised around each phase:
+        # local count, pack, the two all-to-alls with their host sync, merge; every rank's split
+        # gathered to rank 0 as [min, max] per field, with the backend and the world size they saw
+        from shortseq_amd.dist import rank_spread
+        st = {}
+        dist.barrier()
+        sc.count(ascii, L, base_index=i0, check_errors=False, stats=st)
+        allst = [None] * world
+        dist.all_gather_object(allst, st)
+        exch = rank_spread(allst)
     del ascii
     # parity after timing: the whole job's table gathered to rank 0 (all owners' regions), its
     # (key, count, first) rows sorted by key hashed and compared with the generator-derived digest of
@@ -341,7 +355,7 @@ def bench_counter(B, lib, dev, rank, world, n, L, U, steps, warmup, seed=5, pool
             if (uniq, table_digest(keys, counts, first)) != (want["unique"], want["digest"]):
                 raise SystemExit(f"PARITY FAILURE: counter table != {name}")
             check = f"digest {name}"
-    return el, tr.region_ms / steps, uniq, check, passes
+    return el, tr.region_ms / steps, uniq, check, passes, exch
 
 
 def bench_exchange(B, dev, n=125_000_000, U=1 << 24, owners=8, reps=5):
@@ -578,11 +592,21 @@ def bench_host_staged(B, dev, n=32_000_000, L=32, reps=5):
         if [int(out[i, 0])] != known_words(1, int(i), L):
             raise SystemExit("PARITY FAILURE: host-staged encode")
     t = float(np.median(ts))
+    # the stage split of two more (timed) calls, and where the copy threads run
+    st.set_timing(True)
+    st.stats()
+    for _ in range(2):
+        st.encode(host, out=out)
+    split = st.stats()
+    st.set_timing(False)
     del a_dev
+    place = {k: split.pop(k) for k in ("copy_threads", "affinity_cpus", "gpu_numa_node", "pinned_cpus")}
     return {"reads": n, "read_len": L, "ms_per_call": t * 1e3, "nt_per_s": n * L / t,
-            "host_dev_GB_per_s": n * (L + 8) / t / 1e9,
+            "host_dev_GB_per_s": n * (L + 8) / t / 1e9, "stage_ms": split, **place,
             "note": "pageable numpy in -> numpy out through ss_encode_host (64-MiB chunks, 3 slots, "
-                    "8 staging threads); PCIe-bound, not the roofline number"}
+                    "8 staging threads pinned to the GPU's NUMA node within the affinity mask); stage_ms: "
+                    "host copy / wait ms and device H2D / kernel / D2H ms per call (device sums overlap "
+                    "across chunks); PCIe-bound, not the roofline number"}
 
 
 def _median_time(fn, reps=3):
@@ -622,6 +646,27 @@ def bench_c1_dropin(n=1_000_000, L=32):
             "note": "wall time incl. Python object creation (the reference's own API shape), median of 3"}
 
 
+def bench_dropin_multidevice(n=8_000_000, L=32, U=1 << 22):
+    """The drop-in counter over every visible device (only when the process sees
+    >= 2 GPUs): ShortSeqCounter(list, device=[0 .. D-1]) -- one engine per device counts a contiguous
+    slice, then the tree reduce over peer copies (_reduce_fill) -- against the same list on device 0;
+    the dicts must be equal (keys, counts and first-occurrence order)."""
+    import shortseq_amd as sq
+    import shortseq_amd.batch as B
+    D = min(8, torch.cuda.device_count())
+    a = B.synth_pool_reads(n, L, 21, 22, U, device="cuda").cpu().numpy().reshape(-1)
+    reads = [a[i * L:(i + 1) * L].tobytes() for i in range(n)]
+    devs = list(range(D))
+    sq.ShortSeqCounter(reads[:200_000], device=devs)          # warm every engine
+    t1, c1 = _median_time(lambda: sq.ShortSeqCounter(reads, device=0))
+    tD, cD = _median_time(lambda: sq.ShortSeqCounter(reads, device=devs))
+    if list(cD.items())[:1000] != list(c1.items())[:1000] or len(cD) != len(c1) or sum(cD.values()) != n:
+        raise SystemExit("PARITY FAILURE: multi-device drop-in counter")
+    return {"devices": D, "reads": n, "read_len": L, "pool": U, "unique": len(cD), "s_one_device": t1,
+            "s_all_devices": tD, "speedup": t1 / tD,
+            "note": "wall time incl. building the dict; the shards reduce as a tree over peer copies"}
+
+
 def _fastq_case_file():
     """The small-RNA-like FASTQ of tools/probe_fastq_e2e.py: 8.4M ragged 18-32-nt records, 65,536
     distinct sequences each 128 times (528 MB), written once to a temporary file."""
@@ -650,9 +695,23 @@ def bench_fastq_dropin(path, n):
     if len(c) != 65536 or sum(c.values()) != n:
         raise SystemExit("PARITY FAILURE: read_and_count_fastq drop-in")
     t = float(np.median(ts))
-    return {"records": n, "file_bytes": os.path.getsize(path), "s_per_call": t, "records_per_s": n / t,
-            "unique": len(c), "note": "wall time of the drop-in call on a 528-MB small-RNA-like FASTQ "
-                                      "(page-cached), incl. building the 65,536-entry dict"}
+    # the stage split of the last call and the PCIe floor: the file's bytes at the
+    # host -> device rate the same call's H2D copies ran at
+    from shortseq_amd import _shortseq
+    st = (_shortseq.fastq_stage_times() or [{}])[0]
+    fb = os.path.getsize(path)
+    out = {"records": n, "file_bytes": fb, "s_per_call": t, "records_per_s": n / t, "unique": len(c)}
+    if st.get("h2d_dev_ms"):
+        rate = st["h2d_bytes"] / (st["h2d_dev_ms"] * 1e-3)
+        out["stage_ms"] = {k: st[k] for k in ("read_ms", "h2d_dev_ms", "index_ms", "count_ms", "finish_ms",
+                                              "reduce_and_dict_ms", "total_ms") if k in st}
+        out["h2d_GB_per_s"] = rate / 1e9
+        out["pcie_floor_s"] = fb / rate
+        out["floor_frac"] = fb / rate / t
+    out["note"] = ("wall time of the drop-in call on a 528-MB small-RNA-like FASTQ (page-cached), incl. building "
+                   "the 65,536-entry dict; stage_ms of the last call (reads and H2D overlap); floor = file bytes "
+                   "at the H2D rate the call's copies ran at")
+    return out
 
 
 def cpu_baseline(target_s=2.0):
@@ -866,7 +925,7 @@ def main():
             n5, U5 = 125_000_000, 1 << 24
             log(f"C5 counter {n5} x 32 per GPU, pool {U5}")
             s5 = max(3, args.steps // 4)
-            el5, d5, uniq, chk5, pass5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
+            el5, d5, uniq, chk5, pass5, exch5 = bench_counter(B, lib, dev, rank, world, n5, 32, U5, s5, 2)
             # SURVEY §8(d) prices C5 at the 32 B of ASCII per read (the problem's floor): that is the
             # headline frac.  Beside it, the partitioned pipeline's own pass bytes: coarse
             # pass 32 in + 12 out (key, read index), fine scatter 12 + 12, aggregate 12 + the whole
@@ -887,11 +946,13 @@ def main():
                 "merge": (f"all_to_all_single of 16-B (key, count, first) records by owner over {dist.get_backend()}"
                           f"{' (RCCL/xGMI)' if dist.get_backend() == 'nccl' else ' (host-staged rehearsal)'}")
                          if world > 1 else "none (1 GPU)"}
+            if exch5 is not None:      # per-rank [min, max] of the diagnostic count's phases
+                extra["C5_counter_32"]["exchange"] = exch5
             # SURVEY §8(d) C5 variants: the smaller pool and Zipf s = 1.1 skew (same shard size)
             for name, U_, zs in (("C5_counter_32_U20", 1 << 20, None), ("C5_counter_32_zipf1.1_U24", 1 << 24, 1.1),
                                  ("C5_counter_32_zipf1.1_U20", 1 << 20, 1.1)):
                 log(f"C5 counter {n5} x 32 per GPU, pool {U_}, {'zipf ' + str(zs) if zs else 'uniform'}")
-                el_, d_, u_, chk_, pass_ = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
+                el_, d_, u_, chk_, pass_, _x = bench_counter(B, lib, dev, rank, world, n5, 32, U_, s5, 2, zipf=zs)
                 # the same pipeline bytes model with this pool's table (a skewed batch moves fewer records
                 # through the fine passes after deduplication: the model is then an upper bound)
                 pb_ = 32 + 12 + 24 + 12 + 16 * (2 * U_) / n5
@@ -941,6 +1002,9 @@ def main():
             local_extra("C2_host_staged_32", lambda: bench_host_staged(B, dev))
             log("C1 drop-in API")
             local_extra("C1_dropin_1M_32", bench_c1_dropin)
+            if world == 1 and torch.cuda.device_count() >= 2:
+                log("drop-in counter over every visible device")
+                local_extra("C1_dropin_multidevice", bench_dropin_multidevice)
             log("a18 read_and_count_fastq drop-in")
             fq_path, fq_n = _fastq_case_file()
             local_extra("A18_read_and_count_fastq_smallrna", lambda: bench_fastq_dropin(fq_path, fq_n))

@@ -430,6 +430,12 @@ int ss_ingest_add_device(ss_ingest* g, const uint8_t* d_blob, uint64_t nbytes, c
                          const uint32_t* d_lens, uint64_t n);
 int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_read, uint64_t cap, uint64_t* h_len);
 int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords);
+/* Stage split of the engine's FASTQ calls since the last call of this (new,
+ * replaces nothing): h_ms[5] = host ms of the file reads (pread into pinned memory, in pieces whose
+ * H2D copies overlap the next piece's read), device ms of those H2D copies (summed), host ms of the
+ * device index to its sync, host ms of the chunk counts, host ms of ss_ingest_finish; *h_h2d_bytes =
+ * the bytes the H2D copies moved (their rate = the PCIe rate the call saw). */
+int ss_ingest_fastq_stages(ss_ingest* g, double* h_ms, uint64_t* h_h2d_bytes);
 int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words);
 /* Compact results (new in this ABI version; replaces nothing -- the reference's dict holds Python
  * ints): with ss_ingest_set_results_format(g, 1) the finish writes lengths as u16 and counts as u32
@@ -510,6 +516,15 @@ typedef struct ss_stager ss_stager;
 int ss_stager_create(int device, uint64_t chunk_bytes, uint32_t nslots, uint32_t copy_threads,
                      ss_stager** h_out);
 int ss_stager_destroy(ss_stager* st);
+/* Stage split and placement of a stager (new, replaces nothing).  With timing on,
+ * every call records event pairs per chunk.  ss_stager_stats returns, per call since its last call
+ * (timed calls), h_ms[6] = host ms of the pageable -> pinned copies, host ms of the pinned ->
+ * pageable copies, device ms of the H2D copies, the kernels and the D2H copies (sums over chunks:
+ * they overlap across chunks), host ms waiting on the D2H events; and h_info[4] = copy threads, CPUs
+ * in the process's affinity mask, the GPU's NUMA node (-1 unknown), CPUs the copy threads are pinned
+ * to (the node's CPUs within the mask; 0 = not pinned, also with SHORTSEQ_STAGE_PIN=0). */
+int ss_stager_set_timing(ss_stager* st, int on);
+int ss_stager_stats(ss_stager* st, double* h_ms, int32_t* h_info);
 int ss_encode_host(ss_stager* st, const uint8_t* h_ascii, uint64_t n, uint32_t L, uint64_t stride,
                    uint64_t* h_words, uint32_t wpr, uint64_t* h_first_bad);
 int ss_encode_hamming_ref_host(ss_stager* st, const uint8_t* h_ascii, uint64_t n, uint32_t L, uint64_t stride,

@@ -100,6 +100,7 @@ SIGNATURES = [
     ("ss_ingest_add_device", C.c_int, [_P, _P, _U64, _P, _P, _U64]),
     ("ss_ingest_error", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_int), _P, _U64, C.POINTER(C.c_uint64)]),
     ("ss_ingest_finish", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("ss_ingest_fastq_stages", C.c_int, [_P, _P, _P]),
     ("ss_ingest_results", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("ss_ingest_set_results_format", C.c_int, [_P, C.c_int]),
     ("ss_ingest_results_compact", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
@@ -109,6 +110,8 @@ SIGNATURES = [
     ("ss_ingest_reserve_merge", C.c_int, [_P, _P, _U32]),
     ("ss_stager_create", C.c_int, [C.c_int, _U64, _U32, _U32, C.POINTER(C.c_void_p)]),
     ("ss_stager_destroy", C.c_int, [_P]),
+    ("ss_stager_set_timing", C.c_int, [_P, C.c_int]),
+    ("ss_stager_stats", C.c_int, [_P, _P, _P]),
     ("ss_encode_host", C.c_int, [_P, _P, _U64, _U32, _U64, _P, _U32, C.POINTER(C.c_uint64)]),
     ("ss_encode_hamming_ref_host", C.c_int, [_P, _P, _U64, _U32, _U64, _P, _U32, _P, _P, C.POINTER(C.c_uint64)]),
     ("ss_decode_host", C.c_int, [_P, _P, _U64, _U32, _U32, _P, _U64]),

@@ -294,6 +294,24 @@ class HostStager:
             lib().ss_stager_destroy(self._h)
             self._h = None
 
+    STAGES = ("copy_in_host", "copy_out_host", "h2d_dev", "kernel_dev", "d2h_dev", "wait_host")
+
+    def set_timing(self, on: bool = True) -> None:
+        """Record the per-chunk stage split (ss_stager_set_timing)."""
+        check(lib().ss_stager_set_timing(self._h, int(bool(on))), "ss_stager_set_timing")
+
+    def stats(self) -> dict:
+        """Mean ms per timed call of each stage since the last stats() (device stages are sums over
+        chunks, which overlap), and the placement: copy threads, affinity CPUs, the GPU's NUMA node,
+        CPUs the copy threads are pinned to (ss_stager_stats)."""
+        ms = (C.c_double * 6)()
+        info = (C.c_int32 * 4)()
+        check(lib().ss_stager_stats(self._h, ms, info), "ss_stager_stats")
+        out = {k: float(v) for k, v in zip(self.STAGES, ms)}
+        out.update(copy_threads=int(info[0]), affinity_cpus=int(info[1]), gpu_numa_node=int(info[2]),
+                   pinned_cpus=int(info[3]))
+        return out
+
     def __del__(self):
         try:
             self.close()

@@ -71,6 +71,7 @@ ctypedef int (*f_add_blob)(ss_ingest*, const uint8_t*, const uint32_t*, uint64_t
 ctypedef int (*f_add_fastq)(ss_ingest*, const char*, uint64_t, uint64_t*) noexcept nogil
 ctypedef int (*f_error)(ss_ingest*, uint64_t*, int*, uint8_t*, uint64_t, uint64_t*) noexcept nogil
 ctypedef int (*f_finish)(ss_ingest*, uint64_t*, uint64_t*) noexcept nogil
+ctypedef int (*f_fq_stages)(ss_ingest*, double*, uint64_t*) noexcept nogil
 ctypedef int (*f_results)(ss_ingest*, const uint32_t**, const uint64_t**, const uint64_t**) noexcept nogil
 ctypedef int (*f_get_device)(int*) noexcept nogil
 ctypedef int (*f_fastq_split)(const char*, uint32_t, uint64_t*, uint64_t*) noexcept nogil
@@ -90,6 +91,7 @@ cdef struct _Abi:
     f_add_fastq add_fastq
     f_error error
     f_finish finish
+    f_fq_stages fq_stages
     f_results results
     f_get_device get_device
     f_fastq_split fastq_split
@@ -136,6 +138,7 @@ cdef int _bind_abi() except -1:
     _abi.export_keys = <f_export>_sym(h, b"ss_ingest_export")
     _abi.merge = <f_merge>_sym(h, b"ss_ingest_merge")
     _abi.reserve_merge = <f_reserve_merge>_sym(h, b"ss_ingest_reserve_merge")
+    _abi.fq_stages = <f_fq_stages>dlsym(h, b"ss_ingest_fastq_stages")   # (optional: a bench probe)
     _abi_ready = True
     return 0
 
@@ -995,6 +998,16 @@ def read_and_count_fastq(filename, device="auto", *, _chunk_bytes=0):
     return counts
 
 
+_last_fastq_stages = []    # the last GPU call's stage split, per device (fastq_stage_times)
+
+
+def fastq_stage_times():
+    """Stage split of the last GPU read_and_count_fastq call, one dict per device (ms; bench / probes):
+    file reads into pinned memory, device H2D (summed pieces, overlapping the reads), index, count,
+    finish, bytes copied; on the first, the reduce + dict build and the whole call."""
+    return [dict(x) for x in _last_fastq_stages]
+
+
 def _read_and_count_fastq_gpu(filename, devs, uint64_t chunk_bytes=0):
     """The file streamed through one engine per device: range k of ss_fastq_split on devs[k]
     (parallel preads into pinned staging, chunks ending after a newline, one-read FASTQ index, split
@@ -1008,6 +1021,9 @@ def _read_and_count_fastq_gpu(filename, devs, uint64_t chunk_bytes=0):
         raise Exception(f"{str(fname)}: Something went wrong while reading this file.")
     cdef uint64_t* begin = <uint64_t*>calloc(D + 1, sizeof(uint64_t))
     cdef uint64_t* line0 = <uint64_t*>calloc(D + 1, sizeof(uint64_t))
+    cdef double st_ms[5]
+    cdef uint64_t st_bytes = 0
+    stages = []
     if begin == NULL or line0 == NULL:
         free(begin)
         free(line0)
@@ -1023,13 +1039,24 @@ def _read_and_count_fastq_gpu(filename, devs, uint64_t chunk_bytes=0):
         for k in range(D):
             g = <size_t>_engine(devs[k])
             engines.append((devs[k], g))
+            if _abi.fq_stages != NULL:
+                _abi.fq_stages(<ss_ingest*>g, st_ms, &st_bytes)     # (drop what earlier calls left)
             jobs.append((g, 1, 0, 0, 0, fname, begin[k], begin[k + 1], line0[k], chunk_bytes, None))
         per = _run_shard_jobs(jobs)
         nseqs = sum(per)
         t2 = time.time()
+        if _abi.fq_stages != NULL:    # the engines' stage split (before the reduce adds its finish)
+            for d, g in engines:
+                _abi.fq_stages(<ss_ingest*><size_t>g, st_ms, &st_bytes)
+                stages.append([st_ms[i] for i in range(5)] + [st_bytes])
         counts = ShortSeqCounter()
         _reduce_fill(counts, engines, [sum(per[:k]) for k in range(D)])
         t3 = time.time()
+        _last_fastq_stages[:] = [dict(zip(("read_ms", "h2d_dev_ms", "index_ms", "count_ms", "finish_ms", "h2d_bytes"), x))
+                                 for x in stages]
+        if _last_fastq_stages:
+            _last_fastq_stages[0]["reduce_and_dict_ms"] = (t3 - t2) * 1e3
+            _last_fastq_stages[0]["total_ms"] = (t3 - t1) * 1e3
     finally:
         free(begin)
         free(line0)

@@ -954,24 +954,42 @@ __device__ __forceinline__ uint32_t dedup_home(uint64_t key, uint32_t log2n) {
 
 // KEYS: the keys come precomputed (in = n u64 keys, e.g. the drop-in engine's row fingerprints;
 // stride16 / cpr / first_bad unused) instead of being encoded from 16 / 32-nt ASCII rows.
-template <int T, int RPL, bool KEYS>
+// G16 (32-nt rows, round 6): the tile is loaded in k_encode_g16's shape -- per step, lane l of a wave
+// loads 16-B chunk (l & 1) of read (l >> 1) and of read 32 + (l >> 1), so each load instruction
+// covers 1 KB of contiguous ASCII (the lane-per-read form loaded 16 B at a 32-B lane stride: every
+// instruction touched 16 half-used lines, and the second instruction the same lines again); one DPP
+// pair swap then hands the even lane read (l >> 1)'s high half and the odd lane read 32 + (l >> 1)'s
+// low half (and its table-path carry), so every lane again holds one whole key.
+// Staging (round 6): a tile element is its key (skey) and ONE meta word (tile offset | bin << 16 |
+// kMetaDead), where the former kept the global read index and a bin byte apart (three random LDS
+// stores per element, five LDS reads per record in the write-out: bin, the bin's start and base, key,
+// index); a bin's start and reservation base are folded into one delta word (sdelta), so a record
+// takes three LDS reads: meta, key, delta.
+constexpr uint32_t kMetaDead = 0x80000000u;   // staged element folded into another (no record)
+template <int T, int RPL, bool KEYS, bool G16>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_coarse(
         Tbl t, PartWs w, const uint4* __restrict__ in, uint64_t stride16, uint64_t n, uint32_t cpr, uint64_t cap1,
         uint32_t* fill, unsigned long long* first_bad) {
     constexpr uint32_t TILE = T * RPL;
     constexpr uint32_t kHtLog = TILE == 4096 ? 12 : TILE == 2048 ? 11 : 13;
     static_assert((1u << kHtLog) == TILE, "tile must be 2048, 4096 or 8192 reads");
-    __shared__ uint32_t lcount[kCB], lstart[kCB], gbase[kCB], hcnt[kCB], sbase[kCB];
+    static_assert(!(KEYS && G16), "G16 encodes ASCII rows");
+    __shared__ uint32_t lcount[kCB], lstart[kCB], gbase[kCB], hcnt[kCB], sbase[kCB], sdelta[kCB];
     __shared__ uint8_t hflag[kCB];
     __shared__ uint32_t any_heavy;
     __shared__ uint64_t skey[TILE];
-    __shared__ uint32_t sidx[TILE];
-    __shared__ uint8_t sbin[TILE];
+    __shared__ uint32_t smeta[TILE];
     __shared__ uint32_t ht[TILE];
     uint32_t* spill_ctr = fill + fill_at(kSpillCtr);
     const uint32_t shift = w.rbits - kCoarseBits;
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t sub = blockIdx.x % kFinePerBin;   // this block's sub-bin of every bin
+    const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
+    const bool odd = (lane & 1u) != 0;
+    // tile offset of the read a lane holds at step j (G16: the lane-pair permutation of the wave's 64)
+    auto eoff = [&](int j) -> uint32_t {
+        return G16 ? (uint32_t)j * T + wbase + ((lane & 1u) << 5) + (lane >> 1) : (uint32_t)j * T + threadIdx.x;
+    };
     uint4 nx[RPL][2];
     uint64_t nk[RPL];
     // branch-free loads (read index clamped to the last read; lanes past n are never live): the
@@ -980,19 +998,25 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
     auto load_tile = [&](uint64_t tile) {
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
-            const uint64_t r = min(tile * TILE + j * T + threadIdx.x, n - 1);
-            if constexpr (KEYS) {
-                nk[j] = ((const uint64_t*)in)[r];
+            if constexpr (G16) {
+                const uint64_t r0 = tile * TILE + (uint64_t)j * T + wbase + (lane >> 1);
+                nx[j][0] = ld_stream(&in[min(r0, n - 1) * stride16 + (lane & 1u)]);
+                nx[j][1] = ld_stream(&in[min(r0 + 32, n - 1) * stride16 + (lane & 1u)]);
             } else {
-                nx[j][0] = ld_stream(&in[r * stride16]);
-                nx[j][1] = ld_stream(&in[r * stride16 + hi16]);
+                const uint64_t r = min(tile * TILE + j * T + threadIdx.x, n - 1);
+                if constexpr (KEYS) {
+                    nk[j] = ((const uint64_t*)in)[r];
+                } else {
+                    nx[j][0] = ld_stream(&in[r * stride16]);
+                    nx[j][1] = ld_stream(&in[r * stride16 + hi16]);
+                }
             }
         }
     };
     // wave 0 lane, bins b0 = 2 lane and b0 + 1: reserve c0 / c1 slots of their sub-bins (b, sub) with
     // one 64-bit atomic on the pair's word (only the bins flagged in `mask`: bit 0 = b0, bit 1 =
     // b0 + 1); the part past cap1 reserves spill records (a second atomic, rare).  Sets the bins'
-    // bases (gbase) and spill runs (sbase).
+    // bases (gbase, and sdelta = base - start), and spill runs (sbase).
     auto reserve = [&](uint32_t b0, uint32_t c0, uint32_t c1, uint32_t mask) {
         const uint64_t add = ((mask & 1u) ? (uint64_t)c0 : 0ull) | ((mask & 2u) ? (uint64_t)c1 << 32 : 0ull);
         const uint64_t g2 = add ? atomicAdd((unsigned long long*)&fill[fill_at(b0 * kFinePerBin + sub)],
@@ -1003,6 +1027,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
             if (!(mask & (1u << k))) continue;
             const uint32_t g = (uint32_t)(g2 >> (32 * k)), c = k ? c1 : c0;
             gbase[b0 + k] = g;
+            sdelta[b0 + k] = g - lstart[b0 + k];
             const uint64_t end = (uint64_t)g + c, from = max((uint64_t)g, cap1);
             sbase[b0 + k] = end > from ? atomicAdd(spill_ctr, (uint32_t)(end - from)) : 0u;
         }
@@ -1018,16 +1043,28 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
     for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         load_tile(tile);
         uint64_t key[RPL];
-        uint32_t bin[RPL], rank[RPL];
+        uint32_t br[RPL];     // bin << 16 | rank in the bin (one register per read)
         const uint64_t t0 = tile * TILE;
         const uint32_t cnt = (uint32_t)min((uint64_t)TILE, n - t0);
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
-            const uint64_t r = t0 + j * T + threadIdx.x;
-            const bool live = r < n;
+            const bool live = eoff(j) < cnt;
             if constexpr (KEYS) {
                 key[j] = nk[j];
+            } else if constexpr (G16) {
+                // chunk (lane & 1) of read A = (lane >> 1) and of read B = 32 + (lane >> 1), table path
+                const Enc32 a = encode16(nx[j][0].x, nx[j][0].y, nx[j][0].z, nx[j][0].w, true);
+                const Enc32 b = encode16(nx[j][1].x, nx[j][1].y, nx[j][1].z, nx[j][1].w, true);
+                const uint32_t recv = swap_pair(odd ? a.v : b.v);    // even: A's high half; odd: B's low half
+                const uint32_t bc = swap_pair(b.cout);               // odd: the carry out of B's low half
+                const uint32_t lo = odd ? recv : a.v;
+                const uint32_t hi = odd ? (b.v | bc) : (recv | a.cout);
+                const uint64_t ra = t0 + (uint64_t)j * T + wbase + (lane >> 1);
+                report_bad(ra < n && a.bad != 0u, ra, first_bad);
+                report_bad(ra + 32 < n && b.bad != 0u, ra + 32, first_bad);
+                key[j] = (uint64_t)lo | ((uint64_t)hi << 32);
             } else {
+                const uint64_t r = t0 + j * T + threadIdx.x;
                 // table path for both chunks (L <= 32); the low chunk's alias carry into the high half
                 const Enc32 a = encode16(nx[j][0].x, nx[j][0].y, nx[j][0].z, nx[j][0].w, true);
                 const uint4 h = hi16 ? nx[j][1] : make_uint4(0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u);
@@ -1036,13 +1073,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
                 key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
             }
             if (live) {
-                bin[j] = region_of(t, key[j]) >> shift;
-                rank[j] = atomicAdd(&lcount[bin[j]], 1u);
+                const uint32_t b = region_of(t, key[j]) >> shift;
+                br[j] = (b << 16) | atomicAdd(&lcount[b], 1u);
             }
         }
         __syncthreads();                                                  // (A)
         if (threadIdx.x < 64) {       // wave 0: scan, heavy flags, the reservation atomic of bins 2 lane, 2 lane + 1
-            const uint32_t lane = threadIdx.x, b0 = 2 * lane;
+            const uint32_t b0 = 2 * lane;
             const uint32_t c0 = lcount[b0], c1 = lcount[b0 + 1];
             uint32_t incl = c0 + c1;
             for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -1067,12 +1104,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
         const bool heavy_tile = any_heavy != 0;
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
-            const uint32_t e = j * T + threadIdx.x;
+            const uint32_t e = eoff(j);
             if (e < cnt) {
-                const uint32_t sp = lstart[bin[j]] + rank[j];
+                const uint32_t sp = lstart[br[j] >> 16] + (br[j] & 0xFFFFu);
                 skey[sp] = key[j];
-                sidx[sp] = (uint32_t)(t0 + e);
-                sbin[sp] = (uint8_t)bin[j];
+                smeta[sp] = e | (br[j] & 0xFFFF0000u);
             }
         }
         if (heavy_tile)
@@ -1080,19 +1116,20 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
         __syncthreads();                                                  // (C)
         if (heavy_tile) {
             // (D) every element of a heavy bin claims its key's entry or folds into the claimer's:
-            // count += c in the entry, read index min into the claimer's sidx, element marked dead.
+            // count += c in the entry, tile offset min into the claimer's meta, element marked dead.
             // Staged elements are bin-sorted, so a wave's lanes often share a hot key: those fold
             // in registers first (one LDS atomic per wave instead of 64 on one address).
             for (uint32_t i0 = 0; i0 < cnt; i0 += T) {
                 const uint32_t i = i0 + threadIdx.x;
-                bool act = i < cnt && hflag[sbin[i]];
+                const uint32_t meta = i < cnt ? smeta[i] : 0u, b = (meta >> 16) & (kCB - 1);
+                bool act = i < cnt && hflag[b];
                 const uint64_t k = act ? skey[i] : 0ull;
-                uint32_t c = 1, mi = act ? sidx[i] : 0xFFFFFFFFu;
+                uint32_t c = 1, mi = act ? (meta & 0xFFFFu) : 0xFFFFFFFFu;
                 const bool was = act;
                 wave_fold<kCoarseFold>(act, k, c, mi);
-                if (was && !act) sbin[i] = 0xFF;                          // folded into its wave leader
+                if (was && !act) smeta[i] = meta | kMetaDead;             // folded into its wave leader
                 if (!act) continue;
-                sidx[i] = mi;
+                smeta[i] = mi | (b << 16);
                 uint32_t h = dedup_home(k, kHtLog);
                 for (;;) {
                     uint32_t e = ht[h];
@@ -1103,8 +1140,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
                     const uint32_t j = (e & 0xFFFFu) - 1;
                     if (skey[j] == k) {
                         atomicAdd(&ht[h], c << 16);
-                        atomicMin(&sidx[j], mi);
-                        sbin[i] = 0xFF;
+                        atomicMin(&smeta[j], mi | (b << 16));   // (same bin: the min is the offset's)
+                        smeta[i] = kMetaDead;
                         break;
                     }
                     h = (h + 1) & (TILE - 1);
@@ -1112,8 +1149,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
             }
             __syncthreads();                                              // (D)
             for (uint32_t i = threadIdx.x; i < cnt; i += T) {
-                const uint32_t b = sbin[i];
-                if (b != 0xFF && hflag[b]) atomicAdd(&hcnt[b], 1u);
+                const uint32_t meta = smeta[i], b = (meta >> 16) & (kCB - 1);
+                if (!(meta & kMetaDead) && hflag[b]) atomicAdd(&hcnt[b], 1u);
             }
             __syncthreads();                                              // (E)
             if (threadIdx.x < 64) {
@@ -1125,32 +1162,34 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
             __syncthreads();                                              // (F)
         }
         for (uint32_t i = threadIdx.x; i < cnt; i += T) {
-            const uint32_t b = sbin[i];
-            if (b == 0xFF) continue;                                      // folded into its claimer
-            uint32_t local, c = 1;
+            const uint32_t meta = smeta[i];
+            if (meta & kMetaDead) continue;                               // folded into its claimer
+            const uint32_t b = (meta >> 16) & (kCB - 1);
+            uint32_t c = 1;
+            uint64_t pos;
             if (heavy_tile && hflag[b]) {
-                local = atomicAdd(&hcnt[b], 1u);
+                pos = (uint64_t)gbase[b] + atomicAdd(&hcnt[b], 1u);
                 uint32_t h = dedup_home(skey[i], kHtLog);
                 while ((ht[h] & 0xFFFFu) != i + 1) h = (h + 1) & (TILE - 1);
                 c = ht[h] >> 16;
             } else {
-                local = i - lstart[b];
+                pos = (uint32_t)(i + sdelta[b]);                          // base + (i - start)
             }
-            const uint64_t pos = (uint64_t)gbase[b] + local;
             const uint64_t k = skey[i];
+            const uint32_t idx = (uint32_t)t0 + (meta & 0xFFFFu);
             if (pos < cap1) {
                 const uint64_t at = (uint64_t)(b * kFinePerBin + sub) * cap1 + pos;
                 Rec12 r;
                 r.klo = (uint32_t)k;
                 r.khi = (uint32_t)(k >> 32);
-                r.idx = c > 1 ? (sidx[i] | kWeighted) : sidx[i];
+                r.idx = c > 1 ? (idx | kWeighted) : idx;
                 ((Rec12*)w.akey)[at] = r;
                 if (!w.slab) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
                 if (c > 1) w.acnt[at] = c;
             } else {
                 const uint64_t sp = (uint64_t)sbase[b] + (pos - max((uint64_t)gbase[b], cap1));
                 if (sp < w.spill_cap)
-                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), c, sidx[i]);
+                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), c, idx);
                 else
                     atomicOr(t.overflow, kOvfTable);
             }
@@ -3437,15 +3476,19 @@ static int insert_impl(ss_counter* c, const uint8_t* d_ascii, uint64_t n, uint32
                 int dev = 0, cus = 0, per = 0;
                 (void)hipGetDevice(&dev);
                 (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL, false>, kPfT, 0);
+                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL, false, true>, kPfT, 0);
                 return (cus > 0 && per > 0) ? cus * per : (int)kPartBlocks;
             }();
             if (keys_in)
-                hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, true>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
+                hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, true, false>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
                                    (const uint4*)keys_in, (uint64_t)0, n, 0u, cap1, c->ws_fill,
                                    (unsigned long long*)nullptr);
+            else if (L == 32)     // 32-nt rows: coalesced lane-pair loads (G16)
+                hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, false, true>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
+                                   (const uint4*)d_ascii, stride / 16, n, 2u, cap1, c->ws_fill,
+                                   (unsigned long long*)d_first_bad);
             else
-                hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, false>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
+                hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, false, false>), dim3(pf_grid), dim3(kPfT), 0, s, t, w,
                                    (const uint4*)d_ascii, stride / 16, n, L / 16, cap1, c->ws_fill,
                                    (unsigned long long*)d_first_bad);
             const unsigned fine_blocks = kCB * kFinePerBin;

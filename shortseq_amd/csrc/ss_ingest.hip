@@ -47,6 +47,7 @@
 #include <array>
 #include <cmath>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <string>
 #include <thread>
@@ -872,6 +873,12 @@ struct ss_ingest {
     uint64_t nkeys = 0, nwords = 0;
     DBuf<uint64_t> slot, ordered, woff, scan;
     DBuf<GDesc> gdesc;
+    // FASTQ stage split since the last ss_ingest_fastq_stages: host ms of the file
+    // reads, device ms of the H2D pieces (event pairs, summed), host ms of the index (to its sync), of
+    // the chunk counts (process_chunk) and of ss_ingest_finish; the bytes the H2D pieces moved
+    double fq_ms[5] = {};
+    uint64_t fq_h2d_bytes = 0;
+    std::vector<hipEvent_t> fq_ev;     // timing events of the H2D pieces (2 per piece)
 };
 
 namespace {
@@ -1854,6 +1861,8 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->groups.clear();
     for (auto& p : g->pool) ss_counter_destroy(p.second);
     g->pool.clear();
+    for (hipEvent_t e : g->fq_ev) (void)hipEventDestroy(e);
+    g->fq_ev.clear();
     g->stage.release();
     g->out_host.release();
     g->dbuf.release(), g->offs.release(), g->dlens.release(), g->order.release(), g->blkhist.release();
@@ -2011,6 +2020,12 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
     int rc = g->stage.ensure(cap);
     uint64_t carry = 0, pos = begin, seqs0 = g->nreads;
     unsigned threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    using Clock = std::chrono::steady_clock;
+    auto since = [](Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); };
+    // The chunk's bytes are read into pinned memory in pieces of kFqPiece, and each piece's H2D goes
+    // out as soon as it is there, so the file reads and the PCIe copies overlap (one read, then one
+    // copy of the whole chunk, ran them back to back: VERDICT r5 item 7).  Two timing events per piece.
+    constexpr uint64_t kFqPiece = 64ull << 20;
     while (!rc) {
         if (cap >= (1ull << 32)) {
             rc = ss_fail(SS_EARG, "a FASTQ line is longer than 2 GiB");
@@ -2018,7 +2033,34 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
         }
         uint8_t* hv = g->stage.p;
         const uint64_t want = std::min(cap - carry, size - std::min(size, pos));
-        const uint64_t got = read_parallel(fd, hv + carry, want, pos, threads);
+        if ((rc = g->dbuf.ensure(cap + 16))) break;
+        const uint64_t npieces = (want + kFqPiece - 1) / kFqPiece + 1;
+        while (g->fq_ev.size() < 2 * npieces && !rc) {
+            hipEvent_t e = nullptr;
+            rc = ss_check(hipEventCreate(&e), "ingest fastq event");
+            if (!rc) g->fq_ev.push_back(e);
+        }
+        if (rc) break;
+        uint64_t got = 0, np = 0;
+        auto h2d = [&](uint64_t off, uint64_t len) {
+            int r = ss_check(hipEventRecord(g->fq_ev[2 * np], s), "ingest fastq event");
+            if (!r) r = ss_check(hipMemcpyAsync(g->dbuf.p + off, hv + off, len, hipMemcpyHostToDevice, s), "ingest H2D");
+            if (!r) r = ss_check(hipEventRecord(g->fq_ev[2 * np + 1], s), "ingest fastq event");
+            ++np;
+            g->fq_h2d_bytes += len;
+            return r;
+        };
+        if (carry) rc = h2d(0, carry);     // the previous chunk's tail, already in pinned memory
+        for (uint64_t off = 0; off < want && !rc; off += kFqPiece) {
+            const uint64_t len = std::min(kFqPiece, want - off);
+            const auto t0 = Clock::now();
+            const uint64_t r = read_parallel(fd, hv + carry + off, len, pos + off, threads);
+            g->fq_ms[0] += since(t0);
+            got += r;
+            if (r != len) break;
+            rc = h2d(carry + off, len);
+        }
+        if (rc) break;
         if (got != want) {
             rc = ss_fail(SS_EHIP, "short read of the FASTQ file");
             break;
@@ -2036,6 +2078,7 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
                     break;
                 }
             if (use == 0) {     // one line fills the chunk: grow the staging buffer, keep its bytes
+                if ((rc = ss_check(hipStreamSynchronize(s), "ingest fastq grow"))) break;   // (its H2D pieces)
                 HBuf grown;
                 if ((rc = grown.ensure(2 * cap))) break;
                 memcpy(grown.p, hv, n);
@@ -2046,9 +2089,8 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
                 continue;
             }
         }
-        // index the chunk on the device
-        if ((rc = g->dbuf.ensure(use + 16))) break;
-        rc = ss_check(hipMemcpyAsync(g->dbuf.p, hv, use, hipMemcpyHostToDevice, s), "ingest H2D");
+        // index the chunk on the device (its bytes are on the way: the pieces' H2D copies above)
+        const auto ti = Clock::now();
         uint64_t maxr = use / 16 + 2;
         uint64_t nl = 0, nrec = 0;
         while (!rc) {
@@ -2071,8 +2113,16 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
             maxr = nrec;
         }
         if (rc) break;
+        g->fq_ms[2] += since(ti);
+        for (uint64_t q = 0; q < np; ++q) {     // the pieces' H2D times (all complete: the index synced)
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, g->fq_ev[2 * q], g->fq_ev[2 * q + 1]) == hipSuccess) g->fq_ms[1] += ms;
+            else (void)hipGetLastError();
+        }
         if (!at_eof && g->est_scale == 1.0 && use) g->est_scale = (double)(size - begin) / (double)use;
+        const auto tc = Clock::now();
         rc = process_chunk(g, g->dbuf.p, g->offs.p, g->dlens.p, use, nrec, 0, nullptr, hv);
+        g->fq_ms[3] += since(tc);
         if (rc) break;
         line0 += nl;
         if (at_eof || g->bad_index != kNoSlot) break;
@@ -2095,7 +2145,27 @@ int ss_ingest_error(ss_ingest* g, uint64_t* h_index, int* h_kind, uint8_t* h_rea
     return SS_OK;
 }
 
+static int finish_impl(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords);
+
 int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = finish_impl(g, h_nkeys, h_nwords);
+    if (g) g->fq_ms[4] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int ss_ingest_fastq_stages(ss_ingest* g, double* h_ms, uint64_t* h_h2d_bytes) {
+    if (!g || !h_ms || !h_h2d_bytes) return ss_fail(SS_EARG, "null argument");
+    for (int i = 0; i < 5; ++i) {
+        h_ms[i] = g->fq_ms[i];
+        g->fq_ms[i] = 0;
+    }
+    *h_h2d_bytes = g->fq_h2d_bytes;
+    g->fq_h2d_bytes = 0;
+    return SS_OK;
+}
+
+static int finish_impl(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords) {
     if (!g || !h_nkeys || !h_nwords) return ss_fail(SS_EARG, "null argument");
     if (g->failed) return ss_fail(SS_EFULL, "ingest: an earlier add ran a table full; reset and count again");
     (void)hipSetDevice(g->device);

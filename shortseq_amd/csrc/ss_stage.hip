@@ -16,9 +16,15 @@
 // torch.pin_memory) are DMA'd directly and the host copies disappear.  The slowest of PCIe, the
 // staging copies and the kernel bounds the rate: this is the PCIe-inclusive path, never the
 // device-resident roofline number.
+#include <ctype.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <new>
@@ -33,8 +39,17 @@ namespace {
 // thread takes part 0 and blocks until every part is done.
 class CopyPool {
   public:
-    explicit CopyPool(int nthreads) {
-        for (int i = 0; i < nthreads; ++i) th_.emplace_back([this, i] { worker(i); });
+    // cpus: where the workers run (worker i on cpus[i % size]); empty = wherever the OS puts them
+    CopyPool(int nthreads, const std::vector<int>& cpus) {
+        for (int i = 0; i < nthreads; ++i) {
+            th_.emplace_back([this, i] { worker(i); });
+            if (!cpus.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                CPU_SET(cpus[i % cpus.size()], &set);
+                (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof(set), &set);
+            }
+        }
     }
     ~CopyPool() {
         {
@@ -107,7 +122,8 @@ struct Slot {
     uint64_t* d_fb = nullptr;   // the chunk's first-bad read (chunk-relative)
     uint64_t* h_fb = nullptr;   // pinned copy of it
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_out = nullptr;
-    bool busy = false;
+    hipEvent_t ev_h0 = nullptr, ev_k0 = nullptr, ev_o0 = nullptr;   // stage starts (ss_stager_set_timing)
+    bool busy = false, timed = false;
     uint64_t base = 0, m = 0;
 };
 
@@ -147,6 +163,15 @@ struct ss_stager {
     hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
     CopyPool* pool = nullptr;
     bool out2_ready = false;
+    // placement: copy threads, CPUs in the process's affinity mask, the GPU's NUMA
+    // node (-1: unknown), CPUs the copy threads were pinned to (the node's CPUs in the mask; 0: none)
+    int copy_threads = 0, affinity_cpus = 0, numa_node = -1, pinned_cpus = 0;
+    // stage split (ss_stager_set_timing): host ms of the pageable -> pinned copies, the pinned ->
+    // pageable copies and the waits on the D2H events; device ms of H2D, kernel, D2H (event pairs per
+    // chunk); calls since the last ss_stager_stats
+    bool timing = false;
+    double ms[6] = {};
+    uint64_t calls = 0;
 };
 
 namespace {
@@ -169,6 +194,9 @@ void free_stager(ss_stager* st) {
         if (s.ev_in) (void)hipEventDestroy(s.ev_in);
         if (s.ev_k) (void)hipEventDestroy(s.ev_k);
         if (s.ev_out) (void)hipEventDestroy(s.ev_out);
+        if (s.ev_h0) (void)hipEventDestroy(s.ev_h0);
+        if (s.ev_k0) (void)hipEventDestroy(s.ev_k0);
+        if (s.ev_o0) (void)hipEventDestroy(s.ev_o0);
     }
     if (st->s_in) (void)hipStreamDestroy(st->s_in);
     if (st->s_k) (void)hipStreamDestroy(st->s_k);
@@ -189,13 +217,32 @@ int ensure_out2(ss_stager* st) {
 }
 
 // Wait for a slot's chunk, move its outputs to the user buffers, fold in its first-bad read.
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
+
 int drain(ss_stager* st, Slot& s, const HostOp& op, bool out_pinned, bool out2_pinned, uint64_t* first_bad) {
     if (!s.busy) return SS_OK;
     s.busy = false;
+    auto t0 = Clock::now();
     int rc = ss_check(hipEventSynchronize(s.ev_out), "hipEventSynchronize(d2h)");
     if (rc) return rc;
+    st->ms[5] += ms_since(t0);
+    if (s.timed) {     // every event of the chunk has completed (the D2H waited on the kernel, it on the H2D)
+        float a = 0, b = 0, c = 0;
+        if (hipEventElapsedTime(&a, s.ev_h0, s.ev_in) == hipSuccess && hipEventElapsedTime(&b, s.ev_k0, s.ev_k) == hipSuccess &&
+            hipEventElapsedTime(&c, s.ev_o0, s.ev_out) == hipSuccess) {
+            st->ms[2] += a;
+            st->ms[3] += b;
+            st->ms[4] += c;
+        } else {
+            (void)hipGetLastError();
+        }
+        s.timed = false;
+    }
+    t0 = Clock::now();
     if (!out_pinned) st->pool->copy(op.h_out + s.base * op.out_bpr, s.h_out, s.m * op.out_bpr);
     if (op.h_out2 && !out2_pinned) st->pool->copy(op.h_out2 + s.base * op.out2_bpr, s.h_out2, s.m * op.out2_bpr);
+    st->ms[1] += ms_since(t0);
     if (op.has_fb && *s.h_fb != ~0ull && *first_bad == ~0ull) *first_bad = s.base + *s.h_fb;
     return SS_OK;
 }
@@ -216,6 +263,7 @@ int run(ss_stager* st, const HostOp& op, uint64_t n, uint64_t* h_first_bad) {
     uint64_t first_bad = ~0ull;
     const uint32_t ns = (uint32_t)st->slots.size();
     const uint64_t nchunks = (n + rpc - 1) / rpc;
+    if (st->timing) ++st->calls;
     for (uint64_t k = 0; k < nchunks && !rc; ++k) {
         Slot& s = st->slots[k % ns];
         if ((rc = drain(st, s, op, out_pinned, out2_pinned, &first_bad))) break;
@@ -224,15 +272,21 @@ int run(ss_stager* st, const HostOp& op, uint64_t n, uint64_t* h_first_bad) {
         const uint8_t* src = op.h_in + s.base * op.in_bpr;
         const size_t in_b = s.m * op.in_bpr;
         if (!in_pinned) {
+            const auto t0 = Clock::now();
             st->pool->copy(s.h_in, src, in_b);
+            st->ms[0] += ms_since(t0);
             src = s.h_in;
         }
-        rc = ss_check(hipMemcpyAsync(s.d_in, src, in_b, hipMemcpyHostToDevice, st->s_in), "H2D");
+        s.timed = st->timing && s.ev_h0;
+        if (s.timed) rc = ss_check(hipEventRecord(s.ev_h0, st->s_in), "hipEventRecord");
+        if (!rc) rc = ss_check(hipMemcpyAsync(s.d_in, src, in_b, hipMemcpyHostToDevice, st->s_in), "H2D");
         if (!rc) rc = ss_check(hipEventRecord(s.ev_in, st->s_in), "hipEventRecord");
         if (!rc) rc = ss_check(hipStreamWaitEvent(st->s_k, s.ev_in, 0), "hipStreamWaitEvent");
+        if (!rc && s.timed) rc = ss_check(hipEventRecord(s.ev_k0, st->s_k), "hipEventRecord");
         if (!rc) rc = op.launch(op, s.d_in, s.m, s.d_out, s.d_out2, s.d_fb, st->s_k);
         if (!rc) rc = ss_check(hipEventRecord(s.ev_k, st->s_k), "hipEventRecord");
         if (!rc) rc = ss_check(hipStreamWaitEvent(st->s_out, s.ev_k, 0), "hipStreamWaitEvent");
+        if (!rc && s.timed) rc = ss_check(hipEventRecord(s.ev_o0, st->s_out), "hipEventRecord");
         if (!rc) {
             uint8_t* dst = out_pinned ? op.h_out + s.base * op.out_bpr : s.h_out;
             rc = ss_check(hipMemcpyAsync(dst, s.d_out, s.m * op.out_bpr, hipMemcpyDeviceToHost, st->s_out), "D2H");
@@ -267,9 +321,99 @@ int launch_decode(const HostOp& op, const uint8_t* d_in, uint64_t m, uint8_t* d_
     return ss_decode_fixed((const uint64_t*)d_in, m, op.L, op.wpr, d_out, op.stride, s);
 }
 
+// CPUs of a sysfs cpulist ("0-7,64-71")
+std::vector<int> parse_cpulist(const char* path) {
+    std::vector<int> out;
+    FILE* f = fopen(path, "r");
+    if (!f) return out;
+    char buf[4096];
+    const size_t len = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[len] = 0;
+    for (char* p = buf; *p;) {
+        char* e = nullptr;
+        const long a = strtol(p, &e, 10);
+        if (e == p) break;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = strtol(p + 1, &e, 10);
+            p = e;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c) out.push_back((int)c);
+        while (*p == ',' || *p == '\n' || *p == ' ') ++p;
+    }
+    return out;
+}
+
+// The copy threads' CPUs: the GPU's NUMA node's CPUs (sysfs, by PCI bus id) that the process's
+// affinity mask allows; empty when the node is unknown, the intersection is empty, or
+// SHORTSEQ_STAGE_PIN=0.  Fills the stager's placement fields.
+std::vector<int> placement(ss_stager* st) {
+    cpu_set_t mask;
+    CPU_ZERO(&mask);
+    std::vector<int> allowed;
+    if (sched_getaffinity(0, sizeof(mask), &mask) == 0)
+        for (int c = 0; c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &mask)) allowed.push_back(c);
+    st->affinity_cpus = (int)allowed.size();
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), st->device) != hipSuccess) {
+        (void)hipGetLastError();
+        return {};
+    }
+    for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+    char path[256];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE* f = fopen(path, "r");
+    int node = -1;
+    if (f) {
+        if (fscanf(f, "%d", &node) != 1) node = -1;
+        fclose(f);
+    }
+    st->numa_node = node;
+    const char* env = getenv("SHORTSEQ_STAGE_PIN");
+    if (node < 0 || (env && env[0] == '0')) return {};
+    snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+    std::vector<int> mine;
+    for (int c : parse_cpulist(path))
+        if (std::find(allowed.begin(), allowed.end(), c) != allowed.end()) mine.push_back(c);
+    st->pinned_cpus = (int)mine.size();
+    return mine;
+}
+
 }  // namespace
 
 extern "C" {
+
+int ss_stager_set_timing(ss_stager* st, int on) {
+    if (!st) return ss_fail(SS_EARG, "null stager");
+    int rc = ss_check(hipSetDevice(st->device), "hipSetDevice");
+    for (Slot& s : st->slots) {
+        if (rc || !on || s.ev_h0) break;
+        rc = ss_check(hipEventCreate(&s.ev_h0), "hipEventCreate");
+        if (!rc) rc = ss_check(hipEventCreate(&s.ev_k0), "hipEventCreate");
+        if (!rc) rc = ss_check(hipEventCreate(&s.ev_o0), "hipEventCreate");
+    }
+    if (rc) return rc;
+    st->timing = on != 0;
+    return SS_OK;
+}
+
+int ss_stager_stats(ss_stager* st, double* h_ms, int32_t* h_info) {
+    if (!st || !h_ms || !h_info) return ss_fail(SS_EARG, "null argument");
+    const double k = st->calls ? 1.0 / (double)st->calls : 0.0;
+    for (int i = 0; i < 6; ++i) {
+        h_ms[i] = st->ms[i] * k;
+        st->ms[i] = 0;
+    }
+    h_info[0] = st->copy_threads;
+    h_info[1] = st->affinity_cpus;
+    h_info[2] = st->numa_node;
+    h_info[3] = st->pinned_cpus;
+    st->calls = 0;
+    return SS_OK;
+}
 
 int ss_stager_create(int device, uint64_t chunk_bytes, uint32_t nslots, uint32_t copy_threads,
                      ss_stager** h_out) {
@@ -296,15 +440,18 @@ int ss_stager_create(int device, uint64_t chunk_bytes, uint32_t nslots, uint32_t
         if (!rc) rc = ss_check(hipMalloc((void**)&s.d_in, chunk_bytes), "hipMalloc");
         if (!rc) rc = ss_check(hipMalloc((void**)&s.d_out, chunk_bytes), "hipMalloc");
         if (!rc) rc = ss_check(hipMalloc((void**)&s.d_fb, sizeof(uint64_t)), "hipMalloc");
-        if (!rc) rc = ss_check(hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming), "hipEventCreate");
-        if (!rc) rc = ss_check(hipEventCreateWithFlags(&s.ev_k, hipEventDisableTiming), "hipEventCreate");
-        if (!rc) rc = ss_check(hipEventCreateWithFlags(&s.ev_out, hipEventDisableTiming), "hipEventCreate");
+        // (timing-capable: they also end the stage spans of ss_stager_set_timing)
+        if (!rc) rc = ss_check(hipEventCreate(&s.ev_in), "hipEventCreate");
+        if (!rc) rc = ss_check(hipEventCreate(&s.ev_k), "hipEventCreate");
+        if (!rc) rc = ss_check(hipEventCreate(&s.ev_out), "hipEventCreate");
     }
     if (rc) {
         free_stager(st);
         return rc;
     }
-    st->pool = new (std::nothrow) CopyPool((int)copy_threads);
+    st->copy_threads = (int)copy_threads;
+    const std::vector<int> cpus = placement(st);
+    st->pool = new (std::nothrow) CopyPool((int)copy_threads, cpus);
     if (!st->pool) {
         free_stager(st);
         return ss_fail(SS_ENOMEM, "copy pool");

@@ -112,6 +112,23 @@ def exchange_rows(rows: torch.Tensor, part_counts, group=None, flag: int = 0):
     return recv, rc_l, 0
 
 
+def rank_spread(per_rank: list) -> dict:
+    """Per-rank diagnostic dicts (ShardedCounter.count(stats=...)) -> {field: [min, max]} for the
+    numeric fields, plus the backend and the world size every rank saw (a list if they differ)."""
+    out = {}
+    if not per_rank:
+        return out
+    for k in per_rank[0]:
+        vals = [d.get(k) for d in per_rank]
+        if k in ("backend", "world"):
+            u = sorted(set(vals), key=str)
+            out[k] = u[0] if len(u) == 1 else u
+        elif all(isinstance(v, (int, float)) and not isinstance(v, bool) for v in vals) and k != "rank":
+            out[k] = [min(vals), max(vals)]
+    out["ranks"] = len(per_rank)
+    return out
+
+
 def agree_flag(flag: int, device, group=None) -> int:
     """The largest of every rank's flag (one all_reduce MAX): a check that raises on one rank raises
     on all of them, so none is left waiting in the next collective."""
@@ -183,12 +200,34 @@ class ShardedCounter:
     def close(self) -> None:
         self.local.close()
 
-    def count(self, ascii_local: torch.Tensor, L: int, base_index: int, check_errors: bool = True):
+    def _sync(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def count(self, ascii_local: torch.Tensor, L: int, base_index: int, check_errors: bool = True,
+              stats: Optional[dict] = None):
         """Count this rank's shard (global read indices base_index ...) and run the exchange.
-        Returns the rank's table; its owned regions hold the exact counts afterwards."""
+        Returns the rank's table; its owned regions hold the exact counts afterwards.
+        stats (a diagnostic run): the device is synchronised around each phase and
+        the dict receives local_ms (reset + insert), pack_ms, a2a_ms (both all-to-alls and their host
+        sync), merge_ms, records / bytes sent and received, the backend and the world size seen."""
+        import time
+        clk = []
+
+        def mark():
+            if stats is not None:
+                self._sync()
+                clk.append(time.perf_counter())
+
+        mark()
         self.L = L
         self.local.reset()
         self.local.insert(ascii_local, L, base_index=base_index, check_errors=check_errors)
+        mark()
+        if stats is not None:
+            stats.update(world=self.world, rank=self.rank,
+                         backend=dist.get_backend(self.group) if dist.is_initialized() else "none",
+                         local_ms=(clk[1] - clk[0]) * 1e3)
         if self.world == 1:
             return self.local
         if L > 32:
@@ -196,9 +235,11 @@ class ShardedCounter:
             return self.local
         # the other owners' regions as 16-B records (the rank's own part stays in its table)
         rec, parts = self.local.pack_ranges(self.world, skip=self.rank, first_base=base_index)
+        mark()
         # the table's overflow word rides along the exchange's one host sync
         recv, rsizes, rbases, ovf = exchange_packed(rec, parts, base_index, group=self.group,
                                                      extra=self.local.overflow_word())
+        mark()
         if ovf[0]:
             raise RuntimeError("counter pack overflow (a count or first index past 32 bits, or the table)")
         runs, pos = [], 0
@@ -207,6 +248,12 @@ class ShardedCounter:
                 runs.append((pos, pos + n, rbases[src]))
             pos += n
         self.local.merge_packed(recv, runs, self.rank, self.world, L)
+        mark()
+        if stats is not None:
+            sent = int(parts.to(torch.int64).sum().item()) - int(parts[self.rank].item() if parts.numel() > self.rank else 0)
+            stats.update(pack_ms=(clk[2] - clk[1]) * 1e3, a2a_ms=(clk[3] - clk[2]) * 1e3,
+                         merge_ms=(clk[4] - clk[3]) * 1e3, records_sent=sent, bytes_sent=16 * sent,
+                         records_received=int(sum(rsizes)), bytes_received=16 * int(sum(rsizes)))
         return self.local
 
     def _exchange_words(self) -> None:

@@ -317,3 +317,54 @@ def test_sharded_counter_overflow_raises_on_every_rank(L):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == {r: "overflow" for r in range(world)}
+
+
+def _worker_stats(rank, world, port, n, L, U, q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from shortseq_amd.dist import ShardedCounter, rank_spread
+        per = n // world
+        a = oracle.gen_pool_reads(5, 6, U, rank * per, per, L)
+        sc = ShardedCounter(1 << 14, device="cpu", table_factory=HostTable)
+        st = {}
+        sc.count(torch.from_numpy(a).view(per, L), L, base_index=rank * per, stats=st)
+        allst = [None] * world
+        dist.all_gather_object(allst, st)
+        res = sc.gather_items(dst=0)
+        if rank == 0:
+            q.put((allst, rank_spread(allst), len(res[0])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_stats_fields_gloo():
+    """The N > 1 bench line's per-rank split (unmeasured on GPU hardware: the
+    driver's 8-GPU run is the first): ShardedCounter.count(stats=...) over 2 gloo ranks fills local /
+    pack / all-to-all / merge ms, records and bytes sent and received, the backend and the world size;
+    what the ranks sent equals what they received, and rank_spread gives [min, max] per field."""
+    n, L, U, world = 3000, 32, 200, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_stats, args=(r, world, port, n, L, U, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    allst, spread, uniq = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for k in ("local_ms", "pack_ms", "a2a_ms", "merge_ms", "records_sent", "bytes_sent", "records_received",
+              "bytes_received", "backend", "world"):
+        assert all(k in d for d in allst), k
+    assert [d["rank"] for d in allst] == [0, 1]
+    assert all(d["world"] == 2 and d["backend"] == "gloo" for d in allst)
+    assert sum(d["records_sent"] for d in allst) == sum(d["records_received"] for d in allst) > 0
+    assert all(d["bytes_sent"] == 16 * d["records_sent"] for d in allst)
+    assert spread["backend"] == "gloo" and spread["world"] == 2 and spread["ranks"] == 2
+    for k in ("local_ms", "pack_ms", "a2a_ms", "merge_ms", "records_sent"):
+        lo, hi = spread[k]
+        assert lo <= hi and lo == min(d[k] for d in allst)
+    assert "rank" not in spread and uniq == U

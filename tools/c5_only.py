@@ -18,5 +18,6 @@ zs = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-el, d, u, _chk, _passes = bench.bench_counter(B, lib(), dev, 0, 1, 125_000_000, 32, 1 << ulog, steps, 3, zipf=zs or None)
-print(f"C5 U=2^{ulog} zipf={zs}: {el / steps * 1e3:.3f} ms/step wall, {d:.3f} ms device, unique {u}", flush=True)
+el, d, u, _chk, passes, _x = bench.bench_counter(B, lib(), dev, 0, 1, 125_000_000, 32, 1 << ulog, steps, 3, zipf=zs or None)
+pp = " ".join(f"{k} {v:.3f}" for k, v in passes.items())
+print(f"C5 U=2^{ulog} zipf={zs}: {el / steps * 1e3:.3f} ms/step wall, {d:.3f} ms device, unique {u} [{pp}]", flush=True)
