@@ -152,11 +152,12 @@ int ss_hamming_all_pairs(const uint64_t* d_words, uint64_t n, uint32_t L, uint32
 
 /* Method of ss_hamming_all_pairs_ex; every method gives the same counts, total and pair set.
  * TILES: every pair checked (MFMA one-hot tiles for L <= 128, bit-plane tiles above).
- * PIGEONHOLE (L <= 32, max_dist < 16): the min(L + 1, 32) positions split into max_dist + 1
- *   segments; only pairs with an equal segment are checked (bucketed per segment on the device).
+ * PIGEONHOLE (L <= 128, max_dist < 16): the min(L + 1, 32 W) positions split into max_dist + 1
+ *   segments (W = ceil(L/32) words; a segment may cross a word boundary); only pairs with an equal
+ *   segment are checked (bucketed per segment on the device; a segment past 11 nt by a hash).
  *   Blocks the calling thread once on the stream (the candidate totals are read back) only in AUTO;
  *   forced, it queues everything.  Its scratch lives on the device that holds d_words.
- * AUTO: PIGEONHOLE when L <= 32, segments >= 3 nt, n >= 32768 and the bucket histogram shows fewer
+ * AUTO: PIGEONHOLE when L <= 128, segments >= 3 nt, n >= 32768 and the bucket histogram shows fewer
  *   than 1/16 of all pairs as candidates; TILES otherwise.  A stream under hipGraph capture always
  *   gets TILES in AUTO (no allocation, no host read-back: the call stays capturable). */
 #define SS_ALLPAIRS_AUTO 0u

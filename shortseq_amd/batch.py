@@ -616,7 +616,7 @@ def hamming_all_pairs(words: torch.Tensor, L: int, max_dist: int, *, counts: boo
     """Unordered pairs (i < j) of a packed batch within `max_dist` (the reference __xor__ distance)
     -> (neighbour counts int32 [n] or None, pairs int32 [m, 2] or None, total pairs).  Pairs are
     returned sorted; at most max_pairs are kept (0: count only).  method: "tiles" checks every pair,
-    "pigeonhole" (L <= 32) only pairs sharing one of max_dist + 1 segments, "auto" picks
+    "pigeonhole" (L <= 128) only pairs sharing one of max_dist + 1 segments, "auto" picks
     (ss_hamming_all_pairs_ex); the results are the same."""
     _require_cuda(words, "words")
     n, wpr = words.shape

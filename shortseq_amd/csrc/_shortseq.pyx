@@ -1040,7 +1040,7 @@ def _read_and_count_fastq_gpu(filename, devs, uint64_t chunk_bytes=0):
             g = <size_t>_engine(devs[k])
             engines.append((devs[k], g))
             if _abi.fq_stages != NULL:
-                _abi.fq_stages(<ss_ingest*>g, st_ms, &st_bytes)     # (drop what earlier calls left)
+                _abi.fq_stages(<ss_ingest*><size_t>g, st_ms, &st_bytes)     # (drop what earlier calls left)
             jobs.append((g, 1, 0, 0, 0, fname, begin[k], begin[k + 1], line0[k], chunk_bytes, None))
         per = _run_shard_jobs(jobs)
         nseqs = sum(per)

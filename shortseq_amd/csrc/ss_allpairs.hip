@@ -411,6 +411,10 @@ struct PigArgs {
     uint32_t wpr, k, G, nbmax, maxtiles, exact;   // exact: bit g = segment g buckets by value
     uint32_t shift[kPigMaxG], nb[kPigMaxG];
     uint64_t mask[kPigMaxG];
+    // multi-word reads (W = 2 .. 4, L 33 .. 128; k_pigw_*): segment g = positions [seg[g], seg[g + 1])
+    // of the row's 32 W positions (it may cross a word boundary)
+    uint32_t W;
+    uint32_t seg[kPigMaxG + 1];
     uint32_t* hist;       // G << nbmax: counts, then bucket starts (k_pig_apply)
     uint32_t* tile_cnt;   // G * maxtiles: bucket sums, then tile bases
     uint64_t* tile_cand;  // G * maxtiles
@@ -722,6 +726,160 @@ __global__ __launch_bounds__(256) void k_pig_pairs(PigArgs a) {
     if (threadIdx.x == 0 && s_hits) atomicAdd(a.npairs, s_hits);
 }
 
+// ---- Multi-word reads (W = 2 .. 4 words: 33 .. 128 nt).  The same pigeonhole
+// argument over the P = min(L + 1, 32 W) compared positions of the row: G = k + 1 contiguous segments
+// (a segment may cross a word boundary and be longer than 32 positions).  A segment's bucket is its
+// value when it has <= nbmax bits, else a hash of its (up to 128-bit) value; equality, the distance
+// and the first-equal-segment rule are decided on the words of both rows, so a hash collision only
+// adds candidates.  Rows live W words apiece in the bucket-ordered arrays (sw: G x n x W words).
+template <int W>
+__device__ __forceinline__ void pig_row(const PigArgs& a, uint64_t i, uint64_t (&w)[W]) {
+#pragma unroll
+    for (int q = 0; q < W; ++q) w[q] = a.words[i * a.wpr + q];
+}
+// bits [2 b0, 2 b0 + 64) of a row (b0 in positions, < 32 W)
+template <int W>
+__device__ __forceinline__ uint64_t row_bits64(const uint64_t (&w)[W], uint32_t b0) {
+    const uint32_t q = b0 >> 5, sh = 2u * (b0 & 31u);
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        if ((uint32_t)k == q) lo = w[k];
+        if ((uint32_t)k == q + 1u) hi = w[k];
+    }
+    return sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+}
+template <int W>
+__device__ __forceinline__ uint32_t pigw_bucket(const PigArgs& a, uint32_t g, const uint64_t (&w)[W]) {
+    const uint32_t p0 = a.seg[g], len = a.seg[g + 1] - p0;
+    if ((a.exact >> g) & 1u) return (uint32_t)(row_bits64<W>(w, p0) & ((1ull << (2u * len)) - 1ull));
+    uint64_t h = 0x243F6A8885A308D3ull ^ len;
+    for (uint32_t b = 0; b < len; b += 32) {          // the segment's 64-bit pieces, the last masked
+        const uint32_t m = len - b < 32u ? len - b : 32u;
+        uint64_t v = row_bits64<W>(w, p0 + b);
+        if (m < 32u) v &= (1ull << (2u * m)) - 1ull;
+        h = (h ^ v) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+    }
+    return (uint32_t)(h >> (64 - a.nb[g]));
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_pigw_hist(PigArgs a) {
+    if (a.zero_out && blockIdx.x == 0 && threadIdx.x == 0) *a.npairs = 0ull;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256) {
+        if (a.zero_out && a.counts) a.counts[i] = 0u;
+        uint64_t w[W];
+        pig_row<W>(a, i, w);
+        for (uint32_t g = 0; g < a.G; ++g)
+            a.rank[g * a.n + i] = atomicAdd(&a.hist[((uint64_t)g << a.nbmax) + pigw_bucket<W>(a, g, w)], 1u);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_pigw_scatter(PigArgs a) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256) {
+        uint64_t w[W];
+        pig_row<W>(a, i, w);
+        for (uint32_t g = 0; g < a.G; ++g) {
+            const uint64_t pos = a.hist[((uint64_t)g << a.nbmax) + pigw_bucket<W>(a, g, w)] + a.rank[g * a.n + i];
+            uint64_t* dst = a.sw + ((uint64_t)g * a.n + pos) * W;
+#pragma unroll
+            for (int q = 0; q < W; ++q) dst[q] = w[q];
+            a.sid[g * a.n + pos] = (uint32_t)i;
+        }
+    }
+}
+
+// one lane per row in bucket order of segment g = blockIdx.y, each walking its own bucket run (p, end)
+// with kPigStep rows in flight (consecutive lanes on consecutive rows: coalesced).  A candidate is a
+// hit when its distance is <= k and g is the first segment the rows agree on: the <= k differing
+// positions are walked and their segments marked (segment of a position: the boundaries in a.seg).
+template <int W>
+__global__ __launch_bounds__(256) void k_pigw_pairs(PigArgs a) {
+    __shared__ uint2 pbuf[4][kPairBuf];
+    __shared__ unsigned long long s_hits;
+    if (threadIdx.x == 0) s_hits = 0;
+    __syncthreads();
+    const uint32_t g = blockIdx.y, lane = threadIdx.x & 63u;
+    const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool valid = p < a.n;
+    const uint64_t* sw = a.sw + (uint64_t)g * a.n * W;
+    const uint32_t* sid = a.sid + g * a.n;
+    const uint32_t* start = a.hist + ((uint64_t)g << a.nbmax);
+    const uint32_t nbk = 1u << a.nb[g];
+    uint64_t w[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) w[q] = valid ? sw[p * W + q] : 0ull;
+    const uint32_t id = valid ? sid[p] : 0u;
+    const uint32_t b = pigw_bucket<W>(a, g, w);
+    const uint64_t end = valid ? (b + 1 < nbk ? start[b + 1] : a.n) : 0ull;
+    constexpr uint64_t kLo = 0x5555555555555555ull;
+    const uint32_t kmax = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.k);
+    const uint32_t want = (1u << g) - 1u;             // segments 0 .. g - 1 differ, g agrees
+    WaveHits wh;
+    wh.buf = pbuf[threadIdx.x >> 6];
+    uint32_t row = 0;
+    constexpr int kPigStep = 4;
+    uint64_t nx[kPigStep][W];
+#pragma unroll
+    for (int u = 0; u < kPigStep; ++u)
+#pragma unroll
+        for (int q = 0; q < W; ++q) nx[u][q] = p + 1 + u < end ? sw[(p + 1 + u) * W + q] : 0ull;
+    for (uint64_t q0 = p + 1;; q0 += kPigStep) {
+        if (!__ballot(q0 < end)) break;
+        uint64_t cur[kPigStep][W];
+#pragma unroll
+        for (int u = 0; u < kPigStep; ++u) {
+            const uint64_t qn = q0 + kPigStep + u;
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                cur[u][q] = nx[u][q];
+                nx[u][q] = qn < end ? sw[qn * W + q] : 0ull;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kPigStep; ++u) {
+            const uint64_t qq = q0 + u;
+            uint64_t d[W];
+            uint32_t dd = 0;
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const uint64_t x = w[q] ^ cur[u][q];
+                d[q] = (x | (x >> 1)) & kLo;
+                dd += (uint32_t)__popcll(d[q]);
+            }
+            bool hit = (qq < end) & (dd <= kmax);
+            if (hit) {     // the segments the differing positions fall in
+                uint32_t segs = 0;
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    uint64_t m = d[q];
+                    while (m) {
+                        const uint32_t pos = 32u * q + ((uint32_t)__ffsll((long long)m) - 1u) / 2u;
+                        uint32_t sgi = 0;
+                        while (sgi + 1 < a.G && pos >= a.seg[sgi + 1]) ++sgi;
+                        segs |= 1u << sgi;
+                        m &= m - 1ull;
+                    }
+                }
+                hit = (segs & (want | (1u << g))) == want;
+            }
+            const uint64_t mask = __ballot(hit);
+            if (!mask) continue;
+            const uint32_t jd = hit ? sid[qq] : 0u;
+            row += hit ? 1u : 0u;
+            if (hit && a.counts) atomicAdd(&a.counts[jd], 1u);
+            hits_add(a, wh, hit, mask, id, jd);
+        }
+    }
+    if (a.pairs) hits_flush(a, wh);
+    else if (lane == 0 && wh.nh) atomicAdd(&s_hits, (unsigned long long)wh.nh);
+    if (a.counts && row) atomicAdd(&a.counts[id], row);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_hits) atomicAdd(a.npairs, s_hits);
+}
+
 // Per-device scratch of the pigeonhole form, grow-only and stream-ordered: a call holds the device's
 // lock, waits (on its stream) for the previous call's kernels before reusing the buffer, and records
 // its own end.
@@ -748,6 +906,7 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     a.max_pairs = b.max_pairs;
     a.npairs = b.npairs;
     a.zero_out = 1;
+    a.W = b.W;
     uint32_t lg = 0;
     while ((1ull << lg) < a.n) ++lg;
     a.nbmax = lg < 10 ? 10 : (lg > kPigMaxBits ? kPigMaxBits : lg);
@@ -762,8 +921,10 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
         a.mask[g] = len >= 32 ? ~0ull : ((1ull << (2 * len)) - 1ull);
         a.nb[g] = 2 * len < a.nbmax ? 2 * len : a.nbmax;
         if (2 * len <= a.nbmax) a.exact |= 1u << g;
+        a.seg[g] = pos;
         pos += len;
     }
+    a.seg[a.G] = P;
     // the scratch, its event and the pinned totals belong to the device that holds the words (the
     // kernels run there, on the caller's stream), not to whichever device is current
     int cur = 0, dev = 0;
@@ -787,7 +948,7 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     PigScratch& ps = g_pig[dev];
     std::lock_guard<std::mutex> lock(ps.mu);
     const size_t hist_n = (size_t)a.G << a.nbmax, tiles_n = (size_t)a.G * a.maxtiles;
-    const size_t need = tiles_n * 8 + a.G * 8 + (hist_n + 2) * 4 + tiles_n * 4 + 64 + (size_t)a.G * a.n * 16;
+    const size_t need = tiles_n * 8 + a.G * 8 + (hist_n + 2) * 4 + tiles_n * 4 + 64 + (size_t)a.G * a.n * (8 * a.W + 8);
     if (!ps.done) rc = ss_check(hipEventCreateWithFlags(&ps.done, hipEventDisableTiming), "pig event");
     if (!rc && !ps.h_cand) rc = ss_check(hipHostMalloc((void**)&ps.h_cand, kPigMaxG * 8, hipHostMallocDefault), "pinned totals");
     if (!rc && ps.bytes < need) {
@@ -816,7 +977,7 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     a.tile_cand = (uint64_t*)q;
     a.cand = a.tile_cand + tiles_n;
     a.sw = a.cand + a.G;
-    a.hist = (uint32_t*)(a.sw + (size_t)a.G * a.n);
+    a.hist = (uint32_t*)(a.sw + (size_t)a.G * a.n * a.W);
     a.done = a.hist + hist_n;                 // zeroed with hist
     a.tile_cnt = a.done + 2;
     a.sid = a.tile_cnt + tiles_n;
@@ -825,7 +986,10 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     const dim3 tgrid(a.maxtiles, a.G);
     rc = ss_check(hipMemsetAsync(a.hist, 0, (hist_n + 2) * 4, s), "pig hist reset");
     if (!rc) {
-        hipLaunchKernelGGL(k_pig_hist, dim3(rgrid), dim3(256), 0, s, a);
+        if (a.W == 1) hipLaunchKernelGGL(k_pig_hist, dim3(rgrid), dim3(256), 0, s, a);
+        else if (a.W == 2) hipLaunchKernelGGL(k_pigw_hist<2>, dim3(rgrid), dim3(256), 0, s, a);
+        else if (a.W == 3) hipLaunchKernelGGL(k_pigw_hist<3>, dim3(rgrid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_pigw_hist<4>, dim3(rgrid), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_pig_tile, tgrid, dim3(256), 0, s, a);
         rc = ss_check(hipGetLastError(), "k_pig_hist/tile");
     }
@@ -840,9 +1004,15 @@ int pig_all_pairs(const AllPairsArgs& b, uint32_t L, uint32_t P, bool forced, hi
     }
     if (!rc && use) {
         hipLaunchKernelGGL(k_pig_apply, tgrid, dim3(256), 0, s, a);
-        hipLaunchKernelGGL(k_pig_scatter, dim3(rgrid), dim3(256), 0, s, a);
+        if (a.W == 1) hipLaunchKernelGGL(k_pig_scatter, dim3(rgrid), dim3(256), 0, s, a);
+        else if (a.W == 2) hipLaunchKernelGGL(k_pigw_scatter<2>, dim3(rgrid), dim3(256), 0, s, a);
+        else if (a.W == 3) hipLaunchKernelGGL(k_pigw_scatter<3>, dim3(rgrid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_pigw_scatter<4>, dim3(rgrid), dim3(256), 0, s, a);
         const uint64_t pb = (a.n + 255) / 256;
         if (pb > 0x7FFFFFFFull) rc = ss_fail(SS_EARG, "all-pairs: n too large");
+        else if (a.W == 2) hipLaunchKernelGGL(k_pigw_pairs<2>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
+        else if (a.W == 3) hipLaunchKernelGGL(k_pigw_pairs<3>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
+        else if (a.W == 4) hipLaunchKernelGGL(k_pigw_pairs<4>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
         else if (a.G <= 2) hipLaunchKernelGGL(k_pig_pairs<2>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
         else if (a.G <= 4) hipLaunchKernelGGL(k_pig_pairs<4>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
         else if (a.G <= 8) hipLaunchKernelGGL(k_pig_pairs<8>, dim3((unsigned)pb, a.G), dim3(256), 0, s, a);
@@ -876,7 +1046,7 @@ int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uin
     if (n >= (1ull << 32)) return ss_fail(SS_EARG, "n must be < 2^32");
     hipStream_t s = (hipStream_t)stream;
     // the pigeonhole form (tried first when it may apply) zeroes the outputs in its first kernel
-    const uint32_t Pw = L + 1 < 32u ? L + 1 : 32u, Gw = max_dist + 1;
+    const uint32_t Pw = L + 1 < 32u * W ? L + 1 : 32u * W, Gw = max_dist + 1;
     // AUTO on a stream being captured into a hipGraph stays on the tiles: the pigeonhole decision
     // allocates and reads the candidate totals back (a host sync), neither of which a capture allows
     // (the entry point was capturable before AUTO existed)
@@ -886,7 +1056,7 @@ int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uin
         cap = hipStreamCaptureStatusNone;
     }
     const bool capturing = cap != hipStreamCaptureStatusNone;
-    const bool pig_try = n >= 2 && W == 1 && method != SS_ALLPAIRS_TILES && !(capturing && method == SS_ALLPAIRS_AUTO) &&
+    const bool pig_try = n >= 2 && W <= 4 && method != SS_ALLPAIRS_TILES && !(capturing && method == SS_ALLPAIRS_AUTO) &&
                          wpr >= W && d_words &&
                          (method == SS_ALLPAIRS_PIGEONHOLE ? Gw <= (uint32_t)kPigMaxG
                                                            : Gw <= (uint32_t)kPigMaxG && Pw / Gw >= 3 && n >= (1u << 15));
@@ -908,8 +1078,8 @@ int ss_hamming_all_pairs_ex(const uint64_t* d_words, uint64_t n, uint32_t L, uin
     a.pairs = d_pairs;
     a.max_pairs = d_pairs ? max_pairs : 0;
     a.npairs = (unsigned long long*)d_npairs;
-    if (method == SS_ALLPAIRS_PIGEONHOLE && (W != 1 || max_dist + 1 > (uint32_t)kPigMaxG))
-        return ss_fail(SS_EARG, "pigeonhole all-pairs needs L <= 32 and max_dist < 16");
+    if (method == SS_ALLPAIRS_PIGEONHOLE && (W > 4 || max_dist + 1 > (uint32_t)kPigMaxG))
+        return ss_fail(SS_EARG, "pigeonhole all-pairs needs L <= 128 and max_dist < 16");
     // auto: segments of >= 3 nt and a batch large enough to pay the host read of the totals
     if (pig_try) {
         bool done = false;

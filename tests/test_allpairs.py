@@ -64,7 +64,11 @@ def test_all_pairs_gpu(gpu, oracle, L, n, k):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("L,n,k", [(12, 3000, 1), (10, 2500, 2), (32, 1500, 3), (31, 1200, 5), (1, 2000, 0),
-                                   (8, 1000, 15), (20, 1500, 0), (16, 800, 4)])
+                                   (8, 1000, 15), (20, 1500, 0), (16, 800, 4),
+                                   # multi-word rows (round 6): segments across word boundaries, longer
+                                   # than 32 positions (hashed), the alias position in the last word
+                                   (33, 1200, 1), (40, 1500, 2), (64, 1000, 3), (65, 900, 0), (96, 1000, 5),
+                                   (100, 800, 1), (128, 700, 4), (127, 600, 15), (50, 900, 7)])
 def test_all_pairs_pigeonhole_gpu(gpu, oracle, L, n, k):
     """The bucketed pigeonhole form against the oracle's brute force (same pairs, counts, total)."""
     import torch
@@ -139,9 +143,9 @@ def test_all_pairs_pigeonhole_refuses_long_reads(gpu):
     import torch
     import shortseq_amd.batch as B
     from shortseq_amd._native import NativeError
-    d = torch.zeros((10, 2), dtype=torch.int64, device=gpu)
+    d = torch.zeros((10, 5), dtype=torch.int64, device=gpu)
     with pytest.raises(NativeError):
-        B.hamming_all_pairs(d, 40, 1, method="pigeonhole")
+        B.hamming_all_pairs(d, 130, 1, method="pigeonhole")
     with pytest.raises(NativeError):
         B.hamming_all_pairs(d[:, :1].contiguous(), 20, 16, method="pigeonhole")
 
@@ -187,3 +191,26 @@ def test_all_pairs_auto_is_capturable(gpu, oracle):
     g.replay()
     torch.cuda.synchronize(gpu)
     assert int(tot.item()) == tot_e and torch.equal(cnt, cnt_e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,k,U", [(64, 2, 20_000), (100, 1, 30_000), (128, 3, 20_000), (50, 4, 5_000)])
+def test_all_pairs_multiword_methods_agree_large(gpu, oracle, L, k, U):
+    """Multi-word reads at bench-like sizes (n = 60k, where auto may pick either form): the
+    pigeonhole form over the row's words, the tiles and auto give the same counts, totals and pair
+    sets (UMI-like pools with 1-2 substitution variants)."""
+    import torch
+    import shortseq_amd.batch as B
+    n = 60_000
+    ascii = _umis(oracle, n, L, U, L + k)
+    words, _, _ = oracle.encode_batch(ascii, n, L)
+    d = torch.from_numpy(words.view(np.int64)).to(gpu)
+    cnt_t, _, tot_t = B.hamming_all_pairs(d, L, k, method="tiles")
+    for m in ("pigeonhole", "auto"):
+        cnt, _, tot = B.hamming_all_pairs(d, L, k, method=m)
+        assert tot == tot_t and torch.equal(cnt, cnt_t), m
+    if tot_t <= 2_000_000:
+        _, p_t, _ = B.hamming_all_pairs(d, L, k, max_pairs=tot_t, counts=False, method="tiles")
+        _, p_g, _ = B.hamming_all_pairs(d, L, k, max_pairs=tot_t, counts=False, method="pigeonhole")
+        assert np.array_equal(_pair_set(p_t), _pair_set(p_g))
+    assert tot_t > 0

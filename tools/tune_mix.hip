@@ -9,6 +9,12 @@
 //   c2_plain<T>  C2's mix for reference: 32 B in, 4 B per chunk out (8 B per read), nothing else
 //   prod C3      ss_encode_hamming_ref (k_encode_ham_dense) on the same 100M x 96-nt reads
 //   prod C2      ss_encode_fixed (k_encode_g16) on 100M x 32-nt reads
+// and for ss_encode_var (flat at 0.67, bound unnamed), on the F2 batch (50M
+// ragged reads of 50-150 nt, wpr 5):
+//   var_pattern  k_encode_var_dense's exact access pattern (a lane per output word, its read's offset
+//                and length, the three 16-B chunks holding the word) with the encode replaced by a
+//                XOR fold: if it runs at the production kernel's rate, the pattern bounds it
+//   var_dense    the same bytes as one dense stream (blob + offsets + lengths in, wpr words out)
 // Prints ms and the fraction of 8 TB/s over each kernel's bytes (min over reps).
 //
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include tools/tune_mix.hip -o tools/tune_mix
@@ -18,6 +24,8 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+
+#include <vector>
 
 namespace {
 
@@ -92,6 +100,61 @@ __global__ __launch_bounds__(T) void k_c2_plain(const uint4* __restrict__ in, ui
         const uint64_t c = c0 + (uint64_t)j * T + threadIdx.x;
         if (c < nchunks) st_stream(&words[c], x[j].x ^ x[j].y ^ x[j].z ^ x[j].w);
     }
+}
+
+// k_encode_var_dense with the encode math removed (see the header): kVarK = 2 words per lane
+__global__ __launch_bounds__(256) void k_var_pattern(const uint8_t* in, const uint64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ lens, uint64_t n,
+                                                     uint64_t* __restrict__ out, uint32_t wpr, double inv_wpr) {
+    constexpr int K = 2;
+    const uint64_t total = n * wpr;
+    const uint64_t base = ((uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u)) * K + (threadIdx.x & 63u);
+    uint64_t r[K], off[K];
+    uint32_t w[K], L[K], nb[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t g = base + 64u * k;
+        uint64_t rr = (uint64_t)((double)g * inv_wpr);
+        if (rr * wpr > g) --rr;
+        else if ((rr + 1) * wpr <= g) ++rr;
+        r[k] = g < total ? rr : 0;
+        w[k] = (uint32_t)(g - rr * wpr);
+        L[k] = g < total ? lens[r[k]] : 0u;
+        off[k] = g < total ? offs[r[k]] : 0u;
+    }
+    uint4 c0[K], c1[K], c2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        nb[k] = 32u * w[k] < L[k] ? min(32u, L[k] - 32u * w[k]) : 0u;
+        c0[k] = c1[k] = c2[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (nb[k]) {
+            const uintptr_t addr = (uintptr_t)(in + off[k] + 32u * w[k]);
+            const uint4* q = (const uint4*)(addr & ~(uintptr_t)15);
+            const uint32_t last = ((uint32_t)(addr & 15) + nb[k] - 1u) >> 4;
+            c0[k] = q[0];
+            c1[k] = q[min(1u, last)];
+            c2[k] = q[min(2u, last)];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t g = base + 64u * k;
+        if (g >= total) continue;
+        const uint32_t lo = c0[k].x ^ c1[k].y ^ c2[k].z ^ c0[k].w, hi = c1[k].x ^ c2[k].y ^ c0[k].z ^ c2[k].w;
+        out[g] = nb[k] ? ((uint64_t)hi << 32 | lo) : 0ull;
+    }
+}
+
+// a dense stream of the same bytes: nch 16-B chunks read, nout 8-B words written (4 words per lane)
+__global__ __launch_bounds__(256) void k_var_dense(const uint4* __restrict__ in, uint64_t nch, uint64_t* __restrict__ out,
+                                                   uint64_t nout) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, nt = (uint64_t)gridDim.x * 256;
+    uint32_t acc = 0;
+    for (uint64_t c = t; c < nch; c += nt) {
+        const uint4 v = ld_stream(&in[c]);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    for (uint64_t o = t; o < nout; o += nt) out[o] = acc + o;
 }
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -187,5 +250,48 @@ int main(int argc, char** argv) {
     });
     CK(hipFree(a32));
     CK(hipFree(w));
+    {   // ss_encode_var on the F2 batch (bench.py bench_ragged: seed 41, pool 42, 2^20 items, 50-150 nt)
+        const uint64_t nv = 50000000ull;
+        const uint32_t wpr = 5;
+        uint32_t* lens;
+        uint64_t *offs, *out;
+        CK(hipMalloc(&lens, nv * 4));
+        CK(hipMalloc(&offs, nv * 8));
+        CS(ss_synth_ragged_lens(lens, 41, 42, 1u << 20, 0, nv, 50, 150, nullptr));
+        std::vector<uint32_t> hl(nv);
+        std::vector<uint64_t> ho(nv);
+        CK(hipMemcpy(hl.data(), lens, nv * 4, hipMemcpyDeviceToHost));
+        uint64_t tot = 0;
+        for (uint64_t i = 0; i < nv; ++i) {
+            ho[i] = tot;
+            tot += hl[i];
+        }
+        CK(hipMemcpy(offs, ho.data(), nv * 8, hipMemcpyHostToDevice));
+        uint8_t* blob;
+        CK(hipMalloc(&blob, tot + 12 * nv + 64));     // (var_dense streams blob-sized + metadata-sized bytes)
+        CS(ss_synth_ragged_reads(blob, offs, 41, 42, 1u << 20, 0, nv, 50, 150, nullptr));
+        CK(hipMalloc(&out, nv * wpr * 8));
+        CK(hipDeviceSynchronize());
+        const double bv = (double)tot + 12.0 * nv + 8.0 * wpr * nv;
+        printf("F2 batch: %llu reads, %.3f GB blob, algorithmic %.3f GB per call\n", (unsigned long long)nv, tot * 1e-9, bv * 1e-9);
+        const double inv = 1.0 / wpr;
+        const uint64_t words = nv * wpr;
+        const unsigned grid = (unsigned)((words + 511) / 512);
+        timeit("prod ss_encode_var", bv, [&] { CS(ss_encode_var(blob, offs, lens, nv, out, wpr, fb, nullptr)); });
+        timeit("var_pattern (no encode)", bv, [&] {
+            hipLaunchKernelGGL(k_var_pattern, dim3(grid), dim3(256), 0, 0, (const uint8_t*)blob, (const uint64_t*)offs,
+                               (const uint32_t*)lens, nv, out, wpr, inv);
+        });
+        const uint64_t nch = ((uint64_t)tot + 12ull * nv + 15) / 16;
+        timeit("var_dense (same bytes)", bv, [&] {
+            hipLaunchKernelGGL(k_var_dense, dim3(8192), dim3(256), 0, 0, (const uint4*)blob, nch,
+                               out, words);
+        });
+        timeit("prod ss_encode_var", bv, [&] { CS(ss_encode_var(blob, offs, lens, nv, out, wpr, fb, nullptr)); });
+        CK(hipFree(blob));
+        CK(hipFree(lens));
+        CK(hipFree(offs));
+        CK(hipFree(out));
+    }
     return 0;
 }
