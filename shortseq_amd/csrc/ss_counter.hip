@@ -1072,30 +1072,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
                 report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
                 key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
             }
-#ifdef SS_PF_MULTISPLIT
-            {   // (measurement variant, VERDICT r5 lever (b)) wave multisplit: the lanes of one bin
-                // found by 7 ballots over the bin bits; one LDS atomic per (wave, bin) by the bin's
-                // lowest lane, its base broadcast back, each lane's rank = base + its peers below it
-                const uint32_t b = live ? region_of(t, key[j]) >> shift : 0u;
-                uint64_t peers = __ballot(live);
-#pragma unroll
-                for (int k = 0; k < (int)kCoarseBits; ++k) {
-                    const uint64_t bb = __ballot((b >> k) & 1u);
-                    peers &= ((b >> k) & 1u) ? bb : ~bb;
-                }
-                const int leader = live ? __ffsll((long long)peers) - 1 : (int)lane;
-                const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
-                uint32_t base = 0;
-                if (live && (int)lane == leader) base = atomicAdd(&lcount[b], (uint32_t)__popcll(peers));
-                base = (uint32_t)__shfl((int)base, leader);
-                if (live) br[j] = (b << 16) | (base + below);
-            }
-#else
             if (live) {
                 const uint32_t b = region_of(t, key[j]) >> shift;
                 br[j] = (b << 16) | atomicAdd(&lcount[b], 1u);
             }
-#endif
         }
         __syncthreads();                                                  // (A)
         if (threadIdx.x < 64) {       // wave 0: scan, heavy flags, the reservation atomic of bins 2 lane, 2 lane + 1
@@ -2791,8 +2771,6 @@ struct FlatDesc {
     uint64_t* rmap[kRepW1];         // its row map at row0
     uint64_t base;                  // global read index of the chunk's read 0
     uint32_t S;
-    const uint64_t* rows;           // non-null: entries read from their first row (ss_classes_flat_extract),
-                                    // not from the representatives -- so the extract need not wait for them
 };
 
 // rep layout, 8 u64 per scratch slot: the row's words w0 .. w5 (zeros past S), the key, the class W --
@@ -2897,24 +2875,12 @@ __device__ __forceinline__ bool flat_entry(const Tbl& f, const FlatDesc& d, cons
     if (s > f.mask) return false;
     const Slot sl = f.slots[s];
     if (sl.key == kEmpty) return false;
-    if (d.rows) {
-        // the entry's first row (read-order, S words: W words, the length, zeros): W = the index of
-        // its last nonzero word, looked for among words 2 .. S - 1 (a class row has W >= 2)
-        kw = d.rows + (uint64_t)sl.first * d.S;
-        W = 0;
-        for (uint32_t j = d.S - 1; j >= 2; --j)
-            if (kw[j]) {
-                W = j;
-                break;
-            }
-    } else {
-        W = (uint32_t)rep[s * 8 + 7];
-        kw = rep + s * 8;
-    }
+    W = (uint32_t)rep[s * 8 + 7];
     if (W < 2 || W + 1 > d.S || !d.tbl[W].slots) return false;
     fp = sl.key;
     cnt = ~sl.ncount;
     first = sl.first;
+    kw = rep + s * 8;
     return true;
 }
 
@@ -3937,13 +3903,12 @@ int ss_classes_flat_fold(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, 
 }
 
 int ss_classes_flat_extract(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, uint64_t base,
-                            const ss_flat_out* out, const uint32_t* d_zero, void* stream, const uint64_t* d_rows) {
+                            const ss_flat_out* out, const uint32_t* d_zero, void* stream) {
     if (!fpt || !cls || !out || !d_zero) return ss_fail(SS_EARG, "null argument");
     hipStream_t s = (hipStream_t)stream;
     FlatDesc d;
     int rc = flat_desc(cls, S, base, s, d, false);
     if (rc) return rc;
-    d.rows = d_rows;
     FlatOut o{};
     FlatTotals tot{};
     for (uint32_t W = 2; W + 1 <= S; ++W) {

@@ -1173,8 +1173,7 @@ int spec_launch(ss_ingest* g, const uint64_t* need, uint64_t N) {
     if ((rc = ss_check(hipMemsetAsync(sd, 0, 13 * 8, ss), "spec reset")) ||
         (rc = ss_check(hipMemsetAsync(g->slot.p, 0, NB * 8, ss), "spec read map reset")))
         return rc;
-    if ((rc = ss_classes_flat_extract(g->fpt, g->pend_S, g->pend_fc, g->pend_base, fo, g->zero32.p, ss, g->cls_words.p)))
-        return rc;
+    if ((rc = ss_classes_flat_extract(g->fpt, g->pend_S, g->pend_fc, g->pend_base, fo, g->zero32.p, ss))) return rc;
     for (size_t q = 0; q < cls.size(); ++q) {
         Group& gr = *cls[q];
         const uint64_t cap = gr.cap + 1;
@@ -1527,13 +1526,10 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         for (uint32_t W = 2; W < 6; ++W) defer &= !fc[W].table || fc[W].base == 0;
         if (!rc && flat) rc = ss_counter_insert_keys(g->fpt, g->cls_fps.p, n, 0, s);
         if (!rc && flat && defer) {
-            // a first chunk of an add_device / add_blob also queues the speculative finish beside the
-            // representatives and the verify: it reads the scratch's entries from their first rows, so it
-            // starts once the scratch insert is done (round 6: it waited for the representatives, 1.2 ms at
-            // 2^24 distinct keys, while the rows' gather over PCIe is that case's bound)
+            // a first chunk of an add_device / add_blob also queues the speculative finish beside the verify
             const bool spec = spec_ok && base == 0 && g->bad_index == kNoSlot;
-            if (spec) rc = ss_check(hipEventRecord(g->ev_reps, s), "ingest scratch insert event");
-            if (!rc) rc = ss_classes_flat_verify(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, g->cls_flag.p, s, nullptr);
+            rc = ss_classes_flat_verify(g->fpt, g->cls_words.p, w1max, n, g->cls_fps.p, g->cls_flag.p, s,
+                                        spec ? (void*)g->ev_reps : nullptr);
             if (!rc) {      // pending once the flag comes back clear (checked after the sync below)
                 g->pend_S = w1max;
                 g->pend_base = base;
@@ -1716,8 +1712,7 @@ int extract_groups(ss_ingest* g, std::vector<Group*>& placed, bool flat = false)
                                (const uint64_t*)(d_cnt + 3 * q), gr.acc.p, gr.acc_rows);
         placed.push_back(&gr);
     }
-    if (any_flat && (rc = ss_classes_flat_extract(g->fpt, g->pend_S, g->pend_fc, g->pend_base, fo, g->zero32.p, s,
-                                                  g->cls_words.p)))
+    if (any_flat && (rc = ss_classes_flat_extract(g->fpt, g->pend_S, g->pend_fc, g->pend_base, fo, g->zero32.p, s)))
         return rc;
     if (!placed.empty()) {
         rc = ss_check(hipMemcpyAsync(g->h_bad, d_cnt, 3 * placed.size() * 8, hipMemcpyDeviceToHost, s), "ingest");

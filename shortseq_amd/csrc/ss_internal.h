@@ -92,11 +92,8 @@ struct ss_flat_out {
     uint64_t* ovf;        // set nonzero when the class has more than cap entries (those are dropped)
     uint64_t cap;
 };
-// d_rows (nullable): the chunk's read-order rows; the entries are then read from their first rows
-// instead of the representatives, so the extract may run as soon as the scratch insert is done
 extern "C" int ss_classes_flat_extract(ss_counter* fpt, uint32_t S, const ss_flat_class* cls, uint64_t base,
-                                       const ss_flat_out* out, const uint32_t* d_zero, void* stream,
-                                       const uint64_t* d_rows);
+                                       const ss_flat_out* out, const uint32_t* d_zero, void* stream);
 // Every entry's count moved into d_acc[first] (u64, indexed by the entry's first index: the drop-in
 // engine's rows) and the slot's count zeroed (the single-word sentinel keeps 1), so later inserts
 // cannot wrap a slot's u32 count (k_spill_counts).
