@@ -474,14 +474,16 @@ def bench_fastq_index(B, lib, dev, n_rec=8 << 20, L=100, reps=10):
                     "ss_fastq_index; device-resident synthetic FASTQ, every offset / length checked"}
 
 
-def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10, method="tiles"):
+def bench_all_pairs(B, lib, dev, n=100_000, L=12, k=1, reps=10, method="tiles", pool=None):
     """all unordered pairs of n UMIs (L nt) within hamming k.  method "tiles" checks
     every pair on the MFMA tiles (priced against the i8 peak); "pigeonhole" / "auto" check only the
     pairs sharing one of k + 1 segments (bucketed on the device) -- same counts and total, reported
     as covered pairs per second (n (n - 1) / 2 per step), with no MFMA roofline."""
     from shortseq_amd._native import check
     code = B.ALL_PAIRS_METHODS[method]
-    w = B.encode(B.synth_reads(n, L, seed=7, device=dev), L)
+    # pool: reads drawn from `pool` distinct items (duplicates give distance-0 hits), else all random
+    a = B.synth_reads(n, L, seed=7, device=dev) if pool is None else B.synth_pool_reads(n, L, 7, 8, pool, device=dev)
+    w = B.encode(a, L)
     cnt = torch.empty(n, dtype=torch.int32, device=dev)
     tot = torch.empty(1, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
@@ -993,6 +995,16 @@ def main():
             local_extra("F4_all_pairs_umi12", lambda: bench_all_pairs(B, lib, dev))
             # the default entry point (auto: pigeonhole buckets for this batch), same results
             local_extra("F4_all_pairs_umi12_auto", lambda: bench_all_pairs(B, lib, dev, method="auto"))
+            # multi-word reads (round 6: the pigeonhole form for L <= 128): 100k 96-nt reads of a 2^16
+            # pool within distance 3, the default entry point; the tiles' time beside it
+            def f4_96():
+                r = bench_all_pairs(B, lib, dev, n=100_000, L=96, k=3, method="auto", pool=1 << 16)
+                t = bench_all_pairs(B, lib, dev, n=100_000, L=96, k=3, method="tiles", pool=1 << 16, reps=3)
+                if t["hits"] != r["hits"]:
+                    raise SystemExit("PARITY FAILURE: all-pairs 96 nt (auto vs tiles)")
+                return {k_: r[k_] for k_ in ("n", "read_len", "max_dist", "ms_per_step", "pairs_per_s", "hits")} | \
+                    {"tiles_ms_per_step": t["ms_per_step"]}
+            local_extra("F4_all_pairs_96_auto", f4_96)
             log("F2 ragged 50-150 nt")
             local_extra("F2_ragged_50_150", lambda: bench_ragged(B, lib, dev))
             # the same reads over a 2^24-item pool: ~16M distinct keys, tables past the Infinity Cache

@@ -24,9 +24,13 @@ if len(sys.argv) > 1 and sys.argv[1] == "quick":     # one case per method (rocp
     sys.exit(0)
 for _ in range(2):
     print(bench.bench_all_pairs(B, lib(), dev), flush=True)
-for n, L, k in ((100_000, 12, 1), (200_000, 12, 1), (1_000_000, 12, 1), (100_000, 16, 2), (50_000, 32, 2),
-                (200_000, 32, 3), (100_000, 8, 1), (20_000, 96, 4)):
-    for m in (("tiles", "pigeonhole", "auto") if L <= 32 else ("tiles",)):
+CASES = ((100_000, 12, 1), (200_000, 12, 1), (1_000_000, 12, 1), (100_000, 16, 2), (50_000, 32, 2),
+         (200_000, 32, 3), (100_000, 8, 1), (20_000, 96, 4))
+# multi-word reads (round 6: the pigeonhole form for L <= 128): python tools/probe_f4.py multiword
+MULTI = ((100_000, 64, 2), (100_000, 96, 3), (100_000, 128, 4), (200_000, 100, 1), (1_000_000, 96, 2),
+         (100_000, 40, 5))
+for n, L, k in (MULTI if len(sys.argv) > 1 and sys.argv[1] == "multiword" else CASES):
+    for m in (("tiles", "pigeonhole", "auto") if L <= 128 else ("tiles",)):
         if m == "tiles" and n > 200_000:
             continue
         r = bench.bench_all_pairs(B, lib(), dev, n=n, L=L, k=k, method=m, reps=5)
