@@ -605,8 +605,10 @@ def bench_host_staged(B, dev, n=32_000_000, L=32, reps=5):
     place = {k: split.pop(k) for k in ("copy_threads", "affinity_cpus", "gpu_numa_node", "pinned_cpus")}
     return {"reads": n, "read_len": L, "ms_per_call": t * 1e3, "nt_per_s": n * L / t,
             "host_dev_GB_per_s": n * (L + 8) / t / 1e9, "stage_ms": split, **place,
+            # the H2D copies' own time (summed over chunks) is the PCIe floor of the call
+            "h2d_floor_frac": split["h2d_dev"] / (t * 1e3),
             "note": "pageable numpy in -> numpy out through ss_encode_host (64-MiB chunks, 3 slots, "
-                    "8 staging threads pinned to the GPU's NUMA node within the affinity mask); stage_ms: "
+                    "12 staging threads pinned to the GPU's NUMA node within the affinity mask); stage_ms: "
                     "host copy / wait ms and device H2D / kernel / D2H ms per call (device sums overlap "
                     "across chunks); PCIe-bound, not the roofline number"}
 

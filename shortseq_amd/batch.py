@@ -283,7 +283,9 @@ class HostStager:
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         if copy_threads is None:
-            copy_threads = int(os.environ.get("SHORTSEQ_STAGE_THREADS", min(8, os.cpu_count() or 1)))
+            # 12 threads pinned to the GPU's NUMA node: 20.0 ms for 32M x 32-nt reads against 21.4
+            # with 8 and 20.6 with 16, the H2D copies at ~19 ms the floor (profiles/r6/probe_stage_split.log)
+            copy_threads = int(os.environ.get("SHORTSEQ_STAGE_THREADS", min(12, os.cpu_count() or 1)))
         h = C.c_void_p()
         check(lib().ss_stager_create(self.device.index or 0, chunk_bytes, nslots, copy_threads, C.byref(h)),
               "ss_stager_create")
