@@ -381,3 +381,29 @@ def test_fastq_split_host(tmp_path):
             for k in range(parts):
                 assert bs[k] in (0, len(data)) or data[bs[k] - 1:bs[k]] == b"\n", (trial, parts, k)
                 assert l0[k] == data[:bs[k]].count(b"\n"), (trial, parts, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [0, 4096])
+def test_fastq_gpu_stage_split(gpu, tmp_path, chunk):
+    """The engine's FASTQ stage split (ss_ingest_fastq_stages via
+    _shortseq.fastq_stage_times): one entry per device, every stage timed, and the H2D copies moved
+    the file once (one chunk) or once plus the carried partial lines (many chunks); the counts
+    equal the host path's."""
+    from shortseq_amd import _shortseq
+    rng = random.Random(23)
+    data = _random_fastq(rng, 5000, edge=False)
+    p = tmp_path / "s.fq"
+    p.write_bytes(data)
+    d = sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=chunk)
+    h = sq.read_and_count_fastq(str(p), device="host")
+    assert _items(d) == _items(h)
+    st = _shortseq.fastq_stage_times()
+    assert len(st) == 1
+    s0 = st[0]
+    for k in ("read_ms", "h2d_dev_ms", "index_ms", "count_ms", "finish_ms", "reduce_and_dict_ms", "total_ms"):
+        assert s0[k] > 0.0, k
+    if chunk == 0:
+        assert s0["h2d_bytes"] == len(data)
+    else:
+        assert len(data) <= s0["h2d_bytes"] < 2 * len(data)

@@ -102,3 +102,39 @@ def test_encode_host_default_stager_large(gpu, oracle):
     assert np.array_equal(got[::997], oracle.gen_words(4, 0, n, L).reshape(n, 1)[::997])
     back = B.decode_host(got, L)
     assert np.array_equal(back, a)
+
+
+@pytest.mark.parametrize("pin", ["1", "0"])
+def test_stager_stage_split_and_placement(gpu, oracle, monkeypatch, pin):
+    """ss_stager_set_timing / ss_stager_stats: the split of timed calls is
+    reported per call (host copies for pageable buffers, device H2D / kernel / D2H > 0), untimed
+    calls leave nothing, a stats call resets it, and the placement fields are consistent (the copy
+    threads pinned only with SHORTSEQ_STAGE_PIN != 0, to at most the CPUs the process may use); the
+    words stay the oracle's with timing on."""
+    import shortseq_amd.batch as B
+    monkeypatch.setenv("SHORTSEQ_STAGE_PIN", pin)
+    st = B.HostStager(gpu, chunk_bytes=1 << 20, nslots=3, copy_threads=4)
+    rng = np.random.default_rng(7)
+    try:
+        n, L = 200_000, 32
+        a = _reads(rng, n, L)
+        exp, rc, _ = oracle.encode_batch(a.reshape(-1), n, L)
+        st.encode(a)
+        first = st.stats()
+        assert all(first[k] == 0.0 for k in B.HostStager.STAGES)       # nothing timed yet
+        st.set_timing(True)
+        for _ in range(2):
+            got = st.encode(a)
+        sp = st.stats()
+        assert np.array_equal(got.reshape(-1).view(np.uint64), exp.reshape(-1))
+        for k in ("copy_in_host", "copy_out_host", "h2d_dev", "kernel_dev", "d2h_dev"):
+            assert sp[k] > 0.0, k
+        assert st.stats()["h2d_dev"] == 0.0                              # reset by the previous call
+        assert sp["copy_threads"] == 4 and sp["affinity_cpus"] >= 1 and sp["gpu_numa_node"] >= -1
+        if pin == "0" or sp["gpu_numa_node"] < 0:
+            assert sp["pinned_cpus"] == 0
+        else:
+            assert 0 <= sp["pinned_cpus"] <= sp["affinity_cpus"]
+        st.set_timing(False)
+    finally:
+        st.close()
