@@ -419,7 +419,9 @@ int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, ui
  * lines before each range (h_line0[p]).  ss_ingest_add_fastq_range counts one range (line0 = the
  * lines before it, so the j % 4 == 1 selection of fast_read.pyx:13 stays global); the ranges'
  * results, taken in range order, are the file's counter (first-occurrence order kept: every read of
- * range p precedes every read of range p + 1).  Host calls. */
+ * range p precedes every read of range p + 1).  Host calls.  A range longer than one chunk
+ * (chunk_bytes; 0 = 1 GiB) is read by a reader thread into two pinned chunk slots: chunk k + 1's
+ * file reads and H2D copies (their own stream) run while chunk k is indexed and counted. */
 int ss_fastq_split(const char* path, uint32_t nparts, uint64_t* h_begin, uint64_t* h_line0);
 int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, uint64_t end, uint64_t line0,
                               uint64_t chunk_bytes, uint64_t* h_nseqs);
@@ -434,7 +436,9 @@ int ss_ingest_finish(ss_ingest* g, uint64_t* h_nkeys, uint64_t* h_nwords);
 /* Stage split of the engine's FASTQ calls since the last call of this (new,
  * replaces nothing): h_ms[5] = host ms of the file reads (pread into pinned memory, in pieces whose
  * H2D copies overlap the next piece's read), device ms of those H2D copies (summed), host ms of the
- * device index to its sync, host ms of the chunk counts, host ms of ss_ingest_finish; *h_h2d_bytes =
+ * device index to its sync (incl. the wait for its chunk's copies), host ms of the chunk counts,
+ * host ms of ss_ingest_finish (reads and copies of a later chunk overlap the index and count of an
+ * earlier one, so the stages of a multi-chunk range sum to more than its wall time); *h_h2d_bytes =
  * the bytes the H2D copies moved (their rate = the PCIe rate the call saw). */
 int ss_ingest_fastq_stages(ss_ingest* g, double* h_ms, uint64_t* h_h2d_bytes);
 int ss_ingest_results(ss_ingest* g, const uint32_t** h_lens, const uint64_t** h_counts, const uint64_t** h_words);

@@ -48,7 +48,9 @@
 #include <cmath>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -766,6 +768,20 @@ struct HBuf {
     }
 };
 
+// the FASTQ reader ring (ss_ingest_add_fastq_range): a slot is one chunk, pinned and on the device
+constexpr uint64_t kFqPiece = 64ull << 20;           // file read / H2D piece
+constexpr uint64_t kFqChunkDefault = 1ull << 30;     // chunk bytes when the caller passes 0
+struct FqSlot {
+    HBuf h;
+    DBuf<uint8_t> d;
+    hipEvent_t done = nullptr;    // the slot's H2D pieces are complete (recorded on fq_copy)
+    std::vector<hipEvent_t> ev;   // 2 timing events per H2D piece
+    uint32_t np = 0;              // pieces of the chunk in the slot
+    uint64_t n = 0, use = 0;      // bytes in the slot, bytes up to its last newline (n at the range's end)
+    bool at_eof = false;
+    int rc = SS_OK;
+};
+
 struct Group {
     uint32_t L = 0;               // 1..32: the length of every key; 0: a length class
     uint32_t W1 = 1;              // words per table key: 1, or a class's ceil(L/32) + 1 (length word)
@@ -878,7 +894,8 @@ struct ss_ingest {
     // the chunk counts (process_chunk) and of ss_ingest_finish; the bytes the H2D pieces moved
     double fq_ms[5] = {};
     uint64_t fq_h2d_bytes = 0;
-    std::vector<hipEvent_t> fq_ev;     // timing events of the H2D pieces (2 per piece)
+    FqSlot fq[2];
+    hipStream_t fq_copy = nullptr;     // the reader thread's H2D pieces
 };
 
 namespace {
@@ -946,8 +963,7 @@ int table_size(ss_ingest* g, ss_counter* t, uint64_t* out) {
     if (rc) return rc;
     rc = ss_counter_size(t, s.p + kScanBlocks + 2, g->stream);
     if (rc) return rc;
-    rc = ss_check(hipMemcpyAsync(g->h_bad + 2 * kLenBins + 2, s.p + kScanBlocks + 2, 8, hipMemcpyDeviceToHost, g->stream),
-                  "ingest size copy");
+    rc = ss_check(hipMemcpyAsync(g->h_bad + 2 * kLenBins + 2, s.p + kScanBlocks + 2, 8, hipMemcpyDeviceToHost, g->stream), "ingest size copy");
     if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest sync");
     *out = g->h_bad[2 * kLenBins + 2];
     return rc;
@@ -1059,6 +1075,8 @@ int group_room(ss_ingest* g, Group& gr, uint64_t m, uint64_t need) {
     }
     if (gr.table && need <= gr.cap / 2) return SS_OK;
     if (!gr.table) {
+        // (a length's table is sized by this chunk's rows: sized for the whole file's rows, est_scale,
+        // the tables of the later chunks' small inserts were 2-3x slower -- more regions per insert)
         const double scale = gr.L || need < m ? 1.0 : g->est_scale;
         gr.cap = std::min<uint64_t>(1ull << 32, pow2_at_least((uint64_t)(2.0 * (double)need * scale) + 2));
         int rc = table_get(g, gr.cap, gr.W1, m, &gr.table);
@@ -1451,7 +1469,9 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         gr.W1 = cls ? jb.bin - kClassBin0 + 1 : 1u;
         const uint64_t need = std::min<uint64_t>(gr.rows + jb.m, cls ? need_cls[gr.W1 - 1] : ~0ull);
         if ((rc = group_room(g, gr, jb.m, need))) return rc;
-        if ((rc = gr.rowmap.ensure_keep(gr.rows + jb.m, gr.rows, s))) return rc;
+        // (a multi-chunk FASTQ: the first row map holds the whole file's estimated rows, not a doubling per chunk)
+        const uint64_t rm = gr.rowmap.cap || g->est_scale <= 1.0 ? gr.rows + jb.m : (uint64_t)((double)(gr.rows + jb.m) * g->est_scale * 1.1);
+        if ((rc = gr.rowmap.ensure_keep(std::max(rm, gr.rows + jb.m), gr.rows, s))) return rc;
         const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
         if (cls) {
             cls_jobs.push_back(j);     // inserted below, on the class streams
@@ -1466,7 +1486,8 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 src = g->rows.p;
             }
             if ((rc = flush_prep(g))) return rc;
-            if (jb.m >= (1u << 16) && jb.m < (1ull << 31)) (void)ss_counter_reserve(gr.table, jb.m);
+            // (+1/4: the next chunk's slightly larger share of this length reuses the workspace)
+            if (jb.m >= (1u << 16) && jb.m < (1ull << 30)) (void)ss_counter_reserve(gr.table, jb.m + jb.m / 4);
             rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, stride, gr.rows, g->first_bad.p + jb.bin, s);
         }
         if (rc) return rc;
@@ -1861,8 +1882,15 @@ int ss_ingest_destroy(ss_ingest* g) {
     g->groups.clear();
     for (auto& p : g->pool) ss_counter_destroy(p.second);
     g->pool.clear();
-    for (hipEvent_t e : g->fq_ev) (void)hipEventDestroy(e);
-    g->fq_ev.clear();
+    for (FqSlot& sl : g->fq) {
+        for (hipEvent_t e : sl.ev) (void)hipEventDestroy(e);
+        sl.ev.clear();
+        if (sl.done) (void)hipEventDestroy(sl.done);
+        sl.done = nullptr;
+        sl.h.release(), sl.d.release();
+    }
+    if (g->fq_copy) (void)hipStreamDestroy(g->fq_copy);
+    g->fq_copy = nullptr;
     g->stage.release();
     g->out_host.release();
     g->dbuf.release(), g->offs.release(), g->dlens.release(), g->order.release(), g->blkhist.release();
@@ -2014,83 +2042,142 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
         close(fd);
         return SS_OK;
     }
-    if (chunk_bytes == 0) chunk_bytes = 1ull << 30;
-    uint64_t cap = std::max<uint64_t>(16, std::min<uint64_t>(chunk_bytes, size - begin + 16));
+    if (chunk_bytes == 0) chunk_bytes = kFqChunkDefault;
+    const uint64_t cap0 = std::max<uint64_t>(16, std::min<uint64_t>(chunk_bytes, size - begin + 16));
     hipStream_t s = g->stream;
-    int rc = g->stage.ensure(cap);
-    uint64_t carry = 0, pos = begin, seqs0 = g->nreads;
-    unsigned threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    int rc = SS_OK;
+    if (!g->fq_copy) rc = ss_check(hipStreamCreateWithFlags(&g->fq_copy, hipStreamNonBlocking), "ingest fastq stream");
+    for (int i = 0; i < 2 && !rc; ++i)
+        if (!g->fq[i].done) rc = ss_check(hipEventCreateWithFlags(&g->fq[i].done, hipEventDisableTiming), "ingest fastq event");
+    if (rc) {
+        close(fd);
+        return rc;
+    }
+    const uint64_t seqs0 = g->nreads;
+    const unsigned threads = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     using Clock = std::chrono::steady_clock;
     auto since = [](Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); };
-    // The chunk's bytes are read into pinned memory in pieces of kFqPiece, and each piece's H2D goes
-    // out as soon as it is there, so the file reads and the PCIe copies overlap (one read, then one
-    // copy of the whole chunk, ran them back to back: VERDICT r5 item 7).  Two timing events per piece.
-    constexpr uint64_t kFqPiece = 64ull << 20;
-    while (!rc) {
-        if (cap >= (1ull << 32)) {
-            rc = ss_fail(SS_EARG, "a FASTQ line is longer than 2 GiB");
-            break;
-        }
-        uint8_t* hv = g->stage.p;
-        const uint64_t want = std::min(cap - carry, size - std::min(size, pos));
-        if ((rc = g->dbuf.ensure(cap + 16))) break;
-        const uint64_t npieces = (want + kFqPiece - 1) / kFqPiece + 1;
-        while (g->fq_ev.size() < 2 * npieces && !rc) {
-            hipEvent_t e = nullptr;
-            rc = ss_check(hipEventCreate(&e), "ingest fastq event");
-            if (!rc) g->fq_ev.push_back(e);
-        }
-        if (rc) break;
-        uint64_t got = 0, np = 0;
-        auto h2d = [&](uint64_t off, uint64_t len) {
-            int r = ss_check(hipEventRecord(g->fq_ev[2 * np], s), "ingest fastq event");
-            if (!r) r = ss_check(hipMemcpyAsync(g->dbuf.p + off, hv + off, len, hipMemcpyHostToDevice, s), "ingest H2D");
-            if (!r) r = ss_check(hipEventRecord(g->fq_ev[2 * np + 1], s), "ingest fastq event");
-            ++np;
-            g->fq_h2d_bytes += len;
-            return r;
-        };
-        if (carry) rc = h2d(0, carry);     // the previous chunk's tail, already in pinned memory
-        for (uint64_t off = 0; off < want && !rc; off += kFqPiece) {
-            const uint64_t len = std::min(kFqPiece, want - off);
-            const auto t0 = Clock::now();
-            const uint64_t r = read_parallel(fd, hv + carry + off, len, pos + off, threads);
-            g->fq_ms[0] += since(t0);
-            got += r;
-            if (r != len) break;
-            rc = h2d(carry + off, len);
-        }
-        if (rc) break;
-        if (got != want) {
-            rc = ss_fail(SS_EHIP, "short read of the FASTQ file");
-            break;
-        }
-        pos += got;
-        const uint64_t n = carry + got;
-        const bool at_eof = pos >= size;
-        if (n == 0) break;
-        uint64_t use = n;
-        if (!at_eof) {
-            use = 0;
-            for (uint64_t k = n; k > 0; --k)
-                if (hv[k - 1] == '\n') {
-                    use = k;
+    // The reader ring: a reader thread fills chunk k + 1 into slot (k + 1) & 1 -- the previous chunk's
+    // tail (bytes after its last newline) first, then file reads in pieces of kFqPiece, each piece's
+    // H2D queued on fq_copy as soon as it is read -- while this thread indexes and counts chunk k
+    // from slot k & 1 on the engine's stream.  A slot goes back to the reader once the engine's
+    // stream has finished with it.  state[i]: 0 the reader's, 1 filled (this thread's).
+    std::mutex mu;
+    std::condition_variable cv;
+    int state[2] = {0, 0};
+    bool stop = false;
+    auto reader = [&]() {
+        (void)hipSetDevice(g->device);
+        uint64_t pos = begin, cap = cap0, carry = 0;
+        const uint8_t* csrc = nullptr;
+        for (uint64_t k = 0;; ++k) {
+            FqSlot& sl = g->fq[k & 1];
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || state[k & 1] == 0; });
+                if (stop) return;
+            }
+            int r = SS_OK;
+            sl.np = 0;
+            for (;;) {
+                if (cap >= (1ull << 32)) {
+                    r = ss_fail(SS_EARG, "a FASTQ line is longer than 2 GiB");
                     break;
                 }
-            if (use == 0) {     // one line fills the chunk: grow the staging buffer, keep its bytes
-                if ((rc = ss_check(hipStreamSynchronize(s), "ingest fastq grow"))) break;   // (its H2D pieces)
+                if ((r = sl.h.ensure(cap)) || (r = sl.d.ensure(cap + 16))) break;
+                if (carry && csrc != sl.h.p) memcpy(sl.h.p, csrc, carry);
+                uint8_t* hv = sl.h.p;
+                const uint64_t want = std::min(cap - carry, size - std::min(size, pos));
+                const uint64_t npieces = (want + kFqPiece - 1) / kFqPiece + 1;
+                while (sl.ev.size() < 2 * (sl.np + npieces) && !r) {
+                    hipEvent_t e = nullptr;
+                    r = ss_check(hipEventCreate(&e), "ingest fastq event");
+                    if (!r) sl.ev.push_back(e);
+                }
+                if (r) break;
+                auto h2d = [&](uint64_t off, uint64_t len) {
+                    int q = ss_check(hipEventRecord(sl.ev[2 * sl.np], g->fq_copy), "ingest fastq event");
+                    if (!q) q = ss_check(hipMemcpyAsync(sl.d.p + off, hv + off, len, hipMemcpyHostToDevice, g->fq_copy), "ingest H2D");
+                    if (!q) q = ss_check(hipEventRecord(sl.ev[2 * sl.np + 1], g->fq_copy), "ingest fastq event");
+                    ++sl.np;
+                    g->fq_h2d_bytes += len;
+                    return q;
+                };
+                if (carry) r = h2d(0, carry);
+                uint64_t got = 0;
+                for (uint64_t off = 0; off < want && !r; off += kFqPiece) {
+                    const uint64_t len = std::min(kFqPiece, want - off);
+                    const auto t0 = Clock::now();
+                    const uint64_t n = read_parallel(fd, hv + carry + off, len, pos + off, threads);
+                    g->fq_ms[0] += since(t0);
+                    got += n;
+                    if (n != len) break;
+                    r = h2d(carry + off, len);
+                }
+                if (r) break;
+                if (got != want) {
+                    r = ss_fail(SS_EHIP, "short read of the FASTQ file");
+                    break;
+                }
+                pos += got;
+                sl.n = carry + got;
+                sl.at_eof = pos >= size;
+                sl.use = sl.n;
+                if (sl.at_eof || sl.n == 0) break;
+                sl.use = 0;
+                for (uint64_t q = sl.n; q > 0; --q)
+                    if (hv[q - 1] == '\n') {
+                        sl.use = q;
+                        break;
+                    }
+                if (sl.use) break;
+                // one line fills the chunk: grow this slot (its bytes kept, sent again as the carry)
+                if ((r = ss_check(hipStreamSynchronize(g->fq_copy), "ingest fastq grow"))) break;
                 HBuf grown;
-                if ((rc = grown.ensure(2 * cap))) break;
-                memcpy(grown.p, hv, n);
-                g->stage.release();
-                g->stage = grown;
+                if ((r = grown.ensure(2 * cap))) break;
+                memcpy(grown.p, hv, sl.n);
+                sl.h.release();
+                sl.h = grown;
                 cap *= 2;
-                carry = n;
-                continue;
+                carry = sl.n;
+                csrc = sl.h.p;
             }
+            if (!r) r = ss_check(hipEventRecord(sl.done, g->fq_copy), "ingest fastq event");
+            sl.rc = r;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                state[k & 1] = 1;
+            }
+            cv.notify_all();
+            if (r || sl.at_eof || sl.n == 0) return;
+            csrc = sl.h.p + sl.use;
+            carry = sl.n - sl.use;
         }
-        // index the chunk on the device (its bytes are on the way: the pieces' H2D copies above)
+    };
+    // a range that fits one chunk has nothing to overlap: it is read on this thread (no thread start)
+    std::thread rd;
+    if (size - begin <= cap0) {
+        reader();
+    } else {
+        try {
+            rd = std::thread(reader);
+        } catch (...) {
+            close(fd);
+            return ss_fail(SS_EHIP, "cannot start the FASTQ reader thread");
+        }
+    }
+    for (uint64_t k = 0; !rc; ++k) {
+        FqSlot& sl = g->fq[k & 1];
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return state[k & 1] == 1; });
+        }
+        if ((rc = sl.rc) || sl.n == 0) break;
+        const uint64_t use = sl.use;
+        const bool at_eof = sl.at_eof;
+        // index the chunk on the device once its H2D pieces are done (the engine's stream waits for them)
         const auto ti = Clock::now();
+        rc = ss_check(hipStreamWaitEvent(s, sl.done, 0), "ingest fastq wait");
         uint64_t maxr = use / 16 + 2;
         uint64_t nl = 0, nrec = 0;
         while (!rc) {
@@ -2098,7 +2185,7 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
             if ((rc = g->fq_ws.ensure(wsb / 8 + 1)) || (rc = g->offs.ensure(maxr)) || (rc = g->dlens.ensure(maxr)) ||
                 (rc = g->fq_aux.ensure(maxr)) || (rc = g->fq_counts.ensure(3)))
                 break;
-            rc = ss_fastq_index_onepass(g->dbuf.p, use, line0, at_eof ? 1 : 0, g->fq_ws.p, wsb, g->offs.p, g->dlens.p,
+            rc = ss_fastq_index_onepass(sl.d.p, use, line0, at_eof ? 1 : 0, g->fq_ws.p, wsb, g->offs.p, g->dlens.p,
                                         g->fq_aux.p, maxr, g->fq_counts.p, s);
             if (!rc) rc = ss_check(hipMemcpyAsync(g->h_bad, g->fq_counts.p, 24, hipMemcpyDeviceToHost, s), "ingest fq");
             if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest fq");
@@ -2114,22 +2201,33 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
         }
         if (rc) break;
         g->fq_ms[2] += since(ti);
-        for (uint64_t q = 0; q < np; ++q) {     // the pieces' H2D times (all complete: the index synced)
+        for (uint32_t q = 0; q < sl.np; ++q) {     // the pieces' H2D times (all complete: the index synced)
             float ms = 0;
-            if (hipEventElapsedTime(&ms, g->fq_ev[2 * q], g->fq_ev[2 * q + 1]) == hipSuccess) g->fq_ms[1] += ms;
+            if (hipEventElapsedTime(&ms, sl.ev[2 * q], sl.ev[2 * q + 1]) == hipSuccess) g->fq_ms[1] += ms;
             else (void)hipGetLastError();
         }
         if (!at_eof && g->est_scale == 1.0 && use) g->est_scale = (double)(size - begin) / (double)use;
         const auto tc = Clock::now();
-        rc = process_chunk(g, g->dbuf.p, g->offs.p, g->dlens.p, use, nrec, 0, nullptr, hv);
+        rc = process_chunk(g, sl.d.p, g->offs.p, g->dlens.p, use, nrec, 0, nullptr, sl.h.p);
         g->fq_ms[3] += since(tc);
         if (rc) break;
         line0 += nl;
         if (at_eof || g->bad_index != kNoSlot) break;
-        rc = ss_check(hipStreamSynchronize(s), "ingest chunk");
-        carry = n - use;
-        memmove(hv, hv + use, carry);
+        if ((rc = ss_check(hipStreamSynchronize(s), "ingest chunk"))) break;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            state[k & 1] = 0;
+        }
+        cv.notify_all();
     }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+    }
+    cv.notify_all();
+    if (rd.joinable()) rd.join();
+    const int rc2 = ss_check(hipStreamSynchronize(g->fq_copy), "ingest fastq copies");
+    if (!rc) rc = rc2;
     close(fd);
     if (!rc) rc = ss_check(hipStreamSynchronize(s), "ingest fastq");
     if (h_nseqs) *h_nseqs = g->nreads - seqs0;
@@ -2283,8 +2381,7 @@ int ss_ingest_export(ss_ingest* g, uint64_t* h_nkeys) {
             hipLaunchKernelGGL(k_count_max, dim3(std::min<unsigned>(grid_of(gr->m, 256), kCountMaxBlocks)), dim3(256), 0,
                                g->stream, gr->counts.p, gr->m,
                                (unsigned long long*)g->mg_take.p);
-    rc = ss_check(hipMemcpyAsync(g->h_bad + 3 * kLenBins + 4, g->mg_take.p, 8, hipMemcpyDeviceToHost, g->stream),
-                  "ingest export max");
+    rc = ss_check(hipMemcpyAsync(g->h_bad + 3 * kLenBins + 4, g->mg_take.p, 8, hipMemcpyDeviceToHost, g->stream), "ingest export max");
     if (!rc) rc = ss_check(hipStreamSynchronize(g->stream), "ingest export");
     if (rc) return rc;
     g->xmax = g->h_bad[3 * kLenBins + 4];
