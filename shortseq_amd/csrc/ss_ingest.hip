@@ -1448,6 +1448,12 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         }
     }
     std::vector<size_t> cls_jobs;
+    struct FixJob {
+        size_t j;
+        uint64_t off, stride, row0;   // its rows' byte offset in g->rows and stride, its first table row
+    };
+    std::vector<FixJob> fix_jobs;
+    uint64_t rows_bytes = 0;
     // new groups' pooled tables: their resets queued (table_get) and set in one dispatch below, before
     // the first insert; whatever is still queued goes out when this function returns
     g->defer_prep = true;
@@ -1476,23 +1482,54 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         if (cls) {
             cls_jobs.push_back(j);     // inserted below, on the class streams
             continue;
-        } else {
-            const uint8_t* src = d_buf;
-            uint64_t stride = dense_L;
-            if (!dense_L) {
-                stride = (jb.bin + 15) / 16 * 16;
-                if ((rc = g->rows.ensure(jb.m * stride))) return rc;
-                if ((rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.bin, g->rows.p, stride, s))) return rc;
-                src = g->rows.p;
+        }
+        // a length 1..32: its rows gathered at a 16-B stride into its own run of g->rows, inserted below
+        const uint64_t stride = dense_L ? dense_L : (jb.bin + 15) / 16 * 16;
+        fix_jobs.push_back({j, rows_bytes, stride, gr.rows});
+        if (!dense_L) rows_bytes += jb.m * stride;
+        // (+1/4: the next chunk's slightly larger share of this length reuses the workspace)
+        if (jb.m >= (1u << 16) && jb.m < (1ull << 30)) (void)ss_counter_reserve(gr.table, jb.m + jb.m / 4);
+        gr.rows += jb.m;
+    }
+    // The lengths' inserts: every table is sized, its row map grown and its workspace reserved above
+    // (host work, syncs), so the gathers, inserts and row maps of up to kSide + 1 lengths now run on
+    // as many streams at once -- a small-RNA chunk has ~15 lengths of a few 100k reads each, whose
+    // short partition kernels left the GPU mostly idle one length after another.
+    if (!fix_jobs.empty()) {
+        if (rows_bytes && (rc = g->rows.ensure(rows_bytes))) return rc;
+        if ((rc = flush_prep(g))) return rc;
+        int used = 0;
+        if (fix_jobs.size() > 1) rc = ss_check(hipEventRecord(g->ev_fork, s), "ingest fork");
+        for (size_t q = 0; q < fix_jobs.size() && !rc; ++q) {
+            const FixJob& fj = fix_jobs[q];
+            const Job& jb = jobs[fj.j];
+            Group& gr = g->groups[jb.bin];
+            const int k = (int)(q % (ss_ingest::kSide + 1));
+            hipStream_t cs = s;
+            if (k > 0) {
+                cs = g->side[k - 1];
+                if (k > used) {
+                    rc = ss_check(hipStreamWaitEvent(cs, g->ev_fork, 0), "ingest fork wait");
+                    used = k;
+                }
             }
-            if ((rc = flush_prep(g))) return rc;
-            // (+1/4: the next chunk's slightly larger share of this length reuses the workspace)
-            if (jb.m >= (1u << 16) && jb.m < (1ull << 30)) (void)ss_counter_reserve(gr.table, jb.m + jb.m / 4);
-            rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, stride, gr.rows, g->first_bad.p + jb.bin, s);
+            const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
+            const uint8_t* src = d_buf;
+            if (!rc && !dense_L) {
+                src = g->rows.p + fj.off;
+                rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.bin, g->rows.p + fj.off, fj.stride, cs);
+            }
+            if (!rc) rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, fj.stride, fj.row0, g->first_bad.p + jb.bin, cs);
+            if (!rc)
+                hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, cs, sel, jb.m, base,
+                                   gr.rowmap.p + fj.row0);
+        }
+        for (int k = 0; k < used; ++k) {     // join (also after an error: nothing may run on past the call)
+            const int e = ss_check(hipEventRecord(g->ev_join[k], g->side[k]), "ingest join");
+            const int w = e ? e : ss_check(hipStreamWaitEvent(s, g->ev_join[k], 0), "ingest join wait");
+            if (!rc) rc = w;
         }
         if (rc) return rc;
-        hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, s, sel, jb.m, base, gr.rowmap.p + gr.rows);
-        gr.rows += jb.m;
     }
     g->defer_prep = false;
     std::vector<uint64_t> cls_base(nj, 0);     // each class job's first table row (the exact redo)
