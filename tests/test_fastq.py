@@ -407,3 +407,32 @@ def test_fastq_gpu_stage_split(gpu, tmp_path, chunk):
         assert s0["h2d_bytes"] == len(data)
     else:
         assert len(data) <= s0["h2d_bytes"] < 2 * len(data)
+
+
+@pytest.mark.gpu
+def test_fastq_gpu_reader_ring(gpu, tmp_path):
+    """The reader ring (a range longer than one chunk: chunk k + 1 read and copied while chunk k is
+    counted): header lines longer than the chunk (a slot grows while the other slot is in use), many
+    chunks, and a rejected read early in the file (the caller stops while the reader is a chunk
+    ahead): the dict, or the error, equals the host path's."""
+    rng = random.Random(31)
+    recs = []
+    for i in range(4000):
+        L = rng.randint(15, 40)
+        hdr = f"@r{i}" + ("x" * rng.randint(2000, 6000) if i % 500 == 7 else "")
+        s = "".join(rng.choice("ACGT") for _ in range(L))
+        recs.append(f"{hdr}\n{s}\n+\n{'I' * L}\n")
+    p = tmp_path / "ring.fq"
+    p.write_text("".join(recs))
+    h = sq.read_and_count_fastq(str(p), device="host")
+    for chunk in (1024, 4096, 1 << 16):
+        d = sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=chunk)
+        assert _items(d) == _items(h), chunk
+    recs[300] = "@bad\nACGTZACGT\n+\nIIIIIIIII\n"
+    p.write_text("".join(recs))
+    with pytest.raises(Exception) as eh:
+        sq.read_and_count_fastq(str(p), device="host")
+    for chunk in (1024, 1 << 16):
+        with pytest.raises(type(eh.value)) as ed:
+            sq.read_and_count_fastq(str(p), device="cuda", _chunk_bytes=chunk)
+        assert str(ed.value) == str(eh.value), chunk
