@@ -780,6 +780,7 @@ struct FqSlot {
     uint64_t n = 0, use = 0;      // bytes in the slot, bytes up to its last newline (n at the range's end)
     bool at_eof = false;
     int rc = SS_OK;
+    std::string err;              // the reader's error message (its last-error string is thread-local)
 };
 
 struct Group {
@@ -2116,71 +2117,76 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
             }
             int r = SS_OK;
             sl.np = 0;
-            for (;;) {
-                if (cap >= (1ull << 32)) {
-                    r = ss_fail(SS_EARG, "a FASTQ line is longer than 2 GiB");
-                    break;
-                }
-                if ((r = sl.h.ensure(cap)) || (r = sl.d.ensure(cap + 16))) break;
-                if (carry && csrc != sl.h.p) memcpy(sl.h.p, csrc, carry);
-                uint8_t* hv = sl.h.p;
-                const uint64_t want = std::min(cap - carry, size - std::min(size, pos));
-                const uint64_t npieces = (want + kFqPiece - 1) / kFqPiece + 1;
-                while (sl.ev.size() < 2 * (sl.np + npieces) && !r) {
-                    hipEvent_t e = nullptr;
-                    r = ss_check(hipEventCreate(&e), "ingest fastq event");
-                    if (!r) sl.ev.push_back(e);
-                }
-                if (r) break;
-                auto h2d = [&](uint64_t off, uint64_t len) {
-                    int q = ss_check(hipEventRecord(sl.ev[2 * sl.np], g->fq_copy), "ingest fastq event");
-                    if (!q) q = ss_check(hipMemcpyAsync(sl.d.p + off, hv + off, len, hipMemcpyHostToDevice, g->fq_copy), "ingest H2D");
-                    if (!q) q = ss_check(hipEventRecord(sl.ev[2 * sl.np + 1], g->fq_copy), "ingest fastq event");
-                    ++sl.np;
-                    g->fq_h2d_bytes += len;
-                    return q;
-                };
-                if (carry) r = h2d(0, carry);
-                uint64_t got = 0;
-                for (uint64_t off = 0; off < want && !r; off += kFqPiece) {
-                    const uint64_t len = std::min(kFqPiece, want - off);
-                    const auto t0 = Clock::now();
-                    const uint64_t n = read_parallel(fd, hv + carry + off, len, pos + off, threads);
-                    g->fq_ms[0] += since(t0);
-                    got += n;
-                    if (n != len) break;
-                    r = h2d(carry + off, len);
-                }
-                if (r) break;
-                if (got != want) {
-                    r = ss_fail(SS_EHIP, "short read of the FASTQ file");
-                    break;
-                }
-                pos += got;
-                sl.n = carry + got;
-                sl.at_eof = pos >= size;
-                sl.use = sl.n;
-                if (sl.at_eof || sl.n == 0) break;
-                sl.use = 0;
-                for (uint64_t q = sl.n; q > 0; --q)
-                    if (hv[q - 1] == '\n') {
-                        sl.use = q;
+            try {
+                for (;;) {
+                    if (cap >= (1ull << 32)) {
+                        r = ss_fail(SS_EARG, "a FASTQ line is longer than 2 GiB");
                         break;
                     }
-                if (sl.use) break;
-                // one line fills the chunk: grow this slot (its bytes kept, sent again as the carry)
-                if ((r = ss_check(hipStreamSynchronize(g->fq_copy), "ingest fastq grow"))) break;
-                HBuf grown;
-                if ((r = grown.ensure(2 * cap))) break;
-                memcpy(grown.p, hv, sl.n);
-                sl.h.release();
-                sl.h = grown;
-                cap *= 2;
-                carry = sl.n;
-                csrc = sl.h.p;
+                    if ((r = sl.h.ensure(cap)) || (r = sl.d.ensure(cap + 16))) break;
+                    if (carry && csrc != sl.h.p) memcpy(sl.h.p, csrc, carry);
+                    uint8_t* hv = sl.h.p;
+                    const uint64_t want = std::min(cap - carry, size - std::min(size, pos));
+                    const uint64_t npieces = (want + kFqPiece - 1) / kFqPiece + 1;
+                    while (sl.ev.size() < 2 * (sl.np + npieces) && !r) {
+                        hipEvent_t e = nullptr;
+                        r = ss_check(hipEventCreate(&e), "ingest fastq event");
+                        if (!r) sl.ev.push_back(e);
+                    }
+                    if (r) break;
+                    auto h2d = [&](uint64_t off, uint64_t len) {
+                        int q = ss_check(hipEventRecord(sl.ev[2 * sl.np], g->fq_copy), "ingest fastq event");
+                        if (!q) q = ss_check(hipMemcpyAsync(sl.d.p + off, hv + off, len, hipMemcpyHostToDevice, g->fq_copy), "ingest H2D");
+                        if (!q) q = ss_check(hipEventRecord(sl.ev[2 * sl.np + 1], g->fq_copy), "ingest fastq event");
+                        ++sl.np;
+                        g->fq_h2d_bytes += len;
+                        return q;
+                    };
+                    if (carry) r = h2d(0, carry);
+                    uint64_t got = 0;
+                    for (uint64_t off = 0; off < want && !r; off += kFqPiece) {
+                        const uint64_t len = std::min(kFqPiece, want - off);
+                        const auto t0 = Clock::now();
+                        const uint64_t n = read_parallel(fd, hv + carry + off, len, pos + off, threads);
+                        g->fq_ms[0] += since(t0);
+                        got += n;
+                        if (n != len) break;
+                        r = h2d(carry + off, len);
+                    }
+                    if (r) break;
+                    if (got != want) {
+                        r = ss_fail(SS_EHIP, "short read of the FASTQ file");
+                        break;
+                    }
+                    pos += got;
+                    sl.n = carry + got;
+                    sl.at_eof = pos >= size;
+                    sl.use = sl.n;
+                    if (sl.at_eof || sl.n == 0) break;
+                    sl.use = 0;
+                    for (uint64_t q = sl.n; q > 0; --q)
+                        if (hv[q - 1] == '\n') {
+                            sl.use = q;
+                            break;
+                        }
+                    if (sl.use) break;
+                    // one line fills the chunk: grow this slot (its bytes kept, sent again as the carry)
+                    if ((r = ss_check(hipStreamSynchronize(g->fq_copy), "ingest fastq grow"))) break;
+                    HBuf grown;
+                    if ((r = grown.ensure(2 * cap))) break;
+                    memcpy(grown.p, hv, sl.n);
+                    sl.h.release();
+                    sl.h = grown;
+                    cap *= 2;
+                    carry = sl.n;
+                    csrc = sl.h.p;
+                }
+            } catch (...) {     // (the event vector, read_parallel's threads)
+                r = ss_fail(SS_ENOMEM, "FASTQ reader: out of host memory");
             }
             if (!r) r = ss_check(hipEventRecord(sl.done, g->fq_copy), "ingest fastq event");
             sl.rc = r;
+            if (r) sl.err = ss_last_error_string();
             {
                 std::lock_guard<std::mutex> lk(mu);
                 state[k & 1] = 1;
@@ -2209,7 +2215,11 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return state[k & 1] == 1; });
         }
-        if ((rc = sl.rc) || sl.n == 0) break;
+        if (sl.rc) {
+            rc = ss_fail(sl.rc, sl.err.c_str());     // (raised again on this thread: the message is thread-local)
+            break;
+        }
+        if (sl.n == 0) break;
         const uint64_t use = sl.use;
         const bool at_eof = sl.at_eof;
         // index the chunk on the device once its H2D pieces are done (the engine's stream waits for them)
