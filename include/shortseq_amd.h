@@ -421,7 +421,9 @@ int ss_ingest_add_fastq(ss_ingest* g, const char* path, uint64_t chunk_bytes, ui
  * results, taken in range order, are the file's counter (first-occurrence order kept: every read of
  * range p precedes every read of range p + 1).  Host calls.  A range longer than one chunk
  * (chunk_bytes; 0 = 1 GiB) is read by a reader thread into two pinned chunk slots: chunk k + 1's
- * file reads and H2D copies (their own stream) run while chunk k is indexed and counted. */
+ * file reads and H2D copies (their own stream) run while chunk k is indexed and counted.  The reader
+ * runs on the GPU's NUMA node's CPUs within the process's affinity mask (SHORTSEQ_FQ_PIN=0: not
+ * pinned), so its pinned slots and the bytes copied into them are node-local. */
 int ss_fastq_split(const char* path, uint32_t nparts, uint64_t* h_begin, uint64_t* h_line0);
 int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, uint64_t end, uint64_t line0,
                               uint64_t chunk_bytes, uint64_t* h_nseqs);

@@ -38,6 +38,8 @@
 // skipped while rows <= capacity / 2); class tables grow through ss_counter_extract_words +
 // ss_counter_merge_words (a length rare in the first chunk and common later).
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -897,6 +899,10 @@ struct ss_ingest {
     uint64_t fq_h2d_bytes = 0;
     FqSlot fq[2];
     hipStream_t fq_copy = nullptr;     // the reader thread's H2D pieces
+    // the reader thread's CPUs: the GPU's NUMA node's (ss_gpu_numa_cpus; looked up once, fq_node -2
+    // until then), so the pinned slots it allocates and the file bytes it copies in are node-local
+    std::vector<int> fq_cpus;
+    int fq_node = -2;
 };
 
 namespace {
@@ -2104,8 +2110,20 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
     std::condition_variable cv;
     int state[2] = {0, 0};
     bool stop = false;
+    if (g->fq_node == -2) {
+        int allowed = 0;
+        g->fq_cpus = ss_gpu_numa_cpus(g->device, &g->fq_node, &allowed);
+        const char* env = getenv("SHORTSEQ_FQ_PIN");
+        if (env && env[0] == '0') g->fq_cpus.clear();
+    }
     auto reader = [&]() {
         (void)hipSetDevice(g->device);
+        if (!g->fq_cpus.empty()) {     // (read_parallel's threads inherit the mask)
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            for (int c : g->fq_cpus) CPU_SET(c, &set);
+            (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+        }
         uint64_t pos = begin, cap = cap0, carry = 0;
         const uint8_t* csrc = nullptr;
         for (uint64_t k = 0;; ++k) {
@@ -2198,8 +2216,9 @@ int ss_ingest_add_fastq_range(ss_ingest* g, const char* path, uint64_t begin, ui
         }
     };
     // a range that fits one chunk has nothing to overlap: it is read on this thread (no thread start)
+    // unless the reader is to run on the GPU's NUMA node (the caller's affinity is left alone)
     std::thread rd;
-    if (size - begin <= cap0) {
+    if (size - begin <= cap0 && g->fq_cpus.empty()) {
         reader();
     } else {
         try {

@@ -3,6 +3,12 @@
 #include <hip/hip_runtime.h>
 #include "../../include/shortseq_amd.h"
 
+#include <vector>
+
+// The CPUs of `device`'s NUMA node (sysfs, by PCI bus id) that this process's affinity mask allows;
+// *node = that node (-1: unknown), *allowed = the mask's CPU count.  Empty when the node is unknown
+// or the intersection is empty (ss_stage.hip: the stager's copy threads, the FASTQ reader ring).
+std::vector<int> ss_gpu_numa_cpus(int device, int* node, int* allowed);
 // Record `msg` as the thread's last error and return `code`.
 int ss_fail(int code, const char* msg);
 // SS_OK if e == hipSuccess, otherwise record "<what>: <hip error string>" and return SS_EHIP.

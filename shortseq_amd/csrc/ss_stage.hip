@@ -321,8 +321,24 @@ int launch_decode(const HostOp& op, const uint8_t* d_in, uint64_t m, uint8_t* d_
     return ss_decode_fixed((const uint64_t*)d_in, m, op.L, op.wpr, d_out, op.stride, s);
 }
 
+// The copy threads' CPUs: the GPU's NUMA node's CPUs that the process's affinity mask allows
+// (ss_gpu_numa_cpus); empty when the node is unknown, the intersection is empty, or
+// SHORTSEQ_STAGE_PIN=0.  Fills the stager's placement fields.
+std::vector<int> placement(ss_stager* st) {
+    int node = -1, allowed = 0;
+    std::vector<int> mine = ss_gpu_numa_cpus(st->device, &node, &allowed);
+    st->affinity_cpus = allowed;
+    st->numa_node = node;
+    const char* env = getenv("SHORTSEQ_STAGE_PIN");
+    if (node < 0 || (env && env[0] == '0')) return {};
+    st->pinned_cpus = (int)mine.size();
+    return mine;
+}
+
+}  // namespace
+
 // CPUs of a sysfs cpulist ("0-7,64-71")
-std::vector<int> parse_cpulist(const char* path) {
+static std::vector<int> parse_cpulist(const char* path) {
     std::vector<int> out;
     FILE* f = fopen(path, "r");
     if (!f) return out;
@@ -346,19 +362,17 @@ std::vector<int> parse_cpulist(const char* path) {
     return out;
 }
 
-// The copy threads' CPUs: the GPU's NUMA node's CPUs (sysfs, by PCI bus id) that the process's
-// affinity mask allows; empty when the node is unknown, the intersection is empty, or
-// SHORTSEQ_STAGE_PIN=0.  Fills the stager's placement fields.
-std::vector<int> placement(ss_stager* st) {
+std::vector<int> ss_gpu_numa_cpus(int device, int* node_out, int* allowed_out) {
     cpu_set_t mask;
     CPU_ZERO(&mask);
     std::vector<int> allowed;
     if (sched_getaffinity(0, sizeof(mask), &mask) == 0)
         for (int c = 0; c < CPU_SETSIZE; ++c)
             if (CPU_ISSET(c, &mask)) allowed.push_back(c);
-    st->affinity_cpus = (int)allowed.size();
+    if (allowed_out) *allowed_out = (int)allowed.size();
+    if (node_out) *node_out = -1;
     char bus[64] = {0};
-    if (hipDeviceGetPCIBusId(bus, sizeof(bus), st->device) != hipSuccess) {
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) {
         (void)hipGetLastError();
         return {};
     }
@@ -371,18 +385,14 @@ std::vector<int> placement(ss_stager* st) {
         if (fscanf(f, "%d", &node) != 1) node = -1;
         fclose(f);
     }
-    st->numa_node = node;
-    const char* env = getenv("SHORTSEQ_STAGE_PIN");
-    if (node < 0 || (env && env[0] == '0')) return {};
+    if (node_out) *node_out = node;
+    if (node < 0) return {};
     snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
     std::vector<int> mine;
     for (int c : parse_cpulist(path))
         if (std::find(allowed.begin(), allowed.end(), c) != allowed.end()) mine.push_back(c);
-    st->pinned_cpus = (int)mine.size();
     return mine;
 }
-
-}  // namespace
 
 extern "C" {
 
