@@ -217,6 +217,27 @@ __device__ __forceinline__ uint64_t encode_word_at(const uint8_t* p, uint32_t nb
     return (uint64_t)lo.v | ((uint64_t)(hi.v | lo.cout) << 32);
 }
 
+// The drop-in engine's short reads (lengths 1..31) as ONE table's keys (ss_ingest's short group):
+// key = the read's packed word | 1 << (2L + 1).  The marker sits above the word's 2L code bits and
+// above bit 2L, where the table path's carry of an aliased last nucleotide lands, so it
+// is the key's highest set bit: keys of different lengths never meet, and the length and the word
+// come back from the key alone.  Row i = read sel[i] (sel null: read i); dense_L > 0: the reads lie
+// back to back, each dense_L bytes.  A rejected read's chunk index goes to *first_bad (atomicMin).
+__global__ __launch_bounds__(256) void k_short_keys(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offs,
+                                                    const uint32_t* __restrict__ lens, const uint64_t* __restrict__ sel,
+                                                    uint64_t m, uint32_t dense_L, uint64_t* __restrict__ keys,
+                                                    unsigned long long* first_bad) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t r = sel ? sel[i] : i;
+        const uint32_t L = dense_L ? dense_L : lens[r];
+        const uint64_t off = dense_L ? r * dense_L : offs[r];
+        uint32_t bad = 0;
+        const uint64_t word = encode_word_at(in + off, L, true, bad);
+        keys[i] = word | (1ull << (2u * L + 1u));
+        if (bad) atomicMin(first_bad, (unsigned long long)r);
+    }
+}
+
 // The ragged kernel's word loader: the 16-B-aligned chunks that hold the word's bytes (three
 // dwordx4 loads, the third clamped to the last chunk holding a byte of the word, so every load stays
 // inside chunks the read touches: no fault past the buffer's last 16-B chunk) realigned by a
@@ -1382,6 +1403,16 @@ int ss_encode_var(const uint8_t* d_ascii, const uint64_t* d_offsets, const uint3
     hipLaunchKernelGGL(k_encode_var_dense, dim3(grid), dim3(kThreads), 0, s, d_ascii, d_offsets, d_lens, n, d_words,
                        wpr, 1.0 / (double)wpr, (unsigned long long*)d_first_bad);
     return ss_check(hipGetLastError(), "k_encode_var_dense");
+}
+
+int ss_short_keys_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, const uint64_t* d_sel,
+                       uint64_t m, uint32_t dense_L, uint64_t* d_keys, uint64_t* d_first_bad, void* stream) {
+    if (dense_L > 31) return ss_fail(SS_EARG, "k_short_keys: reads of 1 to 31 nt");
+    if (m == 0) return SS_OK;
+    const unsigned grid = grid_for(m, 256, 8192);
+    hipLaunchKernelGGL(k_short_keys, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_buf, d_offs, d_lens, d_sel, m,
+                       dense_L, d_keys, (unsigned long long*)d_first_bad);
+    return ss_check(hipGetLastError(), "k_short_keys");
 }
 
 int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n, uint32_t S,

@@ -66,6 +66,11 @@ namespace {
 constexpr uint32_t kClassBin0 = 31;                 // bin of class W = kClassBin0 + W
 constexpr uint32_t kTooLongBin = kClassBin0 + SS_MAX_NT / 32 + 1;
 constexpr uint32_t kLenBins = kTooLongBin + 1;
+// Lengths 1..31 share ONE table, the short group (kept under bin 1): its keys are the packed word
+// with a length marker above it (k_short_keys), so a chunk of small-RNA reads (~15 lengths) is one
+// key pass and one insert instead of a gather and an insert per length; Group.L / GDesc.L = kShortL
+// (the entry's length and word come back from its key).  Length 32 keeps its own table (all 64 bits).
+constexpr uint32_t kShortBin = 1, kShortL = 0xFFFFu;
 // k_len_count / k_len_scatter: one wave per block, 8 per SIMD (2048 blocks, 2 per SIMD, left both
 // passes latency-bound: 0.21 + 0.49 ms for 50M reads), 8 steps' lengths loaded at once (one a step:
 // the f2 count 50 us slower, profiles/r4/f2/libab_lenstep.log)
@@ -392,6 +397,7 @@ struct GDesc {
 };
 
 __device__ __forceinline__ uint32_t entry_len(const GDesc& d, uint64_t e) {
+    if (d.L == kShortL) return (uint32_t)(63 - __clzll((long long)d.words[e])) >> 1;    // marker at 2L + 1
     return d.L ? d.L : (uint32_t)d.words[e * d.W + d.W - 1];
 }
 
@@ -546,7 +552,7 @@ __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict_
     const uint64_t k0 = (uint64_t)blockIdx.x * 256, k = k0 + threadIdx.x;
     if (k0 >= K) return;
     uint32_t L = 0, nw = 0;
-    uint64_t cnt = 0, wo = 0;
+    uint64_t cnt = 0, wo = 0, smask = ~0ull;     // smask: a short-group key's length marker cleared
     const uint64_t* src = nullptr;
     if (k < K) {
         const uint64_t v = ordered[k];
@@ -560,6 +566,7 @@ __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict_
             nw = d.L ? d.W : (L + 31) / 32;
             cnt = d.counts[e];
             src = d.words + e * d.W;
+            if (d.L == kShortL) smask = ~(1ull << (2 * L + 1));
         }
         wo = woff[k];
         if (o.compact) {
@@ -580,7 +587,7 @@ __global__ __launch_bounds__(256) void k_gather_host(const uint64_t* __restrict_
         const uint64_t c1 = min(hi, c0 + kOutBuf);
         for (uint32_t q = 0; q < nw; ++q) {
             const uint64_t o = wo + q;
-            if (o >= c0 && o < c1) buf[o - c0] = src[q];
+            if (o >= c0 && o < c1) buf[o - c0] = src[q] & smask;
         }
         __syncthreads();
         for (uint64_t o = c0 + threadIdx.x; o < c1; o += 256) h_words[o] = buf[o - c0];
@@ -630,7 +637,7 @@ __global__ __launch_bounds__(256) void k_gather_host_waves(const uint64_t* __res
             wo = woff[kn];
         }
         uint32_t L = 0, nw = 0;
-        uint64_t cnt = 0;
+        uint64_t cnt = 0, smask = ~0ull;
         const uint64_t* src = nullptr;
         if (live) {
             const uint32_t g = (uint32_t)(cv >> 32);
@@ -643,6 +650,7 @@ __global__ __launch_bounds__(256) void k_gather_host_waves(const uint64_t* __res
                 nw = d.L ? d.W : (L + 31) / 32;
                 cnt = d.counts[e];
                 src = d.words + e * d.W;
+                if (d.L == kShortL) smask = ~(1ull << (2 * L + 1));
             }
             if (o.compact) {
                 ((uint16_t*)o.hbase)[k] = (uint16_t)L;
@@ -661,7 +669,7 @@ __global__ __launch_bounds__(256) void k_gather_host_waves(const uint64_t* __res
             const uint64_t c1 = min(hi, c0 + kGatherWin);
             for (uint32_t q = 0; q < nw; ++q) {
                 const uint64_t oo = cwo + q;
-                if (oo >= c0 && oo < c1) wb[oo - c0] = src[q];
+                if (oo >= c0 && oo < c1) wb[oo - c0] = src[q] & smask;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1001,7 +1009,8 @@ double hll_estimate(const uint32_t* reg) {
 
 // key kind of a fresh table: the length (fixed by its first insert) or a class's packed words
 int table_kind(const Group& gr, ss_counter* t) {
-    return gr.L ? ss_counter_set_length(t, gr.L) : ss_counter_set_words(t, gr.W1);
+    // (the short group's keys are whole 64-bit words: a length-32 handle)
+    return gr.L ? ss_counter_set_length(t, gr.L == kShortL ? 32u : gr.L) : ss_counter_set_words(t, gr.W1);
 }
 
 // A group whose rows would pass the table's u32 first index (max_rows: 2^32 - 1 reads of one length
@@ -1291,7 +1300,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     uint32_t spec_S = 0;         // the row encode queued behind the split at this stride (gated on the device)
     if (dense_L) {
         if (dense_L > SS_MAX_NT) return ss_fail(SS_EARG, "ingest: dense length > 1024");
-        jobs.push_back({len_bin(dense_L), n, 0, 0});
+        jobs.push_back({dense_L < 32 ? kShortBin : len_bin(dense_L), n, 0, 0});
     } else {
         if ((rc = g->order.ensure(n)) || (rc = g->blkhist.ensure((uint64_t)kLenBins * kSplitBlocks)) ||
             (rc = g->blkfirst.ensure((uint64_t)kLenBins * kSplitBlocks)) || (rc = g->split_out.ensure(3 * kLenBins + 1)))
@@ -1344,10 +1353,19 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         }
         const uint64_t* hh = g->h_split;
         if (spec_S && hh[3 * kLenBins] != spec_S) spec_S = 0;    // the queued encode did nothing (or is rewritten)
+        Job shortj{kShortBin, 0, 0, kNoSlot};     // lengths 1..31: contiguous bins of the split, one job
         for (uint32_t b = 0; b < kLenBins; ++b) {
             const uint64_t m = hh[b];
             if (!m) continue;
             const uint64_t f = hh[kLenBins + b];
+            if (b >= 1 && b <= 31) {
+                if (shortj.m && shortj.start + shortj.m != hh[2 * kLenBins + b])
+                    return ss_fail(SS_EARG, "ingest: the split's short-length bins are not contiguous");
+                if (!shortj.m) shortj.start = hh[2 * kLenBins + b];
+                shortj.m += m;
+                shortj.first = std::min(shortj.first, f);
+                continue;      // (pushed after the loop, ahead of the others)
+            }
             if (b == 0) {
                 g->empty_count += m;
                 g->empty_first = std::min(g->empty_first, base + f);
@@ -1361,6 +1379,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
                 jobs.push_back({b, m, hh[2 * kLenBins + b], f});
             }
         }
+        if (shortj.m) jobs.insert(jobs.begin(), shortj);
     }
     const size_t nj = jobs.size();
     if ((rc = g->ovf.ensure(nj + 1))) return rc;
@@ -1478,7 +1497,7 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
         // past the first rejected read)
         if (!live(jb) && !(cls && fused)) continue;
         Group& gr = g->groups[jb.bin];
-        gr.L = cls ? 0u : jb.bin;
+        gr.L = cls ? 0u : jb.bin == kShortBin ? kShortL : jb.bin;
         gr.W1 = cls ? jb.bin - kClassBin0 + 1 : 1u;
         const uint64_t need = std::min<uint64_t>(gr.rows + jb.m, cls ? need_cls[gr.W1 - 1] : ~0ull);
         if ((rc = group_room(g, gr, jb.m, need))) return rc;
@@ -1490,10 +1509,12 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             cls_jobs.push_back(j);     // inserted below, on the class streams
             continue;
         }
-        // a length 1..32: its rows gathered at a 16-B stride into its own run of g->rows, inserted below
-        const uint64_t stride = dense_L ? dense_L : (jb.bin + 15) / 16 * 16;
+        // length 32: its rows gathered at a 16-B stride into its own run of g->rows; the short group:
+        // its keys there (8 B per read); inserted below
+        const bool shortg = jb.bin == kShortBin;
+        const uint64_t stride = shortg ? 8 : dense_L ? dense_L : (jb.bin + 15) / 16 * 16;
         fix_jobs.push_back({j, rows_bytes, stride, gr.rows});
-        if (!dense_L) rows_bytes += jb.m * stride;
+        if (shortg || !dense_L) rows_bytes += (jb.m * stride + 255) & ~255ull;     // (runs 16-B aligned)
         // (+1/4: the next chunk's slightly larger share of this length reuses the workspace)
         if (jb.m >= (1u << 16) && jb.m < (1ull << 30)) (void)ss_counter_reserve(gr.table, jb.m + jb.m / 4);
         gr.rows += jb.m;
@@ -1522,11 +1543,17 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
             }
             const uint64_t* sel = dense_L ? nullptr : g->order.p + jb.start;
             const uint8_t* src = d_buf;
-            if (!rc && !dense_L) {
-                src = g->rows.p + fj.off;
-                rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.bin, g->rows.p + fj.off, fj.stride, cs);
+            if (jb.bin == kShortBin) {      // the short group: keys with their length markers, one insert
+                uint64_t* keys = (uint64_t*)(g->rows.p + fj.off);
+                if (!rc) rc = ss_short_keys_impl(d_buf, d_offs, d_lens, sel, jb.m, dense_L, keys, g->first_bad.p + jb.bin, cs);
+                if (!rc) rc = ss_counter_insert_keys(gr.table, keys, jb.m, fj.row0, cs);
+            } else {
+                if (!rc && !dense_L) {
+                    src = g->rows.p + fj.off;
+                    rc = ss_gather_rows(d_buf, nbytes, d_offs, sel, jb.m, jb.bin, g->rows.p + fj.off, fj.stride, cs);
+                }
+                if (!rc) rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, fj.stride, fj.row0, g->first_bad.p + jb.bin, cs);
             }
-            if (!rc) rc = ss_counter_insert_fixed(gr.table, src, jb.m, jb.bin, fj.stride, fj.row0, g->first_bad.p + jb.bin, cs);
             if (!rc)
                 hipLaunchKernelGGL(k_rowmap, dim3(grid_of(jb.m, 256)), dim3(256), 0, cs, sel, jb.m, base,
                                    gr.rowmap.p + fj.row0);
@@ -1700,8 +1727,9 @@ int process_chunk(ss_ingest* g, const uint8_t* d_buf, const uint64_t* d_offs, co
     for (size_t j = 0; j <= nj; ++j) {
         const uint64_t fb = hb[j < nj ? jobs[j].bin : kLenBins];
         if (fb == kNoSlot || (j < nj && base + jobs[j].first > g->bad_index)) continue;
-        // a length's insert reports its row (rows are in read order); the class encodes report the read
-        const bool by_row = j < nj && !dense_L && jobs[j].bin <= 32;
+        // a length's insert reports its row (rows are in read order); the class encodes and the short
+        // group's keys report the read
+        const bool by_row = j < nj && !dense_L && jobs[j].bin <= 32 && jobs[j].bin != kShortBin;
         uint64_t idx = fb;
         if (by_row) {
             rc = ss_check(hipMemcpy(&idx, g->order.p + jobs[j].start + fb, 8, hipMemcpyDeviceToHost), "ingest bad row");

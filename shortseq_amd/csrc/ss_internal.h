@@ -45,6 +45,13 @@ extern "C" int ss_encode_classes_impl(const uint8_t* d_buf, const uint64_t* d_of
 extern "C" int ss_encode_rows_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens, uint64_t n,
                                    uint32_t S, uint64_t* d_out, uint64_t* d_fps, uint32_t* d_hll,
                                    uint64_t* d_first_bad, void* stream, const uint64_t* d_gate = nullptr);
+// The drop-in engine's short reads (1..31 nt) as keys of one table: d_keys[i] = the packed word of
+// read d_sel[i] (d_sel null: read i) | 1 << (2L + 1), the length marker above the word and its
+// table-path carry bit (k_short_keys, ss_codec.hip); dense_L > 0: reads back to back of that length.
+// *d_first_bad (not reset) = min chunk read index with a rejected byte.
+extern "C" int ss_short_keys_impl(const uint8_t* d_buf, const uint64_t* d_offs, const uint32_t* d_lens,
+                                  const uint64_t* d_sel, uint64_t m, uint32_t dense_L, uint64_t* d_keys,
+                                  uint64_t* d_first_bad, void* stream);
 // Single-word keys already computed on the device (d_keys[n], any 64-bit values): counted with the
 // optimistic partitioned insert (12-B records, LDS aggregation) -- e.g. the class rows' fingerprints.
 extern "C" int ss_counter_insert_keys(ss_counter* c, const uint64_t* d_keys, uint64_t n, uint64_t base_index,

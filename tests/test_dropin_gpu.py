@@ -50,6 +50,37 @@ def test_counter_gpu_equals_host_mixed(gpu):
     assert dev[sq.pack("G" * 32)] == host[sq.pack("G" * 32)]
 
 
+def test_counter_gpu_short_group(gpu):
+    """Lengths 1..31 share one table (each key = the packed word with a length marker above it and
+    above its table-path carry bit): a read whose last byte is aliased (\\x01 \\x03 \\x07 \\x14, whose
+    carry lands on bit 2L) stays apart from the read with an 'A' there and from the read one base
+    longer; ragged and dense (one-length) batches; the first rejected read is the first in input
+    order across lengths."""
+    rng = random.Random(41)
+    pool = []
+    for L in range(1, 32):
+        for _ in range(3):
+            s = bytes(rng.choice(b"ACGT") for _ in range(L))
+            pool.append(s)
+            pool += [s[:-1] + a for a in (b"\x01", b"\x03", b"\x07", b"\x14", b"A")]
+            pool.append(s + b"A")
+    reads = [rng.choice(pool) for _ in range(60_000)]
+    host = ShortSeqCounter(reads, device="host")
+    assert _items(ShortSeqCounter(reads, device="cuda")) == _items(host)
+    for L in (1, 7, 20, 31):
+        one = [r for r in pool if len(r) == L]
+        dense = [rng.choice(one) for _ in range(20_000)]
+        assert _items(ShortSeqCounter(dense, device="cuda")) == _items(ShortSeqCounter(dense, device="host")), L
+    bad = list(reads)
+    bad[40_000] = b"ACGTN" + b"A" * 20
+    bad[30_000] = b"ACX"
+    with pytest.raises(Exception) as ei_h:
+        ShortSeqCounter(bad, device="host")
+    with pytest.raises(Exception) as ei_d:
+        ShortSeqCounter(bad, device="cuda")
+    assert str(ei_d.value) == str(ei_h.value) == "Unsupported base character: X"
+
+
 def test_counter_gpu_errors_first_bad(gpu):
     rng = random.Random(4)
     reads = [bytes(rng.choice(b"ACGT") for _ in range(rng.choice([8, 32, 50]))) for _ in range(70_000)]
