@@ -365,7 +365,8 @@ int ss_counter_merge_packed(ss_counter* c, const void* d_rec, const uint64_t* d_
  * Ragged read streams counted on the GPU — the batch engine behind the drop-in ShortSeqCounter(list)
  * (counter.pyx:22-39: _count_py_bytes_list -> _from_py_bytes -> _count_sequence) and
  * read_and_count_fastq (counter.pyx:57-70 + fast_read.pyx:3-20).  Host calls, synchronous, one
- * engine per thread; the engine owns its stream, pinned staging and per-length counter tables.
+ * engine per thread; the engine owns its stream, pinned staging and counter tables (one for lengths 1-31 --
+ * the packed word with a length marker at bit 2L + 1 -- one for 32, one per length class).
  *   ss_ingest_staging:  a pinned buffer of >= nbytes the caller fills with the reads back to back
  *                       (valid until the next staging / add call).
  *   ss_ingest_add_blob: count n reads of h_blob (read i = the next h_lens[i] bytes); global indices
@@ -463,7 +464,7 @@ int ss_ingest_results_compact(ss_ingest* g, const uint16_t** h_lens, const void*
  *                     thread after its adds (the shards' exports run concurrently).
  *   ss_ingest_merge:  fold an exported engine into dst: its entries cross to dst's device (peer copies
  *                     over xGMI, hipMemcpyPeerAsync; a device copy when both share a device), become
- *                     rows of dst's per-length / per-class tables appended as one block (first read =
+ *                     rows of dst's tables (short group, length 32, classes) appended as one block (first read =
  *                     src_base + the entry's own), counts add, first index = min.  Sources follow
  *                     dst's reads in input order (src_base = the reads before the source's shard,
  *                     increasing from call to call).  Then ss_ingest_finish(dst) orders the union.

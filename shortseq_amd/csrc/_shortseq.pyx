@@ -500,7 +500,7 @@ cdef class ShortSeqCounter(dict):
 
     ShortSeqCounter(list_of_bytes, device="auto"): lists of >= GPU_MIN_READS reads are encoded and
     counted on the GPU (ss_ingest: split on the device into lengths 1-32 and length classes 33-1024,
-    one counter table per length / class, the key being (length, words));
+    counter tables keyed by (length, words): lengths 1-31 in one, 32 in one, a class each);
     device="host" forces the per-object host path, device="cuda"/"cuda:N" forces the GPU.
     """
 
@@ -871,7 +871,7 @@ def _count_batch_gpu(ShortSeqCounter self, list reads, devs):
     """Batch path (counter.pyx:22-39 over a whole list): the list is cut into len(devs) contiguous
     shards; each shard's bytes objects are copied back to back into its engine's pinned staging
     buffer and counted on that engine's device (split on the device into lengths 1-32 and length
-    classes, one table per length / class: the length is part of the key, short_seq_64.pyx:41-44),
+    classes, tables keyed by length and words (lengths 1-31 share one): the length is part of the key, short_seq_64.pyx:41-44),
     the shards concurrently.  Several shards reduce on the devices into the first shard's engine
     (_reduce_fill: ss_ingest_export + ss_ingest_merge), which orders the union by global first read
     -- the first-occurrence order of the whole list.  The first rejected read in list order raises
