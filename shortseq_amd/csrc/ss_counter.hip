@@ -987,21 +987,33 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
     const bool odd = (lane & 1u) != 0;
     // tile offset of the read a lane holds at step j (G16: the lane-pair permutation of the wave's 64)
-    auto eoff = [&](int j) -> uint32_t {
-        return G16 ? (uint32_t)j * T + wbase + ((lane & 1u) << 5) + (lane >> 1) : (uint32_t)j * T + threadIdx.x;
-    };
+    // (el: the lane's step-0 offset, made opaque per tile below so that the compiler recomputes the
+    // RPL offsets in each tile instead of keeping them all live across the tile loop)
+    const uint32_t el0 = G16 ? wbase + ((lane & 1u) << 5) + (lane >> 1) : threadIdx.x;
+    uint32_t el = el0;
+    auto eoff = [&](int j) -> uint32_t { return (uint32_t)j * T + el; };
     uint4 nx[RPL][2];
     uint64_t nk[RPL];
     // branch-free loads (read index clamped to the last read; lanes past n are never live): the
     // compiler then waits for each chunk just before its encode instead of for all 2 * RPL loads
     const uint32_t hi16 = cpr > 1 ? 1u : 0u;    // L = 16: one chunk (the high half reads 'A's below)
+    // G16: read A's tile-relative index at step 0 (read B = + 32); inside a tile the index math is
+    // 32-bit from a per-tile base (the 64-bit clamp and multiply per load cost ~10 VALU each, ~1/8 of
+    // the pass's VALU, and held 64-bit indices live through the encode)
+    const uint32_t s16 = (uint32_t)stride16, relA0 = wbase + (lane >> 1);
+    uint32_t relA = relA0;                      // (opaque per tile, as el)
     auto load_tile = [&](uint64_t tile) {
+        const uint32_t offA = relA * s16 + (lane & 1u);     // in 16-B units
+        const uint64_t tb = tile * TILE;
+        const uint4* ub = in + tb * stride16;                                // the tile's rows (uniform)
+        // a partial last tile clamps every offset to its last read's high chunk (lanes past n are
+        // never live); a full tile's bound is no bound
+        const uint32_t lim = tb + TILE <= n ? 0xFFFFFFFFu : (uint32_t)(n - 1 - tb) * s16 + 1u;
 #pragma unroll
         for (int j = 0; j < RPL; ++j) {
             if constexpr (G16) {
-                const uint64_t r0 = tile * TILE + (uint64_t)j * T + wbase + (lane >> 1);
-                nx[j][0] = ld_stream(&in[min(r0, n - 1) * stride16 + (lane & 1u)]);
-                nx[j][1] = ld_stream(&in[min(r0 + 32, n - 1) * stride16 + (lane & 1u)]);
+                nx[j][0] = ld_stream(ub + min(offA + (uint32_t)j * T * s16, lim));
+                nx[j][1] = ld_stream(ub + min(offA + ((uint32_t)j * T + 32u) * s16, lim));
             } else {
                 const uint64_t r = min(tile * TILE + j * T + threadIdx.x, n - 1);
                 if constexpr (KEYS) {
@@ -1041,6 +1053,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
     // for its own barrier B, which every wave reaches only after this tile's write-out.  A tile with
     // a heavy bin adds three: (D) deduplicated, (E) survivors counted, (F) heavy bins reserved.
     for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        relA = relA0;
+        el = el0;
+        asm volatile("" : "+v"(relA), "+v"(el));
         load_tile(tile);
         uint64_t key[RPL];
         uint32_t br[RPL];     // bin << 16 | rank in the bin (one register per read)
@@ -1059,9 +1074,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
                 const uint32_t bc = swap_pair(b.cout);               // odd: the carry out of B's low half
                 const uint32_t lo = odd ? recv : a.v;
                 const uint32_t hi = odd ? (b.v | bc) : (recv | a.cout);
-                const uint64_t ra = t0 + (uint64_t)j * T + wbase + (lane >> 1);
-                report_bad(ra < n && a.bad != 0u, ra, first_bad);
-                report_bad(ra + 32 < n && b.bad != 0u, ra + 32, first_bad);
+                const uint32_t ra = (uint32_t)j * T + relA;      // tile-relative
+                report_bad(ra < cnt && a.bad != 0u, t0 + ra, first_bad);
+                report_bad(ra + 32u < cnt && b.bad != 0u, t0 + ra + 32u, first_bad);
                 key[j] = (uint64_t)lo | ((uint64_t)hi << 32);
             } else {
                 const uint64_t r = t0 + j * T + threadIdx.x;
