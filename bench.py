@@ -671,15 +671,16 @@ def bench_dropin_multidevice(n=8_000_000, L=32, U=1 << 22):
             "note": "wall time incl. building the dict; the shards reduce as a tree over peer copies"}
 
 
-def _fastq_case_file():
+def _fastq_case_file(reps=128):
     """The small-RNA-like FASTQ of tools/probe_fastq_e2e.py: 8.4M ragged 18-32-nt records, 65,536
-    distinct sequences each 128 times (528 MB), written once to a temporary file."""
+    distinct sequences each 128 times (528 MB; reps=512: the same pool 4x as long, 2.1 GB, three
+    1-GiB chunks through the reader ring), written once to a temporary file."""
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import probe_fastq_e2e as P
     d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
-    path = os.path.join(d, "smallrna.fq")
-    n = P.write_pool_file(path)
+    path = os.path.join(d, f"smallrna_{reps}.fq")
+    n = P.write_pool_file(path, reps=reps)
     return path, n
 
 
@@ -1023,6 +1024,18 @@ def main():
             log("a18 read_and_count_fastq drop-in")
             fq_path, fq_n = _fastq_case_file()
             local_extra("A18_read_and_count_fastq_smallrna", lambda: bench_fastq_dropin(fq_path, fq_n))
+            os.remove(fq_path)
+            log("a18 read_and_count_fastq drop-in, 2.1-GB file (three chunks)")
+
+            def a18_long():
+                p4, n4 = _fastq_case_file(512)
+                try:
+                    r = bench_fastq_dropin(p4, n4)
+                finally:
+                    os.remove(p4)
+                return {k: r[k] for k in ("records", "file_bytes", "s_per_call", "records_per_s", "h2d_GB_per_s",
+                                          "floor_frac") if k in r}
+            local_extra("A18_read_and_count_fastq_2GB", a18_long)
         result["extra"] = extra
 
     if rank == 0:
