@@ -511,6 +511,18 @@ __device__ __forceinline__ uint32_t region_of(const Tbl& t, uint64_t key) {
     return (uint32_t)(slot_top(t, key) >> t.slice_log);
 }
 
+// The optimistic partition (k_pf_coarse -> k_pf_scatter -> k_pc_aggregate_slice<REC12>) carries each
+// key as its slot hash h = key * kSlotMul (a bijection of the u64 keys: kSlotInv is the multiplier's
+// inverse mod 2^64), so the passes after the coarse one take region and home slot from h by shifts
+// instead of a 64-bit multiply per use; the aggregate turns h back into the key once per used slot
+// when it writes the slice.  Spill records carry the key itself (k_spill_insert uses tbl_add).
+constexpr uint64_t kSlotMul = 0x9E3779B97F4A7C15ull, kSlotInv = 0xF1DE83E19937733Dull;
+static_assert(kSlotMul * kSlotInv == 1ull, "inverse of the slot hash multiplier");
+constexpr uint64_t kEmptyH = kEmpty * kSlotMul;   // h of the EMPTY key (the sentinel's records)
+__device__ __forceinline__ uint32_t region_of_h(const Tbl& t, uint64_t h) {
+    return t.shift >= 64 ? 0u : (uint32_t)((h >> t.shift) >> t.slice_log);
+}
+
 // bin of a key for a pass: COARSE -> top kCoarseBits of the region id, else the region id
 template <bool COARSE>
 __device__ __forceinline__ uint32_t bin_of(const Tbl& t, const PartWs& w, uint64_t key) {
@@ -1087,8 +1099,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
                 report_bad(live && (a.bad | b.bad) != 0u, r, first_bad);
                 key[j] = (uint64_t)a.v | ((uint64_t)(b.v | a.cout) << 32);
             }
+            key[j] *= kSlotMul;                                          // h from here on
             if (live) {
-                const uint32_t b = region_of(t, key[j]) >> shift;
+                const uint32_t b = region_of_h(t, key[j]) >> shift;
                 br[j] = (b << 16) | atomicAdd(&lcount[b], 1u);
             }
         }
@@ -1199,12 +1212,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4))) void k_p
                 r.khi = (uint32_t)(k >> 32);
                 r.idx = c > 1 ? (idx | kWeighted) : idx;
                 ((Rec12*)w.akey)[at] = r;
-                if (!w.slab) w.areg[at] = (uint8_t)(region_of(t, k) & ((1u << shift) - 1u));
+                if (!w.slab) w.areg[at] = (uint8_t)(region_of_h(t, k) & ((1u << shift) - 1u));
                 if (c > 1) w.acnt[at] = c;
             } else {
                 const uint64_t sp = (uint64_t)sbase[b] + (pos - max((uint64_t)gbase[b], cap1));
+                const uint64_t key = k * kSlotInv;                           // (the spill takes keys)
                 if (sp < w.spill_cap)
-                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), c, idx);
+                    w.spill[sp] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), c, idx);
                 else
                     atomicOr(t.overflow, kOvfTable);
             }
@@ -1399,7 +1413,7 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
         for (int j = 0; j < (int)(kTile / T); ++j) {
             const uint32_t e = j * T + threadIdx.x;
             if (e < cnt) {
-                lb[j] = region_of(t, key[j]) - r0;
+                lb[j] = region_of_h(t, key[j]) - r0;
                 rank[j] = atomicAdd(&lcount[lb[j]], 1u);
             }
         }
@@ -1429,7 +1443,7 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
                 const uint32_t i = i0 + threadIdx.x;
                 const uint64_t k = i < cnt ? skey[i] : 0ull;
                 const uint32_t x = i < cnt ? sidx[i] : kWeighted;
-                const bool act = i < cnt && lcount[region_of(t, k) - r0] > heavy_at && !(x & kWeighted);
+                const bool act = i < cnt && lcount[region_of_h(t, k) - r0] > heavy_at && !(x & kWeighted);
                 if (!act) continue;
                 uint32_t h = dedup_home(k, kHtLog);
                 for (;;) {
@@ -1450,7 +1464,7 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
             }
             __syncthreads();
             for (uint32_t i = threadIdx.x; i < cnt; i += T) {
-                const uint32_t b = region_of(t, skey[i]) - r0;
+                const uint32_t b = region_of_h(t, skey[i]) - r0;
                 if (lcount[b] > heavy_at && sidx[i] != kDead) atomicAdd(&hcnt[b], 1u);
             }
             for (uint32_t i = threadIdx.x; i < nb; i += T)
@@ -1466,7 +1480,7 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
             const uint64_t k = skey[i];
             const uint32_t x = sidx[i];
             if (x == kDead) continue;
-            const uint32_t b = region_of(t, k) - r0;
+            const uint32_t b = region_of_h(t, k) - r0;
             uint32_t local, c = 1;
             if (heavy_tile && lcount[b] > heavy_at) {
                 local = atomicAdd(&lstart[b], 1u);
@@ -1491,8 +1505,9 @@ __global__ __launch_bounds__(T) void k_pf_scatter(Tbl t, PartWs w, uint64_t cap1
                 // the region's slab of this sub-bin is full: the record goes to the spill list
                 // (counted by k_spill_insert after the aggregate)
                 const uint64_t sp = atomicAdd(w.spill_ctr, 1u);
+                const uint64_t key = k * kSlotInv;                           // (the spill takes keys)
                 if (sp < w.spill_cap)
-                    w.spill[sp] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), c, xi & ~kWeighted);
+                    w.spill[sp] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), c, xi & ~kWeighted);
                 else
                     atomicOr(t.overflow, kOvfTable);
                 continue;
@@ -1555,22 +1570,23 @@ constexpr int kAggP = 4;               // records per thread per aggregate step 
 // runs ceil(longest probe / G) rounds instead of the longest probe.  Returns mask + 1 if full.
 constexpr int kAggProbe = 2;   // probe rounds of 1 / 2 / 4 / 8 slots: aggregate 0.72 / 0.58 / 0.60 / 0.63 ms (U 2^24)
 template <int G>
-__device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t mask, uint32_t off, uint64_t key) {
+__device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t mask, uint32_t off, uint64_t key,
+                                              uint64_t empty = kEmpty) {
     const uint32_t S = mask + 1;
     for (uint32_t done = 0; done < S;) {
         unsigned long long cur[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) cur[g] = skey[(off + g) & mask];
         int hit = -1;
-        bool empty = false;
+        bool free_at = false;
 #pragma unroll
-        for (int g = G - 1; g >= 0; --g) {     // the lowest g holding the key or EMPTY
+        for (int g = G - 1; g >= 0; --g) {     // the lowest g holding the key or the empty marker
             if (cur[g] == key) {
                 hit = g;
-                empty = false;
-            } else if (cur[g] == kEmpty) {
+                free_at = false;
+            } else if (cur[g] == empty) {
                 hit = g;
-                empty = true;
+                free_at = true;
             }
         }
         if (hit < 0) {
@@ -1579,9 +1595,9 @@ __device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t
             continue;
         }
         const uint32_t at = (off + (uint32_t)hit) & mask;
-        if (!empty) return at;
-        const unsigned long long prev = atomicCAS(&skey[at], (unsigned long long)kEmpty, (unsigned long long)key);
-        if (prev == kEmpty || prev == key) return at;
+        if (!free_at) return at;
+        const unsigned long long prev = atomicCAS(&skey[at], (unsigned long long)empty, (unsigned long long)key);
+        if (prev == empty || prev == key) return at;
         off = (at + 1) & mask;                 // taken by another key: go on after it
         done += (uint32_t)hit + 1;
     }
@@ -1615,12 +1631,18 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     } else {
         meta = w.rstart[region + (lane & 1u)];
     }
+    // REC12 (the optimistic partition): records, and the LDS slice, hold h = key * kSlotMul; the
+    // sentinel key's h (kEmptyH) never enters the slice, so it marks the free slots there
+    constexpr uint64_t kE = REC12 ? kEmptyH : kEmpty;
     // fresh: the fill does not wait on any load (one loop with a per-slot select waited for the
     // segment-table load in its first iteration)
     if (fresh) {
-        for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = kEmpty;
+        for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = kE;
     } else {
-        for (uint32_t i = threadIdx.x; i < S; i += T) skey[i] = t.slots[slice_base + i].key;
+        for (uint32_t i = threadIdx.x; i < S; i += T) {
+            const uint64_t k = t.slots[slice_base + i].key;
+            skey[i] = REC12 ? (k == kEmpty ? kEmptyH : k * kSlotMul) : k;
+        }
     }
     for (uint32_t i = threadIdx.x; i < S; i += T) {
         bcnt[i] = 0;
@@ -1680,6 +1702,52 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
         }
     };
     if (total) load_step(0);   // in flight across the barrier that publishes the LDS fill
+    // a record's home slot in the slice (before the mask); REC12 records are h already
+    auto home_of = [&](uint64_t k) -> uint64_t {
+        return REC12 ? (t.shift >= 64 ? 0ull : k >> t.shift) : slot_top(t, k);
+    };
+    // one probe round of kAggProbe slots from `off` (the lds_probe rule): true with `at` = the key's
+    // slot (found or claimed by an LDS CAS) or S (the slice is full); false with off / done past it
+    auto probe_round = [&](uint64_t k, uint32_t& off, uint32_t& done, uint32_t& at) -> bool {
+        constexpr int G = kAggProbe;
+        const uint32_t mask = (uint32_t)t.slice_mask;
+        unsigned long long cur[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) cur[g] = skey[(off + g) & mask];
+        int hit = -1;
+        bool free_at = false;
+#pragma unroll
+        for (int g = G - 1; g >= 0; --g) {
+            if (cur[g] == k) {
+                hit = g;
+                free_at = false;
+            } else if (cur[g] == kE) {
+                hit = g;
+                free_at = true;
+            }
+        }
+        if (hit >= 0) {
+            at = (off + (uint32_t)hit) & mask;
+            if (!free_at) return true;
+            const unsigned long long prev = atomicCAS(&skey[at], (unsigned long long)kE, (unsigned long long)k);
+            if (prev == kE || prev == k) return true;
+            off = (at + 1) & mask;                 // taken by another key: go on after it
+            done += (uint32_t)hit + 1;
+        } else {
+            off = (off + G) & mask;
+            done += G;
+        }
+        at = S;
+        return done >= S;
+    };
+    auto commit = [&](uint32_t at, uint32_t c, uint32_t ix) {
+        if (at == S) {
+            atomicOr(t.overflow, kOvfTable);
+        } else {
+            atomicAdd(&bcnt[at], c);
+            atomicMin(&bfst[at], ix);
+        }
+    };
     __syncthreads();
     for (uint32_t e0 = 0; e0 < total; e0 += kP * T) {
         uint64_t key[kP];
@@ -1699,31 +1767,61 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
             cw[q] = (valid && (idx[q] & kWeighted)) ? w.bcnt[el[q]] : 1u;
         }
         load_step(e0 + kP * T);
+        // Every record gets one probe round (kAggProbe slots) first, straight-line; the records still
+        // probing after it (~1 in 7 at half load) are then walked by their own lane one after another,
+        // so the wave runs its longest lane's remaining rounds in total, where a probe loop per record
+        // ran the longest lane's rounds for each of the kP records in turn (~15 rounds per step
+        // against ~9, and ~5 for the stragglers alone, by simulation of a 2048-slot slice at half load)
+        uint32_t pend = 0, soff[kP];
 #pragma unroll
         for (int q = 0; q < kP; ++q) {
             const bool valid = e0 + q * T + threadIdx.x < total;
-            uint32_t c = cw[q], ix = idx[q] & ~kWeighted;
-            if (valid && key[q] == kEmpty) {
-                atomicAdd(&sent[0], c);
-                atomicMin(&sent[1], ix);
+            soff[q] = 0;
+            if (valid && key[q] == kE) {
+                atomicAdd(&sent[0], cw[q]);
+                atomicMin(&sent[1], idx[q] & ~kWeighted);
             }
-            if (!valid || key[q] == kEmpty) continue;
-            const uint32_t off = lds_probe<kAggProbe>(skey, (uint32_t)t.slice_mask,
-                                                          (uint32_t)(slot_top(t, key[q]) & t.slice_mask), key[q]);
-            if (off == S) {
-                atomicOr(t.overflow, kOvfTable);
-                continue;
+            if (!valid || key[q] == kE) continue;
+            uint32_t off = (uint32_t)(home_of(key[q]) & t.slice_mask), done = 0, at;
+            if (probe_round(key[q], off, done, at))
+                commit(at, cw[q], idx[q] & ~kWeighted);
+            else {
+                pend |= 1u << q;
+                soff[q] = off;
             }
-            atomicAdd(&bcnt[off], c);
-            atomicMin(&bfst[off], ix);
+        }
+        if (__ballot(pend != 0)) {
+            uint64_t k = 0;
+            uint32_t off = 0, done = 0, c = 0, ix = 0;
+            auto pick = [&]() {   // the lowest pending record becomes the lane's current one
+#pragma unroll
+                for (int q = kP - 1; q >= 0; --q)
+                    if (pend & (1u << q)) {
+                        k = key[q];
+                        off = soff[q];
+                        c = cw[q];
+                        ix = idx[q] & ~kWeighted;
+                    }
+                done = (off - (uint32_t)home_of(k)) & (uint32_t)t.slice_mask;   // < S while probing
+            };
+            if (pend) pick();
+            while (__ballot(pend != 0)) {
+                uint32_t at;
+                if (pend && probe_round(k, off, done, at)) {
+                    commit(at, c, ix);
+                    pend &= pend - 1u;
+                    if (pend) pick();
+                }
+            }
         }
     }
     __syncthreads();
     uint32_t used = 0;
     uint4* sl = (uint4*)&t.slots[slice_base];
     for (uint32_t i = threadIdx.x; i < S; i += T) {
-        const unsigned long long k = skey[i];
-        used += k != kEmpty ? 1u : 0u;
+        const unsigned long long kh = skey[i];
+        used += kh != kE ? 1u : 0u;
+        const unsigned long long k = REC12 ? (kh != kE ? kh * kSlotInv : kEmpty) : kh;
         const uint32_t bc = bcnt[i];
         if (fresh) {   // every slot, one dwordx4 each (empty slots as the reset pattern)
             sl[i] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), ~bc,
