@@ -1563,45 +1563,47 @@ constexpr int kAggP = 4;               // records per thread per aggregate step 
 // fresh: the table was reset and the reset is still pending (ss_counter_reset is lazy): the slice is
 // taken as empty instead of loaded, and written back whole (empty slots as the 0xFF reset pattern),
 // which replaces the table-sized reset memset and the slice read.
-// Linear probe of an LDS slice (mask + 1 slots) for `key` from its home slot `off`: the first slot
-// holding the key, or the first EMPTY one, claimed with an LDS CAS (a slot another lane claimed
+// Linear probe of an LDS slice (mask + 1 slots) for `key` from its home slot: the first slot
+// holding the key, or the first free one, claimed with an LDS CAS (a slot another lane claimed
 // for a different key first moves the probe on past it) -- the same slot sequential linear probing
-// gives.  G slots are read per round (G independent LDS reads, one wait), so a wave's probe loop
-// runs ceil(longest probe / G) rounds instead of the longest probe.  Returns mask + 1 if full.
+// gives.  G slots are read per round (G independent LDS reads, one wait).
 constexpr int kAggProbe = 2;   // probe rounds of 1 / 2 / 4 / 8 slots: aggregate 0.72 / 0.58 / 0.60 / 0.63 ms (U 2^24)
+// One probe round of G slots from `off` (the rule above): true with `at` = the
+// key's slot (found, or claimed by an LDS CAS) or S (the slice is full); false with off / done
+// advanced past the round.  The aggregate and the owner merge give every record one round first,
+// straight-line, and then walk each lane's unfinished records one after another (see there).
 template <int G>
-__device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t mask, uint32_t off, uint64_t key,
-                                              uint64_t empty = kEmpty) {
+__device__ __forceinline__ bool lds_probe_round(unsigned long long* skey, uint32_t mask, uint64_t empty, uint64_t k,
+                                                uint32_t& off, uint32_t& done, uint32_t& at) {
     const uint32_t S = mask + 1;
-    for (uint32_t done = 0; done < S;) {
-        unsigned long long cur[G];
+    unsigned long long cur[G];
 #pragma unroll
-        for (int g = 0; g < G; ++g) cur[g] = skey[(off + g) & mask];
-        int hit = -1;
-        bool free_at = false;
+    for (int g = 0; g < G; ++g) cur[g] = skey[(off + g) & mask];
+    int hit = -1;
+    bool free_at = false;
 #pragma unroll
-        for (int g = G - 1; g >= 0; --g) {     // the lowest g holding the key or the empty marker
-            if (cur[g] == key) {
-                hit = g;
-                free_at = false;
-            } else if (cur[g] == empty) {
-                hit = g;
-                free_at = true;
-            }
+    for (int g = G - 1; g >= 0; --g) {
+        if (cur[g] == k) {
+            hit = g;
+            free_at = false;
+        } else if (cur[g] == empty) {
+            hit = g;
+            free_at = true;
         }
-        if (hit < 0) {
-            off = (off + G) & mask;
-            done += G;
-            continue;
-        }
-        const uint32_t at = (off + (uint32_t)hit) & mask;
-        if (!free_at) return at;
-        const unsigned long long prev = atomicCAS(&skey[at], (unsigned long long)empty, (unsigned long long)key);
-        if (prev == empty || prev == key) return at;
+    }
+    if (hit >= 0) {
+        at = (off + (uint32_t)hit) & mask;
+        if (!free_at) return true;
+        const unsigned long long prev = atomicCAS(&skey[at], (unsigned long long)empty, (unsigned long long)k);
+        if (prev == empty || prev == k) return true;
         off = (at + 1) & mask;                 // taken by another key: go on after it
         done += (uint32_t)hit + 1;
+    } else {
+        off = (off + G) & mask;
+        done += G;
     }
-    return S;
+    at = S;
+    return done >= S;
 }
 
 // One block per region (a persistent grid walking the regions measured slower: aggregate 0.63 ->
@@ -1706,39 +1708,8 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     auto home_of = [&](uint64_t k) -> uint64_t {
         return REC12 ? (t.shift >= 64 ? 0ull : k >> t.shift) : slot_top(t, k);
     };
-    // one probe round of kAggProbe slots from `off` (the lds_probe rule): true with `at` = the key's
-    // slot (found or claimed by an LDS CAS) or S (the slice is full); false with off / done past it
     auto probe_round = [&](uint64_t k, uint32_t& off, uint32_t& done, uint32_t& at) -> bool {
-        constexpr int G = kAggProbe;
-        const uint32_t mask = (uint32_t)t.slice_mask;
-        unsigned long long cur[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) cur[g] = skey[(off + g) & mask];
-        int hit = -1;
-        bool free_at = false;
-#pragma unroll
-        for (int g = G - 1; g >= 0; --g) {
-            if (cur[g] == k) {
-                hit = g;
-                free_at = false;
-            } else if (cur[g] == kE) {
-                hit = g;
-                free_at = true;
-            }
-        }
-        if (hit >= 0) {
-            at = (off + (uint32_t)hit) & mask;
-            if (!free_at) return true;
-            const unsigned long long prev = atomicCAS(&skey[at], (unsigned long long)kE, (unsigned long long)k);
-            if (prev == kE || prev == k) return true;
-            off = (at + 1) & mask;                 // taken by another key: go on after it
-            done += (uint32_t)hit + 1;
-        } else {
-            off = (off + G) & mask;
-            done += G;
-        }
-        at = S;
-        return done >= S;
+        return lds_probe_round<kAggProbe>(skey, (uint32_t)t.slice_mask, kE, k, off, done, at);
     };
     auto commit = [&](uint32_t at, uint32_t c, uint32_t ix) {
         if (at == S) {
@@ -2009,20 +1980,57 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
                 }
                 recs.load(s_at[lo] + (e - s_pre[lo]), g0 + lo, key[k], c[k], f[k]);
             }
+            // one probe round per record, then each lane's unfinished records in turn (the aggregate's
+            // form: the wave runs its longest lane's remaining rounds, not each record's longest probe)
+            auto commit = [&](uint32_t at, unsigned long long cc, unsigned long long ff) {
+                if (at == S) {
+                    atomicOr(t.overflow, kOvfTable);
+                    return;
+                }
+                if (ff > kMaxIndex) atomicOr(t.overflow, kOvfIndex);
+                const uint32_t old = atomicAdd(&scnt[at], (uint32_t)cc);
+                if ((cc >> 32) || old + (uint32_t)cc < old)     // a carry past 32 bits: rare
+                    count_add_wide(t, base + at, old, (uint32_t)cc, cc & ~0xFFFFFFFFull);
+                atomicMin(&sfst[at], (uint32_t)min((unsigned long long)kMaxIndex, ff));
+            };
+            const uint32_t mask = (uint32_t)t.slice_mask;
+            uint32_t pend = 0, soff[kMergeK];
 #pragma unroll
             for (int k = 0; k < kMergeK; ++k) {
-                if (e0 + (uint32_t)k * kMergeT + threadIdx.x >= tot) break;
-                const uint32_t off = lds_probe<kAggProbe>(skey, (uint32_t)t.slice_mask,
-                                                              (uint32_t)(slot_top(t, key[k]) & t.slice_mask), key[k]);
-                if (off == S) {
-                    atomicOr(t.overflow, kOvfTable);
-                    continue;
+                soff[k] = 0;
+                if (e0 + (uint32_t)k * kMergeT + threadIdx.x >= tot) continue;
+                uint32_t off = (uint32_t)(slot_top(t, key[k]) & mask), done = 0, at;
+                if (lds_probe_round<kAggProbe>(skey, mask, kEmpty, key[k], off, done, at)) {
+                    commit(at, c[k], f[k]);
+                } else {
+                    pend |= 1u << k;
+                    soff[k] = off;
                 }
-                if (f[k] > kMaxIndex) atomicOr(t.overflow, kOvfIndex);
-                const uint32_t old = atomicAdd(&scnt[off], (uint32_t)c[k]);
-                if ((c[k] >> 32) || old + (uint32_t)c[k] < old)     // a carry past 32 bits: rare
-                    count_add_wide(t, base + off, old, (uint32_t)c[k], c[k] & ~0xFFFFFFFFull);
-                atomicMin(&sfst[off], (uint32_t)min((unsigned long long)kMaxIndex, f[k]));
+            }
+            if (__ballot(pend != 0)) {
+                uint64_t kk = 0;
+                unsigned long long cc = 0, ff = 0;
+                uint32_t off = 0, done = 0;
+                auto pick = [&]() {   // the lowest pending record becomes the lane's current one
+#pragma unroll
+                    for (int k = kMergeK - 1; k >= 0; --k)
+                        if (pend & (1u << k)) {
+                            kk = key[k];
+                            cc = c[k];
+                            ff = f[k];
+                            off = soff[k];
+                        }
+                    done = (off - (uint32_t)slot_top(t, kk)) & mask;   // < S while probing
+                };
+                if (pend) pick();
+                while (__ballot(pend != 0)) {
+                    uint32_t at;
+                    if (pend && lds_probe_round<kAggProbe>(skey, mask, kEmpty, kk, off, done, at)) {
+                        commit(at, cc, ff);
+                        pend &= pend - 1u;
+                        if (pend) pick();
+                    }
+                }
             }
         }
         __syncthreads();                  // s_pre / s_at of the next group
