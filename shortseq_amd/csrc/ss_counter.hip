@@ -1568,6 +1568,7 @@ constexpr int kAggP = 4;               // records per thread per aggregate step 
 // for a different key first moves the probe on past it) -- the same slot sequential linear probing
 // gives.  G slots are read per round (G independent LDS reads, one wait).
 constexpr int kAggProbe = 2;   // probe rounds of 1 / 2 / 4 / 8 slots: aggregate 0.72 / 0.58 / 0.60 / 0.63 ms (U 2^24)
+constexpr int kAggProbeS = 4;  // straggler rounds (aggregate, merge): 2 / 4 slots 0.52 / 0.49 ms U 2^24, 0.53 / 0.48 ms U 2^20
 // One probe round of G slots from `off` (the rule above): true with `at` = the
 // key's slot (found, or claimed by an LDS CAS) or S (the slice is full); false with off / done
 // advanced past the round.  The aggregate and the owner merge give every record one round first,
@@ -1711,6 +1712,9 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
     auto probe_round = [&](uint64_t k, uint32_t& off, uint32_t& done, uint32_t& at) -> bool {
         return lds_probe_round<kAggProbe>(skey, (uint32_t)t.slice_mask, kE, k, off, done, at);
     };
+    auto probe_round_s = [&](uint64_t k, uint32_t& off, uint32_t& done, uint32_t& at) -> bool {   // stragglers
+        return lds_probe_round<kAggProbeS>(skey, (uint32_t)t.slice_mask, kE, k, off, done, at);
+    };
     auto commit = [&](uint32_t at, uint32_t c, uint32_t ix) {
         if (at == S) {
             atomicOr(t.overflow, kOvfTable);
@@ -1778,7 +1782,7 @@ __global__ __launch_bounds__(T) void k_pc_aggregate_slice(Tbl t, PartWs w, uint6
             if (pend) pick();
             while (__ballot(pend != 0)) {
                 uint32_t at;
-                if (pend && probe_round(k, off, done, at)) {
+                if (pend && probe_round_s(k, off, done, at)) {
                     commit(at, c, ix);
                     pend &= pend - 1u;
                     if (pend) pick();
@@ -2025,7 +2029,7 @@ __global__ __launch_bounds__(kMergeT) void k_merge_runs(Tbl t, Recs recs,
                 if (pend) pick();
                 while (__ballot(pend != 0)) {
                     uint32_t at;
-                    if (pend && lds_probe_round<kAggProbe>(skey, mask, kEmpty, kk, off, done, at)) {
+                    if (pend && lds_probe_round<kAggProbeS>(skey, mask, kEmpty, kk, off, done, at)) {
                         commit(at, cc, ff);
                         pend &= pend - 1u;
                         if (pend) pick();
