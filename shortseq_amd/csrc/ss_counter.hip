@@ -2963,16 +2963,19 @@ __global__ __launch_bounds__(256) void k_flat_verify(Tbl f, const uint64_t* __re
             at[k] = slot_top(f, fp[k]);
             e[k] = *(const uint4*)(rep + at[k] * 8 + 2u * q);
         }
+        // The kFlatQK rows probe in lockstep: each round decides every row still open and issues the
+        // next slot's loads of all of them together, so a wave waits for one dependent round trip per
+        // probe round of its longest row, where a probe loop per row waited for each row's displaced
+        // quads in turn (most rounds have one: 16 quads per row, ~1 in 3 fingerprints off its home)
+        uint32_t open = (1u << kFlatQK) - 1u;
+        uint32_t probes[kFlatQK];
 #pragma unroll
-        for (int k = 0; k < kFlatQK; ++k) {
-            const bool live = r0 + (uint64_t)k * nq < n;
-            const uint64_t base = at[k] & ~f.slice_mask;
-            uint64_t off = at[k] & f.slice_mask;
-            for (uint64_t probe = 0; probe <= f.slice_mask; ++probe) {
-                if (probe) {
-                    off = (off + 1) & f.slice_mask;
-                    e[k] = *(const uint4*)(rep + (base + off) * 8 + 2u * q);
-                }
+        for (int k = 0; k < kFlatQK; ++k) probes[k] = 0;
+        for (;;) {
+#pragma unroll
+            for (int k = 0; k < kFlatQK; ++k) {
+                if (!(open & (1u << k))) continue;     // (quad-uniform: the quad decides together)
+                const bool live = r0 + (uint64_t)k * nq < n;
                 const uint64_t key = (uint64_t)e[k].y << 32 | e[k].x;     // lane 3's piece: (key, W)
                 const bool same = a[k].x == e[k].x && a[k].y == e[k].y && a[k].z == e[k].z && a[k].w == e[k].w;
                 const uint32_t bits = (q < 3u ? (same ? 1u : 0u) | 6u
@@ -2980,12 +2983,19 @@ __global__ __launch_bounds__(256) void k_flat_verify(Tbl f, const uint64_t* __re
                 const uint32_t all = quad_and(bits);
                 if (all & 2u) {              // the fingerprint's slot: its words decide
                     bad |= live && !(all & 1u);
-                    break;
+                    open &= ~(1u << k);
+                } else if (!(all & 4u) || probes[k] == f.slice_mask) {
+                    bad |= live;             // an empty slot: the fingerprint was never inserted
+                    open &= ~(1u << k);
                 }
-                if (!(all & 4u)) {           // an empty slot: the fingerprint was never inserted
-                    bad |= live;
-                    break;
-                }
+            }
+            if (!__ballot(open != 0u)) break;
+#pragma unroll
+            for (int k = 0; k < kFlatQK; ++k) {
+                if (!(open & (1u << k))) continue;
+                ++probes[k];
+                at[k] = (at[k] & ~f.slice_mask) | ((at[k] + 1) & f.slice_mask);
+                e[k] = *(const uint4*)(rep + at[k] * 8 + 2u * q);
             }
         }
     }
