@@ -133,6 +133,35 @@ def test_counter_sentinel_bulk(gpu, oracle):
     assert oracle.table_digest(k, cnt, f) == oracle.table_digest(*_rows_of(exp, 1000))
 
 
+def test_counter_slot_hash_edge_keys(gpu, oracle):
+    """The partition records carry h = key * C (C the slot-hash multiplier) and the aggregate's LDS
+    slice marks free slots with h(~0): the key whose h is ~0 (K* = ~0 * C^-1) is an ordinary key
+    there, "G" * 32 (key ~0) the sentinel, key 0 ("A" * 32) an ordinary one; all three in bulk among
+    pool reads, over three batches (the later ones load the slices the first wrote back)."""
+    import shortseq_amd.batch as B
+    C = 0x9E3779B97F4A7C15
+    kstar = (((1 << 64) - 1) * pow(C, -1, 1 << 64)) & ((1 << 64) - 1)
+    assert (kstar * C) & ((1 << 64) - 1) == (1 << 64) - 1
+    shifts = np.arange(32, dtype=np.uint64) * np.uint64(2)
+
+    def read_of(key):
+        codes = ((np.uint64(key) >> shifts) & np.uint64(3)).astype(np.int64)
+        return np.frombuffer(b"ACTG", np.uint8)[codes]
+
+    n = 1_200_000
+    a = oracle.gen_pool_reads(6, 9, 60_000, 0, n, 32).reshape(n, 32)
+    rng = np.random.default_rng(11)
+    pick = rng.random(n)
+    a[pick < 0.1] = read_of(kstar)
+    a[(pick >= 0.1) & (pick < 0.2)] = ord("G")
+    a[(pick >= 0.2) & (pick < 0.25)] = read_of(0)
+    a = a.reshape(-1)
+    k, cnt, f = _count_gpu(B, gpu, a, 32, 1 << 20, base=7, splits=3)
+    exp = oracle.count([a[i * 32:(i + 1) * 32].tobytes() for i in range(n)])
+    assert oracle.table_digest(k, cnt, f) == oracle.table_digest(*_rows_of(exp, 7))
+    assert kstar in set(int(x) for x in k)
+
+
 def test_counter_index_limit(gpu):
     """Read indices live in 32 bits: an insert past 2^32 - 1 is refused (SS_EARG), not truncated."""
     import shortseq_amd.batch as B
