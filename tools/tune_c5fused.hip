@@ -13,6 +13,17 @@
 //          shortseq_amd/csrc/ss_codec.hip shortseq_amd/csrc/ss_runtime.hip -o tools/tune_c5fused
 #include "../shortseq_amd/csrc/ss_counter.hip"
 
+namespace {
+// the whole linear probe of the production aggregate's rule (ss_counter.hip now probes per round)
+template <int G>
+__device__ __forceinline__ uint32_t lds_probe(unsigned long long* skey, uint32_t mask, uint32_t off, uint64_t key) {
+    uint32_t done = 0, at;
+    while (!lds_probe_round<G>(skey, mask, kEmpty, key, off, done, at)) {
+    }
+    return at;
+}
+}  // namespace
+
 #include <stdio.h>
 #include <stdlib.h>
 

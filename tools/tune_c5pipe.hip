@@ -37,7 +37,7 @@ void coarse(ss_counter* c, const uint8_t* ascii, uint64_t n, uint64_t* fb, hipSt
     Tbl t = tbl_of(c);
     PartWs w = ws_of(c);
     CK(hipMemsetAsync(c->ws_fill, 0, kFillWords * sizeof(uint32_t), s));
-    hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL>), dim3(g_grid * g_mul), dim3(kPfT), 0, s, t, w, (const uint4*)ascii,
+    hipLaunchKernelGGL((k_pf_coarse<kPfT, kPfRPL, false, false>), dim3(g_grid * g_mul), dim3(kPfT), 0, s, t, w, (const uint4*)ascii,
                        (uint64_t)2, n, 2u, c->ws_cap1, c->ws_fill, (unsigned long long*)fb);
 }
 
@@ -70,7 +70,7 @@ int main(int argc, char** argv) {
     int dev = 0, cus = 0, per = 0;
     CK(hipGetDevice(&dev));
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL>, kPfT, 0));
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_pf_coarse<kPfT, kPfRPL, false, false>, kPfT, 0));
     g_grid = cus * per;
     hipStream_t s0, s1;
     CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
