@@ -3027,6 +3027,33 @@ __device__ __forceinline__ bool flat_entry(const Tbl& f, const FlatDesc& d, cons
 // EXTRACT (the class tables are known to be empty, ss_classes_flat_extract): every entry is new, no
 // probe; found is not written
 extern "C++" {      // (a template inside this file's extern "C" section)
+// The extract's entry loads, all issued together: the slot and its whole 64-B representative (the
+// words, the key, the class) do not depend on each other, so a grid-stride step waits one round
+// trip instead of three (slot -> class -> words, as flat_entry does); kFlatXU slots per step are in
+// flight.  Empty slots' representatives are read too (sequential 64-B rows: whole lines).
+constexpr int kFlatXU = 2;
+struct FlatLoad {
+    uint4 sl;
+    uint4 r[4];
+};
+__device__ __forceinline__ void flat_load(const Tbl& f, const uint64_t* rep, uint64_t s, FlatLoad& e) {
+    const uint64_t sc = min(s, f.mask);                 // (past the table: decoded as no entry)
+    e.sl = *(const uint4*)&f.slots[sc];
+    const uint4* rp = (const uint4*)(rep + sc * 8);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e.r[k] = rp[k];
+}
+// flat_entry's rule on loaded values: the class W (rep word 7) and the slot's count and first read
+__device__ __forceinline__ bool flat_decode(const Tbl& f, const FlatDesc& d, uint64_t s, const FlatLoad& e,
+                                            uint32_t& cnt, uint32_t& W, uint64_t& first) {
+    if (s > f.mask || (e.sl.x == 0xFFFFFFFFu && e.sl.y == 0xFFFFFFFFu)) return false;   // (kEmpty key)
+    W = e.r[3].z;
+    if (W < 2 || W + 1 > d.S || !d.tbl[W].slots) return false;
+    cnt = ~e.sl.z;
+    first = e.sl.w;
+    return true;
+}
+
 template <bool EXTRACT>
 __global__ __launch_bounds__(256) void k_flat_fold_find(Tbl f, FlatDesc d, const uint64_t* __restrict__ rep,
                                                         const uint32_t* __restrict__ flag, uint64_t* __restrict__ found,
@@ -3034,15 +3061,21 @@ __global__ __launch_bounds__(256) void k_flat_fold_find(Tbl f, FlatDesc d, const
     __shared__ uint32_t lc[kRepW1];
     if (threadIdx.x < kRepW1) lc[threadIdx.x] = 0;
     __syncthreads();
-    if (!*flag) {
+    // EXTRACT: the per-block count of k_flat_extract_claim's rows (the same slots per block); the
+    // slot, then its class word -- the branch-free form of the claim (slot and whole representative
+    // together) read 0.5 GB more here for the empty slots and measured 0.37 -> 0.43 ms at 2^24
+    if (EXTRACT && !*flag) {
+        for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
+            uint64_t fp, first;
+            uint32_t cnt, W;
+            const uint64_t* kw;
+            if (flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) atomicAdd(&lc[W], 1u);
+        }
+    } else if (!*flag) {
         for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
             uint64_t fp, first, at = kEmpty;
             uint32_t cnt, W;
             const uint64_t* kw;
-            if (EXTRACT) {
-                if (flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) atomicAdd(&lc[W], 1u);
-                continue;
-            }
             if (flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) {
                 const Tbl& t = d.tbl[W];
                 const uint64_t top = slot_top(t, fp), base = top & ~t.slice_mask;
@@ -3172,21 +3205,31 @@ __global__ __launch_bounds__(256) void k_flat_extract_claim(Tbl f, FlatDesc d, F
     __shared__ uint32_t lc[kRepW1];
     if (threadIdx.x < kRepW1) lc[threadIdx.x] = blkoff[(uint64_t)blockIdx.x * kRepW1 + threadIdx.x];
     __syncthreads();
-    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
-        uint64_t fp, first;
-        uint32_t cnt, W;
-        const uint64_t* kw;
-        if (!flat_entry(f, d, rep, s, fp, cnt, W, kw, first)) continue;
-        const uint32_t row = atomicAdd(&lc[W], 1u);     // LDS: this block's next row of class W
-        if (row >= o.cap[W]) {
-            atomicOr(o.ovf[W], (unsigned long long)kOvfTable);
-            continue;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t s0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; s0 <= f.mask; s0 += kFlatXU * stride) {
+        FlatLoad e[kFlatXU];
+#pragma unroll
+        for (int u = 0; u < kFlatXU; ++u) flat_load(f, rep, s0 + u * stride, e[u]);
+#pragma unroll
+        for (int u = 0; u < kFlatXU; ++u) {
+            uint64_t first;
+            uint32_t cnt, W;
+            if (!flat_decode(f, d, s0 + u * stride, e[u], cnt, W, first)) continue;
+            const uint32_t row = atomicAdd(&lc[W], 1u);     // LDS: this block's next row of class W
+            if (row >= o.cap[W]) {
+                atomicOr(o.ovf[W], (unsigned long long)kOvfTable);
+                continue;
+            }
+            o.rmap[W][row] = d.base + first;
+            o.counts[W][row] = cnt;
+            o.first[W][row] = row;
+            uint64_t* dst = o.words[W] + (uint64_t)row * (W + 1);
+            const uint32_t wd[12] = {e[u].r[0].x, e[u].r[0].y, e[u].r[0].z, e[u].r[0].w, e[u].r[1].x, e[u].r[1].y,
+                                     e[u].r[1].z, e[u].r[1].w, e[u].r[2].x, e[u].r[2].y, e[u].r[2].z, e[u].r[2].w};
+#pragma unroll
+            for (uint32_t q = 0; q < kRepW1; ++q)
+                if (q <= W) dst[q] = (uint64_t)wd[2 * q] | ((uint64_t)wd[2 * q + 1] << 32);
         }
-        o.rmap[W][row] = d.base + first;
-        o.counts[W][row] = cnt;
-        o.first[W][row] = row;
-        uint64_t* dst = o.words[W] + (uint64_t)row * (W + 1);
-        for (uint32_t q = 0; q <= W; ++q) dst[q] = kw[q];
     }
 }
 
