@@ -2901,23 +2901,45 @@ struct FlatDesc {
 // rep layout, 8 u64 per scratch slot: the row's words w0 .. w5 (zeros past S), the key, the class W --
 // so the 16-B pieces of a representative line up with the row's own pieces (w0 w1 | w2 w3 | w4 w5) and
 // with (key, W) last, one piece per lane of k_flat_verify's quads
+// Two slots per step, every load branch-free (an empty slot's row loads are dropped), so a step waits
+// for one slot round trip and one row round trip for both slots: the grid-stride loop walks ~32 slots
+// per thread, and a used slot's row load depends on its slot
+constexpr int kRepU = 2;
 __global__ __launch_bounds__(256) void k_flat_reps(Tbl f, const uint64_t* __restrict__ rows, uint32_t S,
                                                    uint64_t* __restrict__ rep) {
-    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s <= f.mask; s += (uint64_t)gridDim.x * 256) {
-        const Slot sl = f.slots[s];
-        uint64_t v[8] = {0, 0, 0, 0, 0, 0, sl.key, 0};
-        if (sl.key != kEmpty) {
-            const uint64_t* row = rows + (uint64_t)sl.first * S;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t s0 = (uint64_t)blockIdx.x * 256 + threadIdx.x; s0 <= f.mask; s0 += kRepU * stride) {
+        Slot sl[kRepU];
+#pragma unroll
+        for (int u = 0; u < kRepU; ++u) sl[u] = f.slots[min(s0 + u * stride, f.mask)];
+        uint64_t v[kRepU][8];
+#pragma unroll
+        for (int u = 0; u < kRepU; ++u) {
+            const bool used = sl[u].key != kEmpty;
+            // (an empty slot reads the table's own first words: always there, whatever the rows hold)
+            const uint64_t* row = used ? rows + (uint64_t)sl[u].first * S : (const uint64_t*)f.slots;
+#pragma unroll
+            for (uint32_t j = 0; j < kRepW1; ++j) v[u][j] = row[min(j, S - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < kRepU; ++u) {
+            const uint64_t s = s0 + u * stride;
+            if (s > f.mask) continue;
+            const bool used = sl[u].key != kEmpty;
+            uint64_t w[8];
+            w[6] = sl[u].key;
+            w[7] = 0;
 #pragma unroll
             for (uint32_t j = 0; j < kRepW1; ++j) {
-                v[j] = j < S ? row[j] : 0ull;
-                if (v[j]) v[7] = j;
+                w[j] = (used && j < S) ? v[u][j] : 0ull;
+                if (w[j]) w[7] = j;
             }
-        }
-        uint4* dst = (uint4*)(rep + s * 8);
+            uint4* dst = (uint4*)(rep + s * 8);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dst[k] = make_uint4((uint32_t)v[2 * k], (uint32_t)(v[2 * k] >> 32), (uint32_t)v[2 * k + 1],
-                                                       (uint32_t)(v[2 * k + 1] >> 32));
+            for (int k = 0; k < 4; ++k)
+                dst[k] = make_uint4((uint32_t)w[2 * k], (uint32_t)(w[2 * k] >> 32), (uint32_t)w[2 * k + 1],
+                                    (uint32_t)(w[2 * k + 1] >> 32));
+        }
     }
 }
 
